@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Benchmark: GiB/s of fp32 params encoded+decoded (device-resident), 1 % top-k.
+
+One step = one PartialModel top-k encode (fused |x - x0| -> sampled radix select -> ordered
+compaction with counter update) of an N-element fp32 tensor already resident in HBM, plus the
+matching decode (replace the k payload values into a copy of the local model), exactly the
+reference's PartialModel.serialized_model + deserialized_model pair.
+
+Workload (BASELINE.json configs[1]): N = 11,000,000 (ResNet-18-sized), alpha = 0.01 -> k = 110,000.
+Multi-GPU (torchrun): each rank encodes+decodes its own node's tensor (the gossip round is a set
+of independent per-node codecs: no data-path collective) -> weak scaling; value = all ranks'
+params / max-over-ranks time.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (GB/s), /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--n", type=int, default=11_000_000)
+    p.add_argument("--alpha", type=float, default=0.01)
+    p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-extra", action="store_true", help="skip the 64 MiB secondary line")
+    return p.parse_args()
+
+
+def timed_loop(fn, reps, stream):
+    """Average device time of fn() over reps launches, with HIP events on `stream`."""
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        ev0.record(stream)
+        for _ in range(reps):
+            fn()
+        ev1.record(stream)
+    ev1.synchronize()
+    return ev0.elapsed_time(ev1) / reps * 1e-3  # seconds
+
+
+def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist):
+    from decentralizepy_amd import codec
+    k = round(alpha * n)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x = torch.randn(n, device=dev, generator=g)
+    x0 = x - 0.01 * torch.randn(n, device=dev, generator=g)
+    counter = torch.zeros(n, dtype=torch.int32, device=dev)
+    ws = codec.Workspace(dev)
+    idx = torch.empty(k, dtype=torch.int32, device=dev)
+    val = torch.empty(k, dtype=torch.float32, device=dev)
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+
+    def encode():
+        codec.topk_encode(x, k, x0=x0, counter=counter, idx_out=idx, val_out=val, workspace=ws,
+                          asynchronous=True)
+
+    def decode():
+        codec.replace(x0, idx, val, out=out)
+
+    def step():
+        encode()
+        decode()
+
+    for _ in range(warmup):
+        step()
+    fell_back = codec.topk_complete(x, k, idx, val, ws, x0=x0, counter=counter)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([t], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    s_step = t / steps
+    # per-stage device time with events on the launch stream
+    stream = torch.cuda.current_stream(dev)
+    t_enc = timed_loop(encode, max(20, steps // 2), stream)
+    t_dec = timed_loop(decode, max(20, steps // 2), stream)
+    b_enc = 8 * n + 8 * k + 8 * k      # read x, x0; write idx, val; counter[idx] += 1 (r+w)
+    b_dec = 8 * n + 8 * k              # read local, payload; write out
+    return dict(n=n, k=k, s_step=s_step, fell_back=fell_back, t_enc=t_enc, t_dec=t_dec,
+                b_enc=b_enc, b_dec=b_dec,
+                value=world * 4 * n / s_step / 2 ** 30)
+
+
+def cpu_baseline(n, alpha, seconds):
+    from oracle import ref_ops
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(n, generator=g)
+    x0 = x - 0.01 * torch.randn(n, generator=g)
+    counter = torch.zeros(n, dtype=torch.int32)
+    times = []
+    t_start = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        idx, vals = ref_ops.encode(x, x0, alpha, counter)
+        ref_ops.decode(x0, idx, vals)
+        times.append(time.perf_counter() - t0)
+        if len(times) >= 3 and time.perf_counter() - t_start > seconds:
+            break
+    t = sorted(times)[len(times) // 2]
+    return dict(value=4 * n / t / 2 ** 30, unit="GiB/s", cores=torch.get_num_threads(),
+                kind="port",
+                sample=f"reference ATen-CPU op sequence (oracle/ref_ops.py), N={n}, k={round(alpha*n)}, "
+                       f"median of {len(times)} encode+decode steps ({sum(times):.1f} s)")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist_mod
+        torch.cuda.set_device(local_rank)
+        dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist = dist_mod
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    r = gpu_case(args.n, args.alpha, dev, 1234 + rank, args.steps, args.warmup, world, dist)
+    extra = None
+    if not args.no_extra and world == 1:
+        e = gpu_case(16_777_216, 0.01, dev, 99, max(20, args.steps // 2), args.warmup, 1, None)
+        extra = {"workload": "north-star target: 64 MiB fp32 tensor (N=16,777,216), 1% top-k",
+                 "value": round(e["value"], 2), "ms_per_step": round(e["s_step"] * 1e3, 4),
+                 "frac_of_hbm_peak": round((e["b_enc"] + e["b_dec"]) / e["s_step"] / 1e9 / HBM_PEAK_GBS, 4),
+                 "fell_back": e["fell_back"]}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args.n, args.alpha, args.cpu_seconds)
+
+    if rank == 0:
+        t_enc, t_dec = r["t_enc"], r["t_dec"]
+        # dominant kernel: the decode fold kernel is a single launch -> priced per launch
+        dec_gbs = r["b_dec"] / t_dec / 1e9
+        enc_gbs = r["b_enc"] / t_enc / 1e9
+        step_gbs = (r["b_enc"] + r["b_dec"]) / r["s_step"] / 1e9
+        line = {
+            "metric": "GiB/s fp32 params encoded+decoded (device-resident), 1% top-k",
+            "value": round(r["value"], 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(r["s_step"] * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (x ~ N(0,1), x0 = x - 0.01*N(0,1), device-generated)",
+            "config": {
+                "workload": "C2: PartialModel top-k encode + decode of one 11M-fp32 flattened tensor",
+                "n": r["n"], "k": r["k"], "alpha": args.alpha,
+                "parallelism": f"{world} independent per-node codecs (one per GPU), no collective",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "fold_kernel (decode: replace payload into local copy)",
+                "achieved": round(dec_gbs, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(dec_gbs / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "bytes_per_launch": r["b_dec"],
+                "avg_launch_us": round(t_dec * 1e6, 3),
+            },
+            "stages": {
+                "encode": {"avg_us": round(t_enc * 1e6, 3), "alg_bytes": r["b_enc"],
+                           "GBps": round(enc_gbs, 1), "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
+                           "sampled_path_fell_back": r["fell_back"]},
+                "decode": {"avg_us": round(t_dec * 1e6, 3), "alg_bytes": r["b_dec"],
+                           "GBps": round(dec_gbs, 1), "frac": round(dec_gbs / HBM_PEAK_GBS, 4)},
+                "step_frac_of_hbm_peak": round(step_gbs / HBM_PEAK_GBS, 4),
+            },
+            "cpu_baseline": cpu,
+            "secondary": extra,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

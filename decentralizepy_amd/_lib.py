@@ -1,0 +1,76 @@
+"""ctypes binding of libdpzcodec.so (the C ABI declared in include/dpz_codec.h).
+
+The shared library is built in-tree (``decentralizepy_amd/libdpzcodec.so``, see
+``__graft_entry__.build()``).  There is no fallback: if the library is missing or fails to load,
+every codec entry point raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdpzcodec.so")
+
+DPZ_ACC_NONE = 0
+DPZ_ACC_ACCUMULATE = 1
+DPZ_ACC_ADD = 2
+DPZ_TOPK_EXACT = 0x1
+DPZ_TOPK_ASYNC = 0x2
+DPZ_FOLD_SELF = 0x1
+DPZ_FOLD_REPLACE_ONLY = 0x2
+
+_c_void_p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_size = ctypes.c_size_t
+
+# name -> (restype, argtypes); must match include/dpz_codec.h
+SIGNATURES = {
+    "dpz_abi_version": (_int, []),
+    "dpz_error_string": (ctypes.c_char_p, [_int]),
+    "dpz_topk_workspace_bytes": (_size, [_i64, _i64]),
+    "dpz_topk_encode": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64, _i64,
+                               _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size, _int, _c_void_p]),
+    "dpz_topk_complete": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64, _i64,
+                                 _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
+                                 ctypes.POINTER(_int), _c_void_p]),
+    "dpz_decode_average": (_int, [_c_void_p, _i64, _int, ctypes.POINTER(_c_void_p),
+                                  ctypes.POINTER(_c_void_p), ctypes.POINTER(_i64),
+                                  ctypes.POINTER(ctypes.c_float), ctypes.c_float, _int, _c_void_p,
+                                  _c_void_p]),
+    "dpz_wavedec_len": (_i64, [_i64, _int]),
+    "dpz_dwt_sym2": (_int, [_c_void_p, _c_void_p, _i64, _int, _c_void_p, _c_void_p, _int,
+                            _c_void_p]),
+    "dpz_idwt_sym2": (_int, [_c_void_p, _i64, _int, _c_void_p, _c_void_p]),
+    "dpz_pack_fp16": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
+    "dpz_unpack_fp16": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the codec library; raises if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"decentralizepy_amd: HIP codec library not found at {LIB_PATH}; "
+                "build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(or `make -C decentralizepy_amd/csrc`). There is no CPU fallback.")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+class CodecError(RuntimeError):
+    pass
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().dpz_error_string(rc)
+        raise CodecError(f"{what} failed: {rc} ({msg.decode() if msg else '?'})")

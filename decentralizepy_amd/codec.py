@@ -1,0 +1,193 @@
+"""Device-tensor front end of the HIP codec (libdpzcodec.so).
+
+Every function takes and returns torch tensors that live on a ROCm device; PyTorch is used only
+for allocation, streams and tensor handles — the arithmetic runs in the hand-written HIP kernels
+behind the C ABI (``include/dpz_codec.h``).  Calls are enqueued on the current torch stream.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import (DPZ_ACC_ACCUMULATE, DPZ_ACC_ADD, DPZ_ACC_NONE, DPZ_FOLD_REPLACE_ONLY,
+                   DPZ_FOLD_SELF, DPZ_TOPK_ASYNC, DPZ_TOPK_EXACT, check)
+
+__all__ = ["DPZ_ACC_NONE", "DPZ_ACC_ACCUMULATE", "DPZ_ACC_ADD", "Workspace", "topk_encode",
+           "topk_complete", "decode_average", "replace", "wavedec_len", "wavedec", "waverec",
+           "pack_fp16", "unpack_fp16"]
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _require(t, dtype, name):
+    if t is None:
+        return
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor (got {t.device}); no CPU path exists")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+class Workspace:
+    """Caller-owned scratch for the top-k encoder, reused across calls (sized per n)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.buf = None
+        self.n = -1
+
+    def get(self, n, k):
+        need = int(_lib.lib().dpz_topk_workspace_bytes(int(n), int(k)))
+        if self.buf is None or self.buf.numel() < need:
+            self.buf = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+        return self.buf
+
+
+def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, counter=None,
+                idx_out=None, val_out=None, workspace=None, exact=False, asynchronous=False):
+    """Top-k magnitude encode (reference PartialModel.py:164-255 / Wavelet.py:142-197).
+
+    Returns ``(idx int32[k], val fp32[k])`` in ascending index order.  Mutates ``acc`` and
+    ``counter`` in place like the reference mutates ``model.accumulated_changes`` and
+    ``model.shared_parameters_counter``.  With ``asynchronous=True`` the call only enqueues
+    work; call :func:`topk_complete` with the same arguments before reading the result.
+    """
+    _require(x, torch.float32, "x")
+    _require(x0, torch.float32, "x0")
+    _require(acc, torch.float32, "acc")
+    _require(counter, torch.int32, "counter")
+    n = x.numel()
+    k = int(k)
+    if vals_src is None:
+        vals_src = x
+    _require(vals_src, torch.float32, "vals_src")
+    if idx_out is None:
+        idx_out = torch.empty(k, dtype=torch.int32, device=x.device)
+    if val_out is None:
+        val_out = torch.empty(k, dtype=torch.float32, device=x.device)
+    ws = (workspace or Workspace(x.device)).get(n, k)
+    flags = (DPZ_TOPK_EXACT if exact else 0) | (DPZ_TOPK_ASYNC if asynchronous else 0)
+    rc = _lib.lib().dpz_topk_encode(_ptr(x), _ptr(x0), _ptr(acc), int(acc_mode), _ptr(vals_src),
+                                    n, k, _ptr(idx_out), _ptr(val_out), _ptr(counter), _ptr(ws),
+                                    ws.numel(), flags, _stream(x.device))
+    check(rc, "dpz_topk_encode")
+    return idx_out, val_out
+
+
+def topk_complete(x, k, idx_out, val_out, workspace, x0=None, acc=None, acc_mode=DPZ_ACC_NONE,
+                  vals_src=None, counter=None):
+    """Finish an asynchronous encode; returns True if the exact fallback had to run."""
+    n = x.numel()
+    if vals_src is None:
+        vals_src = x
+    ws = workspace.get(n, k)
+    fb = ctypes.c_int(0)
+    rc = _lib.lib().dpz_topk_complete(_ptr(x), _ptr(x0), _ptr(acc), int(acc_mode), _ptr(vals_src),
+                                      n, int(k), _ptr(idx_out), _ptr(val_out), _ptr(counter),
+                                      _ptr(ws), ws.numel(), ctypes.byref(fb), _stream(x.device))
+    check(rc, "dpz_topk_complete")
+    return bool(fb.value)
+
+
+def decode_average(local, payloads, weights=None, w_self=None, out=None, replace_only=False):
+    """Batched replace + Metro-Hastings fold (reference Sharing.py:156-229, PartialModel.py:257-303).
+
+    payloads : list of ``(idx int32 device tensor or None, vals fp32 device tensor)``
+    weights  : per-payload weights (Python floats, rounded to fp32 like torch does)
+    w_self   : weight of the local term, or None for no self term (server variant)
+    """
+    _require(local, torch.float32, "local")
+    n = local.numel()
+    if out is None:
+        out = torch.empty_like(local)
+    _require(out, torch.float32, "out")
+    npay = len(payloads)
+    idx_arr = (ctypes.c_void_p * max(npay, 1))()
+    val_arr = (ctypes.c_void_p * max(npay, 1))()
+    k_arr = (ctypes.c_int64 * max(npay, 1))()
+    w_arr = (ctypes.c_float * max(npay, 1))()
+    for i, (idx, vals) in enumerate(payloads):
+        _require(idx, torch.int32, "idx")
+        _require(vals, torch.float32, "vals")
+        idx_arr[i] = idx.data_ptr() if idx is not None else None
+        val_arr[i] = vals.data_ptr()
+        k_arr[i] = vals.numel()
+        w_arr[i] = float(weights[i]) if weights is not None else 1.0
+    flags = (DPZ_FOLD_SELF if w_self is not None else 0) | (DPZ_FOLD_REPLACE_ONLY if replace_only else 0)
+    rc = _lib.lib().dpz_decode_average(_ptr(local), n, npay, idx_arr, val_arr, k_arr, w_arr,
+                                       float(w_self) if w_self is not None else 0.0, flags,
+                                       _ptr(out), _stream(local.device))
+    check(rc, "dpz_decode_average")
+    return out
+
+
+def replace(local, idx, vals, out=None):
+    """``T = local.clone(); T[idx] = vals`` (reference PartialModel.py:292-295)."""
+    return decode_average(local, [(idx, vals)], out=out, replace_only=True)
+
+
+def wavedec_len(n, level=4):
+    m = int(_lib.lib().dpz_wavedec_len(int(n), int(level)))
+    if m < 0:
+        raise ValueError(f"sym2 level-{level} wavedec unsupported for n={n}")
+    return m
+
+
+def wavedec(x, level=4, x0=None, want_x=True, coeffs_x=None, coeffs_diff=None, accumulate=False):
+    """sym2 multilevel DWT as one ``coeffs_to_array`` vector (reference Wavelet.py:12-32).
+
+    Returns ``(W(x) or None, W(x - x0) or None)``; with ``accumulate=True`` adds W(x - x0) into
+    ``coeffs_diff`` instead of overwriting it.
+    """
+    _require(x, torch.float32, "x")
+    _require(x0, torch.float32, "x0")
+    n = x.numel()
+    m = wavedec_len(n, level)
+    if want_x and coeffs_x is None:
+        coeffs_x = torch.empty(m, dtype=torch.float32, device=x.device)
+    if x0 is not None and coeffs_diff is None:
+        if accumulate:
+            raise ValueError("accumulate needs coeffs_diff")
+        coeffs_diff = torch.empty(m, dtype=torch.float32, device=x.device)
+    rc = _lib.lib().dpz_dwt_sym2(_ptr(x), _ptr(x0), n, int(level),
+                                 _ptr(coeffs_x if want_x else None),
+                                 _ptr(coeffs_diff if x0 is not None else None),
+                                 1 if accumulate else 0, _stream(x.device))
+    check(rc, "dpz_dwt_sym2")
+    return (coeffs_x if want_x else None), (coeffs_diff if x0 is not None else None)
+
+
+def waverec(coeffs, n, level=4, out=None):
+    """sym2 multilevel IDWT, first n outputs (reference Wavelet.py:311-316)."""
+    _require(coeffs, torch.float32, "coeffs")
+    if out is None:
+        out = torch.empty(int(n), dtype=torch.float32, device=coeffs.device)
+    rc = _lib.lib().dpz_idwt_sym2(_ptr(coeffs), int(n), int(level), _ptr(out), _stream(coeffs.device))
+    check(rc, "dpz_idwt_sym2")
+    return out
+
+
+def pack_fp16(x, out=None):
+    _require(x, torch.float32, "x")
+    if out is None:
+        out = torch.empty(x.numel(), dtype=torch.float16, device=x.device)
+    rc = _lib.lib().dpz_pack_fp16(_ptr(x), x.numel(), _ptr(out), _stream(x.device))
+    check(rc, "dpz_pack_fp16")
+    return out
+
+
+def unpack_fp16(h, out=None):
+    _require(h, torch.float16, "h")
+    if out is None:
+        out = torch.empty(h.numel(), dtype=torch.float32, device=h.device)
+    rc = _lib.lib().dpz_unpack_fp16(_ptr(h), h.numel(), _ptr(out), _stream(h.device))
+    check(rc, "dpz_unpack_fp16")
+    return out

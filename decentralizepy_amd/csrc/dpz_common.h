@@ -1,0 +1,87 @@
+// Shared device helpers for the dpz codec kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/dpz_codec.h"
+
+#define DPZ_WAVE 64
+
+#define DPZ_HIP_TRY(expr)                                   \
+  do {                                                      \
+    hipError_t _e = (expr);                                 \
+    if (_e != hipSuccess) return (int)_e;                   \
+  } while (0)
+
+#define DPZ_LAUNCH_CHECK() DPZ_HIP_TRY(hipGetLastError())
+
+namespace dpz {
+
+// |c| as an order-preserving uint32 key: sign cleared, every NaN -> 0x7FC00000 so that NaNs
+// rank above +inf and tie with each other (torch.topk treats NaN as the largest value).
+__device__ __forceinline__ uint32_t key_of(float c) {
+  uint32_t b = __float_as_uint(c) & 0x7FFFFFFFu;
+  return b > 0x7F800000u ? 0x7FC00000u : b;
+}
+
+// Exclusive prefix of `v` over the 64 lanes of a wave plus the wave total (in *total).
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
+  const int lane = threadIdx.x & 63;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  *total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+// Block-wide exclusive scan (blockDim.x multiple of 64, <= 1024). `wsum` is LDS scratch of at
+// least 16 words. Returns the exclusive prefix; *total gets the block sum. Contains barriers:
+// every thread of the block must call it.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nw = blockDim.x >> 6;
+  uint32_t wt;
+  uint32_t ex = wave_excl_scan(v, &wt);
+  if (lane == 0) wsum[wid] = wt;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+  for (int w = 0; w < nw; ++w) {
+    uint32_t s = wsum[w];
+    off += (w < wid) ? s : 0u;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return ex + off;
+}
+
+// Block-wide exclusive scan on 64-bit values (same contract as block_excl_scan).
+__device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t* wsum, uint64_t* total) {
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nw = blockDim.x >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint64_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  uint64_t off = 0, tot = 0;
+  for (int w = 0; w < nw; ++w) {
+    uint64_t s = wsum[w];
+    off += (w < wid) ? s : 0ull;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return x - v + off;
+}
+
+__device__ __forceinline__ bool aligned16(const void* p) {
+  return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+}
+
+}  // namespace dpz

@@ -1,0 +1,276 @@
+// Multilevel sym2 DWT / IDWT (mode "symmetric"), fp32, bit-exact with PyWavelets 1.1.1.
+//
+// Replaces (reference sacs-epfl/decentralizepy, src/decentralizepy/):
+//   sharing/JWINS/Wavelet.py:12-32   change_transformer_wavelet: pywt.wavedec + coeffs_to_array
+//   sharing/JWINS/Wavelet.py:311-316 pywt.array_to_coeffs + pywt.waverec
+//   sharing/PartialModel.py:317-320  W(x) and W(x - x0) computed in one pass (pre-step)
+//   sharing/PartialModel.py:346-349  acc += W(x_new - prev)  (post-step, accumulate mode)
+//
+// Forward: one block owns TL = 128 level-L outputs and the matching 2^(L-l)*TL outputs of every
+// detail level; it stages the input span (16*TL + 30 halo for L = 4) in LDS and walks the levels
+// down in LDS (ping-pong buffers), writing each level's owned details straight to the
+// concatenated [cA_L, cD_L, ..., cD_1] layout.  Every convolution uses pywt's summation order
+// (see oracle/wavelet.py); the whole library is compiled with -ffp-contract=off.
+// Inverse: one block owns 4096 final outputs and reconstructs the (halo'd) ranges of each level
+// top-down in LDS.
+#include "dpz_common.h"
+
+namespace dpz {
+
+constexpr int DWT_MAX_LEVEL = 8;
+constexpr int DWT_TL = 128;  // level-L outputs per block (forward)
+constexpr int IDWT_TILE = 4096;
+
+// sym2 filters (fp32 casts of pywt's double coefficients)
+__constant__ float c_dec_lo[4] = {-0.12940952255092145f, 0.22414386804185735f,
+                                  0.836516303737469f, 0.48296291314469025f};
+__constant__ float c_dec_hi[4] = {-0.48296291314469025f, 0.836516303737469f,
+                                  -0.22414386804185735f, -0.12940952255092145f};
+__constant__ float c_rec_lo[4] = {0.48296291314469025f, 0.836516303737469f,
+                                  0.22414386804185735f, -0.12940952255092145f};
+__constant__ float c_rec_hi[4] = {-0.12940952255092145f, -0.22414386804185735f,
+                                  0.836516303737469f, -0.48296291314469025f};
+
+struct Levels {
+  int64_t len[DWT_MAX_LEVEL + 1];   // len[0] = n, len[l] = floor((len[l-1] + 3) / 2)
+  int64_t doff[DWT_MAX_LEVEL + 1];  // offset of cD_l in the coefficient array
+  int64_t total;
+  int level;
+};
+
+static inline Levels make_levels(int64_t n, int level) {
+  Levels L{};
+  L.level = level;
+  L.len[0] = n;
+  for (int l = 1; l <= level; ++l) L.len[l] = (L.len[l - 1] + 3) / 2;
+  int64_t o = L.len[level];
+  for (int l = level; l >= 1; --l) {
+    L.doff[l] = o;
+    o += L.len[l];
+  }
+  L.total = o;
+  return L;
+}
+
+// one convolution output o of a level whose input (extended, in LDS) is `in` with origin s_in:
+// in[p - s_in] = x~[p].  `last_odd` selects pywt's right-overhang order for the last output of
+// an odd-length input.
+__device__ __forceinline__ float conv4(const float* in, int64_t s_in, int64_t o, const float* f,
+                                       bool last_odd) {
+  const int64_t i = 2 * o + 1 - s_in;
+  if (!last_odd) {
+    float acc = f[0] * in[i];
+    acc = acc + f[1] * in[i - 1];
+    acc = acc + f[2] * in[i - 2];
+    acc = acc + f[3] * in[i - 3];
+    return acc;
+  }
+  float acc = f[2] * in[i - 2];   // x~[n]
+  acc = acc + f[1] * in[i - 1];   // x~[n+1]
+  acc = acc + f[0] * in[i];       // x~[n+2]
+  acc = acc + f[3] * in[i - 3];   // x~[n-1]
+  return acc;
+}
+
+template <bool WX, bool WD, bool ACCUM>
+__global__ void __launch_bounds__(256) dwt_kernel(const float* __restrict__ x,
+                                                  const float* __restrict__ x0, Levels LV,
+                                                  float* cx, float* cd) {
+  constexpr int SPAN0 = 16 * DWT_TL + 64;  // level-0 span (covers L <= 4 with slack)
+  constexpr int SPAN1 = 8 * DWT_TL + 32;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  // pipelines: 0 = W(x), 1 = W(x - x0); buffers A (SPAN0) and B (SPAN1) per pipeline
+  float* bufA[2] = {smem, smem + SPAN0 + SPAN1};
+  float* bufB[2] = {smem + SPAN0, smem + 2 * SPAN0 + SPAN1};
+  const int L = LV.level;
+  const int64_t nL = LV.len[L];
+  const int64_t a = (int64_t)blockIdx.x * DWT_TL;
+  const int64_t b = (a + DWT_TL < nL) ? a + DWT_TL : nL;
+  const bool last_block = (b == nL);
+  // needed ranges per level (top-down)
+  int64_t s[DWT_MAX_LEVEL + 1], e[DWT_MAX_LEVEL + 1];
+  s[L] = a;
+  e[L] = b;
+  for (int l = L; l >= 1; --l) {
+    s[l - 1] = 2 * s[l] - 2;
+    e[l - 1] = 2 * e[l];
+  }
+  // ---- level 0: load x (and x - x0) over [s0, e0) with symmetric extension
+  const int64_t n = LV.len[0];
+  {
+    const int64_t s0 = s[0], e0 = e[0];
+    for (int64_t p = s0 + threadIdx.x; p < e0; p += 256) {
+      if (p >= 0 && p < n) {
+        const float xv = x[p];
+        if (WX) bufA[0][p - s0] = xv;
+        if (WD) bufA[1][p - s0] = xv - x0[p];
+      }
+    }
+    __syncthreads();
+    // extension: only x~[-3..-1] and x~[n..n+2] are ever read
+    if (threadIdx.x < 6) {
+      const int64_t p = threadIdx.x < 3 ? -1 - (int64_t)threadIdx.x : n + (threadIdx.x - 3);
+      const int64_t src = p < 0 ? -1 - p : 2 * n - 1 - p;
+      if (p >= s0 && p < e0 && src >= s0 && src < e0) {
+        if (WX) bufA[0][p - s0] = bufA[0][src - s0];
+        if (WD) bufA[1][p - s0] = bufA[1][src - s0];
+      }
+    }
+    __syncthreads();
+  }
+  float* in[2] = {bufA[0], bufA[1]};
+  float* outb[2] = {bufB[0], bufB[1]};
+  for (int l = 1; l <= L; ++l) {
+    const int64_t nin = LV.len[l - 1], nout = LV.len[l];
+    const int64_t sin = s[l - 1];
+    const int64_t sl = s[l], el = e[l];
+    const bool odd_in = (nin & 1) != 0;
+    // owned detail range at this level
+    const int64_t own_lo = a << (L - l);
+    const int64_t own_hi = last_block ? nout : (b << (L - l));
+    const int64_t c_lo = sl > 0 ? sl : 0;
+    const int64_t c_hi = el < nout ? el : nout;
+    for (int64_t o = c_lo + threadIdx.x; o < c_hi; o += 256) {
+      const bool lo_odd = odd_in && (o == nout - 1);
+      const bool own = (o >= own_lo && o < own_hi);
+      if (WX) {
+        if (l < L) outb[0][o - sl] = conv4(in[0], sin, o, c_dec_lo, lo_odd);
+        if (own) cx[LV.doff[l] + o] = conv4(in[0], sin, o, c_dec_hi, lo_odd);
+        if (l == L && own) cx[o] = conv4(in[0], sin, o, c_dec_lo, lo_odd);
+      }
+      if (WD) {
+        if (l < L) outb[1][o - sl] = conv4(in[1], sin, o, c_dec_lo, lo_odd);
+        if (own) {
+          const float dv = conv4(in[1], sin, o, c_dec_hi, lo_odd);
+          if (ACCUM) cd[LV.doff[l] + o] = cd[LV.doff[l] + o] + dv; else cd[LV.doff[l] + o] = dv;
+        }
+        if (l == L && own) {
+          const float av = conv4(in[1], sin, o, c_dec_lo, lo_odd);
+          if (ACCUM) cd[o] = cd[o] + av; else cd[o] = av;
+        }
+      }
+    }
+    if (l == L) break;
+    __syncthreads();
+    if (threadIdx.x < 6) {
+      const int64_t p = threadIdx.x < 3 ? -1 - (int64_t)threadIdx.x : nout + (threadIdx.x - 3);
+      const int64_t src = p < 0 ? -1 - p : 2 * nout - 1 - p;
+      if (p >= sl && p < el && src >= sl && src < el) {
+        if (WX) outb[0][p - sl] = outb[0][src - sl];
+        if (WD) outb[1][p - sl] = outb[1][src - sl];
+      }
+    }
+    __syncthreads();
+    float* t0 = in[0]; in[0] = outb[0]; outb[0] = t0;
+    float* t1 = in[1]; in[1] = outb[1]; outb[1] = t1;
+  }
+}
+
+// Inverse: block owns final outputs [c, d) (multiple of IDWT_TILE).
+__global__ void __launch_bounds__(256) idwt_kernel(const float* __restrict__ coeffs, Levels LV,
+                                                   float* __restrict__ out) {
+  constexpr int SPANI = IDWT_TILE / 2 + 16;
+  __shared__ __attribute__((aligned(16))) float A[SPANI];
+  __shared__ __attribute__((aligned(16))) float B[SPANI];
+  const int L = LV.level;
+  const int64_t n = LV.len[0];
+  const int64_t c = (int64_t)blockIdx.x * IDWT_TILE;
+  const int64_t d = (c + IDWT_TILE < n) ? c + IDWT_TILE : n;
+  int64_t cl[DWT_MAX_LEVEL + 1], dl[DWT_MAX_LEVEL + 1];
+  cl[0] = c;
+  dl[0] = d;
+  for (int l = 1; l <= L; ++l) {
+    cl[l] = cl[l - 1] >> 1;
+    dl[l] = ((dl[l - 1] - 1) >> 1) + 2;
+    if (dl[l] > LV.len[l]) dl[l] = LV.len[l];
+  }
+  // level L approximation
+  for (int64_t p = cl[L] + threadIdx.x; p < dl[L]; p += 256) A[p - cl[L]] = coeffs[p];
+  __syncthreads();
+  float* a = A;
+  float* bnext = B;
+  const float r0 = c_rec_lo[0], r1 = c_rec_lo[1], r2 = c_rec_lo[2], r3 = c_rec_lo[3];
+  const float h0 = c_rec_hi[0], h1 = c_rec_hi[1], h2 = c_rec_hi[2], h3 = c_rec_hi[3];
+  for (int l = L; l >= 1; --l) {
+    const float* dd = coeffs + LV.doff[l];
+    const int64_t ca = cl[l];
+    const int64_t q_lo = cl[l - 1];
+    int64_t q_hi = dl[l - 1];
+    if (q_hi > LV.len[l - 1]) q_hi = LV.len[l - 1];
+    for (int64_t q = q_lo + threadIdx.x; q < q_hi; q += 256) {
+      const int64_t m = q >> 1;
+      const float am = a[m - ca], am1 = a[m + 1 - ca];
+      const float dm = dd[m], dm1 = dd[m + 1];
+      float ya, yd;
+      if ((q & 1) == 0) {
+        ya = r0 * am1; ya = ya + r2 * am;
+        yd = h0 * dm1; yd = yd + h2 * dm;
+      } else {
+        ya = r1 * am1; ya = ya + r3 * am;
+        yd = h1 * dm1; yd = yd + h3 * dm;
+      }
+      const float y = ya + yd;
+      if (l == 1) out[q] = y; else bnext[q - q_lo] = y;
+    }
+    if (l == 1) break;
+    __syncthreads();
+    float* t = a; a = bnext; bnext = t;
+  }
+}
+
+static int dwt_levels_ok(int64_t n, int level) {
+  if (level < 1 || level > DWT_MAX_LEVEL || n <= 0) return 0;
+  int64_t len = n;
+  for (int l = 1; l <= level; ++l) {
+    if (len < 4) return 0;
+    len = (len + 3) / 2;
+  }
+  return 1;
+}
+
+}  // namespace dpz
+
+using namespace dpz;
+
+extern "C" int64_t dpz_wavedec_len(int64_t n, int level) {
+  if (!dwt_levels_ok(n, level)) return -1;
+  return make_levels(n, level).total;
+}
+
+extern "C" int dpz_dwt_sym2(const float* x, const float* x0, int64_t n, int level,
+                            float* coeffs_x, float* coeffs_diff, int accumulate,
+                            dpz_stream_t stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!x || n <= 0) return DPZ_ERR_ARG;
+  if (!dwt_levels_ok(n, level) || level > 4) return DPZ_ERR_UNSUPPORTED;
+  if (coeffs_diff && !x0) return DPZ_ERR_ARG;
+  if (!coeffs_x && !coeffs_diff) return DPZ_OK;
+  const Levels LV = make_levels(n, level);
+  const unsigned grid = (unsigned)((LV.len[level] + DWT_TL - 1) / DWT_TL);
+  constexpr int SPAN0 = 16 * DWT_TL + 64, SPAN1 = 8 * DWT_TL + 32;
+  const size_t shm = 2 * (SPAN0 + SPAN1) * sizeof(float);
+  const bool wx = coeffs_x != nullptr, wd = coeffs_diff != nullptr;
+  if (wx && wd) {
+    if (accumulate) dwt_kernel<true, true, true><<<grid, 256, shm, st>>>(x, x0, LV, coeffs_x, coeffs_diff);
+    else dwt_kernel<true, true, false><<<grid, 256, shm, st>>>(x, x0, LV, coeffs_x, coeffs_diff);
+  } else if (wx) {
+    dwt_kernel<true, false, false><<<grid, 256, shm, st>>>(x, x0, LV, coeffs_x, nullptr);
+  } else {
+    if (accumulate) dwt_kernel<false, true, true><<<grid, 256, shm, st>>>(x, x0, LV, nullptr, coeffs_diff);
+    else dwt_kernel<false, true, false><<<grid, 256, shm, st>>>(x, x0, LV, nullptr, coeffs_diff);
+  }
+  DPZ_LAUNCH_CHECK();
+  return DPZ_OK;
+}
+
+extern "C" int dpz_idwt_sym2(const float* coeffs, int64_t n, int level, float* out,
+                             dpz_stream_t stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!coeffs || !out || n <= 0) return DPZ_ERR_ARG;
+  if (!dwt_levels_ok(n, level)) return DPZ_ERR_UNSUPPORTED;
+  const Levels LV = make_levels(n, level);
+  const unsigned grid = (unsigned)((n + IDWT_TILE - 1) / IDWT_TILE);
+  idwt_kernel<<<grid, 256, 0, st>>>(coeffs, LV, out);
+  DPZ_LAUNCH_CHECK();
+  return DPZ_OK;
+}

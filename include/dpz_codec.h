@@ -1,0 +1,116 @@
+/*
+ * dpz_codec.h — C ABI of the MI355X-native decentralizepy model-update codec (libdpzcodec.so).
+ *
+ * Every pointer argument is caller-owned DEVICE memory (e.g. torch.Tensor.data_ptr() of a
+ * CUDA/HIP tensor) unless the comment says "host".  `stream` is a hipStream_t (NULL = default
+ * stream).  Every entry point returns an int status: 0 = success, a hipError_t value for HIP
+ * failures, or one of the DPZ_ERR_* codes below.  No entry point allocates device memory:
+ * workspace is sized by the *_workspace_bytes() queries and passed in by the caller.
+ * Entry points are reentrant; the library holds no mutable global state.
+ *
+ * Each function names the reference (sacs-epfl/decentralizepy, src/decentralizepy/...) code it
+ * replaces.  The reference itself has no native layer: these replace ATen-CPU / PyWavelets /
+ * numpy call sites inside its Sharing and Compression plugins (see INTEGRATION.md for the
+ * ctypes binding and DESIGN.md for the kernels behind each call).
+ */
+#ifndef DPZ_CODEC_H
+#define DPZ_CODEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* dpz_stream_t; /* hipStream_t */
+
+/* ---- status codes ------------------------------------------------------------------------ */
+#define DPZ_OK 0
+#define DPZ_ERR_ARG 1001         /* invalid argument (null pointer, negative size, k > n, ...) */
+#define DPZ_ERR_WORKSPACE 1002   /* workspace smaller than the matching *_workspace_bytes()   */
+#define DPZ_ERR_UNSUPPORTED 1003 /* size/config outside what the kernels implement            */
+#define DPZ_ERR_INTERNAL 1004    /* an internal consistency check failed on the device        */
+
+/* ---- key modes for top-k: how the selection key is formed (reference PartialModel.py:305-331)
+ *   DPZ_ACC_NONE       change = x - x0              key = |change|
+ *   DPZ_ACC_ACCUMULATE acc += change (written back)  key = |acc|           (:321-325)
+ *   DPZ_ACC_ADD        key = |change + acc|, acc unchanged before the rewind (:326-329)
+ * With x0 == NULL, change = x (x is already a change vector, e.g. W(x - x0) for JWINS).      */
+#define DPZ_ACC_NONE 0
+#define DPZ_ACC_ACCUMULATE 1
+#define DPZ_ACC_ADD 2
+
+/* ---- top-k flags ---- */
+#define DPZ_TOPK_EXACT 0x1 /* force the exact multi-pass radix path (skip the sampled path)  */
+#define DPZ_TOPK_ASYNC 0x2 /* enqueue only; the caller must call dpz_topk_complete() later   */
+
+/* ---- fold flags ---- */
+#define DPZ_FOLD_SELF 0x1         /* add the local term w_self*local after the payloads        */
+#define DPZ_FOLD_REPLACE_ONLY 0x2 /* out = local with payload[0] values replaced (no weights)  */
+
+int dpz_abi_version(void);
+const char* dpz_error_string(int code);
+
+/* Top-k magnitude encode.
+ * Replaces reference sharing/PartialModel.py:164-255 (extract_top_gradients: abs + torch.topk +
+ * torch.sort; serialized_model: shared_parameters_counter[idx] += 1, rewind_accumulation(idx)
+ * (models/Model.py:53-64), values pre_share_model[idx]) and sharing/JWINS/Wavelet.py:142-197
+ * (apply_wavelet + the same bookkeeping on wavelet coefficients).
+ * Selects the k largest keys (see DPZ_ACC_*), ties at the k-th key broken by lowest index,
+ * and writes them in ascending index order:  idx_out[j] (int32), val_out[j] = vals_src[idx_out[j]].
+ * Side effects: counter[idx] += 1 if counter != NULL; acc[idx] = 0 if acc != NULL and
+ * acc_mode != DPZ_ACC_NONE; acc += change everywhere first when acc_mode == DPZ_ACC_ACCUMULATE.
+ * n < 2^31, 0 <= k <= n.  Without DPZ_TOPK_ASYNC the call blocks until the result is final.    */
+size_t dpz_topk_workspace_bytes(int64_t n, int64_t k);
+int dpz_topk_encode(const float* x, const float* x0, float* acc, int acc_mode,
+                    const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
+                    float* val_out, int32_t* counter, void* ws, size_t ws_bytes, int flags,
+                    dpz_stream_t stream);
+/* Completes a DPZ_TOPK_ASYNC encode issued with the SAME arguments: synchronises `stream`,
+ * and if the sampled path reported a miss, re-runs the selection exactly (blocking).
+ * *used_fallback (host, may be NULL) is set to 1 when that happened.                         */
+int dpz_topk_complete(const float* x, const float* x0, float* acc, int acc_mode,
+                      const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
+                      float* val_out, int32_t* counter, void* ws, size_t ws_bytes,
+                      int* used_fallback, dpz_stream_t stream);
+
+/* Batched decode + Metro-Hastings fold over n_payloads neighbour payloads.
+ * Replaces reference sharing/PartialModel.py:257-303 (T = cat(local); T[idx] = params),
+ * sharing/Sharing.py:156-229 (_averaging / _averaging_server fold) and
+ * sharing/JWINS/Wavelet.py:269-309, 336-366 (the same fold on wavelet coefficients).
+ *   out[j] = fl( ... fl(fl(t_0[j]*w[0]) + fl(t_1[j]*w[1])) ... + fl(local[j]*w_self) )
+ *   t_i[j] = vals[i][m] if idx[i][m] == j for some m, else local[j]  (idx[i] == NULL: dense,
+ *   t_i = vals[i]).  The local term is present only with DPZ_FOLD_SELF.
+ * idx/vals/k/w are HOST arrays of length n_payloads holding DEVICE pointers / sizes / fp32
+ * weights; each idx[i] must be strictly ascending.  out may not alias local.
+ * DPZ_FOLD_REPLACE_ONLY: n_payloads == 1, out = t_0 (no multiply).                           */
+int dpz_decode_average(const float* local, int64_t n, int n_payloads, const int32_t* const* idx,
+                       const float* const* vals, const int64_t* k, const float* w, float w_self,
+                       int flags, float* out, dpz_stream_t stream);
+
+/* Multilevel sym2 DWT, mode "symmetric", fp32, pywt-1.1.1-exact summation order.
+ * Replaces reference sharing/JWINS/Wavelet.py:12-32 (pywt.wavedec + coeffs_to_array).
+ * coeffs layout: [cA_L, cD_L, ..., cD_1], length dpz_wavedec_len(n, level).
+ *   coeffs_x    (may be NULL) = W(x)
+ *   coeffs_diff (may be NULL) = W(x - x0)   (x0 must be non-NULL), or += W(x - x0) when
+ *   accumulate != 0 (PartialModel._post_step acc += T(init - prev), PartialModel.py:346-349).
+ * Requires every level input length >= 4.                                                      */
+int64_t dpz_wavedec_len(int64_t n, int level);
+int dpz_dwt_sym2(const float* x, const float* x0, int64_t n, int level, float* coeffs_x,
+                 float* coeffs_diff, int accumulate, dpz_stream_t stream);
+
+/* Multilevel sym2 IDWT (pywt.array_to_coeffs + pywt.waverec), first n outputs written.
+ * Replaces reference sharing/JWINS/Wavelet.py:311-316.                                        */
+int dpz_idwt_sym2(const float* coeffs, int64_t n, int level, float* out, dpz_stream_t stream);
+
+/* fp16 value packing (round-to-nearest-even, torch.half semantics) and unpacking.
+ * The build's own wire codec for values (BASELINE config C5); the reference's lossy float path
+ * is fpzip (compression/EliasFpzipLossy.py:14-58), which is not byte-compatible.             */
+int dpz_pack_fp16(const float* in, int64_t n, uint16_t* out, dpz_stream_t stream);
+int dpz_unpack_fp16(const uint16_t* in, int64_t n, float* out, dpz_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPZ_CODEC_H */

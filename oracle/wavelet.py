@@ -1,0 +1,113 @@
+"""Oracle: pywt-exact fp32 sym2 multilevel DWT / IDWT — TEST INFRASTRUCTURE ONLY.
+
+The reference calls PyWavelets (third-party, not vendored):
+
+* ``change_transformer_wavelet``  reference ``sharing/JWINS/Wavelet.py:12-32``:
+  ``pywt.wavedec(x, "sym2", level=4)`` (mode "symmetric") then ``pywt.coeffs_to_array`` ->
+  the 1-D concatenation ``[cA_L, cD_L, ..., cD_1]``.
+* ``Wavelet._averaging``          reference ``sharing/JWINS/Wavelet.py:311-316``:
+  ``pywt.array_to_coeffs`` + ``pywt.waverec``; the caller keeps the first N outputs.
+
+Dependency: PyWavelets 1.1.1 (the build present in this image's /opt/conda python3.9; the
+reference's setup.cfg pins no version).  Its published C algorithm
+(``downsampling_convolution`` / ``upsampling_convolution_valid_sf``) is restated below with the
+exact fp32 summation order, verified bit-for-bit against pywt 1.1.1 by
+``tests/golden/make_golden.py`` (fixtures ``tests/golden/wavelet_*.npz``):
+
+forward, output o (input position i = 2o+1), half-sample symmetric extension
+``x~[-1-m] = x[m]``, ``x~[n+m] = x[n-1-m]``::
+
+    out[o] = ((f0*x~[i] + f1*x~[i-1]) + f2*x~[i-2]) + f3*x~[i-3]
+
+except the last output when n is odd (i = n+2), where pywt's right-overhang loop visits the
+extension first::
+
+    out[last] = ((f2*x~[n] + f1*x~[n+1]) + f0*x~[n+2]) + f3*x~[n-1]
+
+inverse (valid part, F/2 = 2 taps per phase), for m in [0, n-1)::
+
+    y[2m+p] = (r[p]*a[m+1] + r[p+2]*a[m]) + (h[p]*d[m+1] + h[p+2]*d[m])
+
+(approximation branch summed first into the zeroed output, detail branch added after).
+"""
+import numpy as np
+
+# sym2 filter bank (pywt 1.1.1 ``Wavelet('sym2')``), as the fp32 casts pywt uses for fp32 data.
+DEC_LO = np.array([-0.12940952255092145, 0.22414386804185735,
+                   0.836516303737469, 0.48296291314469025], dtype=np.float32)
+DEC_HI = np.array([-0.48296291314469025, 0.836516303737469,
+                   -0.22414386804185735, -0.12940952255092145], dtype=np.float32)
+REC_LO = DEC_LO[::-1].copy()
+REC_HI = DEC_HI[::-1].copy()
+
+F = 4
+
+
+def level_lengths(n, level):
+    """[n_0=n, n_1, ..., n_L] with n_l = floor((n_{l-1} + F - 1) / 2)."""
+    lens = [int(n)]
+    for _ in range(level):
+        lens.append((lens[-1] + F - 1) // 2)
+    return lens
+
+
+def coeff_len(n, level):
+    """Length M of ``coeffs_to_array(wavedec(x))`` for a length-n input."""
+    lens = level_lengths(n, level)
+    return lens[level] + sum(lens[1:])
+
+
+def _dwt1(x, flt):
+    x = np.asarray(x, dtype=np.float32)
+    n = x.shape[0]
+    if n < F:
+        raise ValueError("oracle dwt needs n >= 4 at every level")
+    nout = (n + F - 1) // 2
+    xe = np.empty(n + 6, dtype=np.float32)       # x~[-3 .. n+2] at offset 3
+    xe[3:n + 3] = x
+    xe[0:3] = x[2::-1]
+    xe[n + 3:n + 6] = x[n - 1:n - 4:-1]
+    f0, f1, f2, f3 = (np.float32(v) for v in flt)
+    i = 2 * np.arange(nout) + 1 + 3               # offset into xe
+    out = ((f0 * xe[i] + f1 * xe[i - 1]) + f2 * xe[i - 2]) + f3 * xe[i - 3]
+    if n % 2 == 1:
+        out[-1] = ((f2 * xe[n + 3] + f1 * xe[n + 4]) + f0 * xe[n + 5]) + f3 * xe[n + 2]
+    return out.astype(np.float32)
+
+
+def wavedec_array(x, level=4):
+    """``coeffs_to_array(wavedec(x, 'sym2', level=level))`` as one fp32 vector."""
+    a = np.asarray(x, dtype=np.float32)
+    details = []
+    for _ in range(level):
+        d = _dwt1(a, DEC_HI)
+        a = _dwt1(a, DEC_LO)
+        details.append(d)
+    return np.concatenate([a] + details[::-1]).astype(np.float32)
+
+
+def _idwt1(a, d):
+    n = d.shape[0]
+    if a.shape[0] == n + 1:
+        a = a[:n]
+    assert a.shape[0] == n
+    r0, r1, r2, r3 = (np.float32(v) for v in REC_LO)
+    h0, h1, h2, h3 = (np.float32(v) for v in REC_HI)
+    y = np.empty(2 * n - 2, dtype=np.float32)
+    a1, a0, d1, d0 = a[1:], a[:-1], d[1:], d[:-1]
+    y[0::2] = (r0 * a1 + r2 * a0) + (h0 * d1 + h2 * d0)
+    y[1::2] = (r1 * a1 + r3 * a0) + (h1 * d1 + h3 * d0)
+    return y
+
+
+def waverec_array(coeffs, n, level=4):
+    """``waverec(array_to_coeffs(coeffs))`` truncated to the original length n."""
+    lens = level_lengths(n, level)
+    c = np.asarray(coeffs, dtype=np.float32)
+    pos = lens[level]
+    a = c[:pos]
+    for lvl in range(level, 0, -1):
+        d = c[pos:pos + lens[lvl]]
+        pos += lens[lvl]
+        a = _idwt1(a, d)
+    return a[:n].copy()

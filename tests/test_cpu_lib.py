@@ -1,0 +1,63 @@
+"""CPU-only checks of the C ABI: the library loads and exports every symbol include/*.h declares,
+and the pure-host entry points (size queries, argument validation, error strings) behave."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    syms = set()
+    for fn in os.listdir(os.path.join(ROOT, "include")):
+        if fn.endswith(".h"):
+            text = open(os.path.join(ROOT, "include", fn)).read()
+            text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+            syms.update(re.findall(r"\b(dpz_[a-z0-9_]+)\s*\(", text))
+    return syms
+
+
+def test_library_exports_every_declared_symbol():
+    from decentralizepy_amd import _lib
+    handle = ctypes.CDLL(_lib.LIB_PATH)
+    declared = _declared_symbols()
+    assert len(declared) >= 10
+    missing = [s for s in declared if not hasattr(handle, s)]
+    assert not missing, missing
+    # the ctypes signature table covers exactly the declared API
+    assert set(_lib.SIGNATURES) == declared
+
+
+def test_host_only_entry_points():
+    from decentralizepy_amd import _lib
+    L = _lib.lib()
+    assert L.dpz_abi_version() == 1
+    assert L.dpz_error_string(1001) == b"invalid argument"
+    assert L.dpz_topk_workspace_bytes(11_000_000, 110_000) > 0
+    # wavedec length = pywt coeffs_to_array length (sym2, level 4)
+    from oracle import wavelet as owav
+    for n in [64, 101, 100_000, 11_000_000, 25_000_000]:
+        assert L.dpz_wavedec_len(n, 4) == owav.coeff_len(n, 4)
+    assert L.dpz_wavedec_len(10, 4) == -1  # a level input shorter than the filter
+
+
+def test_argument_validation_without_gpu():
+    from decentralizepy_amd import _lib
+    L = _lib.lib()
+    # k > n and negative n are rejected before any device call
+    rc = L.dpz_topk_encode(None, None, None, 0, None, 10, 11, None, None, None, None, 0, 0, None)
+    assert rc == 1001
+    rc = L.dpz_topk_encode(None, None, None, 0, None, -1, 0, None, None, None, None, 0, 0, None)
+    assert rc == 1001
+    rc = L.dpz_decode_average(None, 10, 0, None, None, None, None, 0.0, 0, None, None)
+    assert rc == 1001
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    from decentralizepy_amd import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _lib.lib()

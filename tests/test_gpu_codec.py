@@ -1,0 +1,298 @@
+"""GPU parity tests: HIP kernels (through the C ABI) vs the CPU oracle on identical inputs.
+
+Bar: bit-exact for index sets, gathered values, counters, accumulators, the fp32 fold and the
+wavelet coefficients (the oracle restates the reference's fp32 operation order exactly).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import fold as ofold
+from oracle import topk as otopk
+from oracle import wavelet as owav
+
+pytestmark = pytest.mark.gpu
+
+
+def _codec():
+    from decentralizepy_amd import codec
+    return codec
+
+
+def _inputs(n, seed, scale=0.01):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, generator=g, dtype=torch.float32)
+    x0 = x - scale * torch.randn(n, generator=g, dtype=torch.float32)
+    return x.numpy(), x0.numpy()
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def _run_encode(dev, x, x0, acc, mode, k, counter=True, exact=False, vals_src=None):
+    codec = _codec()
+    tx = torch.from_numpy(x).to(dev)
+    tx0 = torch.from_numpy(x0).to(dev) if x0 is not None else None
+    tacc = torch.from_numpy(acc.copy()).to(dev) if acc is not None else None
+    tcnt = torch.zeros(x.shape[0], dtype=torch.int32, device=dev) if counter else None
+    tvs = torch.from_numpy(vals_src).to(dev) if vals_src is not None else None
+    ws = codec.Workspace(dev)
+    idx, val = codec.topk_encode(tx, k, x0=tx0, acc=tacc, acc_mode=mode, vals_src=tvs,
+                                 counter=tcnt, workspace=ws, exact=exact)
+    torch.cuda.synchronize()
+    return (idx.cpu().numpy(), val.cpu().numpy(),
+            tacc.cpu().numpy() if tacc is not None else None,
+            tcnt.cpu().numpy() if tcnt is not None else None)
+
+
+def _check_encode(dev, x, x0, acc, mode, k, exact=False, vals_src=None):
+    o_acc = acc.copy() if acc is not None else None
+    o_cnt = np.zeros(x.shape[0], dtype=np.int32)
+    oi, ov = otopk.encode(x, x0, o_acc, mode, k, vals_src=vals_src, counter=o_cnt)
+    gi, gv, gacc, gcnt = _run_encode(dev, x, x0, acc, mode, k, exact=exact, vals_src=vals_src)
+    assert gi.dtype == np.int32 and gi.shape == (k,)
+    np.testing.assert_array_equal(gi, oi)
+    np.testing.assert_array_equal(_bits(gv), _bits(ov))
+    np.testing.assert_array_equal(gcnt, o_cnt)
+    if acc is not None:
+        np.testing.assert_array_equal(_bits(gacc), _bits(o_acc))
+
+
+@pytest.mark.parametrize("n", [1000, 100_003, 1_000_000, 4_194_307])
+@pytest.mark.parametrize("alpha", [0.01, 0.001, 0.1, 0.5])
+@pytest.mark.parametrize("exact", [False, True])
+def test_topk_matches_oracle(dev, n, alpha, exact):
+    x, x0 = _inputs(n, seed=n % 97)
+    k = round(alpha * n)
+    _check_encode(dev, x, x0, None, otopk.ACC_NONE, k, exact=exact)
+
+
+@pytest.mark.parametrize("mode", [otopk.ACC_ACCUMULATE, otopk.ACC_ADD])
+@pytest.mark.parametrize("n", [5000, 1_048_576 + 3])
+def test_topk_accumulation_modes(dev, mode, n):
+    x, x0 = _inputs(n, seed=3)
+    acc = (0.01 * np.random.default_rng(1).standard_normal(n)).astype(np.float32)
+    _check_encode(dev, x, x0, acc, mode, round(0.01 * n))
+
+
+def test_topk_full_size_c2(dev):
+    """configs[1]: N = 11,000,000, k = 1 % — index set bit-exact vs the oracle."""
+    n = 11_000_000
+    x, x0 = _inputs(n, seed=0)
+    _check_encode(dev, x, x0, None, otopk.ACC_NONE, round(0.01 * n))
+
+
+def test_topk_64mib(dev):
+    n = 16_777_216
+    x, x0 = _inputs(n, seed=1)
+    _check_encode(dev, x, x0, None, otopk.ACC_NONE, round(0.01 * n))
+
+
+@pytest.mark.parametrize("k", [0, 1, 2, 999, 1000])
+def test_topk_edge_k(dev, k):
+    n = 1000
+    x, x0 = _inputs(n, seed=5)
+    _check_encode(dev, x, x0, None, otopk.ACC_NONE, k)
+
+
+def test_topk_k0_still_accumulates(dev):
+    n = 4099
+    x, x0 = _inputs(n, seed=6)
+    acc = np.zeros(n, dtype=np.float32)
+    _check_encode(dev, x, x0, acc, otopk.ACC_ACCUMULATE, 0)
+
+
+@pytest.mark.parametrize("n", [3001, 600_000])
+def test_topk_heavy_ties_lowest_index_wins(dev, n):
+    # most of the model unchanged: |change| == 0 for ~99.5 % -> k-th key is 0 with massive ties
+    x, x0 = _inputs(n, seed=7)
+    rng = np.random.default_rng(7)
+    keep = rng.random(n) < 0.995
+    x0 = np.where(keep, x, x0).astype(np.float32)
+    _check_encode(dev, x, x0, None, otopk.ACC_NONE, round(0.01 * n))
+    # quantised changes: many exact duplicates at every magnitude
+    x = np.round(x * 64) / 64
+    x0 = np.round(x0 * 64) / 64
+    _check_encode(dev, x.astype(np.float32), x0.astype(np.float32), None, otopk.ACC_NONE,
+                  round(0.02 * n))
+
+
+def test_topk_nan_inf(dev):
+    n = 300_000
+    x, x0 = _inputs(n, seed=8)
+    x[[5, 100, 2000]] = np.nan
+    x[[7, 50_000]] = np.inf
+    x[[9]] = -np.inf
+    _check_encode(dev, x, x0, None, otopk.ACC_NONE, round(0.01 * n))
+    _check_encode(dev, x, x0, None, otopk.ACC_NONE, 4)
+
+
+def test_topk_unaligned_views(dev):
+    n = 300_001
+    x, x0 = _inputs(n + 1, seed=9)
+    # views starting one element in: not 16-byte aligned -> scalar-load kernels
+    _check_encode(dev, x[1:].copy(), x0[1:].copy(), None, otopk.ACC_NONE, 3000)
+    codec = _codec()
+    tx = torch.from_numpy(x).to(dev)[1:]
+    tx0 = torch.from_numpy(x0).to(dev)[1:]
+    idx, val = codec.topk_encode(tx, 3000, x0=tx0)
+    oi, ov = otopk.encode(x[1:], x0[1:], None, 0, 3000)
+    np.testing.assert_array_equal(idx.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(val.cpu().numpy()), _bits(ov))
+
+
+def test_topk_sampled_miss_falls_back(dev):
+    """Adversarial layout: the large changes sit between the sample chunks, so the sampled window
+    misses the k-th key; the device flags it and the exact path must still give the oracle's set."""
+    codec = _codec()
+    n = 1 << 20
+    k = round(0.01 * n)
+    x = np.zeros(n, dtype=np.float32)
+    x0 = np.zeros(n, dtype=np.float32)
+    rng = np.random.default_rng(11)
+    # sample chunk c covers [c*(n-64)/255, +64): put big changes in the middle of the gaps
+    big = []
+    for c in range(255):
+        s = (c * (n - 64)) // 255 + 64
+        e = ((c + 1) * (n - 64)) // 255
+        big.extend(range(s + 100, min(e - 100, s + 100 + 48)))
+    big = np.array(big)
+    x[:] = 1e-6 * rng.standard_normal(n).astype(np.float32)
+    x[big] = rng.uniform(1.0, 2.0, big.shape[0]).astype(np.float32)
+    tx = torch.from_numpy(x).to(dev)
+    tx0 = torch.from_numpy(x0).to(dev)
+    ws = codec.Workspace(dev)
+    idx, val = codec.topk_encode(tx, k, x0=tx0, workspace=ws, asynchronous=True)
+    used = codec.topk_complete(tx, k, idx, val, ws, x0=tx0)
+    assert used, "the adversarial layout should have forced the exact fallback"
+    oi, ov = otopk.encode(x, x0, None, 0, k)
+    np.testing.assert_array_equal(idx.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(val.cpu().numpy()), _bits(ov))
+
+
+def test_topk_dense_segment(dev):
+    """One segment holds far more candidates than its list capacity -> re-read path."""
+    n = 1 << 21
+    x, x0 = _inputs(n, seed=12)
+    # segment 1 ([4096, 8192) at this size) holds no sample chunk; 2000 large changes there
+    # overflow its candidate list (cap 1024) without moving the sampled window
+    sl = slice(4200, 6200)
+    x[sl] = x0[sl] + 0.2 * np.sign(np.random.default_rng(2).standard_normal(2000)).astype(np.float32)
+    codec = _codec()
+    tx, tx0 = torch.from_numpy(x).to(dev), torch.from_numpy(x0).to(dev)
+    ws = codec.Workspace(dev)
+    k = round(0.01 * n)
+    idx, val = codec.topk_encode(tx, k, x0=tx0, workspace=ws, asynchronous=True)
+    used = codec.topk_complete(tx, k, idx, val, ws, x0=tx0)
+    assert not used, "dense segment should be handled inside the sampled path"
+    _check_encode(dev, x, x0, None, otopk.ACC_NONE, k)
+
+
+def test_topk_wavelet_domain_values(dev):
+    """Selection on a change vector with values gathered from another vector (JWINS layout)."""
+    n = 1_000_009
+    c, w = _inputs(n, seed=13)
+    _check_encode(dev, c, None, None, otopk.ACC_NONE, round(0.1 * n), vals_src=w)
+    _check_encode(dev, c, None, None, otopk.ACC_NONE, round(0.01 * n), vals_src=w)
+
+
+# ---------------------------------------------------------------------------------------------
+# decode + fold
+
+def _payload(n, k, seed, local):
+    rng = np.random.default_rng(seed)
+    idx = np.sort(rng.choice(n, size=k, replace=False)).astype(np.int32)
+    vals = (local[idx] + 0.05 * rng.standard_normal(k)).astype(np.float32)
+    return idx, vals
+
+
+@pytest.mark.parametrize("n", [1000, 1_000_003, 11_000_000])
+@pytest.mark.parametrize("npay", [1, 3, 16, 20])
+def test_fold_matches_oracle(dev, n, npay):
+    codec = _codec()
+    rng = np.random.default_rng(n + npay)
+    local = rng.standard_normal(n).astype(np.float32)
+    pays, tpays, degrees = [], [], []
+    for i in range(npay):
+        if i == 1:  # one dense (full-model) payload in the mix
+            vals = rng.standard_normal(n).astype(np.float32)
+            pays.append((None, vals))
+            tpays.append((None, torch.from_numpy(vals).to(dev)))
+        else:
+            idx, vals = _payload(n, max(1, n // 100), seed=i, local=local)
+            pays.append((idx, vals))
+            tpays.append((torch.from_numpy(idx).to(dev), torch.from_numpy(vals).to(dev)))
+        degrees.append(int(rng.integers(1, 20)))
+    weights = [ofold.mh_weight(npay, d) for d in degrees]
+    w_self = 1 - sum(weights)
+    ref = ofold.fold(local, pays, weights, w_self)
+    tl = torch.from_numpy(local).to(dev)
+    out = codec.decode_average(tl, tpays, weights, w_self).cpu().numpy()
+    np.testing.assert_array_equal(_bits(out), _bits(ref))
+    # server variant: no self term
+    ref2 = ofold.fold(local, pays, [1 / npay] * npay, None)
+    out2 = codec.decode_average(tl, tpays, [1 / npay] * npay, None).cpu().numpy()
+    np.testing.assert_array_equal(_bits(out2), _bits(ref2))
+
+
+@pytest.mark.parametrize("n,k", [(1000, 10), (1000, 0), (1000, 1000), (11_000_000, 110_000)])
+def test_replace_matches_oracle(dev, n, k):
+    codec = _codec()
+    rng = np.random.default_rng(k)
+    local = rng.standard_normal(n).astype(np.float32)
+    idx, vals = _payload(n, k, seed=1, local=local)
+    ref = ofold.replace(local, idx, vals)
+    out = codec.replace(torch.from_numpy(local).to(dev), torch.from_numpy(idx).to(dev),
+                        torch.from_numpy(vals).to(dev)).cpu().numpy()
+    np.testing.assert_array_equal(_bits(out), _bits(ref))
+
+
+def test_encode_decode_roundtrip_property(dev):
+    """Full-size property: decode(encode(x)) equals x on the selected set and local elsewhere."""
+    codec = _codec()
+    n = 16_777_216
+    x, x0 = _inputs(n, seed=21)
+    tx, tx0 = torch.from_numpy(x).to(dev), torch.from_numpy(x0).to(dev)
+    idx, val = codec.topk_encode(tx, round(0.01 * n), x0=tx0)
+    out = codec.replace(tx0, idx, val)
+    sel = torch.zeros(n, dtype=torch.bool, device=dev)
+    sel[idx.long()] = True
+    assert torch.equal(out[sel], tx[sel])
+    assert torch.equal(out[~sel], tx0[~sel])
+    assert bool((idx[1:] > idx[:-1]).all())
+
+
+# ---------------------------------------------------------------------------------------------
+# wavelet
+
+@pytest.mark.parametrize("n", [64, 65, 66, 67, 101, 1001, 4096, 100_003, 1_000_000, 11_000_001,
+                               25_000_000])
+def test_wavedec_waverec_bit_exact(dev, n):
+    codec = _codec()
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal(n).astype(np.float32)
+    x0 = (x - 0.01 * rng.standard_normal(n)).astype(np.float32)
+    tx, tx0 = torch.from_numpy(x).to(dev), torch.from_numpy(x0).to(dev)
+    wx, wd = codec.wavedec(tx, 4, x0=tx0)
+    np.testing.assert_array_equal(_bits(wx.cpu().numpy()), _bits(owav.wavedec_array(x)))
+    np.testing.assert_array_equal(_bits(wd.cpu().numpy()), _bits(owav.wavedec_array(x - x0)))
+    # accumulate: acc += W(x - x0)
+    acc = (0.01 * rng.standard_normal(wx.numel())).astype(np.float32)
+    tacc = torch.from_numpy(acc).to(dev)
+    codec.wavedec(tx, 4, x0=tx0, want_x=False, coeffs_diff=tacc, accumulate=True)
+    np.testing.assert_array_equal(_bits(tacc.cpu().numpy()),
+                                  _bits(acc + owav.wavedec_array(x - x0)))
+    rec = codec.waverec(wx, n, 4).cpu().numpy()
+    np.testing.assert_array_equal(_bits(rec), _bits(owav.waverec_array(owav.wavedec_array(x), n)))
+
+
+def test_fp16_pack_roundtrip(dev):
+    codec = _codec()
+    for n in [1, 7, 8, 9, 1_000_003]:
+        x = (np.random.default_rng(n).standard_normal(n) * 10).astype(np.float32)
+        h = codec.pack_fp16(torch.from_numpy(x).to(dev))
+        ref = torch.from_numpy(x).half()
+        assert torch.equal(h.cpu().view(torch.int16), ref.view(torch.int16))
+        back = codec.unpack_fp16(h).cpu()
+        assert torch.equal(back, ref.float())
