@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdpzcodec.so")
+# DPZ_CODEC_LIB selects an alternative build (e.g. the stamped diagnostic build of tools/stamps.py)
+LIB_PATH = os.environ.get("DPZ_CODEC_LIB") or os.path.join(_HERE, "libdpzcodec.so")
 
 DPZ_ACC_NONE = 0
 DPZ_ACC_ACCUMULATE = 1
@@ -33,10 +34,11 @@ SIGNATURES = {
     "dpz_topk_complete": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64, _i64,
                                  _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
                                  ctypes.POINTER(_int), _c_void_p]),
+    "dpz_decode_workspace_bytes": (_size, [_i64, _int]),
     "dpz_decode_average": (_int, [_c_void_p, _i64, _int, ctypes.POINTER(_c_void_p),
                                   ctypes.POINTER(_c_void_p), ctypes.POINTER(_i64),
                                   ctypes.POINTER(ctypes.c_float), ctypes.c_float, _int, _c_void_p,
-                                  _c_void_p]),
+                                  _c_void_p, _size, _c_void_p]),
     "dpz_wavedec_len": (_i64, [_i64, _int]),
     "dpz_dwt_sym2": (_int, [_c_void_p, _c_void_p, _i64, _int, _c_void_p, _c_void_p, _int,
                             _c_void_p]),

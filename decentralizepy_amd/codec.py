@@ -37,18 +37,28 @@ def _require(t, dtype, name):
 
 
 class Workspace:
-    """Caller-owned scratch for the top-k encoder, reused across calls (sized per n)."""
+    """Caller-owned device scratch for the encoder and the decoder, reused across calls.
+
+    The top-k workspace must be zero-filled before its first use (the library keeps it so
+    afterwards), hence ``torch.zeros``.
+    """
 
     def __init__(self, device):
         self.device = torch.device(device)
         self.buf = None
-        self.n = -1
+        self.dbuf = None
 
     def get(self, n, k):
         need = int(_lib.lib().dpz_topk_workspace_bytes(int(n), int(k)))
         if self.buf is None or self.buf.numel() < need:
-            self.buf = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+            self.buf = torch.zeros(max(need, 256), dtype=torch.uint8, device=self.device)
         return self.buf
+
+    def get_decode(self, n, n_payloads):
+        need = int(_lib.lib().dpz_decode_workspace_bytes(int(n), int(n_payloads)))
+        if self.dbuf is None or self.dbuf.numel() < need:
+            self.dbuf = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+        return self.dbuf
 
 
 def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, counter=None,
@@ -97,7 +107,8 @@ def topk_complete(x, k, idx_out, val_out, workspace, x0=None, acc=None, acc_mode
     return bool(fb.value)
 
 
-def decode_average(local, payloads, weights=None, w_self=None, out=None, replace_only=False):
+def decode_average(local, payloads, weights=None, w_self=None, out=None, replace_only=False,
+                   workspace=None):
     """Batched replace + Metro-Hastings fold (reference Sharing.py:156-229, PartialModel.py:257-303).
 
     payloads : list of ``(idx int32 device tensor or None, vals fp32 device tensor)``
@@ -117,21 +128,26 @@ def decode_average(local, payloads, weights=None, w_self=None, out=None, replace
     for i, (idx, vals) in enumerate(payloads):
         _require(idx, torch.int32, "idx")
         _require(vals, torch.float32, "vals")
+        if idx is not None and idx.numel() != vals.numel():
+            raise ValueError("payload idx and vals differ in length")
+        if idx is None and vals.numel() != n:
+            raise ValueError("a dense payload (idx=None) must hold n values")
         idx_arr[i] = idx.data_ptr() if idx is not None else None
         val_arr[i] = vals.data_ptr()
         k_arr[i] = vals.numel()
         w_arr[i] = float(weights[i]) if weights is not None else 1.0
     flags = (DPZ_FOLD_SELF if w_self is not None else 0) | (DPZ_FOLD_REPLACE_ONLY if replace_only else 0)
+    ws = (workspace or Workspace(local.device)).get_decode(n, npay)
     rc = _lib.lib().dpz_decode_average(_ptr(local), n, npay, idx_arr, val_arr, k_arr, w_arr,
                                        float(w_self) if w_self is not None else 0.0, flags,
-                                       _ptr(out), _stream(local.device))
+                                       _ptr(out), _ptr(ws), ws.numel(), _stream(local.device))
     check(rc, "dpz_decode_average")
     return out
 
 
-def replace(local, idx, vals, out=None):
+def replace(local, idx, vals, out=None, workspace=None):
     """``T = local.clone(); T[idx] = vals`` (reference PartialModel.py:292-295)."""
-    return decode_average(local, [(idx, vals)], out=out, replace_only=True)
+    return decode_average(local, [(idx, vals)], out=out, replace_only=True, workspace=workspace)
 
 
 def wavedec_len(n, level=4):

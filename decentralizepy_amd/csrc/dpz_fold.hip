@@ -6,18 +6,26 @@
 //   sharing/Sharing.py:200-229       _averaging_server: w = 1/n, no self term
 //   sharing/JWINS/Wavelet.py:269-309 the same fold on wavelet coefficients
 //
-// One block owns a 4096-element tile of the output.  For each payload (in payload order) the
-// block locates its index range by binary search (idx is strictly ascending), scatters the hits
-// into an LDS value tile tagged with the payload number, and every thread folds its 16 elements:
-//   t = (tag == p) ? hit : local;  total = (p == 0) ? t*w : total + t*w
-// in exactly the reference's fp32 order (compiled with -ffp-contract=off: no FMA contraction).
-// Bytes per element: read local (4) + write out (4) + 8 per payload hit -> HBM-bound.
+// Two launches per group of <= 16 payloads:
+//  * fold_offsets_kernel: one thread per payload entry writes, for every 4096-element output tile
+//    that starts after the previous entry, the first entry index inside that tile
+//    (start[p][t] = lower_bound(idx_p, t*4096)).  Coalesced over idx; replaces a dependent
+//    binary search per tile.
+//  * fold_kernel: one block per output tile.  For each payload in payload order the block
+//    scatters the tile's hits into an LDS value tile tagged with the payload number, and every
+//    thread folds its 16 elements:
+//      t = (tag == p) ? hit : local;  total = (p == 0) ? t*w : total + t*w
+//    in exactly the reference's fp32 order (library compiled with -ffp-contract=off).
+// Algorithmic bytes: read local (4N) + write out (4N) + 8 bytes per payload entry.
 #include "dpz_common.h"
 
 namespace dpz {
 
-constexpr int FOLD_TILE = 4096;
+constexpr int FOLD_TILE_SHIFT = 12;
+constexpr int FOLD_TILE = 1 << FOLD_TILE_SHIFT;
 constexpr int FOLD_MAXP = 16;  // payloads per launch (longer lists are chained)
+constexpr int FOLD_THREADS = 512;
+constexpr int FOLD_GROUPS = FOLD_TILE / (4 * FOLD_THREADS);  // float4 groups per thread
 
 struct FoldPayload {
   const int32_t* idx;  // nullptr: dense payload (vals has n entries)
@@ -29,7 +37,9 @@ struct FoldPayload {
 struct FoldArgs {
   const float* local;
   float* out;
+  const int32_t* starts;  // [np][ntiles + 1]
   int64_t n;
+  int64_t ntiles;
   int np;
   int first;        // total starts from payload 0 (else continue from out)
   int add_self;     // add local * w_self at the end
@@ -38,39 +48,46 @@ struct FoldArgs {
   FoldPayload p[FOLD_MAXP];
 };
 
-__device__ __forceinline__ int64_t lower_bound_i32(const int32_t* a, int64_t len, int64_t v) {
-  int64_t lo = 0, hi = len;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if ((int64_t)a[mid] < v) lo = mid + 1; else hi = mid;
-  }
-  return lo;
+// grid (ceil((kmax+1)/256), np): thread j of payload p handles entry j (j == k: end sentinel).
+__global__ void __launch_bounds__(256) fold_offsets_kernel(FoldArgs a, int32_t* starts) {
+  const int p = blockIdx.y;
+  const FoldPayload& P = a.p[p];
+  if (!P.idx) return;
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t k = P.k;
+  if (j > k) return;
+  const int64_t tprev = j == 0 ? -1 : ((int64_t)P.idx[j - 1] >> FOLD_TILE_SHIFT);
+  int64_t tcur = j == k ? a.ntiles : ((int64_t)P.idx[j] >> FOLD_TILE_SHIFT);
+  if (tcur > a.ntiles) tcur = a.ntiles;
+  int32_t* st = starts + (int64_t)p * (a.ntiles + 1);
+  for (int64_t t = tprev + 1; t <= tcur; ++t) st[t] = (int32_t)j;
 }
 
 template <bool VEC>
-__global__ void __launch_bounds__(256) fold_kernel(FoldArgs a) {
+__global__ void __launch_bounds__(FOLD_THREADS) fold_kernel(FoldArgs a) {
   __shared__ __attribute__((aligned(16))) float hv[FOLD_TILE];
   __shared__ __attribute__((aligned(16))) uint8_t htag[FOLD_TILE];
-  __shared__ int64_t rng[FOLD_MAXP][2];
-  const int64_t tlo = (int64_t)blockIdx.x * FOLD_TILE;
+  __shared__ int32_t rng[FOLD_MAXP][2];
+  const int64_t tile = blockIdx.x;
+  const int64_t tlo = tile * FOLD_TILE;
   const int64_t thi = (tlo + FOLD_TILE < a.n) ? tlo + FOLD_TILE : a.n;
   const int t = threadIdx.x;
   if (t < a.np) {
-    const FoldPayload& P = a.p[t];
-    if (P.idx) {
-      rng[t][0] = lower_bound_i32(P.idx, P.k, tlo);
-      rng[t][1] = lower_bound_i32(P.idx, P.k, thi);
+    if (a.p[t].idx) {
+      const int32_t* st = a.starts + (int64_t)t * (a.ntiles + 1);
+      rng[t][0] = st[tile];
+      rng[t][1] = st[tile + 1];
     } else {
       rng[t][0] = rng[t][1] = 0;
     }
   }
-  for (int j = t * 4; j < FOLD_TILE; j += 1024) *reinterpret_cast<uint32_t*>(&htag[j]) = 0xFFFFFFFFu;
+  for (int j = t * 4; j < FOLD_TILE; j += 4 * FOLD_THREADS) *reinterpret_cast<uint32_t*>(&htag[j]) = 0xFFFFFFFFu;
 
   // this thread's elements: q-th group = tlo + q*1024 + 4t .. +3
-  float L[16], acc[16];
+  float L[4 * FOLD_GROUPS], acc[4 * FOLD_GROUPS];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int64_t i0 = tlo + q * 1024 + t * 4;
+  for (int q = 0; q < FOLD_GROUPS; ++q) {
+    const int64_t i0 = tlo + q * 4 * FOLD_THREADS + t * 4;
     if (VEC && i0 + 3 < thi) {
       float4 v = *reinterpret_cast<const float4*>(a.local + i0);
       L[q * 4 + 0] = v.x; L[q * 4 + 1] = v.y; L[q * 4 + 2] = v.z; L[q * 4 + 3] = v.w;
@@ -93,7 +110,7 @@ __global__ void __launch_bounds__(256) fold_kernel(FoldArgs a) {
     __syncthreads();  // previous payload's reads of hv/htag done; rng visible
     if (P.idx) {
       const int64_t b = rng[p][0], e = rng[p][1];
-      for (int64_t j = b + t; j < e; j += 256) {
+      for (int64_t j = b + t; j < e; j += FOLD_THREADS) {
         const int64_t pos = (int64_t)P.idx[j] - tlo;
         if (pos >= 0 && pos < FOLD_TILE) {  // guards against an unsorted caller array
           hv[pos] = P.val[j];
@@ -104,8 +121,8 @@ __global__ void __launch_bounds__(256) fold_kernel(FoldArgs a) {
     __syncthreads();
     const float w = P.w;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j0 = q * 1024 + t * 4;
+    for (int q = 0; q < FOLD_GROUPS; ++q) {
+      const int j0 = q * 4 * FOLD_THREADS + t * 4;
       const int64_t i0 = tlo + j0;
       float tv[4];
       if (P.idx) {
@@ -137,11 +154,11 @@ __global__ void __launch_bounds__(256) fold_kernel(FoldArgs a) {
   }
   if (a.add_self) {
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = acc[e] + L[e] * a.w_self;
+    for (int e = 0; e < 4 * FOLD_GROUPS; ++e) acc[e] = acc[e] + L[e] * a.w_self;
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int64_t i0 = tlo + q * 1024 + t * 4;
+  for (int q = 0; q < FOLD_GROUPS; ++q) {
+    const int64_t i0 = tlo + q * 4 * FOLD_THREADS + t * 4;
     if (VEC && i0 + 3 < thi) {
       *reinterpret_cast<float4*>(a.out + i0) =
           make_float4(acc[q * 4 + 0], acc[q * 4 + 1], acc[q * 4 + 2], acc[q * 4 + 3]);
@@ -153,14 +170,21 @@ __global__ void __launch_bounds__(256) fold_kernel(FoldArgs a) {
   }
 }
 
+static inline int64_t fold_ntiles(int64_t n) { return (n + FOLD_TILE - 1) / FOLD_TILE; }
+
 }  // namespace dpz
 
 using namespace dpz;
 
+extern "C" size_t dpz_decode_workspace_bytes(int64_t n, int n_payloads) {
+  const int64_t np = n_payloads < FOLD_MAXP ? (n_payloads > 0 ? n_payloads : 1) : FOLD_MAXP;
+  return (size_t)np * (size_t)(fold_ntiles(n > 0 ? n : 1) + 1) * sizeof(int32_t);
+}
+
 extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
                                   const int32_t* const* idx, const float* const* vals,
                                   const int64_t* k, const float* w, float w_self, int flags,
-                                  float* out, dpz_stream_t stream) {
+                                  float* out, void* ws, size_t ws_bytes, dpz_stream_t stream) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (n < 0 || n_payloads < 0) return DPZ_ERR_ARG;
   if (n == 0) return DPZ_OK;
@@ -168,41 +192,55 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
   const bool replace_only = (flags & DPZ_FOLD_REPLACE_ONLY) != 0;
   if (replace_only && n_payloads != 1) return DPZ_ERR_ARG;
   if (n_payloads > 0 && (!vals || !k || (!replace_only && !w))) return DPZ_ERR_ARG;
+  // payload i is dense (a full model) iff idx[i] == NULL and k[i] == n
+  auto is_dense = [&](int i) { return (!idx || !idx[i]) && k[i] == n; };
   for (int i = 0; i < n_payloads; ++i) {
-    if (!vals[i]) return DPZ_ERR_ARG;
-    const bool dense = !idx || !idx[i];
-    if (dense && k[i] != n) return DPZ_ERR_ARG;
-    if (!dense && (k[i] < 0 || k[i] > n)) return DPZ_ERR_ARG;
+    if (k[i] < 0 || k[i] > n) return DPZ_ERR_ARG;
+    if (!vals[i] && k[i] > 0) return DPZ_ERR_ARG;
+    if (!is_dense(i) && k[i] > 0 && (!idx || !idx[i])) return DPZ_ERR_ARG;
   }
+  if (!ws || ws_bytes < dpz_decode_workspace_bytes(n, n_payloads)) return DPZ_ERR_WORKSPACE;
   bool vec = ((reinterpret_cast<uintptr_t>(local) | reinterpret_cast<uintptr_t>(out)) & 15u) == 0;
   for (int i = 0; i < n_payloads; ++i)
-    if ((!idx || !idx[i]) && (reinterpret_cast<uintptr_t>(vals[i]) & 15u)) vec = false;
-  const unsigned grid = (unsigned)((n + FOLD_TILE - 1) / FOLD_TILE);
+    if (is_dense(i) && (reinterpret_cast<uintptr_t>(vals[i]) & 15u)) vec = false;
+  const int64_t ntiles = fold_ntiles(n);
+  const unsigned grid = (unsigned)ntiles;
+  int32_t* starts = static_cast<int32_t*>(ws);
   if (n_payloads == 0) {
     // no payloads: out = w_self * local (self term only) or zeros
     FoldArgs fa{};
-    fa.local = local; fa.out = out; fa.n = n; fa.np = 0; fa.first = 0;
+    fa.local = local; fa.out = out; fa.starts = starts; fa.n = n; fa.ntiles = ntiles;
+    fa.np = 0; fa.first = 0;
     fa.add_self = (flags & DPZ_FOLD_SELF) ? 1 : 0; fa.w_self = w_self;
     DPZ_HIP_TRY(hipMemsetAsync(out, 0, n * sizeof(float), st));
-    if (vec) fold_kernel<true><<<grid, 256, 0, st>>>(fa); else fold_kernel<false><<<grid, 256, 0, st>>>(fa);
+    if (vec) fold_kernel<true><<<grid, FOLD_THREADS, 0, st>>>(fa); else fold_kernel<false><<<grid, FOLD_THREADS, 0, st>>>(fa);
     DPZ_LAUNCH_CHECK();
     return DPZ_OK;
   }
   for (int base = 0; base < n_payloads; base += FOLD_MAXP) {
     FoldArgs fa{};
-    fa.local = local; fa.out = out; fa.n = n;
+    fa.local = local; fa.out = out; fa.starts = starts; fa.n = n; fa.ntiles = ntiles;
     fa.np = (n_payloads - base) < FOLD_MAXP ? (n_payloads - base) : FOLD_MAXP;
     fa.first = base == 0 ? 1 : 0;
     fa.add_self = (base + fa.np == n_payloads && (flags & DPZ_FOLD_SELF)) ? 1 : 0;
     fa.replace_only = replace_only ? 1 : 0;
     fa.w_self = w_self;
+    int64_t kmax = -1;
     for (int i = 0; i < fa.np; ++i) {
-      fa.p[i].idx = idx ? idx[base + i] : nullptr;
+      // an empty sparse payload gets a dummy non-null idx (never read: its range is empty)
+      fa.p[i].idx = is_dense(base + i) ? nullptr
+                    : ((idx && idx[base + i]) ? idx[base + i] : reinterpret_cast<const int32_t*>(starts));
       fa.p[i].val = vals[base + i];
       fa.p[i].k = k[base + i];
       fa.p[i].w = replace_only ? 1.0f : w[base + i];
+      if (fa.p[i].idx && fa.p[i].k > kmax) kmax = fa.p[i].k;
     }
-    if (vec) fold_kernel<true><<<grid, 256, 0, st>>>(fa); else fold_kernel<false><<<grid, 256, 0, st>>>(fa);
+    if (kmax >= 0) {
+      dim3 og((unsigned)((kmax + 1 + 255) / 256), (unsigned)fa.np);
+      fold_offsets_kernel<<<og, 256, 0, st>>>(fa, starts);
+      DPZ_LAUNCH_CHECK();
+    }
+    if (vec) fold_kernel<true><<<grid, FOLD_THREADS, 0, st>>>(fa); else fold_kernel<false><<<grid, FOLD_THREADS, 0, st>>>(fa);
     DPZ_LAUNCH_CHECK();
   }
   return DPZ_OK;

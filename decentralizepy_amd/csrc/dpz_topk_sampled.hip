@@ -1,0 +1,686 @@
+// Sampled single-read top-k (k <= n/16).  See dpz_topk.hip for the contract.
+//
+// Work unit = one WAVE streaming one contiguous "wave segment" of R elements: ordered compaction
+// inside a segment is a ballot + mbcnt prefix (no LDS scan, no barriers in the streaming loop),
+// so the 32 waves of a CU drift apart and keep HBM busy.  Kernels:
+//   sample  : 64 blocks histogram 65,536 sampled keys (1024 chunks x 64) into chist[key >> 20]
+//   filter  : per block, wave 0 turns chist into the key window [lo, hi) while every wave's first
+//             loads are in flight; each wave streams its segment once (x, x0[, acc] -> key),
+//             appends keys >= lo in index order to its candidate list (idx, key; staged in LDS
+//             and flushed in coalesced chunks), and bins them into the block's 256-bin window
+//             histogram (LDS) -> one row per block
+//   selectA : column sums of the rows -> global window histogram
+//   selectB : per wave: threshold bin b* (redundant 257-bin scan), count of its candidates above
+//             b*, bin-b* entries into the segment's own boundary slots (no global atomics: a
+//             contended device-scope atomic costs ~20 ns per arrival on MI355X)
+//   selectC : 1 block: radix select inside bin b* -> exact T and tie cut (lowest index), then
+//             per-segment output offsets by an exclusive scan
+//   compact : per wave: ordered write of selected (idx, vals_src[idx]) + counter / rewind;
+//             block 0 re-zeroes chist for the next call
+// A miss (window does not bracket the k-th key / boundary overflow) sets ctrl->status and compact
+// writes nothing; the host then runs the exact path.  A segment whose candidates overflow its
+// list is DENSE and re-reads its input range in selectB / compact (still exact).
+#include "dpz_topk.h"
+
+namespace dpz {
+
+// ---- optional timing stamps (debug builds with -DDPZ_STAMPS only; s_memrealtime = 100 MHz) ----
+#ifdef DPZ_STAMPS
+__device__ unsigned long long g_stamps[64];
+#define STAMP_MIN(i) do { if (threadIdx.x == 0) atomicMin(&g_stamps[i], __builtin_amdgcn_s_memrealtime()); } while (0)
+#define STAMP_MAX(i) do { __syncthreads(); if (threadIdx.x == 0) atomicMax(&g_stamps[i], __builtin_amdgcn_s_memrealtime()); } while (0)
+#define STAMP_ONE(i) do { if (threadIdx.x == 0) g_stamps[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define STAMP_MIN(i) do {} while (0)
+#define STAMP_MAX(i) do {} while (0)
+#define STAMP_ONE(i) do {} while (0)
+#endif
+
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint32_t fine_bin(uint32_t key, uint32_t lo, uint32_t hi,
+                                             uint32_t shift) {
+  return key >= hi ? (uint32_t)HB : ((key - lo) >> shift);
+}
+
+__device__ __forceinline__ int64_t sample_pos(int c, int lane, int64_t n) {
+  return ((int64_t)c * (n - SMP_CHUNK)) / (SMP_NCHUNK - 1) + lane;  // < 2^41: 64-bit is exact
+}
+
+// 64 blocks x 256: 1024 chunks of 64 contiguous elements spread evenly over [0, n).
+__global__ void __launch_bounds__(256) sampled_sample_kernel(KeySrc s, int64_t n, TopkCtrl* ctrl,
+                                                             uint32_t* chist, uint32_t* ghist) {
+  STAMP_MIN(0);
+  __shared__ uint32_t h[CB];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t i = sample_pos(blockIdx.x * 16 + wave * 4 + r, lane, n);
+    float d = s.x0 ? (s.x[i] - s.x0[i]) : s.x[i];
+    if (s.mode != DPZ_ACC_NONE) d = s.acc[i] + d;
+    v[r] = d;
+  }
+  for (int b = threadIdx.x; b < CB; b += 256) h[b] = 0;
+  if (blockIdx.x == 0) {
+    for (int b = threadIdx.x; b < 512; b += 256) ghist[b] = 0;
+    if (threadIdx.x == 0) {
+      ctrl->status = 0;
+      ctrl->nbound = 0;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) atomicAdd(&h[key_of(v[r]) >> CB_SHIFT], 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < CB; b += 256) {
+    const uint32_t c = h[b];
+    if (c) atomicAdd(&chist[b], c);
+  }
+  STAMP_MAX(1);
+}
+
+// Wave-level: window [lo, hi) around the k-th key from the coarse sample histogram.
+// cv = this lane's 32 bins [2016-32l, 2047-32l] (ascending in memory).
+// Ranks are 1-based, descending, with a 6-sigma + 16 margin.  Result written to win[0..2].
+__device__ __forceinline__ void wave_window(const uint4 (&cv)[8], int64_t n, int64_t k,
+                                            uint32_t* win) {
+  const int lane = threadIdx.x & 63;
+  const double r_est = (double)k * SMP_N / (double)n;
+  const double sd = sqrt(r_est);
+  const double rlo_d = ceil(r_est + 6.0 * sd + 16.0);
+  const double rhi_d = floor(r_est - 6.0 * sd - 16.0);
+  const uint32_t r_lo = rlo_d > SMP_N ? (uint32_t)SMP_N + 1 : (uint32_t)rlo_d;
+  const uint32_t r_hi = rhi_d < 1.0 ? 0u : (uint32_t)rhi_d;
+  uint32_t local = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) local += cv[q].x + cv[q].y + cv[q].z + cv[q].w;
+  uint32_t tot;
+  uint32_t before = wave_excl_scan(local, &tot);
+  if (lane == 0) {
+    win[3] = 0xFFFFFFFFu;  // bin of rank r_lo
+    win[2] = 0xFFFFFFFFu;  // bin of rank r_hi
+  }
+  // descending: bin 2047-32l first = cv[7].w
+#pragma unroll
+  for (int q = 7; q >= 0; --q) {
+    const uint32_t hv4[4] = {cv[q].w, cv[q].z, cv[q].y, cv[q].x};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t bin = (uint32_t)(2016 - 32 * lane + 4 * q + 3 - e);
+      const uint32_t hv = hv4[e];
+      if (r_lo <= (uint32_t)SMP_N && before < r_lo && r_lo <= before + hv) win[3] = bin;
+      if (r_hi >= 1 && before < r_hi && r_hi <= before + hv) win[2] = bin;
+      before += hv;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): LDS writes of this wave done
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) {
+    const uint32_t blo = win[3], bhi = win[2];
+    const uint32_t lo = (blo != 0xFFFFFFFFu) ? (blo << CB_SHIFT) : 0u;
+    const uint64_t h64 = (bhi != 0xFFFFFFFFu) ? ((uint64_t)(bhi + 1) << CB_SHIFT) : (1ull << 31);
+    const uint32_t hi = (uint32_t)(h64 > (1ull << 31) ? (1ull << 31) : h64);
+    const uint32_t width = hi - lo;
+    uint32_t sft = 0;
+    while ((((uint64_t)width + (1ull << sft) - 1) >> sft) > (uint64_t)HB) ++sft;
+    win[0] = lo;
+    win[1] = hi;
+    win[2] = sft;
+  }
+}
+
+// Per-wave candidate list append through an LDS stage, flushed in coalesced 64-lane chunks.
+struct WaveList {
+  uint32_t* gidx;   // this segment's global candidate list
+  uint32_t* gkey;
+  uint32_t* sidx;   // this wave's LDS stage
+  uint32_t* skey;
+  uint32_t staged;  // entries in the stage (wave-uniform)
+  uint32_t flushed; // entries already in the global list (wave-uniform)
+
+  __device__ __forceinline__ void flush(int lane) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LDS stage writes done
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t j = lane; j < staged; j += 64) {
+      gidx[flushed + j] = sidx[j];
+      gkey[flushed + j] = skey[j];
+    }
+    __builtin_amdgcn_wave_barrier();
+    flushed += staged;
+    staged = 0;
+  }
+};
+
+// B blocks x 256 threads; wave w of block b owns wave segment seg = 4b + w = [seg*R, +R) of [0, n).
+template <bool VEC>
+__global__ void __launch_bounds__(256, 8) sampled_filter_kernel(
+    KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl,
+    const uint32_t* __restrict__ chist, uint32_t* rows, uint32_t* segcnt, uint32_t* cidx,
+    uint32_t* ckey) {
+  __shared__ uint32_t h[HBR];
+  __shared__ uint32_t win[4];
+  __shared__ uint32_t st_idx[4][STAGE], st_key[4][STAGE];
+  STAMP_MIN(2);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int b = threadIdx.x; b < HBR; b += 256) h[b] = 0;
+  const int64_t seg = (int64_t)blockIdx.x * 4 + wid;
+  const int64_t beg = seg * R;
+  const int64_t end = (beg + R < n) ? beg + R : n;
+  const bool store_acc = (s.mode == DPZ_ACC_ACCUMULATE) && !s.rekey;
+  uint32_t key[4][4];
+  int cnt[4];
+  // waves 1-3 start streaming at once; wave 0 first turns the coarse sample histogram into the
+  // key window (its 32 bin registers die before its own stream starts, after the barrier)
+  if (wid != 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t i0 = beg + q * 256 + lane * 4;
+      cnt[q] = i0 < end ? load_keys4<VEC>(s, i0, end, store_acc, key[q]) : 0;
+    }
+  } else {
+    uint4 cv[8];
+    const uint4* c4 = reinterpret_cast<const uint4*>(chist) + (504 - 8 * lane);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) cv[q] = c4[q];
+    wave_window(cv, n, k, win);
+  }
+  __syncthreads();
+  if (wid == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t i0 = beg + q * 256 + lane * 4;
+      cnt[q] = i0 < end ? load_keys4<VEC>(s, i0, end, store_acc, key[q]) : 0;
+    }
+  }
+  const uint32_t lo = win[0], hi = win[1], shift = win[2];
+  if (seg == 0 && lane == 0) {
+    ctrl->lo = lo;
+    ctrl->hi = hi;
+    ctrl->shift = shift;
+  }
+  WaveList L{cidx + seg * CAP, ckey + seg * CAP, st_idx[wid], st_key[wid], 0u, 0u};
+  uint32_t run = 0;
+  bool dense = false;
+  for (int64_t base = beg; base < end; base += 1024) {
+    if (base != beg) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t i0 = base + q * 256 + lane * 4;
+        cnt[q] = i0 < end ? load_keys4<VEC>(s, i0, end, store_acc, key[q]) : 0;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bool f[4];
+      uint32_t pre = 0, tot = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        f[e] = e < cnt[q] && key[q][e] >= lo;
+        if (f[e]) atomicAdd(&h[fine_bin(key[q][e], lo, hi, shift)], 1u);
+        const uint64_t m = __ballot(f[e]);
+        pre += mbcnt64(m);
+        tot += (uint32_t)__popcll(m);
+      }
+      if (tot) {
+        if (!dense && run + tot <= (uint32_t)CAP) {
+          const uint32_t i0 = (uint32_t)(base + q * 256 + lane * 4);
+          if (L.staged + tot > STAGE) L.flush(lane);
+          if (tot > STAGE) {  // too many for the stage: write this group straight through
+            uint32_t p = L.flushed + pre;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              if (f[e]) { L.gidx[p] = i0 + e; L.gkey[p] = key[q][e]; ++p; }
+            }
+            L.flushed += tot;
+          } else {
+            uint32_t p = L.staged + pre;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              if (f[e]) { L.sidx[p] = i0 + e; L.skey[p] = key[q][e]; ++p; }
+            }
+            L.staged += tot;
+          }
+        } else {
+          dense = true;
+        }
+        run += tot;
+      }
+    }
+  }
+  if (!dense) L.flush(lane);
+  __syncthreads();
+  uint32_t* row = rows + (int64_t)blockIdx.x * HBR;
+  for (int b = threadIdx.x; b < HBR; b += 256) row[b] = h[b];
+  if (lane == 0 && seg < W) segcnt[seg] = dense ? DENSE : run;
+  STAMP_MAX(3);
+}
+
+// column sums of the per-block window histograms (unrolled independent loads)
+__global__ void __launch_bounds__(256) sampled_selectA_kernel(const uint32_t* __restrict__ rows,
+                                                              int64_t B, uint32_t* ghist) {
+  STAMP_MIN(4);
+  const int64_t per = (B + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = blockIdx.x * per;
+  const int64_t r1 = (r0 + per < B) ? r0 + per : B;
+  if (r0 >= r1) return;
+  for (int b = threadIdx.x; b < HBR; b += 256) {
+    uint32_t sum = 0;
+    int64_t r = r0;
+    for (; r + 8 <= r1; r += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = rows[(r + u) * HBR + b];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sum += v[u];
+    }
+    for (; r < r1; ++r) sum += rows[r * HBR + b];
+    if (sum) atomicAdd(&ghist[b], sum);
+  }
+  STAMP_MAX(5);
+}
+
+// Wave-level threshold bin from the global window histogram.  ghv = fine bins [252-4l, 255-4l].
+__device__ __forceinline__ bool wave_bstar(uint4 ghv, uint32_t above, uint32_t k, uint32_t* bstar,
+                                           uint32_t* need) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t local = ghv.x + ghv.y + ghv.z + ghv.w;
+  uint32_t tot;
+  uint32_t before = wave_excl_scan(local, &tot) + above;
+  uint32_t fb = 0xFFFFFFFFu, fn = 0;
+  const uint32_t hv4[4] = {ghv.w, ghv.z, ghv.y, ghv.x};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (before < k && k <= before + hv4[e]) {
+      fb = (uint32_t)(255 - 4 * lane - e);
+      fn = k - before;
+    }
+    before += hv4[e];
+  }
+  const uint64_t m = __ballot(fb != 0xFFFFFFFFu);
+  const bool ok = (above < k) && (above + tot >= k) && m != 0;
+  const int src = m ? (int)__ffsll((long long)m) - 1 : 0;
+  *bstar = __shfl(fb, src, 64);
+  *need = __shfl(fn, src, 64);
+  return ok;
+}
+
+// ceil(W/4) blocks x 256: wave per segment.  No global atomics: bin-b* entries go to the
+// segment's own BSLOT boundary slots (count in bcnt; > BSLOT -> selectC reports a miss).
+template <bool VEC>
+__global__ void __launch_bounds__(256, 8) sampled_selectB_kernel(
+    KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl,
+    const uint32_t* __restrict__ ghist, const uint32_t* __restrict__ segcnt,
+    const uint32_t* __restrict__ cidx, const uint32_t* __restrict__ ckey, uint32_t* segabove,
+    uint32_t* bcnt, uint32_t* bkey, uint32_t* bidx) {
+  STAMP_MIN(6);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t seg = (int64_t)blockIdx.x * 4 + wid;
+  const uint4 ghv = reinterpret_cast<const uint4*>(ghist)[63 - lane];
+  const uint32_t above_bin = ghist[HB];
+  const uint32_t cnt = seg < W ? segcnt[seg] : 0u;
+  const uint32_t lo = ctrl->lo, hi = ctrl->hi, shift = ctrl->shift;
+  uint32_t bstar, need;
+  const bool ok = wave_bstar(ghv, above_bin, (uint32_t)k, &bstar, &need);
+  if (!ok) {
+    if (seg == 0 && lane == 0) ctrl->status = 1;
+    return;
+  }
+  if (seg == 0 && lane == 0) {
+    ctrl->bstar = bstar;
+    ctrl->need = need;
+  }
+  if (seg >= W) return;
+  uint32_t* my_bkey = bkey + seg * BSLOT;
+  uint32_t* my_bidx = bidx + seg * BSLOT;
+  uint32_t above = 0, brun = 0;
+  if (cnt != DENSE) {
+    for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      uint32_t key = 0, b = 0;
+      if (j < cnt) {
+        key = ckey[seg * CAP + j];
+        b = fine_bin(key, lo, hi, shift);
+      }
+      const bool in = j < cnt && b == bstar;
+      above += (uint32_t)__popcll(__ballot(j < cnt && b > bstar));
+      const uint64_t m = __ballot(in);
+      if (in) {
+        const uint32_t p = brun + mbcnt64(m);
+        if (p < BSLOT) {
+          my_bkey[p] = key;
+          my_bidx[p] = cidx[seg * CAP + j];
+        }
+      }
+      brun += (uint32_t)__popcll(m);
+    }
+  } else {
+    const int64_t beg = seg * R;
+    const int64_t end = (beg + R < n) ? beg + R : n;
+    for (int64_t i0 = beg + lane * 4; i0 - lane * 4 < end; i0 += 256) {
+      uint32_t key[4];
+      const int c = i0 < end ? load_keys4<VEC>(s, i0, end, false, key) : 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool valid = e < c && key[e] >= lo;
+        const uint32_t b = valid ? fine_bin(key[e], lo, hi, shift) : 0u;
+        const bool in = valid && b == bstar;
+        above += (uint32_t)__popcll(__ballot(valid && b > bstar));
+        const uint64_t m = __ballot(in);
+        if (in) {
+          const uint32_t p = brun + mbcnt64(m);
+          if (p < BSLOT) {
+            my_bkey[p] = key[e];
+            my_bidx[p] = (uint32_t)(i0 + e);
+          }
+        }
+        brun += (uint32_t)__popcll(m);
+      }
+    }
+  }
+  if (lane == 0) {
+    segabove[seg] = above;
+    bcnt[seg] = brun;
+  }
+#ifdef DPZ_STAMPS
+  if (lane == 0) atomicMax(&g_stamps[7], __builtin_amdgcn_s_memrealtime());
+#endif
+}
+
+// One block of 1024 threads: gather the boundary slots, radix-select inside bin b* -> exact T and
+// tie cut, then per-segment output offsets.
+__global__ void __launch_bounds__(1024) sampled_selectC_kernel(
+    int64_t k, int64_t W, int64_t R, TopkCtrl* ctrl, const uint32_t* __restrict__ bcnt,
+    const uint32_t* __restrict__ bkey, const uint32_t* __restrict__ bidx,
+    const uint32_t* __restrict__ segabove, uint32_t* segoff) {
+  constexpr int PER = BCAP / 1024;
+  constexpr int SPT = W_MAX / 1024;  // segments per thread (contiguous)
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t segsel[W_MAX];  // first per-segment boundary bases, then selected counts
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t sh[4];
+  STAMP_ONE(8);
+  const int t = threadIdx.x;
+  const uint32_t status = ctrl->status;
+  const uint32_t need = ctrl->need;
+  const uint32_t lo = ctrl->lo, shift = ctrl->shift, bstar = ctrl->bstar;
+  uint32_t sa[SPT], bc[SPT];
+  uint32_t mycnt = 0, over = 0;
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    const int64_t sg = (int64_t)t * SPT + q;
+    sa[q] = sg < W ? segabove[sg] : 0u;
+    bc[q] = sg < W ? bcnt[sg] : 0u;
+  }
+  if (status) return;
+  STAMP_ONE(9);
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    over |= bc[q] > (uint32_t)BSLOT;
+    mycnt += bc[q];
+  }
+  uint32_t nb;
+  uint32_t lbase = block_excl_scan(mycnt, wsum, &nb);
+  const int anyover = __syncthreads_or((int)over);
+  if (anyover || nb > BCAP || need == 0 || need > nb) {
+    if (t == 0) ctrl->status = 1;
+    return;
+  }
+  {  // per-segment bases of the flattened boundary list
+    uint32_t b = lbase;
+#pragma unroll
+    for (int q = 0; q < SPT; ++q) {
+      segsel[t * SPT + q] = b;
+      b += bc[q];
+    }
+  }
+  __syncthreads();
+  STAMP_ONE(10);
+  // entry j -> owning segment = last segment whose base <= j (LDS binary search); all the
+  // global loads of this thread are independent and issue together
+  uint32_t kk[PER], ii[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const uint32_t j = t + q * 1024;
+    kk[q] = 0u;
+    ii[q] = 0u;
+    if (j < nb) {
+      uint32_t a = 0, z = (uint32_t)W;
+      while (z - a > 1) {
+        const uint32_t mid = (a + z) >> 1;
+        if (segsel[mid] <= j) a = mid; else z = mid;
+      }
+      const uint32_t slot = j - segsel[a];
+      kk[q] = bkey[(int64_t)a * BSLOT + slot];
+      ii[q] = bidx[(int64_t)a * BSLOT + slot];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) segsel[t * SPT + q] = 0;
+  // radix select of the need-th largest key inside bin b*: offsets o = key - base < 2^shift
+  const uint32_t base = lo + (bstar << shift);
+  uint32_t prefix = 0;   // resolved high bits of the offset
+  uint32_t rem = need;   // rank still to resolve among entries matching prefix (1-based)
+  uint32_t eqcnt = nb;   // entries equal to T (exact after the last digit)
+  for (int top = (int)shift; top > 0; top -= 8) {
+    const int d = top >= 8 ? 8 : top;
+    const int low = top - d;
+    if (t < 256) hist[t] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const uint32_t j = t + q * 1024;
+      if (j < nb) {
+        const uint32_t o = kk[q] - base;
+        if ((uint32_t)((uint64_t)o >> top) == (uint32_t)((uint64_t)prefix >> top))
+          atomicAdd(&hist[(o >> low) & ((1u << d) - 1)], 1u);
+      }
+    }
+    __syncthreads();
+    const uint32_t hb = t < 256 ? hist[255 - t] : 0u;  // descending digit 255 - t
+    uint32_t tot;
+    const uint32_t before = block_excl_scan(hb, wsum, &tot);
+    if (t < 256 && before < rem && rem <= before + hb) {
+      sh[0] = 255 - t;
+      sh[1] = rem - before;
+      sh[2] = hb;
+    }
+    __syncthreads();
+    prefix |= sh[0] << low;
+    rem = sh[1];
+    eqcnt = sh[2];
+    __syncthreads();
+  }
+  const uint32_t T = base + prefix;
+  STAMP_ONE(11);
+  // ties: take the `rem` lowest indices among entries with key == T
+  uint32_t icut = 0xFFFFFFFFu;
+  if (rem < eqcnt) {
+    uint32_t ipre = 0, irem = rem;
+    for (int top = 32; top > 0; top -= 8) {
+      const int low = top - 8;
+      if (t < 256) hist[t] = 0;
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const uint32_t j = t + q * 1024;
+        if (j < nb && kk[q] == T && (top == 32 || (ii[q] >> top) == (ipre >> top)))
+          atomicAdd(&hist[(ii[q] >> low) & 255u], 1u);
+      }
+      __syncthreads();
+      const uint32_t hb = t < 256 ? hist[t] : 0u;  // ascending digit t
+      uint32_t tot;
+      const uint32_t before = block_excl_scan(hb, wsum, &tot);
+      if (t < 256 && before < irem && irem <= before + hb) {
+        sh[0] = t;
+        sh[1] = irem - before;
+      }
+      __syncthreads();
+      ipre |= sh[0] << low;
+      irem = sh[1];
+      __syncthreads();
+    }
+    icut = ipre;
+  }
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const uint32_t j = t + q * 1024;
+    if (j < nb && (kk[q] > T || (kk[q] == T && ii[q] <= icut)))
+      atomicAdd(&segsel[ii[q] / (uint32_t)R], 1u);
+  }
+  if (t == 0) {
+    ctrl->T = T;
+    ctrl->icut = icut;
+  }
+  __syncthreads();
+  uint32_t v[SPT], local = 0;
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    v[q] = sa[q] + segsel[t * SPT + q];
+    local += v[q];
+  }
+  uint32_t tot;
+  uint32_t ex = block_excl_scan(local, wsum, &tot);
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    const int64_t sg = (int64_t)t * SPT + q;
+    if (sg < W) segoff[sg] = ex;
+    ex += v[q];
+  }
+  if (t == 0 && tot != (uint32_t)k) ctrl->status = 2;  // internal inconsistency
+  STAMP_ONE(12);
+}
+
+template <bool VEC>
+__global__ void __launch_bounds__(256, 8) sampled_compact_kernel(
+    KeySrc s, int64_t n, int64_t W, int64_t R, int64_t CAP, const TopkCtrl* ctrl, uint32_t* chist,
+    const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ segoff,
+    const uint32_t* __restrict__ cidx, const uint32_t* __restrict__ ckey, const float* vals_src,
+    int32_t* idx_out, float* val_out, int32_t* counter, float* rewind, int64_t k) {
+  STAMP_MIN(13);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (blockIdx.x == 0) {  // leave the coarse sample histogram zeroed for the next call
+    for (int b = threadIdx.x; b < CB; b += 256) chist[b] = 0;
+  }
+  const int64_t seg = (int64_t)blockIdx.x * 4 + wid;
+  const uint32_t status = ctrl->status;
+  const uint32_t T = ctrl->T, icut = ctrl->icut, lo = ctrl->lo;
+  const uint32_t cnt = seg < W ? segcnt[seg] : 0u;
+  uint32_t run = seg < W ? segoff[seg] : 0u;
+  if (status || seg >= W) return;
+  if (cnt != DENSE) {
+    for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      bool sel = false;
+      uint32_t idx = 0;
+      if (j < cnt) {
+        const uint32_t key = ckey[seg * CAP + j];
+        idx = cidx[seg * CAP + j];
+        sel = key > T || (key == T && idx <= icut);
+      }
+      const uint64_t m = __ballot(sel);
+      if (sel) {
+        const uint32_t pos = run + mbcnt64(m);
+        if (pos < (uint64_t)k) {
+          idx_out[pos] = (int32_t)idx;
+          val_out[pos] = vals_src[idx];
+          if (counter) counter[idx] += 1;
+          if (rewind) rewind[idx] = 0.0f;
+        }
+      }
+      run += (uint32_t)__popcll(m);
+    }
+  } else {
+    const int64_t beg = seg * R;
+    const int64_t end = (beg + R < n) ? beg + R : n;
+    for (int64_t i0 = beg + lane * 4; i0 - lane * 4 < end; i0 += 256) {
+      uint32_t key[4];
+      const int c = i0 < end ? load_keys4<VEC>(s, i0, end, false, key) : 0;
+      bool f[4];
+      uint32_t pre = 0, tot = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        f[e] = e < c && key[e] >= lo &&
+               (key[e] > T || (key[e] == T && (uint32_t)(i0 + e) <= icut));
+        const uint64_t m = __ballot(f[e]);
+        pre += mbcnt64(m);
+        tot += (uint32_t)__popcll(m);
+      }
+      uint32_t pos = run + pre;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (f[e]) {
+          if (pos < (uint64_t)k) {
+            const int64_t i = i0 + e;
+            idx_out[pos] = (int32_t)i;
+            val_out[pos] = vals_src[i];
+            if (counter) counter[i] += 1;
+            if (rewind) rewind[i] = 0.0f;
+          }
+          ++pos;
+        }
+      }
+      run += tot;
+    }
+  }
+}
+
+template <bool VEC>
+static int run_sampled_t(const EncodeArgs& a, const WsLayout& L) {
+  KeySrc s{a.x, a.x0, a.acc, a.acc_mode, 0};
+  TopkCtrl* ctrl = reinterpret_cast<TopkCtrl*>(a.ws + L.ctrl);
+  uint32_t* chist = reinterpret_cast<uint32_t*>(a.ws + L.chist);
+  uint32_t* ghist = reinterpret_cast<uint32_t*>(a.ws + L.f_ghist);
+  uint32_t* rows = reinterpret_cast<uint32_t*>(a.ws + L.f_rows);
+  uint32_t* segcnt = reinterpret_cast<uint32_t*>(a.ws + L.f_segcnt);
+  uint32_t* segabove = reinterpret_cast<uint32_t*>(a.ws + L.f_segabove);
+  uint32_t* segoff = reinterpret_cast<uint32_t*>(a.ws + L.f_segoff);
+  uint32_t* cidx = reinterpret_cast<uint32_t*>(a.ws + L.f_cidx);
+  uint32_t* ckey = reinterpret_cast<uint32_t*>(a.ws + L.f_ckey);
+  uint32_t* bcnt = reinterpret_cast<uint32_t*>(a.ws + L.f_bcnt);
+  uint32_t* bkey = reinterpret_cast<uint32_t*>(a.ws + L.f_bkey);
+  uint32_t* bidx = reinterpret_cast<uint32_t*>(a.ws + L.f_bidx);
+  const FastGeom& g = L.fg;
+  const unsigned nb = (unsigned)g.B;
+  sampled_sample_kernel<<<SMP_BLOCKS, 256, 0, a.st>>>(s, a.n, ctrl, chist, ghist);
+  DPZ_LAUNCH_CHECK();
+  sampled_filter_kernel<VEC><<<nb, 256, 0, a.st>>>(s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist,
+                                                   rows, segcnt, cidx, ckey);
+  DPZ_LAUNCH_CHECK();
+  s.rekey = 1;
+  sampled_selectA_kernel<<<32, 256, 0, a.st>>>(rows, g.B, ghist);
+  DPZ_LAUNCH_CHECK();
+  sampled_selectB_kernel<VEC><<<nb, 256, 0, a.st>>>(s, a.n, a.k, g.W, g.R, g.CAP, ctrl, ghist,
+                                                    segcnt, cidx, ckey, segabove, bcnt, bkey, bidx);
+  DPZ_LAUNCH_CHECK();
+  sampled_selectC_kernel<<<1, 1024, 0, a.st>>>(a.k, g.W, g.R, ctrl, bcnt, bkey, bidx, segabove,
+                                               segoff);
+  DPZ_LAUNCH_CHECK();
+  float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE) ? a.acc : nullptr;
+  sampled_compact_kernel<VEC><<<nb, 256, 0, a.st>>>(s, a.n, g.W, g.R, g.CAP, ctrl, chist, segcnt,
+                                                    segoff, cidx, ckey, a.vals_src,
+                                                    a.idx_out, a.val_out, a.counter, rewind, a.k);
+  DPZ_LAUNCH_CHECK();
+  return DPZ_OK;
+}
+
+#ifdef DPZ_STAMPS
+extern "C" int dpz_debug_stamps(unsigned long long* host_out, int reset) {
+  if (host_out) DPZ_HIP_TRY(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)));
+  if (reset) {
+    unsigned long long init[64];
+    for (int i = 0; i < 64; ++i) init[i] = (i == 0 || i == 2 || i == 4 || i == 6 || i == 13) ? ~0ull : 0ull;
+    DPZ_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), init, sizeof(init)));
+  }
+  return 0;
+}
+#endif
+
+int run_sampled(const EncodeArgs& a, const WsLayout& L, bool vec) {
+  return vec ? run_sampled_t<true>(a, L) : run_sampled_t<false>(a, L);
+}
+
+}  // namespace dpz

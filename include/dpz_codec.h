@@ -61,7 +61,9 @@ const char* dpz_error_string(int code);
  * and writes them in ascending index order:  idx_out[j] (int32), val_out[j] = vals_src[idx_out[j]].
  * Side effects: counter[idx] += 1 if counter != NULL; acc[idx] = 0 if acc != NULL and
  * acc_mode != DPZ_ACC_NONE; acc += change everywhere first when acc_mode == DPZ_ACC_ACCUMULATE.
- * n < 2^31, 0 <= k <= n.  Without DPZ_TOPK_ASYNC the call blocks until the result is final.    */
+ * n < 2^31, 0 <= k <= n.  Without DPZ_TOPK_ASYNC the call blocks until the result is final.
+ * ws: device scratch of at least dpz_topk_workspace_bytes(n, k) bytes, ZERO-FILLED before its
+ * first use (hipMemset once); the library keeps the small region it relies on zeroed after.   */
 size_t dpz_topk_workspace_bytes(int64_t n, int64_t k);
 int dpz_topk_encode(const float* x, const float* x0, float* acc, int acc_mode,
                     const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
@@ -80,14 +82,17 @@ int dpz_topk_complete(const float* x, const float* x0, float* acc, int acc_mode,
  * sharing/Sharing.py:156-229 (_averaging / _averaging_server fold) and
  * sharing/JWINS/Wavelet.py:269-309, 336-366 (the same fold on wavelet coefficients).
  *   out[j] = fl( ... fl(fl(t_0[j]*w[0]) + fl(t_1[j]*w[1])) ... + fl(local[j]*w_self) )
- *   t_i[j] = vals[i][m] if idx[i][m] == j for some m, else local[j]  (idx[i] == NULL: dense,
- *   t_i = vals[i]).  The local term is present only with DPZ_FOLD_SELF.
- * idx/vals/k/w are HOST arrays of length n_payloads holding DEVICE pointers / sizes / fp32
- * weights; each idx[i] must be strictly ascending.  out may not alias local.
- * DPZ_FOLD_REPLACE_ONLY: n_payloads == 1, out = t_0 (no multiply).                           */
+ *   t_i[j] = vals[i][m] if idx[i][m] == j for some m, else local[j].
+ * Payload i is DENSE (a full model: t_i = vals[i]) iff idx[i] == NULL and k[i] == n; otherwise
+ * idx[i] holds k[i] strictly ascending indices (idx[i] may be NULL when k[i] == 0).
+ * The local term is present only with DPZ_FOLD_SELF.  idx/vals/k/w are HOST arrays of length
+ * n_payloads holding DEVICE pointers / sizes / fp32 weights.  out may not alias local.
+ * DPZ_FOLD_REPLACE_ONLY: n_payloads == 1, out = t_0 (no multiply).
+ * ws: device scratch of at least dpz_decode_workspace_bytes(n, n_payloads) bytes.              */
+size_t dpz_decode_workspace_bytes(int64_t n, int n_payloads);
 int dpz_decode_average(const float* local, int64_t n, int n_payloads, const int32_t* const* idx,
                        const float* const* vals, const int64_t* k, const float* w, float w_self,
-                       int flags, float* out, dpz_stream_t stream);
+                       int flags, float* out, void* ws, size_t ws_bytes, dpz_stream_t stream);
 
 /* Multilevel sym2 DWT, mode "symmetric", fp32, pywt-1.1.1-exact summation order.
  * Replaces reference sharing/JWINS/Wavelet.py:12-32 (pywt.wavedec + coeffs_to_array).

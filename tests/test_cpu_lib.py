@@ -51,7 +51,7 @@ def test_argument_validation_without_gpu():
     assert rc == 1001
     rc = L.dpz_topk_encode(None, None, None, 0, None, -1, 0, None, None, None, None, 0, 0, None)
     assert rc == 1001
-    rc = L.dpz_decode_average(None, 10, 0, None, None, None, None, 0.0, 0, None, None)
+    rc = L.dpz_decode_average(None, 10, 0, None, None, None, None, 0.0, 0, None, None, 0, None)
     assert rc == 1001
 
 

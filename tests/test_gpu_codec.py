@@ -151,12 +151,12 @@ def test_topk_sampled_miss_falls_back(dev):
     x = np.zeros(n, dtype=np.float32)
     x0 = np.zeros(n, dtype=np.float32)
     rng = np.random.default_rng(11)
-    # sample chunk c covers [c*(n-64)/255, +64): put big changes in the middle of the gaps
+    # sample chunk c covers [c*(n-64)/1023, +64): put big changes in the middle of the gaps
     big = []
-    for c in range(255):
-        s = (c * (n - 64)) // 255 + 64
-        e = ((c + 1) * (n - 64)) // 255
-        big.extend(range(s + 100, min(e - 100, s + 100 + 48)))
+    for c in range(1023):
+        s = (c * (n - 64)) // 1023 + 64
+        e = ((c + 1) * (n - 64)) // 1023
+        big.extend(range(s + 100, min(e - 100, s + 100 + 12)))
     big = np.array(big)
     x[:] = 1e-6 * rng.standard_normal(n).astype(np.float32)
     x[big] = rng.uniform(1.0, 2.0, big.shape[0]).astype(np.float32)
