@@ -1,0 +1,117 @@
+"""Device plumbing for the Sharing plugins: device choice, pinned host staging, host views.
+
+The reference runs one node per OS process with the model on the CPU (node/Node.py,
+eval/testing.py:54-80).  The plugins keep the codec state on the GPU chosen by the node's local
+rank and move only the flat model and the payloads across PCIe, through pinned staging buffers.
+"""
+import os
+
+import numpy as np
+import torch
+
+
+def pick_device(rank):
+    """GPU for a node process: DPZ_DEVICE overrides, else local rank modulo the visible GPUs."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("decentralizepy_amd needs a ROCm GPU (MI355X); none is visible. "
+                           "There is no CPU path.")
+    env = os.environ.get("DPZ_DEVICE")
+    if env is not None:
+        return torch.device("cuda", int(env))
+    return torch.device("cuda", int(rank) % torch.cuda.device_count())
+
+
+class Staging:
+    """Reusable pinned host buffers keyed by (name, dtype); grown on demand.
+
+    A buffer handed out again waits for the last asynchronous copy that read it (``mark``),
+    so a pinned source is never overwritten while its DMA is in flight."""
+
+    def __init__(self):
+        self._bufs = {}
+        self._events = {}
+
+    def get(self, name, n, dtype):
+        key = (name, dtype)
+        ev = self._events.pop(key, None)
+        if ev is not None:
+            ev.synchronize()
+        buf = self._bufs.get(key)
+        if buf is None or buf.numel() < n:
+            buf = torch.empty(max(int(n), 1), dtype=dtype, pin_memory=True)
+            self._bufs[key] = buf
+        return buf[:n]
+
+    def mark(self, name, dtype, stream):
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        self._events[(name, dtype)] = ev
+
+
+def flatten_state(state_dict):
+    """``torch.cat`` of the flattened state tensors (reference sharing/Sharing.py:93-112)."""
+    return torch.cat([v.flatten() for v in state_dict.values()])
+
+
+def state_version(state_dict):
+    """In-place modification stamp of a state_dict (torch version counters of its tensors)."""
+    return tuple(v._version for v in state_dict.values())
+
+
+def to_device_flat(flat_cpu, device, staging, name):
+    """H2D of a host fp32 vector through a pinned buffer."""
+    if flat_cpu.dtype != torch.float32:
+        raise NotImplementedError(
+            f"the flattened model is {flat_cpu.dtype}; the HIP codec handles fp32 models only")
+    host = staging.get(name, flat_cpu.numel(), torch.float32)
+    host.copy_(flat_cpu)
+    out = host.to(device, non_blocking=True)
+    staging.mark(name, torch.float32, torch.cuda.current_stream(device))
+    return out
+
+
+def to_host(t, staging, name):
+    """D2H into a pinned buffer; returns a numpy array that owns its memory."""
+    host = staging.get(name, t.numel(), t.dtype)
+    host.copy_(t, non_blocking=True)
+    torch.cuda.current_stream(t.device).synchronize()
+    return host.numpy().copy()
+
+
+class DeviceCounter:
+    """Host-visible view of the device-resident ``shared_parameters_counter``.
+
+    The reference keeps the counter as a CPU int32 tensor on the model
+    (sharing/PartialModel.py:143-145) and the node dumps it with ``.numpy().tolist()`` at the end
+    of a run (node/DPSGDNode.py:186-194); this view offers the same calls, copying on demand.
+    """
+
+    def __init__(self, t):
+        self.device_tensor = t
+
+    def numpy(self):
+        return self.device_tensor.cpu().numpy()
+
+    def cpu(self):
+        return self.device_tensor.cpu()
+
+    def tolist(self):
+        return self.numpy().tolist()
+
+    @property
+    def shape(self):
+        return self.device_tensor.shape
+
+    def __len__(self):
+        return self.device_tensor.numel()
+
+    def __getitem__(self, item):
+        return self.device_tensor.cpu()[item]
+
+    def __array__(self, dtype=None):
+        a = self.numpy()
+        return a if dtype is None else a.astype(dtype)
+
+
+def np_int32(a):
+    return np.ascontiguousarray(np.asarray(a), dtype=np.int32)

@@ -43,6 +43,7 @@ SIGNATURES = {
     "dpz_dwt_sym2": (_int, [_c_void_p, _c_void_p, _i64, _int, _c_void_p, _c_void_p, _int,
                             _c_void_p]),
     "dpz_idwt_sym2": (_int, [_c_void_p, _i64, _int, _c_void_p, _c_void_p]),
+    "dpz_scatter_fill": (_int, [_c_void_p, _i64, _c_void_p, _i64, ctypes.c_float, _c_void_p]),
     "dpz_pack_fp16": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
     "dpz_unpack_fp16": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
 }

@@ -191,6 +191,16 @@ def waverec(coeffs, n, level=4, out=None):
     return out
 
 
+def scatter_fill(dst, idx, value):
+    """``dst[idx] = value`` (reference models/Model.py:53-64 rewind_accumulation)."""
+    _require(dst, torch.float32, "dst")
+    _require(idx, torch.int32, "idx")
+    rc = _lib.lib().dpz_scatter_fill(_ptr(dst), dst.numel(), _ptr(idx), idx.numel(), float(value),
+                                     _stream(dst.device))
+    check(rc, "dpz_scatter_fill")
+    return dst
+
+
 def pack_fp16(x, out=None):
     _require(x, torch.float32, "x")
     if out is None:

@@ -95,3 +95,24 @@ extern "C" int dpz_unpack_fp16(const uint16_t* in, int64_t n, float* out, dpz_st
   DPZ_LAUNCH_CHECK();
   return DPZ_OK;
 }
+
+namespace dpz {
+__global__ void __launch_bounds__(256) scatter_fill_kernel(float* __restrict__ dst,
+                                                           const int32_t* __restrict__ idx,
+                                                           int64_t k, int64_t n, float v) {
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < k; j += (int64_t)gridDim.x * 256) {
+    const int64_t i = idx[j];
+    if (i >= 0 && i < n) dst[i] = v;
+  }
+}
+}  // namespace dpz
+
+extern "C" int dpz_scatter_fill(float* dst, int64_t n, const int32_t* idx, int64_t k, float value,
+                                dpz_stream_t stream) {
+  if (n < 0 || k < 0 || (k > 0 && (!dst || !idx))) return DPZ_ERR_ARG;
+  if (k == 0) return DPZ_OK;
+  scatter_fill_kernel<<<grid_for((k + 255) / 256 * 32), 256, 0,
+                        static_cast<hipStream_t>(stream)>>>(dst, idx, k, n, value);
+  DPZ_LAUNCH_CHECK();
+  return DPZ_OK;
+}

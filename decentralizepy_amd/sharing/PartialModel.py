@@ -1,0 +1,238 @@
+"""PartialModel plugin: top-k magnitude sparsification of the model change, on the MI355X codec.
+
+Drop-in for the reference ``decentralizepy.sharing.PartialModel.PartialModel``
+(``src/decentralizepy/sharing/PartialModel.py``): identical constructor keyword arguments
+(``alpha, dict_ordered, save_shared, metadata_cap, accumulation, save_accumulated,
+change_transformer, accumulate_averaging_changes, compress, compression_package,
+compression_class, float_precision``), identical wire payload
+``{alpha, indices: int32[k], params: fp32[k], send_partial: True}`` and identical side effects on
+the model (``shared_parameters_counter[idx] += 1``, ``accumulated_changes`` accumulate/rewind).
+
+Device state (HBM, fp32): ``init_model`` (x0), ``pre_share_model`` (x), ``accumulated_changes``,
+``prev`` and the int32 share counter.  Per round: one H2D of the flat model, one fused HIP top-k
+encode (|x - x0| [+acc] -> sampled radix select -> ordered compaction, counter/rewind fused), one
+D2H of the (idx, val) payload; on receive one batched replace+fold over all neighbour payloads,
+one D2H of the averaged model.
+
+Selection parity: the index set equals the reference's ``torch.topk`` set whenever the k-th key is
+unique; at a tie this build takes the lowest indices (torch's CPU choice is implementation-defined,
+SURVEY.md §0 item 5).
+"""
+import json
+import logging
+import os
+from pathlib import Path
+
+import numpy as np
+import torch
+
+from .. import codec
+from .._device import DeviceCounter, flatten_state, state_version, to_device_flat, to_host
+from ..utils import conditional_value, identity
+from .Sharing import Sharing
+
+
+class PartialModel(Sharing):
+    """This class implements the vanilla version of partial model sharing."""
+
+    def __init__(self, rank, machine_id, communication, mapping, graph, model, dataset, log_dir,
+                 alpha=1.0, dict_ordered=True, save_shared=False, metadata_cap=1.0,
+                 accumulation=False, save_accumulated="", change_transformer=identity,
+                 accumulate_averaging_changes=False, compress=False, compression_package=None,
+                 compression_class=None, float_precision=None):
+        super().__init__(rank, machine_id, communication, mapping, graph, model, dataset, log_dir,
+                         compress, compression_package, compression_class, float_precision)
+        # reference PartialModel.py:96-145
+        self.alpha = alpha
+        self.dict_ordered = dict_ordered
+        self.save_shared = save_shared
+        self.metadata_cap = metadata_cap
+        self.accumulation = accumulation
+        self.save_accumulated = conditional_value(save_accumulated, "", False)
+        self.change_transformer = change_transformer
+        self.accumulate_averaging_changes = accumulate_averaging_changes
+        if self.save_accumulated:
+            raise NotImplementedError(
+                "save_accumulated (per-round JSON dumps of the full change vector) is not "
+                "supported by the device codec")
+        self._check_transformer()
+
+        with torch.no_grad():
+            flat = flatten_state(self.model.state_dict())
+        self.init_model = to_device_flat(flat, self.device, self.staging, "local")
+        # the fold output can stand in for a re-read of the loaded model only if every state
+        # tensor is fp32 (load_state_dict casts other dtypes)
+        self._all_fp32 = all(v.dtype == torch.float32 for v in self.model.state_dict().values())
+        self._pre_version = None
+        self.number_of_params = self.init_model.numel()
+        self.transformed_len = self._transformed_len()
+        if self.accumulation:
+            self.model.accumulated_changes = torch.zeros(self.transformed_len, dtype=torch.float32,
+                                                         device=self.device)
+            self.prev = self.init_model
+        if self.save_shared and not (rank == 0 or rank == 1):
+            self.save_shared = False
+        if self.save_shared:
+            self.folder_path = os.path.join(self.log_dir, "shared_params/{}".format(self.rank))
+            Path(self.folder_path).mkdir(parents=True, exist_ok=True)
+        self._counter = torch.zeros(self.transformed_len, dtype=torch.int32, device=self.device)
+        self.model.shared_parameters_counter = DeviceCounter(self._counter)
+        self.pre_share_model = None
+        self.pre_share_model_transformed = None
+
+    # ---- hooks the wavelet subclass overrides --------------------------------------------------
+    def _check_transformer(self):
+        if self.change_transformer is not identity:
+            raise NotImplementedError(
+                "PartialModel on the device codec supports the identity change_transformer; "
+                "use decentralizepy_amd.sharing.JWINS.Wavelet for the wavelet transform")
+
+    def _transformed_len(self):
+        return self.number_of_params
+
+    def _transform_pre_step(self, x):
+        """(T(x), T(x - init)) on device; identity: the change is formed inside the encoder."""
+        return x, None
+
+    # ---- wire format ------------------------------------------------------------------------------
+    def compress_data(self, data):
+        result = dict(data)
+        if self.compress:
+            if "indices" in result:
+                result["indices"] = self.compressor.compress(result["indices"])
+            if "params" in result:
+                result["params"] = self.compressor.compress_float(result["params"])
+        return result
+
+    def decompress_data(self, data):
+        if self.compress:
+            if "indices" in data:
+                data["indices"] = self.compressor.decompress(data["indices"])
+            if "params" in data:
+                data["params"] = self.compressor.decompress_float(data["params"])
+        return data
+
+    # ---- encode -----------------------------------------------------------------------------------
+    def _acc_mode(self):
+        if not self.accumulation:
+            return codec.DPZ_ACC_NONE
+        return codec.DPZ_ACC_ADD if self.accumulate_averaging_changes else codec.DPZ_ACC_ACCUMULATE
+
+    def _pre_step(self):
+        """reference PartialModel.py:305-331: the change (and the accumulation) is fused into the
+        encode kernel; here only the flat model moves to the device."""
+        logging.debug("PartialModel _pre_step")
+        with torch.no_grad():
+            sd = self.model.state_dict()
+            flat = flatten_state(sd)
+            self.pre_share_model = to_device_flat(flat, self.device, self.staging, "local")
+            self._pre_version = state_version(sd)
+            self.pre_share_model_transformed, self._change_dev = \
+                self._transform_pre_step(self.pre_share_model)
+
+    def _encode(self, k):
+        """Top-k encode; returns device (idx int32[k], val fp32[k])."""
+        key_src = self._change_dev if self._change_dev is not None else self.pre_share_model
+        x0 = None if self._change_dev is not None else self.init_model
+        acc = self.model.accumulated_changes if self.accumulation else None
+        return codec.topk_encode(key_src, k, x0=x0, acc=acc, acc_mode=self._acc_mode(),
+                                 vals_src=self.pre_share_model_transformed, counter=self._counter,
+                                 workspace=self.workspace)
+
+    def _zero_accumulation(self):
+        if getattr(self.model, "accumulated_changes", None) is not None:
+            self.model.accumulated_changes.zero_()
+
+    def _full_share(self):
+        """alpha >= metadata_cap: the whole (transformed) model (reference PartialModel.py:198-203)."""
+        self._zero_accumulation()
+        return Sharing.serialized_model(self)
+
+    def serialized_model(self):
+        """reference PartialModel.py:188-255"""
+        if self.alpha >= self.metadata_cap:  # Share fully
+            return self._full_share()
+        with torch.no_grad():
+            k = round(self.alpha * self.transformed_len)
+            idx_dev, val_dev = self._encode(k)
+            indices = to_host(idx_dev, self.staging, "idx")
+            params = to_host(val_dev, self.staging, "val")
+            if self.save_shared:
+                self._dump_shared(indices)
+            if not self.dict_ordered:
+                raise NotImplementedError
+            m = self._message(indices, params)
+            assert len(m["indices"]) == len(m["params"])
+            logging.debug("Elements sending: {}".format(len(m["indices"])))
+            return self.compress_data(m)
+
+    def _message(self, indices, params):
+        m = dict()  # key order of reference PartialModel.py:235-246
+        m["alpha"] = self.alpha
+        m["indices"] = indices.astype(np.int32)
+        m["params"] = params
+        m["send_partial"] = True
+        return m
+
+    def _dump_shared(self, indices):
+        shared_params = dict()
+        shared_params["order"] = list(self.model.state_dict().keys())
+        shared_params["shapes"] = {k: list(v.shape) for k, v in self.model.state_dict().items()}
+        shared_params[self.communication_round] = indices.tolist()
+        with open(os.path.join(self.folder_path,
+                               "{}_shared_params.json".format(self.communication_round + 1)),
+                  "w") as of:
+            json.dump(shared_params, of)
+
+    # ---- decode -----------------------------------------------------------------------------------
+    def _device_payload(self, data):
+        if "send_partial" not in data:
+            return super()._device_payload(data)
+        idx = torch.from_numpy(np.ascontiguousarray(data["indices"], dtype=np.int32))
+        vals = torch.from_numpy(np.ascontiguousarray(data["params"], dtype=np.float32))
+        return idx.to(self.device, non_blocking=True), vals.to(self.device, non_blocking=True)
+
+    def deserialized_model(self, m):
+        """Received dict -> state_dict: ``T = cat(local); T[idx] = params`` on the device
+        (reference PartialModel.py:257-303)."""
+        if "send_partial" not in m:
+            return super().deserialized_model(m)
+        with torch.no_grad():
+            m = self.decompress_data(m)
+            idx, vals = self._device_payload(m)
+            local = self._local_flat_device()
+            out = codec.replace(local, idx, vals, workspace=self.workspace)
+            return self._unflatten(to_host(out, self.staging, "result"))
+
+    def _post_step(self):
+        """reference PartialModel.py:333-353; the new model is already on the device (fold output)."""
+        logging.debug("PartialModel _post_step")
+        with torch.no_grad():
+            post = getattr(self, "_post_model_dev", None)
+            if post is None or not self._all_fp32:
+                flat = flatten_state(self.model.state_dict())
+                post = to_device_flat(flat, self.device, self.staging, "local")
+            self._post_model_dev = None
+            self.init_model = post
+            if self.accumulation:
+                if self.accumulate_averaging_changes:
+                    self._accumulate_change(self.init_model, self.prev)
+                self.prev = self.init_model
+            self.model.model_change = None
+
+    def _accumulate_change(self, new, prev):
+        """acc += T(new - prev) (identity: the encoder's accumulate-only kernel)."""
+        codec.topk_encode(new, 0, x0=prev, acc=self.model.accumulated_changes,
+                          acc_mode=codec.DPZ_ACC_ACCUMULATE, workspace=self.workspace)
+
+    def _local_flat_device(self):
+        """The fold's local term: the pre-share copy if the model was not touched since
+        _pre_step (torch version counters), else a fresh H2D of the current model."""
+        if self.pre_share_model is not None and self._pre_version == state_version(
+                self.model.state_dict()):
+            return self.pre_share_model
+        return super()._local_flat_device()
+
+    def _load_flat(self, out_dev):
+        super()._load_flat(out_dev)
+        self._post_model_dev = out_dev

@@ -109,6 +109,12 @@ int dpz_dwt_sym2(const float* x, const float* x0, int64_t n, int level, float* c
  * Replaces reference sharing/JWINS/Wavelet.py:311-316.                                        */
 int dpz_idwt_sym2(const float* coeffs, int64_t n, int level, float* out, dpz_stream_t stream);
 
+/* dst[idx[j]] = value for j < k (indices outside [0, n) are ignored).
+ * Replaces reference models/Model.py:53-64 (rewind_accumulation: acc[idx] = 0) where the rewind
+ * is not fused into dpz_topk_encode (Wavelet with change_based_selection = False).             */
+int dpz_scatter_fill(float* dst, int64_t n, const int32_t* idx, int64_t k, float value,
+                     dpz_stream_t stream);
+
 /* fp16 value packing (round-to-nearest-even, torch.half semantics) and unpacking.
  * The build's own wire codec for values (BASELINE config C5); the reference's lossy float path
  * is fpzip (compression/EliasFpzipLossy.py:14-58), which is not byte-compatible.             */

@@ -1,0 +1,327 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ from the UNMODIFIED reference.
+
+Run in the build container only (the reference is not present on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+It imports sacs-epfl/decentralizepy from /root/reference/src (Sharing, PartialModel, Wavelet,
+JWINS, Elias, Linear mapping, Model) and replays multi-round gossip scenarios: a node's model is
+set, "trained" (a fixed random perturbation), encoded with get_data_to_send, and averaged with
+synthetic neighbour payloads through _averaging — twice, so the accumulation bookkeeping of
+_pre_step/_post_step is exercised.  Every input and every output (payload indices/params,
+shared_parameters_counter, accumulated_changes, averaged model) is saved as plain numpy arrays
+(allow_pickle=False) together with the scenario description in JSON.
+
+The reference's Wavelet imports PyWavelets, which exists in this image only for
+/opt/conda/bin/python3.9 (PyWavelets 1.1.1).  A minimal in-process ``pywt`` module forwards the
+four functions the reference calls (wavedec, coeffs_to_array, array_to_coeffs, waverec) to that
+interpreter; the reference classes themselves run unmodified.
+
+Scenarios are generated tie-free at the k-th key (checked on the reference's own model_change),
+because torch.topk's CPU tie order is implementation-defined.
+"""
+import json
+import os
+import pickle
+import subprocess
+import sys
+import tempfile
+import types
+from collections import deque
+
+import numpy as np
+
+sys.dont_write_bytecode = True
+REF = "/root/reference/src"
+OUT = os.path.dirname(os.path.abspath(__file__))
+PY39 = "/opt/conda/bin/python3.9"
+
+# ---------------------------------------------------------------------------------------------
+# pywt bridge (forwards to PyWavelets 1.1.1 in python3.9)
+_BRIDGE = r"""
+import pickle, sys, warnings
+warnings.filterwarnings("ignore")
+import pywt
+fn, args, kwargs = pickle.load(sys.stdin.buffer)
+res = getattr(pywt, fn)(*args, **kwargs)
+sys.stdout.buffer.write(pickle.dumps(res, protocol=4))
+"""
+
+
+def _call_pywt(fn, *args, **kwargs):
+    p = subprocess.run([PY39, "-c", _BRIDGE], input=pickle.dumps((fn, args, kwargs), protocol=4),
+                       capture_output=True, check=True)
+    return pickle.loads(p.stdout)
+
+
+def _np(x):
+    try:
+        import torch
+        if isinstance(x, torch.Tensor):
+            return x.numpy()
+    except ImportError:
+        pass
+    return np.asarray(x)
+
+
+pywt = types.ModuleType("pywt")
+pywt.wavedec = lambda x, wavelet, level=None, **kw: _call_pywt("wavedec", _np(x), wavelet, level=level, **kw)
+pywt.coeffs_to_array = lambda c, **kw: _call_pywt("coeffs_to_array", [_np(a) for a in c], **kw)
+pywt.array_to_coeffs = lambda a, s, **kw: _call_pywt("array_to_coeffs", _np(a), s, **kw)
+pywt.waverec = lambda c, wavelet, **kw: _call_pywt("waverec", [_np(a) for a in c], wavelet, **kw)
+sys.modules["pywt"] = pywt
+
+sys.path.insert(0, REF)
+import torch  # noqa: E402
+
+from decentralizepy.compression.Elias import Elias  # noqa: E402
+from decentralizepy.mappings.Linear import Linear  # noqa: E402
+from decentralizepy.models.Model import Model  # noqa: E402
+from decentralizepy.sharing.JWINS.JWINS import JWINS  # noqa: E402
+from decentralizepy.sharing.JWINS.Wavelet import Wavelet  # noqa: E402
+from decentralizepy.sharing.PartialModel import PartialModel  # noqa: E402
+from decentralizepy.sharing.Sharing import Sharing  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+from oracle import topk as otopk  # noqa: E402
+
+
+class Net(Model):
+    """Two-tensor model: weight (rows, cols) and bias (nb,)."""
+
+    def __init__(self, rows, cols, nb):
+        super().__init__()
+        self.weight = torch.nn.Parameter(torch.zeros(rows, cols))
+        self.bias = torch.nn.Parameter(torch.zeros(nb))
+
+
+class Graph:
+    def __init__(self, nbrs):
+        self.nbrs = set(nbrs)
+
+    def neighbors(self, uid):
+        return self.nbrs
+
+
+def set_flat(model, flat):
+    sd = model.state_dict()
+    pos = 0
+    new = {}
+    for k, v in sd.items():
+        new[k] = torch.from_numpy(flat[pos:pos + v.numel()].reshape(v.shape).copy())
+        pos += v.numel()
+    model.load_state_dict(new)
+
+
+def get_flat(model):
+    return torch.cat([v.flatten() for v in model.state_dict().values()]).numpy().copy()
+
+
+def neighbour_payloads(rng, length, kind, n_nbrs, rnd, alpha):
+    """Synthetic neighbour messages in the reference wire format."""
+    msgs = []
+    for i in range(n_nbrs):
+        deg = int(rng.integers(2, 6))
+        if kind[i] == "full":
+            m = {"params": rng.standard_normal(length).astype(np.float32)}
+        else:
+            k = max(1, round(alpha * length))
+            idx = np.sort(rng.choice(length, size=k, replace=False)).astype(np.int32)
+            m = {"alpha": alpha, "indices": idx,
+                 "params": (0.05 * rng.standard_normal(k)).astype(np.float32), "send_partial": True}
+        m["degree"] = deg
+        m["iteration"] = rnd
+        m["CHANNEL"] = "DPSGD"
+        msgs.append(m)
+    return msgs
+
+
+def record_msgs(prefix, msgs, arrays):
+    meta = []
+    for i, m in enumerate(msgs):
+        arrays[f"{prefix}_nbr{i}_params"] = np.asarray(m["params"])
+        if "indices" in m:
+            arrays[f"{prefix}_nbr{i}_indices"] = np.asarray(m["indices"])
+        meta.append({"degree": m["degree"], "partial": "send_partial" in m,
+                     "alpha": m.get("alpha")})
+    return meta
+
+
+def kth_tie(change, k):
+    return otopk.kth_has_tie(otopk.keys_u32(change.numpy()), k)
+
+
+class TieError(RuntimeError):
+    pass
+
+
+def run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed, wavelet=False, nbr_kinds=None):
+    """Replay; on a tie at the k-th key (fp32 differences are quantised) retry with the next seed."""
+    for attempt in range(40):
+        try:
+            meta = _run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed + 1000 * attempt,
+                                 wavelet, nbr_kinds)
+            meta["seed"] = seed + 1000 * attempt
+            return meta
+        except TieError as e:
+            print("retry:", e)
+    raise RuntimeError(f"{name}: no tie-free seed found")
+
+
+def _run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed, wavelet, nbr_kinds):
+    rng = np.random.default_rng(seed)
+    n = rows * cols + nb
+    model = Net(rows, cols, nb)
+    x0 = rng.standard_normal(n).astype(np.float32)
+    set_flat(model, x0)
+    uid_nbrs = [1, 2, 3]
+    mapping = Linear(1, 4)
+    with tempfile.TemporaryDirectory() as tmp:
+        plugin = cls(0, 0, None, mapping, Graph(uid_nbrs), model, None, tmp, **kwargs)
+    arrays = {"x0": x0}
+    meta = {"name": name, "class": cls.__name__, "kwargs": kwargs, "shape": [rows, cols, nb],
+            "n": n, "rounds": []}
+    length = n
+    for r in range(rounds):
+        cur = get_flat(model)
+        train = (0.01 * rng.standard_normal(n)).astype(np.float32)
+        x_r = (cur + train).astype(np.float32)
+        set_flat(model, x_r)
+        arrays[f"r{r}_x"] = x_r
+        data = plugin.get_data_to_send(degree=len(uid_nbrs))
+        change = plugin.model.model_change
+        rmeta = {"alpha": float(plugin.alpha), "partial": "send_partial" in data}
+        if wavelet:
+            length = int(plugin.wt_shape[0])
+            rmeta["coeff_len"] = length
+        if "send_partial" in data:
+            k = len(data["indices"])
+            rmeta["k"] = k
+            if plugin.change_based_selection if wavelet else True:
+                if kth_tie(change, k):
+                    raise TieError(f"{name}: tie at the k-th key in round {r} (seed {seed})")
+            arrays[f"r{r}_indices"] = np.asarray(data["indices"])
+        arrays[f"r{r}_params"] = np.asarray(data["params"])
+        rmeta["degree"] = data["degree"]
+        arrays[f"r{r}_counter_after_encode"] = plugin.model.shared_parameters_counter.numpy().copy()
+        if plugin.model.accumulated_changes is not None:
+            arrays[f"r{r}_acc_after_encode"] = plugin.model.accumulated_changes.numpy().copy()
+        kinds = nbr_kinds[r] if nbr_kinds else ["partial"] * len(uid_nbrs)
+        msgs = neighbour_payloads(rng, length, kinds, len(uid_nbrs), r, 0.05)
+        rmeta["neighbours"] = record_msgs(f"r{r}", msgs, arrays)
+        peer = {uid: deque([m]) for uid, m in zip(uid_nbrs, msgs)}
+        plugin._averaging(peer)
+        arrays[f"r{r}_model_after"] = get_flat(model)
+        if plugin.model.accumulated_changes is not None:
+            arrays[f"r{r}_acc_after_avg"] = plugin.model.accumulated_changes.numpy().copy()
+        meta["rounds"].append(rmeta)
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **arrays)
+    return meta
+
+
+def sharing_scenario():
+    rng = np.random.default_rng(5)
+    rows, cols, nb = 31, 33, 7
+    n = rows * cols + nb
+    model = Net(rows, cols, nb)
+    x0 = rng.standard_normal(n).astype(np.float32)
+    set_flat(model, x0)
+    with tempfile.TemporaryDirectory() as tmp:
+        plugin = Sharing(0, 0, None, Linear(1, 4), Graph([1, 2, 3]), model, None, tmp)
+    data = plugin.get_data_to_send(degree=3)
+    msgs = neighbour_payloads(rng, n, ["full"] * 3, 3, 0, 1.0)
+    arrays = {"x0": x0, "sent_params": np.asarray(data["params"])}
+    meta = {"name": "sharing_full", "class": "Sharing", "n": n, "shape": [rows, cols, nb],
+            "neighbours": record_msgs("r0", msgs, arrays)}
+    plugin._averaging({uid: deque([m]) for uid, m in zip([1, 2, 3], msgs)})
+    arrays["r0_model_after"] = get_flat(model)
+    np.savez_compressed(os.path.join(OUT, "sharing_full.npz"), **arrays)
+    return meta
+
+
+def elias_vectors():
+    rng = np.random.default_rng(9)
+    cases = {"kat": np.array([10, 3, 6, 5], dtype=np.int32)}
+    cases["consecutive"] = np.arange(100, 400, dtype=np.int32)
+    cases["two"] = np.array([7, 2**31 - 1], dtype=np.int32)
+    cases["pow2_gaps"] = np.cumsum(np.array([0] + [2**j for j in range(30)], dtype=np.int64)).astype(np.int32)
+    for name, n, k in [("sparse_1pct", 1_000_000, 10_000), ("dense_40pct", 50_000, 20_000),
+                       ("tiny", 1000, 17)]:
+        cases[name] = rng.choice(n, size=k, replace=False).astype(np.int32)
+    arrays = {}
+    for name, a in cases.items():
+        inp = a.copy()
+        enc = Elias().compress(inp)           # sorts inp in place, as the reference does
+        dec = Elias().decompress(enc)
+        arrays[f"{name}_input"] = a
+        arrays[f"{name}_sorted"] = inp
+        arrays[f"{name}_bytes"] = np.asarray(enc, dtype=np.uint8)
+        arrays[f"{name}_decoded"] = np.asarray(dec)
+    np.savez_compressed(os.path.join(OUT, "elias.npz"), **arrays)
+    return sorted(cases)
+
+
+def pywt_vectors():
+    """sym2 level-4 wavedec/coeffs_to_array and waverec straight from PyWavelets 1.1.1."""
+    rng = np.random.default_rng(41)
+    arrays = {}
+    sizes = [64, 65, 66, 67, 101, 1001, 4099, 10000]
+    for n in sizes:
+        x = rng.standard_normal(n).astype(np.float32)
+        arr, sl = pywt.coeffs_to_array(pywt.wavedec(x, "sym2", level=4))
+        rec = pywt.waverec(pywt.array_to_coeffs(arr, sl, output_format="wavedec"), wavelet="sym2")
+        arrays[f"n{n}_x"] = x
+        arrays[f"n{n}_coeffs"] = np.asarray(arr, dtype=np.float32)
+        arrays[f"n{n}_rec"] = np.asarray(rec, dtype=np.float32)
+    np.savez_compressed(os.path.join(OUT, "wavelet_pywt.npz"), **arrays)
+    return sizes
+
+
+def main():
+    torch.set_num_threads(4)
+    scen = []
+    pm_common = {"dict_ordered": True}
+    scen.append(run_scenario("pm_a01_plain", PartialModel, {**pm_common, "alpha": 0.1},
+                             40, 100, 99, 2, seed=11, nbr_kinds=[["partial", "full", "partial"]] * 2))
+    scen.append(run_scenario("pm_a01_acc", PartialModel,
+                             {**pm_common, "alpha": 0.1, "accumulation": True}, 40, 100, 99, 2,
+                             seed=12))
+    scen.append(run_scenario("pm_a02_accavg", PartialModel,
+                             {**pm_common, "alpha": 0.2, "accumulation": True,
+                              "accumulate_averaging_changes": True}, 40, 100, 99, 2, seed=13))
+    scen.append(run_scenario("pm_a001_large", PartialModel, {**pm_common, "alpha": 0.01},
+                             300, 333, 103, 1, seed=14))
+    scen.append(run_scenario("pm_fullshare", PartialModel,
+                             {**pm_common, "alpha": 0.6, "metadata_cap": 0.5, "accumulation": True},
+                             40, 100, 99, 1, seed=15))
+    wv = {"wavelet": "sym2", "level": 4, "alpha": 0.1, "metadata_cap": 0.5}
+    scen.append(run_scenario("wv_plain", Wavelet, wv, 20, 50, 1, 2, seed=21, wavelet=True,
+                             nbr_kinds=[["partial", "full", "partial"]] * 2))
+    scen.append(run_scenario("wv_acc", Wavelet, {**wv, "accumulation": True}, 40, 100, 99, 2,
+                             seed=22, wavelet=True))
+    scen.append(run_scenario("wv_accavg", Wavelet,
+                             {**wv, "accumulation": True, "accumulate_averaging_changes": True},
+                             40, 100, 99, 2, seed=23, wavelet=True))
+    scen.append(run_scenario("wv_nochange_sel", Wavelet,
+                             {**wv, "accumulation": True, "change_based_selection": False},
+                             40, 100, 99, 2, seed=24, wavelet=True))
+    jw = {"alpha_list": "[0.1,0.15,0.2,0.25,0.3,0.4,1.0]", "wavelet": "sym2", "level": 4,
+          "accumulation": True, "accumulate_averaging_changes": True, "metadata_cap": 0.5,
+          "change_based_selection": True}
+    scen.append(run_scenario("jwins_tutorial", JWINS, jw, 100, 100, 103, 4, seed=31,
+                             wavelet=True))
+    scen.append(sharing_scenario())
+    elias = elias_vectors()
+    wsizes = pywt_vectors()
+    with open(os.path.join(OUT, "scenarios.json"), "w") as f:
+        json.dump({"scenarios": scen, "elias_cases": elias, "wavelet_sizes": wsizes,
+                   "generator": "tests/golden/make_golden.py",
+                   "reference": "sacs-epfl/decentralizepy v1 (/root/reference/src)",
+                   "pywavelets": "1.1.1 (python3.9 bridge)",
+                   "torch": torch.__version__}, f, indent=1)
+    print("wrote", len(scen), "scenarios")
+
+
+if __name__ == "__main__":
+    main()

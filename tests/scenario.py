@@ -1,0 +1,241 @@
+"""Replay the golden multi-round gossip scenarios (tests/golden/make_golden.py) against a backend.
+
+Two backends:
+  * OracleNode — the numpy restatement (oracle/) of the reference Sharing logic, to pin the
+    oracle against the reference's recorded outputs (CPU tests);
+  * the device plugin classes of decentralizepy_amd (GPU tests), driven exactly like the Node
+    drives the reference: get_data_to_send(), then _averaging(peer_deques).
+"""
+import json
+import os
+import random
+from collections import deque
+
+import numpy as np
+
+from oracle import fold as ofold
+from oracle import topk as otopk
+from oracle import wavelet as owav
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load_meta():
+    with open(os.path.join(GOLDEN, "scenarios.json")) as f:
+        return json.load(f)
+
+
+def scenario_names(cls_filter=None):
+    return [s["name"] for s in load_meta()["scenarios"]
+            if "rounds" in s and (cls_filter is None or s["class"] in cls_filter)]
+
+
+def load(name):
+    meta = next(s for s in load_meta()["scenarios"] if s["name"] == name)
+    arrays = dict(np.load(os.path.join(GOLDEN, f"{name}.npz")))
+    return meta, arrays
+
+
+def neighbour_msgs(meta_round, arrays, r):
+    msgs = []
+    for i, nm in enumerate(meta_round["neighbours"]):
+        m = {"params": arrays[f"r{r}_nbr{i}_params"].copy()}
+        if nm["partial"]:
+            m = {"alpha": nm["alpha"], "indices": arrays[f"r{r}_nbr{i}_indices"].copy(),
+                 "params": arrays[f"r{r}_nbr{i}_params"].copy(), "send_partial": True}
+        m["degree"] = nm["degree"]
+        m["iteration"] = r
+        m["CHANNEL"] = "DPSGD"
+        msgs.append(m)
+    return msgs
+
+
+class OracleNode:
+    """numpy mirror of reference PartialModel / Wavelet / JWINS round logic (fp32 exact)."""
+
+    def __init__(self, meta, x0):
+        kw = meta["kwargs"]
+        self.cls = meta["class"]
+        self.wavelet = self.cls in ("Wavelet", "JWINS")
+        self.level = int(kw.get("level", 4))
+        self.alpha = kw.get("alpha", 1.0)
+        self.cap = kw.get("metadata_cap", 1.0)
+        self.accumulation = kw.get("accumulation", False)
+        self.aac = kw.get("accumulate_averaging_changes", False)
+        self.cbs = kw.get("change_based_selection", True)
+        self.n = x0.shape[0]
+        self.init = x0.copy()
+        self.model = x0.copy()
+        self.L = owav.coeff_len(self.n, self.level) if self.wavelet else self.n
+        self.acc = np.zeros(self.L, np.float32) if self.accumulation else None
+        self.prev = self.init
+        self.counter = np.zeros(self.L, np.int32)
+        if self.cls == "JWINS":
+            self.alpha_list = eval(kw["alpha_list"])
+            random.seed(0)  # uid of rank 0 / machine 0
+
+    def T(self, v):
+        return owav.wavedec_array(v, self.level) if self.wavelet else v
+
+    def get_data_to_send(self):
+        if self.cls == "JWINS":
+            self.alpha = random.choice(self.alpha_list)
+        x = self.model.copy()
+        self.xT = self.T(x)
+        if self.wavelet:
+            change = owav.wavedec_array(x - self.init, self.level)
+            x0 = None
+        else:
+            change, x0 = x, self.init
+        mode = otopk.ACC_NONE
+        if self.accumulation:
+            mode = otopk.ACC_ADD if self.aac else otopk.ACC_ACCUMULATE
+        if self.alpha >= self.cap:
+            if self.accumulation:
+                if mode == otopk.ACC_ACCUMULATE:  # pre-step accumulation happens before the zeroing
+                    self.acc += (change - x0) if x0 is not None else change
+                self.acc[:] = 0
+            return {"params": self.xT.copy()}
+        k = round(self.alpha * self.L)
+        if self.wavelet and not self.cbs:
+            if mode == otopk.ACC_ACCUMULATE:
+                self.acc += change
+            idx, val = otopk.encode(self.xT, None, None, otopk.ACC_NONE, k, vals_src=self.xT,
+                                    counter=self.counter)
+            if self.acc is not None:
+                self.acc[idx] = 0
+        else:
+            idx, val = otopk.encode(change, x0, self.acc, mode, k, vals_src=self.xT,
+                                    counter=self.counter)
+        return {"alpha": self.alpha, "indices": idx, "params": val, "send_partial": True}
+
+    def averaging(self, msgs):
+        pays, degs = [], []
+        for m in msgs:
+            pays.append((m["indices"], m["params"]) if "send_partial" in m else (None, m["params"]))
+            degs.append(m["degree"])
+        w = [ofold.mh_weight(len(msgs), d) for d in degs]
+        wt = 0
+        for v in w:
+            wt += v
+        local = self.xT if self.wavelet else self.model
+        total = ofold.fold(local, pays, w, 1 - wt)
+        self.model = owav.waverec_array(total, self.n, self.level) if self.wavelet else total
+        # post step
+        new = self.model.copy()
+        if self.accumulation and self.aac:
+            d = new - self.prev
+            self.acc += self.T(d) if self.wavelet else d
+        self.init = new
+        if self.accumulation:
+            self.prev = new
+
+
+def check_round(got, arrays, r, meta_round, bits=True):
+    """Compare one round's outputs: got = dict(payload, counter_enc, acc_enc, model, acc_avg)."""
+    pay = got["payload"]
+    if meta_round["partial"]:
+        np.testing.assert_array_equal(np.asarray(pay["indices"]), arrays[f"r{r}_indices"])
+    np.testing.assert_array_equal(np.asarray(pay["params"]).view(np.uint32),
+                                  arrays[f"r{r}_params"].view(np.uint32))
+    np.testing.assert_array_equal(np.asarray(got["counter_enc"]),
+                                  arrays[f"r{r}_counter_after_encode"])
+    if f"r{r}_acc_after_encode" in arrays:
+        np.testing.assert_array_equal(np.asarray(got["acc_enc"]).view(np.uint32),
+                                      arrays[f"r{r}_acc_after_encode"].view(np.uint32))
+    np.testing.assert_array_equal(np.asarray(got["model"]).view(np.uint32),
+                                  arrays[f"r{r}_model_after"].view(np.uint32))
+    if f"r{r}_acc_after_avg" in arrays:
+        np.testing.assert_array_equal(np.asarray(got["acc_avg"]).view(np.uint32),
+                                      arrays[f"r{r}_acc_after_avg"].view(np.uint32))
+
+
+def replay_oracle(name):
+    meta, arrays = load(name)
+    node = OracleNode(meta, arrays["x0"])
+    for r, mr in enumerate(meta["rounds"]):
+        node.model = arrays[f"r{r}_x"].copy()
+        pay = node.get_data_to_send()
+        got = {"payload": pay, "counter_enc": node.counter.copy(),
+               "acc_enc": None if node.acc is None else node.acc.copy()}
+        node.averaging(neighbour_msgs(mr, arrays, r))
+        got["model"] = node.model
+        got["acc_avg"] = None if node.acc is None else node.acc.copy()
+        check_round(got, arrays, r, mr)
+
+
+# ---- device plugin backend ---------------------------------------------------------------------
+class _Mapping:
+    def __init__(self, procs=4):
+        self.procs = procs
+
+    def get_uid(self, rank, machine_id):
+        return machine_id * self.procs + rank
+
+
+class _Graph:
+    def __init__(self, nbrs):
+        self.nbrs = set(nbrs)
+
+    def neighbors(self, uid):
+        return self.nbrs
+
+
+def make_model(shape):
+    import torch
+
+    class Net(torch.nn.Module):
+        """Stand-in for the reference Model (models/Model.py:15-25 codec fields)."""
+
+        def __init__(self, rows, cols, nb):
+            super().__init__()
+            self.weight = torch.nn.Parameter(torch.zeros(rows, cols))
+            self.bias = torch.nn.Parameter(torch.zeros(nb))
+            self.model_change = None
+            self.accumulated_changes = None
+            self.shared_parameters_counter = None
+
+    return Net(*shape)
+
+
+def set_flat(model, flat):
+    import torch
+    sd = model.state_dict()
+    pos, new = 0, {}
+    for k, v in sd.items():
+        new[k] = torch.from_numpy(flat[pos:pos + v.numel()].reshape(v.shape).copy())
+        pos += v.numel()
+    model.load_state_dict(new)
+
+
+def get_flat(model):
+    import torch
+    return torch.cat([v.flatten() for v in model.state_dict().values()]).numpy().copy()
+
+
+def replay_plugin(name, tmpdir):
+    import torch  # noqa: F401
+
+    from decentralizepy_amd.sharing.JWINS.JWINS import JWINS
+    from decentralizepy_amd.sharing.JWINS.Wavelet import Wavelet
+    from decentralizepy_amd.sharing.PartialModel import PartialModel
+    classes = {"PartialModel": PartialModel, "Wavelet": Wavelet, "JWINS": JWINS}
+    meta, arrays = load(name)
+    model = make_model(meta["shape"])
+    set_flat(model, arrays["x0"])
+    plugin = classes[meta["class"]](0, 0, None, _Mapping(), _Graph([1, 2, 3]), model, None,
+                                    str(tmpdir), **meta["kwargs"])
+    for r, mr in enumerate(meta["rounds"]):
+        set_flat(model, arrays[f"r{r}_x"])
+        data = plugin.get_data_to_send(degree=3)
+        acc = getattr(model, "accumulated_changes", None)
+        got = {"payload": data, "counter_enc": model.shared_parameters_counter.numpy().copy(),
+               "acc_enc": None if acc is None else acc.cpu().numpy().copy()}
+        assert data["degree"] == mr["degree"]
+        peer = {uid: deque([m]) for uid, m in zip([1, 2, 3], neighbour_msgs(mr, arrays, r))}
+        plugin._averaging(peer)
+        got["model"] = get_flat(model)
+        acc = getattr(model, "accumulated_changes", None)
+        got["acc_avg"] = None if acc is None else acc.cpu().numpy().copy()
+        check_round(got, arrays, r, mr)
+    return plugin

@@ -1,0 +1,63 @@
+"""CPU: host-side behaviour of the plugin classes that needs no GPU (kwargs surface, config
+coercion, loud failure without a device)."""
+import inspect
+
+import pytest
+import torch
+
+from tests import scenario
+
+
+def _ref_kwargs():
+    # keyword surface of the reference classes, as their signatures define it
+    pm = ["alpha", "dict_ordered", "save_shared", "metadata_cap", "accumulation",
+          "save_accumulated", "change_transformer", "accumulate_averaging_changes", "compress",
+          "compression_package", "compression_class", "float_precision"]
+    wv = ["alpha", "dict_ordered", "save_shared", "metadata_cap", "wavelet", "level",
+          "change_based_selection", "save_accumulated", "accumulation",
+          "accumulate_averaging_changes", "compress", "compression_package", "compression_class"]
+    jw = ["alpha_list"] + wv[1:]
+    return {"PartialModel": pm, "Wavelet": wv, "JWINS": jw}
+
+
+def test_constructor_keyword_surface_matches_reference():
+    from decentralizepy_amd.sharing.JWINS.JWINS import JWINS
+    from decentralizepy_amd.sharing.JWINS.Wavelet import Wavelet
+    from decentralizepy_amd.sharing.PartialModel import PartialModel
+    from decentralizepy_amd.sharing.Sharing import Sharing
+    positional = ["self", "rank", "machine_id", "communication", "mapping", "graph", "model",
+                  "dataset", "log_dir"]
+    for cls, names in [(PartialModel, "PartialModel"), (Wavelet, "Wavelet"), (JWINS, "JWINS")]:
+        params = list(inspect.signature(cls.__init__).parameters)
+        assert params[:9] == positional
+        assert params[9:] == _ref_kwargs()[names], cls
+    assert list(inspect.signature(Sharing.__init__).parameters)[9:] == [
+        "compress", "compression_package", "compression_class", "float_precision"]
+
+
+def test_wavelet_coeff_slices_match_pywt_layout():
+    from decentralizepy_amd.sharing.JWINS.Wavelet import coeff_slices
+    from oracle import wavelet as owav
+    for n in [64, 101, 10103, 11_000_000]:
+        sl, m = coeff_slices(n, 4)
+        assert m == owav.coeff_len(n, 4)
+        lens = owav.level_lengths(n, 4)
+        assert sl[0] == slice(0, lens[4])
+        assert sl[-1]["d"][0].stop == m
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure mode")
+def test_plugin_fails_loudly_without_gpu(tmp_path):
+    from decentralizepy_amd.sharing.PartialModel import PartialModel
+    model = scenario.make_model([4, 4, 2])
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        PartialModel(0, 0, None, scenario._Mapping(), scenario._Graph([1]), model, None,
+                     str(tmp_path), alpha=0.1)
+
+
+def test_unsupported_wavelet_is_rejected(tmp_path):
+    from decentralizepy_amd.sharing.JWINS.Wavelet import Wavelet
+    model = scenario.make_model([4, 4, 2])
+    with pytest.raises(NotImplementedError, match="haar"):
+        Wavelet(0, 0, None, scenario._Mapping(), scenario._Graph([1]), model, None,
+                str(tmp_path), wavelet="haar")
