@@ -18,6 +18,11 @@ DPZ_TOPK_EXACT = 0x1
 DPZ_TOPK_ASYNC = 0x2
 DPZ_FOLD_SELF = 0x1
 DPZ_FOLD_REPLACE_ONLY = 0x2
+DPZ_OK = 0
+DPZ_ERR_ARG = 1001
+DPZ_ERR_WORKSPACE = 1002
+DPZ_ERR_UNSUPPORTED = 1003
+DPZ_ERR_INTERNAL = 1004
 
 _c_void_p = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -46,6 +51,12 @@ SIGNATURES = {
     "dpz_scatter_fill": (_int, [_c_void_p, _i64, _c_void_p, _i64, ctypes.c_float, _c_void_p]),
     "dpz_pack_fp16": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
     "dpz_unpack_fp16": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
+    "dpz_elias_max_bytes": (_i64, [_i64]),
+    "dpz_elias_workspace_bytes": (_size, [_i64, _i64]),
+    "dpz_elias_encode": (_int, [_c_void_p, _i64, _c_void_p, _i64, ctypes.POINTER(_i64),
+                                _c_void_p, _size, _c_void_p]),
+    "dpz_elias_decode": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _i64,
+                                ctypes.POINTER(_i64), _c_void_p, _size, _c_void_p]),
 }
 
 _lib = None

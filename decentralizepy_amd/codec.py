@@ -14,7 +14,7 @@ from ._lib import (DPZ_ACC_ACCUMULATE, DPZ_ACC_ADD, DPZ_ACC_NONE, DPZ_FOLD_REPLA
 
 __all__ = ["DPZ_ACC_NONE", "DPZ_ACC_ACCUMULATE", "DPZ_ACC_ADD", "Workspace", "topk_encode",
            "topk_complete", "decode_average", "replace", "wavedec_len", "wavedec", "waverec",
-           "pack_fp16", "unpack_fp16"]
+           "pack_fp16", "unpack_fp16", "elias_encode", "elias_decode"]
 
 
 def _ptr(t):
@@ -47,6 +47,7 @@ class Workspace:
         self.device = torch.device(device)
         self.buf = None
         self.dbuf = None
+        self.ebuf = None
 
     def get(self, n, k):
         need = int(_lib.lib().dpz_topk_workspace_bytes(int(n), int(k)))
@@ -59,6 +60,12 @@ class Workspace:
         if self.dbuf is None or self.dbuf.numel() < need:
             self.dbuf = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
         return self.dbuf
+
+    def get_elias(self, k, nbytes):
+        need = int(_lib.lib().dpz_elias_workspace_bytes(int(k), int(nbytes)))
+        if self.ebuf is None or self.ebuf.numel() < need:
+            self.ebuf = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+        return self.ebuf
 
 
 def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, counter=None,
@@ -217,3 +224,53 @@ def unpack_fp16(h, out=None):
     rc = _lib.lib().dpz_unpack_fp16(_ptr(h), h.numel(), _ptr(out), _stream(h.device))
     check(rc, "dpz_unpack_fp16")
     return out
+
+
+def elias_encode(idx, out=None, workspace=None):
+    """Elias-gamma stream of a strictly increasing device int32 index array (k >= 2).
+
+    Returns a device uint8 view of exactly the reference's byte count (compression/Elias.py:20-52).
+    """
+    _require(idx, torch.int32, "idx")
+    k = idx.numel()
+    if k < 2:
+        raise IndexError("Elias coding needs at least two indices (reference Elias.py:38-46)")
+    cap = int(_lib.lib().dpz_elias_max_bytes(k))
+    if out is None or out.numel() < cap:
+        out = torch.empty(cap, dtype=torch.uint8, device=idx.device)
+    workspace = workspace or Workspace(idx.device)
+    ws = workspace.get_elias(k, 0)
+    nbytes = ctypes.c_int64(0)
+    rc = _lib.lib().dpz_elias_encode(_ptr(idx), k, _ptr(out), out.numel(), ctypes.byref(nbytes),
+                                     _ptr(ws), ws.numel(), _stream(idx.device))
+    if rc == _lib.DPZ_ERR_ARG:
+        raise ValueError("Elias coding needs strictly increasing indices")
+    check(rc, "dpz_elias_encode")
+    return out[:nbytes.value]
+
+
+def elias_decode(buf, nbytes, nbits, first, count, dtype=torch.int64, workspace=None):
+    """Values of an Elias-gamma stream held on the device (compression/Elias.py:54-97).
+
+    ``buf`` is a device uint8 tensor with at least round_up(nbytes, 4) + 16 bytes; ``nbits`` and
+    ``first`` come from the stream's trailer; ``count`` bounds the output (the stream encodes at
+    most (nbits - 128) + 1 values).
+    """
+    _require(buf, torch.uint8, "buf")
+    if buf.numel() < ((nbytes + 3) // 4) * 4 + 16:
+        raise ValueError("buf must be padded to round_up(nbytes, 4) + 16 bytes")
+    out = torch.empty(max(count, 1), dtype=dtype, device=buf.device)
+    workspace = workspace or Workspace(buf.device)
+    ws = workspace.get_elias(2, nbytes)
+    n = ctypes.c_int64(0)
+    o64 = out if dtype == torch.int64 else None
+    o32 = out if dtype == torch.int32 else None
+    if o64 is None and o32 is None:
+        raise ValueError("dtype must be torch.int64 or torch.int32")
+    rc = _lib.lib().dpz_elias_decode(_ptr(buf), nbytes, nbits, first, _ptr(o64), _ptr(o32),
+                                     out.numel(), ctypes.byref(n), _ptr(ws), ws.numel(),
+                                     _stream(buf.device))
+    if rc == _lib.DPZ_ERR_ARG:
+        raise ValueError("malformed Elias stream")
+    check(rc, "dpz_elias_decode")
+    return out[:n.value]

@@ -1,0 +1,77 @@
+"""Elias-gamma index compressor on the MI355X codec (byte-identical to the reference).
+
+Drop-in for ``decentralizepy.compression.Elias.Elias`` (compression/Elias.py:15-97): the same
+host surface (``compress(np.int32[k]) -> np.uint8[...]`` sorting its argument in place,
+``decompress(bytes) -> np.int64[k]``), with the bit packing and the code-boundary chase running as
+HIP kernels (``dpz_elias_encode`` / ``dpz_elias_decode``).  The sharing plugins call the device
+entry points ``compress_device`` / ``decompress_device`` directly, so a payload's indices go
+device -> stream -> host once instead of through a host round trip.
+"""
+import numpy as np
+import torch
+
+from .. import codec
+from .._device import pick_device
+from .Compression import Compression
+
+
+def parse_trailer(buf):
+    """(nbits, first) from the last 16 bytes (int64 LE each, reference Elias.py:48-51, 72-76)."""
+    b = np.frombuffer(memoryview(buf), dtype=np.uint8)
+    if b.size < 16:
+        raise ValueError("Elias stream shorter than its 16-byte trailer")
+    first = int(b[-16:-8].view("<i8")[0])
+    nbits = int(b[-8:].view("<i8")[0])
+    return nbits, first
+
+
+class Elias(Compression):
+    """Elias-gamma coding of sorted index gaps."""
+
+    def __init__(self, *args, **kwargs):
+        self.device = None
+        self._ws = None
+
+    # ---- device ----------------------------------------------------------------------------------
+    def _dev(self, device=None):
+        if device is not None:
+            self.device = torch.device(device)
+        if self.device is None:
+            self.device = pick_device(0)
+        if self._ws is None or self._ws.device != self.device:
+            self._ws = codec.Workspace(self.device)
+        return self.device
+
+    def compress_device(self, idx_dev):
+        """Strictly increasing device int32 indices -> host uint8 stream."""
+        self._dev(idx_dev.device)
+        enc = codec.elias_encode(idx_dev, workspace=self._ws)
+        return enc.cpu().numpy()
+
+    def decompress_device(self, buf, dtype=torch.int32, device=None):
+        """Host stream -> device index tensor (int32 for the fold kernels, or int64)."""
+        dev = self._dev(device)
+        b = np.frombuffer(memoryview(buf), dtype=np.uint8)
+        nbits, first = parse_trailer(b)
+        nbytes = b.size
+        padded = torch.zeros(((nbytes + 3) // 4) * 4 + 16, dtype=torch.uint8)
+        padded[:nbytes] = torch.from_numpy(b.copy())
+        dbuf = padded.to(dev)
+        count = max(nbits - 128, 0) + 1
+        return codec.elias_decode(dbuf, nbytes, nbits, first, count, dtype=dtype,
+                                  workspace=self._ws)
+
+    # ---- reference host surface ----------------------------------------------------------------
+    def compress(self, arr):
+        """reference Elias.py:20-52: sorts ``arr`` in place, returns the packed stream."""
+        if arr.size < 2:
+            raise IndexError("index 0 is out of bounds" if arr.size == 0 else
+                             "list index out of range")
+        if np.any(arr[1:] < arr[:-1]):
+            arr.sort()
+        idx = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int32)).to(self._dev())
+        return self.compress_device(idx)
+
+    def decompress(self, bytes):
+        """reference Elias.py:54-97: int64 values."""
+        return self.decompress_device(bytes, dtype=torch.int64).cpu().numpy()

@@ -95,19 +95,29 @@ class PartialModel(Sharing):
         return x, None
 
     # ---- wire format ------------------------------------------------------------------------------
-    def compress_data(self, data):
+    def compress_data(self, data, idx_dev=None):
+        """reference PartialModel.py:147-154; a device compressor codes the (already sorted)
+        device indices directly."""
         result = dict(data)
         if self.compress:
             if "indices" in result:
-                result["indices"] = self.compressor.compress(result["indices"])
+                if idx_dev is not None and hasattr(self.compressor, "compress_device"):
+                    result["indices"] = self.compressor.compress_device(idx_dev)
+                else:
+                    result["indices"] = self.compressor.compress(result["indices"])
             if "params" in result:
                 result["params"] = self.compressor.compress_float(result["params"])
         return result
 
-    def decompress_data(self, data):
+    def decompress_data(self, data, device=False):
+        """reference PartialModel.py:156-162; with ``device`` a device compressor decodes the
+        indices straight into a device int32 tensor for the fold."""
         if self.compress:
             if "indices" in data:
-                data["indices"] = self.compressor.decompress(data["indices"])
+                if device and hasattr(self.compressor, "decompress_device"):
+                    data["indices"] = self.compressor.decompress_device(data["indices"])
+                else:
+                    data["indices"] = self.compressor.decompress(data["indices"])
             if "params" in data:
                 data["params"] = self.compressor.decompress_float(data["params"])
         return data
@@ -164,7 +174,7 @@ class PartialModel(Sharing):
             m = self._message(indices, params)
             assert len(m["indices"]) == len(m["params"])
             logging.debug("Elements sending: {}".format(len(m["indices"])))
-            return self.compress_data(m)
+            return self.compress_data(m, idx_dev=idx_dev)
 
     def _message(self, indices, params):
         m = dict()  # key order of reference PartialModel.py:235-246
@@ -188,9 +198,14 @@ class PartialModel(Sharing):
     def _device_payload(self, data):
         if "send_partial" not in data:
             return super()._device_payload(data)
-        idx = torch.from_numpy(np.ascontiguousarray(data["indices"], dtype=np.int32))
         vals = torch.from_numpy(np.ascontiguousarray(data["params"], dtype=np.float32))
-        return idx.to(self.device, non_blocking=True), vals.to(self.device, non_blocking=True)
+        idx = data["indices"]
+        if isinstance(idx, torch.Tensor):  # decoded on the device by the compressor
+            idx = idx.to(self.device, torch.int32)
+        else:
+            idx = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int32))
+            idx = idx.to(self.device, non_blocking=True)
+        return idx, vals.to(self.device, non_blocking=True)
 
     def deserialized_model(self, m):
         """Received dict -> state_dict: ``T = cat(local); T[idx] = params`` on the device

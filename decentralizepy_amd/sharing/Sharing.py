@@ -59,6 +59,8 @@ class Sharing:
         self.device = pick_device(rank)
         self.staging = Staging()
         self.workspace = codec.Workspace(self.device)
+        if hasattr(getattr(self, "compressor", None), "compress_device"):
+            self.compressor.device = self.device  # device compressors run on this node's GPU
 
     # ---- wire format -----------------------------------------------------------------------
     def compress_data(self, data):
@@ -68,7 +70,7 @@ class Sharing:
                 result["params"] = self.compressor.compress_float(result["params"])
         return result
 
-    def decompress_data(self, data):
+    def decompress_data(self, data, device=False):
         if self.compress:
             if "params" in data:
                 data["params"] = self.compressor.decompress_float(data["params"])
@@ -132,7 +134,7 @@ class Sharing:
             del data["iteration"]
             del data["CHANNEL"]
             logging.debug("Averaging model from neighbor {} of iteration {}".format(n, iteration))
-            data = self.decompress_data(data)
+            data = self.decompress_data(data, device=True)
             payloads.append(self._device_payload(data))
             degrees.append(degree)
         return payloads, degrees

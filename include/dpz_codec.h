@@ -121,6 +121,31 @@ int dpz_scatter_fill(float* dst, int64_t n, const int32_t* idx, int64_t k, float
 int dpz_pack_fp16(const float* in, int64_t n, uint16_t* out, dpz_stream_t stream);
 int dpz_unpack_fp16(const uint16_t* in, int64_t n, float* out, dpz_stream_t stream);
 
+/* ---- Elias-gamma index coding (byte-identical to the reference wire format) ------------------
+ * Replaces compression/Elias.py:20-52 (Elias.compress) and :54-97 (Elias.decompress).
+ * Format: l = floor(log2(gap)) zero bits then the gap in l+1 bits, MSB-first, for every gap of the
+ * sorted int32 array; 128 zero bits; np.packbits byte order; bytes [-16:-8] = int64 LE first
+ * value, [-8:] = int64 LE total bit count (code bits + 128).                                   */
+
+/* Upper bound of the encoded size for k values (all gaps 2^31-1), rounded up to 4 bytes. */
+int64_t dpz_elias_max_bytes(int64_t k);
+/* Device workspace for an encode of k values or a decode of an nbytes stream (the max of both). */
+size_t dpz_elias_workspace_bytes(int64_t k, int64_t nbytes);
+/* idx: device int32[k], strictly increasing (k >= 2; the reference raises IndexError below 2).
+ * out: device buffer, 4-byte aligned, out_cap >= dpz_elias_max_bytes(k).  Writes the stream and
+ * returns its length in *nbytes_host (host pointer; the call synchronises `stream`).
+ * DPZ_ERR_ARG if the indices are not strictly increasing.                                      */
+int dpz_elias_encode(const int32_t* idx, int64_t k, uint8_t* out, int64_t out_cap,
+                     int64_t* nbytes_host, void* ws, size_t ws_bytes, dpz_stream_t stream);
+/* in: device copy of the stream, 4-byte aligned, readable up to round_up(nbytes, 4) + 16 bytes.
+ * nbits/first: the stream's trailer (the caller holds the bytes).  Writes first + running gap
+ * sums into out64 (int64, as the reference returns) and/or out32 (either may be NULL); the value
+ * count goes to *count_host (host pointer; synchronises).  DPZ_ERR_ARG on a malformed stream,
+ * DPZ_ERR_WORKSPACE if the count exceeds out_cap, DPZ_ERR_UNSUPPORTED above 2^26 code bits.    */
+int dpz_elias_decode(const uint8_t* in, int64_t nbytes, int64_t nbits, int64_t first,
+                     int64_t* out64, int32_t* out32, int64_t out_cap, int64_t* count_host,
+                     void* ws, size_t ws_bytes, dpz_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

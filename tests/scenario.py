@@ -213,8 +213,26 @@ def get_flat(model):
     return torch.cat([v.flatten() for v in model.state_dict().values()]).numpy().copy()
 
 
-def replay_plugin(name, tmpdir):
+def _elias_wire(msgs, check_cls):
+    """Neighbour messages as an Elias(-Fpzip) sender puts them on the wire (oracle encoder)."""
+    from oracle import elias as oelias
+    out = []
+    for m in msgs:
+        m = dict(m)
+        if "indices" in m:
+            m["indices"] = oelias.encode(m["indices"])
+        if check_cls == "EliasFpzip" and "params" in m:
+            m["params"] = np.ascontiguousarray(m["params"], np.float32).view(np.uint8).copy()
+        out.append(m)
+    return out
+
+
+def replay_plugin(name, tmpdir, compression_class=None):
+    """Drive the device plugin through the scenario; with ``compression_class`` ("Elias" or
+    "EliasFpzip" of decentralizepy_amd.compression) the wire payloads are compressed and the
+    outgoing index stream is checked against the oracle's reference-pinned Elias bytes."""
     import torch  # noqa: F401
+    from oracle import elias as oelias
 
     from decentralizepy_amd.sharing.JWINS.JWINS import JWINS
     from decentralizepy_amd.sharing.JWINS.Wavelet import Wavelet
@@ -223,16 +241,29 @@ def replay_plugin(name, tmpdir):
     meta, arrays = load(name)
     model = make_model(meta["shape"])
     set_flat(model, arrays["x0"])
+    kwargs = dict(meta["kwargs"])
+    if compression_class:
+        kwargs.update(compress=True, compression_class=compression_class,
+                      compression_package=f"decentralizepy_amd.compression.{compression_class}")
     plugin = classes[meta["class"]](0, 0, None, _Mapping(), _Graph([1, 2, 3]), model, None,
-                                    str(tmpdir), **meta["kwargs"])
+                                    str(tmpdir), **kwargs)
     for r, mr in enumerate(meta["rounds"]):
         set_flat(model, arrays[f"r{r}_x"])
         data = plugin.get_data_to_send(degree=3)
+        if compression_class:
+            data = dict(data)
+            if "indices" in data:
+                np.testing.assert_array_equal(np.asarray(data["indices"]),
+                                              oelias.encode(arrays[f"r{r}_indices"]))
+            data = plugin.decompress_data(data)
         acc = getattr(model, "accumulated_changes", None)
         got = {"payload": data, "counter_enc": model.shared_parameters_counter.numpy().copy(),
                "acc_enc": None if acc is None else acc.cpu().numpy().copy()}
         assert data["degree"] == mr["degree"]
-        peer = {uid: deque([m]) for uid, m in zip([1, 2, 3], neighbour_msgs(mr, arrays, r))}
+        msgs = neighbour_msgs(mr, arrays, r)
+        if compression_class:
+            msgs = _elias_wire(msgs, compression_class)
+        peer = {uid: deque([m]) for uid, m in zip([1, 2, 3], msgs)}
         plugin._averaging(peer)
         got["model"] = get_flat(model)
         acc = getattr(model, "accumulated_changes", None)

@@ -61,3 +61,33 @@ def test_unsupported_wavelet_is_rejected(tmp_path):
     with pytest.raises(NotImplementedError, match="haar"):
         Wavelet(0, 0, None, scenario._Mapping(), scenario._Graph([1]), model, None,
                 str(tmp_path), wavelet="haar")
+
+
+def test_compression_surface_and_trailer():
+    import numpy as np
+
+    from decentralizepy_amd.compression.Compression import Compression
+    from decentralizepy_amd.compression.Elias import Elias, parse_trailer
+    from decentralizepy_amd.compression.EliasFpzip import EliasFpzip
+    c = Compression(float_precision=None)
+    a = np.arange(5, dtype=np.int32)
+    assert c.compress(a) is a and c.decompress(a) is a
+    assert c.compress_float(a) is a and c.decompress_float(a) is a
+    # trailer of the SURVEY.md §8a known-answer stream
+    kat = bytes.fromhex("520003000000000000008900000000000000")
+    assert parse_trailer(kat) == (137, 3)
+    x = np.random.default_rng(0).standard_normal(33).astype(np.float32)
+    f = EliasFpzip(float_precision=None)
+    np.testing.assert_array_equal(f.decompress_float(f.compress_float(x)).view(np.uint32),
+                                  x.view(np.uint32))
+    for cls in (Elias, EliasFpzip):
+        assert issubclass(cls, Compression)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure mode")
+def test_elias_fails_loudly_without_gpu():
+    import numpy as np
+
+    from decentralizepy_amd.compression.Elias import Elias
+    with pytest.raises(RuntimeError, match="no CPU path|CPU fallback"):
+        Elias().compress(np.array([1, 5, 9], np.int32))
