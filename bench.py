@@ -85,7 +85,7 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True):
     torch.cuda.synchronize()
     run = step
     if use_graph:
-        # one step = 8 dependent kernels; capture them once and replay (hipGraph), so the timed
+        # one step = 7 dependent kernels; capture them once and replay (hipGraph), so the timed
         # loop is not bound by per-kernel host launch cost.  Every kernel still runs every step.
         graph = torch.cuda.CUDAGraph()
         side = torch.cuda.Stream(dev)
@@ -115,13 +115,51 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True):
     s_step = t / steps
     # per-stage device time with events on the launch stream
     stream = torch.cuda.current_stream(dev)
-    t_enc = timed_loop(encode, max(20, steps // 2), stream)
-    t_dec = timed_loop(decode, max(20, steps // 2), stream)
+    reps = max(20, steps // 2)
+    t_enc = timed_loop(encode, reps, stream)
+    t_dec = timed_loop(decode, reps, stream)
+    # per-kernel device time: the library brackets every launch with a HIP event pair on the
+    # stream it launches on.  A GPU-side spin first lets the host queue all `reps` steps, so the
+    # kernels then run back-to-back as in the graph replay (no host-launch gaps inside a pair).
+    with codec.KernelTimer() as kt:
+        torch.cuda._sleep(int(200e6))  # ~0.1 s of GPU cycles while the steps are enqueued
+        for _ in range(reps):
+            step()
+        torch.cuda.synchronize()
+    kernels = {name: {"avg_us": ms / cnt * 1e3, "launches_per_step": cnt / reps}
+               for name, (ms, cnt) in kt.result.items()}
     b_enc = 8 * n + 8 * k + 8 * k      # read x, x0; write idx, val; counter[idx] += 1 (r+w)
     b_dec = 8 * n + 8 * k              # read local, payload; write out
     return dict(n=n, k=k, s_step=s_step, fell_back=fell_back, t_enc=t_enc, t_dec=t_dec,
-                b_enc=b_enc, b_dec=b_dec,
+                b_enc=b_enc, b_dec=b_dec, kernels=kernels,
                 value=world * 4 * n / s_step / 2 ** 30)
+
+
+def kernel_alg_bytes(name, n, k):
+    """Algorithmic HBM bytes of one launch: the bytes the operation must move,
+    not what the implementation happens to move (candidate lists, histograms are excluded)."""
+    return {
+        "topk_sample": 8 * 65536,          # x, x0 at the 65,536 sampled positions
+        "topk_filter": 8 * n,              # read x, x0 once
+        "topk_select": 0,                  # works on the ~1.9k candidates only
+        "topk_resolve": 0,                 # works on the ~k/256 boundary entries only
+        "topk_compact": 8 * k + 4 * k + 8 * k,  # write idx, val; gather vals; counter r+w
+        "fold_offsets": 4 * k,             # read the payload indices
+        "fold": 8 * n + 8 * k,             # read local, payload (idx, val); write out
+    }.get(name, 0)
+
+
+def load_pmc(kernel):
+    """HBM traffic per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pmc = json.load(f)
+    ent = pmc.get("kernels", {}).get(kernel)
+    if not ent:
+        return None
+    return ent.get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(n, alpha, seconds):
@@ -171,16 +209,34 @@ def main():
                  "frac_of_hbm_peak": round((e["b_enc"] + e["b_dec"]) / e["s_step"] / 1e9 / HBM_PEAK_GBS, 4),
                  "fell_back": e["fell_back"]}
 
+    copy_gbs = None
+    if rank == 0:  # context: what a plain device-to-device copy reaches on this box
+        a = torch.empty(64 * 2 ** 20, dtype=torch.float32, device=dev)
+        b = torch.empty_like(a)
+        for _ in range(3):
+            b.copy_(a)
+        t_copy = timed_loop(lambda: b.copy_(a), 20, torch.cuda.current_stream(dev))
+        copy_gbs = round(2 * a.numel() * 4 / t_copy / 1e9, 1)
+        del a, b
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.n, args.alpha, args.cpu_seconds)
 
     if rank == 0:
         t_enc, t_dec = r["t_enc"], r["t_dec"]
-        # dominant kernel: the decode fold kernel is a single launch -> priced per launch
         dec_gbs = r["b_dec"] / t_dec / 1e9
         enc_gbs = r["b_enc"] / t_enc / 1e9
         step_gbs = (r["b_enc"] + r["b_dec"]) / r["s_step"] / 1e9
+        kern = r["kernels"]
+        for name, kv in kern.items():
+            b = kernel_alg_bytes(name, r["n"], r["k"])
+            kv["alg_bytes"] = b
+            kv["GBps"] = round(b / (kv["avg_us"] * 1e-6) / 1e9, 1) if b else 0.0
+            kv["avg_us"] = round(kv["avg_us"], 3)
+        dom = max(kern, key=lambda nm: kern[nm]["avg_us"] * kern[nm]["launches_per_step"])
+        dk = kern[dom]
+        traffic = load_pmc(dom)
         line = {
             "metric": "GiB/s fp32 params encoded+decoded (device-resident), 1% top-k",
             "value": round(r["value"], 3),
@@ -198,18 +254,18 @@ def main():
                 "workload": "C2: PartialModel top-k encode + decode of one 11M-fp32 flattened tensor",
                 "n": r["n"], "k": r["k"], "alpha": args.alpha,
                 "parallelism": f"{world} independent per-node codecs (one per GPU), no collective",
-                "launch": "eager" if args.no_graph else "hipGraph replay of the 8-kernel step",
+                "launch": "eager" if args.no_graph else "hipGraph replay of the whole step",
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "fold_kernel (decode: replace payload into local copy; + its tile-offset pre-pass)",
-                "achieved": round(dec_gbs, 1),
+                "kernel": dom,
+                "achieved": dk["GBps"],
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(dec_gbs / HBM_PEAK_GBS, 4),
-                "traffic": None,
-                "bytes_per_launch": r["b_dec"],
-                "avg_launch_us": round(t_dec * 1e6, 3),
+                "frac": round(dk["GBps"] / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "alg_bytes_per_launch": dk["alg_bytes"],
+                "avg_launch_us": dk["avg_us"],
             },
             "stages": {
                 "encode": {"avg_us": round(t_enc * 1e6, 3), "alg_bytes": r["b_enc"],
@@ -218,6 +274,8 @@ def main():
                 "decode": {"avg_us": round(t_dec * 1e6, 3), "alg_bytes": r["b_dec"],
                            "GBps": round(dec_gbs, 1), "frac": round(dec_gbs / HBM_PEAK_GBS, 4)},
                 "step_frac_of_hbm_peak": round(step_gbs / HBM_PEAK_GBS, 4),
+                "kernels": kern,
+                "torch_copy_GBps_256MiB": copy_gbs,
             },
             "cpu_baseline": cpu,
             "secondary": extra,

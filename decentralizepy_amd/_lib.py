@@ -51,6 +51,9 @@ SIGNATURES = {
     "dpz_scatter_fill": (_int, [_c_void_p, _i64, _c_void_p, _i64, ctypes.c_float, _c_void_p]),
     "dpz_pack_fp16": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
     "dpz_unpack_fp16": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
+    "dpz_timing_enable": (_int, [_int]),
+    "dpz_timing_read": (_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64), _int]),
+    "dpz_kernel_name": (ctypes.c_char_p, [_int]),
     "dpz_elias_max_bytes": (_i64, [_i64]),
     "dpz_elias_workspace_bytes": (_size, [_i64, _i64]),
     "dpz_elias_encode": (_int, [_c_void_p, _i64, _c_void_p, _i64, ctypes.POINTER(_i64),

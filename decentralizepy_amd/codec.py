@@ -14,7 +14,8 @@ from ._lib import (DPZ_ACC_ACCUMULATE, DPZ_ACC_ADD, DPZ_ACC_NONE, DPZ_FOLD_REPLA
 
 __all__ = ["DPZ_ACC_NONE", "DPZ_ACC_ACCUMULATE", "DPZ_ACC_ADD", "Workspace", "topk_encode",
            "topk_complete", "decode_average", "replace", "wavedec_len", "wavedec", "waverec",
-           "pack_fp16", "unpack_fp16", "elias_encode", "elias_decode"]
+           "pack_fp16", "unpack_fp16", "elias_encode", "elias_decode",
+           "KernelTimer"]
 
 
 def _ptr(t):
@@ -274,3 +275,36 @@ def elias_decode(buf, nbytes, nbits, first, count, dtype=torch.int64, workspace=
         raise ValueError("malformed Elias stream")
     check(rc, "dpz_elias_decode")
     return out[:n.value]
+
+
+class KernelTimer:
+    """Per-kernel device time measured by the library with HIP event pairs on each launch's own
+    stream (``dpz_timing_*``).  Launches into a capturing stream are not timed.
+
+    >>> with KernelTimer() as t:
+    ...     topk_encode(...)
+    >>> t.result  # {"topk_filter": (ms_total, launches), ...}
+    """
+
+    N_MAX = 64
+
+    def __enter__(self):
+        _lib.lib().dpz_timing_enable(1)
+        self.result = {}
+        return self
+
+    def __exit__(self, *exc):
+        self.result = self.read()
+        _lib.lib().dpz_timing_enable(0)
+        return False
+
+    @classmethod
+    def read(cls):
+        ms = (ctypes.c_double * cls.N_MAX)()
+        cnt = (ctypes.c_int64 * cls.N_MAX)()
+        nk = _lib.lib().dpz_timing_read(ms, cnt, cls.N_MAX)
+        out = {}
+        for i in range(min(nk, cls.N_MAX)):
+            if cnt[i]:
+                out[_lib.lib().dpz_kernel_name(i).decode()] = (ms[i], int(cnt[i]))
+        return out

@@ -15,6 +15,21 @@
 #define DPZ_LAUNCH_CHECK() DPZ_HIP_TRY(hipGetLastError())
 
 namespace dpz {
+// dpz_timing.hip: optional per-kernel event timing (no-ops unless dpz_timing_enable(1))
+int timing_begin(int id, hipStream_t st);
+void timing_end(int slot, hipStream_t st);
+}  // namespace dpz
+
+// launch + error check, bracketed by timing events when timing is enabled
+#define DPZ_TIMED(id, st, ...)                          \
+  do {                                                  \
+    const int _dpz_tslot = ::dpz::timing_begin(id, st); \
+    __VA_ARGS__;                                        \
+    DPZ_LAUNCH_CHECK();                                 \
+    ::dpz::timing_end(_dpz_tslot, st);                  \
+  } while (0)
+
+namespace dpz {
 
 // |c| as an order-preserving uint32 key: sign cleared, every NaN -> 0x7FC00000 so that NaNs
 // rank above +inf and tie with each other (torch.topk treats NaN as the largest value).

@@ -250,6 +250,7 @@ extern "C" int dpz_dwt_sym2(const float* x, const float* x0, int64_t n, int leve
   constexpr int SPAN0 = 16 * DWT_TL + 64, SPAN1 = 8 * DWT_TL + 32;
   const size_t shm = 2 * (SPAN0 + SPAN1) * sizeof(float);
   const bool wx = coeffs_x != nullptr, wd = coeffs_diff != nullptr;
+  const int tslot = timing_begin(DPZ_KT_DWT, st);
   if (wx && wd) {
     if (accumulate) dwt_kernel<true, true, true><<<grid, 256, shm, st>>>(x, x0, LV, coeffs_x, coeffs_diff);
     else dwt_kernel<true, true, false><<<grid, 256, shm, st>>>(x, x0, LV, coeffs_x, coeffs_diff);
@@ -260,6 +261,7 @@ extern "C" int dpz_dwt_sym2(const float* x, const float* x0, int64_t n, int leve
     else dwt_kernel<false, true, false><<<grid, 256, shm, st>>>(x, x0, LV, nullptr, coeffs_diff);
   }
   DPZ_LAUNCH_CHECK();
+  timing_end(tslot, st);
   return DPZ_OK;
 }
 
@@ -270,7 +272,6 @@ extern "C" int dpz_idwt_sym2(const float* coeffs, int64_t n, int level, float* o
   if (!dwt_levels_ok(n, level)) return DPZ_ERR_UNSUPPORTED;
   const Levels LV = make_levels(n, level);
   const unsigned grid = (unsigned)((n + IDWT_TILE - 1) / IDWT_TILE);
-  idwt_kernel<<<grid, 256, 0, st>>>(coeffs, LV, out);
-  DPZ_LAUNCH_CHECK();
+  DPZ_TIMED(DPZ_KT_IDWT, st, idwt_kernel<<<grid, 256, 0, st>>>(coeffs, LV, out));
   return DPZ_OK;
 }

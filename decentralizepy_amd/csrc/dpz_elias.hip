@@ -397,12 +397,9 @@ extern "C" int dpz_elias_encode(const int32_t* idx, int64_t k, uint8_t* out, int
   uint64_t* blk_off = reinterpret_cast<uint64_t*>(p + al256(sizeof(ElHdr)) + al256(nblk * 8));
   uint32_t* out32 = reinterpret_cast<uint32_t*>(out);
   DPZ_HIP_TRY(hipMemsetAsync(hdr, 0, sizeof(ElHdr), st));
-  elias_count_kernel<<<(unsigned)nblk, 256, 0, st>>>(idx, ncodes, blk_bits, hdr);
-  DPZ_LAUNCH_CHECK();
-  elias_scan_kernel<<<1, 1024, 0, st>>>(idx, nblk, blk_bits, blk_off, hdr, out32);
-  DPZ_LAUNCH_CHECK();
-  elias_pack_kernel<<<(unsigned)nblk, 256, 0, st>>>(idx, ncodes, blk_bits, blk_off, out32);
-  DPZ_LAUNCH_CHECK();
+  DPZ_TIMED(DPZ_KT_ELIAS_COUNT, st, elias_count_kernel<<<(unsigned)nblk, 256, 0, st>>>(idx, ncodes, blk_bits, hdr));
+  DPZ_TIMED(DPZ_KT_ELIAS_SCAN, st, elias_scan_kernel<<<1, 1024, 0, st>>>(idx, nblk, blk_bits, blk_off, hdr, out32));
+  DPZ_TIMED(DPZ_KT_ELIAS_PACK, st, elias_pack_kernel<<<(unsigned)nblk, 256, 0, st>>>(idx, ncodes, blk_bits, blk_off, out32));
   ElHdr h;
   DPZ_HIP_TRY(hipMemcpyAsync(&h, hdr, sizeof(h), hipMemcpyDeviceToHost, st));
   DPZ_HIP_TRY(hipStreamSynchronize(st));
@@ -448,13 +445,10 @@ extern "C" int dpz_elias_decode(const uint8_t* in, int64_t nbytes, int64_t nbits
   const uint64_t nwords_in = (uint64_t)(nbytes - 16 + 3) / 4;  // code + padding words (trailer excluded)
   DPZ_HIP_TRY(hipMemsetAsync(hdr, 0, sizeof(ElHdr), st));
   const unsigned grid = (unsigned)((nch + 3) / 4);
-  elias_spec_kernel<<<grid, 256, 0, st>>>(in32, nwords_in, L, nch, exit_tab, cnt_tab, sum_tab);
-  DPZ_LAUNCH_CHECK();
-  elias_resolve_kernel<<<1, 1024, 0, st>>>(nch, exit_tab, cnt_tab, sum_tab, centry, cpos, cbase, hdr);
-  DPZ_LAUNCH_CHECK();
-  elias_write_kernel<<<grid, 256, 0, st>>>(in32, nwords_in, L, nch, first, centry, cpos, cbase, hdr,
-                                           out_cap, out64, out32);
-  DPZ_LAUNCH_CHECK();
+  DPZ_TIMED(DPZ_KT_ELIAS_SPEC, st, elias_spec_kernel<<<grid, 256, 0, st>>>(in32, nwords_in, L, nch, exit_tab, cnt_tab, sum_tab));
+  DPZ_TIMED(DPZ_KT_ELIAS_RESOLVE, st, elias_resolve_kernel<<<1, 1024, 0, st>>>(nch, exit_tab, cnt_tab, sum_tab, centry, cpos, cbase, hdr));
+  DPZ_TIMED(DPZ_KT_ELIAS_WRITE, st, elias_write_kernel<<<grid, 256, 0, st>>>(in32, nwords_in, L, nch, first, centry, cpos, cbase, hdr,
+                                           out_cap, out64, out32));
   ElHdr h;
   DPZ_HIP_TRY(hipMemcpyAsync(&h, hdr, sizeof(h), hipMemcpyDeviceToHost, st));
   DPZ_HIP_TRY(hipStreamSynchronize(st));

@@ -213,8 +213,8 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
     fa.np = 0; fa.first = 0;
     fa.add_self = (flags & DPZ_FOLD_SELF) ? 1 : 0; fa.w_self = w_self;
     DPZ_HIP_TRY(hipMemsetAsync(out, 0, n * sizeof(float), st));
-    if (vec) fold_kernel<true><<<grid, FOLD_THREADS, 0, st>>>(fa); else fold_kernel<false><<<grid, FOLD_THREADS, 0, st>>>(fa);
-    DPZ_LAUNCH_CHECK();
+    if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<true><<<grid, FOLD_THREADS, 0, st>>>(fa));
+    else DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<false><<<grid, FOLD_THREADS, 0, st>>>(fa));
     return DPZ_OK;
   }
   for (int base = 0; base < n_payloads; base += FOLD_MAXP) {
@@ -237,11 +237,10 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
     }
     if (kmax >= 0) {
       dim3 og((unsigned)((kmax + 1 + 255) / 256), (unsigned)fa.np);
-      fold_offsets_kernel<<<og, 256, 0, st>>>(fa, starts);
-      DPZ_LAUNCH_CHECK();
+      DPZ_TIMED(DPZ_KT_FOLD_OFFSETS, st, fold_offsets_kernel<<<og, 256, 0, st>>>(fa, starts));
     }
-    if (vec) fold_kernel<true><<<grid, FOLD_THREADS, 0, st>>>(fa); else fold_kernel<false><<<grid, FOLD_THREADS, 0, st>>>(fa);
-    DPZ_LAUNCH_CHECK();
+    if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<true><<<grid, FOLD_THREADS, 0, st>>>(fa));
+    else DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<false><<<grid, FOLD_THREADS, 0, st>>>(fa));
   }
   return DPZ_OK;
 }

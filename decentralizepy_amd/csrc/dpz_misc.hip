@@ -81,8 +81,8 @@ extern "C" int dpz_pack_fp16(const float* in, int64_t n, uint16_t* out, dpz_stre
   if (n == 0) return DPZ_OK;
   if ((reinterpret_cast<uintptr_t>(in) & 15u) || (reinterpret_cast<uintptr_t>(out) & 15u))
     return DPZ_ERR_ARG;
-  pack_fp16_kernel<<<grid_for(n >> 3), 256, 0, static_cast<hipStream_t>(stream)>>>(in, n, out);
-  DPZ_LAUNCH_CHECK();
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  DPZ_TIMED(DPZ_KT_FP16, st, pack_fp16_kernel<<<grid_for(n >> 3), 256, 0, st>>>(in, n, out));
   return DPZ_OK;
 }
 
@@ -91,8 +91,8 @@ extern "C" int dpz_unpack_fp16(const uint16_t* in, int64_t n, float* out, dpz_st
   if (n == 0) return DPZ_OK;
   if ((reinterpret_cast<uintptr_t>(in) & 15u) || (reinterpret_cast<uintptr_t>(out) & 15u))
     return DPZ_ERR_ARG;
-  unpack_fp16_kernel<<<grid_for(n >> 3), 256, 0, static_cast<hipStream_t>(stream)>>>(in, n, out);
-  DPZ_LAUNCH_CHECK();
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  DPZ_TIMED(DPZ_KT_FP16, st, unpack_fp16_kernel<<<grid_for(n >> 3), 256, 0, st>>>(in, n, out));
   return DPZ_OK;
 }
 
@@ -111,8 +111,8 @@ extern "C" int dpz_scatter_fill(float* dst, int64_t n, const int32_t* idx, int64
                                 dpz_stream_t stream) {
   if (n < 0 || k < 0 || (k > 0 && (!dst || !idx))) return DPZ_ERR_ARG;
   if (k == 0) return DPZ_OK;
-  scatter_fill_kernel<<<grid_for((k + 255) / 256 * 32), 256, 0,
-                        static_cast<hipStream_t>(stream)>>>(dst, idx, k, n, value);
-  DPZ_LAUNCH_CHECK();
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  DPZ_TIMED(DPZ_KT_SCATTER, st,
+            scatter_fill_kernel<<<grid_for((k + 255) / 256 * 32), 256, 0, st>>>(dst, idx, k, n, value));
   return DPZ_OK;
 }

@@ -96,8 +96,16 @@ constexpr int HB = 256;            // fine window bins (+1 "above window" bin)
 constexpr int HBR = HB + 1;
 constexpr int W_MAX = 8192;        // wave segments (one wave streams one contiguous segment)
 constexpr int W_MIN_RANGE = 1024;
-constexpr int BCAP = 8192;         // boundary entries selectC can hold
-constexpr int BSLOT = 32;          // boundary entries one wave segment can hold (more -> fallback)
+constexpr int GH_COPIES = 16;      // window histogram copies (filter block b adds into copy b % 16)
+constexpr int GH_STRIDE = 272;     // >= HBR, 16-aligned
+constexpr int SEL_SEGS = 32;       // wave segments per select block (16 waves x 2)
+constexpr int SEL_LCAP = 1024;     // boundary entries one select block stages in LDS
+constexpr int CMP_SEGS = 16;       // wave segments per compact block (16 waves x 1)
+constexpr int NSUB = 16;           // boundary sub-lists (one atomic per select block each)
+constexpr int SUBCAP = 256;        // entries per sub-list (more -> miss -> exact fallback)
+constexpr int BCAP = NSUB * SUBCAP;  // boundary entries compact can hold (more -> miss)
+constexpr int RANK_MAX = 1024;     // up to this many boundary entries: rank counting, else radix
+constexpr int B_MAX = W_MAX / 4;   // filter blocks (4 wave segments each)
 constexpr int STAGE = 128;         // per-wave LDS candidate staging (flushed in coalesced chunks)
 constexpr uint32_t DENSE = 0xFFFFFFFFu;
 
@@ -127,7 +135,7 @@ static inline size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
 
 struct WsLayout {
   size_t ctrl, chist, ex_hist, ex_gt, ex_eq, ex_off, ex_eqb;
-  size_t f_ghist, f_rows, f_segcnt, f_segabove, f_segoff, f_cidx, f_ckey, f_bcnt, f_bkey, f_bidx;
+  size_t f_ghist, f_segcnt, f_blkabove, f_cidx, f_ckey, f_blcnt, f_blkey, f_blidx;
   size_t total;
   int64_t ex_nblk;
   FastGeom fg;
@@ -146,16 +154,14 @@ static inline WsLayout ws_layout(int64_t n) {
   L.ex_eq = o; o += align256(L.ex_nblk * 4);
   L.ex_off = o; o += align256(L.ex_nblk * 4);
   L.ex_eqb = o; o += align256(L.ex_nblk * 4);
-  L.f_ghist = o; o += align256(512 * 4);
-  L.f_rows = o; o += align256((size_t)L.fg.B * HBR * 4);
+  L.f_ghist = o; o += align256(GH_COPIES * GH_STRIDE * 4);
+  L.f_blcnt = o; o += align256(NSUB * 4);
   L.f_segcnt = o; o += align256(L.fg.W * 4);
-  L.f_segabove = o; o += align256(L.fg.W * 4);
-  L.f_segoff = o; o += align256(L.fg.W * 4);
+  L.f_blkabove = o; o += align256(L.fg.B * 4);
   L.f_cidx = o; o += align256((size_t)L.fg.W * L.fg.CAP * 4);
   L.f_ckey = o; o += align256((size_t)L.fg.W * L.fg.CAP * 4);
-  L.f_bcnt = o; o += align256(L.fg.W * 4);
-  L.f_bkey = o; o += align256((size_t)L.fg.W * BSLOT * 4);
-  L.f_bidx = o; o += align256((size_t)L.fg.W * BSLOT * 4);
+  L.f_blkey = o; o += align256((size_t)BCAP * 4);
+  L.f_blidx = o; o += align256((size_t)BCAP * 4);
   L.total = o;
   return L;
 }

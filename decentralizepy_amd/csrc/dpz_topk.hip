@@ -54,8 +54,7 @@ static int run_accumulate_only(const EncodeArgs& a) {
   int nb = (int)((groups + 255) / 256);
   if (nb > 4096) nb = 4096;
   if (nb < 1) nb = 1;
-  accumulate_only_kernel<VEC><<<nb, 256, 0, a.st>>>(s, a.n);
-  DPZ_LAUNCH_CHECK();
+  DPZ_TIMED(DPZ_KT_ACCUMULATE, a.st, accumulate_only_kernel<VEC><<<nb, 256, 0, a.st>>>(s, a.n));
   return DPZ_OK;
 }
 

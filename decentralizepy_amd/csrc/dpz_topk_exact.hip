@@ -204,31 +204,22 @@ static int run_exact_t(const EncodeArgs& a, const WsLayout& L, int rekey) {
   if (hb > EX_HIST_BLOCKS) hb = EX_HIST_BLOCKS;
   if (hb < 1) hb = 1;
   const int store_acc = (a.acc_mode == DPZ_ACC_ACCUMULATE && !rekey) ? 1 : 0;
-  exact_hist_kernel<VEC, 0><<<hb, 256, 0, a.st>>>(s, a.n, ctrl, hist, store_acc);
-  DPZ_LAUNCH_CHECK();
+  DPZ_TIMED(DPZ_KT_EXACT_HIST, a.st, exact_hist_kernel<VEC, 0><<<hb, 256, 0, a.st>>>(s, a.n, ctrl, hist, store_acc));
   s.rekey = 1;
-  exact_resolve_kernel<0><<<1, 1024, 0, a.st>>>(ctrl, hist, (uint32_t)a.k);
-  DPZ_LAUNCH_CHECK();
-  exact_hist_kernel<VEC, 1><<<hb, 256, 0, a.st>>>(s, a.n, ctrl, hist + 1024, 0);
-  DPZ_LAUNCH_CHECK();
-  exact_resolve_kernel<1><<<1, 1024, 0, a.st>>>(ctrl, hist + 1024, (uint32_t)a.k);
-  DPZ_LAUNCH_CHECK();
-  exact_hist_kernel<VEC, 2><<<hb, 256, 0, a.st>>>(s, a.n, ctrl, hist + 3072, 0);
-  DPZ_LAUNCH_CHECK();
-  exact_resolve_kernel<2><<<1, 1024, 0, a.st>>>(ctrl, hist + 3072, (uint32_t)a.k);
-  DPZ_LAUNCH_CHECK();
+  DPZ_TIMED(DPZ_KT_EXACT_RESOLVE, a.st, exact_resolve_kernel<0><<<1, 1024, 0, a.st>>>(ctrl, hist, (uint32_t)a.k));
+  DPZ_TIMED(DPZ_KT_EXACT_HIST, a.st, exact_hist_kernel<VEC, 1><<<hb, 256, 0, a.st>>>(s, a.n, ctrl, hist + 1024, 0));
+  DPZ_TIMED(DPZ_KT_EXACT_RESOLVE, a.st, exact_resolve_kernel<1><<<1, 1024, 0, a.st>>>(ctrl, hist + 1024, (uint32_t)a.k));
+  DPZ_TIMED(DPZ_KT_EXACT_HIST, a.st, exact_hist_kernel<VEC, 2><<<hb, 256, 0, a.st>>>(s, a.n, ctrl, hist + 3072, 0));
+  DPZ_TIMED(DPZ_KT_EXACT_RESOLVE, a.st, exact_resolve_kernel<2><<<1, 1024, 0, a.st>>>(ctrl, hist + 3072, (uint32_t)a.k));
   uint32_t* bgt = reinterpret_cast<uint32_t*>(a.ws + L.ex_gt);
   uint32_t* beq = reinterpret_cast<uint32_t*>(a.ws + L.ex_eq);
   uint32_t* boff = reinterpret_cast<uint32_t*>(a.ws + L.ex_off);
   uint32_t* beqb = reinterpret_cast<uint32_t*>(a.ws + L.ex_eqb);
-  exact_count_kernel<VEC><<<(unsigned)L.ex_nblk, 256, 0, a.st>>>(s, a.n, ctrl, bgt, beq);
-  DPZ_LAUNCH_CHECK();
-  exact_scan_kernel<<<1, 1024, 0, a.st>>>(ctrl, L.ex_nblk, bgt, beq, boff, beqb);
-  DPZ_LAUNCH_CHECK();
+  DPZ_TIMED(DPZ_KT_EXACT_COUNT, a.st, exact_count_kernel<VEC><<<(unsigned)L.ex_nblk, 256, 0, a.st>>>(s, a.n, ctrl, bgt, beq));
+  DPZ_TIMED(DPZ_KT_EXACT_SCAN, a.st, exact_scan_kernel<<<1, 1024, 0, a.st>>>(ctrl, L.ex_nblk, bgt, beq, boff, beqb));
   float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE) ? a.acc : nullptr;
-  exact_write_kernel<VEC><<<(unsigned)L.ex_nblk, 256, 0, a.st>>>(
-      s, a.n, ctrl, boff, beqb, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, a.k);
-  DPZ_LAUNCH_CHECK();
+  DPZ_TIMED(DPZ_KT_EXACT_WRITE, a.st, exact_write_kernel<VEC><<<(unsigned)L.ex_nblk, 256, 0, a.st>>>(
+      s, a.n, ctrl, boff, beqb, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, a.k));
   return DPZ_OK;
 }
 

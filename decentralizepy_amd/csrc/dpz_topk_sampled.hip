@@ -2,24 +2,26 @@
 //
 // Work unit = one WAVE streaming one contiguous "wave segment" of R elements: ordered compaction
 // inside a segment is a ballot + mbcnt prefix (no LDS scan, no barriers in the streaming loop),
-// so the 32 waves of a CU drift apart and keep HBM busy.  Kernels:
-//   sample  : 64 blocks histogram 65,536 sampled keys (1024 chunks x 64) into chist[key >> 20]
+// so the 32 waves of a CU drift apart and keep HBM busy.  Five kernels per call:
+//   sample  : 64 blocks histogram 65,536 sampled keys (1024 chunks x 64) into chist[key >> 20];
+//             zero this call's window-histogram copies and boundary sub-list counters
 //   filter  : per block, wave 0 turns chist into the key window [lo, hi) while every wave's first
 //             loads are in flight; each wave streams its segment once (x, x0[, acc] -> key),
 //             appends keys >= lo in index order to its candidate list (idx, key; staged in LDS
-//             and flushed in coalesced chunks), and bins them into the block's 256-bin window
-//             histogram (LDS) -> one row per block
-//   selectA : column sums of the rows -> global window histogram
-//   selectB : per wave: threshold bin b* (redundant 257-bin scan), count of its candidates above
-//             b*, bin-b* entries into the segment's own boundary slots (no global atomics: a
-//             contended device-scope atomic costs ~20 ns per arrival on MI355X)
-//   selectC : 1 block: radix select inside bin b* -> exact T and tie cut (lowest index), then
-//             per-segment output offsets by an exclusive scan
-//   compact : per wave: ordered write of selected (idx, vals_src[idx]) + counter / rewind;
-//             block 0 re-zeroes chist for the next call
+//             and flushed in coalesced chunks) and bins them into a 256-bin window histogram in
+//             LDS, folded into copy (block % 16) of the global histogram with atomics
+//   select  : 32 segments per block: sum the 16 copies, threshold bin b* (wave 0), per filter
+//             block the count above b*, bin-b* entries staged in LDS and appended to sub-list
+//             (block % 16) with one atomic (a contended device-scope atomic costs ~20 ns per
+//             arrival on MI355X, so no single global counter anywhere)
+//   resolve : 1 block: radix select over the ~k/256 boundary entries -> exact threshold T and
+//             tie cut (lowest index); checks above + selected == k
+//   compact : 16 segments per block: output offset from the above counts of the filter blocks
+//             before it + the selected boundary entries below it, then each wave writes its
+//             selected (idx, vals_src[idx]) in index order (+ counter / rewind)
 // A miss (window does not bracket the k-th key / boundary overflow) sets ctrl->status and compact
 // writes nothing; the host then runs the exact path.  A segment whose candidates overflow its
-// list is DENSE and re-reads its input range in selectB / compact (still exact).
+// list is DENSE and re-reads its input range in select / compact (still exact).
 #include "dpz_topk.h"
 
 namespace dpz {
@@ -30,7 +32,11 @@ __device__ unsigned long long g_stamps[64];
 #define STAMP_MIN(i) do { if (threadIdx.x == 0) atomicMin(&g_stamps[i], __builtin_amdgcn_s_memrealtime()); } while (0)
 #define STAMP_MAX(i) do { __syncthreads(); if (threadIdx.x == 0) atomicMax(&g_stamps[i], __builtin_amdgcn_s_memrealtime()); } while (0)
 #define STAMP_ONE(i) do { if (threadIdx.x == 0) g_stamps[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// per-block phase stamps of one kernel (plain stores, no contention): g_bst[phase][block]
+__device__ unsigned long long g_bst[16][4096];
+#define STAMP_T0(i) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_bst[i][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
+#define STAMP_T0(i) do {} while (0)
 #define STAMP_MIN(i) do {} while (0)
 #define STAMP_MAX(i) do {} while (0)
 #define STAMP_ONE(i) do {} while (0)
@@ -51,7 +57,8 @@ __device__ __forceinline__ int64_t sample_pos(int c, int lane, int64_t n) {
 
 // 64 blocks x 256: 1024 chunks of 64 contiguous elements spread evenly over [0, n).
 __global__ void __launch_bounds__(256) sampled_sample_kernel(KeySrc s, int64_t n, TopkCtrl* ctrl,
-                                                             uint32_t* chist, uint32_t* ghist) {
+                                                             uint32_t* chist, uint32_t* ghist,
+                                                             uint32_t* blcnt) {
   STAMP_MIN(0);
   __shared__ uint32_t h[CB];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -64,8 +71,11 @@ __global__ void __launch_bounds__(256) sampled_sample_kernel(KeySrc s, int64_t n
     v[r] = d;
   }
   for (int b = threadIdx.x; b < CB; b += 256) h[b] = 0;
+  // this call's window histogram copies and boundary sub-list counters start at zero
+  for (int b = blockIdx.x * 256 + threadIdx.x; b < GH_COPIES * GH_STRIDE; b += SMP_BLOCKS * 256)
+    ghist[b] = 0;
   if (blockIdx.x == 0) {
-    for (int b = threadIdx.x; b < 512; b += 256) ghist[b] = 0;
+    if (threadIdx.x < NSUB) blcnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
       ctrl->status = 0;
       ctrl->nbound = 0;
@@ -158,7 +168,7 @@ struct WaveList {
 template <bool VEC>
 __global__ void __launch_bounds__(256, 8) sampled_filter_kernel(
     KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl,
-    const uint32_t* __restrict__ chist, uint32_t* rows, uint32_t* segcnt, uint32_t* cidx,
+    const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt, uint32_t* cidx,
     uint32_t* ckey) {
   __shared__ uint32_t h[HBR];
   __shared__ uint32_t win[4];
@@ -252,34 +262,15 @@ __global__ void __launch_bounds__(256, 8) sampled_filter_kernel(
   }
   if (!dense) L.flush(lane);
   __syncthreads();
-  uint32_t* row = rows + (int64_t)blockIdx.x * HBR;
-  for (int b = threadIdx.x; b < HBR; b += 256) row[b] = h[b];
+  // fold the block's window histogram into copy b % 16 (non-returning atomics; ~B/16 arrivals
+  // per address instead of B)
+  uint32_t* gcopy = ghist + (blockIdx.x & (GH_COPIES - 1)) * GH_STRIDE;
+  for (int b = threadIdx.x; b < HBR; b += 256) {
+    const uint32_t v = h[b];
+    if (v) atomicAdd(&gcopy[b], v);
+  }
   if (lane == 0 && seg < W) segcnt[seg] = dense ? DENSE : run;
   STAMP_MAX(3);
-}
-
-// column sums of the per-block window histograms (unrolled independent loads)
-__global__ void __launch_bounds__(256) sampled_selectA_kernel(const uint32_t* __restrict__ rows,
-                                                              int64_t B, uint32_t* ghist) {
-  STAMP_MIN(4);
-  const int64_t per = (B + gridDim.x - 1) / gridDim.x;
-  const int64_t r0 = blockIdx.x * per;
-  const int64_t r1 = (r0 + per < B) ? r0 + per : B;
-  if (r0 >= r1) return;
-  for (int b = threadIdx.x; b < HBR; b += 256) {
-    uint32_t sum = 0;
-    int64_t r = r0;
-    for (; r + 8 <= r1; r += 8) {
-      uint32_t v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = rows[(r + u) * HBR + b];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) sum += v[u];
-    }
-    for (; r < r1; ++r) sum += rows[r * HBR + b];
-    if (sum) atomicAdd(&ghist[b], sum);
-  }
-  STAMP_MAX(5);
 }
 
 // Wave-level threshold bin from the global window histogram.  ghv = fine bins [252-4l, 255-4l].
@@ -307,139 +298,47 @@ __device__ __forceinline__ bool wave_bstar(uint4 ghv, uint32_t above, uint32_t k
   return ok;
 }
 
-// ceil(W/4) blocks x 256: wave per segment.  No global atomics: bin-b* entries go to the
-// segment's own BSLOT boundary slots (count in bcnt; > BSLOT -> selectC reports a miss).
-template <bool VEC>
-__global__ void __launch_bounds__(256, 8) sampled_selectB_kernel(
-    KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl,
-    const uint32_t* __restrict__ ghist, const uint32_t* __restrict__ segcnt,
-    const uint32_t* __restrict__ cidx, const uint32_t* __restrict__ ckey, uint32_t* segabove,
-    uint32_t* bcnt, uint32_t* bkey, uint32_t* bidx) {
-  STAMP_MIN(6);
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t seg = (int64_t)blockIdx.x * 4 + wid;
-  const uint4 ghv = reinterpret_cast<const uint4*>(ghist)[63 - lane];
-  const uint32_t above_bin = ghist[HB];
-  const uint32_t cnt = seg < W ? segcnt[seg] : 0u;
-  const uint32_t lo = ctrl->lo, hi = ctrl->hi, shift = ctrl->shift;
-  uint32_t bstar, need;
-  const bool ok = wave_bstar(ghv, above_bin, (uint32_t)k, &bstar, &need);
-  if (!ok) {
-    if (seg == 0 && lane == 0) ctrl->status = 1;
-    return;
-  }
-  if (seg == 0 && lane == 0) {
-    ctrl->bstar = bstar;
-    ctrl->need = need;
-  }
-  if (seg >= W) return;
-  uint32_t* my_bkey = bkey + seg * BSLOT;
-  uint32_t* my_bidx = bidx + seg * BSLOT;
-  uint32_t above = 0, brun = 0;
-  if (cnt != DENSE) {
-    for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
-      const uint32_t j = j0 + lane;
-      uint32_t key = 0, b = 0;
-      if (j < cnt) {
-        key = ckey[seg * CAP + j];
-        b = fine_bin(key, lo, hi, shift);
-      }
-      const bool in = j < cnt && b == bstar;
-      above += (uint32_t)__popcll(__ballot(j < cnt && b > bstar));
-      const uint64_t m = __ballot(in);
-      if (in) {
-        const uint32_t p = brun + mbcnt64(m);
-        if (p < BSLOT) {
-          my_bkey[p] = key;
-          my_bidx[p] = cidx[seg * CAP + j];
-        }
-      }
-      brun += (uint32_t)__popcll(m);
-    }
-  } else {
-    const int64_t beg = seg * R;
-    const int64_t end = (beg + R < n) ? beg + R : n;
-    for (int64_t i0 = beg + lane * 4; i0 - lane * 4 < end; i0 += 256) {
-      uint32_t key[4];
-      const int c = i0 < end ? load_keys4<VEC>(s, i0, end, false, key) : 0;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bool valid = e < c && key[e] >= lo;
-        const uint32_t b = valid ? fine_bin(key[e], lo, hi, shift) : 0u;
-        const bool in = valid && b == bstar;
-        above += (uint32_t)__popcll(__ballot(valid && b > bstar));
-        const uint64_t m = __ballot(in);
-        if (in) {
-          const uint32_t p = brun + mbcnt64(m);
-          if (p < BSLOT) {
-            my_bkey[p] = key[e];
-            my_bidx[p] = (uint32_t)(i0 + e);
-          }
-        }
-        brun += (uint32_t)__popcll(m);
-      }
-    }
-  }
-  if (lane == 0) {
-    segabove[seg] = above;
-    bcnt[seg] = brun;
-  }
-#ifdef DPZ_STAMPS
-  if (lane == 0) atomicMax(&g_stamps[7], __builtin_amdgcn_s_memrealtime());
-#endif
-}
-
-// One block of 1024 threads: gather the boundary slots, radix-select inside bin b* -> exact T and
-// tie cut, then per-segment output offsets.
-__global__ void __launch_bounds__(1024) sampled_selectC_kernel(
-    int64_t k, int64_t W, int64_t R, TopkCtrl* ctrl, const uint32_t* __restrict__ bcnt,
-    const uint32_t* __restrict__ bkey, const uint32_t* __restrict__ bidx,
-    const uint32_t* __restrict__ segabove, uint32_t* segoff) {
+// One block of 1024 threads: gather the boundary sub-lists, radix-select the need-th largest key
+// inside bin b* (offsets below 2^shift, 8-bit digits), then the tie cut (the lowest indices among
+// keys == T), and check that above + selected == k.  Writes T, icut or a status for the host.
+__global__ void __launch_bounds__(1024) sampled_resolve_kernel(
+    int64_t k, int64_t B, TopkCtrl* ctrl, const uint32_t* __restrict__ blcnt,
+    const uint32_t* __restrict__ blkey, const uint32_t* __restrict__ blidx,
+    const uint32_t* __restrict__ blkabove) {
   constexpr int PER = BCAP / 1024;
-  constexpr int SPT = W_MAX / 1024;  // segments per thread (contiguous)
+  constexpr int BPT = B_MAX / 1024;
   __shared__ uint32_t hist[256];
-  __shared__ uint32_t segsel[W_MAX];  // first per-segment boundary bases, then selected counts
+  __shared__ uint32_t subbase[NSUB + 1];
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t sh[4];
-  STAMP_ONE(8);
+  STAMP_T0(12);
   const int t = threadIdx.x;
   const uint32_t status = ctrl->status;
-  const uint32_t need = ctrl->need;
-  const uint32_t lo = ctrl->lo, shift = ctrl->shift, bstar = ctrl->bstar;
-  uint32_t sa[SPT], bc[SPT];
-  uint32_t mycnt = 0, over = 0;
+  const uint32_t need = ctrl->need, lo = ctrl->lo, shift = ctrl->shift, bstar = ctrl->bstar;
+  const uint32_t sc = t < NSUB ? blcnt[t] : 0u;
+  uint32_t ba = 0;
 #pragma unroll
-  for (int q = 0; q < SPT; ++q) {
-    const int64_t sg = (int64_t)t * SPT + q;
-    sa[q] = sg < W ? segabove[sg] : 0u;
-    bc[q] = sg < W ? bcnt[sg] : 0u;
+  for (int q = 0; q < BPT; ++q) {
+    const int64_t fb = (int64_t)t * BPT + q;
+    ba += fb < B ? blkabove[fb] : 0u;
   }
   if (status) return;
-  STAMP_ONE(9);
-#pragma unroll
-  for (int q = 0; q < SPT; ++q) {
-    over |= bc[q] > (uint32_t)BSLOT;
-    mycnt += bc[q];
-  }
-  uint32_t nb;
-  uint32_t lbase = block_excl_scan(mycnt, wsum, &nb);
-  const int anyover = __syncthreads_or((int)over);
-  if (anyover || nb > BCAP || need == 0 || need > nb) {
-    if (t == 0) ctrl->status = 1;
-    return;
-  }
-  {  // per-segment bases of the flattened boundary list
-    uint32_t b = lbase;
-#pragma unroll
-    for (int q = 0; q < SPT; ++q) {
-      segsel[t * SPT + q] = b;
-      b += bc[q];
+  if (t < 64) {
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan(sc, &tot);
+    const bool over = __ballot(sc > (uint32_t)SUBCAP) != 0;
+    if (t < NSUB) subbase[t] = ex;
+    if (t == 0) {
+      subbase[NSUB] = tot;
+      sh[3] = over ? 1u : 0u;
     }
   }
   __syncthreads();
-  STAMP_ONE(10);
-  // entry j -> owning segment = last segment whose base <= j (LDS binary search); all the
-  // global loads of this thread are independent and issue together
+  const uint32_t nb = subbase[NSUB];
+  if (sh[3] || nb > BCAP || need == 0 || need > nb) {
+    if (t == 0) ctrl->status = 1;
+    return;
+  }
   uint32_t kk[PER], ii[PER];
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
@@ -447,24 +346,17 @@ __global__ void __launch_bounds__(1024) sampled_selectC_kernel(
     kk[q] = 0u;
     ii[q] = 0u;
     if (j < nb) {
-      uint32_t a = 0, z = (uint32_t)W;
-      while (z - a > 1) {
-        const uint32_t mid = (a + z) >> 1;
-        if (segsel[mid] <= j) a = mid; else z = mid;
-      }
-      const uint32_t slot = j - segsel[a];
-      kk[q] = bkey[(int64_t)a * BSLOT + slot];
-      ii[q] = bidx[(int64_t)a * BSLOT + slot];
+      int sb = 0;
+#pragma unroll
+      for (int u = 1; u < NSUB; ++u) sb += subbase[u] <= j ? 1 : 0;
+      const uint32_t slot = j - subbase[sb];
+      kk[q] = blkey[sb * SUBCAP + slot];
+      ii[q] = blidx[sb * SUBCAP + slot];
     }
   }
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < SPT; ++q) segsel[t * SPT + q] = 0;
-  // radix select of the need-th largest key inside bin b*: offsets o = key - base < 2^shift
+  STAMP_T0(13);
   const uint32_t base = lo + (bstar << shift);
-  uint32_t prefix = 0;   // resolved high bits of the offset
-  uint32_t rem = need;   // rank still to resolve among entries matching prefix (1-based)
-  uint32_t eqcnt = nb;   // entries equal to T (exact after the last digit)
+  uint32_t prefix = 0, rem = need, eqcnt = nb;
   for (int top = (int)shift; top > 0; top -= 8) {
     const int d = top >= 8 ? 8 : top;
     const int low = top - d;
@@ -495,8 +387,7 @@ __global__ void __launch_bounds__(1024) sampled_selectC_kernel(
     __syncthreads();
   }
   const uint32_t T = base + prefix;
-  STAMP_ONE(11);
-  // ties: take the `rem` lowest indices among entries with key == T
+  STAMP_T0(14);
   uint32_t icut = 0xFFFFFFFFu;
   if (rem < eqcnt) {
     uint32_t ipre = 0, irem = rem;
@@ -525,54 +416,272 @@ __global__ void __launch_bounds__(1024) sampled_selectC_kernel(
     }
     icut = ipre;
   }
+  uint32_t nsel = 0;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const uint32_t j = t + q * 1024;
-    if (j < nb && (kk[q] > T || (kk[q] == T && ii[q] <= icut)))
-      atomicAdd(&segsel[ii[q] / (uint32_t)R], 1u);
+    nsel += (j < nb && (kk[q] > T || (kk[q] == T && ii[q] <= icut))) ? 1u : 0u;
   }
+  uint32_t tot_a, tot_s;
+  (void)block_excl_scan(ba, wsum, &tot_a);
+  (void)block_excl_scan(nsel, wsum, &tot_s);
   if (t == 0) {
     ctrl->T = T;
     ctrl->icut = icut;
+    if (tot_a + tot_s != (uint32_t)k) ctrl->status = 2;  // internal inconsistency
   }
-  __syncthreads();
-  uint32_t v[SPT], local = 0;
-#pragma unroll
-  for (int q = 0; q < SPT; ++q) {
-    v[q] = sa[q] + segsel[t * SPT + q];
-    local += v[q];
-  }
-  uint32_t tot;
-  uint32_t ex = block_excl_scan(local, wsum, &tot);
-#pragma unroll
-  for (int q = 0; q < SPT; ++q) {
-    const int64_t sg = (int64_t)t * SPT + q;
-    if (sg < W) segoff[sg] = ex;
-    ex += v[q];
-  }
-  if (t == 0 && tot != (uint32_t)k) ctrl->status = 2;  // internal inconsistency
-  STAMP_ONE(12);
 }
 
+// ceil(W/32) blocks x 1024 (16 waves x 2 wave segments).  Sums the 16 window-histogram copies,
+// finds the threshold bin b* (wave 0), counts each filter block's candidates above b*
+// (blkabove) and appends the bin-b* entries, staged in LDS, to sub-list (block % 16) with one
+// atomic per block.
 template <bool VEC>
-__global__ void __launch_bounds__(256, 8) sampled_compact_kernel(
-    KeySrc s, int64_t n, int64_t W, int64_t R, int64_t CAP, const TopkCtrl* ctrl, uint32_t* chist,
-    const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ segoff,
-    const uint32_t* __restrict__ cidx, const uint32_t* __restrict__ ckey, const float* vals_src,
-    int32_t* idx_out, float* val_out, int32_t* counter, float* rewind, int64_t k) {
-  STAMP_MIN(13);
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (blockIdx.x == 0) {  // leave the coarse sample histogram zeroed for the next call
-    for (int b = threadIdx.x; b < CB; b += 256) chist[b] = 0;
+__global__ void __launch_bounds__(1024) sampled_select_kernel(
+    KeySrc s, int64_t n, int64_t k, int64_t W, int64_t B, int64_t R, int64_t CAP, TopkCtrl* ctrl,
+    const uint32_t* __restrict__ ghist, const uint32_t* __restrict__ segcnt,
+    const uint32_t* __restrict__ cidx, const uint32_t* __restrict__ ckey, uint32_t* blkabove,
+    uint32_t* blcnt, uint32_t* blkey, uint32_t* blidx) {
+  STAMP_MIN(6);
+  STAMP_T0(8);
+  __shared__ __attribute__((aligned(16))) uint32_t gh[GH_STRIDE];
+  __shared__ uint32_t fbabove[SEL_SEGS / 4];
+  __shared__ uint32_t lkey[SEL_LCAP], lidx[SEL_LCAP];
+  __shared__ uint32_t lcnt, gbase, sb_bstar, sb_need, sb_ok;
+  const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
+  const int64_t seg0 = (int64_t)blockIdx.x * SEL_SEGS + wid * 2;
+  const uint32_t cnt0 = seg0 < W ? segcnt[seg0] : 0u;
+  const uint32_t cnt1 = seg0 + 1 < W ? segcnt[seg0 + 1] : 0u;
+  const uint32_t lo = ctrl->lo, hi = ctrl->hi, shift = ctrl->shift;
+  if (t < HBR) {
+    uint32_t v[GH_COPIES];
+#pragma unroll
+    for (int c = 0; c < GH_COPIES; ++c) v[c] = ghist[c * GH_STRIDE + t];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int c = 0; c < GH_COPIES; ++c) sum += v[c];
+    gh[t] = sum;
   }
-  const int64_t seg = (int64_t)blockIdx.x * 4 + wid;
+  if (t < SEL_SEGS / 4) fbabove[t] = 0;
+  if (t == 0) lcnt = 0;
+  __syncthreads();
+  if (wid == 0) {
+    uint32_t bstar, need;
+    const uint4 ghv = reinterpret_cast<const uint4*>(gh)[63 - lane];
+    const bool ok = wave_bstar(ghv, gh[HB], (uint32_t)k, &bstar, &need);
+    if (lane == 0) {
+      sb_bstar = bstar;
+      sb_need = need;
+      sb_ok = ok ? 1u : 0u;
+    }
+  }
+  __syncthreads();
+  if (!sb_ok) {  // identical in every block: the whole grid leaves
+    if (blockIdx.x == 0 && t == 0) ctrl->status = 1;
+    return;
+  }
+  STAMP_T0(9);
+  const uint32_t bstar = sb_bstar;
+  if (blockIdx.x == 0 && t == 0) {
+    ctrl->bstar = bstar;
+    ctrl->need = sb_need;
+  }
+  auto append = [&](bool in, uint32_t key, uint32_t idx) {
+    const uint64_t m = __ballot(in);
+    if (m) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&lcnt, (uint32_t)__popcll(m));
+      base = __shfl(base, 0, 64);
+      if (in) {
+        const uint32_t p = base + mbcnt64(m);
+        if (p < SEL_LCAP) {
+          lkey[p] = key;
+          lidx[p] = idx;
+        }
+      }
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int64_t seg = seg0 + u;
+    const uint32_t cnt = u ? cnt1 : cnt0;
+    uint32_t above = 0;
+    if (seg < W && cnt != DENSE) {
+      for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        uint32_t key = 0, b = 0, idx = 0;
+        if (j < cnt) {
+          key = ckey[seg * CAP + j];
+          idx = cidx[seg * CAP + j];
+          b = fine_bin(key, lo, hi, shift);
+        }
+        above += (uint32_t)__popcll(__ballot(j < cnt && b > bstar));
+        append(j < cnt && b == bstar, key, idx);
+      }
+    } else if (seg < W) {
+      const int64_t beg = seg * R;
+      const int64_t end = (beg + R < n) ? beg + R : n;
+      for (int64_t i0 = beg + lane * 4; i0 - lane * 4 < end; i0 += 256) {
+        uint32_t key[4];
+        const int c = i0 < end ? load_keys4<VEC>(s, i0, end, false, key) : 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool valid = e < c && key[e] >= lo;
+          const uint32_t b = valid ? fine_bin(key[e], lo, hi, shift) : 0u;
+          above += (uint32_t)__popcll(__ballot(valid && b > bstar));
+          append(valid && b == bstar, key[e], (uint32_t)(i0 + e));
+        }
+      }
+    }
+    if (lane == 0 && above) atomicAdd(&fbabove[(wid * 2 + u) >> 2], above);
+  }
+  __syncthreads();
+  if (t < SEL_SEGS / 4) {
+    const int64_t fb = (int64_t)blockIdx.x * (SEL_SEGS / 4) + t;
+    if (fb < B) blkabove[fb] = fbabove[t];
+  }
+  STAMP_T0(10);
+  const uint32_t nl = lcnt;
+  if (nl) {
+    const int sub = (int)(blockIdx.x & (NSUB - 1));
+    if (t == 0) gbase = atomicAdd(&blcnt[sub], nl > SEL_LCAP ? (uint32_t)BCAP : nl);
+    __syncthreads();
+    const uint32_t gb = gbase;
+    for (uint32_t j = t; j < nl && j < SEL_LCAP; j += 1024) {
+      const uint32_t p = gb + j;
+      if (p < SUBCAP) {
+        blkey[sub * SUBCAP + p] = lkey[j];
+        blidx[sub * SUBCAP + p] = lidx[j];
+      }
+    }
+  }
+  STAMP_T0(11);
+}
+
+// ceil(W/16) blocks x 1024 (16 waves x 1 wave segment).  Every block redundantly resolves the
+// exact threshold T and tie cut from the ~k/256 boundary entries (L2-resident), derives its output
+// offset from the per-filter-block above counts and the selected boundary entries below its
+// range, checks the total against k, then each wave writes its selected (idx, vals_src[idx]) in
+// index order with counter / rewind updates.  Block 0 re-zeroes the sample histogram.
+template <bool VEC>
+__global__ void __launch_bounds__(1024) sampled_compact_kernel(
+    KeySrc s, int64_t n, int64_t k, int64_t W, int64_t B, int64_t R, int64_t CAP, TopkCtrl* ctrl,
+    uint32_t* chist, const uint32_t* __restrict__ blcnt, const uint32_t* __restrict__ blkey,
+    const uint32_t* __restrict__ blidx, const uint32_t* __restrict__ blkabove,
+    const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ cidx,
+    const uint32_t* __restrict__ ckey, const float* vals_src, int32_t* idx_out, float* val_out,
+    int32_t* counter, float* rewind) {
+  constexpr int BPT = B_MAX / 1024;
+  __shared__ uint32_t subbase[NSUB + 1];
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t wcnt[16];
+  STAMP_MIN(13);
+  STAMP_T0(0);
+  const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
+  const int64_t seg = (int64_t)blockIdx.x * CMP_SEGS + wid;
+  const int64_t fb0 = (int64_t)blockIdx.x * (CMP_SEGS / 4);  // first filter block of this block
+  // independent loads first
   const uint32_t status = ctrl->status;
-  const uint32_t T = ctrl->T, icut = ctrl->icut, lo = ctrl->lo;
+  const uint32_t lo = ctrl->lo, T = ctrl->T, icut = ctrl->icut;
+  const uint32_t sc = t < NSUB ? blcnt[t] : 0u;
+  uint32_t ba[BPT];
+#pragma unroll
+  for (int q = 0; q < BPT; ++q) {
+    const int64_t fb = (int64_t)t * BPT + q;
+    ba[q] = fb < B ? blkabove[fb] : 0u;
+  }
   const uint32_t cnt = seg < W ? segcnt[seg] : 0u;
-  uint32_t run = seg < W ? segoff[seg] : 0u;
-  if (status || seg >= W) return;
-  if (cnt != DENSE) {
-    for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
+  const bool dense = cnt == DENSE;
+  uint32_t key0 = 0, idx0 = 0;
+  if (seg < W && !dense && (uint32_t)lane < cnt) {
+    key0 = ckey[seg * CAP + lane];
+    idx0 = cidx[seg * CAP + lane];
+  }
+  if (blockIdx.x == 0) {  // leave the sample histogram zeroed for the next call
+    for (int b = t; b < CB; b += 1024) chist[b] = 0;
+  }
+  if (status) return;
+  if (t < 64) {
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan(sc, &tot);
+    if (t < NSUB) subbase[t] = ex;
+    if (t == 0) subbase[NSUB] = tot;
+  }
+  __syncthreads();
+  STAMP_T0(1);
+  // output offset of this block: above counts of the filter blocks before it + the selected
+  // boundary entries below its first index
+  const uint32_t nb = subbase[NSUB];
+  const uint32_t start_idx = (uint32_t)(fb0 * 4 * R);
+  uint32_t before = 0;
+#pragma unroll
+  for (int q = 0; q < BPT; ++q) {
+    const int64_t fb = (int64_t)t * BPT + q;
+    if (fb < fb0) before += ba[q];
+  }
+  for (uint32_t j = t; j < nb; j += 1024) {
+    int sb = 0;
+#pragma unroll
+    for (int u = 1; u < NSUB; ++u) sb += subbase[u] <= j ? 1 : 0;
+    const uint32_t slot = j - subbase[sb];
+    const uint32_t key = blkey[sb * SUBCAP + slot], idx = blidx[sb * SUBCAP + slot];
+    before += (idx < start_idx && (key > T || (key == T && idx <= icut))) ? 1u : 0u;
+  }
+  uint32_t base_off;
+  (void)block_excl_scan(before, wsum, &base_off);
+  STAMP_T0(2);
+  // count pass (first 64 list entries stay in registers), wave offsets, write pass
+  uint32_t mine = 0;
+  bool sel0 = false;
+  if (seg < W && !dense) {
+    sel0 = (uint32_t)lane < cnt && (key0 > T || (key0 == T && idx0 <= icut));
+    mine = (uint32_t)__popcll(__ballot(sel0));
+    for (uint32_t j0 = 64; j0 < cnt; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      bool sel = false;
+      if (j < cnt) {
+        const uint32_t key = ckey[seg * CAP + j];
+        const uint32_t idx = cidx[seg * CAP + j];
+        sel = key > T || (key == T && idx <= icut);
+      }
+      mine += (uint32_t)__popcll(__ballot(sel));
+    }
+  } else if (seg < W) {
+    const int64_t beg = seg * R;
+    const int64_t end = (beg + R < n) ? beg + R : n;
+    for (int64_t i0 = beg + lane * 4; i0 - lane * 4 < end; i0 += 256) {
+      uint32_t key[4];
+      const int c = i0 < end ? load_keys4<VEC>(s, i0, end, false, key) : 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool f = e < c && key[e] >= lo &&
+                       (key[e] > T || (key[e] == T && (uint32_t)(i0 + e) <= icut));
+        mine += (uint32_t)__popcll(__ballot(f));
+      }
+    }
+  }
+  if (lane == 0) wcnt[wid] = mine;
+  __syncthreads();
+  STAMP_T0(3);
+  uint32_t run = base_off;
+  for (int w = 0; w < wid; ++w) run += wcnt[w];
+  if (seg >= W) return;
+  auto emit = [&](bool sel, uint32_t idx) {
+    const uint64_t m = __ballot(sel);
+    if (sel) {
+      const uint32_t pos = run + mbcnt64(m);
+      if (pos < (uint64_t)k) {
+        idx_out[pos] = (int32_t)idx;
+        val_out[pos] = vals_src[idx];
+        if (counter) counter[idx] += 1;
+        if (rewind) rewind[idx] = 0.0f;
+      }
+    }
+    run += (uint32_t)__popcll(m);
+  };
+  if (!dense) {
+    emit(sel0, idx0);
+    for (uint32_t j0 = 64; j0 < cnt; j0 += 64) {
       const uint32_t j = j0 + lane;
       bool sel = false;
       uint32_t idx = 0;
@@ -581,17 +690,7 @@ __global__ void __launch_bounds__(256, 8) sampled_compact_kernel(
         idx = cidx[seg * CAP + j];
         sel = key > T || (key == T && idx <= icut);
       }
-      const uint64_t m = __ballot(sel);
-      if (sel) {
-        const uint32_t pos = run + mbcnt64(m);
-        if (pos < (uint64_t)k) {
-          idx_out[pos] = (int32_t)idx;
-          val_out[pos] = vals_src[idx];
-          if (counter) counter[idx] += 1;
-          if (rewind) rewind[idx] = 0.0f;
-        }
-      }
-      run += (uint32_t)__popcll(m);
+      emit(sel, idx);
     }
   } else {
     const int64_t beg = seg * R;
@@ -626,6 +725,7 @@ __global__ void __launch_bounds__(256, 8) sampled_compact_kernel(
       run += tot;
     }
   }
+  STAMP_T0(4);
 }
 
 template <bool VEC>
@@ -634,40 +734,39 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L) {
   TopkCtrl* ctrl = reinterpret_cast<TopkCtrl*>(a.ws + L.ctrl);
   uint32_t* chist = reinterpret_cast<uint32_t*>(a.ws + L.chist);
   uint32_t* ghist = reinterpret_cast<uint32_t*>(a.ws + L.f_ghist);
-  uint32_t* rows = reinterpret_cast<uint32_t*>(a.ws + L.f_rows);
   uint32_t* segcnt = reinterpret_cast<uint32_t*>(a.ws + L.f_segcnt);
-  uint32_t* segabove = reinterpret_cast<uint32_t*>(a.ws + L.f_segabove);
-  uint32_t* segoff = reinterpret_cast<uint32_t*>(a.ws + L.f_segoff);
+  uint32_t* blkabove = reinterpret_cast<uint32_t*>(a.ws + L.f_blkabove);
   uint32_t* cidx = reinterpret_cast<uint32_t*>(a.ws + L.f_cidx);
   uint32_t* ckey = reinterpret_cast<uint32_t*>(a.ws + L.f_ckey);
-  uint32_t* bcnt = reinterpret_cast<uint32_t*>(a.ws + L.f_bcnt);
-  uint32_t* bkey = reinterpret_cast<uint32_t*>(a.ws + L.f_bkey);
-  uint32_t* bidx = reinterpret_cast<uint32_t*>(a.ws + L.f_bidx);
+  uint32_t* blcnt = reinterpret_cast<uint32_t*>(a.ws + L.f_blcnt);
+  uint32_t* blkey = reinterpret_cast<uint32_t*>(a.ws + L.f_blkey);
+  uint32_t* blidx = reinterpret_cast<uint32_t*>(a.ws + L.f_blidx);
   const FastGeom& g = L.fg;
   const unsigned nb = (unsigned)g.B;
-  sampled_sample_kernel<<<SMP_BLOCKS, 256, 0, a.st>>>(s, a.n, ctrl, chist, ghist);
-  DPZ_LAUNCH_CHECK();
-  sampled_filter_kernel<VEC><<<nb, 256, 0, a.st>>>(s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist,
-                                                   rows, segcnt, cidx, ckey);
-  DPZ_LAUNCH_CHECK();
+  const unsigned nsel = (unsigned)((g.W + SEL_SEGS - 1) / SEL_SEGS);
+  const unsigned ncmp = (unsigned)((g.W + CMP_SEGS - 1) / CMP_SEGS);
+  DPZ_TIMED(DPZ_KT_TOPK_SAMPLE, a.st, sampled_sample_kernel<<<SMP_BLOCKS, 256, 0, a.st>>>(
+      s, a.n, ctrl, chist, ghist, blcnt));
+  DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC><<<nb, 256, 0, a.st>>>(
+      s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey));
   s.rekey = 1;
-  sampled_selectA_kernel<<<32, 256, 0, a.st>>>(rows, g.B, ghist);
-  DPZ_LAUNCH_CHECK();
-  sampled_selectB_kernel<VEC><<<nb, 256, 0, a.st>>>(s, a.n, a.k, g.W, g.R, g.CAP, ctrl, ghist,
-                                                    segcnt, cidx, ckey, segabove, bcnt, bkey, bidx);
-  DPZ_LAUNCH_CHECK();
-  sampled_selectC_kernel<<<1, 1024, 0, a.st>>>(a.k, g.W, g.R, ctrl, bcnt, bkey, bidx, segabove,
-                                               segoff);
-  DPZ_LAUNCH_CHECK();
+  DPZ_TIMED(DPZ_KT_TOPK_SELECT, a.st, sampled_select_kernel<VEC><<<nsel, 1024, 0, a.st>>>(
+      s, a.n, a.k, g.W, g.B, g.R, g.CAP, ctrl, ghist, segcnt, cidx, ckey, blkabove, blcnt, blkey,
+      blidx));
+  DPZ_TIMED(DPZ_KT_TOPK_RESOLVE, a.st, sampled_resolve_kernel<<<1, 1024, 0, a.st>>>(
+      a.k, g.B, ctrl, blcnt, blkey, blidx, blkabove));
   float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE) ? a.acc : nullptr;
-  sampled_compact_kernel<VEC><<<nb, 256, 0, a.st>>>(s, a.n, g.W, g.R, g.CAP, ctrl, chist, segcnt,
-                                                    segoff, cidx, ckey, a.vals_src,
-                                                    a.idx_out, a.val_out, a.counter, rewind, a.k);
-  DPZ_LAUNCH_CHECK();
+  DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC><<<ncmp, 1024, 0, a.st>>>(
+      s, a.n, a.k, g.W, g.B, g.R, g.CAP, ctrl, chist, blcnt, blkey, blidx, blkabove, segcnt, cidx,
+      ckey, a.vals_src, a.idx_out, a.val_out, a.counter, rewind));
   return DPZ_OK;
 }
 
 #ifdef DPZ_STAMPS
+extern "C" int dpz_debug_block_stamps(unsigned long long* host_out) {
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_bst), sizeof(g_bst));
+}
+
 extern "C" int dpz_debug_stamps(unsigned long long* host_out, int reset) {
   if (host_out) DPZ_HIP_TRY(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)));
   if (reset) {

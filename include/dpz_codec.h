@@ -6,7 +6,8 @@
  * stream).  Every entry point returns an int status: 0 = success, a hipError_t value for HIP
  * failures, or one of the DPZ_ERR_* codes below.  No entry point allocates device memory:
  * workspace is sized by the *_workspace_bytes() queries and passed in by the caller.
- * Entry points are reentrant; the library holds no mutable global state.
+ * Codec entry points are reentrant; the only mutable global state is the opt-in per-kernel
+ * timing facility (dpz_timing_*), a measurement aid.
  *
  * Each function names the reference (sacs-epfl/decentralizepy, src/decentralizepy/...) code it
  * replaces.  The reference itself has no native layer: these replace ATen-CPU / PyWavelets /
@@ -120,6 +121,23 @@ int dpz_scatter_fill(float* dst, int64_t n, const int32_t* idx, int64_t k, float
  * is fpzip (compression/EliasFpzipLossy.py:14-58), which is not byte-compatible.             */
 int dpz_pack_fp16(const float* in, int64_t n, uint16_t* out, dpz_stream_t stream);
 int dpz_unpack_fp16(const uint16_t* in, int64_t n, float* out, dpz_stream_t stream);
+
+/* ---- Per-kernel timing (measurement only; not thread-safe) -----------------------------------
+ * While enabled, every kernel launch records a HIP event pair on its own stream (launches into a
+ * capturing stream are skipped).  dpz_timing_read waits for the pending pairs and fills the summed
+ * milliseconds and launch counts per kernel id; it returns DPZ_KT_COUNT.                     */
+enum {
+  DPZ_KT_TOPK_SAMPLE = 0, DPZ_KT_TOPK_FILTER, DPZ_KT_TOPK_SELECT, DPZ_KT_TOPK_RESOLVE,
+  DPZ_KT_TOPK_COMPACT,
+  DPZ_KT_EXACT_HIST, DPZ_KT_EXACT_RESOLVE, DPZ_KT_EXACT_COUNT, DPZ_KT_EXACT_SCAN,
+  DPZ_KT_EXACT_WRITE, DPZ_KT_ACCUMULATE,
+  DPZ_KT_FOLD_OFFSETS, DPZ_KT_FOLD, DPZ_KT_DWT, DPZ_KT_IDWT, DPZ_KT_ELIAS_COUNT,
+  DPZ_KT_ELIAS_SCAN, DPZ_KT_ELIAS_PACK, DPZ_KT_ELIAS_SPEC, DPZ_KT_ELIAS_RESOLVE,
+  DPZ_KT_ELIAS_WRITE, DPZ_KT_FP16, DPZ_KT_SCATTER, DPZ_KT_COUNT
+};
+int dpz_timing_enable(int on);  /* also clears the accumulators */
+int dpz_timing_read(double* ms_sum, int64_t* count, int max_ids);
+const char* dpz_kernel_name(int id);
 
 /* ---- Elias-gamma index coding (byte-identical to the reference wire format) ------------------
  * Replaces compression/Elias.py:20-52 (Elias.compress) and :54-97 (Elias.decompress).

@@ -296,3 +296,27 @@ def test_fp16_pack_roundtrip(dev):
         assert torch.equal(h.cpu().view(torch.int16), ref.view(torch.int16))
         back = codec.unpack_fp16(h).cpu()
         assert torch.equal(back, ref.float())
+
+
+def test_topk_workspace_reuse_across_calls_and_misses(dev):
+    """The sampled path's self-cleaning workspace (sample histogram, boundary sub-list counters)
+    must be clean after normal calls and after a miss that fell back to the exact path."""
+    codec = _codec()
+    ws = codec.Workspace(dev)
+    n = 1 << 20
+    k = round(0.01 * n)
+    for seed in (21, 22):
+        x, x0 = _inputs(n, seed=seed)
+        tx, tx0 = torch.from_numpy(x).to(dev), torch.from_numpy(x0).to(dev)
+        for _ in range(2):
+            idx, val = codec.topk_encode(tx, k, x0=tx0, workspace=ws)
+            oi, ov = otopk.encode(x, x0, None, 0, k)
+            np.testing.assert_array_equal(idx.cpu().numpy(), oi)
+        # quantised input: thousands of equal keys in the threshold bin overflow the boundary
+        # sub-lists -> miss -> exact fallback; the next call must start clean
+        xq = (np.round(x * 8) / 8).astype(np.float32)
+        tq = torch.from_numpy(xq).to(dev)
+        idx, val = codec.topk_encode(tq, k, x0=tx0, workspace=ws)
+        oi, ov = otopk.encode(xq, x0, None, 0, k)
+        np.testing.assert_array_equal(idx.cpu().numpy(), oi)
+        np.testing.assert_array_equal(_bits(val.cpu().numpy()), _bits(ov))

@@ -14,9 +14,8 @@ import torch  # noqa: E402
 from decentralizepy_amd import _lib, codec  # noqa: E402
 
 NAMES = {0: "sample first-in", 1: "sample last-out", 2: "filter first-in", 3: "filter last-out",
-         4: "selA first-in", 5: "selA last-out", 6: "selB first-in", 7: "selB last-out",
-         8: "selC start", 9: "selC loads done", 10: "selC gathered", 11: "selC radix done",
-         12: "selC end", 13: "compact first-in"}
+         6: "select first-in", 7: "select last-out", 13: "compact first-in"}
+PHASES = ["entry", "loads", "offset", "counted", "end"]
 
 
 def main():
@@ -42,6 +41,32 @@ def main():
         t0 = arr[0]
         line = "  ".join(f"{NAMES[i]}={(arr[i] - t0) / 100:.1f}" for i in sorted(NAMES) if 0 < arr[i] < 2**63)
         print(f"iter {it}: (us from sample start) {line}")
+        if it == 5:
+            import numpy as np
+            L.dpz_debug_block_stamps.argtypes = [ctypes.c_void_p]
+            bs = (ctypes.c_ulonglong * (16 * 4096))()
+            L.dpz_debug_block_stamps(ctypes.addressof(bs))
+            ball = np.frombuffer(bs, dtype=np.uint64).reshape(16, 4096).astype(np.int64)
+            sel = ball[8:12]
+            ns = int((sel[0] > 0).sum())
+            rs = ball[12:15, 0]
+            print(f"resolve: start->gathered {(rs[1]-rs[0])/100:.2f} us, ->T {(rs[2]-rs[1])/100:.2f}, ->end {(rs[2]-rs[0])/100:.2f}")
+            sel = sel[:, :ns]
+            print(f"select blocks: {ns}")
+            sp = ["entry", "b*", "appended", "arrived"]
+            for p in range(1, 4):
+                d = (sel[p] - sel[p - 1]) / 100
+                print(f"  {sp[p - 1]:>8} -> {sp[p]:<8} {d.mean():7.2f} {d.max():7.2f}")
+            b = ball[:8]
+            nblk = int((b[0] > 0).sum())
+            b = b[:, :nblk]
+            ok = b[4] > 0
+            print(f"compact blocks: {nblk}; per-block phase latency (us, mean/max over blocks):")
+            for p in range(1, 5):
+                d = (b[p] - b[p - 1])[ok] / 100
+                print(f"  {PHASES[p - 1]:>8} -> {PHASES[p]:<8} {d.mean():7.2f} {d.max():7.2f}")
+            e = (b[0][ok] - b[0][ok].min()) / 100
+            print(f"  block entry spread: {e.max():.2f} us; block start->end mean {((b[4]-b[0])[ok]/100).mean():.2f}")
 
 
 if __name__ == "__main__":
