@@ -38,6 +38,11 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 64 MiB secondary line")
+    p.add_argument("--workload", choices=["c2", "c4"], default="c2",
+                   help="c2: one node's 11M tensor per GPU (default); c4: the 96-node gossip "
+                        "round of eval/96_regular.edges sharded over the GPUs")
+    p.add_argument("--rotate", type=int, default=None,
+                   help="independent node states cycled per step (default: enough for > 2x L3)")
     p.add_argument("--no-graph", action="store_true",
                    help="launch kernels eagerly instead of replaying a captured hipGraph")
     return p.parse_args()
@@ -56,53 +61,82 @@ def timed_loop(fn, reps, stream):
     return ev0.elapsed_time(ev1) / reps * 1e-3  # seconds
 
 
-def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True):
+L3_BYTES = 256 * 2 ** 20  # MI355X Infinity Cache (MI355X_MICROARCH.md § Infinity Cache)
+
+
+def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True, rotate=None):
+    """Time `steps` encode+decode steps.  Consecutive steps rotate over R independent node states
+    (x, x0, counter, payload, output) so the timed working set is > 2x the 256 MiB Infinity
+    Cache: every step streams its inputs from HBM, as a real round does after training."""
     from decentralizepy_amd import codec
     k = round(alpha * n)
+    per_set = 4 * n * 4 + 8 * k          # x, x0, counter, out + payload
+    R = rotate or max(1, math.ceil(2 * L3_BYTES / per_set) + 1)
     g = torch.Generator(device=dev).manual_seed(seed)
-    x = torch.randn(n, device=dev, generator=g)
-    x0 = x - 0.01 * torch.randn(n, device=dev, generator=g)
-    counter = torch.zeros(n, dtype=torch.int32, device=dev)
+    sets = []
+    for _ in range(R):
+        x = torch.randn(n, device=dev, generator=g)
+        x0 = x - 0.01 * torch.randn(n, device=dev, generator=g)
+        sets.append(dict(x=x, x0=x0, counter=torch.zeros(n, dtype=torch.int32, device=dev),
+                         idx=torch.empty(k, dtype=torch.int32, device=dev),
+                         val=torch.empty(k, dtype=torch.float32, device=dev),
+                         out=torch.empty(n, dtype=torch.float32, device=dev)))
     ws = codec.Workspace(dev)
-    idx = torch.empty(k, dtype=torch.int32, device=dev)
-    val = torch.empty(k, dtype=torch.float32, device=dev)
-    out = torch.empty(n, dtype=torch.float32, device=dev)
 
-    def encode():
-        codec.topk_encode(x, k, x0=x0, counter=counter, idx_out=idx, val_out=val, workspace=ws,
-                          asynchronous=True)
+    def encode(d):
+        codec.topk_encode(d["x"], k, x0=d["x0"], counter=d["counter"], idx_out=d["idx"],
+                          val_out=d["val"], workspace=ws, asynchronous=True)
 
-    def decode():
-        codec.replace(x0, idx, val, out=out, workspace=ws)
+    def decode(d):
+        codec.replace(d["x0"], d["idx"], d["val"], out=d["out"], workspace=ws)
 
-    def step():
-        encode()
-        decode()
+    def step(i):
+        d = sets[i % R]
+        encode(d)
+        decode(d)
 
-    for _ in range(warmup):
-        step()
-    fell_back = codec.topk_complete(x, k, idx, val, ws, x0=x0, counter=counter)
+    for i in range(max(warmup, R)):
+        step(i)
+    fell_back = False
+    for d in sets:  # completes the last async encode of every state (exact re-run on a miss)
+        fell_back |= codec.topk_complete(d["x"], k, d["idx"], d["val"], ws, x0=d["x0"],
+                                         counter=d["counter"])
     torch.cuda.synchronize()
-    run = step
-    if use_graph:
-        # one step = 7 dependent kernels; capture them once and replay (hipGraph), so the timed
-        # loop is not bound by per-kernel host launch cost.  Every kernel still runs every step.
+
+    def make_graph(m):
+        # m consecutive steps (7 dependent kernels each) captured once and replayed (hipGraph),
+        # so the timed loop is not bound by per-kernel host launch cost; every kernel still runs
+        # every step
         graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for i in range(m):
+                step(i)
+        return graph
+
+    if use_graph:
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
-            step()
+            step(0)
         torch.cuda.current_stream(dev).wait_stream(side)
-        with torch.cuda.graph(graph):
-            step()
+        full = make_graph(R)
+        tail = make_graph(steps % R) if steps % R else None
         torch.cuda.synchronize()
-        run = graph.replay
+
+        def run_all():
+            for _ in range(steps // R):
+                full.replay()
+            if tail is not None:
+                tail.replay()
+    else:
+        def run_all():
+            for i in range(steps):
+                step(i)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        run()
+    run_all()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -115,24 +149,65 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True):
     s_step = t / steps
     # per-stage device time with events on the launch stream
     stream = torch.cuda.current_stream(dev)
-    reps = max(20, steps // 2)
-    t_enc = timed_loop(encode, reps, stream)
-    t_dec = timed_loop(decode, reps, stream)
+    reps = max(2 * R, steps // 2)
+    cnt = iter(range(10 ** 9))
+    t_enc = timed_loop(lambda: encode(sets[next(cnt) % R]), reps, stream)
+    cnt = iter(range(10 ** 9))
+    t_dec = timed_loop(lambda: decode(sets[next(cnt) % R]), reps, stream)
     # per-kernel device time: the library brackets every launch with a HIP event pair on the
     # stream it launches on.  A GPU-side spin first lets the host queue all `reps` steps, so the
     # kernels then run back-to-back as in the graph replay (no host-launch gaps inside a pair).
     with codec.KernelTimer() as kt:
         torch.cuda._sleep(int(200e6))  # ~0.1 s of GPU cycles while the steps are enqueued
-        for _ in range(reps):
-            step()
+        for i in range(reps):
+            step(i)
         torch.cuda.synchronize()
-    kernels = {name: {"avg_us": ms / cnt * 1e3, "launches_per_step": cnt / reps}
-               for name, (ms, cnt) in kt.result.items()}
+    kernels = {name: {"avg_us": ms / c * 1e3, "launches_per_step": c / reps}
+               for name, (ms, c) in kt.result.items()}
     b_enc = 8 * n + 8 * k + 8 * k      # read x, x0; write idx, val; counter[idx] += 1 (r+w)
     b_dec = 8 * n + 8 * k              # read local, payload; write out
     return dict(n=n, k=k, s_step=s_step, fell_back=fell_back, t_enc=t_enc, t_dec=t_dec,
-                b_enc=b_enc, b_dec=b_dec, kernels=kernels,
+                b_enc=b_enc, b_dec=b_dec, kernels=kernels, rotate=R,
                 value=world * 4 * n / s_step / 2 ** 30)
+
+
+def gossip_case(n, alpha, dev, rank, world, dist, rounds, warmup):
+    """C4: one synchronous gossip round of the 96-node regular topology (reference
+    eval/96_regular.edges, copied as data under tests/golden/), nodes sharded over the ranks,
+    payloads exchanged by one RCCL all-gather (decentralizepy_amd/gossip.py).  A "training"
+    perturbation between rounds is excluded from the timed region."""
+    from decentralizepy_amd.gossip import GossipRound, read_edges, shard
+    adj = read_edges(os.path.join(ROOT, "tests", "golden", "96_regular.edges"))
+    lo, hi, _ = shard(len(adj), world, rank)
+    g = torch.Generator(device=dev).manual_seed(77 + rank)
+    x = torch.randn(hi - lo, n, device=dev, generator=g)
+    eng = GossipRound(adj, x, alpha, rank=rank, world=world, device=dev)
+    del x
+    noise = 0.01 * torch.randn(hi - lo, n, device=dev, generator=g)
+    total = 0.0
+    for r in range(warmup + rounds):
+        eng.x += noise
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        eng.step()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if dist is not None:
+            tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        if r >= warmup:
+            total += dt
+    s_round = total / rounds
+    k = eng.k
+    nsum = sum(len(a) for a in adj)
+    return dict(n=n, k=k, s_step=s_round, nodes=len(adj), edges=nsum // 2,
+                value=len(adj) * 4 * n / s_round / 2 ** 30,
+                alg_bytes=len(adj) * (8 * n + 16 * k) + len(adj) * 8 * n + nsum * 8 * k)
 
 
 def kernel_alg_bytes(name, n, k):
@@ -198,8 +273,32 @@ def main():
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 
+    if args.workload == "c4":
+        rounds = max(3, min(args.steps, 20))
+        r = gossip_case(args.n, args.alpha, dev, rank, world, dist, rounds, max(1, min(args.warmup, 3)))
+        if rank == 0:
+            print(json.dumps({
+                "metric": "GiB/s fp32 params encoded+decoded (device-resident), 1% top-k",
+                "value": round(r["value"], 3), "unit": "GiB/s", "n_gpus": world,
+                "steps": rounds, "warmup": max(1, min(args.warmup, 3)),
+                "ms_per_step": round(r["s_step"] * 1e3, 4), "higher_is_better": True,
+                "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+                "data": "synthetic (x ~ N(0,1), +0.01*N(0,1) per round), device-generated",
+                "config": {"workload": "C4: one gossip round of eval/96_regular.edges (96 nodes, "
+                                       "190 edges), every node top-k encodes and MH-folds its "
+                                       "neighbours' payloads",
+                           "n": r["n"], "k": r["k"], "alpha": args.alpha,
+                           "parallelism": f"{r['nodes']} nodes sharded over {world} GPU(s), one "
+                                          "RCCL all-gather of the payloads per round"},
+                "round_alg_bytes": r["alg_bytes"],
+                "round_frac_of_hbm_peak": round(r["alg_bytes"] / r["s_step"] / 1e9 / HBM_PEAK_GBS / world, 4),
+            }), flush=True)
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     r = gpu_case(args.n, args.alpha, dev, 1234 + rank, args.steps, args.warmup, world, dist,
-                 use_graph=not args.no_graph)
+                 use_graph=not args.no_graph, rotate=args.rotate)
     extra = None
     if not args.no_extra and world == 1:
         e = gpu_case(16_777_216, 0.01, dev, 99, max(20, args.steps // 2), args.warmup, 1, None,
@@ -255,6 +354,7 @@ def main():
                 "n": r["n"], "k": r["k"], "alpha": args.alpha,
                 "parallelism": f"{world} independent per-node codecs (one per GPU), no collective",
                 "launch": "eager" if args.no_graph else "hipGraph replay of the whole step",
+                "rotated_states": r["rotate"],
             },
             "roofline": {
                 "bound": "hbm",

@@ -1,0 +1,127 @@
+"""CPU (gloo, world_size 2): the gossip-round engine's node sharding, payload all-gather and
+Metro-Hastings neighbourhoods, with the oracle standing in for the HIP codec (the device path is
+covered by tests/test_gpu_gossip.py).  Topologies are the reference's own data files
+(eval/96_regular.edges, tutorial/JWINS/regular_16.txt) copied under tests/golden/."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import fold as ofold
+from oracle import topk as otopk
+from tests import scenario
+
+EDGES96 = os.path.join(scenario.GOLDEN, "96_regular.edges")
+EDGES16 = os.path.join(scenario.GOLDEN, "regular_16.edges")
+
+
+def _oracle_encode(x, x0, k, counter, idx_out, val_out):
+    c = counter.numpy()
+    idx, val = otopk.encode(x.numpy(), x0.numpy(), None, otopk.ACC_NONE, k, counter=c)
+    idx_out.copy_(torch.from_numpy(idx))
+    val_out.copy_(torch.from_numpy(val))
+
+
+def _oracle_fold(local, payloads, weights, w_self, out):
+    pays = [(i.numpy(), v.numpy()) for i, v in payloads]
+    out.copy_(torch.from_numpy(ofold.fold(local.numpy(), pays, weights, w_self)))
+
+
+def _models(n_nodes, n, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n_nodes, n, generator=g)
+
+
+def _train(eng, r):
+    g = torch.Generator().manual_seed(100 + r)
+    noise = 0.01 * torch.randn(eng.n_nodes, eng.N, generator=g)
+    eng.x += noise[eng.lo:eng.hi]
+
+
+def _direct_round(adj, x, x0, k):
+    """The reference semantics written out node by node (no sharding, no all-gather)."""
+    from decentralizepy_amd.gossip import mh_weights
+    pays = [otopk.encode(x[i], x0[i], None, otopk.ACC_NONE, k) for i in range(len(adj))]
+    out = np.empty_like(x)
+    for i in range(len(adj)):
+        nbrs, w, w_self = mh_weights(adj, i)
+        out[i] = ofold.fold(x[i], [pays[j] for j in nbrs], w, w_self)
+    return out
+
+
+def test_read_edges_and_weights():
+    from decentralizepy_amd.gossip import mh_weights, read_edges, shard
+    adj = read_edges(EDGES96)
+    assert len(adj) == 96
+    assert sum(len(a) for a in adj) == 380          # sum of degrees
+    assert {len(a) for a in adj} <= {3, 4}
+    nbrs, w, w_self = mh_weights(adj, 0)
+    assert nbrs == sorted(adj[0]) and abs(sum(w) + w_self - 1) < 1e-12
+    adj16 = read_edges(EDGES16)
+    assert len(adj16) == 16 and {len(a) for a in adj16} == {3}
+    lo, hi, per = shard(96, 8, 7)
+    assert (lo, hi, per) == (84, 96, 12)
+    assert shard(10, 4, 3) == (9, 10, 3)
+
+
+def test_single_rank_round_matches_direct_simulation():
+    from decentralizepy_amd.gossip import GossipRound, read_edges
+    adj = read_edges(EDGES16)
+    n = 2000
+    x = _models(16, n)
+    eng = GossipRound(adj, x, 0.05, encode=_oracle_encode, fold=_oracle_fold)
+    ref_x, ref_x0 = x.numpy().copy(), x.numpy().copy()
+    for r in range(2):
+        _train(eng, r)
+        g = torch.Generator().manual_seed(100 + r)
+        ref_x = ref_x + (0.01 * torch.randn(16, n, generator=g)).numpy()
+        eng.step()
+        ref_x = _direct_round(adj, ref_x, ref_x0, eng.k)
+        ref_x0 = ref_x.copy()
+        np.testing.assert_array_equal(eng.x.numpy().view(np.uint32), ref_x.view(np.uint32))
+
+
+def _worker(rank, world, port, n, path, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from decentralizepy_amd.gossip import GossipRound, read_edges, shard
+        adj = read_edges(path)
+        x = _models(len(adj), n)
+        lo, hi, _ = shard(len(adj), world, rank)
+        eng = GossipRound(adj, x[lo:hi], 0.05, rank=rank, world=world, encode=_oracle_encode,
+                          fold=_oracle_fold)
+        for r in range(2):
+            _train(eng, r)
+            eng.step()
+        q.put((rank, lo, eng.x.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("path,n", [(EDGES16, 1500), (EDGES96, 600)])
+def test_two_rank_round_equals_single_rank(path, n):
+    from decentralizepy_amd.gossip import GossipRound, read_edges
+    adj = read_edges(path)
+    x = _models(len(adj), n)
+    single = GossipRound(adj, x, 0.05, encode=_oracle_encode, fold=_oracle_fold)
+    for r in range(2):
+        _train(single, r)
+        single.step()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, path, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, lo, xs in got:
+        np.testing.assert_array_equal(xs.view(np.uint32),
+                                      single.x.numpy()[lo:lo + xs.shape[0]].view(np.uint32))
