@@ -94,8 +94,14 @@ constexpr int CB_SHIFT = 20;       // coarse bins: key >> 20 (2048 bins, 8 per o
 constexpr int CB = 2048;
 constexpr int HB = 256;            // fine window bins (+1 "above window" bin)
 constexpr int HBR = HB + 1;
-constexpr int W_MAX = 8192;        // wave segments (one wave streams one contiguous segment)
-constexpr int W_MIN_RANGE = 1024;
+#ifndef DPZ_WMAX
+#define DPZ_WMAX 8192
+#endif
+#ifndef DPZ_WMIN_RANGE
+#define DPZ_WMIN_RANGE 1024
+#endif
+constexpr int W_MAX = DPZ_WMAX;    // wave segments (one wave streams one contiguous segment)
+constexpr int W_MIN_RANGE = DPZ_WMIN_RANGE;
 constexpr int GH_COPIES = 16;      // window histogram copies (filter block b adds into copy b % 16)
 constexpr int GH_STRIDE = 272;     // >= HBR, 16-aligned
 constexpr int SEL_SEGS = 32;       // wave segments per select block (16 waves x 2)

@@ -191,11 +191,15 @@ __global__ void __launch_bounds__(256, 8) sampled_filter_kernel(
       cnt[q] = i0 < end ? load_keys4<VEC>(s, i0, end, store_acc, key[q]) : 0;
     }
   } else {
+#ifdef DPZ_ABLATE_WINDOW  // timing only: a fixed window instead of the sample histogram's
+    if (lane == 0) { win[0] = 0x3CBF0000u; win[1] = 0x3CD00000u; win[2] = 13; }
+#else
     uint4 cv[8];
     const uint4* c4 = reinterpret_cast<const uint4*>(chist) + (504 - 8 * lane);
 #pragma unroll
     for (int q = 0; q < 8; ++q) cv[q] = c4[q];
     wave_window(cv, n, k, win);
+#endif
   }
   __syncthreads();
   if (wid == 0) {
@@ -229,12 +233,18 @@ __global__ void __launch_bounds__(256, 8) sampled_filter_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         f[e] = e < cnt[q] && key[q][e] >= lo;
+#ifndef DPZ_ABLATE_HIST
         if (f[e]) atomicAdd(&h[fine_bin(key[q][e], lo, hi, shift)], 1u);
+#endif
         const uint64_t m = __ballot(f[e]);
         pre += mbcnt64(m);
         tot += (uint32_t)__popcll(m);
       }
+#ifdef DPZ_ABLATE_APPEND
+      if (false) {
+#else
       if (tot) {
+#endif
         if (!dense && run + tot <= (uint32_t)CAP) {
           const uint32_t i0 = (uint32_t)(base + q * 256 + lane * 4);
           if (L.staged + tot > STAGE) L.flush(lane);
@@ -306,7 +316,7 @@ __global__ void __launch_bounds__(1024) sampled_resolve_kernel(
     const uint32_t* __restrict__ blkey, const uint32_t* __restrict__ blidx,
     const uint32_t* __restrict__ blkabove) {
   constexpr int PER = BCAP / 1024;
-  constexpr int BPT = B_MAX / 1024;
+  constexpr int BPT = (B_MAX + 1023) / 1024;
   __shared__ uint32_t hist[256];
   __shared__ uint32_t subbase[NSUB + 1];
   __shared__ uint32_t wsum[16];
@@ -571,7 +581,7 @@ __global__ void __launch_bounds__(1024) sampled_compact_kernel(
     const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ cidx,
     const uint32_t* __restrict__ ckey, const float* vals_src, int32_t* idx_out, float* val_out,
     int32_t* counter, float* rewind) {
-  constexpr int BPT = B_MAX / 1024;
+  constexpr int BPT = (B_MAX + 1023) / 1024;
   __shared__ uint32_t subbase[NSUB + 1];
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t wcnt[16];

@@ -1,0 +1,52 @@
+"""Per-launch HBM traffic of the codec kernels from rocprofv3 FETCH_SIZE / WRITE_SIZE passes.
+
+FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide
+coalesced reads (MI355X_MICROARCH.md § HBM), so traffic = 2 * FETCH_SIZE + WRITE_SIZE.
+Usage: pmc2json.py fetch.csv write.csv out.json
+"""
+import collections
+import csv
+import json
+import sys
+
+NAMES = {"sampled_sample_kernel": "topk_sample", "sampled_filter_kernel": "topk_filter",
+         "sampled_select_kernel": "topk_select", "sampled_resolve_kernel": "topk_resolve",
+         "sampled_compact_kernel": "topk_compact", "fold_offsets_kernel": "fold_offsets",
+         "fold_kernel": "fold"}
+
+
+def short(name):
+    base = name.split("(")[0].replace("void ", "").split("::")[-1].split("<")[0]
+    return NAMES.get(base)
+
+
+def load(path, counter):
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        k = short(r["Kernel_Name"])
+        if k:
+            acc[k].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main(fetch, write, out):
+    f, w = load(fetch, "FETCH_SIZE"), load(write, "WRITE_SIZE")
+    kernels = {}
+    for k in sorted(set(f) | set(w)):
+        fk, wk = f.get(k, 0.0), w.get(k, 0.0)
+        kernels[k] = {"FETCH_SIZE_KiB": round(fk, 2), "WRITE_SIZE_KiB": round(wk, 2),
+                      "hbm_bytes_per_launch": int(round((2 * fk + wk) * 1024))}
+    doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
+                     "`python3 bench.py --steps 100 --warmup 10 --no-cpu --no-extra`; "
+                     "traffic = 2*FETCH_SIZE (gfx950 half-count correction) + WRITE_SIZE",
+           "kernels": kernels}
+    with open(out, "w") as fh:
+        json.dump(doc, fh, indent=1)
+    for k, v in kernels.items():
+        print(f"{k:14s} {v['hbm_bytes_per_launch'] / 1e6:9.2f} MB/launch")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
