@@ -172,6 +172,54 @@ __global__ void __launch_bounds__(FOLD_THREADS) fold_kernel(FoldArgs a) {
 
 static inline int64_t fold_ntiles(int64_t n) { return (n + FOLD_TILE - 1) / FOLD_TILE; }
 
+// Replace-only decode of ONE sparse payload (reference PartialModel.py:257-303, T[idx] = params):
+// block j owns payload entries [64j, 64j + 64) and the element range from its first entry's
+// index to the next block's first entry's index (block 0 from 0, the last block to n) - a
+// contiguous partition of [0, n) known after one load, so no tile-offset pre-pass.  The block
+// copies its range local -> out (float4 body), then scatters its entries' values.
+constexpr int RP_E = 64;
+
+__global__ void __launch_bounds__(256) replace_kernel(const float* __restrict__ local,
+                                                      const int32_t* __restrict__ idx,
+                                                      const float* __restrict__ val, int64_t k,
+                                                      int64_t n, float* __restrict__ out) {
+  const int t = threadIdx.x;
+  const int64_t e0 = (int64_t)blockIdx.x * RP_E;
+  const int64_t e1 = (e0 + RP_E < k) ? e0 + RP_E : k;
+  const int64_t a = blockIdx.x == 0 ? 0 : (int64_t)idx[e0];
+  const int64_t b = e1 >= k ? n : (int64_t)idx[e1];
+  int64_t my_i = -1;
+  float my_v = 0.0f;
+  if (t < e1 - e0) {
+    my_i = idx[e0 + t];
+    my_v = val[e0 + t];
+  }
+  if (a < b) {
+    const int64_t a4 = (a + 3) & ~int64_t(3);
+    const int64_t b4 = b & ~int64_t(3);
+    if (a4 < b4) {
+      if (t < a4 - a) out[a + t] = local[a + t];
+      if (t < b - b4) out[b4 + t] = local[b4 + t];
+      const float4* __restrict__ l4 = reinterpret_cast<const float4*>(local);
+      float4* __restrict__ o4 = reinterpret_cast<float4*>(out);
+      const int64_t q0 = a4 >> 2, q1 = b4 >> 2;
+      int64_t q = q0 + t;
+      for (; q + 3 * 256 < q1; q += 4 * 256) {
+        const float4 v0 = l4[q], v1 = l4[q + 256], v2 = l4[q + 512], v3 = l4[q + 768];
+        o4[q] = v0;
+        o4[q + 256] = v1;
+        o4[q + 512] = v2;
+        o4[q + 768] = v3;
+      }
+      for (; q < q1; q += 256) o4[q] = l4[q];
+    } else {
+      for (int64_t i = a + t; i < b; i += 256) out[i] = local[i];
+    }
+  }
+  __syncthreads();  // the range copy is in place before this block's entries overwrite it
+  if (my_i >= 0 && my_i < n) out[my_i] = my_v;
+}
+
 }  // namespace dpz
 
 using namespace dpz;
@@ -215,6 +263,12 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
     DPZ_HIP_TRY(hipMemsetAsync(out, 0, n * sizeof(float), st));
     if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<true><<<grid, FOLD_THREADS, 0, st>>>(fa));
     else DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<false><<<grid, FOLD_THREADS, 0, st>>>(fa));
+    return DPZ_OK;
+  }
+  // one sparse payload, replace only: single-kernel range-partitioned copy + scatter
+  if (replace_only && !is_dense(0) && k[0] > 0 && vec) {
+    const unsigned nblk = (unsigned)((k[0] + RP_E - 1) / RP_E);
+    DPZ_TIMED(DPZ_KT_FOLD, st, replace_kernel<<<nblk, 256, 0, st>>>(local, idx[0], vals[0], k[0], n, out));
     return DPZ_OK;
   }
   for (int base = 0; base < n_payloads; base += FOLD_MAXP) {
