@@ -100,13 +100,16 @@ constexpr int HBR = HB + 1;
 #ifndef DPZ_WMIN_RANGE
 #define DPZ_WMIN_RANGE 1024
 #endif
+#ifndef DPZ_FG
+#define DPZ_FG 4
+#endif
 constexpr int W_MAX = DPZ_WMAX;    // wave segments (one wave streams one contiguous segment)
+constexpr int FG = DPZ_FG;         // float4 groups of 256 elements a filter wave loads at once
 constexpr int W_MIN_RANGE = DPZ_WMIN_RANGE;
 constexpr int GH_COPIES = 16;      // window histogram copies (filter block b adds into copy b % 16)
 constexpr int GH_STRIDE = 272;     // >= HBR, 16-aligned
 constexpr int SEL_SEGS = 32;       // wave segments per select block (16 waves x 2)
 constexpr int SEL_LCAP = 1024;     // boundary entries one select block stages in LDS
-constexpr int CMP_SEGS = 16;       // wave segments per compact block (16 waves x 1)
 constexpr int NSUB = 16;           // boundary sub-lists (one atomic per select block each)
 constexpr int SUBCAP = 256;        // entries per sub-list (more -> miss -> exact fallback)
 constexpr int BCAP = NSUB * SUBCAP;  // boundary entries compact can hold (more -> miss)
@@ -141,7 +144,7 @@ static inline size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
 
 struct WsLayout {
   size_t ctrl, chist, ex_hist, ex_gt, ex_eq, ex_off, ex_eqb;
-  size_t f_ghist, f_segcnt, f_blkabove, f_cidx, f_ckey, f_blcnt, f_blkey, f_blidx;
+  size_t f_ghist, f_segcnt, f_blkabove, f_blkoff, f_cidx, f_ckey, f_blcnt, f_blkey, f_blidx;
   size_t total;
   int64_t ex_nblk;
   FastGeom fg;
@@ -164,6 +167,7 @@ static inline WsLayout ws_layout(int64_t n) {
   L.f_blcnt = o; o += align256(NSUB * 4);
   L.f_segcnt = o; o += align256(L.fg.W * 4);
   L.f_blkabove = o; o += align256(L.fg.B * 4);
+  L.f_blkoff = o; o += align256(L.fg.B * 4);
   L.f_cidx = o; o += align256((size_t)L.fg.W * L.fg.CAP * 4);
   L.f_ckey = o; o += align256((size_t)L.fg.W * L.fg.CAP * 4);
   L.f_blkey = o; o += align256((size_t)BCAP * 4);

@@ -15,10 +15,10 @@
 //             (block % 16) with one atomic (a contended device-scope atomic costs ~20 ns per
 //             arrival on MI355X, so no single global counter anywhere)
 //   resolve : 1 block: radix select over the ~k/256 boundary entries -> exact threshold T and
-//             tie cut (lowest index); checks above + selected == k
-//   compact : 16 segments per block: output offset from the above counts of the filter blocks
-//             before it + the selected boundary entries below it, then each wave writes its
-//             selected (idx, vals_src[idx]) in index order (+ counter / rewind)
+//             tie cut (lowest index); every filter block's output offset (scan of above +
+//             selected boundary counts over <= 2048 blocks); checks the total == k
+//   compact : per filter block: each wave counts, takes its offset inside the block's range and
+//             writes its selected (idx, vals_src[idx]) in index order (+ counter / rewind)
 // A miss (window does not bracket the k-th key / boundary overflow) sets ctrl->status and compact
 // writes nothing; the host then runs the exact path.  A segment whose candidates overflow its
 // list is DENSE and re-reads its input range in select / compact (still exact).
@@ -35,8 +35,12 @@ __device__ unsigned long long g_stamps[64];
 // per-block phase stamps of one kernel (plain stores, no contention): g_bst[phase][block]
 __device__ unsigned long long g_bst[16][4096];
 #define STAMP_T0(i) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_bst[i][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// per-wave phase stamps of the filter: g_fst[phase][wave segment]
+__device__ unsigned long long g_fst[6][8192];
+#define STAMP_W(i) do { const int64_t _sg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); if ((threadIdx.x & 63) == 0 && _sg < 8192) g_fst[i][_sg] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define STAMP_T0(i) do {} while (0)
+#define STAMP_W(i) do {} while (0)
 #define STAMP_MIN(i) do {} while (0)
 #define STAMP_MAX(i) do {} while (0)
 #define STAMP_ONE(i) do {} while (0)
@@ -166,27 +170,27 @@ struct WaveList {
 
 // B blocks x 256 threads; wave w of block b owns wave segment seg = 4b + w = [seg*R, +R) of [0, n).
 template <bool VEC>
-__global__ void __launch_bounds__(256, 8) sampled_filter_kernel(
+__global__ void __launch_bounds__(256, FG <= 4 ? 8 : (FG <= 6 ? 7 : 6)) sampled_filter_kernel(
     KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl,
     const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt, uint32_t* cidx,
     uint32_t* ckey) {
   __shared__ uint32_t h[HBR];
   __shared__ uint32_t win[4];
   __shared__ uint32_t st_idx[4][STAGE], st_key[4][STAGE];
-  STAMP_MIN(2);
+  STAMP_W(0);
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int b = threadIdx.x; b < HBR; b += 256) h[b] = 0;
   const int64_t seg = (int64_t)blockIdx.x * 4 + wid;
   const int64_t beg = seg * R;
   const int64_t end = (beg + R < n) ? beg + R : n;
   const bool store_acc = (s.mode == DPZ_ACC_ACCUMULATE) && !s.rekey;
-  uint32_t key[4][4];
-  int cnt[4];
+  uint32_t key[FG][4];
+  int cnt[FG];
   // waves 1-3 start streaming at once; wave 0 first turns the coarse sample histogram into the
   // key window (its 32 bin registers die before its own stream starts, after the barrier)
   if (wid != 0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < FG; ++q) {
       const int64_t i0 = beg + q * 256 + lane * 4;
       cnt[q] = i0 < end ? load_keys4<VEC>(s, i0, end, store_acc, key[q]) : 0;
     }
@@ -201,10 +205,12 @@ __global__ void __launch_bounds__(256, 8) sampled_filter_kernel(
     wave_window(cv, n, k, win);
 #endif
   }
+  STAMP_W(1);
   __syncthreads();
+  STAMP_W(2);
   if (wid == 0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < FG; ++q) {
       const int64_t i0 = beg + q * 256 + lane * 4;
       cnt[q] = i0 < end ? load_keys4<VEC>(s, i0, end, store_acc, key[q]) : 0;
     }
@@ -218,16 +224,16 @@ __global__ void __launch_bounds__(256, 8) sampled_filter_kernel(
   WaveList L{cidx + seg * CAP, ckey + seg * CAP, st_idx[wid], st_key[wid], 0u, 0u};
   uint32_t run = 0;
   bool dense = false;
-  for (int64_t base = beg; base < end; base += 1024) {
+  for (int64_t base = beg; base < end; base += FG * 256) {
     if (base != beg) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < FG; ++q) {
         const int64_t i0 = base + q * 256 + lane * 4;
         cnt[q] = i0 < end ? load_keys4<VEC>(s, i0, end, store_acc, key[q]) : 0;
       }
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < FG; ++q) {
       bool f[4];
       uint32_t pre = 0, tot = 0;
 #pragma unroll
@@ -270,7 +276,9 @@ __global__ void __launch_bounds__(256, 8) sampled_filter_kernel(
       }
     }
   }
+  STAMP_W(3);
   if (!dense) L.flush(lane);
+  STAMP_W(4);
   __syncthreads();
   // fold the block's window histogram into copy b % 16 (non-returning atomics; ~B/16 arrivals
   // per address instead of B)
@@ -280,7 +288,7 @@ __global__ void __launch_bounds__(256, 8) sampled_filter_kernel(
     if (v) atomicAdd(&gcopy[b], v);
   }
   if (lane == 0 && seg < W) segcnt[seg] = dense ? DENSE : run;
-  STAMP_MAX(3);
+  STAMP_W(5);
 }
 
 // Wave-level threshold bin from the global window histogram.  ghv = fine bins [252-4l, 255-4l].
@@ -312,25 +320,27 @@ __device__ __forceinline__ bool wave_bstar(uint4 ghv, uint32_t above, uint32_t k
 // inside bin b* (offsets below 2^shift, 8-bit digits), then the tie cut (the lowest indices among
 // keys == T), and check that above + selected == k.  Writes T, icut or a status for the host.
 __global__ void __launch_bounds__(1024) sampled_resolve_kernel(
-    int64_t k, int64_t B, TopkCtrl* ctrl, const uint32_t* __restrict__ blcnt,
+    int64_t k, int64_t B, int64_t R4, TopkCtrl* ctrl, const uint32_t* __restrict__ blcnt,
     const uint32_t* __restrict__ blkey, const uint32_t* __restrict__ blidx,
-    const uint32_t* __restrict__ blkabove) {
+    const uint32_t* __restrict__ blkabove, uint32_t* blkoff) {
   constexpr int PER = BCAP / 1024;
   constexpr int BPT = (B_MAX + 1023) / 1024;
   __shared__ uint32_t hist[256];
   __shared__ uint32_t subbase[NSUB + 1];
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t sh[4];
+  __shared__ uint32_t blksel[B_MAX];
   STAMP_T0(12);
   const int t = threadIdx.x;
   const uint32_t status = ctrl->status;
   const uint32_t need = ctrl->need, lo = ctrl->lo, shift = ctrl->shift, bstar = ctrl->bstar;
   const uint32_t sc = t < NSUB ? blcnt[t] : 0u;
-  uint32_t ba = 0;
+  uint32_t ba[BPT];
 #pragma unroll
   for (int q = 0; q < BPT; ++q) {
     const int64_t fb = (int64_t)t * BPT + q;
-    ba += fb < B ? blkabove[fb] : 0u;
+    ba[q] = fb < B ? blkabove[fb] : 0u;
+    if (fb < B_MAX) blksel[fb] = 0;
   }
   if (status) return;
   if (t < 64) {
@@ -426,19 +436,33 @@ __global__ void __launch_bounds__(1024) sampled_resolve_kernel(
     }
     icut = ipre;
   }
-  uint32_t nsel = 0;
+  // every filter block's output offset: above counts + selected boundary entries, scanned
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const uint32_t j = t + q * 1024;
-    nsel += (j < nb && (kk[q] > T || (kk[q] == T && ii[q] <= icut))) ? 1u : 0u;
+    if (j < nb && (kk[q] > T || (kk[q] == T && ii[q] <= icut)))
+      atomicAdd(&blksel[ii[q] / (uint32_t)R4], 1u);
   }
-  uint32_t tot_a, tot_s;
-  (void)block_excl_scan(ba, wsum, &tot_a);
-  (void)block_excl_scan(nsel, wsum, &tot_s);
+  __syncthreads();
+  uint32_t v[BPT], local = 0;
+#pragma unroll
+  for (int q = 0; q < BPT; ++q) {
+    const int64_t fb = (int64_t)t * BPT + q;
+    v[q] = fb < B ? ba[q] + blksel[fb] : 0u;
+    local += v[q];
+  }
+  uint32_t tot;
+  uint32_t ex = block_excl_scan(local, wsum, &tot);
+#pragma unroll
+  for (int q = 0; q < BPT; ++q) {
+    const int64_t fb = (int64_t)t * BPT + q;
+    if (fb < B) blkoff[fb] = ex;
+    ex += v[q];
+  }
   if (t == 0) {
     ctrl->T = T;
     ctrl->icut = icut;
-    if (tot_a + tot_s != (uint32_t)k) ctrl->status = 2;  // internal inconsistency
+    if (tot != (uint32_t)k) ctrl->status = 2;  // internal inconsistency: compact writes nothing
   }
 }
 
@@ -568,39 +592,23 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
   STAMP_T0(11);
 }
 
-// ceil(W/16) blocks x 1024 (16 waves x 1 wave segment).  Every block redundantly resolves the
-// exact threshold T and tie cut from the ~k/256 boundary entries (L2-resident), derives its output
-// offset from the per-filter-block above counts and the selected boundary entries below its
-// range, checks the total against k, then each wave writes its selected (idx, vals_src[idx]) in
-// index order with counter / rewind updates.  Block 0 re-zeroes the sample histogram.
+// One block of 256 threads per filter block (4 wave segments): output offset from resolve, then
+// per wave a count pass, in-block wave offsets, and the ordered write of the selected
+// (idx, vals_src[idx]) with counter / rewind updates.  Block 0 re-zeroes the sample histogram.
 template <bool VEC>
-__global__ void __launch_bounds__(1024) sampled_compact_kernel(
-    KeySrc s, int64_t n, int64_t k, int64_t W, int64_t B, int64_t R, int64_t CAP, TopkCtrl* ctrl,
-    uint32_t* chist, const uint32_t* __restrict__ blcnt, const uint32_t* __restrict__ blkey,
-    const uint32_t* __restrict__ blidx, const uint32_t* __restrict__ blkabove,
-    const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ cidx,
-    const uint32_t* __restrict__ ckey, const float* vals_src, int32_t* idx_out, float* val_out,
-    int32_t* counter, float* rewind) {
-  constexpr int BPT = (B_MAX + 1023) / 1024;
-  __shared__ uint32_t subbase[NSUB + 1];
-  __shared__ uint32_t wsum[16];
-  __shared__ uint32_t wcnt[16];
-  STAMP_MIN(13);
+__global__ void __launch_bounds__(256, 8) sampled_compact_kernel(
+    KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, const TopkCtrl* ctrl,
+    uint32_t* chist, const uint32_t* __restrict__ blkoff, const uint32_t* __restrict__ segcnt,
+    const uint32_t* __restrict__ cidx, const uint32_t* __restrict__ ckey, const float* vals_src,
+    int32_t* idx_out, float* val_out, int32_t* counter, float* rewind) {
+  __shared__ uint32_t wcnt[4];
   STAMP_T0(0);
   const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
-  const int64_t seg = (int64_t)blockIdx.x * CMP_SEGS + wid;
-  const int64_t fb0 = (int64_t)blockIdx.x * (CMP_SEGS / 4);  // first filter block of this block
-  // independent loads first
+  const int64_t seg = (int64_t)blockIdx.x * 4 + wid;
   const uint32_t status = ctrl->status;
   const uint32_t lo = ctrl->lo, T = ctrl->T, icut = ctrl->icut;
-  const uint32_t sc = t < NSUB ? blcnt[t] : 0u;
-  uint32_t ba[BPT];
-#pragma unroll
-  for (int q = 0; q < BPT; ++q) {
-    const int64_t fb = (int64_t)t * BPT + q;
-    ba[q] = fb < B ? blkabove[fb] : 0u;
-  }
   const uint32_t cnt = seg < W ? segcnt[seg] : 0u;
+  const uint32_t boff = blkoff[blockIdx.x];
   const bool dense = cnt == DENSE;
   uint32_t key0 = 0, idx0 = 0;
   if (seg < W && !dense && (uint32_t)lane < cnt) {
@@ -608,38 +616,10 @@ __global__ void __launch_bounds__(1024) sampled_compact_kernel(
     idx0 = cidx[seg * CAP + lane];
   }
   if (blockIdx.x == 0) {  // leave the sample histogram zeroed for the next call
-    for (int b = t; b < CB; b += 1024) chist[b] = 0;
+    for (int b = t; b < CB; b += 256) chist[b] = 0;
   }
   if (status) return;
-  if (t < 64) {
-    uint32_t tot;
-    const uint32_t ex = wave_excl_scan(sc, &tot);
-    if (t < NSUB) subbase[t] = ex;
-    if (t == 0) subbase[NSUB] = tot;
-  }
-  __syncthreads();
   STAMP_T0(1);
-  // output offset of this block: above counts of the filter blocks before it + the selected
-  // boundary entries below its first index
-  const uint32_t nb = subbase[NSUB];
-  const uint32_t start_idx = (uint32_t)(fb0 * 4 * R);
-  uint32_t before = 0;
-#pragma unroll
-  for (int q = 0; q < BPT; ++q) {
-    const int64_t fb = (int64_t)t * BPT + q;
-    if (fb < fb0) before += ba[q];
-  }
-  for (uint32_t j = t; j < nb; j += 1024) {
-    int sb = 0;
-#pragma unroll
-    for (int u = 1; u < NSUB; ++u) sb += subbase[u] <= j ? 1 : 0;
-    const uint32_t slot = j - subbase[sb];
-    const uint32_t key = blkey[sb * SUBCAP + slot], idx = blidx[sb * SUBCAP + slot];
-    before += (idx < start_idx && (key > T || (key == T && idx <= icut))) ? 1u : 0u;
-  }
-  uint32_t base_off;
-  (void)block_excl_scan(before, wsum, &base_off);
-  STAMP_T0(2);
   // count pass (first 64 list entries stay in registers), wave offsets, write pass
   uint32_t mine = 0;
   bool sel0 = false;
@@ -672,8 +652,8 @@ __global__ void __launch_bounds__(1024) sampled_compact_kernel(
   }
   if (lane == 0) wcnt[wid] = mine;
   __syncthreads();
-  STAMP_T0(3);
-  uint32_t run = base_off;
+  STAMP_T0(2);
+  uint32_t run = boff;
   for (int w = 0; w < wid; ++w) run += wcnt[w];
   if (seg >= W) return;
   auto emit = [&](bool sel, uint32_t idx) {
@@ -735,7 +715,7 @@ __global__ void __launch_bounds__(1024) sampled_compact_kernel(
       run += tot;
     }
   }
-  STAMP_T0(4);
+  STAMP_T0(3);
 }
 
 template <bool VEC>
@@ -746,6 +726,7 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L) {
   uint32_t* ghist = reinterpret_cast<uint32_t*>(a.ws + L.f_ghist);
   uint32_t* segcnt = reinterpret_cast<uint32_t*>(a.ws + L.f_segcnt);
   uint32_t* blkabove = reinterpret_cast<uint32_t*>(a.ws + L.f_blkabove);
+  uint32_t* blkoff = reinterpret_cast<uint32_t*>(a.ws + L.f_blkoff);
   uint32_t* cidx = reinterpret_cast<uint32_t*>(a.ws + L.f_cidx);
   uint32_t* ckey = reinterpret_cast<uint32_t*>(a.ws + L.f_ckey);
   uint32_t* blcnt = reinterpret_cast<uint32_t*>(a.ws + L.f_blcnt);
@@ -754,7 +735,6 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L) {
   const FastGeom& g = L.fg;
   const unsigned nb = (unsigned)g.B;
   const unsigned nsel = (unsigned)((g.W + SEL_SEGS - 1) / SEL_SEGS);
-  const unsigned ncmp = (unsigned)((g.W + CMP_SEGS - 1) / CMP_SEGS);
   DPZ_TIMED(DPZ_KT_TOPK_SAMPLE, a.st, sampled_sample_kernel<<<SMP_BLOCKS, 256, 0, a.st>>>(
       s, a.n, ctrl, chist, ghist, blcnt));
   DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC><<<nb, 256, 0, a.st>>>(
@@ -764,15 +744,19 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L) {
       s, a.n, a.k, g.W, g.B, g.R, g.CAP, ctrl, ghist, segcnt, cidx, ckey, blkabove, blcnt, blkey,
       blidx));
   DPZ_TIMED(DPZ_KT_TOPK_RESOLVE, a.st, sampled_resolve_kernel<<<1, 1024, 0, a.st>>>(
-      a.k, g.B, ctrl, blcnt, blkey, blidx, blkabove));
+      a.k, g.B, 4 * g.R, ctrl, blcnt, blkey, blidx, blkabove, blkoff));
   float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE) ? a.acc : nullptr;
-  DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC><<<ncmp, 1024, 0, a.st>>>(
-      s, a.n, a.k, g.W, g.B, g.R, g.CAP, ctrl, chist, blcnt, blkey, blidx, blkabove, segcnt, cidx,
-      ckey, a.vals_src, a.idx_out, a.val_out, a.counter, rewind));
+  DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC><<<nb, 256, 0, a.st>>>(
+      s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkoff, segcnt, cidx, ckey, a.vals_src,
+      a.idx_out, a.val_out, a.counter, rewind));
   return DPZ_OK;
 }
 
 #ifdef DPZ_STAMPS
+extern "C" int dpz_debug_filter_stamps(unsigned long long* host_out) {
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_fst), sizeof(g_fst));
+}
+
 extern "C" int dpz_debug_block_stamps(unsigned long long* host_out) {
   return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_bst), sizeof(g_bst));
 }

@@ -15,7 +15,7 @@ from decentralizepy_amd import _lib, codec  # noqa: E402
 
 NAMES = {0: "sample first-in", 1: "sample last-out", 2: "filter first-in", 3: "filter last-out",
          6: "select first-in", 7: "select last-out", 13: "compact first-in"}
-PHASES = ["entry", "loads", "offset", "counted", "end"]
+PHASES = ["entry", "loads", "counted", "end"]
 
 
 def main():
@@ -58,15 +58,32 @@ def main():
                 d = (sel[p] - sel[p - 1]) / 100
                 print(f"  {sp[p - 1]:>8} -> {sp[p]:<8} {d.mean():7.2f} {d.max():7.2f}")
             b = ball[:8]
+            L.dpz_debug_filter_stamps.argtypes = [ctypes.c_void_p]
+            fs = (ctypes.c_ulonglong * (6 * 8192))()
+            L.dpz_debug_filter_stamps(ctypes.addressof(fs))
+            f = np.frombuffer(fs, dtype=np.uint64).reshape(6, 8192).astype(np.int64)
+            nw = int((f[0] > 0).sum())
+            f = f[:, :nw]
+            t0 = f[0].min()
+            fp = ["entry", "pre-barrier", "post-barrier", "loop done", "flushed", "end"]
+            print(f"filter waves: {nw}; start spread {(f[0].max()-t0)/100:.2f} us, last end {(f[5].max()-t0)/100:.2f} us")
+            for p in range(1, 6):
+                d = (f[p] - f[p - 1]) / 100
+                print(f"  {fp[p - 1]:>12} -> {fp[p]:<12} mean {d.mean():6.2f}  p50 {np.median(d):6.2f}  max {d.max():6.2f}")
+            w0 = f[:, 0::4]
+            print(f"  wave0: entry->pre-barrier mean {((w0[1]-w0[0])/100).mean():.2f}; others {((f[1]-f[0])/100).mean():.2f}")
+            life = (f[5] - f[0]) / 100
+            print(f"  wave lifetime mean {life.mean():.2f} max {life.max():.2f}; end times p10/p50/p90 "
+                  f"{np.percentile((f[5]-t0)/100, 10):.2f}/{np.percentile((f[5]-t0)/100, 50):.2f}/{np.percentile((f[5]-t0)/100, 90):.2f}")
             nblk = int((b[0] > 0).sum())
             b = b[:, :nblk]
-            ok = b[4] > 0
+            ok = b[3] > 0
             print(f"compact blocks: {nblk}; per-block phase latency (us, mean/max over blocks):")
-            for p in range(1, 5):
+            for p in range(1, 4):
                 d = (b[p] - b[p - 1])[ok] / 100
                 print(f"  {PHASES[p - 1]:>8} -> {PHASES[p]:<8} {d.mean():7.2f} {d.max():7.2f}")
             e = (b[0][ok] - b[0][ok].min()) / 100
-            print(f"  block entry spread: {e.max():.2f} us; block start->end mean {((b[4]-b[0])[ok]/100).mean():.2f}")
+            print(f"  block entry spread: {e.max():.2f} us; block start->end mean {((b[3]-b[0])[ok]/100).mean():.2f}")
 
 
 if __name__ == "__main__":
