@@ -16,6 +16,8 @@ DPZ_ACC_ACCUMULATE = 1
 DPZ_ACC_ADD = 2
 DPZ_TOPK_EXACT = 0x1
 DPZ_TOPK_ASYNC = 0x2
+DPZ_TOPK_STREAM = 0x4
+DPZ_TOPK_TAIL = 0x8
 DPZ_FOLD_SELF = 0x1
 DPZ_FOLD_REPLACE_ONLY = 0x2
 DPZ_OK = 0

@@ -10,7 +10,8 @@ import torch
 
 from . import _lib
 from ._lib import (DPZ_ACC_ACCUMULATE, DPZ_ACC_ADD, DPZ_ACC_NONE, DPZ_FOLD_REPLACE_ONLY,
-                   DPZ_FOLD_SELF, DPZ_TOPK_ASYNC, DPZ_TOPK_EXACT, check)
+                   DPZ_FOLD_SELF, DPZ_TOPK_ASYNC, DPZ_TOPK_EXACT, DPZ_TOPK_STREAM,
+                   DPZ_TOPK_TAIL, check)
 
 __all__ = ["DPZ_ACC_NONE", "DPZ_ACC_ACCUMULATE", "DPZ_ACC_ADD", "Workspace", "topk_encode",
            "topk_complete", "decode_average", "replace", "wavedec_len", "wavedec", "waverec",
@@ -70,13 +71,16 @@ class Workspace:
 
 
 def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, counter=None,
-                idx_out=None, val_out=None, workspace=None, exact=False, asynchronous=False):
+                idx_out=None, val_out=None, workspace=None, exact=False, asynchronous=False,
+                phase=None):
     """Top-k magnitude encode (reference PartialModel.py:164-255 / Wavelet.py:142-197).
 
     Returns ``(idx int32[k], val fp32[k])`` in ascending index order.  Mutates ``acc`` and
     ``counter`` in place like the reference mutates ``model.accumulated_changes`` and
     ``model.shared_parameters_counter``.  With ``asynchronous=True`` the call only enqueues
     work; call :func:`topk_complete` with the same arguments before reading the result.
+    ``phase="stream"`` / ``"tail"`` split the enqueue in two (both asynchronous; see
+    DPZ_TOPK_STREAM in dpz_codec.h) so independent work can overlap the latency-bound tail.
     """
     _require(x, torch.float32, "x")
     _require(x0, torch.float32, "x0")
@@ -93,6 +97,8 @@ def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, c
         val_out = torch.empty(k, dtype=torch.float32, device=x.device)
     ws = (workspace or Workspace(x.device)).get(n, k)
     flags = (DPZ_TOPK_EXACT if exact else 0) | (DPZ_TOPK_ASYNC if asynchronous else 0)
+    if phase is not None:
+        flags |= {"stream": DPZ_TOPK_STREAM, "tail": DPZ_TOPK_TAIL}[phase]
     rc = _lib.lib().dpz_topk_encode(_ptr(x), _ptr(x0), _ptr(acc), int(acc_mode), _ptr(vals_src),
                                     n, k, _ptr(idx_out), _ptr(val_out), _ptr(counter), _ptr(ws),
                                     ws.numel(), flags, _stream(x.device))
@@ -113,6 +119,14 @@ def topk_complete(x, k, idx_out, val_out, workspace, x0=None, acc=None, acc_mode
                                       _ptr(ws), ws.numel(), ctypes.byref(fb), _stream(x.device))
     check(rc, "dpz_topk_complete")
     return bool(fb.value)
+
+
+def topk_status(workspace):
+    """Status word of the last sampled encode in ``workspace`` (0 = ok, else the exact path ran or
+    must run).  Synchronises with the device."""
+    if workspace.buf is None:
+        return 0
+    return int(workspace.buf[8:12].view(torch.int32).item())
 
 
 def decode_average(local, payloads, weights=None, w_self=None, out=None, replace_only=False,

@@ -184,7 +184,8 @@ struct EncodeArgs {
 
 // dpz_topk_exact.hip / dpz_topk_sampled.hip
 int run_exact(const EncodeArgs& a, const WsLayout& L, int rekey, bool vec);
-int run_sampled(const EncodeArgs& a, const WsLayout& L, bool vec);
+// phases: bit 0 = streaming pass (sample, filter), bit 1 = selection tail (select .. compact)
+int run_sampled(const EncodeArgs& a, const WsLayout& L, bool vec, int phases = 3);
 static inline bool use_sampled(int64_t n, int64_t k) {
   return n >= (1 << 18) && k >= 1 && k <= n / 16;
 }

@@ -14,21 +14,16 @@
 //  * EXACT  — three radix histogram passes (10/11/10 bits) resolve the k-th key T and the number
 //             of ties to take, then a count pass, a 1-block scan and an ordered-compaction pass.
 //             Works for every n, k (also k = n, heavy ties, NaN).  ~5 reads of the key stream.
-//  * SAMPLED (k <= n/16, n >= 2^18) — one read of the inputs:
-//      sample  : 64 blocks histogram 65,536 sampled keys into a 2048-bin coarse histogram
-//      filter  : every block derives the key window [lo, hi) bracketing the k-th key from the
-//                coarse histogram (redundantly, overlapped with its first loads), then streams its
-//                contiguous segment of x/x0/acc once: keys >= lo are appended in index order to a
-//                per-segment candidate list (idx,key,val) and binned into a 256-bin window
-//                histogram row per segment
-//      selectA : column sums of the per-segment rows -> global window histogram
-//      selectB : threshold bin b*; per-segment count above b*; bin-b* entries -> boundary list
-//      selectC : 1 block radix-selects inside bin b* -> exact T, tie cut, per-segment offsets
-//      compact : ordered write of idx/val + counter / rewind side effects
+//  * SAMPLED (k <= n/16, n >= 2^18) — one read of the inputs, four launches
+//             (dpz_topk_sampled.hip): sample -> filter (window [lo, hi) around the k-th key,
+//             candidates >= lo appended per wave segment in index order, window histogram) ->
+//             select (threshold bin b*, per-block counts above it, bin-b* boundary list) ->
+//             compact (exact T and tie cut resolved redundantly per block, ordered write of
+//             idx/val + counter / rewind side effects).
 //    Any miss (window did not bracket the k-th key, boundary overflow) sets ctrl->status; the
 //    compact kernel then writes nothing and the host re-runs the EXACT path with keys re-derived
 //    from the post-filter state ("rekey").  A segment whose candidates overflow its list is marked
-//    dense and re-reads its own input range in selectB / compact instead (still exact).
+//    dense and re-reads its own input range in select / compact instead (still exact).
 #include "dpz_topk.h"
 
 namespace dpz {
@@ -90,14 +85,17 @@ static int dpz_topk_dispatch(const EncodeArgs& a, int flags) {
       return vec ? run_accumulate_only<true>(a) : run_accumulate_only<false>(a);
     return DPZ_OK;
   }
+  const int phases = (flags & DPZ_TOPK_STREAM) ? 1 : ((flags & DPZ_TOPK_TAIL) ? 2 : 3);
+  if (phases != 3) flags |= DPZ_TOPK_ASYNC;
   if (!(flags & DPZ_TOPK_EXACT) && use_sampled(a.n, a.k)) {
-    int rc = run_sampled(a, L, vec);
+    int rc = run_sampled(a, L, vec, phases);
     if (rc != DPZ_OK) return rc;
     if (flags & DPZ_TOPK_ASYNC) return DPZ_OK;
     int fb = 0;
     return dpz_topk_complete(a.x, a.x0, a.acc, a.acc_mode, a.vals_src, a.n, a.k, a.idx_out,
                              a.val_out, a.counter, a.ws, L.total, &fb, a.st);
   }
+  if (phases == 2) return DPZ_OK;  // the exact path ran whole in the STREAM call
   int rc = run_exact(a, L, 0, vec);
   if (rc != DPZ_OK) return rc;
   if (!(flags & DPZ_TOPK_ASYNC)) DPZ_HIP_TRY(hipStreamSynchronize(a.st));

@@ -316,9 +316,15 @@ __device__ __forceinline__ bool wave_bstar(uint4 ghv, uint32_t above, uint32_t k
   return ok;
 }
 
-// One block of 1024 threads: gather the boundary sub-lists, radix-select the need-th largest key
-// inside bin b* (offsets below 2^shift, 8-bit digits), then the tie cut (the lowest indices among
-// keys == T), and check that above + selected == k.  Writes T, icut or a status for the host.
+// One block of 1024 threads: gather the boundary sub-lists and find the pivot, the need-th entry of
+// bin b* in (key descending, index ascending) order; an entry of bin b* is selected iff it is not
+// after the pivot, i.e. key > T or (key == T and idx <= icut) with (T, icut) = the pivot.  One
+// 8-bit digit pass over the offsets inside bin b* (~k/256 entries) leaves a handful in the pivot's
+// digit; if at most 64, one wave ranks them against each other (register broadcasts) and the
+// entry of rank rem - 1 is the pivot — ties cost nothing extra.  Otherwise (heavy ties, wide
+// bins): radix select of T over the remaining digits, then of the tie cut on the index.
+// Then every filter block's output offset (above + selected boundary entries, scanned) and the
+// check that the total is k.  Writes T, icut or a status for the host.
 __global__ void __launch_bounds__(1024) sampled_resolve_kernel(
     int64_t k, int64_t B, int64_t R4, TopkCtrl* ctrl, const uint32_t* __restrict__ blcnt,
     const uint32_t* __restrict__ blkey, const uint32_t* __restrict__ blidx,
@@ -330,6 +336,8 @@ __global__ void __launch_bounds__(1024) sampled_resolve_kernel(
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t sh[4];
   __shared__ uint32_t blksel[B_MAX];
+  __shared__ uint2 ent[64];
+  __shared__ uint32_t bcnt;
   STAMP_T0(12);
   const int t = threadIdx.x;
   const uint32_t status = ctrl->status;
@@ -375,67 +383,120 @@ __global__ void __launch_bounds__(1024) sampled_resolve_kernel(
     }
   }
   STAMP_T0(13);
+  uint32_t T, icut;
+  // first digit pass (top <= 8 bits of the offset inside bin b*): digit d*, rank left in it, size
   const uint32_t base = lo + (bstar << shift);
-  uint32_t prefix = 0, rem = need, eqcnt = nb;
-  for (int top = (int)shift; top > 0; top -= 8) {
-    const int d = top >= 8 ? 8 : top;
-    const int low = top - d;
-    if (t < 256) hist[t] = 0;
-    __syncthreads();
+  const int d1 = shift >= 8 ? 8 : (int)shift;
+  const int low1 = (int)shift - d1;
+  if (t < 256) hist[t] = 0;
+  if (t == 0) bcnt = 0;
+  __syncthreads();
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const uint32_t j = t + q * 1024;
-      if (j < nb) {
-        const uint32_t o = kk[q] - base;
-        if ((uint32_t)((uint64_t)o >> top) == (uint32_t)((uint64_t)prefix >> top))
-          atomicAdd(&hist[(o >> low) & ((1u << d) - 1)], 1u);
-      }
-    }
-    __syncthreads();
+  for (int q = 0; q < PER; ++q) {
+    const uint32_t j = t + q * 1024;
+    if (j < nb) atomicAdd(&hist[((kk[q] - base) >> low1) & ((1u << d1) - 1)], 1u);
+  }
+  __syncthreads();
+  {
     const uint32_t hb = t < 256 ? hist[255 - t] : 0u;  // descending digit 255 - t
     uint32_t tot;
     const uint32_t before = block_excl_scan(hb, wsum, &tot);
-    if (t < 256 && before < rem && rem <= before + hb) {
+    if (t < 256 && before < need && need <= before + hb) {
       sh[0] = 255 - t;
-      sh[1] = rem - before;
+      sh[1] = need - before;
       sh[2] = hb;
     }
     __syncthreads();
-    prefix |= sh[0] << low;
-    rem = sh[1];
-    eqcnt = sh[2];
-    __syncthreads();
   }
-  const uint32_t T = base + prefix;
-  STAMP_T0(14);
-  uint32_t icut = 0xFFFFFFFFu;
-  if (rem < eqcnt) {
-    uint32_t ipre = 0, irem = rem;
-    for (int top = 32; top > 0; top -= 8) {
-      const int low = top - 8;
+  const uint32_t dstar = sh[0], rem1 = sh[1], eq1 = sh[2];
+  if (eq1 <= 64) {
+    // the pivot is the rem1-th entry of the <= 64 in digit d* (key descending, index ascending):
+    // gather them, one wave ranks each against all (register broadcasts, no LDS round trips)
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const uint32_t j = t + q * 1024;
+      if (j < nb && (((kk[q] - base) >> low1) & ((1u << d1) - 1)) == dstar)
+        ent[atomicAdd(&bcnt, 1u)] = make_uint2(kk[q], ii[q]);
+    }
+    __syncthreads();
+    if (t < 64) {
+      const uint2 me = t < (int)eq1 ? ent[t] : make_uint2(0u, 0xFFFFFFFFu);
+      uint32_t rank = 0;
+      for (uint32_t f = 0; f < eq1; ++f) {
+        const uint32_t ok = __builtin_amdgcn_readlane(me.x, f);
+        const uint32_t oi = __builtin_amdgcn_readlane(me.y, f);
+        rank += (ok > me.x || (ok == me.x && oi < me.y)) ? 1u : 0u;
+      }
+      if (t < (int)eq1 && rank == rem1 - 1) {
+        sh[0] = me.x;
+        sh[1] = me.y;
+      }
+    }
+    __syncthreads();
+    T = sh[0];
+    icut = sh[1];
+  } else {
+    uint32_t prefix = 0, rem = need, eqcnt = nb;
+    for (int top = (int)shift; top > 0; top -= 8) {
+      const int d = top >= 8 ? 8 : top;
+      const int low = top - d;
       if (t < 256) hist[t] = 0;
       __syncthreads();
 #pragma unroll
       for (int q = 0; q < PER; ++q) {
         const uint32_t j = t + q * 1024;
-        if (j < nb && kk[q] == T && (top == 32 || (ii[q] >> top) == (ipre >> top)))
-          atomicAdd(&hist[(ii[q] >> low) & 255u], 1u);
+        if (j < nb) {
+          const uint32_t o = kk[q] - base;
+          if ((uint32_t)((uint64_t)o >> top) == (uint32_t)((uint64_t)prefix >> top))
+            atomicAdd(&hist[(o >> low) & ((1u << d) - 1)], 1u);
+        }
       }
       __syncthreads();
-      const uint32_t hb = t < 256 ? hist[t] : 0u;  // ascending digit t
+      const uint32_t hb = t < 256 ? hist[255 - t] : 0u;  // descending digit 255 - t
       uint32_t tot;
       const uint32_t before = block_excl_scan(hb, wsum, &tot);
-      if (t < 256 && before < irem && irem <= before + hb) {
-        sh[0] = t;
-        sh[1] = irem - before;
+      if (t < 256 && before < rem && rem <= before + hb) {
+        sh[0] = 255 - t;
+        sh[1] = rem - before;
+        sh[2] = hb;
       }
       __syncthreads();
-      ipre |= sh[0] << low;
-      irem = sh[1];
+      prefix |= sh[0] << low;
+      rem = sh[1];
+      eqcnt = sh[2];
       __syncthreads();
     }
-    icut = ipre;
+    T = base + prefix;
+    icut = 0xFFFFFFFFu;
+    if (rem < eqcnt) {
+      uint32_t ipre = 0, irem = rem;
+      for (int top = 32; top > 0; top -= 8) {
+        const int low = top - 8;
+        if (t < 256) hist[t] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+          const uint32_t j = t + q * 1024;
+          if (j < nb && kk[q] == T && (top == 32 || (ii[q] >> top) == (ipre >> top)))
+            atomicAdd(&hist[(ii[q] >> low) & 255u], 1u);
+        }
+        __syncthreads();
+        const uint32_t hb = t < 256 ? hist[t] : 0u;  // ascending digit t
+        uint32_t tot;
+        const uint32_t before = block_excl_scan(hb, wsum, &tot);
+        if (t < 256 && before < irem && irem <= before + hb) {
+          sh[0] = t;
+          sh[1] = irem - before;
+        }
+        __syncthreads();
+        ipre |= sh[0] << low;
+        irem = sh[1];
+        __syncthreads();
+      }
+      icut = ipre;
+    }
   }
+  STAMP_T0(14);
   // every filter block's output offset: above counts + selected boundary entries, scanned
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
@@ -719,7 +780,7 @@ __global__ void __launch_bounds__(256, 8) sampled_compact_kernel(
 }
 
 template <bool VEC>
-static int run_sampled_t(const EncodeArgs& a, const WsLayout& L) {
+static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
   KeySrc s{a.x, a.x0, a.acc, a.acc_mode, 0};
   TopkCtrl* ctrl = reinterpret_cast<TopkCtrl*>(a.ws + L.ctrl);
   uint32_t* chist = reinterpret_cast<uint32_t*>(a.ws + L.chist);
@@ -735,10 +796,13 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L) {
   const FastGeom& g = L.fg;
   const unsigned nb = (unsigned)g.B;
   const unsigned nsel = (unsigned)((g.W + SEL_SEGS - 1) / SEL_SEGS);
-  DPZ_TIMED(DPZ_KT_TOPK_SAMPLE, a.st, sampled_sample_kernel<<<SMP_BLOCKS, 256, 0, a.st>>>(
-      s, a.n, ctrl, chist, ghist, blcnt));
-  DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC><<<nb, 256, 0, a.st>>>(
-      s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey));
+  if (phases & 1) {
+    DPZ_TIMED(DPZ_KT_TOPK_SAMPLE, a.st, sampled_sample_kernel<<<SMP_BLOCKS, 256, 0, a.st>>>(
+        s, a.n, ctrl, chist, ghist, blcnt));
+    DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC><<<nb, 256, 0, a.st>>>(
+        s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey));
+  }
+  if (!(phases & 2)) return DPZ_OK;
   s.rekey = 1;
   DPZ_TIMED(DPZ_KT_TOPK_SELECT, a.st, sampled_select_kernel<VEC><<<nsel, 1024, 0, a.st>>>(
       s, a.n, a.k, g.W, g.B, g.R, g.CAP, ctrl, ghist, segcnt, cidx, ckey, blkabove, blcnt, blkey,
@@ -772,8 +836,8 @@ extern "C" int dpz_debug_stamps(unsigned long long* host_out, int reset) {
 }
 #endif
 
-int run_sampled(const EncodeArgs& a, const WsLayout& L, bool vec) {
-  return vec ? run_sampled_t<true>(a, L) : run_sampled_t<false>(a, L);
+int run_sampled(const EncodeArgs& a, const WsLayout& L, bool vec, int phases) {
+  return vec ? run_sampled_t<true>(a, L, phases) : run_sampled_t<false>(a, L, phases);
 }
 
 }  // namespace dpz

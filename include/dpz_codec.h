@@ -45,6 +45,13 @@ typedef void* dpz_stream_t; /* hipStream_t */
 /* ---- top-k flags ---- */
 #define DPZ_TOPK_EXACT 0x1 /* force the exact multi-pass radix path (skip the sampled path)  */
 #define DPZ_TOPK_ASYNC 0x2 /* enqueue only; the caller must call dpz_topk_complete() later   */
+/* Split enqueue (implies DPZ_TOPK_ASYNC), for callers that overlap independent work with the
+ * latency-bound part of the encode: STREAM enqueues the pass that reads the inputs (sample +
+ * filter); a second call with TAIL and the SAME arguments, on the same stream or one ordered
+ * after it, enqueues the selection tail (select, resolve, compact).  On the exact path STREAM
+ * enqueues everything and TAIL nothing.                                                       */
+#define DPZ_TOPK_STREAM 0x4
+#define DPZ_TOPK_TAIL 0x8
 
 /* ---- fold flags ---- */
 #define DPZ_FOLD_SELF 0x1         /* add the local term w_self*local after the payloads        */

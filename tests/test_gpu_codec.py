@@ -320,3 +320,36 @@ def test_topk_workspace_reuse_across_calls_and_misses(dev):
         oi, ov = otopk.encode(xq, x0, None, 0, k)
         np.testing.assert_array_equal(idx.cpu().numpy(), oi)
         np.testing.assert_array_equal(_bits(val.cpu().numpy()), _bits(ov))
+
+
+@pytest.mark.parametrize("n,alpha", [(1_000_003, 0.01), (300_000, 0.2)])
+def test_split_stream_tail_enqueue(dev, n, alpha):
+    """DPZ_TOPK_STREAM then DPZ_TOPK_TAIL (another stream's decode in between) == one-shot encode;
+    alpha = 0.2 takes the exact path, where STREAM does everything and TAIL nothing."""
+    codec = _codec()
+    x, x0 = _inputs(n, 21)
+    k = round(alpha * n)
+    o_cnt = np.zeros(n, dtype=np.int32)
+    oi, ov = otopk.encode(x, x0, None, 0, k, counter=o_cnt)
+    tx, tx0 = torch.from_numpy(x).to(dev), torch.from_numpy(x0).to(dev)
+    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    idx = torch.empty(k, dtype=torch.int32, device=dev)
+    val = torch.empty(k, dtype=torch.float32, device=dev)
+    ws = codec.Workspace(dev)
+    side = torch.cuda.Stream(dev)
+    codec.topk_encode(tx, k, x0=tx0, counter=cnt, idx_out=idx, val_out=val, workspace=ws,
+                      phase="stream")
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):  # unrelated decode on the other stream meanwhile
+        other = codec.replace(tx0, torch.tensor([5], dtype=torch.int32, device=dev),
+                              torch.tensor([1.5], dtype=torch.float32, device=dev))
+    codec.topk_encode(tx, k, x0=tx0, counter=cnt, idx_out=idx, val_out=val, workspace=ws,
+                      phase="tail")
+    codec.topk_complete(tx, k, idx, val, ws, x0=tx0, counter=cnt)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(idx.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(val.cpu().numpy()), _bits(ov))
+    np.testing.assert_array_equal(cnt.cpu().numpy(), o_cnt)
+    want = x0.copy()
+    want[5] = 1.5
+    np.testing.assert_array_equal(_bits(other.cpu().numpy()), _bits(want))
