@@ -17,56 +17,90 @@ struct KeySrc {
   int rekey;
 };
 
-template <bool VEC>
-__device__ __forceinline__ int load_keys4(const KeySrc& s, int64_t i0, int64_t n, bool store_acc,
-                                          uint32_t key[4]) {
-  float c[4];
+// The raw loads of 4 consecutive elements (x, x0, acc as the mode needs), split from the key
+// computation so a caller can keep them in flight while it does other work.
+struct Raw4 {
+  float4 a, b, q;
+  int cnt;
+};
+
+// ACC = false: the caller guarantees s.mode == DPZ_ACC_NONE (no acc registers are held).
+template <bool VEC, bool ACC = true>
+__device__ __forceinline__ void load_raw4(const KeySrc& s, int64_t i0, int64_t n, Raw4& r) {
   const int64_t rem = n - i0;
-  const int cnt = rem >= 4 ? 4 : (rem > 0 ? (int)rem : 0);
-  if (VEC && cnt == 4) {
-    if (s.mode == DPZ_ACC_ACCUMULATE && s.rekey) {
-      float4 q = *reinterpret_cast<const float4*>(s.acc + i0);
-      c[0] = q.x; c[1] = q.y; c[2] = q.z; c[3] = q.w;
+  r.cnt = rem >= 4 ? 4 : (rem > 0 ? (int)rem : 0);
+  const int mode = ACC ? s.mode : DPZ_ACC_NONE;
+  const bool rekey = mode == DPZ_ACC_ACCUMULATE && s.rekey;
+  if (VEC && r.cnt == 4) {
+    if (rekey) {
+      r.q = *reinterpret_cast<const float4*>(s.acc + i0);
     } else {
-      float4 a = *reinterpret_cast<const float4*>(s.x + i0);
-      c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w;
-      if (s.x0) {
-        float4 b = *reinterpret_cast<const float4*>(s.x0 + i0);
-        c[0] = a.x - b.x; c[1] = a.y - b.y; c[2] = a.z - b.z; c[3] = a.w - b.w;
-      }
-      if (s.mode != DPZ_ACC_NONE) {
-        float4 q = *reinterpret_cast<const float4*>(s.acc + i0);
-        float4 r;
-        r.x = q.x + c[0]; r.y = q.y + c[1]; r.z = q.z + c[2]; r.w = q.w + c[3];
-        if (s.mode == DPZ_ACC_ACCUMULATE && store_acc) *reinterpret_cast<float4*>(s.acc + i0) = r;
-        c[0] = r.x; c[1] = r.y; c[2] = r.z; c[3] = r.w;
-      }
+      r.a = *reinterpret_cast<const float4*>(s.x + i0);
+      if (s.x0) r.b = *reinterpret_cast<const float4*>(s.x0 + i0);
+      if (mode != DPZ_ACC_NONE) r.q = *reinterpret_cast<const float4*>(s.acc + i0);
     }
   } else {
+    float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f}, q[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      if (e < cnt) {
+      if (e < r.cnt) {
         const int64_t i = i0 + e;
-        float v;
-        if (s.mode == DPZ_ACC_ACCUMULATE && s.rekey) {
-          v = s.acc[i];
+        if (rekey) {
+          q[e] = s.acc[i];
         } else {
-          v = s.x0 ? (s.x[i] - s.x0[i]) : s.x[i];
-          if (s.mode != DPZ_ACC_NONE) {
-            float r = s.acc[i] + v;
-            if (s.mode == DPZ_ACC_ACCUMULATE && store_acc) s.acc[i] = r;
-            v = r;
-          }
+          a[e] = s.x[i];
+          if (s.x0) b[e] = s.x0[i];
+          if (mode != DPZ_ACC_NONE) q[e] = s.acc[i];
         }
-        c[e] = v;
-      } else {
-        c[e] = 0.0f;
       }
+    }
+    r.a = make_float4(a[0], a[1], a[2], a[3]);
+    r.b = make_float4(b[0], b[1], b[2], b[3]);
+    r.q = make_float4(q[0], q[1], q[2], q[3]);
+  }
+}
+
+// Keys of the 4 elements of r (elements past the end get key 0); stores acc += change for the
+// first pass of DPZ_ACC_ACCUMULATE when store_acc.  Returns the element count.
+template <bool VEC, bool ACC = true>
+__device__ __forceinline__ int finish_keys4(const KeySrc& s, int64_t i0, bool store_acc,
+                                            const Raw4& r, uint32_t key[4]) {
+  const int mode = ACC ? s.mode : DPZ_ACC_NONE;
+  const float ra[4] = {r.a.x, r.a.y, r.a.z, r.a.w};
+  const float rb[4] = {r.b.x, r.b.y, r.b.z, r.b.w};
+  const float rq[4] = {r.q.x, r.q.y, r.q.z, r.q.w};
+  float c[4];
+  const bool rekey = mode == DPZ_ACC_ACCUMULATE && s.rekey;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (rekey) {
+      c[e] = rq[e];
+    } else {
+      float v = s.x0 ? (ra[e] - rb[e]) : ra[e];
+      if (mode != DPZ_ACC_NONE) v = rq[e] + v;
+      c[e] = v;
+    }
+  }
+  if (!rekey && mode == DPZ_ACC_ACCUMULATE && store_acc) {
+    if (VEC && r.cnt == 4) {
+      *reinterpret_cast<float4*>(s.acc + i0) = make_float4(c[0], c[1], c[2], c[3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (e < r.cnt) s.acc[i0 + e] = c[e];
     }
   }
 #pragma unroll
-  for (int e = 0; e < 4; ++e) key[e] = key_of(c[e]);
-  return cnt;
+  for (int e = 0; e < 4; ++e) key[e] = e < r.cnt ? key_of(c[e]) : 0u;
+  return r.cnt;
+}
+
+template <bool VEC>
+__device__ __forceinline__ int load_keys4(const KeySrc& s, int64_t i0, int64_t n, bool store_acc,
+                                          uint32_t key[4]) {
+  Raw4 r;
+  load_raw4<VEC>(s, i0, n, r);
+  return finish_keys4<VEC>(s, i0, store_acc, r, key);
 }
 
 // Control block in the workspace (first 256 bytes).
@@ -101,10 +135,14 @@ constexpr int HBR = HB + 1;
 #define DPZ_WMIN_RANGE 1024
 #endif
 #ifndef DPZ_FG
-#define DPZ_FG 4
+#define DPZ_FG 2
 #endif
 constexpr int W_MAX = DPZ_WMAX;    // wave segments (one wave streams one contiguous segment)
 constexpr int FG = DPZ_FG;         // float4 groups of 256 elements a filter wave loads at once
+#ifndef DPZ_FOCC
+#define DPZ_FOCC 8
+#endif
+constexpr int FOCC = DPZ_FOCC;     // filter waves per SIMD the register budget is sized for
 constexpr int W_MIN_RANGE = DPZ_WMIN_RANGE;
 constexpr int GH_COPIES = 16;      // window histogram copies (filter block b adds into copy b % 16)
 constexpr int GH_STRIDE = 272;     // >= HBR, 16-aligned

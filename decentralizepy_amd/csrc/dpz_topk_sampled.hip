@@ -96,43 +96,33 @@ __global__ void __launch_bounds__(256) sampled_sample_kernel(KeySrc s, int64_t n
   STAMP_MAX(1);
 }
 
-// Wave-level: window [lo, hi) around the k-th key from the coarse sample histogram.
-// cv = this lane's 32 bins [2016-32l, 2047-32l] (ascending in memory).
-// Ranks are 1-based, descending, with a 6-sigma + 16 margin.  Result written to win[0..2].
-__device__ __forceinline__ void wave_window(const uint4 (&cv)[8], int64_t n, int64_t k,
-                                            uint32_t* win) {
-  const int lane = threadIdx.x & 63;
-  const double r_est = (double)k * SMP_N / (double)n;
-  const double sd = sqrt(r_est);
-  const double rlo_d = ceil(r_est + 6.0 * sd + 16.0);
-  const double rhi_d = floor(r_est - 6.0 * sd - 16.0);
-  const uint32_t r_lo = rlo_d > SMP_N ? (uint32_t)SMP_N + 1 : (uint32_t)rlo_d;
-  const uint32_t r_hi = rhi_d < 1.0 ? 0u : (uint32_t)rhi_d;
-  uint32_t local = 0;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) local += cv[q].x + cv[q].y + cv[q].z + cv[q].w;
-  uint32_t tot;
-  uint32_t before = wave_excl_scan(local, &tot);
-  if (lane == 0) {
+// Block-level (256 threads): window [lo, hi) around the k-th key from the coarse sample histogram.
+// Thread t holds the 8 bins cv = [2040-8t, 2047-8t] (ascending in memory).  Ranks r_lo / r_hi are
+// 1-based, descending (window_ranks).  Result in win[0..2] after the call (barriers inside: every
+// thread of the block must call it).
+__device__ __forceinline__ void block_window(const uint4 (&cv)[2], uint32_t r_lo, uint32_t r_hi,
+                                             uint32_t* win, uint32_t* wsum) {
+  const int t = threadIdx.x;
+  if (t == 0) {
     win[3] = 0xFFFFFFFFu;  // bin of rank r_lo
     win[2] = 0xFFFFFFFFu;  // bin of rank r_hi
   }
-  // descending: bin 2047-32l first = cv[7].w
+  const uint32_t hv8[8] = {cv[1].w, cv[1].z, cv[1].y, cv[1].x, cv[0].w, cv[0].z, cv[0].y, cv[0].x};
+  uint32_t local = 0;
 #pragma unroll
-  for (int q = 7; q >= 0; --q) {
-    const uint32_t hv4[4] = {cv[q].w, cv[q].z, cv[q].y, cv[q].x};
+  for (int e = 0; e < 8; ++e) local += hv8[e];
+  uint32_t tot;
+  uint32_t before = block_excl_scan(local, wsum, &tot);  // barriers order the win[] init first
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const uint32_t bin = (uint32_t)(2016 - 32 * lane + 4 * q + 3 - e);
-      const uint32_t hv = hv4[e];
-      if (r_lo <= (uint32_t)SMP_N && before < r_lo && r_lo <= before + hv) win[3] = bin;
-      if (r_hi >= 1 && before < r_hi && r_hi <= before + hv) win[2] = bin;
-      before += hv;
-    }
+  for (int e = 0; e < 8; ++e) {  // descending: bin 2047-8t first
+    const uint32_t bin = (uint32_t)(2047 - 8 * t - e);
+    const uint32_t hv = hv8[e];
+    if (r_lo <= (uint32_t)SMP_N && before < r_lo && r_lo <= before + hv) win[3] = bin;
+    if (r_hi >= 1 && before < r_hi && r_hi <= before + hv) win[2] = bin;
+    before += hv;
   }
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): LDS writes of this wave done
-  __builtin_amdgcn_wave_barrier();
-  if (lane == 0) {
+  __syncthreads();
+  if (t == 0) {
     const uint32_t blo = win[3], bhi = win[2];
     const uint32_t lo = (blo != 0xFFFFFFFFu) ? (blo << CB_SHIFT) : 0u;
     const uint64_t h64 = (bhi != 0xFFFFFFFFu) ? ((uint64_t)(bhi + 1) << CB_SHIFT) : (1ull << 31);
@@ -144,6 +134,18 @@ __device__ __forceinline__ void wave_window(const uint4 (&cv)[8], int64_t n, int
     win[1] = hi;
     win[2] = sft;
   }
+  __syncthreads();
+}
+
+// Sample ranks (1-based, descending) that bracket the k-th key with a 6-sigma + 16 margin: the
+// k-th largest of n sits near rank k * SMP_N / n of the SMP_N samples (binomial sd ~ sqrt).
+static inline void window_ranks(int64_t n, int64_t k, uint32_t* r_lo, uint32_t* r_hi) {
+  const double r_est = (double)k * SMP_N / (double)n;
+  const double sd = sqrt(r_est);
+  const double rlo_d = ceil(r_est + 6.0 * sd + 16.0);
+  const double rhi_d = floor(r_est - 6.0 * sd - 16.0);
+  *r_lo = rlo_d > SMP_N ? (uint32_t)SMP_N + 1 : (uint32_t)rlo_d;
+  *r_hi = rhi_d < 1.0 ? 0u : (uint32_t)rhi_d;
 }
 
 // Per-wave candidate list append through an LDS stage, flushed in coalesced 64-lane chunks.
@@ -155,12 +157,18 @@ struct WaveList {
   uint32_t staged;  // entries in the stage (wave-uniform)
   uint32_t flushed; // entries already in the global list (wave-uniform)
 
-  __device__ __forceinline__ void flush(int lane) {
+  // write the stage to the global list (if `write`) and bin its keys into the window histogram
+  __device__ __forceinline__ void flush(int lane, bool write, uint32_t* h, uint32_t lo, uint32_t hi,
+                                        uint32_t shift) {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LDS stage writes done
     __builtin_amdgcn_wave_barrier();
     for (uint32_t j = lane; j < staged; j += 64) {
-      gidx[flushed + j] = sidx[j];
-      gkey[flushed + j] = skey[j];
+      const uint32_t key = skey[j];
+      atomicAdd(&h[fine_bin(key, lo, hi, shift)], 1u);
+      if (write) {
+        gidx[flushed + j] = sidx[j];
+        gkey[flushed + j] = key;
+      }
     }
     __builtin_amdgcn_wave_barrier();
     flushed += staged;
@@ -168,14 +176,42 @@ struct WaveList {
   }
 };
 
+// A wave's G float4 groups [base, base + G*256): every load is issued before any is used, so
+// G x (2 or 3) 16-byte loads per lane are in flight at once; full groups take a branch-free path.
+template <bool VEC, bool ACC, int G>
+__device__ __forceinline__ void load_groups(const KeySrc& s, int64_t base, int64_t end, int lane,
+                                            Raw4 (&raw)[G]) {
+  if (VEC && base + G * 256 <= end) {
+    const bool rekey = ACC && s.mode == DPZ_ACC_ACCUMULATE && s.rekey;
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      const int64_t i0 = base + q * 256 + lane * 4;
+      raw[q].cnt = 4;
+      if (!rekey) {
+        raw[q].a = *reinterpret_cast<const float4*>(s.x + i0);
+        if (s.x0) raw[q].b = *reinterpret_cast<const float4*>(s.x0 + i0);
+      }
+      if (ACC && s.mode != DPZ_ACC_NONE) raw[q].q = *reinterpret_cast<const float4*>(s.acc + i0);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      const int64_t i0 = base + q * 256 + lane * 4;
+      raw[q].cnt = 0;
+      if (i0 < end) load_raw4<VEC, ACC>(s, i0, end, raw[q]);
+    }
+  }
+}
+
 // B blocks x 256 threads; wave w of block b owns wave segment seg = 4b + w = [seg*R, +R) of [0, n).
-template <bool VEC>
-__global__ void __launch_bounds__(256, FG <= 4 ? 8 : (FG <= 6 ? 7 : 6)) sampled_filter_kernel(
-    KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl,
-    const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt, uint32_t* cidx,
-    uint32_t* ckey) {
+template <bool VEC, bool ACC, int G>
+__global__ void __launch_bounds__(256, FOCC) sampled_filter_kernel(
+    KeySrc s, int64_t n, uint32_t r_lo, uint32_t r_hi, int64_t W, int64_t R, int64_t CAP,
+    TopkCtrl* ctrl, const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt,
+    uint32_t* cidx, uint32_t* ckey) {
   __shared__ uint32_t h[HBR];
   __shared__ uint32_t win[4];
+  __shared__ uint32_t wsum[16];
   __shared__ uint32_t st_idx[4][STAGE], st_key[4][STAGE];
   STAMP_W(0);
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -184,37 +220,20 @@ __global__ void __launch_bounds__(256, FG <= 4 ? 8 : (FG <= 6 ? 7 : 6)) sampled_
   const int64_t beg = seg * R;
   const int64_t end = (beg + R < n) ? beg + R : n;
   const bool store_acc = (s.mode == DPZ_ACC_ACCUMULATE) && !s.rekey;
-  uint32_t key[FG][4];
-  int cnt[FG];
-  // waves 1-3 start streaming at once; wave 0 first turns the coarse sample histogram into the
-  // key window (its 32 bin registers die before its own stream starts, after the barrier)
-  if (wid != 0) {
-#pragma unroll
-    for (int q = 0; q < FG; ++q) {
-      const int64_t i0 = beg + q * 256 + lane * 4;
-      cnt[q] = i0 < end ? load_keys4<VEC>(s, i0, end, store_acc, key[q]) : 0;
-    }
-  } else {
-#ifdef DPZ_ABLATE_WINDOW  // timing only: a fixed window instead of the sample histogram's
-    if (lane == 0) { win[0] = 0x3CBF0000u; win[1] = 0x3CD00000u; win[2] = 13; }
-#else
-    uint4 cv[8];
-    const uint4* c4 = reinterpret_cast<const uint4*>(chist) + (504 - 8 * lane);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) cv[q] = c4[q];
-    wave_window(cv, n, k, win);
-#endif
+  // The coarse sample histogram is loaded first (L2), then every wave's first G groups: loads
+  // complete in issue order, so the block turns the histogram into the key window while the
+  // stream loads are still in flight, and only then waits for them.
+  uint4 cv[2];
+  {
+    const uint4* c4 = reinterpret_cast<const uint4*>(chist) + (510 - 2 * threadIdx.x);
+    cv[0] = c4[0];
+    cv[1] = c4[1];
   }
+  Raw4 raw[G];
+  load_groups<VEC, ACC, G>(s, beg, end, lane, raw);
+  block_window(cv, r_lo, r_hi, win, wsum);
   STAMP_W(1);
-  __syncthreads();
   STAMP_W(2);
-  if (wid == 0) {
-#pragma unroll
-    for (int q = 0; q < FG; ++q) {
-      const int64_t i0 = beg + q * 256 + lane * 4;
-      cnt[q] = i0 < end ? load_keys4<VEC>(s, i0, end, store_acc, key[q]) : 0;
-    }
-  }
   const uint32_t lo = win[0], hi = win[1], shift = win[2];
   if (seg == 0 && lane == 0) {
     ctrl->lo = lo;
@@ -224,60 +243,49 @@ __global__ void __launch_bounds__(256, FG <= 4 ? 8 : (FG <= 6 ? 7 : 6)) sampled_
   WaveList L{cidx + seg * CAP, ckey + seg * CAP, st_idx[wid], st_key[wid], 0u, 0u};
   uint32_t run = 0;
   bool dense = false;
-  for (int64_t base = beg; base < end; base += FG * 256) {
-    if (base != beg) {
+  for (int64_t base = beg; base < end; base += G * 256) {
+    if (base != beg) load_groups<VEC, ACC, G>(s, base, end, lane, raw);
 #pragma unroll
-      for (int q = 0; q < FG; ++q) {
-        const int64_t i0 = base + q * 256 + lane * 4;
-        cnt[q] = i0 < end ? load_keys4<VEC>(s, i0, end, store_acc, key[q]) : 0;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < FG; ++q) {
+    for (int q = 0; q < G; ++q) {
+      uint32_t kq[4];
+      const int cq = raw[q].cnt;
+      if (cq) finish_keys4<VEC, ACC>(s, base + q * 256 + lane * 4, store_acc, raw[q], kq);
       bool f[4];
       uint32_t pre = 0, tot = 0;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        f[e] = e < cnt[q] && key[q][e] >= lo;
-#ifndef DPZ_ABLATE_HIST
-        if (f[e]) atomicAdd(&h[fine_bin(key[q][e], lo, hi, shift)], 1u);
-#endif
+        f[e] = e < cq && kq[e] >= lo;
         const uint64_t m = __ballot(f[e]);
         pre += mbcnt64(m);
         tot += (uint32_t)__popcll(m);
       }
-#ifdef DPZ_ABLATE_APPEND
-      if (false) {
-#else
       if (tot) {
-#endif
-        if (!dense && run + tot <= (uint32_t)CAP) {
+        // candidates are staged in LDS and binned into the window histogram when the stage is
+        // flushed (all lanes busy), not one divergent LDS atomic per element here
+        if (!dense && run + tot <= (uint32_t)CAP && tot <= (uint32_t)STAGE) {
           const uint32_t i0 = (uint32_t)(base + q * 256 + lane * 4);
-          if (L.staged + tot > STAGE) L.flush(lane);
-          if (tot > STAGE) {  // too many for the stage: write this group straight through
-            uint32_t p = L.flushed + pre;
+          if (L.staged + tot > STAGE) L.flush(lane, true, h, lo, hi, shift);
+          uint32_t p = L.staged + pre;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              if (f[e]) { L.gidx[p] = i0 + e; L.gkey[p] = key[q][e]; ++p; }
-            }
-            L.flushed += tot;
-          } else {
-            uint32_t p = L.staged + pre;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              if (f[e]) { L.sidx[p] = i0 + e; L.skey[p] = key[q][e]; ++p; }
-            }
-            L.staged += tot;
+          for (int e = 0; e < 4; ++e) {
+            if (f[e]) { L.sidx[p] = i0 + e; L.skey[p] = kq[e]; ++p; }
           }
+          L.staged += tot;
         } else {
+          // segment list overflow (or one group denser than the stage): the segment turns DENSE
+          // (select / compact re-read its input range); what was staged is binned, not written
+          if (!dense) L.flush(lane, false, h, lo, hi, shift);
           dense = true;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (f[e]) atomicAdd(&h[fine_bin(kq[e], lo, hi, shift)], 1u);
         }
         run += tot;
       }
     }
   }
   STAMP_W(3);
-  if (!dense) L.flush(lane);
+  if (!dense) L.flush(lane, true, h, lo, hi, shift);
   STAMP_W(4);
   __syncthreads();
   // fold the block's window histogram into copy b % 16 (non-returning atomics; ~B/16 arrivals
@@ -799,8 +807,14 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
   if (phases & 1) {
     DPZ_TIMED(DPZ_KT_TOPK_SAMPLE, a.st, sampled_sample_kernel<<<SMP_BLOCKS, 256, 0, a.st>>>(
         s, a.n, ctrl, chist, ghist, blcnt));
-    DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC><<<nb, 256, 0, a.st>>>(
-        s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey));
+    uint32_t r_lo, r_hi;
+    window_ranks(a.n, a.k, &r_lo, &r_hi);
+    if (a.acc_mode == DPZ_ACC_NONE)
+      DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC, false, FG><<<nb, 256, 0, a.st>>>(
+          s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey));
+    else
+      DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC, true, 1><<<nb, 256, 0, a.st>>>(
+          s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey));
   }
   if (!(phases & 2)) return DPZ_OK;
   s.rekey = 1;
