@@ -26,6 +26,12 @@
 
 namespace dpz {
 
+// x / x0 are streamed once by the filter: non-temporal loads (1) keep them from displacing the
+// step's other working set in L2 / the L3 (filter 29 -> 21 us in the C2 step on MI355X).
+#ifndef DPZ_FILTER_NT
+#define DPZ_FILTER_NT 1
+#endif
+
 // ---- optional timing stamps (debug builds with -DDPZ_STAMPS only; s_memrealtime = 100 MHz) ----
 #ifdef DPZ_STAMPS
 __device__ unsigned long long g_stamps[64];
@@ -188,8 +194,18 @@ __device__ __forceinline__ void load_groups(const KeySrc& s, int64_t base, int64
       const int64_t i0 = base + q * 256 + lane * 4;
       raw[q].cnt = 4;
       if (!rekey) {
+#if DPZ_FILTER_NT
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        const v4f va = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(s.x + i0));
+        raw[q].a = make_float4(va.x, va.y, va.z, va.w);
+        if (s.x0) {
+          const v4f vb = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(s.x0 + i0));
+          raw[q].b = make_float4(vb.x, vb.y, vb.z, vb.w);
+        }
+#else
         raw[q].a = *reinterpret_cast<const float4*>(s.x + i0);
         if (s.x0) raw[q].b = *reinterpret_cast<const float4*>(s.x0 + i0);
+#endif
       }
       if (ACC && s.mode != DPZ_ACC_NONE) raw[q].q = *reinterpret_cast<const float4*>(s.acc + i0);
     }
