@@ -43,6 +43,13 @@ def parse():
                         "round of eval/96_regular.edges sharded over the GPUs")
     p.add_argument("--rotate", type=int, default=None,
                    help="independent node states cycled per step (default: enough for > 2x L3)")
+    p.add_argument("--serial", action="store_true",
+                   help="one stream, each decode consumes the same step's payload (dependent "
+                        "encode -> decode) instead of the pipelined step (decode of the previous "
+                        "step's payload co-scheduled inside the encode)")
+    p.add_argument("--streams", type=int, default=3,
+                   help="S > 1: S independent node codecs share the GPU on S streams (as "
+                        "decentralizepy runs procs_per_machine nodes per machine); 1: one node")
     p.add_argument("--graph", action="store_true",
                    help="replay the steps as a captured hipGraph instead of eager launches (on "
                         "ROCm 7.2 the graph replay measured ~3 us per step slower than eager "
@@ -66,7 +73,8 @@ def timed_loop(fn, reps, stream):
 L3_BYTES = 256 * 2 ** 20  # MI355X Infinity Cache (MI355X_MICROARCH.md § Infinity Cache)
 
 
-def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True, rotate=None):
+def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True, rotate=None,
+             pipeline=True, streams=1):
     """Time `steps` encode+decode steps.  Consecutive steps rotate over R independent node states
     (x, x0, counter, payload, output) so the timed working set is > 2x the 256 MiB Infinity
     Cache: every step streams its inputs from HBM, as a real round does after training."""
@@ -74,6 +82,8 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True, ro
     k = round(alpha * n)
     per_set = 4 * n * 4 + 8 * k          # x, x0, counter, out + payload
     R = rotate or max(1, math.ceil(2 * L3_BYTES / per_set) + 1)
+    if streams > 1:  # a state is only ever reused by the same stream
+        R = -(-R // streams) * streams
     g = torch.Generator(device=dev).manual_seed(seed)
     sets = []
     for _ in range(R):
@@ -97,6 +107,19 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True, ro
         encode(d)
         decode(d)
 
+    # Pipelined step (default): step i encodes node state i and decodes the payload encoded in
+    # step i-1 (node state i-1) — a node's round is exactly this pair of independent operations
+    # (encode its own model, decode a neighbour's payload).  One call (dpz_topk_encode_replace)
+    # runs the decode's chunks in blocks appended to the encoder's latency-bound selection
+    # launches, on one stream.  Every step still does one full encode and one full decode inside
+    # the timed region.  (Two streams instead measured slower on ROCm 7.2: a cross-stream event
+    # wait costs ~15 us, tools/diag/streams_probe.py.)
+    def step_pipe(i):
+        d, p = sets[i % R], sets[(i - 1) % R]
+        codec.topk_encode(d["x"], k, x0=d["x0"], counter=d["counter"], idx_out=d["idx"],
+                          val_out=d["val"], workspace=ws, asynchronous=True,
+                          co_replace=(p["x0"], p["idx"], p["val"], p["out"]))
+
     for i in range(max(warmup, R)):
         step(i)
     fell_back = False
@@ -105,24 +128,39 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True, ro
                                          counter=d["counter"])
     torch.cuda.synchronize()
 
-    def make_graph(m):
-        # m consecutive steps (7 dependent kernels each) captured once and replayed (hipGraph),
-        # so the timed loop is not bound by per-kernel host launch cost; every kernel still runs
-        # every step
+    # Concurrent node codecs (--streams S > 1): step i runs the dependent encode -> decode of
+    # state i on stream i % S with a workspace of its own, so S nodes' codecs share the GPU the
+    # way decentralizepy runs procs_per_machine node processes per machine.  No cross-stream
+    # dependency (state i is reused only S*ceil(R/S) steps later on the same stream).
+    s_list = [torch.cuda.Stream(dev) for _ in range(max(1, streams))]
+    ws_list = [ws] + [codec.Workspace(dev) for _ in range(max(1, streams) - 1)]
+
+    def step_multi(i):
+        q = i % len(s_list)
+        d = sets[i % R]
+        with torch.cuda.stream(s_list[q]):
+            codec.topk_encode(d["x"], k, x0=d["x0"], counter=d["counter"], idx_out=d["idx"],
+                              val_out=d["val"], workspace=ws_list[q], asynchronous=True)
+            codec.replace(d["x0"], d["idx"], d["val"], out=d["out"], workspace=ws_list[q])
+
+    def make_graph(m, fn):
+        # m consecutive steps captured once and replayed (hipGraph), so the timed loop is not
+        # bound by per-kernel host launch cost; every kernel still runs every step
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             for i in range(m):
-                step(i)
+                fn(i)
         return graph
 
     if use_graph:
+        f = step_pipe if pipeline else step
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
-            step(0)
+            f(0)
         torch.cuda.current_stream(dev).wait_stream(side)
-        full = make_graph(R)
-        tail = make_graph(steps % R) if steps % R else None
+        full = make_graph(R, f)
+        tail = make_graph(steps % R, f) if steps % R else None
         torch.cuda.synchronize()
 
         def run_all():
@@ -130,6 +168,18 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True, ro
                 full.replay()
             if tail is not None:
                 tail.replay()
+    elif streams > 1:
+        for i in range(2 * R):
+            step_multi(i)
+        torch.cuda.synchronize()
+
+        def run_all():
+            for i in range(steps):
+                step_multi(i)
+    elif pipeline:
+        def run_all():
+            for i in range(steps):
+                step_pipe(i)
     else:
         def run_all():
             for i in range(steps):
@@ -139,6 +189,7 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True, ro
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run_all()
+    t_host = time.perf_counter() - t0  # host enqueue time (host-bound if close to t)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -149,6 +200,21 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True, ro
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
     s_step = t / steps
+    # the dependent (encode -> decode of the same payload, one stream) step, for reference
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    torch.cuda.synchronize()
+    s_serial = (time.perf_counter() - t0) / steps
+    # one node alone on the GPU, pipelined (decode of the previous payload co-scheduled inside
+    # the encode's latency-bound launches), one stream
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step_pipe(i)
+    torch.cuda.synchronize()
+    s_cosched = (time.perf_counter() - t0) / steps
     # per-stage device time with events on the launch stream
     stream = torch.cuda.current_stream(dev)
     reps = max(2 * R, steps // 2)
@@ -162,14 +228,14 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True, ro
     with codec.KernelTimer() as kt:
         torch.cuda._sleep(int(200e6))  # ~0.1 s of GPU cycles while the steps are enqueued
         for i in range(reps):
-            step(i)
+            step(i)  # kernels alone (no co-scheduled or concurrent work) for the roofline
         torch.cuda.synchronize()
     kernels = {name: {"avg_us": ms / c * 1e3, "launches_per_step": c / reps}
                for name, (ms, c) in kt.result.items()}
     b_enc = 8 * n + 8 * k + 8 * k      # read x, x0; write idx, val; counter[idx] += 1 (r+w)
     b_dec = 8 * n + 8 * k              # read local, payload; write out
     fell_back |= codec.topk_status(ws) != 0  # the timed steps' last encode
-    return dict(n=n, k=k, s_step=s_step, fell_back=fell_back, t_enc=t_enc, t_dec=t_dec,
+    return dict(n=n, k=k, s_step=s_step, s_serial=s_serial, s_cosched=s_cosched, s_host=t_host / steps, fell_back=fell_back, t_enc=t_enc, t_dec=t_dec,
                 b_enc=b_enc, b_dec=b_dec, kernels=kernels, rotate=R,
                 value=world * 4 * n / s_step / 2 ** 30)
 
@@ -301,14 +367,18 @@ def main():
             dist.destroy_process_group()
         return
     r = gpu_case(args.n, args.alpha, dev, 1234 + rank, args.steps, args.warmup, world, dist,
-                 use_graph=args.graph, rotate=args.rotate)
+                 use_graph=args.graph, rotate=args.rotate, pipeline=not args.serial,
+                 streams=args.streams)
     extra = None
     if not args.no_extra and world == 1:
         e = gpu_case(16_777_216, 0.01, dev, 99, max(20, args.steps // 2), args.warmup, 1, None,
-                     use_graph=args.graph)
+                     use_graph=args.graph, pipeline=not args.serial, streams=args.streams)
         extra = {"workload": "north-star target: 64 MiB fp32 tensor (N=16,777,216), 1% top-k",
                  "value": round(e["value"], 2), "ms_per_step": round(e["s_step"] * 1e3, 4),
                  "frac_of_hbm_peak": round((e["b_enc"] + e["b_dec"]) / e["s_step"] / 1e9 / HBM_PEAK_GBS, 4),
+                 "one_node_serial_ms_per_step": round(e["s_serial"] * 1e3, 4),
+                 "one_node_cosched_ms_per_step": round(e["s_cosched"] * 1e3, 4),
+                 "host_enqueue_ms_per_step": round(e["s_host"] * 1e3, 4),
                  "fell_back": e["fell_back"]}
 
     copy_gbs = None
@@ -355,8 +425,15 @@ def main():
             "config": {
                 "workload": "C2: PartialModel top-k encode + decode of one 11M-fp32 flattened tensor",
                 "n": r["n"], "k": r["k"], "alpha": args.alpha,
-                "parallelism": f"{world} independent per-node codecs (one per GPU), no collective",
-                "launch": "hipGraph replay of the whole step" if args.graph else "eager, one stream",
+                "parallelism": (f"{world} GPU(s) x {args.streams} concurrent node codecs (one "
+                                f"stream each), no collective" if args.streams > 1 else
+                                f"{world} GPU(s) x 1 node codec, no collective"),
+                "launch": ("hipGraph replay of the whole step, one stream" if args.graph else
+                           f"eager; step i = dependent encode -> decode of node state i on stream "
+                           f"i % {args.streams}" if args.streams > 1 else
+                           "eager, one stream (encode -> decode of its payload)" if args.serial else
+                           "eager, one stream, pipelined: encode of state i with the decode of "
+                           "state i-1's payload co-scheduled in its selection launches"),
                 "rotated_states": r["rotate"],
             },
             "roofline": {
@@ -377,6 +454,9 @@ def main():
                 "decode": {"avg_us": round(t_dec * 1e6, 3), "alg_bytes": r["b_dec"],
                            "GBps": round(dec_gbs, 1), "frac": round(dec_gbs / HBM_PEAK_GBS, 4)},
                 "step_frac_of_hbm_peak": round(step_gbs / HBM_PEAK_GBS, 4),
+                "one_node_serial_ms_per_step": round(r["s_serial"] * 1e3, 5),
+                "one_node_cosched_ms_per_step": round(r["s_cosched"] * 1e3, 5),
+                "host_enqueue_ms_per_step": round(r["s_host"] * 1e3, 5),
                 "kernels": kern,
                 "torch_copy_GBps_256MiB": copy_gbs,
             },

@@ -38,6 +38,10 @@ SIGNATURES = {
     "dpz_topk_workspace_bytes": (_size, [_i64, _i64]),
     "dpz_topk_encode": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64, _i64,
                                _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size, _int, _c_void_p]),
+    "dpz_topk_encode_replace": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64,
+                                       _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
+                                       _int, _c_void_p, _c_void_p, _c_void_p, _i64, _i64,
+                                       _c_void_p, _c_void_p, _size, _c_void_p]),
     "dpz_topk_complete": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64, _i64,
                                  _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
                                  ctypes.POINTER(_int), _c_void_p]),

@@ -48,13 +48,17 @@ class Workspace:
     def __init__(self, device):
         self.device = torch.device(device)
         self.buf = None
+        self._nk = None
         self.dbuf = None
         self.ebuf = None
 
     def get(self, n, k):
+        if self.buf is not None and self._nk == (n, k):
+            return self.buf
         need = int(_lib.lib().dpz_topk_workspace_bytes(int(n), int(k)))
         if self.buf is None or self.buf.numel() < need:
             self.buf = torch.zeros(max(need, 256), dtype=torch.uint8, device=self.device)
+        self._nk = (n, k)
         return self.buf
 
     def get_decode(self, n, n_payloads):
@@ -72,7 +76,7 @@ class Workspace:
 
 def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, counter=None,
                 idx_out=None, val_out=None, workspace=None, exact=False, asynchronous=False,
-                phase=None):
+                phase=None, co_replace=None):
     """Top-k magnitude encode (reference PartialModel.py:164-255 / Wavelet.py:142-197).
 
     Returns ``(idx int32[k], val fp32[k])`` in ascending index order.  Mutates ``acc`` and
@@ -81,6 +85,10 @@ def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, c
     work; call :func:`topk_complete` with the same arguments before reading the result.
     ``phase="stream"`` / ``"tail"`` split the enqueue in two (both asynchronous; see
     DPZ_TOPK_STREAM in dpz_codec.h) so independent work can overlap the latency-bound tail.
+    ``co_replace=(local, idx, vals, out)`` also performs the independent decode
+    ``replace(local, idx, vals, out=out)`` of a received payload inside the encoder's
+    latency-bound selection launches (dpz_topk_encode_replace); it is complete when the encode's
+    stream work is.
     """
     _require(x, torch.float32, "x")
     _require(x0, torch.float32, "x0")
@@ -99,10 +107,29 @@ def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, c
     flags = (DPZ_TOPK_EXACT if exact else 0) | (DPZ_TOPK_ASYNC if asynchronous else 0)
     if phase is not None:
         flags |= {"stream": DPZ_TOPK_STREAM, "tail": DPZ_TOPK_TAIL}[phase]
-    rc = _lib.lib().dpz_topk_encode(_ptr(x), _ptr(x0), _ptr(acc), int(acc_mode), _ptr(vals_src),
-                                    n, k, _ptr(idx_out), _ptr(val_out), _ptr(counter), _ptr(ws),
-                                    ws.numel(), flags, _stream(x.device))
-    check(rc, "dpz_topk_encode")
+    if co_replace is None:
+        rc = _lib.lib().dpz_topk_encode(_ptr(x), _ptr(x0), _ptr(acc), int(acc_mode),
+                                        _ptr(vals_src), n, k, _ptr(idx_out), _ptr(val_out),
+                                        _ptr(counter), _ptr(ws), ws.numel(), flags,
+                                        _stream(x.device))
+        check(rc, "dpz_topk_encode")
+        return idx_out, val_out
+    if phase is not None:
+        raise ValueError("co_replace cannot be combined with a phase split")
+    r_local, r_idx, r_val, r_out = co_replace
+    _require(r_local, torch.float32, "co_replace local")
+    _require(r_idx, torch.int32, "co_replace idx")
+    _require(r_val, torch.float32, "co_replace vals")
+    _require(r_out, torch.float32, "co_replace out")
+    if r_idx.numel() != r_val.numel() or r_out.numel() != r_local.numel():
+        raise ValueError("co_replace: idx/vals or local/out sizes differ")
+    r_n = r_local.numel()
+    dws = (workspace or Workspace(x.device)).get_decode(r_n, 1)
+    rc = _lib.lib().dpz_topk_encode_replace(
+        _ptr(x), _ptr(x0), _ptr(acc), int(acc_mode), _ptr(vals_src), n, k, _ptr(idx_out),
+        _ptr(val_out), _ptr(counter), _ptr(ws), ws.numel(), flags, _ptr(r_local), _ptr(r_idx),
+        _ptr(r_val), r_idx.numel(), r_n, _ptr(r_out), _ptr(dws), dws.numel(), _stream(x.device))
+    check(rc, "dpz_topk_encode_replace")
     return idx_out, val_out
 
 

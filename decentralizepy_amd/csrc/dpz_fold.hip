@@ -18,6 +18,7 @@
 //    in exactly the reference's fp32 order (library compiled with -ffp-contract=off).
 // Algorithmic bytes: read local (4N) + write out (4N) + 8 bytes per payload entry.
 #include "dpz_common.h"
+#include "dpz_replace.h"
 
 namespace dpz {
 
@@ -173,75 +174,13 @@ __global__ void __launch_bounds__(FOLD_THREADS) fold_kernel(FoldArgs a) {
 static inline int64_t fold_ntiles(int64_t n) { return (n + FOLD_TILE - 1) / FOLD_TILE; }
 
 // Replace-only decode of ONE sparse payload (reference PartialModel.py:257-303, T[idx] = params):
-// block j owns payload entries [64j, 64j + 64) and the element range from its first entry's
-// index to the next block's first entry's index (block 0 from 0, the last block to n) - a
-// contiguous partition of [0, n) known after one load, so no tile-offset pre-pass.  The block
-// copies its range local -> out (float4 body), then scatters its entries' values.
-constexpr int RP_E = 64;
-typedef float v4f __attribute__((ext_vector_type(4)));
-// Non-temporal (streaming) policy of the range copy: 2 = nt loads of local and nt stores of out
-// (measured on MI355X in the encode+decode step: C2 570 -> 606 GiB/s together with the filter's
-// nt loads; the once-touched 4N bytes no longer evict the next kernel's inputs from the L3),
-// 1 = nt stores only, 0 = default policy.
-#ifndef DPZ_REPLACE_NT
-#define DPZ_REPLACE_NT 2
-#endif
+// one 256-thread block per chunk of RP_E payload entries (dpz_replace.h).
+__global__ void __launch_bounds__(256) replace_kernel(ReplaceJob j) { replace_block(j, blockIdx.x); }
 
-__global__ void __launch_bounds__(256) replace_kernel(const float* __restrict__ local,
-                                                      const int32_t* __restrict__ idx,
-                                                      const float* __restrict__ val, int64_t k,
-                                                      int64_t n, float* __restrict__ out) {
-  const int t = threadIdx.x;
-  const int64_t e0 = (int64_t)blockIdx.x * RP_E;
-  const int64_t e1 = (e0 + RP_E < k) ? e0 + RP_E : k;
-  const int64_t a = blockIdx.x == 0 ? 0 : (int64_t)idx[e0];
-  const int64_t b = e1 >= k ? n : (int64_t)idx[e1];
-  int64_t my_i = -1;
-  float my_v = 0.0f;
-  if (t < e1 - e0) {
-    my_i = idx[e0 + t];
-    my_v = val[e0 + t];
-  }
-  if (a < b) {
-    const int64_t a4 = (a + 3) & ~int64_t(3);
-    const int64_t b4 = b & ~int64_t(3);
-    if (a4 < b4) {
-      if (t < a4 - a) out[a + t] = local[a + t];
-      if (t < b - b4) out[b4 + t] = local[b4 + t];
-      const float4* __restrict__ l4 = reinterpret_cast<const float4*>(local);
-      float4* __restrict__ o4 = reinterpret_cast<float4*>(out);
-      const int64_t q0 = a4 >> 2, q1 = b4 >> 2;
-      int64_t q = q0 + t;
-      for (; q + 3 * 256 < q1; q += 4 * 256) {
-#if DPZ_REPLACE_NT >= 2
-        const v4f* lv = reinterpret_cast<const v4f*>(l4);
-        const v4f v0 = __builtin_nontemporal_load(&lv[q]), v1 = __builtin_nontemporal_load(&lv[q + 256]),
-                  v2 = __builtin_nontemporal_load(&lv[q + 512]), v3 = __builtin_nontemporal_load(&lv[q + 768]);
-#else
-        const v4f* lv = reinterpret_cast<const v4f*>(l4);
-        const v4f v0 = lv[q], v1 = lv[q + 256], v2 = lv[q + 512], v3 = lv[q + 768];
-#endif
-#if DPZ_REPLACE_NT >= 1
-        v4f* ov = reinterpret_cast<v4f*>(o4);
-        __builtin_nontemporal_store(v0, &ov[q]);
-        __builtin_nontemporal_store(v1, &ov[q + 256]);
-        __builtin_nontemporal_store(v2, &ov[q + 512]);
-        __builtin_nontemporal_store(v3, &ov[q + 768]);
-#else
-        v4f* ov = reinterpret_cast<v4f*>(o4);
-        ov[q] = v0;
-        ov[q + 256] = v1;
-        ov[q + 512] = v2;
-        ov[q + 768] = v3;
-#endif
-      }
-      for (; q < q1; q += 256) o4[q] = l4[q];
-    } else {
-      for (int64_t i = a + t; i < b; i += 256) out[i] = local[i];
-    }
-  }
-  __syncthreads();  // the range copy is in place before this block's entries overwrite it
-  if (my_i >= 0 && my_i < n) out[my_i] = my_v;
+int launch_replace(const ReplaceJob& j, hipStream_t st) {
+  if (j.c1 > j.c0)
+    DPZ_TIMED(DPZ_KT_FOLD, st, replace_kernel<<<(unsigned)(j.c1 - j.c0), 256, 0, st>>>(j));
+  return DPZ_OK;
 }
 
 }  // namespace dpz
@@ -291,9 +230,8 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
   }
   // one sparse payload, replace only: single-kernel range-partitioned copy + scatter
   if (replace_only && !is_dense(0) && k[0] > 0 && vec) {
-    const unsigned nblk = (unsigned)((k[0] + RP_E - 1) / RP_E);
-    DPZ_TIMED(DPZ_KT_FOLD, st, replace_kernel<<<nblk, 256, 0, st>>>(local, idx[0], vals[0], k[0], n, out));
-    return DPZ_OK;
+    const int64_t nc = replace_chunks(k[0]);
+    return launch_replace(ReplaceJob{local, idx[0], vals[0], k[0], n, out, 0, nc}, st);
   }
   for (int base = 0; base < n_payloads; base += FOLD_MAXP) {
     FoldArgs fa{};

@@ -1,6 +1,7 @@
 // Shared declarations of the top-k encoder (exact + sampled paths). See dpz_topk.hip.
 #pragma once
 #include "dpz_common.h"
+#include "dpz_replace.h"
 
 namespace dpz {
 
@@ -218,6 +219,7 @@ struct EncodeArgs {
   const float* x; const float* x0; float* acc; int acc_mode; const float* vals_src;
   int64_t n, k; int32_t* idx_out; float* val_out; int32_t* counter; char* ws;
   hipStream_t st;
+  const ReplaceJob* job;  // co-scheduled replace decode (sampled path only), or nullptr
 };
 
 // dpz_topk_exact.hip / dpz_topk_sampled.hip

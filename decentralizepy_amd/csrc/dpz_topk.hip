@@ -114,6 +114,52 @@ extern "C" int dpz_topk_encode(const float* x, const float* x0, float* acc, int 
   return dpz_topk_dispatch(a, flags);
 }
 
+static bool overlaps(const void* p, size_t pb, const void* q, size_t qb) {
+  if (!p || !q || pb == 0 || qb == 0) return false;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p), b = reinterpret_cast<uintptr_t>(q);
+  return a < b + qb && b < a + pb;
+}
+
+extern "C" int dpz_topk_encode_replace(const float* x, const float* x0, float* acc, int acc_mode,
+                                       const float* vals_src, int64_t n, int64_t k,
+                                       int32_t* idx_out, float* val_out, int32_t* counter,
+                                       void* ws, size_t ws_bytes, int flags,
+                                       const float* r_local, const int32_t* r_idx,
+                                       const float* r_val, int64_t r_k, int64_t r_n, float* r_out,
+                                       void* r_ws, size_t r_ws_bytes, dpz_stream_t stream) {
+  EncodeArgs a{x, x0, acc, acc_mode, vals_src, n, k, idx_out, val_out, counter,
+               static_cast<char*>(ws), static_cast<hipStream_t>(stream)};
+  int rc = validate(a, ws_bytes);
+  if (rc != DPZ_OK) return rc;
+  if (flags & (DPZ_TOPK_STREAM | DPZ_TOPK_TAIL)) return DPZ_ERR_ARG;
+  if (r_n <= 0 || r_k < 0 || r_k > r_n || !r_local || !r_out) return DPZ_ERR_ARG;
+  if (r_k > 0 && (!r_idx || !r_val)) return DPZ_ERR_ARG;
+  // the replace job is independent work: its output may not overlap anything the encode touches
+  const size_t ob = (size_t)r_n * 4;
+  if (overlaps(r_out, ob, r_local, ob) || overlaps(r_out, ob, x, (size_t)n * 4) ||
+      overlaps(r_out, ob, x0, (size_t)n * 4) || overlaps(r_out, ob, acc, (size_t)n * 4) ||
+      overlaps(r_out, ob, vals_src, (size_t)n * 4) || overlaps(r_out, ob, counter, (size_t)n * 4) ||
+      overlaps(r_out, ob, idx_out, (size_t)k * 4) || overlaps(r_out, ob, val_out, (size_t)k * 4) ||
+      overlaps(r_out, ob, ws, ws_bytes) || overlaps(r_out, ob, r_ws, r_ws_bytes))
+    return DPZ_ERR_ARG;
+  const ReplaceJob job{r_local, r_idx, r_val, r_k, r_n, r_out, 0, replace_chunks(r_k)};
+  const bool r_vec = ((reinterpret_cast<uintptr_t>(r_local) | reinterpret_cast<uintptr_t>(r_out)) & 15u) == 0;
+  const bool carried = n > 0 && k > 0 && r_k > 0 && r_vec && !(flags & DPZ_TOPK_EXACT) &&
+                       use_sampled(n, k);
+  if (!carried) {  // run it on its own first (same stream), then the plain encode
+    const float* vp = r_val;
+    const int32_t* ip = r_idx;
+    const int64_t kk = r_k;
+    rc = dpz_decode_average(r_local, r_n, 1, &ip, &vp, &kk, nullptr, 0.0f, DPZ_FOLD_REPLACE_ONLY,
+                            r_out, r_ws, r_ws_bytes, stream);
+    if (rc != DPZ_OK) return rc;
+    if (n == 0) return DPZ_OK;
+    return dpz_topk_dispatch(a, flags);
+  }
+  a.job = &job;
+  return dpz_topk_dispatch(a, flags);
+}
+
 extern "C" int dpz_topk_complete(const float* x, const float* x0, float* acc, int acc_mode,
                                  const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
                                  float* val_out, int32_t* counter, void* ws, size_t ws_bytes,

@@ -22,6 +22,9 @@
 // A miss (window does not bracket the k-th key / boundary overflow) sets ctrl->status and compact
 // writes nothing; the host then runs the exact path.  A segment whose candidates overflow its
 // list is DENSE and re-reads its input range in select / compact (still exact).
+#include <cstdio>
+#include <cstdlib>
+
 #include "dpz_topk.h"
 
 namespace dpz {
@@ -68,7 +71,11 @@ __device__ __forceinline__ int64_t sample_pos(int c, int lane, int64_t n) {
 // 64 blocks x 256: 1024 chunks of 64 contiguous elements spread evenly over [0, n).
 __global__ void __launch_bounds__(256) sampled_sample_kernel(KeySrc s, int64_t n, TopkCtrl* ctrl,
                                                              uint32_t* chist, uint32_t* ghist,
-                                                             uint32_t* blcnt) {
+                                                             uint32_t* blcnt, ReplaceJob pj) {
+  if (blockIdx.x >= SMP_BLOCKS) {  // co-scheduled replace decode (independent work)
+    replace_block(pj, blockIdx.x - SMP_BLOCKS);
+    return;
+  }
   STAMP_MIN(0);
   __shared__ uint32_t h[CB];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -340,217 +347,6 @@ __device__ __forceinline__ bool wave_bstar(uint4 ghv, uint32_t above, uint32_t k
   return ok;
 }
 
-// One block of 1024 threads: gather the boundary sub-lists and find the pivot, the need-th entry of
-// bin b* in (key descending, index ascending) order; an entry of bin b* is selected iff it is not
-// after the pivot, i.e. key > T or (key == T and idx <= icut) with (T, icut) = the pivot.  One
-// 8-bit digit pass over the offsets inside bin b* (~k/256 entries) leaves a handful in the pivot's
-// digit; if at most 64, one wave ranks them against each other (register broadcasts) and the
-// entry of rank rem - 1 is the pivot — ties cost nothing extra.  Otherwise (heavy ties, wide
-// bins): radix select of T over the remaining digits, then of the tie cut on the index.
-// Then every filter block's output offset (above + selected boundary entries, scanned) and the
-// check that the total is k.  Writes T, icut or a status for the host.
-__global__ void __launch_bounds__(1024) sampled_resolve_kernel(
-    int64_t k, int64_t B, int64_t R4, TopkCtrl* ctrl, const uint32_t* __restrict__ blcnt,
-    const uint32_t* __restrict__ blkey, const uint32_t* __restrict__ blidx,
-    const uint32_t* __restrict__ blkabove, uint32_t* blkoff) {
-  constexpr int PER = BCAP / 1024;
-  constexpr int BPT = (B_MAX + 1023) / 1024;
-  __shared__ uint32_t hist[256];
-  __shared__ uint32_t subbase[NSUB + 1];
-  __shared__ uint32_t wsum[16];
-  __shared__ uint32_t sh[4];
-  __shared__ uint32_t blksel[B_MAX];
-  __shared__ uint2 ent[64];
-  __shared__ uint32_t bcnt;
-  STAMP_T0(12);
-  const int t = threadIdx.x;
-  const uint32_t status = ctrl->status;
-  const uint32_t need = ctrl->need, lo = ctrl->lo, shift = ctrl->shift, bstar = ctrl->bstar;
-  const uint32_t sc = t < NSUB ? blcnt[t] : 0u;
-  uint32_t ba[BPT];
-#pragma unroll
-  for (int q = 0; q < BPT; ++q) {
-    const int64_t fb = (int64_t)t * BPT + q;
-    ba[q] = fb < B ? blkabove[fb] : 0u;
-    if (fb < B_MAX) blksel[fb] = 0;
-  }
-  if (status) return;
-  if (t < 64) {
-    uint32_t tot;
-    const uint32_t ex = wave_excl_scan(sc, &tot);
-    const bool over = __ballot(sc > (uint32_t)SUBCAP) != 0;
-    if (t < NSUB) subbase[t] = ex;
-    if (t == 0) {
-      subbase[NSUB] = tot;
-      sh[3] = over ? 1u : 0u;
-    }
-  }
-  __syncthreads();
-  const uint32_t nb = subbase[NSUB];
-  if (sh[3] || nb > BCAP || need == 0 || need > nb) {
-    if (t == 0) ctrl->status = 1;
-    return;
-  }
-  uint32_t kk[PER], ii[PER];
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const uint32_t j = t + q * 1024;
-    kk[q] = 0u;
-    ii[q] = 0u;
-    if (j < nb) {
-      int sb = 0;
-#pragma unroll
-      for (int u = 1; u < NSUB; ++u) sb += subbase[u] <= j ? 1 : 0;
-      const uint32_t slot = j - subbase[sb];
-      kk[q] = blkey[sb * SUBCAP + slot];
-      ii[q] = blidx[sb * SUBCAP + slot];
-    }
-  }
-  STAMP_T0(13);
-  uint32_t T, icut;
-  // first digit pass (top <= 8 bits of the offset inside bin b*): digit d*, rank left in it, size
-  const uint32_t base = lo + (bstar << shift);
-  const int d1 = shift >= 8 ? 8 : (int)shift;
-  const int low1 = (int)shift - d1;
-  if (t < 256) hist[t] = 0;
-  if (t == 0) bcnt = 0;
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const uint32_t j = t + q * 1024;
-    if (j < nb) atomicAdd(&hist[((kk[q] - base) >> low1) & ((1u << d1) - 1)], 1u);
-  }
-  __syncthreads();
-  {
-    const uint32_t hb = t < 256 ? hist[255 - t] : 0u;  // descending digit 255 - t
-    uint32_t tot;
-    const uint32_t before = block_excl_scan(hb, wsum, &tot);
-    if (t < 256 && before < need && need <= before + hb) {
-      sh[0] = 255 - t;
-      sh[1] = need - before;
-      sh[2] = hb;
-    }
-    __syncthreads();
-  }
-  const uint32_t dstar = sh[0], rem1 = sh[1], eq1 = sh[2];
-  if (eq1 <= 64) {
-    // the pivot is the rem1-th entry of the <= 64 in digit d* (key descending, index ascending):
-    // gather them, one wave ranks each against all (register broadcasts, no LDS round trips)
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const uint32_t j = t + q * 1024;
-      if (j < nb && (((kk[q] - base) >> low1) & ((1u << d1) - 1)) == dstar)
-        ent[atomicAdd(&bcnt, 1u)] = make_uint2(kk[q], ii[q]);
-    }
-    __syncthreads();
-    if (t < 64) {
-      const uint2 me = t < (int)eq1 ? ent[t] : make_uint2(0u, 0xFFFFFFFFu);
-      uint32_t rank = 0;
-      for (uint32_t f = 0; f < eq1; ++f) {
-        const uint32_t ok = __builtin_amdgcn_readlane(me.x, f);
-        const uint32_t oi = __builtin_amdgcn_readlane(me.y, f);
-        rank += (ok > me.x || (ok == me.x && oi < me.y)) ? 1u : 0u;
-      }
-      if (t < (int)eq1 && rank == rem1 - 1) {
-        sh[0] = me.x;
-        sh[1] = me.y;
-      }
-    }
-    __syncthreads();
-    T = sh[0];
-    icut = sh[1];
-  } else {
-    uint32_t prefix = 0, rem = need, eqcnt = nb;
-    for (int top = (int)shift; top > 0; top -= 8) {
-      const int d = top >= 8 ? 8 : top;
-      const int low = top - d;
-      if (t < 256) hist[t] = 0;
-      __syncthreads();
-#pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const uint32_t j = t + q * 1024;
-        if (j < nb) {
-          const uint32_t o = kk[q] - base;
-          if ((uint32_t)((uint64_t)o >> top) == (uint32_t)((uint64_t)prefix >> top))
-            atomicAdd(&hist[(o >> low) & ((1u << d) - 1)], 1u);
-        }
-      }
-      __syncthreads();
-      const uint32_t hb = t < 256 ? hist[255 - t] : 0u;  // descending digit 255 - t
-      uint32_t tot;
-      const uint32_t before = block_excl_scan(hb, wsum, &tot);
-      if (t < 256 && before < rem && rem <= before + hb) {
-        sh[0] = 255 - t;
-        sh[1] = rem - before;
-        sh[2] = hb;
-      }
-      __syncthreads();
-      prefix |= sh[0] << low;
-      rem = sh[1];
-      eqcnt = sh[2];
-      __syncthreads();
-    }
-    T = base + prefix;
-    icut = 0xFFFFFFFFu;
-    if (rem < eqcnt) {
-      uint32_t ipre = 0, irem = rem;
-      for (int top = 32; top > 0; top -= 8) {
-        const int low = top - 8;
-        if (t < 256) hist[t] = 0;
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < PER; ++q) {
-          const uint32_t j = t + q * 1024;
-          if (j < nb && kk[q] == T && (top == 32 || (ii[q] >> top) == (ipre >> top)))
-            atomicAdd(&hist[(ii[q] >> low) & 255u], 1u);
-        }
-        __syncthreads();
-        const uint32_t hb = t < 256 ? hist[t] : 0u;  // ascending digit t
-        uint32_t tot;
-        const uint32_t before = block_excl_scan(hb, wsum, &tot);
-        if (t < 256 && before < irem && irem <= before + hb) {
-          sh[0] = t;
-          sh[1] = irem - before;
-        }
-        __syncthreads();
-        ipre |= sh[0] << low;
-        irem = sh[1];
-        __syncthreads();
-      }
-      icut = ipre;
-    }
-  }
-  STAMP_T0(14);
-  // every filter block's output offset: above counts + selected boundary entries, scanned
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const uint32_t j = t + q * 1024;
-    if (j < nb && (kk[q] > T || (kk[q] == T && ii[q] <= icut)))
-      atomicAdd(&blksel[ii[q] / (uint32_t)R4], 1u);
-  }
-  __syncthreads();
-  uint32_t v[BPT], local = 0;
-#pragma unroll
-  for (int q = 0; q < BPT; ++q) {
-    const int64_t fb = (int64_t)t * BPT + q;
-    v[q] = fb < B ? ba[q] + blksel[fb] : 0u;
-    local += v[q];
-  }
-  uint32_t tot;
-  uint32_t ex = block_excl_scan(local, wsum, &tot);
-#pragma unroll
-  for (int q = 0; q < BPT; ++q) {
-    const int64_t fb = (int64_t)t * BPT + q;
-    if (fb < B) blkoff[fb] = ex;
-    ex += v[q];
-  }
-  if (t == 0) {
-    ctrl->T = T;
-    ctrl->icut = icut;
-    if (tot != (uint32_t)k) ctrl->status = 2;  // internal inconsistency: compact writes nothing
-  }
-}
-
 // ceil(W/32) blocks x 1024 (16 waves x 2 wave segments).  Sums the 16 window-histogram copies,
 // finds the threshold bin b* (wave 0), counts each filter block's candidates above b*
 // (blkabove) and appends the bin-b* entries, staged in LDS, to sub-list (block % 16) with one
@@ -560,7 +356,14 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
     KeySrc s, int64_t n, int64_t k, int64_t W, int64_t B, int64_t R, int64_t CAP, TopkCtrl* ctrl,
     const uint32_t* __restrict__ ghist, const uint32_t* __restrict__ segcnt,
     const uint32_t* __restrict__ cidx, const uint32_t* __restrict__ ckey, uint32_t* blkabove,
-    uint32_t* blcnt, uint32_t* blkey, uint32_t* blidx) {
+    uint32_t* blcnt, uint32_t* blkey, uint32_t* blidx, ReplaceJob pj) {
+  {
+    const int64_t own = (W + SEL_SEGS - 1) / SEL_SEGS;
+    if ((int64_t)blockIdx.x >= own) {  // co-scheduled replace decode
+      replace_block(pj, (int64_t)blockIdx.x - own);
+      return;
+    }
+  }
   STAMP_MIN(6);
   STAMP_T0(8);
   __shared__ __attribute__((aligned(16))) uint32_t gh[GH_STRIDE];
@@ -657,7 +460,7 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
   __syncthreads();
   if (t < SEL_SEGS / 4) {
     const int64_t fb = (int64_t)blockIdx.x * (SEL_SEGS / 4) + t;
-    if (fb < B) blkabove[fb] = fbabove[t];
+    blkabove[fb] = fb < B ? fbabove[t] : 0u;  // zero-padded to a multiple of 8 (compact)
   }
   STAMP_T0(10);
   const uint32_t nl = lcnt;
@@ -677,23 +480,306 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
   STAMP_T0(11);
 }
 
-// One block of 256 threads per filter block (4 wave segments): output offset from resolve, then
-// per wave a count pass, in-block wave offsets, and the ordered write of the selected
-// (idx, vals_src[idx]) with counter / rewind updates.  Block 0 re-zeroes the sample histogram.
+// Boundary entry j (0 <= j < nb) of the 16 sub-lists: sub-list sb with subbase[sb] <= j.
+__device__ __forceinline__ uint32_t bound_slot(const uint32_t* subbase, uint32_t j) {
+  int sb = 0;
+#pragma unroll
+  for (int u = 1; u < NSUB; ++u) sb += subbase[u] <= j ? 1 : 0;
+  return (uint32_t)sb * SUBCAP + (j - subbase[sb]);
+}
+
+// 256-thread block: the exact threshold key T and tie cut icut inside bin b* from the boundary
+// sub-lists — the pivot is the need-th entry of bin b* in (key descending, index ascending)
+// order; an entry of bin b* is selected iff it is not after the pivot (key > T, or key == T and
+// idx <= icut).  One 8-bit digit pass over the offsets inside bin b* (~k/256 entries) leaves a
+// handful in the pivot's digit; if at most 64, one wave ranks them against each other (register
+// broadcasts) and the entry of rank rem - 1 is the pivot (ties cost nothing extra).  Otherwise
+// (heavy ties, wide bins) radix select of T over the remaining digits, then of the tie cut on the
+// index.  The first BLDS entries are staged in LDS, the rest are re-read (L2).
+constexpr int BLDS = 1024;
+struct Bound {
+  const uint32_t* key;
+  const uint32_t* idx;
+  const uint32_t* subbase;  // LDS
+  uint32_t* sk;             // LDS [BLDS]
+  uint32_t* si;             // LDS [BLDS]
+  uint32_t nb;
+  __device__ __forceinline__ void load() {
+    uint32_t kk[BLDS / 256], ii[BLDS / 256];
+#pragma unroll
+    for (int q = 0; q < BLDS / 256; ++q) {
+      const uint32_t j = threadIdx.x + q * 256u;
+      if (j < nb) {
+        const uint32_t sl = bound_slot(subbase, j);
+        kk[q] = key[sl];
+        ii[q] = idx[sl];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < BLDS / 256; ++q) {
+      const uint32_t j = threadIdx.x + q * 256u;
+      if (j < nb) {
+        sk[j] = kk[q];
+        si[j] = ii[q];
+      }
+    }
+    __syncthreads();
+  }
+  // f(key, idx) for every entry of this thread
+  template <class F>
+  __device__ __forceinline__ void each(F f) const {
+    const uint32_t m = nb < (uint32_t)BLDS ? nb : (uint32_t)BLDS;
+    for (uint32_t j = threadIdx.x; j < m; j += 256u) f(sk[j], si[j]);
+    for (uint32_t j = threadIdx.x + BLDS; j < nb; j += 256u) {
+      const uint32_t sl = bound_slot(subbase, j);
+      f(key[sl], idx[sl]);
+    }
+  }
+};
+
+struct ResolveLds {
+  uint32_t hist[256];
+  uint32_t wsum[16];
+  uint32_t sh[4];
+  uint2 ent[64];
+  uint32_t bcnt;
+};
+
+__device__ __forceinline__ void block_resolve(const Bound& bd, uint32_t need, uint32_t base,
+                                              uint32_t shift, ResolveLds& L, uint32_t* T_out,
+                                              uint32_t* icut_out) {
+  const int t = threadIdx.x;
+  const int d1 = shift >= 8 ? 8 : (int)shift;
+  const int low1 = (int)shift - d1;
+  const uint32_t m1 = (1u << d1) - 1u;
+  L.hist[t] = 0;
+  if (t == 0) L.bcnt = 0;
+  __syncthreads();
+  bd.each([&](uint32_t kv, uint32_t) { atomicAdd(&L.hist[((kv - base) >> low1) & m1], 1u); });
+  __syncthreads();
+  {
+    const uint32_t hb = L.hist[255 - t];  // descending digit 255 - t
+    uint32_t tot;
+    const uint32_t before = block_excl_scan(hb, L.wsum, &tot);
+    if (before < need && need <= before + hb) {
+      L.sh[0] = 255 - t;
+      L.sh[1] = need - before;
+      L.sh[2] = hb;
+    }
+    __syncthreads();
+  }
+  const uint32_t dstar = L.sh[0], rem1 = L.sh[1], eq1 = L.sh[2];
+  __syncthreads();
+  if (eq1 <= 64) {
+    bd.each([&](uint32_t kv, uint32_t iv) {
+      if ((((kv - base) >> low1) & m1) == dstar) L.ent[atomicAdd(&L.bcnt, 1u)] = make_uint2(kv, iv);
+    });
+    __syncthreads();
+    if (t < 64) {
+      const uint2 me = t < (int)eq1 ? L.ent[t] : make_uint2(0u, 0xFFFFFFFFu);
+      uint32_t rank = 0;
+      for (uint32_t f = 0; f < eq1; ++f) {
+        const uint32_t ok = __builtin_amdgcn_readlane(me.x, f);
+        const uint32_t oi = __builtin_amdgcn_readlane(me.y, f);
+        rank += (ok > me.x || (ok == me.x && oi < me.y)) ? 1u : 0u;
+      }
+      if (t < (int)eq1 && rank == rem1 - 1) {
+        L.sh[0] = me.x;
+        L.sh[1] = me.y;
+      }
+    }
+    __syncthreads();
+    *T_out = L.sh[0];
+    *icut_out = L.sh[1];
+    __syncthreads();
+    return;
+  }
+  uint32_t prefix = 0, rem = need, eqcnt = bd.nb;
+  for (int top = (int)shift; top > 0; top -= 8) {
+    const int d = top >= 8 ? 8 : top;
+    const int low = top - d;
+    L.hist[t] = 0;
+    __syncthreads();
+    bd.each([&](uint32_t kv, uint32_t) {
+      const uint32_t o = kv - base;
+      if ((uint32_t)((uint64_t)o >> top) == (uint32_t)((uint64_t)prefix >> top))
+        atomicAdd(&L.hist[(o >> low) & ((1u << d) - 1)], 1u);
+    });
+    __syncthreads();
+    const uint32_t hb = L.hist[255 - t];
+    uint32_t tot;
+    const uint32_t before = block_excl_scan(hb, L.wsum, &tot);
+    if (before < rem && rem <= before + hb) {
+      L.sh[0] = 255 - t;
+      L.sh[1] = rem - before;
+      L.sh[2] = hb;
+    }
+    __syncthreads();
+    prefix |= L.sh[0] << low;
+    rem = L.sh[1];
+    eqcnt = L.sh[2];
+    __syncthreads();
+  }
+  const uint32_t T = base + prefix;
+  uint32_t icut = 0xFFFFFFFFu;
+  if (rem < eqcnt) {
+    uint32_t ipre = 0, irem = rem;
+    for (int top = 32; top > 0; top -= 8) {
+      const int low = top - 8;
+      L.hist[t] = 0;
+      __syncthreads();
+      bd.each([&](uint32_t kv, uint32_t iv) {
+        if (kv == T && (top == 32 || (iv >> top) == (ipre >> top)))
+          atomicAdd(&L.hist[(iv >> low) & 255u], 1u);
+      });
+      __syncthreads();
+      const uint32_t hb = L.hist[t];  // ascending digit t
+      uint32_t tot;
+      const uint32_t before = block_excl_scan(hb, L.wsum, &tot);
+      if (before < irem && irem <= before + hb) {
+        L.sh[0] = t;
+        L.sh[1] = irem - before;
+      }
+      __syncthreads();
+      ipre |= L.sh[0] << low;
+      irem = L.sh[1];
+      __syncthreads();
+    }
+    icut = ipre;
+  }
+  *T_out = T;
+  *icut_out = icut;
+}
+
+// Sum over the block of a pair of counters (each < 2^32), packed in 64 bits.
+__device__ __forceinline__ uint64_t block_sum64(uint64_t v, uint64_t* wsum64) {
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  if (lane == 0) wsum64[wid] = v;
+  __syncthreads();
+  uint64_t tot = 0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += wsum64[w];
+  __syncthreads();
+  return tot;
+}
+
+// DENSE segments (candidate list overflowed in the filter) re-read their input range: rare, kept
+// out of line so the common path's register budget is not sized for it.
+template <bool VEC>
+__device__ __forceinline__ uint32_t dense_count(const KeySrc s, int64_t seg, int64_t R,
+                                                          int64_t n, uint32_t lo, uint32_t T,
+                                                          uint32_t icut) {
+  const int lane = threadIdx.x & 63;
+  const int64_t beg = seg * R;
+  const int64_t end = (beg + R < n) ? beg + R : n;
+  uint32_t mine = 0;
+  for (int64_t i0 = beg + lane * 4; i0 - lane * 4 < end; i0 += 256) {
+    uint32_t key[4];
+    const int c = i0 < end ? load_keys4<VEC>(s, i0, end, false, key) : 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool f = e < c && key[e] >= lo &&
+                     (key[e] > T || (key[e] == T && (uint32_t)(i0 + e) <= icut));
+      mine += (uint32_t)__popcll(__ballot(f));
+    }
+  }
+  return mine;
+}
+
+template <bool VEC>
+__device__ __forceinline__ void dense_write(const KeySrc s, int64_t seg, int64_t R,
+                                                      int64_t n, int64_t k, uint32_t lo,
+                                                      uint32_t T, uint32_t icut, uint32_t run,
+                                                      const float* vals_src, int32_t* idx_out,
+                                                      float* val_out, int32_t* counter,
+                                                      float* rewind) {
+  const int lane = threadIdx.x & 63;
+  const int64_t beg = seg * R;
+  const int64_t end = (beg + R < n) ? beg + R : n;
+  for (int64_t i0 = beg + lane * 4; i0 - lane * 4 < end; i0 += 256) {
+    uint32_t key[4];
+    const int c = i0 < end ? load_keys4<VEC>(s, i0, end, false, key) : 0;
+    bool f[4];
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      f[e] = e < c && key[e] >= lo &&
+             (key[e] > T || (key[e] == T && (uint32_t)(i0 + e) <= icut));
+      const uint64_t m = __ballot(f[e]);
+      pre += mbcnt64(m);
+      tot += (uint32_t)__popcll(m);
+    }
+    uint32_t pos = run + pre;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (f[e]) {
+        if (pos < (uint64_t)k) {
+          const int64_t i = i0 + e;
+          idx_out[pos] = (int32_t)i;
+          val_out[pos] = vals_src[i];
+          if (counter) atomicAdd(&counter[i], 1);
+          if (rewind) rewind[i] = 0.0f;
+        }
+        ++pos;
+      }
+    }
+    run += tot;
+  }
+}
+
+// One block of 256 threads per filter block (4 wave segments).  Prologue, redundantly in every
+// block (no single-block launch in between — a launch boundary plus a one-CU kernel cost more
+// than the ~15 KB of L2 reads per block): the exact T / icut from the boundary sub-lists, the
+// block's output offset = above-b* counts of the earlier filter blocks + selected boundary
+// entries before the block, and the check that the grand total is k.  Then per wave a count
+// pass, in-block wave offsets, and the ordered write of (idx, vals_src[idx]) with counter /
+// rewind updates.  Block 0 re-zeroes the sample histogram and publishes T / icut / status.
 template <bool VEC>
 __global__ void __launch_bounds__(256, 8) sampled_compact_kernel(
-    KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, const TopkCtrl* ctrl,
-    uint32_t* chist, const uint32_t* __restrict__ blkoff, const uint32_t* __restrict__ segcnt,
-    const uint32_t* __restrict__ cidx, const uint32_t* __restrict__ ckey, const float* vals_src,
-    int32_t* idx_out, float* val_out, int32_t* counter, float* rewind) {
+    KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl,
+    uint32_t* chist, const uint32_t* __restrict__ blkabove, const uint32_t* __restrict__ blcnt,
+    const uint32_t* __restrict__ blkey, const uint32_t* __restrict__ blidx,
+    const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ cidx,
+    const uint32_t* __restrict__ ckey, const float* vals_src, int32_t* idx_out, float* val_out,
+    int32_t* counter, float* rewind, ReplaceJob pj) {
   __shared__ uint32_t wcnt[4];
+  __shared__ uint32_t subbase[NSUB + 1];
+  __shared__ uint32_t flag;
+  __shared__ uint64_t wsum64[4];
+  __shared__ ResolveLds RL;
+  __shared__ uint32_t bsk[BLDS], bsi[BLDS];
+  const int64_t B = (W + 3) / 4;
+  if ((int64_t)blockIdx.x >= B) {  // co-scheduled replace decode
+    replace_block(pj, (int64_t)blockIdx.x - B);
+    return;
+  }
   STAMP_T0(0);
   const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
   const int64_t seg = (int64_t)blockIdx.x * 4 + wid;
+  // every independent load first: control words, sub-list counts, above counts, own candidates
   const uint32_t status = ctrl->status;
-  const uint32_t lo = ctrl->lo, T = ctrl->T, icut = ctrl->icut;
+  const uint32_t need = ctrl->need, lo = ctrl->lo, shift = ctrl->shift, bstar = ctrl->bstar;
+  const uint32_t sc = t < NSUB ? blcnt[t] : 0u;
+  static_assert(B_MAX <= 256 * 8, "above counts: 8 per thread");
+  uint32_t abv_before = 0, abv_all = 0;
+  {
+    // blkabove holds B entries, zero-padded to a multiple of 8 by select (ws is 256-B aligned)
+    const uint32_t fb0 = (uint32_t)t * 8u;
+    uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+    if ((int64_t)fb0 < B) {
+      v0 = reinterpret_cast<const uint4*>(blkabove)[2 * t];
+      v1 = reinterpret_cast<const uint4*>(blkabove)[2 * t + 1];
+    }
+    const uint32_t v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    const uint32_t bx = blockIdx.x;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      abv_all += v[q];
+      abv_before += fb0 + q < bx ? v[q] : 0u;
+    }
+  }
   const uint32_t cnt = seg < W ? segcnt[seg] : 0u;
-  const uint32_t boff = blkoff[blockIdx.x];
   const bool dense = cnt == DENSE;
   uint32_t key0 = 0, idx0 = 0;
   if (seg < W && !dense && (uint32_t)lane < cnt) {
@@ -703,8 +789,45 @@ __global__ void __launch_bounds__(256, 8) sampled_compact_kernel(
   if (blockIdx.x == 0) {  // leave the sample histogram zeroed for the next call
     for (int b = t; b < CB; b += 256) chist[b] = 0;
   }
-  if (status) return;
+  if (status) return;  // select reported a miss: the host runs the exact path
+  if (t < 64) {
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan(sc, &tot);
+    const bool over = __ballot(sc > (uint32_t)SUBCAP) != 0;
+    if (t < NSUB) subbase[t] = ex;
+    if (t == 0) {
+      subbase[NSUB] = tot;
+      flag = (over || tot > (uint32_t)BCAP || need == 0 || need > tot) ? 1u : 0u;
+    }
+  }
+  __syncthreads();
+  if (flag) {  // identical in every block
+    if (blockIdx.x == 0 && t == 0) ctrl->status = 1;
+    return;
+  }
   STAMP_T0(1);
+  Bound bd{blkey, blidx, subbase, bsk, bsi, subbase[NSUB]};
+  bd.load();
+  uint32_t T, icut;
+  block_resolve(bd, need, lo + (bstar << shift), shift, RL, &T, &icut);
+  STAMP_T0(2);
+  // selected boundary entries before this block / overall, plus the above counts
+  const uint32_t bstart = (uint32_t)((int64_t)blockIdx.x * 4 * R);
+  uint32_t sb_before = 0, sb_all = 0;
+  bd.each([&](uint32_t kv, uint32_t iv) {
+    const bool sel = kv > T || (kv == T && iv <= icut);
+    sb_all += sel ? 1u : 0u;
+    sb_before += (sel && iv < bstart) ? 1u : 0u;
+  });
+  const uint64_t tot2 = block_sum64(((uint64_t)(abv_all + sb_all) << 32) |
+                                        (uint64_t)(abv_before + sb_before), wsum64);
+  const uint32_t boff = (uint32_t)tot2, grand = (uint32_t)(tot2 >> 32);
+  if (blockIdx.x == 0 && t == 0) {
+    ctrl->T = T;
+    ctrl->icut = icut;
+    if (grand != (uint32_t)k) ctrl->status = 2;  // internal inconsistency
+  }
+  if (grand != (uint32_t)k) return;  // identical in every block: nothing is written
   // count pass (first 64 list entries stay in registers), wave offsets, write pass
   uint32_t mine = 0;
   bool sel0 = false;
@@ -722,22 +845,11 @@ __global__ void __launch_bounds__(256, 8) sampled_compact_kernel(
       mine += (uint32_t)__popcll(__ballot(sel));
     }
   } else if (seg < W) {
-    const int64_t beg = seg * R;
-    const int64_t end = (beg + R < n) ? beg + R : n;
-    for (int64_t i0 = beg + lane * 4; i0 - lane * 4 < end; i0 += 256) {
-      uint32_t key[4];
-      const int c = i0 < end ? load_keys4<VEC>(s, i0, end, false, key) : 0;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bool f = e < c && key[e] >= lo &&
-                       (key[e] > T || (key[e] == T && (uint32_t)(i0 + e) <= icut));
-        mine += (uint32_t)__popcll(__ballot(f));
-      }
-    }
+    mine = dense_count<VEC>(s, seg, R, n, lo, T, icut);
   }
   if (lane == 0) wcnt[wid] = mine;
   __syncthreads();
-  STAMP_T0(2);
+  STAMP_T0(3);
   uint32_t run = boff;
   for (int w = 0; w < wid; ++w) run += wcnt[w];
   if (seg >= W) return;
@@ -748,7 +860,7 @@ __global__ void __launch_bounds__(256, 8) sampled_compact_kernel(
       if (pos < (uint64_t)k) {
         idx_out[pos] = (int32_t)idx;
         val_out[pos] = vals_src[idx];
-        if (counter) counter[idx] += 1;
+        if (counter) atomicAdd(&counter[idx], 1);  // non-returning: no round trip to wait on
         if (rewind) rewind[idx] = 0.0f;
       }
     }
@@ -768,39 +880,26 @@ __global__ void __launch_bounds__(256, 8) sampled_compact_kernel(
       emit(sel, idx);
     }
   } else {
-    const int64_t beg = seg * R;
-    const int64_t end = (beg + R < n) ? beg + R : n;
-    for (int64_t i0 = beg + lane * 4; i0 - lane * 4 < end; i0 += 256) {
-      uint32_t key[4];
-      const int c = i0 < end ? load_keys4<VEC>(s, i0, end, false, key) : 0;
-      bool f[4];
-      uint32_t pre = 0, tot = 0;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        f[e] = e < c && key[e] >= lo &&
-               (key[e] > T || (key[e] == T && (uint32_t)(i0 + e) <= icut));
-        const uint64_t m = __ballot(f[e]);
-        pre += mbcnt64(m);
-        tot += (uint32_t)__popcll(m);
-      }
-      uint32_t pos = run + pre;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (f[e]) {
-          if (pos < (uint64_t)k) {
-            const int64_t i = i0 + e;
-            idx_out[pos] = (int32_t)i;
-            val_out[pos] = vals_src[i];
-            if (counter) counter[i] += 1;
-            if (rewind) rewind[i] = 0.0f;
-          }
-          ++pos;
-        }
-      }
-      run += tot;
+    dense_write<VEC>(s, seg, R, n, k, lo, T, icut, run, vals_src, idx_out, val_out, counter,
+                     rewind);
+  }
+  STAMP_T0(4);
+}
+
+// Fractions of a co-scheduled replace job's chunks carried by sample / select / compact;
+// DPZ_COSCHED="f0,f1,f2" overrides (read per call: a tuning knob, no global state).
+// Defaults measured on MI355X, see DESIGN.md §3.6.
+static void cosched_shares(double f[3]) {
+  f[0] = 0.45; f[1] = 0.55; f[2] = 0.0;
+  if (const char* e = getenv("DPZ_COSCHED")) {
+    double v[3];
+    if (sscanf(e, "%lf,%lf,%lf", &v[0], &v[1], &v[2]) == 3 && v[0] >= 0 && v[1] >= 0 &&
+        v[2] >= 0) {
+      const double t = v[0] + v[1] + v[2];
+      if (t > 0)
+        for (int i = 0; i < 3; ++i) f[i] = v[i] / t;
     }
   }
-  STAMP_T0(3);
 }
 
 template <bool VEC>
@@ -811,7 +910,6 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
   uint32_t* ghist = reinterpret_cast<uint32_t*>(a.ws + L.f_ghist);
   uint32_t* segcnt = reinterpret_cast<uint32_t*>(a.ws + L.f_segcnt);
   uint32_t* blkabove = reinterpret_cast<uint32_t*>(a.ws + L.f_blkabove);
-  uint32_t* blkoff = reinterpret_cast<uint32_t*>(a.ws + L.f_blkoff);
   uint32_t* cidx = reinterpret_cast<uint32_t*>(a.ws + L.f_cidx);
   uint32_t* ckey = reinterpret_cast<uint32_t*>(a.ws + L.f_ckey);
   uint32_t* blcnt = reinterpret_cast<uint32_t*>(a.ws + L.f_blcnt);
@@ -820,9 +918,32 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
   const FastGeom& g = L.fg;
   const unsigned nb = (unsigned)g.B;
   const unsigned nsel = (unsigned)((g.W + SEL_SEGS - 1) / SEL_SEGS);
+  // co-scheduled replace decode: its chunks are split over the four latency-bound launches
+  // (sample, select, resolve, compact) and run in blocks appended after each launch's own
+  ReplaceJob jb[3] = {};
+  unsigned pb[3] = {0, 0, 0};
+  if (a.job && phases == 3) {
+    const int64_t C = a.job->c1 - a.job->c0;
+    double f[3];
+    cosched_shares(f);
+    const int per[3] = {1, 4, 1};  // chunks per appended block (256- / 1024-thread blocks)
+    int64_t c = a.job->c0;
+    double acc_f = 0.0;
+    for (int i = 0; i < 3; ++i) {
+      acc_f += f[i];
+      int64_t e = (i == 2) ? a.job->c1 : a.job->c0 + (int64_t)(acc_f * (double)C + 0.5);
+      if (e > a.job->c1) e = a.job->c1;
+      if (e < c) e = c;
+      jb[i] = *a.job;
+      jb[i].c0 = c;
+      jb[i].c1 = e;
+      pb[i] = (unsigned)((e - c + per[i] - 1) / per[i]);
+      c = e;
+    }
+  }
   if (phases & 1) {
-    DPZ_TIMED(DPZ_KT_TOPK_SAMPLE, a.st, sampled_sample_kernel<<<SMP_BLOCKS, 256, 0, a.st>>>(
-        s, a.n, ctrl, chist, ghist, blcnt));
+    DPZ_TIMED(DPZ_KT_TOPK_SAMPLE, a.st, sampled_sample_kernel<<<SMP_BLOCKS + pb[0], 256, 0, a.st>>>(
+        s, a.n, ctrl, chist, ghist, blcnt, jb[0]));
     uint32_t r_lo, r_hi;
     window_ranks(a.n, a.k, &r_lo, &r_hi);
     if (a.acc_mode == DPZ_ACC_NONE)
@@ -834,15 +955,13 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
   }
   if (!(phases & 2)) return DPZ_OK;
   s.rekey = 1;
-  DPZ_TIMED(DPZ_KT_TOPK_SELECT, a.st, sampled_select_kernel<VEC><<<nsel, 1024, 0, a.st>>>(
+  DPZ_TIMED(DPZ_KT_TOPK_SELECT, a.st, sampled_select_kernel<VEC><<<nsel + pb[1], 1024, 0, a.st>>>(
       s, a.n, a.k, g.W, g.B, g.R, g.CAP, ctrl, ghist, segcnt, cidx, ckey, blkabove, blcnt, blkey,
-      blidx));
-  DPZ_TIMED(DPZ_KT_TOPK_RESOLVE, a.st, sampled_resolve_kernel<<<1, 1024, 0, a.st>>>(
-      a.k, g.B, 4 * g.R, ctrl, blcnt, blkey, blidx, blkabove, blkoff));
+      blidx, jb[1]));
   float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE) ? a.acc : nullptr;
-  DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC><<<nb, 256, 0, a.st>>>(
-      s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkoff, segcnt, cidx, ckey, a.vals_src,
-      a.idx_out, a.val_out, a.counter, rewind));
+  DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC><<<nb + pb[2], 256, 0, a.st>>>(
+      s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, cidx,
+      ckey, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, jb[2]));
   return DPZ_OK;
 }
 

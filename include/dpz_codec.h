@@ -77,6 +77,23 @@ int dpz_topk_encode(const float* x, const float* x0, float* acc, int acc_mode,
                     const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
                     float* val_out, int32_t* counter, void* ws, size_t ws_bytes, int flags,
                     dpz_stream_t stream);
+/* Top-k encode (exactly dpz_topk_encode with the same arguments) TOGETHER WITH one independent
+ * replace decode (exactly dpz_decode_average(r_local, r_n, 1, &r_idx, &r_val, &r_k, NULL, 0,
+ * DPZ_FOLD_REPLACE_ONLY, r_out, r_ws, r_ws_bytes) — reference sharing/PartialModel.py:257-303,
+ * `T[idx] = params` on a neighbour's payload).  A node's round does both (encode its own model,
+ * decode a received payload); on the sampled path the decode's chunks run in blocks appended to
+ * the encoder's four latency-bound selection launches, so its HBM streaming fills the CUs those
+ * leave idle (a cross-stream event wait costs ~15 us on ROCm 7.2, measured, so a second stream
+ * does not pay).  Otherwise the decode is enqueued first on `stream`, then the encode.
+ * r_out may not overlap r_local or any buffer of the encode (DPZ_ERR_ARG).  The decode is
+ * complete when the encode's stream work is (DPZ_TOPK_ASYNC applies to both); the STREAM / TAIL
+ * phase flags are not accepted.  r_ws: the decode workspace (only used when not carried).      */
+int dpz_topk_encode_replace(const float* x, const float* x0, float* acc, int acc_mode,
+                            const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
+                            float* val_out, int32_t* counter, void* ws, size_t ws_bytes, int flags,
+                            const float* r_local, const int32_t* r_idx, const float* r_val,
+                            int64_t r_k, int64_t r_n, float* r_out, void* r_ws, size_t r_ws_bytes,
+                            dpz_stream_t stream);
 /* Completes a DPZ_TOPK_ASYNC encode issued with the SAME arguments: synchronises `stream`,
  * and if the sampled path reported a miss, re-runs the selection exactly (blocking).
  * *used_fallback (host, may be NULL) is set to 1 when that happened.                         */

@@ -353,3 +353,52 @@ def test_split_stream_tail_enqueue(dev, n, alpha):
     want = x0.copy()
     want[5] = 1.5
     np.testing.assert_array_equal(_bits(other.cpu().numpy()), _bits(want))
+
+
+@pytest.mark.parametrize("n,alpha,rn,rk,shares", [
+    (11_000_000, 0.01, 11_000_000, 110_000, None),          # C2: the bench's pipelined step
+    (16_777_216, 0.01, 1_000_003, 10_000, None),            # different sizes of the two jobs
+    (1_000_003, 0.01, 16_777_216, 167_772, "1,0,0"),      # everything in one host launch
+    (1_000_003, 0.01, 4_000_000, 40_000, "0,0,1"),
+    (1_000_003, 0.01, 4_000_000, 40_000, "0,1,0"),
+    (300_000, 0.2, 500_000, 5_000, None),                   # exact path: decode runs on its own
+    (1_000_003, 0.01, 1000, 0, None),                        # empty payload: plain copy
+])
+def test_encode_with_coscheduled_replace(dev, n, alpha, rn, rk, shares, monkeypatch):
+    """dpz_topk_encode_replace == dpz_topk_encode + an independent replace decode, bit-exact,
+    for any split of the decode's chunks over the encoder's launches (DPZ_COSCHED)."""
+    codec = _codec()
+    if shares is not None:
+        monkeypatch.setenv("DPZ_COSCHED", shares)
+    x, x0 = _inputs(n, 5)
+    k = round(alpha * n)
+    o_cnt = np.zeros(n, dtype=np.int32)
+    oi, ov = otopk.encode(x, x0, None, 0, k, counter=o_cnt)
+    rng = np.random.default_rng(rk + 3)
+    local = rng.standard_normal(rn).astype(np.float32)
+    ridx, rvals = _payload(rn, rk, seed=2, local=local)
+    ref = ofold.replace(local, ridx, rvals)
+    tx, tx0 = torch.from_numpy(x).to(dev), torch.from_numpy(x0).to(dev)
+    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    tl = torch.from_numpy(local).to(dev)
+    out = torch.full_like(tl, float("nan"))
+    ws = codec.Workspace(dev)
+    idx, val = codec.topk_encode(tx, k, x0=tx0, counter=cnt, workspace=ws,
+                                 co_replace=(tl, torch.from_numpy(ridx).to(dev),
+                                             torch.from_numpy(rvals).to(dev), out))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(idx.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(val.cpu().numpy()), _bits(ov))
+    np.testing.assert_array_equal(cnt.cpu().numpy(), o_cnt)
+    np.testing.assert_array_equal(_bits(out.cpu().numpy()), _bits(ref))
+
+
+def test_coscheduled_replace_rejects_aliasing(dev):
+    codec = _codec()
+    n = 1_000_003
+    x, x0 = _inputs(n, 5)
+    tx, tx0 = torch.from_numpy(x).to(dev), torch.from_numpy(x0).to(dev)
+    p_idx = torch.tensor([3], dtype=torch.int32, device=dev)
+    p_val = torch.tensor([1.0], dtype=torch.float32, device=dev)
+    with pytest.raises(RuntimeError):  # decode output overlapping the encoder's input
+        codec.topk_encode(tx, 10_000, x0=tx0, co_replace=(tx0.clone(), p_idx, p_val, tx))
