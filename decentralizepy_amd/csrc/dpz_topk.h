@@ -183,7 +183,7 @@ static inline size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
 
 struct WsLayout {
   size_t ctrl, chist, ex_hist, ex_gt, ex_eq, ex_off, ex_eqb;
-  size_t f_ghist, f_segcnt, f_blkabove, f_blkoff, f_cidx, f_ckey, f_blcnt, f_blkey, f_blidx;
+  size_t f_ghist, f_segcnt, f_blkabove, f_blkoff, f_cidx, f_ckey, f_cval, f_blcnt, f_blkey, f_blidx;
   size_t total;
   int64_t ex_nblk;
   FastGeom fg;
@@ -209,6 +209,7 @@ static inline WsLayout ws_layout(int64_t n) {
   L.f_blkoff = o; o += align256(L.fg.B * 4);
   L.f_cidx = o; o += align256((size_t)L.fg.W * L.fg.CAP * 4);
   L.f_ckey = o; o += align256((size_t)L.fg.W * L.fg.CAP * 4);
+  L.f_cval = o; o += align256((size_t)L.fg.W * L.fg.CAP * 4);
   L.f_blkey = o; o += align256((size_t)BCAP * 4);
   L.f_blidx = o; o += align256((size_t)BCAP * 4);
   L.total = o;

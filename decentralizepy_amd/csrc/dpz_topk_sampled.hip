@@ -165,8 +165,10 @@ static inline void window_ranks(int64_t n, int64_t k, uint32_t* r_lo, uint32_t* 
 struct WaveList {
   uint32_t* gidx;   // this segment's global candidate list
   uint32_t* gkey;
+  float* gval;      // candidate values x[idx] (nullptr: not carried, compact gathers vals_src)
   uint32_t* sidx;   // this wave's LDS stage
   uint32_t* skey;
+  float* sval;
   uint32_t staged;  // entries in the stage (wave-uniform)
   uint32_t flushed; // entries already in the global list (wave-uniform)
 
@@ -181,6 +183,7 @@ struct WaveList {
       if (write) {
         gidx[flushed + j] = sidx[j];
         gkey[flushed + j] = key;
+        if (gval) gval[flushed + j] = sval[j];
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -231,11 +234,12 @@ template <bool VEC, bool ACC, int G>
 __global__ void __launch_bounds__(256, FOCC) sampled_filter_kernel(
     KeySrc s, int64_t n, uint32_t r_lo, uint32_t r_hi, int64_t W, int64_t R, int64_t CAP,
     TopkCtrl* ctrl, const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt,
-    uint32_t* cidx, uint32_t* ckey) {
+    uint32_t* cidx, uint32_t* ckey, float* cval) {
   __shared__ uint32_t h[HBR];
   __shared__ uint32_t win[4];
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t st_idx[4][STAGE], st_key[4][STAGE];
+  __shared__ float st_val[4][STAGE];
   STAMP_W(0);
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int b = threadIdx.x; b < HBR; b += 256) h[b] = 0;
@@ -263,7 +267,8 @@ __global__ void __launch_bounds__(256, FOCC) sampled_filter_kernel(
     ctrl->hi = hi;
     ctrl->shift = shift;
   }
-  WaveList L{cidx + seg * CAP, ckey + seg * CAP, st_idx[wid], st_key[wid], 0u, 0u};
+  WaveList L{cidx + seg * CAP, ckey + seg * CAP, cval ? cval + seg * CAP : nullptr,
+             st_idx[wid], st_key[wid], st_val[wid], 0u, 0u};
   uint32_t run = 0;
   bool dense = false;
   for (int64_t base = beg; base < end; base += G * 256) {
@@ -289,9 +294,15 @@ __global__ void __launch_bounds__(256, FOCC) sampled_filter_kernel(
           const uint32_t i0 = (uint32_t)(base + q * 256 + lane * 4);
           if (L.staged + tot > STAGE) L.flush(lane, true, h, lo, hi, shift);
           uint32_t p = L.staged + pre;
+          const float xv[4] = {raw[q].a.x, raw[q].a.y, raw[q].a.z, raw[q].a.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            if (f[e]) { L.sidx[p] = i0 + e; L.skey[p] = kq[e]; ++p; }
+            if (f[e]) {
+              L.sidx[p] = i0 + e;
+              L.skey[p] = kq[e];
+              L.sval[p] = xv[e];  // x[i] (used only when carried: vals_src == x, no rekey)
+              ++p;
+            }
           }
           L.staged += tot;
         } else {
@@ -374,6 +385,15 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
   const int64_t seg0 = (int64_t)blockIdx.x * SEL_SEGS + wid * 2;
   const uint32_t cnt0 = seg0 < W ? segcnt[seg0] : 0u;
   const uint32_t cnt1 = seg0 + 1 < W ? segcnt[seg0 + 1] : 0u;
+  // the first 64 entries of both lists are loaded with the counts and the histogram, not after
+  // b* is known (CAP >= 64; entries past the count are ignored)
+  uint32_t pk[2], pi[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int64_t sg = seg0 + u;
+    pk[u] = sg < W ? ckey[sg * CAP + lane] : 0u;
+    pi[u] = sg < W ? cidx[sg * CAP + lane] : 0u;
+  }
   const uint32_t lo = ctrl->lo, hi = ctrl->hi, shift = ctrl->shift;
   if (t < HBR) {
     uint32_t v[GH_COPIES];
@@ -433,8 +453,8 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
         const uint32_t j = j0 + lane;
         uint32_t key = 0, b = 0, idx = 0;
         if (j < cnt) {
-          key = ckey[seg * CAP + j];
-          idx = cidx[seg * CAP + j];
+          key = j0 == 0 ? pk[u] : ckey[seg * CAP + j];
+          idx = j0 == 0 ? pi[u] : cidx[seg * CAP + j];
           b = fine_bin(key, lo, hi, shift);
         }
         above += (uint32_t)__popcll(__ballot(j < cnt && b > bstar));
@@ -728,35 +748,39 @@ __device__ __forceinline__ void dense_write(const KeySrc s, int64_t seg, int64_t
   }
 }
 
-// One block of 256 threads per filter block (4 wave segments).  Prologue, redundantly in every
-// block (no single-block launch in between — a launch boundary plus a one-CU kernel cost more
-// than the ~15 KB of L2 reads per block): the exact T / icut from the boundary sub-lists, the
-// block's output offset = above-b* counts of the earlier filter blocks + selected boundary
-// entries before the block, and the check that the grand total is k.  Then per wave a count
-// pass, in-block wave offsets, and the ordered write of (idx, vals_src[idx]) with counter /
-// rewind updates.  Block 0 re-zeroes the sample histogram and publishes T / icut / status.
+// One block of 256 threads per CSEG = 8 wave segments (2 filter blocks), two segments per wave:
+// half as many blocks as segments-per-4, so 4 waves per SIMD hold the whole grid and the kernel
+// gets 128 VGPRs (no spills).  Prologue, redundantly in every block (no single-block launch in
+// between — a launch boundary plus a one-CU kernel cost more than the ~15 KB of L2 reads per
+// block): the exact T / icut from the boundary sub-lists, the block's output offset = above-b*
+// counts of the earlier filter blocks + selected boundary entries before the block, and the
+// check that the grand total is k.  Then per wave a count pass over its two segments, in-block
+// offsets, and the ordered write of (idx, vals_src[idx]) with counter / rewind updates.  Block 0
+// re-zeroes the sample histogram and publishes T / icut / status.
+constexpr int CSEG = 8;
 template <bool VEC>
-__global__ void __launch_bounds__(256, 8) sampled_compact_kernel(
+__global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl,
     uint32_t* chist, const uint32_t* __restrict__ blkabove, const uint32_t* __restrict__ blcnt,
     const uint32_t* __restrict__ blkey, const uint32_t* __restrict__ blidx,
     const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ cidx,
-    const uint32_t* __restrict__ ckey, const float* vals_src, int32_t* idx_out, float* val_out,
-    int32_t* counter, float* rewind, ReplaceJob pj) {
-  __shared__ uint32_t wcnt[4];
+    const uint32_t* __restrict__ ckey, const float* __restrict__ cval, const float* vals_src,
+    int32_t* idx_out, float* val_out, int32_t* counter, float* rewind, ReplaceJob pj) {
+  __shared__ uint32_t wcnt[CSEG];
   __shared__ uint32_t subbase[NSUB + 1];
   __shared__ uint32_t flag;
   __shared__ uint64_t wsum64[4];
   __shared__ ResolveLds RL;
   __shared__ uint32_t bsk[BLDS], bsi[BLDS];
-  const int64_t B = (W + 3) / 4;
-  if ((int64_t)blockIdx.x >= B) {  // co-scheduled replace decode
-    replace_block(pj, (int64_t)blockIdx.x - B);
+  const int64_t CB_ = (W + CSEG - 1) / CSEG;
+  const int64_t B = (W + 3) / 4;  // filter blocks (above counts)
+  if ((int64_t)blockIdx.x >= CB_) {  // co-scheduled replace decode
+    replace_block(pj, (int64_t)blockIdx.x - CB_);
     return;
   }
   STAMP_T0(0);
   const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
-  const int64_t seg = (int64_t)blockIdx.x * 4 + wid;
+  const int64_t seg0 = (int64_t)blockIdx.x * CSEG + wid * 2;
   // every independent load first: control words, sub-list counts, above counts, own candidates
   const uint32_t status = ctrl->status;
   const uint32_t need = ctrl->need, lo = ctrl->lo, shift = ctrl->shift, bstar = ctrl->bstar;
@@ -772,19 +796,24 @@ __global__ void __launch_bounds__(256, 8) sampled_compact_kernel(
       v1 = reinterpret_cast<const uint4*>(blkabove)[2 * t + 1];
     }
     const uint32_t v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    const uint32_t bx = blockIdx.x;
+    const uint32_t fbx = blockIdx.x * (uint32_t)(CSEG / 4);  // first filter block of this block
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       abv_all += v[q];
-      abv_before += fb0 + q < bx ? v[q] : 0u;
+      abv_before += fb0 + q < fbx ? v[q] : 0u;
     }
   }
-  const uint32_t cnt = seg < W ? segcnt[seg] : 0u;
-  const bool dense = cnt == DENSE;
-  uint32_t key0 = 0, idx0 = 0;
-  if (seg < W && !dense && (uint32_t)lane < cnt) {
-    key0 = ckey[seg * CAP + lane];
-    idx0 = cidx[seg * CAP + lane];
+  uint32_t cnt[2], key0[2], idx0[2];
+  float val0[2] = {0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int64_t seg = seg0 + u;
+    cnt[u] = seg < W ? segcnt[seg] : 0u;
+    // the first 64 list entries are loaded without waiting for the count (CAP >= 64; entries
+    // past the count are ignored)
+    key0[u] = seg < W ? ckey[seg * CAP + lane] : 0u;
+    idx0[u] = seg < W ? cidx[seg * CAP + lane] : 0u;
+    if (cval && seg < W) val0[u] = cval[seg * CAP + lane];
   }
   if (blockIdx.x == 0) {  // leave the sample histogram zeroed for the next call
     for (int b = t; b < CB; b += 256) chist[b] = 0;
@@ -812,7 +841,7 @@ __global__ void __launch_bounds__(256, 8) sampled_compact_kernel(
   block_resolve(bd, need, lo + (bstar << shift), shift, RL, &T, &icut);
   STAMP_T0(2);
   // selected boundary entries before this block / overall, plus the above counts
-  const uint32_t bstart = (uint32_t)((int64_t)blockIdx.x * 4 * R);
+  const uint32_t bstart = (uint32_t)((int64_t)blockIdx.x * CSEG * R);
   uint32_t sb_before = 0, sb_all = 0;
   bd.each([&](uint32_t kv, uint32_t iv) {
     const bool sel = kv > T || (kv == T && iv <= icut);
@@ -828,60 +857,71 @@ __global__ void __launch_bounds__(256, 8) sampled_compact_kernel(
     if (grand != (uint32_t)k) ctrl->status = 2;  // internal inconsistency
   }
   if (grand != (uint32_t)k) return;  // identical in every block: nothing is written
-  // count pass (first 64 list entries stay in registers), wave offsets, write pass
-  uint32_t mine = 0;
-  bool sel0 = false;
-  if (seg < W && !dense) {
-    sel0 = (uint32_t)lane < cnt && (key0 > T || (key0 == T && idx0 <= icut));
-    mine = (uint32_t)__popcll(__ballot(sel0));
-    for (uint32_t j0 = 64; j0 < cnt; j0 += 64) {
-      const uint32_t j = j0 + lane;
-      bool sel = false;
-      if (j < cnt) {
-        const uint32_t key = ckey[seg * CAP + j];
-        const uint32_t idx = cidx[seg * CAP + j];
-        sel = key > T || (key == T && idx <= icut);
+  // count pass (first 64 list entries stay in registers), in-block offsets, write pass
+  bool sel0[2] = {false, false};
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int64_t seg = seg0 + u;
+    uint32_t mine = 0;
+    if (seg < W && cnt[u] != DENSE) {
+      sel0[u] = (uint32_t)lane < cnt[u] && (key0[u] > T || (key0[u] == T && idx0[u] <= icut));
+      mine = (uint32_t)__popcll(__ballot(sel0[u]));
+      for (uint32_t j0 = 64; j0 < cnt[u]; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        bool sel = false;
+        if (j < cnt[u]) {
+          const uint32_t key = ckey[seg * CAP + j];
+          const uint32_t idx = cidx[seg * CAP + j];
+          sel = key > T || (key == T && idx <= icut);
+        }
+        mine += (uint32_t)__popcll(__ballot(sel));
       }
-      mine += (uint32_t)__popcll(__ballot(sel));
+    } else if (seg < W) {
+      mine = dense_count<VEC>(s, seg, R, n, lo, T, icut);
     }
-  } else if (seg < W) {
-    mine = dense_count<VEC>(s, seg, R, n, lo, T, icut);
+    if (lane == 0) wcnt[wid * 2 + u] = mine;
   }
-  if (lane == 0) wcnt[wid] = mine;
   __syncthreads();
   STAMP_T0(3);
   uint32_t run = boff;
-  for (int w = 0; w < wid; ++w) run += wcnt[w];
-  if (seg >= W) return;
-  auto emit = [&](bool sel, uint32_t idx) {
-    const uint64_t m = __ballot(sel);
-    if (sel) {
-      const uint32_t pos = run + mbcnt64(m);
-      if (pos < (uint64_t)k) {
-        idx_out[pos] = (int32_t)idx;
-        val_out[pos] = vals_src[idx];
-        if (counter) atomicAdd(&counter[idx], 1);  // non-returning: no round trip to wait on
-        if (rewind) rewind[idx] = 0.0f;
+  for (int w = 0; w < wid * 2; ++w) run += wcnt[w];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int64_t seg = seg0 + u;
+    if (seg >= W) break;
+    if (cnt[u] != DENSE) {
+      auto emit = [&](bool sel, uint32_t idx, float v) {
+        const uint64_t m = __ballot(sel);
+        if (sel) {
+          const uint32_t pos = run + mbcnt64(m);
+          if (pos < (uint64_t)k) {
+            idx_out[pos] = (int32_t)idx;
+            val_out[pos] = cval ? v : vals_src[idx];
+            if (counter) atomicAdd(&counter[idx], 1);  // non-returning: no round trip to wait on
+            if (rewind) rewind[idx] = 0.0f;
+          }
+        }
+        run += (uint32_t)__popcll(m);
+      };
+      emit(sel0[u], idx0[u], val0[u]);
+      for (uint32_t j0 = 64; j0 < cnt[u]; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        bool sel = false;
+        uint32_t idx = 0;
+        float v = 0.f;
+        if (j < cnt[u]) {
+          const uint32_t key = ckey[seg * CAP + j];
+          idx = cidx[seg * CAP + j];
+          if (cval) v = cval[seg * CAP + j];
+          sel = key > T || (key == T && idx <= icut);
+        }
+        emit(sel, idx, v);
       }
+    } else {
+      dense_write<VEC>(s, seg, R, n, k, lo, T, icut, run, vals_src, idx_out, val_out, counter,
+                       rewind);
+      run += wcnt[wid * 2 + u];
     }
-    run += (uint32_t)__popcll(m);
-  };
-  if (!dense) {
-    emit(sel0, idx0);
-    for (uint32_t j0 = 64; j0 < cnt; j0 += 64) {
-      const uint32_t j = j0 + lane;
-      bool sel = false;
-      uint32_t idx = 0;
-      if (j < cnt) {
-        const uint32_t key = ckey[seg * CAP + j];
-        idx = cidx[seg * CAP + j];
-        sel = key > T || (key == T && idx <= icut);
-      }
-      emit(sel, idx);
-    }
-  } else {
-    dense_write<VEC>(s, seg, R, n, k, lo, T, icut, run, vals_src, idx_out, val_out, counter,
-                     rewind);
   }
   STAMP_T0(4);
 }
@@ -912,6 +952,8 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
   uint32_t* blkabove = reinterpret_cast<uint32_t*>(a.ws + L.f_blkabove);
   uint32_t* cidx = reinterpret_cast<uint32_t*>(a.ws + L.f_cidx);
   uint32_t* ckey = reinterpret_cast<uint32_t*>(a.ws + L.f_ckey);
+  // candidate values carried from the filter when the payload values are x itself (PartialModel)
+  float* cval = (a.vals_src == a.x) ? reinterpret_cast<float*>(a.ws + L.f_cval) : nullptr;
   uint32_t* blcnt = reinterpret_cast<uint32_t*>(a.ws + L.f_blcnt);
   uint32_t* blkey = reinterpret_cast<uint32_t*>(a.ws + L.f_blkey);
   uint32_t* blidx = reinterpret_cast<uint32_t*>(a.ws + L.f_blidx);
@@ -948,10 +990,10 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
     window_ranks(a.n, a.k, &r_lo, &r_hi);
     if (a.acc_mode == DPZ_ACC_NONE)
       DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC, false, FG><<<nb, 256, 0, a.st>>>(
-          s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey));
+          s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval));
     else
       DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC, true, 1><<<nb, 256, 0, a.st>>>(
-          s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey));
+          s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval));
   }
   if (!(phases & 2)) return DPZ_OK;
   s.rekey = 1;
@@ -959,9 +1001,10 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
       s, a.n, a.k, g.W, g.B, g.R, g.CAP, ctrl, ghist, segcnt, cidx, ckey, blkabove, blcnt, blkey,
       blidx, jb[1]));
   float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE) ? a.acc : nullptr;
-  DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC><<<nb + pb[2], 256, 0, a.st>>>(
+  const unsigned ncmp = (unsigned)((g.W + CSEG - 1) / CSEG);
+  DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC><<<ncmp + pb[2], 256, 0, a.st>>>(
       s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, cidx,
-      ckey, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, jb[2]));
+      ckey, cval, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, jb[2]));
   return DPZ_OK;
 }
 
