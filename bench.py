@@ -38,9 +38,11 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 64 MiB secondary line")
-    p.add_argument("--workload", choices=["c2", "c4"], default="c2",
+    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "e2e"], default="c2",
                    help="c2: one node's 11M tensor per GPU (default); c4: the 96-node gossip "
-                        "round of eval/96_regular.edges sharded over the GPUs")
+                        "round of eval/96_regular.edges sharded over the GPUs; c3: JWINS wavelet "
+                        "25M + 16-payload decode; c5: 256 MiB, 0.1%%, fp16 values; e2e: "
+                        "PCIe-inclusive rates (bench_workloads.py)")
     p.add_argument("--rotate", type=int, default=None,
                    help="independent node states cycled per step (default: enough for > 2x L3)")
     p.add_argument("--serial", action="store_true",
@@ -362,6 +364,25 @@ def main():
                 "round_alg_bytes": r["alg_bytes"],
                 "round_frac_of_hbm_peak": round(r["alg_bytes"] / r["s_step"] / 1e9 / HBM_PEAK_GBS / world, 4),
             }), flush=True)
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    if args.workload in ("c3", "c5", "e2e"):
+        import bench_workloads as bw
+        if args.workload == "c3":
+            r = [bw.c3_case(dev, alpha=a, steps=min(args.steps, 40)) for a in (0.01, 0.1)]
+        elif args.workload == "c5":
+            r = bw.c5_case(dev, steps=min(args.steps, 40), streams=args.streams)
+        else:
+            r = {"c2": bw.e2e_case(dev, 11_000_000, 0.01, streams=args.streams),
+                 "64MiB": bw.e2e_case(dev, 16_777_216, 0.01, streams=args.streams),
+                 "c5_fp16": bw.e2e_case(dev, 67_108_864, 0.001, fp16=True,
+                                        streams=args.streams)}
+        if rank == 0:
+            print(json.dumps({"metric": "GiB/s fp32 params encoded+decoded", "unit": "GiB/s",
+                              "workload": args.workload, "n_gpus": world, "result": r}),
+                  flush=True)
         if dist is not None:
             dist.barrier()
             dist.destroy_process_group()

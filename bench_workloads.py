@@ -1,0 +1,212 @@
+"""Secondary workloads of bench.py: C3 (JWINS wavelet + top-k, 16-payload
+batched decode + weighted average), C5 (256 MiB, 0.1 % top-k, fp16 value packing) and the
+PCIe-inclusive end-to-end rate (the reference path starts and ends in host memory: pyzmq socket
+buffers / CPU model parameters).
+
+Every function times whole steps with the device already holding what a node keeps resident
+across rounds (init_model, accumulated changes, counters); inputs are synthetic (device PRNG).
+Node states rotate so each step streams its inputs from HBM, not the 256 MiB Infinity Cache.
+"""
+import math
+import time
+
+import torch
+
+L3_BYTES = 256 * 2 ** 20
+
+
+def _sync_time(fn, steps):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        fn(i)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def c3_case(dev, n=25_000_000, alpha=0.01, npay=16, steps=40, warmup=5, seed=3):
+    """C3: one JWINS receiver round on an N-parameter model (reference Wavelet.py:142-329 with
+    the tutorial/JWINS/config.ini settings change_based_selection, accumulation and
+    accumulate_averaging_changes on): encode = W(x), W(x - x0) in one DWT launch, top-k of
+    |W(x - x0) + acc| (PartialModel.py:322-327: change += acc), acc rewind and counter at the
+    selected coefficients, values from W(x); decode =
+    16 neighbour payloads replaced + Metro-Hastings-folded in the wavelet domain in one batched
+    launch (w = 1/17 each, self 1 - 16/17), then one IDWT launch back to N parameters.
+    Algorithmic bytes: B_enc = 8N + 8M + 12k (+ acc 8M read/write), B_dec =
+    4M + 4N + 8 n k."""
+    from decentralizepy_amd import codec
+    level = 4
+    m = codec.wavedec_len(n, level)
+    k = round(alpha * m)
+    per_set = 4 * (2 * n + 4 * m) + 8 * k
+    R = max(2, math.ceil(2 * L3_BYTES / per_set) + 1)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    sets = []
+    for _ in range(R):
+        x = torch.randn(n, device=dev, generator=g)
+        sets.append(dict(x=x, x0=x - 0.01 * torch.randn(n, device=dev, generator=g),
+                         acc=0.01 * torch.randn(m, device=dev, generator=g),
+                         cnt=torch.zeros(m, dtype=torch.int32, device=dev),
+                         wx=torch.empty(m, device=dev), wc=torch.empty(m, device=dev),
+                         idx=torch.empty(k, dtype=torch.int32, device=dev),
+                         val=torch.empty(k, device=dev), tot=torch.empty(m, device=dev),
+                         out=torch.empty(n, device=dev)))
+    # 16 received payloads (fixed, distinct index sets)
+    pays = []
+    for j in range(npay):
+        idx = torch.sort(torch.randperm(m, device=dev, generator=g)[:k])[0].to(torch.int32)
+        pays.append((idx, torch.randn(k, device=dev, generator=g)))
+    w = [1 / (npay + 1)] * npay
+    wt = 0.0
+    for v in w:
+        wt += v
+    w_self = 1 - wt
+    ws = codec.Workspace(dev)
+
+    def encode(d):
+        codec.wavedec(d["x"], level, x0=d["x0"], coeffs_x=d["wx"], coeffs_diff=d["wc"])
+        codec.topk_encode(d["wc"], k, acc=d["acc"], acc_mode=codec.DPZ_ACC_ADD,
+                          vals_src=d["wx"], counter=d["cnt"], idx_out=d["idx"],
+                          val_out=d["val"], workspace=ws, asynchronous=True)
+
+    def decode(d):
+        codec.decode_average(d["wx"], pays, w, w_self, out=d["tot"], workspace=ws)
+        codec.waverec(d["tot"], n, level, out=d["out"])
+
+    def step(i):
+        d = sets[i % R]
+        encode(d)
+        decode(d)
+
+    for i in range(max(warmup, R)):
+        step(i)
+    t_step = _sync_time(step, steps)
+    t_enc = _sync_time(lambda i: encode(sets[i % R]), steps)
+    t_dec = _sync_time(lambda i: decode(sets[i % R]), steps)
+    fb = codec.topk_status(ws) != 0
+    with codec.KernelTimer() as kt:
+        torch.cuda._sleep(int(100e6))
+        for i in range(R * 2):
+            step(i)
+        torch.cuda.synchronize()
+    kern = {nm: round(ms / c * 1e3, 2) for nm, (ms, c) in kt.result.items()}
+    b_enc = 8 * n + 8 * m + 8 * m + 12 * k  # x, x0 -> W(x), W(dx); read W(dx), acc; k triples
+    b_dec = 4 * m + 4 * n + 8 * npay * k + 8 * m
+    return dict(workload=f"C3: JWINS sym2 level-4 wavelet + top-k (accumulation) of an "
+                         f"N={n} tensor (M={m} coefficients), {npay}-payload batched decode + "
+                         f"MH average + IDWT", n=n, m=m, k=k, alpha=alpha, rotated_states=R,
+                value=4 * n / t_step / 2 ** 30, ms_per_step=t_step * 1e3,
+                encode_us=t_enc * 1e6, decode_us=t_dec * 1e6,
+                alg_bytes_enc=b_enc, alg_bytes_dec=b_dec,
+                step_frac_of_hbm_peak=(b_enc + b_dec) / t_step / 8e12, fell_back=fb,
+                kernels_avg_us=kern)
+
+
+def c5_case(dev, n=67_108_864, alpha=0.001, steps=40, warmup=5, seed=5, streams=3):
+    """C5: 256 MiB fp32 tensor, 0.1 % top-k, payload values packed to fp16 (RNE, torch.half
+    semantics): encode = top-k + fp16 pack; decode = fp16 unpack + replace.  B = 16N + 12k."""
+    from decentralizepy_amd import codec
+    k = round(alpha * n)
+    per_set = 4 * n * 4 + 10 * k
+    R = max(streams, math.ceil(2 * L3_BYTES / per_set) + 1)
+    R = -(-R // streams) * streams
+    g = torch.Generator(device=dev).manual_seed(seed)
+    sets = []
+    for _ in range(R):
+        x = torch.randn(n, device=dev, generator=g)
+        sets.append(dict(x=x, x0=x - 0.01 * torch.randn(n, device=dev, generator=g),
+                         cnt=torch.zeros(n, dtype=torch.int32, device=dev),
+                         idx=torch.empty(k, dtype=torch.int32, device=dev),
+                         val=torch.empty(k, device=dev),
+                         h=torch.empty(k, dtype=torch.float16, device=dev),
+                         v32=torch.empty(k, device=dev), out=torch.empty(n, device=dev)))
+    S = [torch.cuda.Stream(dev) for _ in range(streams)]
+    W = [codec.Workspace(dev) for _ in range(streams)]
+
+    def step_on(d, ws):
+        codec.topk_encode(d["x"], k, x0=d["x0"], counter=d["cnt"], idx_out=d["idx"],
+                          val_out=d["val"], workspace=ws, asynchronous=True)
+        codec.pack_fp16(d["val"], out=d["h"])
+        codec.unpack_fp16(d["h"], out=d["v32"])
+        codec.replace(d["x0"], d["idx"], d["v32"], out=d["out"], workspace=ws)
+
+    def step(i):
+        step_on(sets[i % R], W[0])
+
+    def step_multi(i):
+        q = i % streams
+        with torch.cuda.stream(S[q]):
+            step_on(sets[i % R], W[q])
+
+    for i in range(max(warmup, R)):
+        step_multi(i)
+    t_multi = _sync_time(step_multi, steps)
+    t_one = _sync_time(step, steps)
+    fb = codec.topk_status(W[0]) != 0
+    b = 16 * n + 12 * k
+    return dict(workload=f"C5: N={n} (256 MiB) fp32, alpha={alpha} top-k, fp16 value packing",
+                n=n, k=k, rotated_states=R, streams=streams,
+                value=4 * n / t_multi / 2 ** 30, ms_per_step=t_multi * 1e3,
+                one_node_ms_per_step=t_one * 1e3, alg_bytes=b,
+                step_frac_of_hbm_peak=b / t_multi / 8e12, fell_back=fb)
+
+
+def e2e_case(dev, n, alpha, fp16=False, steps=20, warmup=3, seed=7, streams=3):
+    """PCIe-inclusive rate: the node's flat model arrives from host memory (pinned, H2D 4N), the
+    payload leaves for the socket (D2H 8k, or 6k with fp16 values); a received payload arrives
+    (H2D) and the averaged model returns to host memory (D2H 4N) — the reference's Sharing path
+    starts and ends in numpy buffers.  init_model / counters stay resident on the device.
+    Reported for one node (one stream: every copy serialised with the kernels) and for
+    `streams` concurrent nodes (H2D and D2H of different nodes overlap on the full-duplex link)."""
+    from decentralizepy_amd import codec
+    k = round(alpha * n)
+    R = streams * 2
+    g = torch.Generator(device=dev).manual_seed(seed)
+    vdt = torch.float16 if fp16 else torch.float32
+    sets = []
+    for _ in range(R):
+        x = torch.randn(n, device=dev, generator=g)
+        d = dict(x=torch.empty(n, device=dev), x0=x - 0.01 * torch.randn(n, device=dev, generator=g),
+                 cnt=torch.zeros(n, dtype=torch.int32, device=dev),
+                 idx=torch.empty(k, dtype=torch.int32, device=dev),
+                 val=torch.empty(k, device=dev), h=torch.empty(k, dtype=torch.float16, device=dev),
+                 ridx=torch.empty(k, dtype=torch.int32, device=dev),
+                 rval=torch.empty(k, dtype=vdt, device=dev), v32=torch.empty(k, device=dev),
+                 out=torch.empty(n, device=dev),
+                 hx=x.cpu().pin_memory(), hidx=torch.empty(k, dtype=torch.int32).pin_memory(),
+                 hval=torch.empty(k, dtype=vdt).pin_memory(),
+                 hout=torch.empty(n).pin_memory())
+        sets.append(d)
+    S = [torch.cuda.Stream(dev) for _ in range(streams)]
+    W = [codec.Workspace(dev) for _ in range(streams)]
+
+    def step_on(d, ws):
+        d["x"].copy_(d["hx"], non_blocking=True)                       # model params in
+        codec.topk_encode(d["x"], k, x0=d["x0"], counter=d["cnt"], idx_out=d["idx"],
+                          val_out=d["val"], workspace=ws, asynchronous=True)
+        v = codec.pack_fp16(d["val"], out=d["h"]) if fp16 else d["val"]
+        d["hidx"].copy_(d["idx"], non_blocking=True)                   # payload out
+        d["hval"].copy_(v, non_blocking=True)
+        d["ridx"].copy_(d["hidx"], non_blocking=True)                  # a payload in
+        d["rval"].copy_(d["hval"], non_blocking=True)
+        rv = codec.unpack_fp16(d["rval"], out=d["v32"]) if fp16 else d["rval"]
+        codec.replace(d["x0"], d["ridx"], rv, out=d["out"], workspace=ws)
+        d["hout"].copy_(d["out"], non_blocking=True)                   # averaged model out
+
+    def step(i):
+        step_on(sets[i % R], W[0])
+
+    def step_multi(i):
+        q = i % streams
+        with torch.cuda.stream(S[q]):
+            step_on(sets[i % R], W[q])
+
+    for i in range(max(warmup, R)):
+        step_multi(i)
+    t_one = _sync_time(step, steps)
+    t_multi = _sync_time(step_multi, steps)
+    pcie = 8 * n + (2 * (4 + (2 if fp16 else 4)) * k)
+    return dict(n=n, k=k, fp16_values=fp16, pcie_bytes_per_step=pcie,
+                one_node_GiBps=4 * n / t_one / 2 ** 30, one_node_ms_per_step=t_one * 1e3,
+                concurrent_GiBps=4 * n / t_multi / 2 ** 30, concurrent_ms_per_step=t_multi * 1e3,
+                concurrent_pcie_GBps=pcie / t_multi / 1e9, streams=streams)

@@ -57,8 +57,11 @@ __global__ void __launch_bounds__(256) fold_offsets_kernel(FoldArgs a, int32_t* 
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t k = P.k;
   if (j > k) return;
-  const int64_t tprev = j == 0 ? -1 : ((int64_t)P.idx[j - 1] >> FOLD_TILE_SHIFT);
+  int64_t tprev = j == 0 ? -1 : ((int64_t)P.idx[j - 1] >> FOLD_TILE_SHIFT);
   int64_t tcur = j == k ? a.ntiles : ((int64_t)P.idx[j] >> FOLD_TILE_SHIFT);
+  // an invalid payload (negative / too large / unsorted indices) must not write out of bounds
+  if (tprev < -1) tprev = -1;
+  if (tprev > a.ntiles) tprev = a.ntiles;
   if (tcur > a.ntiles) tcur = a.ntiles;
   int32_t* st = starts + (int64_t)p * (a.ntiles + 1);
   for (int64_t t = tprev + 1; t <= tcur; ++t) st[t] = (int32_t)j;

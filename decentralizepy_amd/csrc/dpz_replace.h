@@ -46,8 +46,11 @@ __device__ __forceinline__ void replace_chunk(const ReplaceJob& j, int64_t c, bo
     const int64_t k = j.k, n = j.n;
     const int64_t e0 = c * RP_E;
     const int64_t e1 = (e0 + RP_E < k) ? e0 + RP_E : k;
-    const int64_t a = c == 0 ? 0 : (int64_t)j.idx[e0];
-    const int64_t b = e1 >= k ? n : (int64_t)j.idx[e1];
+    int64_t a = c == 0 ? 0 : (int64_t)j.idx[e0];
+    int64_t b = e1 >= k ? n : (int64_t)j.idx[e1];
+    // an invalid payload (indices outside [0, n)) must not fault: clamp the range
+    a = a < 0 ? 0 : (a > n ? n : a);
+    b = b < 0 ? 0 : (b > n ? n : b);
     if (t < e1 - e0) {
       my_i = j.idx[e0 + t];
       my_v = j.val[e0 + t];

@@ -127,8 +127,15 @@ constexpr int SMP_NCHUNK = SMP_N / SMP_CHUNK;
 constexpr int SMP_BLOCKS = 64;     // 16 chunks per block: 4 waves x 4 rounds
 constexpr int CB_SHIFT = 20;       // coarse bins: key >> 20 (2048 bins, 8 per octave)
 constexpr int CB = 2048;
-constexpr int HB = 256;            // fine window bins (+1 "above window" bin)
+#ifndef DPZ_HB
+#define DPZ_HB 1024
+#endif
+// fine window bins (+1 "above window" bin): 1024 keep the threshold bin at ~k/1000 entries even
+// where the window is wide in count (C3: 25M wavelet coefficients, 256 bins overflowed the
+// boundary list)
+constexpr int HB = DPZ_HB;
 constexpr int HBR = HB + 1;
+static_assert(HB % 256 == 0 && HB <= 1024, "fine bins: multiple of 256, at most 1024");
 #ifndef DPZ_WMAX
 #define DPZ_WMAX 8192
 #endif
@@ -146,7 +153,7 @@ constexpr int FG = DPZ_FG;         // float4 groups of 256 elements a filter wav
 constexpr int FOCC = DPZ_FOCC;     // filter waves per SIMD the register budget is sized for
 constexpr int W_MIN_RANGE = DPZ_WMIN_RANGE;
 constexpr int GH_COPIES = 16;      // window histogram copies (filter block b adds into copy b % 16)
-constexpr int GH_STRIDE = 272;     // >= HBR, 16-aligned
+constexpr int GH_STRIDE = HB + 16; // >= HBR, 16-aligned
 constexpr int SEL_SEGS = 32;       // wave segments per select block (16 waves x 2)
 constexpr int SEL_LCAP = 1024;     // boundary entries one select block stages in LDS
 constexpr int NSUB = 16;           // boundary sub-lists (one atomic per select block each)

@@ -158,7 +158,10 @@ static inline void window_ranks(int64_t n, int64_t k, uint32_t* r_lo, uint32_t* 
   const double rlo_d = ceil(r_est + 6.0 * sd + 16.0);
   const double rhi_d = floor(r_est - 6.0 * sd - 16.0);
   *r_lo = rlo_d > SMP_N ? (uint32_t)SMP_N + 1 : (uint32_t)rlo_d;
-  *r_hi = rhi_d < 1.0 ? 0u : (uint32_t)rhi_d;
+  // at least rank 1 (the largest sample): an open-ended window [lo, 2^31) would make each of
+  // the 256 fine bins an octave wide and overflow the boundary list at small alpha (C5); keys
+  // above the largest sample's coarse bin are ~n / SMP_N elements, far fewer than k there
+  *r_hi = rhi_d < 1.0 ? 1u : (uint32_t)rhi_d;
 }
 
 // Per-wave candidate list append through an LDS stage, flushed in coalesced 64-lane chunks.
@@ -333,22 +336,35 @@ __global__ void __launch_bounds__(256, FOCC) sampled_filter_kernel(
   STAMP_W(5);
 }
 
-// Wave-level threshold bin from the global window histogram.  ghv = fine bins [252-4l, 255-4l].
-__device__ __forceinline__ bool wave_bstar(uint4 ghv, uint32_t above, uint32_t k, uint32_t* bstar,
-                                           uint32_t* need) {
+// Wave-level threshold bin from the global window histogram gh (LDS, HB fine bins + the
+// above-window count `above`): lane l holds the HB/64 bins [HB - HB/64 (l + 1), HB - HB/64 l).
+__device__ __forceinline__ bool wave_bstar(const uint32_t* gh, uint32_t above, uint32_t k,
+                                           uint32_t* bstar, uint32_t* need) {
+  constexpr int PL = HB / 64;
   const int lane = threadIdx.x & 63;
-  const uint32_t local = ghv.x + ghv.y + ghv.z + ghv.w;
+  uint32_t hv[PL];  // descending: hv[e] = bin HB - 1 - PL*lane - e
+  const uint4* g4 = reinterpret_cast<const uint4*>(gh) + (HB / 4 - (PL / 4) * (lane + 1));
+#pragma unroll
+  for (int q = 0; q < PL / 4; ++q) {
+    const uint4 v = g4[PL / 4 - 1 - q];
+    hv[4 * q + 0] = v.w;
+    hv[4 * q + 1] = v.z;
+    hv[4 * q + 2] = v.y;
+    hv[4 * q + 3] = v.x;
+  }
+  uint32_t local = 0;
+#pragma unroll
+  for (int e = 0; e < PL; ++e) local += hv[e];
   uint32_t tot;
   uint32_t before = wave_excl_scan(local, &tot) + above;
   uint32_t fb = 0xFFFFFFFFu, fn = 0;
-  const uint32_t hv4[4] = {ghv.w, ghv.z, ghv.y, ghv.x};
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    if (before < k && k <= before + hv4[e]) {
-      fb = (uint32_t)(255 - 4 * lane - e);
+  for (int e = 0; e < PL; ++e) {
+    if (before < k && k <= before + hv[e]) {
+      fb = (uint32_t)(HB - 1 - PL * lane - e);
       fn = k - before;
     }
-    before += hv4[e];
+    before += hv[e];
   }
   const uint64_t m = __ballot(fb != 0xFFFFFFFFu);
   const bool ok = (above < k) && (above + tot >= k) && m != 0;
@@ -395,22 +411,21 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
     pi[u] = sg < W ? cidx[sg * CAP + lane] : 0u;
   }
   const uint32_t lo = ctrl->lo, hi = ctrl->hi, shift = ctrl->shift;
-  if (t < HBR) {
+  for (int b = t; b < HBR; b += 1024) {
     uint32_t v[GH_COPIES];
 #pragma unroll
-    for (int c = 0; c < GH_COPIES; ++c) v[c] = ghist[c * GH_STRIDE + t];
+    for (int c = 0; c < GH_COPIES; ++c) v[c] = ghist[c * GH_STRIDE + b];
     uint32_t sum = 0;
 #pragma unroll
     for (int c = 0; c < GH_COPIES; ++c) sum += v[c];
-    gh[t] = sum;
+    gh[b] = sum;
   }
   if (t < SEL_SEGS / 4) fbabove[t] = 0;
   if (t == 0) lcnt = 0;
   __syncthreads();
   if (wid == 0) {
     uint32_t bstar, need;
-    const uint4 ghv = reinterpret_cast<const uint4*>(gh)[63 - lane];
-    const bool ok = wave_bstar(ghv, gh[HB], (uint32_t)k, &bstar, &need);
+    const bool ok = wave_bstar(gh, gh[HB], (uint32_t)k, &bstar, &need);
     if (lane == 0) {
       sb_bstar = bstar;
       sb_need = need;
