@@ -210,13 +210,15 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True, ro
     torch.cuda.synchronize()
     s_serial = (time.perf_counter() - t0) / steps
     # one node alone on the GPU, pipelined (decode of the previous payload co-scheduled inside
-    # the encode's latency-bound launches), one stream
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(steps):
-        step_pipe(i)
-    torch.cuda.synchronize()
-    s_cosched = (time.perf_counter() - t0) / steps
+    # the encode's latency-bound launches), one stream (skipped with --serial, the profiling run)
+    s_cosched = None
+    if pipeline:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step_pipe(i)
+        torch.cuda.synchronize()
+        s_cosched = (time.perf_counter() - t0) / steps
     # per-stage device time with events on the launch stream
     stream = torch.cuda.current_stream(dev)
     reps = max(2 * R, steps // 2)
@@ -398,7 +400,7 @@ def main():
                  "value": round(e["value"], 2), "ms_per_step": round(e["s_step"] * 1e3, 4),
                  "frac_of_hbm_peak": round((e["b_enc"] + e["b_dec"]) / e["s_step"] / 1e9 / HBM_PEAK_GBS, 4),
                  "one_node_serial_ms_per_step": round(e["s_serial"] * 1e3, 4),
-                 "one_node_cosched_ms_per_step": round(e["s_cosched"] * 1e3, 4),
+                 "one_node_cosched_ms_per_step": (round(e["s_cosched"] * 1e3, 4) if e["s_cosched"] else None),
                  "host_enqueue_ms_per_step": round(e["s_host"] * 1e3, 4),
                  "fell_back": e["fell_back"]}
 
@@ -476,7 +478,7 @@ def main():
                            "GBps": round(dec_gbs, 1), "frac": round(dec_gbs / HBM_PEAK_GBS, 4)},
                 "step_frac_of_hbm_peak": round(step_gbs / HBM_PEAK_GBS, 4),
                 "one_node_serial_ms_per_step": round(r["s_serial"] * 1e3, 5),
-                "one_node_cosched_ms_per_step": round(r["s_cosched"] * 1e3, 5),
+                "one_node_cosched_ms_per_step": (round(r["s_cosched"] * 1e3, 5) if r["s_cosched"] else None),
                 "host_enqueue_ms_per_step": round(r["s_host"] * 1e3, 5),
                 "kernels": kern,
                 "torch_copy_GBps_256MiB": copy_gbs,

@@ -99,11 +99,48 @@ __global__ void __launch_bounds__(256) dwt_kernel(const float* __restrict__ x,
   const int64_t n = LV.len[0];
   {
     const int64_t s0 = s[0], e0 = e[0];
-    for (int64_t p = s0 + threadIdx.x; p < e0; p += 256) {
-      if (p >= 0 && p < n) {
-        const float xv = x[p];
-        if (WX) bufA[0][p - s0] = xv;
-        if (WD) bufA[1][p - s0] = xv - x0[p];
+    // every load of the span is issued before any is used (float4 groups from the 4-aligned
+    // start below s0; a group that is not wholly inside [0, n) or an unaligned input falls back
+    // to scalar loads) — one memory latency per block instead of one per loop trip
+    constexpr int NG = (SPAN0 + 4 + 4 * 256 - 1) / (4 * 256);  // float4 groups per thread
+    const int64_t g0 = s0 >= 0 ? (s0 & ~int64_t(3)) : -((-s0 + 3) & ~int64_t(3));
+    const bool vec = aligned16(x) && (!WD || aligned16(x0));
+    float4 va[NG], vb[NG];
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      const int64_t p = g0 + 4 * (threadIdx.x + 256 * q);
+      va[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      vb[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p < e0) {
+        if (vec && p >= 0 && p + 4 <= n) {
+          va[q] = *reinterpret_cast<const float4*>(x + p);
+          if (WD) vb[q] = *reinterpret_cast<const float4*>(x0 + p);
+        } else {
+          float ta[4] = {0.f, 0.f, 0.f, 0.f}, tb[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (p + e >= 0 && p + e < n) {
+              ta[e] = x[p + e];
+              if (WD) tb[e] = x0[p + e];
+            }
+          }
+          va[q] = make_float4(ta[0], ta[1], ta[2], ta[3]);
+          vb[q] = make_float4(tb[0], tb[1], tb[2], tb[3]);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      const int64_t p = g0 + 4 * (threadIdx.x + 256 * q);
+      const float xa[4] = {va[q].x, va[q].y, va[q].z, va[q].w};
+      const float xb[4] = {vb[q].x, vb[q].y, vb[q].z, vb[q].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t pe = p + e;
+        if (pe >= s0 && pe < e0 && pe >= 0 && pe < n) {
+          if (WX) bufA[0][pe - s0] = xa[e];
+          if (WD) bufA[1][pe - s0] = xa[e] - xb[e];
+        }
       }
     }
     __syncthreads();

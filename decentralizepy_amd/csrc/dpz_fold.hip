@@ -27,6 +27,7 @@ constexpr int FOLD_TILE = 1 << FOLD_TILE_SHIFT;
 constexpr int FOLD_MAXP = 16;  // payloads per launch (longer lists are chained)
 constexpr int FOLD_THREADS = 512;
 constexpr int FOLD_GROUPS = FOLD_TILE / (4 * FOLD_THREADS);  // float4 groups per thread
+constexpr int FOLD_EQ = 4;  // payload entries per thread preloaded at tile start
 
 struct FoldPayload {
   const int32_t* idx;  // nullptr: dense payload (vals has n entries)
@@ -72,6 +73,7 @@ __global__ void __launch_bounds__(FOLD_THREADS) fold_kernel(FoldArgs a) {
   __shared__ __attribute__((aligned(16))) float hv[FOLD_TILE];
   __shared__ __attribute__((aligned(16))) uint8_t htag[FOLD_TILE];
   __shared__ int32_t rng[FOLD_MAXP][2];
+  __shared__ int32_t pre[FOLD_MAXP + 1];  // flattened entry offset of each payload's tile range
   const int64_t tile = blockIdx.x;
   const int64_t tlo = tile * FOLD_TILE;
   const int64_t thi = (tlo + FOLD_TILE < a.n) ? tlo + FOLD_TILE : a.n;
@@ -109,14 +111,59 @@ __global__ void __launch_bounds__(FOLD_THREADS) fold_kernel(FoldArgs a) {
     }
   }
 
+  __syncthreads();  // rng visible
+  if (t == 0) {
+    int32_t acc_e = 0;
+    for (int p = 0; p < a.np; ++p) {
+      pre[p] = acc_e;
+      const int32_t cnt = rng[p][1] - rng[p][0];
+      acc_e += cnt > 0 ? cnt : 0;
+    }
+    pre[a.np] = acc_e;
+  }
+  __syncthreads();
+  // every payload's entries of this tile (flattened, the first FOLD_EQ * FOLD_THREADS of them)
+  // are loaded before any is used: one memory latency per tile instead of one per payload
+  int ep[FOLD_EQ];
+  int32_t ei[FOLD_EQ];
+  float evl[FOLD_EQ];
+  const int32_t etot = pre[a.np];
+#pragma unroll
+  for (int q = 0; q < FOLD_EQ; ++q) {
+    const int32_t j = t + q * FOLD_THREADS;
+    ep[q] = -1;
+    ei[q] = 0;
+    evl[q] = 0.0f;
+    if (j < etot) {
+      int p = 0;
+      for (int u = 1; u < a.np; ++u) p += pre[u] <= j ? 1 : 0;
+      const int64_t src = (int64_t)rng[p][0] + (j - pre[p]);
+      ep[q] = p;
+      ei[q] = a.p[p].idx[src];
+      evl[q] = a.p[p].val[src];
+    }
+  }
+
   for (int p = 0; p < a.np; ++p) {
     const FoldPayload& P = a.p[p];
-    __syncthreads();  // previous payload's reads of hv/htag done; rng visible
+    __syncthreads();  // previous payload's reads of hv/htag done
     if (P.idx) {
+#pragma unroll
+      for (int q = 0; q < FOLD_EQ; ++q) {
+        if (ep[q] == p) {
+          const int64_t pos = (int64_t)ei[q] - tlo;
+          if (pos >= 0 && pos < FOLD_TILE) {  // guards against an unsorted caller array
+            hv[pos] = evl[q];
+            htag[pos] = (uint8_t)p;
+          }
+        }
+      }
+      // entries past the preloaded ones (dense payload ranges): loaded here
       const int64_t b = rng[p][0], e = rng[p][1];
-      for (int64_t j = b + t; j < e; j += FOLD_THREADS) {
+      const int64_t first = (int64_t)FOLD_EQ * FOLD_THREADS - pre[p];  // relative to b
+      for (int64_t j = b + (first > 0 ? first : 0) + t; j < e; j += FOLD_THREADS) {
         const int64_t pos = (int64_t)P.idx[j] - tlo;
-        if (pos >= 0 && pos < FOLD_TILE) {  // guards against an unsorted caller array
+        if (pos >= 0 && pos < FOLD_TILE) {
           hv[pos] = P.val[j];
           htag[pos] = (uint8_t)p;
         }

@@ -152,7 +152,13 @@ constexpr int FG = DPZ_FG;         // float4 groups of 256 elements a filter wav
 #endif
 constexpr int FOCC = DPZ_FOCC;     // filter waves per SIMD the register budget is sized for
 constexpr int W_MIN_RANGE = DPZ_WMIN_RANGE;
-constexpr int GH_COPIES = 16;      // window histogram copies (filter block b adds into copy b % 16)
+#ifndef DPZ_GH_COPIES
+#define DPZ_GH_COPIES 8
+#endif
+// window histogram copies (filter block b adds into copy b % GH_COPIES): enough to spread the
+// filter's end-of-block atomics over the 1024 bins, few enough that every select block can
+// sum them (each select block reads GH_COPIES x 4 KiB)
+constexpr int GH_COPIES = DPZ_GH_COPIES;
 constexpr int GH_STRIDE = HB + 16; // >= HBR, 16-aligned
 constexpr int SEL_SEGS = 32;       // wave segments per select block (16 waves x 2)
 constexpr int SEL_LCAP = 1024;     // boundary entries one select block stages in LDS

@@ -234,7 +234,7 @@ __device__ __forceinline__ void load_groups(const KeySrc& s, int64_t base, int64
 
 // B blocks x 256 threads; wave w of block b owns wave segment seg = 4b + w = [seg*R, +R) of [0, n).
 template <bool VEC, bool ACC, int G>
-__global__ void __launch_bounds__(256, FOCC) sampled_filter_kernel(
+__global__ void __launch_bounds__(256, ACC ? 4 : FOCC) sampled_filter_kernel(
     KeySrc s, int64_t n, uint32_t r_lo, uint32_t r_hi, int64_t W, int64_t R, int64_t CAP,
     TopkCtrl* ctrl, const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt,
     uint32_t* cidx, uint32_t* ckey, float* cval) {
@@ -1007,7 +1007,7 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
       DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC, false, FG><<<nb, 256, 0, a.st>>>(
           s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval));
     else
-      DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC, true, 1><<<nb, 256, 0, a.st>>>(
+      DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC, true, 3><<<nb, 256, 0, a.st>>>(
           s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval));
   }
   if (!(phases & 2)) return DPZ_OK;

@@ -39,7 +39,7 @@ def main(fetch, write, out):
         kernels[k] = {"FETCH_SIZE_KiB": round(fk, 2), "WRITE_SIZE_KiB": round(wk, 2),
                       "hbm_bytes_per_launch": int(round((2 * fk + wk) * 1024))}
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
-                     "`python3 bench.py --steps 100 --warmup 10 --no-cpu --no-extra`; "
+                     "`python3 bench.py --steps 100 --warmup 10 --no-cpu --no-extra --streams 1 --serial`; "
                      "traffic = 2*FETCH_SIZE (gfx950 half-count correction) + WRITE_SIZE",
            "kernels": kernels}
     with open(out, "w") as fh:
