@@ -60,6 +60,12 @@ SIGNATURES = {
     "dpz_timing_enable": (_int, [_int]),
     "dpz_timing_read": (_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64), _int]),
     "dpz_kernel_name": (ctypes.c_char_p, [_int]),
+    "dpz_topk_encode_batch": (_int, [_int, _c_void_p, _c_void_p, _i64, _i64, _c_void_p,
+                                     _c_void_p, _c_void_p, _c_void_p, _size, _int, _c_void_p,
+                                     _c_void_p]),
+    "dpz_decode_average_batch": (_int, [_int, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
+                                        _c_void_p, _c_void_p, _c_void_p, _c_void_p, _int,
+                                        _c_void_p, _size, _int, _c_void_p]),
     "dpz_elias_max_bytes": (_i64, [_i64]),
     "dpz_elias_workspace_bytes": (_size, [_i64, _i64]),
     "dpz_elias_encode": (_int, [_c_void_p, _i64, _c_void_p, _i64, ctypes.POINTER(_i64),

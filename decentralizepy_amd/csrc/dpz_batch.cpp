@@ -1,0 +1,54 @@
+// Batched enqueue of many node codecs (the gossip-round engine, decentralizepy_amd/gossip.py).
+//
+// A simulated round encodes every node's model and folds every node's neighbourhood
+// (reference: each node process calls sharing/PartialModel.py:188-255 get_data_to_send, then
+// sharing/Sharing.py:156-190 _averaging).  With 12-96 nodes per GPU the per-call host cost of a
+// Python enqueue (~30-50 us) exceeds the kernels' device time, so the loop over nodes lives here:
+// node j goes to stream j % n_streams (one workspace per stream), and its sampled-path status
+// word is copied to status[j] (device) on the same stream so the caller reads all of them once.
+#include <hip/hip_runtime.h>
+
+#include "../../include/dpz_codec.h"
+
+extern "C" int dpz_topk_encode_batch(int m, const float* const* x, const float* const* x0,
+                                     int64_t n, int64_t k, int32_t* const* counter,
+                                     int32_t* const* idx_out, float* const* val_out,
+                                     void* const* ws, size_t ws_bytes, int n_streams,
+                                     const dpz_stream_t* streams, int32_t* status) {
+  if (m < 0 || n_streams < 1 || !x || !idx_out || !val_out || !ws || !streams) return DPZ_ERR_ARG;
+  for (int j = 0; j < m; ++j) {
+    const int q = j % n_streams;
+    int rc = dpz_topk_encode(x[j], x0 ? x0[j] : nullptr, nullptr, DPZ_ACC_NONE, x[j], n, k,
+                             idx_out[j], val_out[j], counter ? counter[j] : nullptr, ws[q],
+                             ws_bytes, DPZ_TOPK_ASYNC, streams[q]);
+    if (rc != DPZ_OK) return rc;
+    if (status) {
+      // TopkCtrl.status is the third 32-bit word of the workspace (dpz_topk.h)
+      hipError_t e = hipMemcpyAsync(status + j, static_cast<char*>(ws[q]) + 8, sizeof(int32_t),
+                                    hipMemcpyDeviceToDevice, static_cast<hipStream_t>(streams[q]));
+      if (e != hipSuccess) return (int)e;
+    }
+  }
+  return DPZ_OK;
+}
+
+extern "C" int dpz_decode_average_batch(int m, const float* const* local, float* const* out,
+                                        int64_t n, const int* n_payloads,
+                                        const int32_t* const* idx, const float* const* vals,
+                                        const int64_t* k, const float* w, const float* w_self,
+                                        int flags, void* const* ws, size_t ws_bytes,
+                                        int n_streams, const dpz_stream_t* streams) {
+  if (m < 0 || n_streams < 1 || !local || !out || !n_payloads || !ws || !streams) return DPZ_ERR_ARG;
+  int64_t off = 0;
+  for (int j = 0; j < m; ++j) {
+    const int q = j % n_streams;
+    const int np = n_payloads[j];
+    if (np < 0) return DPZ_ERR_ARG;
+    int rc = dpz_decode_average(local[j], n, np, idx + off, vals + off, k + off, w + off,
+                                w_self ? w_self[j] : 0.0f, flags, out[j], ws[q], ws_bytes,
+                                streams[q]);
+    if (rc != DPZ_OK) return rc;
+    off += np;
+  }
+  return DPZ_OK;
+}

@@ -14,6 +14,7 @@ at N = 11M), and each rank folds its own nodes' neighbourhoods locally.  No redu
 The encode / fold callables are injectable so the sharding and exchange logic can be tested with
 the CPU gloo backend; the defaults are the HIP codec (no CPU fallback).
 """
+import ctypes
 import math
 
 import torch
@@ -58,7 +59,7 @@ class GossipRound:
     """Nodes [lo, hi) of a topology on this rank; ``step()`` runs one full round."""
 
     def __init__(self, adj, x_init, alpha, rank=0, world=1, group=None, encode=None, fold=None,
-                 device=None):
+                 device=None, streams=3):
         """adj: adjacency sets of all nodes; x_init: (hi - lo, N) fp32 tensor with this rank's
         nodes' flat models (device tensor for the HIP codec)."""
         self.adj = adj
@@ -80,55 +81,137 @@ class GossipRound:
                                     device=self.device)
         self.out = torch.empty_like(self.x)
         self.weights = [mh_weights(adj, i) for i in range(self.lo, self.hi)]
-        if encode is None or fold is None:
-            from . import codec
-            self.ws = codec.Workspace(self.device)
         self._encode = encode or self._hip_encode
         self._fold = fold or self._hip_fold
+        self._hip = encode is None and fold is None
+        if self._hip:
+            # the nodes of this rank run as `streams` concurrent codecs (one workspace each):
+            # one node's latency-bound selection tail overlaps another's streaming kernels
+            from . import codec
+            self.streams = [torch.cuda.Stream(self.device) for _ in range(max(1, streams))]
+            self.wss = [codec.Workspace(self.device) for _ in self.streams]
+            self.status = torch.zeros(max(1, self.hi - self.lo), dtype=torch.int32,
+                                      device=self.device)
 
     # ---- default device implementations ---------------------------------------------------
     def _hip_encode(self, x, x0, k, counter, idx_out, val_out):
         from . import codec
         codec.topk_encode(x, k, x0=x0, counter=counter, idx_out=idx_out, val_out=val_out,
-                          workspace=self.ws, asynchronous=True)
+                          workspace=self.wss[0], asynchronous=True)
 
     def _hip_fold(self, local, payloads, weights, w_self, out):
         from . import codec
-        codec.decode_average(local, payloads, weights, w_self, out=out, workspace=self.ws)
-
-    def _complete(self):
-        """Finish the asynchronous encodes (a sampled-path miss re-runs exactly, rarely)."""
-        if self._encode != self._hip_encode:
-            return
-        from . import codec
-        for j in range(self.hi - self.lo):
-            codec.topk_complete(self.x[j], self.k, self.send_idx[j], self.send_val[j], self.ws,
-                                x0=self.x0[j], counter=self.counter[j])
+        codec.decode_average(local, payloads, weights, w_self, out=out, workspace=self.wss[0])
 
     # ---- one round ----------------------------------------------------------------------------
+    @staticmethod
+    def _ptrs(rows):
+        """Host array of device pointers: the rows of a 2-D tensor (computed, no views) or the
+        tensors of a list."""
+        if isinstance(rows, torch.Tensor):
+            base, step = rows.data_ptr(), rows.stride(0) * rows.element_size()
+            return (ctypes.c_void_p * max(1, rows.shape[0]))(
+                *[base + j * step for j in range(rows.shape[0])])
+        return (ctypes.c_void_p * max(1, len(rows)))(*[t.data_ptr() for t in rows])
+
+    def _stream_args(self):
+        m = self.hi - self.lo
+        streams = (ctypes.c_void_p * len(self.streams))(*[s.cuda_stream for s in self.streams])
+        n = self.N
+        k = self.k
+        ws_bytes = min(w.get(n, k).numel() for w in self.wss)
+        wsp = self._ptrs([w.buf for w in self.wss])
+        return m, streams, ws_bytes, wsp
+
     def encode_all(self):
-        for j in range(self.hi - self.lo):
-            self._encode(self.x[j], self.x0[j], self.k, self.counter[j], self.send_idx[j],
-                         self.send_val[j])
-        self._complete()
+        if not self._hip:
+            for j in range(self.hi - self.lo):
+                self._encode(self.x[j], self.x0[j], self.k, self.counter[j], self.send_idx[j],
+                             self.send_val[j])
+            return
+        from . import _lib, codec
+        m, streams, ws_bytes, wsp = self._stream_args()
+        cur = torch.cuda.current_stream(self.device)
+        for st in self.streams:
+            st.wait_stream(cur)
+        # one native call enqueues every node's encode (node j on stream j % S) and copies each
+        # node's sampled-path status word to self.status[j]
+        rc = _lib.lib().dpz_topk_encode_batch(
+            m, self._ptrs(self.x[:m]), self._ptrs(self.x0[:m]), self.N, self.k,
+            self._ptrs(self.counter[:m]), self._ptrs(self.send_idx[:m]),
+            self._ptrs(self.send_val[:m]), wsp, ws_bytes, len(self.streams), streams,
+            self.status.data_ptr())
+        _lib.check(rc, "dpz_topk_encode_batch")
+        for st in self.streams:
+            cur.wait_stream(st)
+        # a sampled-path miss (rare) re-runs that node's selection exactly
+        bad = torch.nonzero(self.status[:m]).flatten().tolist()
+        for j in bad:  # the missed sampled call wrote nothing (no counter update either)
+            codec.topk_encode(self.x[j], self.k, x0=self.x0[j], counter=self.counter[j],
+                              idx_out=self.send_idx[j], val_out=self.send_val[j],
+                              workspace=self.wss[0], exact=True)
 
     def exchange(self):
         if self.world == 1:
-            self.recv_idx[: self.per].copy_(self.send_idx)
-            self.recv_val[: self.per].copy_(self.send_val)
+            self.recv_idx, self.recv_val = self.send_idx, self.send_val  # no copy on one rank
             return
         import torch.distributed as dist
         dist.all_gather_into_tensor(self.recv_idx, self.send_idx, group=self.group)
         dist.all_gather_into_tensor(self.recv_val, self.send_val, group=self.group)
 
+    def _fold_tables(self):
+        """Host tables of the batched fold (payload pointers, sizes, weights), built once: the
+        receive buffers and the neighbourhoods do not change between rounds."""
+        m = self.hi - self.lo
+        counts, idx, val, kk, w, ws_ = [], [], [], [], [], []
+        for j in range(m):
+            nbrs, wj, w_self = self.weights[j]
+            counts.append(len(nbrs))
+            for q in nbrs:
+                idx.append(self.recv_idx[self._slot(q)].data_ptr())
+                val.append(self.recv_val[self._slot(q)].data_ptr())
+                kk.append(self.k)
+            w.extend(wj)
+            ws_.append(w_self)
+        tot = max(1, len(idx))
+        return dict(np=(ctypes.c_int * max(1, m))(*counts), idx=(ctypes.c_void_p * tot)(*idx),
+                    val=(ctypes.c_void_p * tot)(*val), k=(ctypes.c_int64 * tot)(*kk),
+                    w=(ctypes.c_float * tot)(*w), w_self=(ctypes.c_float * max(1, m))(*ws_),
+                    key=(self.recv_idx.data_ptr(), self.recv_val.data_ptr()))
+
     def fold_all(self):
-        for j in range(self.hi - self.lo):
-            nbrs, w, w_self = self.weights[j]
-            payloads = [(self.recv_idx[self._slot(q)], self.recv_val[self._slot(q)]) for q in nbrs]
-            self._fold(self.x[j], payloads, w, w_self, self.out[j])
-        # post step: the averaged model becomes both the model and init_model
-        self.x.copy_(self.out)
-        self.x0.copy_(self.out)
+        nodes = range(self.hi - self.lo)
+        if self._hip:
+            from . import _lib
+            from ._lib import DPZ_FOLD_SELF
+            tab = getattr(self, "_tab", None)
+            if tab is None or tab["key"] != (self.recv_idx.data_ptr(), self.recv_val.data_ptr()):
+                tab = self._tab = self._fold_tables()
+            m = self.hi - self.lo
+            streams = (ctypes.c_void_p * len(self.streams))(*[s.cuda_stream for s in self.streams])
+            maxp = max((len(self.weights[j][0]) for j in nodes), default=1)
+            dws = [w.get_decode(self.N, maxp) for w in self.wss]
+            cur = torch.cuda.current_stream(self.device)
+            for st in self.streams:
+                st.wait_stream(cur)
+            rc = _lib.lib().dpz_decode_average_batch(
+                m, self._ptrs(self.x[:m]), self._ptrs(self.out[:m]), self.N, tab["np"],
+                tab["idx"], tab["val"], tab["k"], tab["w"], tab["w_self"], DPZ_FOLD_SELF,
+                self._ptrs(dws), min(d.numel() for d in dws), len(self.streams), streams)
+            _lib.check(rc, "dpz_decode_average_batch")
+            for st in self.streams:
+                cur.wait_stream(st)
+        else:
+            for j in nodes:
+                nbrs, w, w_self = self.weights[j]
+                payloads = [(self.recv_idx[self._slot(q)], self.recv_val[self._slot(q)])
+                            for q in nbrs]
+                self._fold(self.x[j], payloads, w, w_self, self.out[j])
+        # post step: the averaged model becomes both the model and init_model (reference
+        # Sharing._averaging load_state_dict + PartialModel._post_step): init_model takes the
+        # fold output buffer (swap, no copy), the model gets one copy of it
+        self.x0, self.out = self.out, self.x0
+        self.x.copy_(self.x0)
 
     def _slot(self, node):
         r = node // self.per

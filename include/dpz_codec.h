@@ -119,6 +119,27 @@ int dpz_decode_average(const float* local, int64_t n, int n_payloads, const int3
                        const float* const* vals, const int64_t* k, const float* w, float w_self,
                        int flags, float* out, void* ws, size_t ws_bytes, dpz_stream_t stream);
 
+/* Batched enqueue for a simulated gossip round (decentralizepy_amd/gossip.py): m node codecs,
+ * node j on streams[j % n_streams] with workspace ws[j % n_streams].
+ * dpz_topk_encode_batch == for each j: dpz_topk_encode(x[j], x0[j], NULL, DPZ_ACC_NONE, x[j], n,
+ *   k, idx_out[j], val_out[j], counter[j], ws[q], ws_bytes, DPZ_TOPK_ASYNC, streams[q]), then the
+ *   node's sampled-path status word is copied to status[j] (DEVICE int32[m], may be NULL) on the
+ *   same stream (0 = final; otherwise re-run that node with DPZ_TOPK_EXACT).
+ * dpz_decode_average_batch == for each j: dpz_decode_average(local[j], n, n_payloads[j],
+ *   idx + o_j, vals + o_j, k + o_j, w + o_j, w_self[j], flags, out[j], ws[q], ws_bytes,
+ *   streams[q]) with o_j = sum of n_payloads[< j] (all arrays HOST, holding device pointers).
+ * Replaces the per-node loops of reference node processes (sharing/PartialModel.py:188-255,
+ * sharing/Sharing.py:156-190) run side by side.                                               */
+int dpz_topk_encode_batch(int m, const float* const* x, const float* const* x0, int64_t n,
+                          int64_t k, int32_t* const* counter, int32_t* const* idx_out,
+                          float* const* val_out, void* const* ws, size_t ws_bytes, int n_streams,
+                          const dpz_stream_t* streams, int32_t* status);
+int dpz_decode_average_batch(int m, const float* const* local, float* const* out, int64_t n,
+                             const int* n_payloads, const int32_t* const* idx,
+                             const float* const* vals, const int64_t* k, const float* w,
+                             const float* w_self, int flags, void* const* ws, size_t ws_bytes,
+                             int n_streams, const dpz_stream_t* streams);
+
 /* Multilevel sym2 DWT, mode "symmetric", fp32, pywt-1.1.1-exact summation order.
  * Replaces reference sharing/JWINS/Wavelet.py:12-32 (pywt.wavedec + coeffs_to_array).
  * coeffs layout: [cA_L, cD_L, ..., cD_1], length dpz_wavedec_len(n, level).
