@@ -402,3 +402,56 @@ def test_coscheduled_replace_rejects_aliasing(dev):
     p_val = torch.tensor([1.0], dtype=torch.float32, device=dev)
     with pytest.raises(RuntimeError):  # decode output overlapping the encoder's input
         codec.topk_encode(tx, 10_000, x0=tx0, co_replace=(tx0.clone(), p_idx, p_val, tx))
+
+
+def _sampled_status(ws):
+    return int(ws.buf[8:12].view(torch.int32).item())
+
+
+def test_topk_c5_alpha_0001_stays_on_sampled_path(dev):
+    """C5 (N = 2^26, alpha = 0.001): bit-exact vs the oracle AND no exact-path fallback (the
+    window's top rank is clamped to the largest sample; an open window overflowed the boundary
+    list here)."""
+    codec = _codec()
+    n = 67_108_864
+    k = round(0.001 * n)
+    x, x0 = _inputs(n, seed=4)
+    o_cnt = np.zeros(n, dtype=np.int32)
+    oi, ov = otopk.encode(x, x0, None, otopk.ACC_NONE, k, counter=o_cnt)
+    tx, tx0 = torch.from_numpy(x).to(dev), torch.from_numpy(x0).to(dev)
+    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    ws = codec.Workspace(dev)
+    idx, val = codec.topk_encode(tx, k, x0=tx0, counter=cnt, workspace=ws, asynchronous=True)
+    torch.cuda.synchronize()
+    assert _sampled_status(ws) == 0, "C5 shape fell back to the exact path"
+    np.testing.assert_array_equal(idx.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(val.cpu().numpy()), _bits(ov))
+    np.testing.assert_array_equal(cnt.cpu().numpy(), o_cnt)
+
+
+def test_topk_c3_wavelet_rounds_stay_on_sampled_path(dev):
+    """C3 shape (M = 25,000,009 wavelet coefficients, alpha = 0.01, ADD accumulation with the
+    rewind of selected coefficients, 4 rounds): no exact-path fallback (256 fine bins
+    overflowed the boundary list here) and the last round bit-exact vs the oracle."""
+    codec = _codec()
+    n = 25_000_000
+    m = codec.wavedec_len(n, 4)
+    k = round(0.01 * m)
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(n, device=dev, generator=g)
+    x0 = x - 0.01 * torch.randn(n, device=dev, generator=g)
+    acc = 0.01 * torch.randn(m, device=dev, generator=g)
+    wx, wc = codec.wavedec(x, 4, x0=x0)
+    ws = codec.Workspace(dev)
+    for r in range(4):
+        acc_before = acc.cpu().numpy().copy()
+        idx, val = codec.topk_encode(wc, k, acc=acc, acc_mode=codec.DPZ_ACC_ADD, vals_src=wx,
+                                     workspace=ws, asynchronous=True)
+        torch.cuda.synchronize()
+        assert _sampled_status(ws) == 0, f"round {r} fell back to the exact path"
+    o_acc = acc_before.copy()
+    oi, ov = otopk.encode(wc.cpu().numpy(), None, o_acc, otopk.ACC_ADD, k,
+                          vals_src=wx.cpu().numpy())
+    np.testing.assert_array_equal(idx.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(val.cpu().numpy()), _bits(ov))
+    np.testing.assert_array_equal(_bits(acc.cpu().numpy()), _bits(o_acc))
