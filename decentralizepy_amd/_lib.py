@@ -20,6 +20,8 @@ DPZ_TOPK_STREAM = 0x4
 DPZ_TOPK_TAIL = 0x8
 DPZ_FOLD_SELF = 0x1
 DPZ_FOLD_REPLACE_ONLY = 0x2
+DPZ_FOLD_ZERO_BASE = 0x4
+DPZ_FOLD_ADD_ONLY = 0x8
 DPZ_OK = 0
 DPZ_ERR_ARG = 1001
 DPZ_ERR_WORKSPACE = 1002

@@ -157,12 +157,15 @@ def topk_status(workspace):
 
 
 def decode_average(local, payloads, weights=None, w_self=None, out=None, replace_only=False,
-                   workspace=None):
+                   workspace=None, zero_base=False, add_only=False):
     """Batched replace + Metro-Hastings fold (reference Sharing.py:156-229, PartialModel.py:257-303).
 
     payloads : list of ``(idx int32 device tensor or None, vals fp32 device tensor)``
     weights  : per-payload weights (Python floats, rounded to fp32 like torch does)
     w_self   : weight of the local term, or None for no self term (server variant)
+    zero_base: sparse payloads are zero off their indices (STC's ``T = zeros; T[idx] = params``)
+               and the fold starts from +0.0 (DPZ_FOLD_ZERO_BASE)
+    add_only : one payload, ``out = local + T`` with T zero-based (DPZ_FOLD_ADD_ONLY)
     """
     _require(local, torch.float32, "local")
     n = local.numel()
@@ -185,7 +188,10 @@ def decode_average(local, payloads, weights=None, w_self=None, out=None, replace
         val_arr[i] = vals.data_ptr()
         k_arr[i] = vals.numel()
         w_arr[i] = float(weights[i]) if weights is not None else 1.0
-    flags = (DPZ_FOLD_SELF if w_self is not None else 0) | (DPZ_FOLD_REPLACE_ONLY if replace_only else 0)
+    flags = ((DPZ_FOLD_SELF if w_self is not None else 0)
+             | (DPZ_FOLD_REPLACE_ONLY if replace_only else 0)
+             | (_lib.DPZ_FOLD_ZERO_BASE if zero_base else 0)
+             | (_lib.DPZ_FOLD_ADD_ONLY if add_only else 0))
     ws = (workspace or Workspace(local.device)).get_decode(n, npay)
     rc = _lib.lib().dpz_decode_average(_ptr(local), n, npay, idx_arr, val_arr, k_arr, w_arr,
                                        float(w_self) if w_self is not None else 0.0, flags,

@@ -46,6 +46,7 @@ struct FoldArgs {
   int first;        // total starts from payload 0 (else continue from out)
   int add_self;     // add local * w_self at the end
   int replace_only; // out = t_0
+  int zero_base;    // sparse payloads contribute 0 off their entries; first term = +0 + t0*w0
   float w_self;
   FoldPayload p[FOLD_MAXP];
 };
@@ -182,7 +183,8 @@ __global__ void __launch_bounds__(FOLD_THREADS) fold_kernel(FoldArgs a) {
         const float hh[4] = {h4.x, h4.y, h4.z, h4.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          tv[e] = (((g4 >> (8 * e)) & 0xFFu) == (uint32_t)p) ? hh[e] : L[q * 4 + e];
+          tv[e] = (((g4 >> (8 * e)) & 0xFFu) == (uint32_t)p) ? hh[e]
+                                                               : (a.zero_base ? 0.0f : L[q * 4 + e]);
       } else {
         if (VEC && i0 + 3 < thi) {
           float4 v = *reinterpret_cast<const float4*>(P.val + i0);
@@ -198,7 +200,8 @@ __global__ void __launch_bounds__(FOLD_THREADS) fold_kernel(FoldArgs a) {
           acc[q * 4 + e] = tv[e];
         } else {
           const float term = tv[e] * w;
-          acc[q * 4 + e] = (a.first && p == 0) ? term : acc[q * 4 + e] + term;
+          acc[q * 4 + e] = (a.first && p == 0) ? (a.zero_base ? 0.0f + term : term)
+                                               : acc[q * 4 + e] + term;
         }
       }
     }
@@ -251,8 +254,11 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
   if (n == 0) return DPZ_OK;
   if (!local || !out || local == out) return DPZ_ERR_ARG;
   const bool replace_only = (flags & DPZ_FOLD_REPLACE_ONLY) != 0;
-  if (replace_only && n_payloads != 1) return DPZ_ERR_ARG;
-  if (n_payloads > 0 && (!vals || !k || (!replace_only && !w))) return DPZ_ERR_ARG;
+  const bool add_only = (flags & DPZ_FOLD_ADD_ONLY) != 0;
+  const bool zero_base = (flags & DPZ_FOLD_ZERO_BASE) != 0;
+  if ((replace_only || add_only) && n_payloads != 1) return DPZ_ERR_ARG;
+  if (replace_only && add_only) return DPZ_ERR_ARG;
+  if (n_payloads > 0 && (!vals || !k || (!replace_only && !add_only && !w))) return DPZ_ERR_ARG;
   // payload i is dense (a full model) iff idx[i] == NULL and k[i] == n
   auto is_dense = [&](int i) { return (!idx || !idx[i]) && k[i] == n; };
   for (int i = 0; i < n_payloads; ++i) {
@@ -281,16 +287,26 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
   // one sparse payload, replace only: single-kernel range-partitioned copy + scatter
   if (replace_only && !is_dense(0) && k[0] > 0 && vec) {
     const int64_t nc = replace_chunks(k[0]);
-    return launch_replace(ReplaceJob{local, idx[0], vals[0], k[0], n, out, 0, nc}, st);
+    return launch_replace(ReplaceJob{local, idx[0], vals[0], k[0], n, out, 0, nc, 0}, st);
+  }
+  if (add_only) {
+    // out = local + T_0: the range-partitioned chunk kernel in add mode (k = 0: one virtual
+    // chunk list over [0, n) with no entries is not possible, so k = 0 and dense payloads take
+    // the fold path below with weight 1 and the self term)
+    if (!is_dense(0) && k[0] > 0 && vec) {
+      const int64_t nc = replace_chunks(k[0]);
+      return launch_replace(ReplaceJob{local, idx[0], vals[0], k[0], n, out, 0, nc, 1}, st);
+    }
   }
   for (int base = 0; base < n_payloads; base += FOLD_MAXP) {
     FoldArgs fa{};
     fa.local = local; fa.out = out; fa.starts = starts; fa.n = n; fa.ntiles = ntiles;
     fa.np = (n_payloads - base) < FOLD_MAXP ? (n_payloads - base) : FOLD_MAXP;
     fa.first = base == 0 ? 1 : 0;
-    fa.add_self = (base + fa.np == n_payloads && (flags & DPZ_FOLD_SELF)) ? 1 : 0;
+    fa.add_self = (base + fa.np == n_payloads && ((flags & DPZ_FOLD_SELF) || add_only)) ? 1 : 0;
     fa.replace_only = replace_only ? 1 : 0;
-    fa.w_self = w_self;
+    fa.zero_base = (zero_base || add_only) ? 1 : 0;
+    fa.w_self = add_only ? 1.0f : w_self;
     int64_t kmax = -1;
     for (int i = 0; i < fa.np; ++i) {
       // an empty sparse payload gets a dummy non-null idx (never read: its range is empty)
@@ -298,7 +314,7 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
                     : ((idx && idx[base + i]) ? idx[base + i] : reinterpret_cast<const int32_t*>(starts));
       fa.p[i].val = vals[base + i];
       fa.p[i].k = k[base + i];
-      fa.p[i].w = replace_only ? 1.0f : w[base + i];
+      fa.p[i].w = (replace_only || add_only) ? 1.0f : w[base + i];
       if (fa.p[i].idx && fa.p[i].k > kmax) kmax = fa.p[i].k;
     }
     if (kmax >= 0) {

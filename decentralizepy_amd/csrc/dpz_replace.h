@@ -31,6 +31,7 @@ struct ReplaceJob {
   int64_t k, n;
   float* out;
   int64_t c0, c1;  // chunks [c0, c1) of this launch
+  int add;         // 0: out = local with entries replaced; 1: out = local + T (T zero-based)
 };
 
 static inline int64_t replace_chunks(int64_t k) { return (k + RP_E - 1) / RP_E; }
@@ -59,19 +60,29 @@ __device__ __forceinline__ void replace_chunk(const ReplaceJob& j, int64_t c, bo
       const int64_t a4 = (a + 3) & ~int64_t(3);
       const int64_t b4 = b & ~int64_t(3);
       if (a4 < b4) {
-        if (t < a4 - a) out[a + t] = local[a + t];
-        if (t < b - b4) out[b4 + t] = local[b4 + t];
+        if (t < a4 - a) out[a + t] = j.add ? local[a + t] + 0.0f : local[a + t];
+        if (t < b - b4) out[b4 + t] = j.add ? local[b4 + t] + 0.0f : local[b4 + t];
         const rp_v4f* __restrict__ lv = reinterpret_cast<const rp_v4f*>(local);
         rp_v4f* __restrict__ ov = reinterpret_cast<rp_v4f*>(out);
         const int64_t q1 = b4 >> 2;
         int64_t q = (a4 >> 2) + t;
+        // replace: a bit copy; add: out = local + 0.0 off the entries, as the reference's dense
+        // `local + T` (fl(-0 + +0) = +0, NaNs quieted) — a uniform branch per launch
+        const bool add = j.add != 0;
+        const rp_v4f z = {0.f, 0.f, 0.f, 0.f};
         for (; q + 3 * 256 < q1; q += 4 * 256) {
 #if DPZ_REPLACE_NT >= 2
-          const rp_v4f v0 = __builtin_nontemporal_load(&lv[q]), v1 = __builtin_nontemporal_load(&lv[q + 256]),
-                       v2 = __builtin_nontemporal_load(&lv[q + 512]), v3 = __builtin_nontemporal_load(&lv[q + 768]);
+          rp_v4f v0 = __builtin_nontemporal_load(&lv[q]), v1 = __builtin_nontemporal_load(&lv[q + 256]),
+                 v2 = __builtin_nontemporal_load(&lv[q + 512]), v3 = __builtin_nontemporal_load(&lv[q + 768]);
 #else
-          const rp_v4f v0 = lv[q], v1 = lv[q + 256], v2 = lv[q + 512], v3 = lv[q + 768];
+          rp_v4f v0 = lv[q], v1 = lv[q + 256], v2 = lv[q + 512], v3 = lv[q + 768];
 #endif
+          if (add) {
+            v0 = v0 + z;
+            v1 = v1 + z;
+            v2 = v2 + z;
+            v3 = v3 + z;
+          }
 #if DPZ_REPLACE_NT >= 1
           __builtin_nontemporal_store(v0, &ov[q]);
           __builtin_nontemporal_store(v1, &ov[q + 256]);
@@ -84,14 +95,14 @@ __device__ __forceinline__ void replace_chunk(const ReplaceJob& j, int64_t c, bo
           ov[q + 768] = v3;
 #endif
         }
-        for (; q < q1; q += 256) ov[q] = lv[q];
+        for (; q < q1; q += 256) ov[q] = add ? lv[q] + z : lv[q];
       } else {
-        for (int64_t i = a + t; i < b; i += 256) out[i] = local[i];
+        for (int64_t i = a + t; i < b; i += 256) out[i] = j.add ? local[i] + 0.0f : local[i];
       }
     }
   }
   __syncthreads();  // the range copy is in place before this chunk's entries overwrite it
-  if (my_i >= 0 && my_i < j.n) j.out[my_i] = my_v;
+  if (my_i >= 0 && my_i < j.n) j.out[my_i] = j.add ? j.local[my_i] + my_v : my_v;
 }
 
 // A whole block of blockDim.x (a multiple of 256) threads: sub-block s runs chunk

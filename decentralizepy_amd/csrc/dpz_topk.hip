@@ -142,7 +142,7 @@ extern "C" int dpz_topk_encode_replace(const float* x, const float* x0, float* a
       overlaps(r_out, ob, idx_out, (size_t)k * 4) || overlaps(r_out, ob, val_out, (size_t)k * 4) ||
       overlaps(r_out, ob, ws, ws_bytes) || overlaps(r_out, ob, r_ws, r_ws_bytes))
     return DPZ_ERR_ARG;
-  const ReplaceJob job{r_local, r_idx, r_val, r_k, r_n, r_out, 0, replace_chunks(r_k)};
+  const ReplaceJob job{r_local, r_idx, r_val, r_k, r_n, r_out, 0, replace_chunks(r_k), 0};
   const bool r_vec = ((reinterpret_cast<uintptr_t>(r_local) | reinterpret_cast<uintptr_t>(r_out)) & 15u) == 0;
   const bool carried = n > 0 && k > 0 && r_k > 0 && r_vec && !(flags & DPZ_TOPK_EXACT) &&
                        use_sampled(n, k);

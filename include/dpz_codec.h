@@ -56,6 +56,11 @@ typedef void* dpz_stream_t; /* hipStream_t */
 /* ---- fold flags ---- */
 #define DPZ_FOLD_SELF 0x1         /* add the local term w_self*local after the payloads        */
 #define DPZ_FOLD_REPLACE_ONLY 0x2 /* out = local with payload[0] values replaced (no weights)  */
+#define DPZ_FOLD_ZERO_BASE 0x4    /* sparse payloads are zero off their indices, not local, and
+                                     the fold starts from +0.0 (reference STC.py:181-206, 336-361:
+                                     T = zeros; T[idx] = params; total = zeros; total += w*T)  */
+#define DPZ_FOLD_ADD_ONLY 0x8     /* n_payloads == 1: out = local + T_0 with T_0 zero-based
+                                     (reference STC.py:290-303 process_received)              */
 
 int dpz_abi_version(void);
 const char* dpz_error_string(int code);
@@ -113,6 +118,9 @@ int dpz_topk_complete(const float* x, const float* x0, float* acc, int acc_mode,
  * The local term is present only with DPZ_FOLD_SELF.  idx/vals/k/w are HOST arrays of length
  * n_payloads holding DEVICE pointers / sizes / fp32 weights.  out may not alias local.
  * DPZ_FOLD_REPLACE_ONLY: n_payloads == 1, out = t_0 (no multiply).
+ * DPZ_FOLD_ZERO_BASE: t_i[j] = 0 where payload i has no entry (instead of local[j]) and the
+ *   first term is fl(+0.0 + fl(t_0[j]*w[0])).  DPZ_FOLD_ADD_ONLY: n_payloads == 1,
+ *   out[j] = fl(local[j] + T_0[j]) with T_0 zero-based (no weights).
  * ws: device scratch of at least dpz_decode_workspace_bytes(n, n_payloads) bytes.              */
 size_t dpz_decode_workspace_bytes(int64_t n, int n_payloads);
 int dpz_decode_average(const float* local, int64_t n, int n_payloads, const int32_t* const* idx,

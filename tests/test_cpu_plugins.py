@@ -91,3 +91,13 @@ def test_elias_fails_loudly_without_gpu():
     from decentralizepy_amd.compression.Elias import Elias
     with pytest.raises(RuntimeError, match="no CPU path|CPU fallback"):
         Elias().compress(np.array([1, 5, 9], np.int32))
+
+
+def test_stc_constructor_keyword_surface_matches_reference():
+    """reference sharing/STC.py:16-31"""
+    from decentralizepy_amd.sharing.STC import STC
+    params = list(inspect.signature(STC.__init__).parameters)
+    assert params[:9] == ["self", "rank", "machine_id", "communication", "mapping", "graph",
+                          "model", "dataset", "log_dir"]
+    assert params[9:] == ["alpha", "dict_ordered", "change_transformer", "compress",
+                          "compression_package", "compression_class", "float_precision"]
