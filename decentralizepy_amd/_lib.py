@@ -22,6 +22,10 @@ DPZ_FOLD_SELF = 0x1
 DPZ_FOLD_REPLACE_ONLY = 0x2
 DPZ_FOLD_ZERO_BASE = 0x4
 DPZ_FOLD_ADD_ONLY = 0x8
+DPZ_FOLD_ACCUMULATE = 0x10
+DPZ_EW_SUB = 1
+DPZ_EW_ADD = 2
+DPZ_EW_CHOCO = 3
 DPZ_OK = 0
 DPZ_ERR_ARG = 1001
 DPZ_ERR_WORKSPACE = 1002
@@ -44,6 +48,11 @@ SIGNATURES = {
                                        _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
                                        _int, _c_void_p, _c_void_p, _c_void_p, _i64, _i64,
                                        _c_void_p, _c_void_p, _size, _c_void_p]),
+    "dpz_topk_threshold": (_int, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _i64, _c_void_p,
+                                  _size, ctypes.POINTER(_i64), _c_void_p]),
+    "dpz_mask_below_threshold": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p]),
+    "dpz_elementwise": (_int, [_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_float, _i64,
+                               _c_void_p, _c_void_p]),
     "dpz_topk_complete": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64, _i64,
                                  _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
                                  ctypes.POINTER(_int), _c_void_p]),

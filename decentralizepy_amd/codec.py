@@ -9,11 +9,14 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import (DPZ_ACC_ACCUMULATE, DPZ_ACC_ADD, DPZ_ACC_NONE, DPZ_FOLD_REPLACE_ONLY,
+from ._lib import (DPZ_ACC_ACCUMULATE, DPZ_ACC_ADD, DPZ_ACC_NONE, DPZ_EW_ADD, DPZ_EW_CHOCO,
+                   DPZ_EW_SUB, DPZ_FOLD_REPLACE_ONLY,
                    DPZ_FOLD_SELF, DPZ_TOPK_ASYNC, DPZ_TOPK_EXACT, DPZ_TOPK_STREAM,
                    DPZ_TOPK_TAIL, check)
 
-__all__ = ["DPZ_ACC_NONE", "DPZ_ACC_ACCUMULATE", "DPZ_ACC_ADD", "Workspace", "topk_encode",
+__all__ = ["DPZ_ACC_NONE", "DPZ_ACC_ACCUMULATE", "DPZ_ACC_ADD", "DPZ_EW_SUB", "DPZ_EW_ADD",
+           "DPZ_EW_CHOCO", "Workspace", "topk_encode",
+           "topk_threshold", "mask_below_threshold", "elementwise",
            "topk_complete", "decode_average", "replace", "wavedec_len", "wavedec", "waverec",
            "pack_fp16", "unpack_fp16", "elias_encode", "elias_decode",
            "KernelTimer"]
@@ -157,7 +160,7 @@ def topk_status(workspace):
 
 
 def decode_average(local, payloads, weights=None, w_self=None, out=None, replace_only=False,
-                   workspace=None, zero_base=False, add_only=False):
+                   workspace=None, zero_base=False, add_only=False, accumulate=False):
     """Batched replace + Metro-Hastings fold (reference Sharing.py:156-229, PartialModel.py:257-303).
 
     payloads : list of ``(idx int32 device tensor or None, vals fp32 device tensor)``
@@ -166,6 +169,7 @@ def decode_average(local, payloads, weights=None, w_self=None, out=None, replace
     zero_base: sparse payloads are zero off their indices (STC's ``T = zeros; T[idx] = params``)
                and the fold starts from +0.0 (DPZ_FOLD_ZERO_BASE)
     add_only : one payload, ``out = local + T`` with T zero-based (DPZ_FOLD_ADD_ONLY)
+    accumulate: ``out`` holds a running total the fold continues (DPZ_FOLD_ACCUMULATE)
     """
     _require(local, torch.float32, "local")
     n = local.numel()
@@ -191,12 +195,53 @@ def decode_average(local, payloads, weights=None, w_self=None, out=None, replace
     flags = ((DPZ_FOLD_SELF if w_self is not None else 0)
              | (DPZ_FOLD_REPLACE_ONLY if replace_only else 0)
              | (_lib.DPZ_FOLD_ZERO_BASE if zero_base else 0)
-             | (_lib.DPZ_FOLD_ADD_ONLY if add_only else 0))
+             | (_lib.DPZ_FOLD_ADD_ONLY if add_only else 0)
+             | (_lib.DPZ_FOLD_ACCUMULATE if accumulate else 0))
     ws = (workspace or Workspace(local.device)).get_decode(n, npay)
     rc = _lib.lib().dpz_decode_average(_ptr(local), n, npay, idx_arr, val_arr, k_arr, w_arr,
                                        float(w_self) if w_self is not None else 0.0, flags,
                                        _ptr(out), _ptr(ws), ws.numel(), _stream(local.device))
     check(rc, "dpz_decode_average")
+    return out
+
+
+def topk_threshold(x, k, workspace=None, cap=None):
+    """Choco's threshold selection (reference sharing/Choco.py:117-161): every element with
+    ``|x| >= T`` (T = the k-th largest |x|, all ties kept; 0 when k == 0) that is nonzero, in
+    ascending index order.  Returns ``(idx int32[c], vals fp32[c])`` (blocks for the count)."""
+    _require(x, torch.float32, "x")
+    n = x.numel()
+    cap = n if cap is None else int(cap)
+    idx = torch.empty(max(cap, 1), dtype=torch.int32, device=x.device)
+    val = torch.empty(max(cap, 1), dtype=torch.float32, device=x.device)
+    ws = (workspace or Workspace(x.device)).get(n, int(k))
+    cnt = ctypes.c_int64(0)
+    rc = _lib.lib().dpz_topk_threshold(_ptr(x), n, int(k), _ptr(idx), _ptr(val), cap, _ptr(ws),
+                                       ws.numel(), ctypes.byref(cnt), _stream(x.device))
+    check(rc, "dpz_topk_threshold")
+    c = int(cnt.value)
+    return idx[:c], val[:c]
+
+
+def mask_below_threshold(x, workspace, out=None):
+    """``x[|x| < T] = 0`` with T of the last :func:`topk_threshold` on ``workspace``."""
+    _require(x, torch.float32, "x")
+    out = x if out is None else out
+    rc = _lib.lib().dpz_mask_below_threshold(_ptr(x), x.numel(), _ptr(workspace.buf), _ptr(out),
+                                             _stream(x.device))
+    check(rc, "dpz_mask_below_threshold")
+    return out
+
+
+def elementwise(op, a, b, d=None, c=0.0, out=None):
+    """fp32 elementwise helpers of the Choco update (DPZ_EW_SUB / ADD / CHOCO)."""
+    for t, nm in ((a, "a"), (b, "b"), (d, "d")):
+        _require(t, torch.float32, nm)
+    if out is None:
+        out = torch.empty_like(a)
+    rc = _lib.lib().dpz_elementwise(int(op), _ptr(a), _ptr(b), _ptr(d), float(c), a.numel(),
+                                    _ptr(out), _stream(a.device))
+    check(rc, "dpz_elementwise")
     return out
 
 

@@ -95,7 +95,7 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t* wsum
   return x - v + off;
 }
 
-__device__ __forceinline__ bool aligned16(const void* p) {
+__host__ __device__ __forceinline__ bool aligned16(const void* p) {
   return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
 }
 

@@ -279,7 +279,7 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
     fa.local = local; fa.out = out; fa.starts = starts; fa.n = n; fa.ntiles = ntiles;
     fa.np = 0; fa.first = 0;
     fa.add_self = (flags & DPZ_FOLD_SELF) ? 1 : 0; fa.w_self = w_self;
-    DPZ_HIP_TRY(hipMemsetAsync(out, 0, n * sizeof(float), st));
+    if (!(flags & DPZ_FOLD_ACCUMULATE)) DPZ_HIP_TRY(hipMemsetAsync(out, 0, n * sizeof(float), st));
     if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<true><<<grid, FOLD_THREADS, 0, st>>>(fa));
     else DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<false><<<grid, FOLD_THREADS, 0, st>>>(fa));
     return DPZ_OK;
@@ -302,7 +302,7 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
     FoldArgs fa{};
     fa.local = local; fa.out = out; fa.starts = starts; fa.n = n; fa.ntiles = ntiles;
     fa.np = (n_payloads - base) < FOLD_MAXP ? (n_payloads - base) : FOLD_MAXP;
-    fa.first = base == 0 ? 1 : 0;
+    fa.first = (base == 0 && !(flags & DPZ_FOLD_ACCUMULATE)) ? 1 : 0;
     fa.add_self = (base + fa.np == n_payloads && ((flags & DPZ_FOLD_SELF) || add_only)) ? 1 : 0;
     fa.replace_only = replace_only ? 1 : 0;
     fa.zero_base = (zero_base || add_only) ? 1 : 0;

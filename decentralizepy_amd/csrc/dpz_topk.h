@@ -237,7 +237,10 @@ struct EncodeArgs {
 };
 
 // dpz_topk_exact.hip / dpz_topk_sampled.hip
-int run_exact(const EncodeArgs& a, const WsLayout& L, int rekey, bool vec);
+// keep_ties: select every key >= T (the k-th largest key), no zero keys when T == 0, writing at
+// most cap entries; the selected count is left in TopkCtrl.nbound
+int run_exact(const EncodeArgs& a, const WsLayout& L, int rekey, bool vec, int keep_ties = 0,
+              int64_t cap = 0);
 // phases: bit 0 = streaming pass (sample, filter), bit 1 = selection tail (select .. compact)
 int run_sampled(const EncodeArgs& a, const WsLayout& L, bool vec, int phases = 3);
 static inline bool use_sampled(int64_t n, int64_t k) {

@@ -160,6 +160,28 @@ extern "C" int dpz_topk_encode_replace(const float* x, const float* x0, float* a
   return dpz_topk_dispatch(a, flags);
 }
 
+extern "C" int dpz_topk_threshold(const float* x, int64_t n, int64_t k, int32_t* idx_out,
+                                  float* val_out, int64_t cap, void* ws, size_t ws_bytes,
+                                  int64_t* count, dpz_stream_t stream) {
+  EncodeArgs a{x, nullptr, nullptr, DPZ_ACC_NONE, x, n, k, idx_out, val_out, nullptr,
+               static_cast<char*>(ws), static_cast<hipStream_t>(stream)};
+  if (cap < 0 || !count) return DPZ_ERR_ARG;
+  int rc = validate(a, ws_bytes);
+  if (rc != DPZ_OK) return rc;
+  *count = 0;
+  if (n == 0) return DPZ_OK;
+  if (cap > 0 && (!idx_out || !val_out)) return DPZ_ERR_ARG;
+  const WsLayout L = ws_layout(n);
+  rc = run_exact(a, L, 0, all_aligned(a), 1, cap);
+  if (rc != DPZ_OK) return rc;
+  uint32_t c = 0;
+  DPZ_HIP_TRY(hipMemcpyAsync(&c, a.ws + L.ctrl + offsetof(TopkCtrl, nbound), sizeof(c),
+                             hipMemcpyDeviceToHost, a.st));
+  DPZ_HIP_TRY(hipStreamSynchronize(a.st));
+  *count = c;
+  return c > (uint64_t)cap ? DPZ_ERR_ARG : DPZ_OK;
+}
+
 extern "C" int dpz_topk_complete(const float* x, const float* x0, float* acc, int acc_mode,
                                  const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
                                  float* val_out, int32_t* counter, void* ws, size_t ws_bytes,

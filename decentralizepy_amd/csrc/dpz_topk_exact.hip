@@ -104,12 +104,20 @@ __global__ void __launch_bounds__(256) exact_count_kernel(KeySrc s, int64_t n, c
 }
 
 // One block of 1024 threads: per-block output offsets and tie allotments (in index order).
-__global__ void __launch_bounds__(1024) exact_scan_kernel(const TopkCtrl* ctrl, int64_t nblk,
+// Ties taken at the threshold T = ctrl->prefix: the k-th-key tie allotment (top-k), or with
+// keep_ties (threshold selection, reference sharing/Choco.py:117-140) every tie — except when
+// T == 0, where exact zeros are not selected (Choco sends nonzero(q), Choco.py:148-161).
+__device__ __forceinline__ uint32_t exact_ties(const TopkCtrl* ctrl, int keep_ties) {
+  if (!keep_ties) return ctrl->krem;
+  return ctrl->prefix == 0u ? 0u : 0xFFFFFFFFu;
+}
+
+__global__ void __launch_bounds__(1024) exact_scan_kernel(TopkCtrl* ctrl, int64_t nblk,
                                                           const uint32_t* blk_gt,
                                                           const uint32_t* blk_eq, uint32_t* blk_off,
-                                                          uint32_t* blk_eqb) {
+                                                          uint32_t* blk_eqb, int keep_ties) {
   __shared__ uint64_t wsum[16];
-  const uint64_t ties = ctrl->krem;
+  const uint64_t ties = exact_ties(ctrl, keep_ties);
   uint64_t carry_eq = 0, carry_off = 0;
   for (int64_t base = 0; base < nblk; base += 1024) {
     const int64_t b = base + threadIdx.x;
@@ -128,6 +136,7 @@ __global__ void __launch_bounds__(1024) exact_scan_kernel(const TopkCtrl* ctrl, 
     carry_eq += te;
     carry_off += ts;
   }
+  if (threadIdx.x == 0) ctrl->nbound = (uint32_t)carry_off;  // entries selected in total
 }
 
 template <bool VEC>
@@ -136,10 +145,11 @@ __global__ void __launch_bounds__(256) exact_write_kernel(KeySrc s, int64_t n, c
                                                           const uint32_t* blk_eqb,
                                                           const float* vals_src, int32_t* idx_out,
                                                           float* val_out, int32_t* counter,
-                                                          float* rewind, int64_t k) {
+                                                          float* rewind, int64_t k,
+                                                          int keep_ties) {
   __shared__ uint32_t wsum[16];
   const uint32_t T = ctrl->prefix;
-  const uint32_t ties = ctrl->krem;
+  const uint32_t ties = exact_ties(ctrl, keep_ties);
   const uint32_t off0 = blk_off[blockIdx.x];
   const uint32_t eqb = blk_eqb[blockIdx.x];
   const uint32_t quota = ties > eqb ? ties - eqb : 0u;
@@ -193,7 +203,8 @@ __global__ void __launch_bounds__(256) exact_write_kernel(KeySrc s, int64_t n, c
 }
 
 template <bool VEC>
-static int run_exact_t(const EncodeArgs& a, const WsLayout& L, int rekey) {
+static int run_exact_t(const EncodeArgs& a, const WsLayout& L, int rekey, int keep_ties,
+                       int64_t cap) {
   KeySrc s{a.x, a.x0, a.acc, a.acc_mode, rekey};
   TopkCtrl* ctrl = reinterpret_cast<TopkCtrl*>(a.ws + L.ctrl);
   uint32_t* hist = reinterpret_cast<uint32_t*>(a.ws + L.ex_hist);
@@ -216,16 +227,19 @@ static int run_exact_t(const EncodeArgs& a, const WsLayout& L, int rekey) {
   uint32_t* boff = reinterpret_cast<uint32_t*>(a.ws + L.ex_off);
   uint32_t* beqb = reinterpret_cast<uint32_t*>(a.ws + L.ex_eqb);
   DPZ_TIMED(DPZ_KT_EXACT_COUNT, a.st, exact_count_kernel<VEC><<<(unsigned)L.ex_nblk, 256, 0, a.st>>>(s, a.n, ctrl, bgt, beq));
-  DPZ_TIMED(DPZ_KT_EXACT_SCAN, a.st, exact_scan_kernel<<<1, 1024, 0, a.st>>>(ctrl, L.ex_nblk, bgt, beq, boff, beqb));
+  DPZ_TIMED(DPZ_KT_EXACT_SCAN, a.st, exact_scan_kernel<<<1, 1024, 0, a.st>>>(ctrl, L.ex_nblk, bgt, beq, boff, beqb, keep_ties));
   float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE) ? a.acc : nullptr;
   DPZ_TIMED(DPZ_KT_EXACT_WRITE, a.st, exact_write_kernel<VEC><<<(unsigned)L.ex_nblk, 256, 0, a.st>>>(
-      s, a.n, ctrl, boff, beqb, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, a.k));
+      s, a.n, ctrl, boff, beqb, a.vals_src, a.idx_out, a.val_out, a.counter, rewind,
+      keep_ties ? cap : a.k, keep_ties));
   return DPZ_OK;
 }
 
 
-int run_exact(const EncodeArgs& a, const WsLayout& L, int rekey, bool vec) {
-  return vec ? run_exact_t<true>(a, L, rekey) : run_exact_t<false>(a, L, rekey);
+int run_exact(const EncodeArgs& a, const WsLayout& L, int rekey, bool vec, int keep_ties,
+              int64_t cap) {
+  return vec ? run_exact_t<true>(a, L, rekey, keep_ties, cap)
+             : run_exact_t<false>(a, L, rekey, keep_ties, cap);
 }
 
 }  // namespace dpz

@@ -59,6 +59,9 @@ typedef void* dpz_stream_t; /* hipStream_t */
 #define DPZ_FOLD_ZERO_BASE 0x4    /* sparse payloads are zero off their indices, not local, and
                                      the fold starts from +0.0 (reference STC.py:181-206, 336-361:
                                      T = zeros; T[idx] = params; total = zeros; total += w*T)  */
+#define DPZ_FOLD_ACCUMULATE 0x10  /* out holds the running total on entry: the fold continues
+                                     from it instead of starting a new one (Choco.py:433-441:
+                                     s += w * T_i; s += (1 - sum w) * q)                      */
 #define DPZ_FOLD_ADD_ONLY 0x8     /* n_payloads == 1: out = local + T_0 with T_0 zero-based
                                      (reference STC.py:290-303 process_received)              */
 
@@ -99,6 +102,29 @@ int dpz_topk_encode_replace(const float* x, const float* x0, float* acc, int acc
                             const float* r_local, const int32_t* r_idx, const float* r_val,
                             int64_t r_k, int64_t r_n, float* r_out, void* r_ws, size_t r_ws_bytes,
                             dpz_stream_t stream);
+/* Threshold selection keeping every tie (reference sharing/Choco.py:117-161:
+ * cutoff = kthvalue(-|x|, k); x[|x| < -cutoff] = 0; then nonzero()): T = the k-th largest key
+ * |x| (T = 0 when k == 0), selects every i with key(x[i]) >= T and x[i] != 0, in ascending
+ * index order: idx_out[j], val_out[j] = x[idx_out[j]], at most cap entries.  Blocks; *count
+ * (host) = the number selected; returns DPZ_ERR_ARG (with *count set) if it exceeds cap.
+ * The selected threshold key stays readable on the device for dpz_mask_below_threshold.       */
+int dpz_topk_threshold(const float* x, int64_t n, int64_t k, int32_t* idx_out, float* val_out,
+                       int64_t cap, void* ws, size_t ws_bytes, int64_t* count,
+                       dpz_stream_t stream);
+/* out[i] = key(x[i]) < T ? +0.0f : x[i], T = the threshold key of the last dpz_topk_threshold on
+ * this workspace (Choco's in-place sparsification of q, Choco.py:117-140).  out may alias x.   */
+int dpz_mask_below_threshold(const float* x, int64_t n, const void* ws, float* out,
+                             dpz_stream_t stream);
+/* Elementwise fp32 helpers of the Choco update (reference Choco.py:353-447), one rounding per op:
+ *   DPZ_EW_SUB   out = a - b
+ *   DPZ_EW_ADD   out = a + b
+ *   DPZ_EW_CHOCO out = a + c * (b - d)      (x + gamma * (s - x_hat))
+ * out may alias a.  c is rounded to fp32 like a torch scalar multiply.                        */
+#define DPZ_EW_SUB 1
+#define DPZ_EW_ADD 2
+#define DPZ_EW_CHOCO 3
+int dpz_elementwise(int op, const float* a, const float* b, const float* d, float c, int64_t n,
+                    float* out, dpz_stream_t stream);
 /* Completes a DPZ_TOPK_ASYNC encode issued with the SAME arguments: synchronises `stream`,
  * and if the sampled path reported a miss, re-runs the selection exactly (blocking).
  * *used_fallback (host, may be NULL) is set to 1 when that happened.                         */

@@ -101,3 +101,11 @@ def test_stc_constructor_keyword_surface_matches_reference():
                           "model", "dataset", "log_dir"]
     assert params[9:] == ["alpha", "dict_ordered", "change_transformer", "compress",
                           "compression_package", "compression_class", "float_precision"]
+
+
+def test_choco_constructor_keyword_surface_matches_reference():
+    """reference sharing/Choco.py:201-216"""
+    from decentralizepy_amd.sharing.Choco import Choco
+    params = list(inspect.signature(Choco.__init__).parameters)
+    assert params[9:] == ["step_size", "alpha", "compress", "compression_package",
+                          "compression_class", "float_precision"]
