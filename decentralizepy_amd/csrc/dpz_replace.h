@@ -13,7 +13,14 @@
 
 namespace dpz {
 
-constexpr int RP_E = 64;  // payload entries per chunk (one 256-thread sub-block)
+#ifndef DPZ_RP_E
+#define DPZ_RP_E 64
+#endif
+constexpr int RP_E = DPZ_RP_E;  // payload entries per chunk (one 256-thread sub-block)
+#ifndef DPZ_RP_U
+#define DPZ_RP_U 8
+#endif
+constexpr int RP_U = DPZ_RP_U;  // float4 loads per thread in flight in the range copy
 typedef float rp_v4f __attribute__((ext_vector_type(4)));
 
 // Non-temporal (streaming) policy of the range copy: 2 = nt loads of local and nt stores of out
@@ -65,37 +72,38 @@ __device__ __forceinline__ void replace_chunk(const ReplaceJob& j, int64_t c, bo
         const rp_v4f* __restrict__ lv = reinterpret_cast<const rp_v4f*>(local);
         rp_v4f* __restrict__ ov = reinterpret_cast<rp_v4f*>(out);
         const int64_t q1 = b4 >> 2;
-        int64_t q = (a4 >> 2) + t;
         // replace: a bit copy; add: out = local + 0.0 off the entries, as the reference's dense
         // `local + T` (fl(-0 + +0) = +0, NaNs quieted) — a uniform branch per launch
         const bool add = j.add != 0;
         const rp_v4f z = {0.f, 0.f, 0.f, 0.f};
-        for (; q + 3 * 256 < q1; q += 4 * 256) {
+        // passes of RP_U float4 per thread: every load of a pass is issued before its stores
+        // (guarded, no remainder loop of dependent load -> store trips)
+        for (int64_t base = (a4 >> 2) + t; base < q1; base += RP_U * 256) {
+          rp_v4f v[RP_U];
+#pragma unroll
+          for (int u = 0; u < RP_U; ++u) {
+            const int64_t q = base + u * 256;
+            if (q < q1) {
 #if DPZ_REPLACE_NT >= 2
-          rp_v4f v0 = __builtin_nontemporal_load(&lv[q]), v1 = __builtin_nontemporal_load(&lv[q + 256]),
-                 v2 = __builtin_nontemporal_load(&lv[q + 512]), v3 = __builtin_nontemporal_load(&lv[q + 768]);
+              v[u] = __builtin_nontemporal_load(&lv[q]);
 #else
-          rp_v4f v0 = lv[q], v1 = lv[q + 256], v2 = lv[q + 512], v3 = lv[q + 768];
+              v[u] = lv[q];
 #endif
-          if (add) {
-            v0 = v0 + z;
-            v1 = v1 + z;
-            v2 = v2 + z;
-            v3 = v3 + z;
+            }
           }
+#pragma unroll
+          for (int u = 0; u < RP_U; ++u) {
+            const int64_t q = base + u * 256;
+            if (q < q1) {
+              const rp_v4f w = add ? v[u] + z : v[u];
 #if DPZ_REPLACE_NT >= 1
-          __builtin_nontemporal_store(v0, &ov[q]);
-          __builtin_nontemporal_store(v1, &ov[q + 256]);
-          __builtin_nontemporal_store(v2, &ov[q + 512]);
-          __builtin_nontemporal_store(v3, &ov[q + 768]);
+              __builtin_nontemporal_store(w, &ov[q]);
 #else
-          ov[q] = v0;
-          ov[q + 256] = v1;
-          ov[q + 512] = v2;
-          ov[q + 768] = v3;
+              ov[q] = w;
 #endif
+            }
+          }
         }
-        for (; q < q1; q += 256) ov[q] = add ? lv[q] + z : lv[q];
       } else {
         for (int64_t i = a + t; i < b; i += 256) out[i] = j.add ? local[i] + 0.0f : local[i];
       }

@@ -169,9 +169,8 @@ struct WaveList {
   uint32_t* gidx;   // this segment's global candidate list
   uint32_t* gkey;
   float* gval;      // candidate values x[idx] (nullptr: not carried, compact gathers vals_src)
-  uint32_t* sidx;   // this wave's LDS stage
-  uint32_t* skey;
-  float* sval;
+  uint32_t* stg;    // this wave's LDS stage: [0, STAGE) idx, [STAGE, 2 STAGE) key, then value
+                    // (one base register; the offsets fold into the ds instructions)
   uint32_t staged;  // entries in the stage (wave-uniform)
   uint32_t flushed; // entries already in the global list (wave-uniform)
 
@@ -181,12 +180,12 @@ struct WaveList {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LDS stage writes done
     __builtin_amdgcn_wave_barrier();
     for (uint32_t j = lane; j < staged; j += 64) {
-      const uint32_t key = skey[j];
+      const uint32_t key = stg[STAGE + j];
       atomicAdd(&h[fine_bin(key, lo, hi, shift)], 1u);
       if (write) {
-        gidx[flushed + j] = sidx[j];
+        gidx[flushed + j] = stg[j];
         gkey[flushed + j] = key;
-        if (gval) gval[flushed + j] = sval[j];
+        if (gval) gval[flushed + j] = __uint_as_float(stg[2 * STAGE + j]);
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -241,8 +240,7 @@ __global__ void __launch_bounds__(256, ACC ? 4 : FOCC) sampled_filter_kernel(
   __shared__ uint32_t h[HBR];
   __shared__ uint32_t win[4];
   __shared__ uint32_t wsum[16];
-  __shared__ uint32_t st_idx[4][STAGE], st_key[4][STAGE];
-  __shared__ float st_val[4][STAGE];
+  __shared__ uint32_t st[4][3 * STAGE];
   STAMP_W(0);
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int b = threadIdx.x; b < HBR; b += 256) h[b] = 0;
@@ -270,8 +268,8 @@ __global__ void __launch_bounds__(256, ACC ? 4 : FOCC) sampled_filter_kernel(
     ctrl->hi = hi;
     ctrl->shift = shift;
   }
-  WaveList L{cidx + seg * CAP, ckey + seg * CAP, cval ? cval + seg * CAP : nullptr,
-             st_idx[wid], st_key[wid], st_val[wid], 0u, 0u};
+  WaveList L{cidx + seg * CAP, ckey + seg * CAP, cval ? cval + seg * CAP : nullptr, st[wid], 0u,
+             0u};
   uint32_t run = 0;
   bool dense = false;
   for (int64_t base = beg; base < end; base += G * 256) {
@@ -301,9 +299,9 @@ __global__ void __launch_bounds__(256, ACC ? 4 : FOCC) sampled_filter_kernel(
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             if (f[e]) {
-              L.sidx[p] = i0 + e;
-              L.skey[p] = kq[e];
-              L.sval[p] = xv[e];  // x[i] (used only when carried: vals_src == x, no rekey)
+              L.stg[p] = i0 + e;
+              L.stg[STAGE + p] = kq[e];
+              L.stg[2 * STAGE + p] = __float_as_uint(xv[e]);  // x[i] (used when carried)
               ++p;
             }
           }

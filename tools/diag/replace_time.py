@@ -1,0 +1,28 @@
+"""Diagnostic: replace-decode kernel time at C2 / 64 MiB on HBM-rotated inputs (KernelTimer)."""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from decentralizepy_amd import codec  # noqa: E402
+
+dev = torch.device("cuda", 0)
+g = torch.Generator(device=dev).manual_seed(1)
+for n in (11_000_000, 16_777_216):
+    k = round(0.01 * n)
+    R = 6
+    locs = [torch.randn(n, device=dev, generator=g) for _ in range(R)]
+    outs = [torch.empty(n, device=dev) for _ in range(R)]
+    pays = [(torch.sort(torch.randperm(n, device=dev, generator=g)[:k])[0].to(torch.int32),
+             torch.randn(k, device=dev, generator=g)) for _ in range(R)]
+    ws = codec.Workspace(dev)
+    for i in range(R):
+        codec.replace(locs[i], *pays[i], out=outs[i], workspace=ws)
+    with codec.KernelTimer() as kt:
+        torch.cuda._sleep(int(50e6))
+        for i in range(60):
+            codec.replace(locs[i % R], *pays[i % R], out=outs[i % R], workspace=ws)
+        torch.cuda.synchronize()
+    us = kt.result["fold"][0] / kt.result["fold"][1] * 1e3
+    print(f"n={n} replace {us:.2f} us  {(8 * n + 8 * k) / us / 1e3:.0f} GB/s", flush=True)
+    del locs, outs, pays
