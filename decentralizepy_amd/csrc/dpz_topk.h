@@ -167,7 +167,8 @@ constexpr int SUBCAP = 256;        // entries per sub-list (more -> miss -> exac
 constexpr int BCAP = NSUB * SUBCAP;  // boundary entries compact can hold (more -> miss)
 constexpr int RANK_MAX = 1024;     // up to this many boundary entries: rank counting, else radix
 constexpr int B_MAX = W_MAX / 4;   // filter blocks (4 wave segments each)
-constexpr int STAGE = 128;         // per-wave LDS candidate staging (flushed in coalesced chunks)
+constexpr int STAGE = 256;         // per-wave LDS candidate staging (flushed in coalesced chunks;
+                                   // >= one group's candidates at large alpha)
 constexpr uint32_t DENSE = 0xFFFFFFFFu;
 
 struct FastGeom {
@@ -177,7 +178,9 @@ struct FastGeom {
   int64_t CAP;    // candidate capacity per wave segment
 };
 
-static inline FastGeom fast_geom(int64_t n) {
+// k > 0: the candidate capacity per segment grows with alpha = k / n (the key window holds
+// about alpha + a few percent of the elements; a segment over capacity turns DENSE, still exact)
+static inline FastGeom fast_geom(int64_t n, int64_t k = 0) {
   FastGeom g;
   int64_t W = (n + W_MIN_RANGE - 1) / W_MIN_RANGE;
   if (W > W_MAX) W = W_MAX;
@@ -186,8 +189,13 @@ static inline FastGeom fast_geom(int64_t n) {
   R = (R + 3) & ~int64_t(3);
   W = (n + R - 1) / R;
   int64_t cap = ((R / 4) + 63) & ~int64_t(63);
+  if (k > n / 16) {
+    const double frac = 1.25 * (double)k / (double)n + 0.05;
+    cap = ((int64_t)(frac * (double)R) + 63) & ~int64_t(63);
+    if (cap > ((R + 63) & ~int64_t(63))) cap = (R + 63) & ~int64_t(63);
+  }
   if (cap < 64) cap = 64;
-  if (cap > 1024) cap = 1024;
+  if (k <= n / 16 && cap > 1024) cap = 1024;
   g.W = W; g.B = (W + 3) / 4; g.R = R; g.CAP = cap;
   return g;
 }
@@ -202,12 +210,12 @@ struct WsLayout {
   FastGeom fg;
 };
 
-static inline WsLayout ws_layout(int64_t n) {
+static inline WsLayout ws_layout(int64_t n, int64_t k = 0) {
   WsLayout L;
   size_t o = 0;
   L.ex_nblk = (n + EX_CHUNK - 1) / EX_CHUNK;
   if (L.ex_nblk < 1) L.ex_nblk = 1;
-  L.fg = fast_geom(n > 0 ? n : 1);
+  L.fg = fast_geom(n > 0 ? n : 1, k);
   L.ctrl = o; o += align256(sizeof(TopkCtrl));
   L.chist = o; o += align256(CB * 4);  // must be zero before the first sampled call (self-cleaning)
   L.ex_hist = o; o += align256(4096 * 4);
@@ -244,7 +252,7 @@ int run_exact(const EncodeArgs& a, const WsLayout& L, int rekey, bool vec, int k
 // phases: bit 0 = streaming pass (sample, filter), bit 1 = selection tail (select .. compact)
 int run_sampled(const EncodeArgs& a, const WsLayout& L, bool vec, int phases = 3);
 static inline bool use_sampled(int64_t n, int64_t k) {
-  return n >= (1 << 18) && k >= 1 && k <= n / 16;
+  return n >= (1 << 18) && k >= 1 && k <= n / 2;
 }
 
 }  // namespace dpz

@@ -64,7 +64,7 @@ static int validate(const EncodeArgs& a, size_t ws_bytes) {
   if (a.n > 0 && !a.x) return DPZ_ERR_ARG;
   if (a.acc_mode != DPZ_ACC_NONE && !a.acc) return DPZ_ERR_ARG;
   if (a.k > 0 && (!a.idx_out || !a.val_out || !a.vals_src)) return DPZ_ERR_ARG;
-  if (a.n > 0 && (!a.ws || ws_bytes < ws_layout(a.n).total)) return DPZ_ERR_WORKSPACE;
+  if (a.n > 0 && (!a.ws || ws_bytes < ws_layout(a.n, a.k).total)) return DPZ_ERR_WORKSPACE;
   return DPZ_OK;
 }
 
@@ -74,11 +74,11 @@ using namespace dpz;
 
 extern "C" size_t dpz_topk_workspace_bytes(int64_t n, int64_t k) {
   (void)k;
-  return ws_layout(n > 0 ? n : 1).total;
+  return ws_layout(n > 0 ? n : 1, k).total;
 }
 
 static int dpz_topk_dispatch(const EncodeArgs& a, int flags) {
-  const WsLayout L = ws_layout(a.n);
+  const WsLayout L = ws_layout(a.n, a.k);
   const bool vec = all_aligned(a);
   if (a.k == 0) {
     if (a.acc_mode == DPZ_ACC_ACCUMULATE && a.n > 0)
@@ -171,7 +171,7 @@ extern "C" int dpz_topk_threshold(const float* x, int64_t n, int64_t k, int32_t*
   *count = 0;
   if (n == 0) return DPZ_OK;
   if (cap > 0 && (!idx_out || !val_out)) return DPZ_ERR_ARG;
-  const WsLayout L = ws_layout(n);
+  const WsLayout L = ws_layout(n, k);
   rc = run_exact(a, L, 0, all_aligned(a), 1, cap);
   if (rc != DPZ_OK) return rc;
   uint32_t c = 0;
@@ -193,7 +193,7 @@ extern "C" int dpz_topk_complete(const float* x, const float* x0, float* acc, in
   if (used_fallback) *used_fallback = 0;
   DPZ_HIP_TRY(hipStreamSynchronize(a.st));
   if (n == 0 || k == 0 || !use_sampled(n, k)) return DPZ_OK;
-  const WsLayout L = ws_layout(n);
+  const WsLayout L = ws_layout(n, k);
   uint32_t status = 0;
   DPZ_HIP_TRY(hipMemcpy(&status, a.ws + L.ctrl + offsetof(TopkCtrl, status), sizeof(status),
                         hipMemcpyDeviceToHost));

@@ -401,22 +401,48 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
   const uint32_t cnt1 = seg0 + 1 < W ? segcnt[seg0 + 1] : 0u;
   // the first 64 entries of both lists are loaded with the counts and the histogram, not after
   // b* is known (CAP >= 64; entries past the count are ignored)
-  uint32_t pk[2], pi[2];
+  constexpr int PFS = 4;  // chunks of 64 per segment held in registers
+  uint32_t pk[2][PFS], pi[2][PFS];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int64_t sg = seg0 + u;
-    pk[u] = sg < W ? ckey[sg * CAP + lane] : 0u;
-    pi[u] = sg < W ? cidx[sg * CAP + lane] : 0u;
+    pk[u][0] = sg < W ? ckey[sg * CAP + lane] : 0u;
+    pi[u][0] = sg < W ? cidx[sg * CAP + lane] : 0u;
   }
   const uint32_t lo = ctrl->lo, hi = ctrl->hi, shift = ctrl->shift;
-  for (int b = t; b < HBR; b += 1024) {
-    uint32_t v[GH_COPIES];
+  // histogram copies (bins t and, for t == 0, the above-window bin HB), then chunks 1 .. PFS-1
+  // of segments with more than 64 candidates — all loads issued before any sum is formed
+  static_assert(HB == 1024, "select: one fine bin per thread + the above-window bin");
+  uint32_t v[GH_COPIES], va[GH_COPIES];
 #pragma unroll
-    for (int c = 0; c < GH_COPIES; ++c) v[c] = ghist[c * GH_STRIDE + b];
-    uint32_t sum = 0;
+  for (int c = 0; c < GH_COPIES; ++c) {
+    v[c] = ghist[c * GH_STRIDE + t];
+    va[c] = t == 0 ? ghist[c * GH_STRIDE + HB] : 0u;
+  }
 #pragma unroll
-    for (int c = 0; c < GH_COPIES; ++c) sum += v[c];
-    gh[b] = sum;
+  for (int u = 0; u < 2; ++u) {
+    const int64_t sg = seg0 + u;
+    const uint32_t cu = u ? cnt1 : cnt0;
+#pragma unroll
+    for (int c = 1; c < PFS; ++c) {
+      const uint32_t j = c * 64u + lane;
+      pk[u][c] = 0u;
+      pi[u][c] = 0u;
+      if (sg < W && cu != DENSE && j < cu) {
+        pk[u][c] = ckey[sg * CAP + j];
+        pi[u][c] = cidx[sg * CAP + j];
+      }
+    }
+  }
+  {
+    uint32_t sum = 0, suma = 0;
+#pragma unroll
+    for (int c = 0; c < GH_COPIES; ++c) {
+      sum += v[c];
+      suma += va[c];
+    }
+    gh[t] = sum;
+    if (t == 0) gh[HB] = suma;
   }
   if (t < SEL_SEGS / 4) fbabove[t] = 0;
   if (t == 0) lcnt = 0;
@@ -466,8 +492,20 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
         const uint32_t j = j0 + lane;
         uint32_t key = 0, b = 0, idx = 0;
         if (j < cnt) {
-          key = j0 == 0 ? pk[u] : ckey[seg * CAP + j];
-          idx = j0 == 0 ? pi[u] : cidx[seg * CAP + j];
+          const uint32_t c = j0 >> 6;
+          if (c < (uint32_t)PFS) {
+            key = 0u;
+            idx = 0u;
+#pragma unroll
+            for (int cc = 0; cc < PFS; ++cc)
+              if (cc == (int)c) {
+                key = pk[u][cc];
+                idx = pi[u][cc];
+              }
+          } else {
+            key = ckey[seg * CAP + j];
+            idx = cidx[seg * CAP + j];
+          }
           b = fine_bin(key, lo, hi, shift);
         }
         above += (uint32_t)__popcll(__ballot(j < cnt && b > bstar));
@@ -816,17 +854,24 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
       abv_before += fb0 + q < fbx ? v[q] : 0u;
     }
   }
-  uint32_t cnt[2], key0[2], idx0[2];
-  float val0[2] = {0.f, 0.f};
+  // candidate chunks of 64 kept in registers per segment (PFC chunks: up to 256 candidates);
+  // chunk 0 is loaded without waiting for the count (CAP >= 64; entries past it are ignored)
+  constexpr int PFC = 4;
+  uint32_t cnt[2], kk[2][PFC], ii[2][PFC];
+  float vv[2][PFC];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int64_t seg = seg0 + u;
     cnt[u] = seg < W ? segcnt[seg] : 0u;
-    // the first 64 list entries are loaded without waiting for the count (CAP >= 64; entries
-    // past the count are ignored)
-    key0[u] = seg < W ? ckey[seg * CAP + lane] : 0u;
-    idx0[u] = seg < W ? cidx[seg * CAP + lane] : 0u;
-    if (cval && seg < W) val0[u] = cval[seg * CAP + lane];
+#pragma unroll
+    for (int c = 0; c < PFC; ++c) {
+      kk[u][c] = 0u;
+      ii[u][c] = 0u;
+      vv[u][c] = 0.f;
+    }
+    kk[u][0] = seg < W ? ckey[seg * CAP + lane] : 0u;
+    ii[u][0] = seg < W ? cidx[seg * CAP + lane] : 0u;
+    if (cval && seg < W) vv[u][0] = cval[seg * CAP + lane];
   }
   if (blockIdx.x == 0) {  // leave the sample histogram zeroed for the next call
     for (int b = t; b < CB; b += 256) chist[b] = 0;
@@ -870,23 +915,38 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     if (grand != (uint32_t)k) ctrl->status = 2;  // internal inconsistency
   }
   if (grand != (uint32_t)k) return;  // identical in every block: nothing is written
-  // count pass (first 64 list entries stay in registers), in-block offsets, write pass
-  bool sel0[2] = {false, false};
+  // chunks 1 .. PFC-1 of every segment with more than 64 candidates: all issued together
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int64_t seg = seg0 + u;
+    if (seg < W && cnt[u] != DENSE && cnt[u] > 64u) {
+#pragma unroll
+      for (int c = 1; c < PFC; ++c) {
+        const uint32_t j = c * 64u + lane;
+        if (j < cnt[u]) {
+          kk[u][c] = ckey[seg * CAP + j];
+          ii[u][c] = cidx[seg * CAP + j];
+          if (cval) vv[u][c] = cval[seg * CAP + j];
+        }
+      }
+    }
+  }
+  // count pass (the first PFC chunks from registers), in-block offsets, write pass
+  auto is_sel = [&](uint32_t key, uint32_t idx) { return key > T || (key == T && idx <= icut); };
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int64_t seg = seg0 + u;
     uint32_t mine = 0;
     if (seg < W && cnt[u] != DENSE) {
-      sel0[u] = (uint32_t)lane < cnt[u] && (key0[u] > T || (key0[u] == T && idx0[u] <= icut));
-      mine = (uint32_t)__popcll(__ballot(sel0[u]));
-      for (uint32_t j0 = 64; j0 < cnt[u]; j0 += 64) {
+#pragma unroll
+      for (int c = 0; c < PFC; ++c) {
+        const uint32_t j = c * 64u + lane;
+        mine += (uint32_t)__popcll(__ballot(j < cnt[u] && is_sel(kk[u][c], ii[u][c])));
+      }
+      for (uint32_t j0 = PFC * 64u; j0 < cnt[u]; j0 += 64) {
         const uint32_t j = j0 + lane;
         bool sel = false;
-        if (j < cnt[u]) {
-          const uint32_t key = ckey[seg * CAP + j];
-          const uint32_t idx = cidx[seg * CAP + j];
-          sel = key > T || (key == T && idx <= icut);
-        }
+        if (j < cnt[u]) sel = is_sel(ckey[seg * CAP + j], cidx[seg * CAP + j]);
         mine += (uint32_t)__popcll(__ballot(sel));
       }
     } else if (seg < W) {
@@ -916,8 +976,12 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
         }
         run += (uint32_t)__popcll(m);
       };
-      emit(sel0[u], idx0[u], val0[u]);
-      for (uint32_t j0 = 64; j0 < cnt[u]; j0 += 64) {
+#pragma unroll
+      for (int c = 0; c < PFC; ++c) {
+        const uint32_t j = c * 64u + lane;
+        if (c * 64u < cnt[u]) emit(j < cnt[u] && is_sel(kk[u][c], ii[u][c]), ii[u][c], vv[u][c]);
+      }
+      for (uint32_t j0 = PFC * 64u; j0 < cnt[u]; j0 += 64) {
         const uint32_t j = j0 + lane;
         bool sel = false;
         uint32_t idx = 0;
@@ -926,7 +990,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
           const uint32_t key = ckey[seg * CAP + j];
           idx = cidx[seg * CAP + j];
           if (cval) v = cval[seg * CAP + j];
-          sel = key > T || (key == T && idx <= icut);
+          sel = is_sel(key, idx);
         }
         emit(sel, idx, v);
       }

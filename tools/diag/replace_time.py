@@ -8,7 +8,7 @@ from decentralizepy_amd import codec  # noqa: E402
 
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev).manual_seed(1)
-for n in (11_000_000, 16_777_216):
+for n in (11_000_000, 16_777_216, 25_000_000):
     k = round(0.01 * n)
     R = 6
     locs = [torch.randn(n, device=dev, generator=g) for _ in range(R)]
