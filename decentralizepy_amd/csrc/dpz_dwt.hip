@@ -18,7 +18,10 @@
 namespace dpz {
 
 constexpr int DWT_MAX_LEVEL = 8;
-constexpr int DWT_TL = 128;  // level-L outputs per block (forward)
+#ifndef DPZ_DWT_TL
+#define DPZ_DWT_TL 128
+#endif
+constexpr int DWT_TL = DPZ_DWT_TL;  // level-L outputs per block (forward)
 constexpr int IDWT_TILE = 4096;
 
 // sym2 filters (fp32 casts of pywt's double coefficients)
