@@ -38,11 +38,12 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 64 MiB secondary line")
-    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "e2e"], default="c2",
+    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "e2e", "shard"], default="c2",
                    help="c2: one node's 11M tensor per GPU (default); c4: the 96-node gossip "
                         "round of eval/96_regular.edges sharded over the GPUs; c3: JWINS wavelet "
                         "25M + 16-payload decode; c5: 256 MiB, 0.1%%, fp16 values; e2e: "
-                        "PCIe-inclusive rates (bench_workloads.py)")
+                        "PCIe-inclusive rates; shard: one C5 tensor sharded over the GPUs "
+                        "(bench_workloads.py)")
     p.add_argument("--rotate", type=int, default=None,
                    help="independent node states cycled per step (default: enough for > 2x L3)")
     p.add_argument("--serial", action="store_true",
@@ -370,9 +371,11 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         return
-    if args.workload in ("c3", "c5", "e2e"):
+    if args.workload in ("c3", "c5", "e2e", "shard"):
         import bench_workloads as bw
-        if args.workload == "c3":
+        if args.workload == "shard":
+            r = bw.shard_case(dev, rank, world, dist, steps=min(args.steps, 40))
+        elif args.workload == "c3":
             r = [bw.c3_case(dev, alpha=a, steps=min(args.steps, 40)) for a in (0.01, 0.1)]
         elif args.workload == "c5":
             r = bw.c5_case(dev, steps=min(args.steps, 40), streams=args.streams)

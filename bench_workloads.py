@@ -210,3 +210,52 @@ def e2e_case(dev, n, alpha, fp16=False, steps=20, warmup=3, seed=7, streams=3):
                 one_node_GiBps=4 * n / t_one / 2 ** 30, one_node_ms_per_step=t_one * 1e3,
                 concurrent_GiBps=4 * n / t_multi / 2 ** 30, concurrent_ms_per_step=t_multi * 1e3,
                 concurrent_pcie_GBps=pcie / t_multi / 1e9, streams=streams)
+
+
+def shard_case(dev, rank, world, dist, n=67_108_864, alpha=0.001, steps=20, warmup=3, seed=9):
+    """One tensor of N parameters sharded over the ranks (SURVEY §8e, C5 on 8 GPUs): the global
+    top-k with one all-gather of every rank's k candidates (decentralizepy_amd/shard.py), then
+    each rank decodes the global payload into its own slice (replace; indices outside the slice
+    fall outside [0, n_r) and are skipped).  Strong scaling: N fixed, value = N params / time."""
+    from decentralizepy_amd import codec
+    from decentralizepy_amd.shard import HipShardOps, sharded_topk_encode
+    k = round(alpha * n)
+    lo = n * rank // world
+    hi = n * (rank + 1) // world
+    nl = hi - lo
+    R = 3
+    g = torch.Generator(device=dev).manual_seed(seed + rank)
+    sets = []
+    for _ in range(R):
+        x = torch.randn(nl, device=dev, generator=g)
+        sets.append(dict(x=x, x0=x - 0.01 * torch.randn(nl, device=dev, generator=g),
+                         cnt=torch.zeros(nl, dtype=torch.int32, device=dev),
+                         out=torch.empty(nl, device=dev)))
+    ops = HipShardOps(dev)
+    ws = codec.Workspace(dev)
+
+    def step(i):
+        d = sets[i % R]
+        idx, val = sharded_topk_encode(d["x"], d["x0"], k, lo, counter=d["cnt"], ops=ops)
+        codec.replace(d["x0"], idx - lo, val, out=d["out"], workspace=ws)
+
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t = (time.perf_counter() - t0) / steps
+    if dist is not None:
+        tt = torch.tensor([t], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    return dict(workload=f"one N={n} tensor sharded over {world} GPU(s), alpha={alpha}: sharded "
+                         f"top-k (one all-gather of {world} x {k} candidates) + slice decode",
+                n=n, k=k, world=world, value=4 * n / t / 2 ** 30, ms_per_step=t * 1e3,
+                scaling="strong")

@@ -53,6 +53,11 @@ SIGNATURES = {
     "dpz_mask_below_threshold": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p]),
     "dpz_elementwise": (_int, [_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_float, _i64,
                                _c_void_p, _c_void_p]),
+    "dpz_gather_change": (_int, [_c_void_p, _c_void_p, _i64, _c_void_p, _i64, _c_void_p,
+                                 _c_void_p]),
+    "dpz_gather_u32": (_int, [_c_void_p, _i64, _c_void_p, _i64, _c_void_p, _c_void_p]),
+    "dpz_scatter_add_i32": (_int, [_c_void_p, _i64, _c_void_p, _i64, _i64, ctypes.c_int32,
+                                   _c_void_p]),
     "dpz_topk_complete": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64, _i64,
                                  _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
                                  ctypes.POINTER(_int), _c_void_p]),

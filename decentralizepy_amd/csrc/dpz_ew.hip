@@ -92,3 +92,78 @@ extern "C" int dpz_mask_below_threshold(const float* x, int64_t n, const void* w
   DPZ_LAUNCH_CHECK();
   return DPZ_OK;
 }
+
+// ---- sharded top-k helpers (decentralizepy_amd/shard.py) --------------------------------------
+namespace dpz {
+
+// out[j] = x[idx[j]] - x0[idx[j]]  (the change at a candidate; x0 may be null: out = x[idx])
+__global__ void __launch_bounds__(256) gather_change_kernel(const float* x, const float* x0,
+                                                            const int32_t* idx, int64_t k,
+                                                            int64_t n, float* out) {
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < k; j += (int64_t)gridDim.x * 256) {
+    const int64_t i = idx[j];
+    float v = 0.0f;
+    if (i >= 0 && i < n) v = x0 ? x[i] - x0[i] : x[i];
+    out[j] = v;
+  }
+}
+
+// out[j] = src[pos[j]] for 32-bit words (bit copy)
+__global__ void __launch_bounds__(256) gather_u32_kernel(const uint32_t* src, int64_t m,
+                                                         const int32_t* pos, int64_t k,
+                                                         uint32_t* out) {
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < k; j += (int64_t)gridDim.x * 256) {
+    const int64_t p = pos[j];
+    out[j] = (p >= 0 && p < m) ? src[p] : 0u;
+  }
+}
+
+// dst[idx[j] - offset] += value for idx[j] in [offset, offset + n)
+__global__ void __launch_bounds__(256) scatter_add_i32_kernel(int32_t* dst, int64_t n,
+                                                              const int32_t* idx, int64_t k,
+                                                              int64_t offset, int32_t value) {
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < k; j += (int64_t)gridDim.x * 256) {
+    const int64_t i = (int64_t)idx[j] - offset;
+    if (i >= 0 && i < n) atomicAdd(&dst[i], value);
+  }
+}
+
+static unsigned small_grid(int64_t k) {
+  int64_t g = (k + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+}  // namespace dpz
+
+extern "C" int dpz_gather_change(const float* x, const float* x0, int64_t n, const int32_t* idx,
+                                 int64_t k, float* out, dpz_stream_t stream) {
+  if (n < 0 || k < 0 || (k > 0 && (!x || !idx || !out))) return DPZ_ERR_ARG;
+  if (k == 0) return DPZ_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  gather_change_kernel<<<small_grid(k), 256, 0, st>>>(x, x0, idx, k, n, out);
+  DPZ_LAUNCH_CHECK();
+  return DPZ_OK;
+}
+
+extern "C" int dpz_gather_u32(const void* src, int64_t m, const int32_t* pos, int64_t k,
+                              void* out, dpz_stream_t stream) {
+  if (m < 0 || k < 0 || (k > 0 && (!src || !pos || !out))) return DPZ_ERR_ARG;
+  if (k == 0) return DPZ_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  gather_u32_kernel<<<small_grid(k), 256, 0, st>>>(static_cast<const uint32_t*>(src), m, pos, k,
+                                                   static_cast<uint32_t*>(out));
+  DPZ_LAUNCH_CHECK();
+  return DPZ_OK;
+}
+
+extern "C" int dpz_scatter_add_i32(int32_t* dst, int64_t n, const int32_t* idx, int64_t k,
+                                   int64_t offset, int32_t value, dpz_stream_t stream) {
+  if (n < 0 || k < 0 || (k > 0 && (!dst || !idx))) return DPZ_ERR_ARG;
+  if (k == 0 || n == 0) return DPZ_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  scatter_add_i32_kernel<<<small_grid(k), 256, 0, st>>>(dst, n, idx, k, offset, value);
+  DPZ_LAUNCH_CHECK();
+  return DPZ_OK;
+}

@@ -125,6 +125,15 @@ int dpz_mask_below_threshold(const float* x, int64_t n, const void* ws, float* o
 #define DPZ_EW_CHOCO 3
 int dpz_elementwise(int op, const float* a, const float* b, const float* d, float c, int64_t n,
                     float* out, dpz_stream_t stream);
+/* Helpers of the sharded top-k (one tensor split over ranks, decentralizepy_amd/shard.py,
+ * SURVEY §8e): out[j] = x[idx[j]] - x0[idx[j]] (x0 may be NULL); out[j] = src[pos[j]] for 32-bit
+ * words; dst[idx[j] - offset] += value where idx[j] - offset lies in [0, n).                    */
+int dpz_gather_change(const float* x, const float* x0, int64_t n, const int32_t* idx, int64_t k,
+                      float* out, dpz_stream_t stream);
+int dpz_gather_u32(const void* src, int64_t m, const int32_t* pos, int64_t k, void* out,
+                   dpz_stream_t stream);
+int dpz_scatter_add_i32(int32_t* dst, int64_t n, const int32_t* idx, int64_t k, int64_t offset,
+                        int32_t value, dpz_stream_t stream);
 /* Completes a DPZ_TOPK_ASYNC encode issued with the SAME arguments: synchronises `stream`,
  * and if the sampled path reported a miss, re-runs the selection exactly (blocking).
  * *used_fallback (host, may be NULL) is set to 1 when that happened.                         */
