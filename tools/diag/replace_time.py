@@ -26,3 +26,20 @@ for n in (11_000_000, 16_777_216, 25_000_000):
     us = kt.result["fold"][0] / kt.result["fold"][1] * 1e3
     print(f"n={n} replace {us:.2f} us  {(8 * n + 8 * k) / us / 1e3:.0f} GB/s", flush=True)
     del locs, outs, pays
+# reference: a plain device copy of the same bytes (torch), HBM-rotated
+for n in (11_000_000, 16_777_216):
+    R = 6
+    src = [torch.randn(n, device=dev, generator=g) for _ in range(R)]
+    dst = [torch.empty(n, device=dev) for _ in range(R)]
+    for i in range(R):
+        dst[i].copy_(src[i])
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(60):
+        dst[i % R].copy_(src[i % R])
+    e1.record()
+    e1.synchronize()
+    us = e0.elapsed_time(e1) / 60 * 1e3
+    print(f"n={n} torch copy {us:.2f} us  {8 * n / us / 1e3:.0f} GB/s", flush=True)
+    del src, dst
