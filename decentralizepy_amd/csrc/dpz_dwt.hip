@@ -75,19 +75,105 @@ __device__ __forceinline__ float conv4(const float* in, int64_t s_in, int64_t o,
   return acc;
 }
 
+constexpr int DWT_SPAN0 = 16 * DWT_TL + 64;  // level-0 span (covers L <= 4 with slack)
+constexpr int DWT_SPAN1 = 8 * DWT_TL + 32;
+constexpr int DWT_NG = (DWT_SPAN0 + 4 + 4 * 256 - 1) / (4 * 256);  // float4 groups per thread
+
+// level-0 input span [s0, e0) of a tile (its level-L outputs [a, b) and the halos below)
+__device__ __forceinline__ void dwt_span(const Levels& LV, int64_t tile, int64_t* s0,
+                                         int64_t* e0) {
+  const int L = LV.level;
+  const int64_t nL = LV.len[L];
+  int64_t sl = tile * DWT_TL;
+  int64_t el = (sl + DWT_TL < nL) ? sl + DWT_TL : nL;
+  for (int l = L; l >= 1; --l) {
+    sl = 2 * sl - 2;
+    el = 2 * el;
+  }
+  *s0 = sl;
+  *e0 = el;
+}
+
+// Every load of a span is issued before any is used (float4 groups from the 4-aligned start below
+// s0; a group not wholly inside [0, n) or an unaligned input takes scalar loads).
+template <bool WD>
+__device__ __forceinline__ void dwt_span_load(const float* __restrict__ x,
+                                              const float* __restrict__ x0, int64_t n, int64_t s0,
+                                              int64_t e0, float4 (&va)[DWT_NG],
+                                              float4 (&vb)[DWT_NG]) {
+  const int64_t g0 = s0 >= 0 ? (s0 & ~int64_t(3)) : -((-s0 + 3) & ~int64_t(3));
+  const bool vec = aligned16(x) && (!WD || aligned16(x0));
+#pragma unroll
+  for (int q = 0; q < DWT_NG; ++q) {
+    const int64_t p = g0 + 4 * (threadIdx.x + 256 * q);
+    va[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    vb[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p < e0) {
+      if (vec && p >= 0 && p + 4 <= n) {
+        va[q] = *reinterpret_cast<const float4*>(x + p);
+        if (WD) vb[q] = *reinterpret_cast<const float4*>(x0 + p);
+      } else {
+        float ta[4] = {0.f, 0.f, 0.f, 0.f}, tb[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (p + e >= 0 && p + e < n) {
+            ta[e] = x[p + e];
+            if (WD) tb[e] = x0[p + e];
+          }
+        }
+        va[q] = make_float4(ta[0], ta[1], ta[2], ta[3]);
+        vb[q] = make_float4(tb[0], tb[1], tb[2], tb[3]);
+      }
+    }
+  }
+}
+
+// The span into LDS (x and / or x - x0) plus pywt's symmetric extension at the array ends.
+template <bool WX, bool WD>
+__device__ __forceinline__ void dwt_span_store(const float4 (&va)[DWT_NG],
+                                               const float4 (&vb)[DWT_NG], int64_t n, int64_t s0,
+                                               int64_t e0, float* smem) {
+  float* bufA[2] = {smem, smem + DWT_SPAN0 + DWT_SPAN1};
+  const int64_t g0 = s0 >= 0 ? (s0 & ~int64_t(3)) : -((-s0 + 3) & ~int64_t(3));
+#pragma unroll
+  for (int q = 0; q < DWT_NG; ++q) {
+    const int64_t p = g0 + 4 * (threadIdx.x + 256 * q);
+    const float xa[4] = {va[q].x, va[q].y, va[q].z, va[q].w};
+    const float xb[4] = {vb[q].x, vb[q].y, vb[q].z, vb[q].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t pe = p + e;
+      if (pe >= s0 && pe < e0 && pe >= 0 && pe < n) {
+        if (WX) bufA[0][pe - s0] = xa[e];
+        if (WD) bufA[1][pe - s0] = xa[e] - xb[e];
+      }
+    }
+  }
+  __syncthreads();
+  // extension: only x~[-3..-1] and x~[n..n+2] are ever read
+  if (threadIdx.x < 6) {
+    const int64_t p = threadIdx.x < 3 ? -1 - (int64_t)threadIdx.x : n + (threadIdx.x - 3);
+    const int64_t src = p < 0 ? -1 - p : 2 * n - 1 - p;
+    if (p >= s0 && p < e0 && src >= s0 && src < e0) {
+      if (WX) bufA[0][p - s0] = bufA[0][src - s0];
+      if (WD) bufA[1][p - s0] = bufA[1][src - s0];
+    }
+  }
+  __syncthreads();
+}
+
+// The levels of one tile from its level-0 span in LDS.
 template <bool WX, bool WD, bool ACCUM>
-__global__ void __launch_bounds__(256) dwt_kernel(const float* __restrict__ x,
-                                                  const float* __restrict__ x0, Levels LV,
-                                                  float* cx, float* cd) {
-  constexpr int SPAN0 = 16 * DWT_TL + 64;  // level-0 span (covers L <= 4 with slack)
-  constexpr int SPAN1 = 8 * DWT_TL + 32;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+__device__ __forceinline__ void dwt_levels(const Levels& LV, float* cx, float* cd, int64_t tile,
+                                           float* smem) {
+  constexpr int SPAN0 = DWT_SPAN0;
+  constexpr int SPAN1 = DWT_SPAN1;
   // pipelines: 0 = W(x), 1 = W(x - x0); buffers A (SPAN0) and B (SPAN1) per pipeline
   float* bufA[2] = {smem, smem + SPAN0 + SPAN1};
   float* bufB[2] = {smem + SPAN0, smem + 2 * SPAN0 + SPAN1};
   const int L = LV.level;
   const int64_t nL = LV.len[L];
-  const int64_t a = (int64_t)blockIdx.x * DWT_TL;
+  const int64_t a = tile * DWT_TL;
   const int64_t b = (a + DWT_TL < nL) ? a + DWT_TL : nL;
   const bool last_block = (b == nL);
   // needed ranges per level (top-down)
@@ -97,66 +183,6 @@ __global__ void __launch_bounds__(256) dwt_kernel(const float* __restrict__ x,
   for (int l = L; l >= 1; --l) {
     s[l - 1] = 2 * s[l] - 2;
     e[l - 1] = 2 * e[l];
-  }
-  // ---- level 0: load x (and x - x0) over [s0, e0) with symmetric extension
-  const int64_t n = LV.len[0];
-  {
-    const int64_t s0 = s[0], e0 = e[0];
-    // every load of the span is issued before any is used (float4 groups from the 4-aligned
-    // start below s0; a group that is not wholly inside [0, n) or an unaligned input falls back
-    // to scalar loads) — one memory latency per block instead of one per loop trip
-    constexpr int NG = (SPAN0 + 4 + 4 * 256 - 1) / (4 * 256);  // float4 groups per thread
-    const int64_t g0 = s0 >= 0 ? (s0 & ~int64_t(3)) : -((-s0 + 3) & ~int64_t(3));
-    const bool vec = aligned16(x) && (!WD || aligned16(x0));
-    float4 va[NG], vb[NG];
-#pragma unroll
-    for (int q = 0; q < NG; ++q) {
-      const int64_t p = g0 + 4 * (threadIdx.x + 256 * q);
-      va[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-      vb[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (p < e0) {
-        if (vec && p >= 0 && p + 4 <= n) {
-          va[q] = *reinterpret_cast<const float4*>(x + p);
-          if (WD) vb[q] = *reinterpret_cast<const float4*>(x0 + p);
-        } else {
-          float ta[4] = {0.f, 0.f, 0.f, 0.f}, tb[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (p + e >= 0 && p + e < n) {
-              ta[e] = x[p + e];
-              if (WD) tb[e] = x0[p + e];
-            }
-          }
-          va[q] = make_float4(ta[0], ta[1], ta[2], ta[3]);
-          vb[q] = make_float4(tb[0], tb[1], tb[2], tb[3]);
-        }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < NG; ++q) {
-      const int64_t p = g0 + 4 * (threadIdx.x + 256 * q);
-      const float xa[4] = {va[q].x, va[q].y, va[q].z, va[q].w};
-      const float xb[4] = {vb[q].x, vb[q].y, vb[q].z, vb[q].w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int64_t pe = p + e;
-        if (pe >= s0 && pe < e0 && pe >= 0 && pe < n) {
-          if (WX) bufA[0][pe - s0] = xa[e];
-          if (WD) bufA[1][pe - s0] = xa[e] - xb[e];
-        }
-      }
-    }
-    __syncthreads();
-    // extension: only x~[-3..-1] and x~[n..n+2] are ever read
-    if (threadIdx.x < 6) {
-      const int64_t p = threadIdx.x < 3 ? -1 - (int64_t)threadIdx.x : n + (threadIdx.x - 3);
-      const int64_t src = p < 0 ? -1 - p : 2 * n - 1 - p;
-      if (p >= s0 && p < e0 && src >= s0 && src < e0) {
-        if (WX) bufA[0][p - s0] = bufA[0][src - s0];
-        if (WD) bufA[1][p - s0] = bufA[1][src - s0];
-      }
-    }
-    __syncthreads();
   }
   float* in[2] = {bufA[0], bufA[1]};
   float* outb[2] = {bufB[0], bufB[1]};
@@ -206,15 +232,45 @@ __global__ void __launch_bounds__(256) dwt_kernel(const float* __restrict__ x,
   }
 }
 
+// Persistent grid (about as many blocks as the CUs hold at once, each walking tiles with a
+// grid stride): the per-tile blocks were short enough (~2.6 us) that the workgroup dispatcher,
+// not HBM, bounded the launch (SQ_WAVE_CYCLES showed ~21 % of the wave slots in use).
+template <bool WX, bool WD, bool ACCUM>
+__global__ void __launch_bounds__(256) dwt_kernel(const float* __restrict__ x,
+                                                  const float* __restrict__ x0, Levels LV,
+                                                  float* cx, float* cd, int64_t ntiles) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int64_t n = LV.len[0];
+  int64_t tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  float4 va[DWT_NG], vb[DWT_NG];
+  int64_t s0, e0;
+  dwt_span(LV, tile, &s0, &e0);
+  dwt_span_load<WD>(x, x0, n, s0, e0, va, vb);
+  for (;;) {
+    dwt_span_store<WX, WD>(va, vb, n, s0, e0, smem);
+    // the next tile's span loads are in flight while this tile's levels are computed
+    const int64_t next = tile + gridDim.x;
+    if (next < ntiles) {
+      dwt_span(LV, next, &s0, &e0);
+      dwt_span_load<WD>(x, x0, n, s0, e0, va, vb);
+    }
+    dwt_levels<WX, WD, ACCUM>(LV, cx, cd, tile, smem);
+    __syncthreads();  // the next tile reuses the LDS buffers
+    if (next >= ntiles) break;
+    tile = next;
+  }
+}
+
 // Inverse: block owns final outputs [c, d) (multiple of IDWT_TILE).
-__global__ void __launch_bounds__(256) idwt_kernel(const float* __restrict__ coeffs, Levels LV,
-                                                   float* __restrict__ out) {
+__device__ __forceinline__ void idwt_tile(const float* __restrict__ coeffs, const Levels& LV,
+                                          float* __restrict__ out, int64_t tile, float* A,
+                                          float* B) {
   constexpr int SPANI = IDWT_TILE / 2 + 16;
-  __shared__ __attribute__((aligned(16))) float A[SPANI];
-  __shared__ __attribute__((aligned(16))) float B[SPANI];
+  (void)SPANI;
   const int L = LV.level;
   const int64_t n = LV.len[0];
-  const int64_t c = (int64_t)blockIdx.x * IDWT_TILE;
+  const int64_t c = tile * IDWT_TILE;
   const int64_t d = (c + IDWT_TILE < n) ? c + IDWT_TILE : n;
   int64_t cl[DWT_MAX_LEVEL + 1], dl[DWT_MAX_LEVEL + 1];
   cl[0] = c;
@@ -258,6 +314,34 @@ __global__ void __launch_bounds__(256) idwt_kernel(const float* __restrict__ coe
   }
 }
 
+__global__ void __launch_bounds__(256) idwt_kernel(const float* __restrict__ coeffs, Levels LV,
+                                                   float* __restrict__ out, int64_t ntiles) {
+  constexpr int SPANI = IDWT_TILE / 2 + 16;
+  __shared__ __attribute__((aligned(16))) float A[SPANI];
+  __shared__ __attribute__((aligned(16))) float B[SPANI];
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    idwt_tile(coeffs, LV, out, tile, A, B);
+    __syncthreads();
+  }
+}
+
+// blocks of the persistent grids: what the CUs hold at once for the kernel (occupancy API)
+template <class K>
+static unsigned persistent_grid(K kernel, size_t shm, int64_t ntiles) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, shm) != hipSuccess || per < 1)
+    per = 1;
+  const int64_t g = (int64_t)cus * per;
+  return (unsigned)(ntiles < g ? (ntiles > 0 ? ntiles : 1) : g);
+}
+
 static int dwt_levels_ok(int64_t n, int level) {
   if (level < 1 || level > DWT_MAX_LEVEL || n <= 0) return 0;
   int64_t len = n;
@@ -286,19 +370,19 @@ extern "C" int dpz_dwt_sym2(const float* x, const float* x0, int64_t n, int leve
   if (coeffs_diff && !x0) return DPZ_ERR_ARG;
   if (!coeffs_x && !coeffs_diff) return DPZ_OK;
   const Levels LV = make_levels(n, level);
-  const unsigned grid = (unsigned)((LV.len[level] + DWT_TL - 1) / DWT_TL);
+  const int64_t ntiles = (LV.len[level] + DWT_TL - 1) / DWT_TL;
   constexpr int SPAN0 = 16 * DWT_TL + 64, SPAN1 = 8 * DWT_TL + 32;
   const size_t shm = 2 * (SPAN0 + SPAN1) * sizeof(float);
   const bool wx = coeffs_x != nullptr, wd = coeffs_diff != nullptr;
   const int tslot = timing_begin(DPZ_KT_DWT, st);
   if (wx && wd) {
-    if (accumulate) dwt_kernel<true, true, true><<<grid, 256, shm, st>>>(x, x0, LV, coeffs_x, coeffs_diff);
-    else dwt_kernel<true, true, false><<<grid, 256, shm, st>>>(x, x0, LV, coeffs_x, coeffs_diff);
+    if (accumulate) dwt_kernel<true, true, true><<<persistent_grid(dwt_kernel<true, true, true>, shm, ntiles), 256, shm, st>>>(x, x0, LV, coeffs_x, coeffs_diff, ntiles);
+    else dwt_kernel<true, true, false><<<persistent_grid(dwt_kernel<true, true, false>, shm, ntiles), 256, shm, st>>>(x, x0, LV, coeffs_x, coeffs_diff, ntiles);
   } else if (wx) {
-    dwt_kernel<true, false, false><<<grid, 256, shm, st>>>(x, x0, LV, coeffs_x, nullptr);
+    dwt_kernel<true, false, false><<<persistent_grid(dwt_kernel<true, false, false>, shm, ntiles), 256, shm, st>>>(x, x0, LV, coeffs_x, nullptr, ntiles);
   } else {
-    if (accumulate) dwt_kernel<false, true, true><<<grid, 256, shm, st>>>(x, x0, LV, nullptr, coeffs_diff);
-    else dwt_kernel<false, true, false><<<grid, 256, shm, st>>>(x, x0, LV, nullptr, coeffs_diff);
+    if (accumulate) dwt_kernel<false, true, true><<<persistent_grid(dwt_kernel<false, true, true>, shm, ntiles), 256, shm, st>>>(x, x0, LV, nullptr, coeffs_diff, ntiles);
+    else dwt_kernel<false, true, false><<<persistent_grid(dwt_kernel<false, true, false>, shm, ntiles), 256, shm, st>>>(x, x0, LV, nullptr, coeffs_diff, ntiles);
   }
   DPZ_LAUNCH_CHECK();
   timing_end(tslot, st);
@@ -311,7 +395,7 @@ extern "C" int dpz_idwt_sym2(const float* coeffs, int64_t n, int level, float* o
   if (!coeffs || !out || n <= 0) return DPZ_ERR_ARG;
   if (!dwt_levels_ok(n, level)) return DPZ_ERR_UNSUPPORTED;
   const Levels LV = make_levels(n, level);
-  const unsigned grid = (unsigned)((n + IDWT_TILE - 1) / IDWT_TILE);
-  DPZ_TIMED(DPZ_KT_IDWT, st, idwt_kernel<<<grid, 256, 0, st>>>(coeffs, LV, out));
+  const int64_t ntiles = (n + IDWT_TILE - 1) / IDWT_TILE;
+  DPZ_TIMED(DPZ_KT_IDWT, st, idwt_kernel<<<persistent_grid(idwt_kernel, 0, ntiles), 256, 0, st>>>(coeffs, LV, out, ntiles));
   return DPZ_OK;
 }
