@@ -17,17 +17,32 @@
 //      t = (tag == p) ? hit : local;  total = (p == 0) ? t*w : total + t*w
 //    in exactly the reference's fp32 order (library compiled with -ffp-contract=off).
 // Algorithmic bytes: read local (4N) + write out (4N) + 8 bytes per payload entry.
+#include <cstdlib>
+
 #include "dpz_common.h"
 #include "dpz_replace.h"
 
 namespace dpz {
 
-constexpr int FOLD_TILE_SHIFT = 12;
+#ifndef DPZ_FOLD_TS
+#define DPZ_FOLD_TS 12
+#endif
+#ifndef DPZ_FOLD_THREADS
+#define DPZ_FOLD_THREADS 512
+#endif
+constexpr int FOLD_TILE_SHIFT = DPZ_FOLD_TS;
 constexpr int FOLD_TILE = 1 << FOLD_TILE_SHIFT;
 constexpr int FOLD_MAXP = 16;  // payloads per launch (longer lists are chained)
-constexpr int FOLD_THREADS = 512;
+constexpr int FOLD_THREADS = DPZ_FOLD_THREADS;
 constexpr int FOLD_GROUPS = FOLD_TILE / (4 * FOLD_THREADS);  // float4 groups per thread
 constexpr int FOLD_EQ = 4;  // payload entries per thread preloaded at tile start
+// hit-chain path: per-element chain head (u32) + per-entry value and (next | payload << 16),
+// the tile's local values and the distinct-hit list: 61 KB of LDS at 2816 entries (2 blocks of
+// 512 threads per CU, as the registers allow)
+constexpr int FOLD_CAP = FOLD_TILE / 16 * 11;
+constexpr int FOLD_LDS_MASK = FOLD_TILE * 4 + FOLD_CAP * 8 + FOLD_TILE * 4 + FOLD_CAP * 2;
+constexpr int FOLD_LDS_PHASE = FOLD_TILE * 4 + FOLD_TILE;
+constexpr int FOLD_LDS_BYTES = FOLD_LDS_MASK > FOLD_LDS_PHASE ? FOLD_LDS_MASK : FOLD_LDS_PHASE;
 
 struct FoldPayload {
   const int32_t* idx;  // nullptr: dense payload (vals has n entries)
@@ -47,6 +62,8 @@ struct FoldArgs {
   int add_self;     // add local * w_self at the end
   int replace_only; // out = t_0
   int zero_base;    // sparse payloads contribute 0 off their entries; first term = +0 + t0*w0
+  int all_sparse;   // no dense payload in this group: the one-phase hit-chain path may run
+  uint32_t dense_mask;  // bit p: payload p is dense (idx == nullptr)
   float w_self;
   FoldPayload p[FOLD_MAXP];
 };
@@ -69,26 +86,73 @@ __global__ void __launch_bounds__(256) fold_offsets_kernel(FoldArgs a, int32_t* 
   for (int64_t t = tprev + 1; t <= tcur; ++t) st[t] = (int32_t)j;
 }
 
+// one payload term of the fold in the reference's fp32 order: the first term of a fresh total is
+// t*w (+0 first with a zero base), later terms add; replace-only keeps the payload value
+__device__ __forceinline__ void fold_term(float& acc, float tv, float w, bool first_term,
+                                          int replace_only, int zero_base) {
+  if (replace_only) {
+    acc = tv;
+  } else {
+    const float term = tv * w;
+    acc = first_term ? (zero_base ? 0.0f + term : term) : acc + term;
+  }
+}
+
 template <bool VEC>
-__global__ void __launch_bounds__(FOLD_THREADS) fold_kernel(FoldArgs a) {
-  __shared__ __attribute__((aligned(16))) float hv[FOLD_TILE];
-  __shared__ __attribute__((aligned(16))) uint8_t htag[FOLD_TILE];
+__global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
+  // phase path: hv (value tile) + htag (payload tag); hit-mask path: msk + epos + ev
+  __shared__ __attribute__((aligned(16))) uint8_t lds_raw[FOLD_LDS_BYTES];
+  float* hv = reinterpret_cast<float*>(lds_raw);
+  uint8_t* htag = lds_raw + FOLD_TILE * sizeof(float);
   __shared__ int32_t rng[FOLD_MAXP][2];
   __shared__ int32_t pre[FOLD_MAXP + 1];  // flattened entry offset of each payload's tile range
-  const int64_t tile = blockIdx.x;
-  const int64_t tlo = tile * FOLD_TILE;
-  const int64_t thi = (tlo + FOLD_TILE < a.n) ? tlo + FOLD_TILE : a.n;
   const int t = threadIdx.x;
-  if (t < a.np) {
-    if (a.p[t].idx) {
-      const int32_t* st = a.starts + (int64_t)t * (a.ntiles + 1);
-      rng[t][0] = st[tile];
-      rng[t][1] = st[tile + 1];
-    } else {
-      rng[t][0] = rng[t][1] = 0;
+  // payload pointer table in LDS: the entry loads below pick their payload per lane, and a
+  // per-lane index into the kernel-argument array is a dependent global load per tile
+  __shared__ const int32_t* s_idx[FOLD_MAXP];
+  __shared__ const float* s_val[FOLD_MAXP];
+  __shared__ uint32_t s_nhit;
+  __shared__ float s_w[FOLD_MAXP];
+  if (t == 0) {
+    for (int p = 0; p < a.np; ++p) {
+      s_idx[p] = a.p[p].idx;
+      s_val[p] = a.p[p].val;
+      s_w[p] = a.p[p].w;
     }
   }
-  for (int j = t * 4; j < FOLD_TILE; j += 4 * FOLD_THREADS) *reinterpret_cast<uint32_t*>(&htag[j]) = 0xFFFFFFFFu;
+  // persistent blocks: tile, tile + gridDim.x, ...; the next tile's entry ranges are loaded
+  // while the current tile is folded
+  int32_t nr0 = 0, nr1 = 0;
+  const bool rng_lane = t < a.np && !((a.dense_mask >> t) & 1u);
+  if (rng_lane && (int64_t)blockIdx.x < a.ntiles) {
+    const int32_t* st = a.starts + (int64_t)t * (a.ntiles + 1);
+    nr0 = st[blockIdx.x];
+    nr1 = st[blockIdx.x + 1];
+  }
+  for (int64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+  const int64_t tlo = tile * FOLD_TILE;
+  const int64_t thi = (tlo + FOLD_TILE < a.n) ? tlo + FOLD_TILE : a.n;
+  if (t < 64) {
+    // entry ranges and their flattened offsets (a wave scan; pre[u] = etot for u >= np)
+    const int32_t c = (t < a.np && nr1 > nr0) ? nr1 - nr0 : 0;
+    if (t < a.np) {
+      rng[t][0] = nr0;
+      rng[t][1] = nr1;
+    }
+    int32_t incl = c;
+#pragma unroll
+    for (int d = 1; d < FOLD_MAXP; d <<= 1) {
+      const int32_t v = __shfl_up(incl, d, 64);
+      if (t >= d) incl += v;
+    }
+    if (t < FOLD_MAXP) pre[t + 1] = incl;
+    if (t == 0) pre[0] = 0;
+  }
+  if (rng_lane && tile + gridDim.x < a.ntiles) {
+    const int32_t* st = a.starts + (int64_t)t * (a.ntiles + 1);
+    nr0 = st[tile + gridDim.x];
+    nr1 = st[tile + gridDim.x + 1];
+  }
 
   // this thread's elements: q-th group = tlo + q*1024 + 4t .. +3
   float L[4 * FOLD_GROUPS], acc[4 * FOLD_GROUPS];
@@ -112,23 +176,17 @@ __global__ void __launch_bounds__(FOLD_THREADS) fold_kernel(FoldArgs a) {
     }
   }
 
-  __syncthreads();  // rng visible
-  if (t == 0) {
-    int32_t acc_e = 0;
-    for (int p = 0; p < a.np; ++p) {
-      pre[p] = acc_e;
-      const int32_t cnt = rng[p][1] - rng[p][0];
-      acc_e += cnt > 0 ? cnt : 0;
-    }
-    pre[a.np] = acc_e;
-  }
-  __syncthreads();
+  __syncthreads();  // rng / pre visible
   // every payload's entries of this tile (flattened, the first FOLD_EQ * FOLD_THREADS of them)
   // are loaded before any is used: one memory latency per tile instead of one per payload
   int ep[FOLD_EQ];
   int32_t ei[FOLD_EQ];
   float evl[FOLD_EQ];
+#if defined(DPZ_FOLD_SKIP) && DPZ_FOLD_SKIP == 1
+  const int32_t etot = 0;  // ablation: no entries (timing only)
+#else
   const int32_t etot = pre[a.np];
+#endif
 #pragma unroll
   for (int q = 0; q < FOLD_EQ; ++q) {
     const int32_t j = t + q * FOLD_THREADS;
@@ -136,15 +194,164 @@ __global__ void __launch_bounds__(FOLD_THREADS) fold_kernel(FoldArgs a) {
     ei[q] = 0;
     evl[q] = 0.0f;
     if (j < etot) {
+      // payload of flattened entry j: binary search over pre[0..15] (pre[u] = etot > j for
+      // u >= np), four dependent LDS reads instead of a read per payload
       int p = 0;
-      for (int u = 1; u < a.np; ++u) p += pre[u] <= j ? 1 : 0;
+#pragma unroll
+      for (int s = FOLD_MAXP / 2; s >= 1; s >>= 1) p += pre[p + s] <= j ? s : 0;
       const int64_t src = (int64_t)rng[p][0] + (j - pre[p]);
       ep[q] = p;
-      ei[q] = a.p[p].idx[src];
-      evl[q] = a.p[p].val[src];
+      ei[q] = s_idx[p][src];
+      evl[q] = s_val[p][src];
     }
   }
 
+  if (a.all_sparse && etot <= FOLD_CAP) {
+    // Hit-chain path.  The fold is VALU-bound when every element runs the per-payload select
+    // (16 payloads x 8 elements x ~6 instructions per thread), so it is split:
+    //  A) every element folds its base value alone (no hits): 2 flops per payload term, packed;
+    //  B) the tile's hit elements (~15 % at 16 payloads x 1 %), compacted to a list, are folded
+    //     exactly with their payload values by one thread each and overwrite A's result.
+    // Entries are pushed on per-element hit chains (head[pos] -> j -> ...) in one scatter phase.
+    uint32_t* head = reinterpret_cast<uint32_t*>(lds_raw);
+    uint32_t* meta = head + FOLD_TILE;                       // next (low 16) | payload << 16
+    float* ev = reinterpret_cast<float*>(meta + FOLD_CAP);
+    float* lv = ev + FOLD_CAP;                               // the tile's local values
+    uint16_t* hitl = reinterpret_cast<uint16_t*>(lv + FOLD_TILE);  // distinct hit elements
+    for (int j = t * 4; j < FOLD_TILE; j += 4 * FOLD_THREADS)
+      *reinterpret_cast<uint4*>(&head[j]) = make_uint4(~0u, ~0u, ~0u, ~0u);
+#pragma unroll
+    for (int q = 0; q < FOLD_GROUPS; ++q)
+      *reinterpret_cast<float4*>(&lv[q * 4 * FOLD_THREADS + t * 4]) =
+          make_float4(L[q * 4 + 0], L[q * 4 + 1], L[q * 4 + 2], L[q * 4 + 3]);
+    if (t == 0) s_nhit = 0;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < FOLD_EQ; ++q) {
+      if (ep[q] >= 0) {
+        const int32_t j = t + q * FOLD_THREADS;
+        const int64_t pos = (int64_t)ei[q] - tlo;
+        ev[j] = evl[q];
+        if (pos >= 0 && pos < FOLD_TILE) {  // guards against an unsorted caller array
+          const uint32_t old = atomicExch(&head[pos], (uint32_t)j);
+          meta[j] = (old & 0xFFFFu) | ((uint32_t)ep[q] << 16);
+          if (old == ~0u) hitl[atomicAdd(&s_nhit, 1u)] = (uint16_t)pos;
+        }
+      }
+    }
+    for (int32_t j = FOLD_EQ * FOLD_THREADS + t; j < etot; j += FOLD_THREADS) {
+      // payload of flattened entry j: binary search over pre[0..15] (pre[u] = etot > j for
+      // u >= np), four dependent LDS reads instead of a read per payload
+      int p = 0;
+#pragma unroll
+      for (int s = FOLD_MAXP / 2; s >= 1; s >>= 1) p += pre[p + s] <= j ? s : 0;
+      const int64_t src = (int64_t)rng[p][0] + (j - pre[p]);
+      const int64_t pos = (int64_t)s_idx[p][src] - tlo;
+      ev[j] = s_val[p][src];
+      if (pos >= 0 && pos < FOLD_TILE) {
+        const uint32_t old = atomicExch(&head[pos], (uint32_t)j);
+        meta[j] = (old & 0xFFFFu) | ((uint32_t)p << 16);
+        if (old == ~0u) hitl[atomicAdd(&s_nhit, 1u)] = (uint16_t)pos;
+      }
+    }
+    __syncthreads();
+    // A) base fold of this thread's elements; remember which of them carry hits
+    uint32_t hitbits = 0;
+#pragma unroll
+    for (int q = 0; q < FOLD_GROUPS; ++q) {
+      const uint4 h4 = *reinterpret_cast<const uint4*>(&head[q * 4 * FOLD_THREADS + t * 4]);
+      hitbits |= ((h4.x != ~0u) ? 1u : 0u) << (4 * q);
+      hitbits |= ((h4.y != ~0u) ? 1u : 0u) << (4 * q + 1);
+      hitbits |= ((h4.z != ~0u) ? 1u : 0u) << (4 * q + 2);
+      hitbits |= ((h4.w != ~0u) ? 1u : 0u) << (4 * q + 3);
+    }
+    {
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      f2 b2[2 * FOLD_GROUPS], a2[2 * FOLD_GROUPS];
+#pragma unroll
+      for (int h = 0; h < 2 * FOLD_GROUPS; ++h) {
+        b2[h] = a.zero_base ? f2{0.0f, 0.0f} : f2{L[2 * h], L[2 * h + 1]};
+        a2[h] = f2{acc[2 * h], acc[2 * h + 1]};
+      }
+      if (a.replace_only) {
+#pragma unroll
+        for (int h = 0; h < 2 * FOLD_GROUPS; ++h) a2[h] = b2[h];
+      } else {
+        // weights from LDS (uniform reads); an unrolled loop over scalar weights spilled SGPRs
+        // into VGPR lanes and cost occupancy
+        int p0 = 0;
+        if (a.first) {
+          const float w = s_w[0];
+          const f2 w2 = {w, w};
+#pragma unroll
+          for (int h = 0; h < 2 * FOLD_GROUPS; ++h) {
+            const f2 term = b2[h] * w2;
+            a2[h] = a.zero_base ? f2{0.0f, 0.0f} + term : term;
+          }
+          p0 = 1;
+        }
+        for (int p = p0; p < a.np; ++p) {
+          const float w = s_w[p];
+          const f2 w2 = {w, w};
+#pragma unroll
+          for (int h = 0; h < 2 * FOLD_GROUPS; ++h) a2[h] = a2[h] + b2[h] * w2;
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2 * FOLD_GROUPS; ++h) {
+        acc[2 * h] = a2[h].x;
+        acc[2 * h + 1] = a2[h].y;
+      }
+    }
+    __syncthreads();  // every owner has read its hit flags before B overwrites head[]
+    // B) exact fold of the hit elements, one per thread; the result replaces head[pos]
+    const uint32_t nhit = s_nhit;
+    for (uint32_t s = t; s < nhit; s += FOLD_THREADS) {
+      const int pos = hitl[s];
+      const float b = a.zero_base ? 0.0f : lv[pos];
+      float av = a.first ? 0.0f : a.out[tlo + pos];
+      uint32_t p1 = 0xFFFFu, p2 = 0xFFFFu, more = 0xFFFFu;
+      float v1 = 0.0f, v2 = 0.0f;
+      const uint32_t c1 = head[pos] & 0xFFFFu;
+      {
+        const uint32_t m1 = meta[c1];
+        p1 = m1 >> 16;
+        v1 = ev[c1];
+        const uint32_t c2 = m1 & 0xFFFFu;
+        if (c2 != 0xFFFFu) {
+          const uint32_t m2 = meta[c2];
+          p2 = m2 >> 16;
+          v2 = ev[c2];
+          more = m2 & 0xFFFFu;
+        }
+      }
+      for (int p = 0; p < a.np; ++p) {
+        float tv = ((uint32_t)p == p1) ? v1 : (((uint32_t)p == p2) ? v2 : b);
+        if (more != 0xFFFFu && (uint32_t)p != p1 && (uint32_t)p != p2) {
+          for (uint32_t c = more; c != 0xFFFFu;) {  // a third hit or more (rare)
+            const uint32_t m = meta[c];
+            if ((m >> 16) == (uint32_t)p) {
+              tv = ev[c];
+              break;
+            }
+            c = m & 0xFFFFu;
+          }
+        }
+        fold_term(av, tv, s_w[p], a.first && p == 0, a.replace_only, a.zero_base);
+      }
+      head[pos] = __float_as_uint(av);
+    }
+    __syncthreads();
+    if (hitbits) {
+#pragma unroll
+      for (int q = 0; q < FOLD_GROUPS; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if ((hitbits >> (4 * q + e)) & 1u)
+            acc[q * 4 + e] = __uint_as_float(head[q * 4 * FOLD_THREADS + t * 4 + e]);
+    }
+  } else {
+  for (int j = t * 4; j < FOLD_TILE; j += 4 * FOLD_THREADS) *reinterpret_cast<uint32_t*>(&htag[j]) = 0xFFFFFFFFu;
   for (int p = 0; p < a.np; ++p) {
     const FoldPayload& P = a.p[p];
     __syncthreads();  // previous payload's reads of hv/htag done
@@ -206,6 +413,7 @@ __global__ void __launch_bounds__(FOLD_THREADS) fold_kernel(FoldArgs a) {
       }
     }
   }
+  }  // phase path
   if (a.add_self) {
 #pragma unroll
     for (int e = 0; e < 4 * FOLD_GROUPS; ++e) acc[e] = acc[e] + L[e] * a.w_self;
@@ -222,6 +430,28 @@ __global__ void __launch_bounds__(FOLD_THREADS) fold_kernel(FoldArgs a) {
         if (i0 + e < thi) a.out[i0 + e] = acc[q * 4 + e];
     }
   }
+  __syncthreads();  // the next tile reuses rng / pre / the LDS tile
+  }  // tile loop
+}
+
+// blocks of the persistent fold grid: what the CUs hold at once (occupancy API)
+template <bool VEC>
+static unsigned fold_grid(int64_t ntiles) {
+  static int slots = 0;
+  if (slots == 0) {
+    int dev = 0, cus = 256, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fold_kernel<VEC>, FOLD_THREADS, 0) !=
+            hipSuccess || per < 1)
+      per = 1;
+    slots = cus * per;
+  }
+  // DPZ_FOLD_BLOCKS=N caps the grid at N blocks (A/B diagnostics; 0 = the occupancy slots)
+  static const int64_t cap = getenv("DPZ_FOLD_BLOCKS") ? atoll(getenv("DPZ_FOLD_BLOCKS")) : 0;
+  const int64_t g = cap > 0 ? cap : slots;
+  return (unsigned)(ntiles < g ? (ntiles > 0 ? ntiles : 1) : g);
 }
 
 static inline int64_t fold_ntiles(int64_t n) { return (n + FOLD_TILE - 1) / FOLD_TILE; }
@@ -271,7 +501,6 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
   for (int i = 0; i < n_payloads; ++i)
     if (is_dense(i) && (reinterpret_cast<uintptr_t>(vals[i]) & 15u)) vec = false;
   const int64_t ntiles = fold_ntiles(n);
-  const unsigned grid = (unsigned)ntiles;
   int32_t* starts = static_cast<int32_t*>(ws);
   if (n_payloads == 0) {
     // no payloads: out = w_self * local (self term only) or zeros
@@ -280,8 +509,8 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
     fa.np = 0; fa.first = 0;
     fa.add_self = (flags & DPZ_FOLD_SELF) ? 1 : 0; fa.w_self = w_self;
     if (!(flags & DPZ_FOLD_ACCUMULATE)) DPZ_HIP_TRY(hipMemsetAsync(out, 0, n * sizeof(float), st));
-    if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<true><<<grid, FOLD_THREADS, 0, st>>>(fa));
-    else DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<false><<<grid, FOLD_THREADS, 0, st>>>(fa));
+    if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<true><<<fold_grid<true>(ntiles), FOLD_THREADS, 0, st>>>(fa));
+    else DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<false><<<fold_grid<false>(ntiles), FOLD_THREADS, 0, st>>>(fa));
     return DPZ_OK;
   }
   // one sparse payload, replace only: single-kernel range-partitioned copy + scatter
@@ -317,12 +546,21 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
       fa.p[i].w = (replace_only || add_only) ? 1.0f : w[base + i];
       if (fa.p[i].idx && fa.p[i].k > kmax) kmax = fa.p[i].k;
     }
+    // DPZ_FOLD_PHASES=1 forces the per-payload phase path (A/B diagnostics)
+    static const bool force_phases = getenv("DPZ_FOLD_PHASES") && atoi(getenv("DPZ_FOLD_PHASES"));
+    fa.all_sparse = force_phases ? 0 : 1;
+    fa.dense_mask = 0;
+    for (int i = 0; i < fa.np; ++i)
+      if (!fa.p[i].idx) {
+        fa.all_sparse = 0;
+        fa.dense_mask |= 1u << i;
+      }
     if (kmax >= 0) {
       dim3 og((unsigned)((kmax + 1 + 255) / 256), (unsigned)fa.np);
       DPZ_TIMED(DPZ_KT_FOLD_OFFSETS, st, fold_offsets_kernel<<<og, 256, 0, st>>>(fa, starts));
     }
-    if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<true><<<grid, FOLD_THREADS, 0, st>>>(fa));
-    else DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<false><<<grid, FOLD_THREADS, 0, st>>>(fa));
+    if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<true><<<fold_grid<true>(ntiles), FOLD_THREADS, 0, st>>>(fa));
+    else DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<false><<<fold_grid<false>(ntiles), FOLD_THREADS, 0, st>>>(fa));
   }
   return DPZ_OK;
 }

@@ -236,6 +236,37 @@ def test_fold_matches_oracle(dev, n, npay):
     np.testing.assert_array_equal(_bits(out2), _bits(ref2))
 
 
+@pytest.mark.parametrize("n,alpha,npay", [(1_000_003, 0.01, 16), (1_000_003, 0.05, 16),
+                                          (4_000_037, 0.01, 20), (300_001, 0.2, 3),
+                                          (300_001, 0.04, 5)])
+def test_fold_all_sparse_overlapping(dev, n, alpha, npay):
+    """All-sparse payload groups take the one-phase hit-chain fold (tiles with more than its LDS
+    capacity of entries fall back to the per-payload phases inside the same launch); payloads
+    share many indices so elements carry 2, 3 and more hits."""
+    codec = _codec()
+    rng = np.random.default_rng(int(n * alpha) + npay)
+    local = rng.standard_normal(n).astype(np.float32)
+    k = max(1, round(alpha * n))
+    base = rng.choice(n, size=k, replace=False)
+    pays, tpays = [], []
+    for i in range(npay):
+        own = rng.choice(n, size=k, replace=False)
+        take = rng.random(k) < (0.5 if i % 2 else 0.2)  # shared with payload 0's set
+        idx = np.unique(np.where(take, base, own)).astype(np.int32)
+        vals = rng.standard_normal(idx.size).astype(np.float32)
+        pays.append((idx, vals))
+        tpays.append((torch.from_numpy(idx).to(dev), torch.from_numpy(vals).to(dev)))
+    weights = [ofold.mh_weight(npay, int(d)) for d in rng.integers(1, 20, size=npay)]
+    w_self = 1 - sum(weights)
+    tl = torch.from_numpy(local).to(dev)
+    ref = ofold.fold(local, pays, weights, w_self)
+    out = codec.decode_average(tl, tpays, weights, w_self).cpu().numpy()
+    np.testing.assert_array_equal(_bits(out), _bits(ref))
+    ref2 = ofold.fold(local, pays, [1 / npay] * npay, None)
+    out2 = codec.decode_average(tl, tpays, [1 / npay] * npay, None).cpu().numpy()
+    np.testing.assert_array_equal(_bits(out2), _bits(ref2))
+
+
 @pytest.mark.parametrize("n,k", [(1000, 10), (1000, 0), (1000, 1000), (11_000_000, 110_000)])
 def test_replace_matches_oracle(dev, n, k):
     codec = _codec()
