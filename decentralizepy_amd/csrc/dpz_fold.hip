@@ -305,7 +305,11 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
     }
     __syncthreads();  // every owner has read its hit flags before B overwrites head[]
     // B) exact fold of the hit elements, one per thread; the result replaces head[pos]
+#if defined(DPZ_FOLD_SKIP) && DPZ_FOLD_SKIP == 3
+    const uint32_t nhit = 0;  // ablation: no exact fold of the hit elements (timing only)
+#else
     const uint32_t nhit = s_nhit;
+#endif
     for (uint32_t s = t; s < nhit; s += FOLD_THREADS) {
       const int pos = hitl[s];
       const float b = a.zero_base ? 0.0f : lv[pos];
@@ -325,7 +329,14 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
           more = m2 & 0xFFFFu;
         }
       }
-      for (int p = 0; p < a.np; ++p) {
+      // unrolled over the 16 payload slots with the weights read from LDS up front: a rolled
+      // loop waited on one LDS read per payload for every hit element
+      float wr[FOLD_MAXP];
+#pragma unroll
+      for (int p = 0; p < FOLD_MAXP; ++p) wr[p] = s_w[p];
+#pragma unroll
+      for (int p = 0; p < FOLD_MAXP; ++p) {
+        if (p >= a.np) break;
         float tv = ((uint32_t)p == p1) ? v1 : (((uint32_t)p == p2) ? v2 : b);
         if (more != 0xFFFFu && (uint32_t)p != p1 && (uint32_t)p != p2) {
           for (uint32_t c = more; c != 0xFFFFu;) {  // a third hit or more (rare)
@@ -337,7 +348,7 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
             c = m & 0xFFFFu;
           }
         }
-        fold_term(av, tv, s_w[p], a.first && p == 0, a.replace_only, a.zero_base);
+        fold_term(av, tv, wr[p], a.first && p == 0, a.replace_only, a.zero_base);
       }
       head[pos] = __float_as_uint(av);
     }

@@ -3,4 +3,4 @@
 set -e
 mkdir -p gpurun_out; export TMPDIR=/tmp
 echo "== default"; timeout -k 10 120 python tools/diag/fold_time.py
-for s in a b c; do echo "== variant $s"; DPZ_CODEC_LIB=$PWD/decentralizepy_amd/libdpz_abl_fold$s.so timeout -k 10 120 python tools/diag/fold_time.py; done
+for s in 1 3; do echo "== variant $s"; DPZ_CODEC_LIB=$PWD/decentralizepy_amd/libdpz_abl_fold$s.so timeout -k 10 120 python tools/diag/fold_time.py; done
