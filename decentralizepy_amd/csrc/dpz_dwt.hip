@@ -21,7 +21,11 @@ constexpr int DWT_MAX_LEVEL = 8;
 #ifndef DPZ_DWT_TL
 #define DPZ_DWT_TL 128
 #endif
-constexpr int DWT_TL = DPZ_DWT_TL;  // level-L outputs per block (forward)
+constexpr int DWT_TL = DPZ_DWT_TL;
+// waves per SIMD the forward kernel is register-bounded for (3 without the bound: 150 VGPRs)
+#ifndef DPZ_DWT_WAVES
+#define DPZ_DWT_WAVES 4
+#endif  // level-L outputs per block (forward)
 constexpr int IDWT_TILE = 4096;
 
 // sym2 filters (fp32 casts of pywt's double coefficients)
@@ -61,6 +65,22 @@ static inline Levels make_levels(int64_t n, int level) {
 __device__ __forceinline__ float conv4(const float* in, int64_t s_in, int64_t o, const float* f,
                                        bool last_odd) {
   const int64_t i = 2 * o + 1 - s_in;
+  if (!last_odd) {
+    float acc = f[0] * in[i];
+    acc = acc + f[1] * in[i - 1];
+    acc = acc + f[2] * in[i - 2];
+    acc = acc + f[3] * in[i - 3];
+    return acc;
+  }
+  float acc = f[2] * in[i - 2];   // x~[n]
+  acc = acc + f[1] * in[i - 1];   // x~[n+1]
+  acc = acc + f[0] * in[i];       // x~[n+2]
+  acc = acc + f[3] * in[i - 3];   // x~[n-1]
+  return acc;
+}
+
+// conv4 on a 32-bit LDS offset i (= 2 o + 1 - s_in), same summation orders
+__device__ __forceinline__ float conv4r(const float* in, int i, const float* f, bool last_odd) {
   if (!last_odd) {
     float acc = f[0] * in[i];
     acc = acc + f[1] * in[i - 1];
@@ -188,7 +208,6 @@ __device__ __forceinline__ void dwt_levels(const Levels& LV, float* cx, float* c
   float* outb[2] = {bufB[0], bufB[1]};
   for (int l = 1; l <= L; ++l) {
     const int64_t nin = LV.len[l - 1], nout = LV.len[l];
-    const int64_t sin = s[l - 1];
     const int64_t sl = s[l], el = e[l];
     const bool odd_in = (nin & 1) != 0;
     // owned detail range at this level
@@ -196,23 +215,36 @@ __device__ __forceinline__ void dwt_levels(const Levels& LV, float* cx, float* c
     const int64_t own_hi = last_block ? nout : (b << (L - l));
     const int64_t c_lo = sl > 0 ? sl : 0;
     const int64_t c_hi = el < nout ? el : nout;
-    for (int64_t o = c_lo + threadIdx.x; o < c_hi; o += 256) {
-      const bool lo_odd = odd_in && (o == nout - 1);
-      const bool own = (o >= own_lo && o < own_hi);
+    // 32-bit offsets relative to sl (the block-uniform level origin): the input of output
+    // sl + r starts at in[2r + 3 - 3] (sin = 2 sl - 2), so conv4's window top is in[2r + 3]
+    const int r_lo = (int)(c_lo - sl), r_hi = (int)(c_hi - sl);
+    const int64_t own_lo_r = own_lo - sl, own_hi_r = own_hi - sl;
+    const int own_a = (int)(own_lo_r < 0 ? 0 : own_lo_r);
+    const int own_b = (int)(own_hi_r > r_hi ? r_hi : own_hi_r);
+    const int64_t odd_r64 = odd_in ? (nout - 1 - sl) : -1;
+    const int odd_r = (odd_r64 >= r_lo && odd_r64 < r_hi) ? (int)odd_r64 : -1;
+    float* const cxd = WX ? cx + LV.doff[l] + sl : nullptr;
+    float* const cdd = WD ? cd + LV.doff[l] + sl : nullptr;
+    float* const cxa = WX ? cx + sl : nullptr;
+    float* const cda = WD ? cd + sl : nullptr;
+    for (int r = r_lo + (int)threadIdx.x; r < r_hi; r += 256) {
+      const bool lo_odd = (r == odd_r);
+      const bool own = (r >= own_a && r < own_b);
+      const int i = 2 * r + 3;
       if (WX) {
-        if (l < L) outb[0][o - sl] = conv4(in[0], sin, o, c_dec_lo, lo_odd);
-        if (own) cx[LV.doff[l] + o] = conv4(in[0], sin, o, c_dec_hi, lo_odd);
-        if (l == L && own) cx[o] = conv4(in[0], sin, o, c_dec_lo, lo_odd);
+        if (l < L) outb[0][r] = conv4r(in[0], i, c_dec_lo, lo_odd);
+        if (own) cxd[r] = conv4r(in[0], i, c_dec_hi, lo_odd);
+        if (l == L && own) cxa[r] = conv4r(in[0], i, c_dec_lo, lo_odd);
       }
       if (WD) {
-        if (l < L) outb[1][o - sl] = conv4(in[1], sin, o, c_dec_lo, lo_odd);
+        if (l < L) outb[1][r] = conv4r(in[1], i, c_dec_lo, lo_odd);
         if (own) {
-          const float dv = conv4(in[1], sin, o, c_dec_hi, lo_odd);
-          if (ACCUM) cd[LV.doff[l] + o] = cd[LV.doff[l] + o] + dv; else cd[LV.doff[l] + o] = dv;
+          const float dv = conv4r(in[1], i, c_dec_hi, lo_odd);
+          if (ACCUM) cdd[r] = cdd[r] + dv; else cdd[r] = dv;
         }
         if (l == L && own) {
-          const float av = conv4(in[1], sin, o, c_dec_lo, lo_odd);
-          if (ACCUM) cd[o] = cd[o] + av; else cd[o] = av;
+          const float av = conv4r(in[1], i, c_dec_lo, lo_odd);
+          if (ACCUM) cda[r] = cda[r] + av; else cda[r] = av;
         }
       }
     }
@@ -236,7 +268,7 @@ __device__ __forceinline__ void dwt_levels(const Levels& LV, float* cx, float* c
 // grid stride): the per-tile blocks were short enough (~2.6 us) that the workgroup dispatcher,
 // not HBM, bounded the launch (SQ_WAVE_CYCLES showed ~21 % of the wave slots in use).
 template <bool WX, bool WD, bool ACCUM>
-__global__ void __launch_bounds__(256) dwt_kernel(const float* __restrict__ x,
+__global__ void __launch_bounds__(256, DPZ_DWT_WAVES) dwt_kernel(const float* __restrict__ x,
                                                   const float* __restrict__ x0, Levels LV,
                                                   float* cx, float* cd, int64_t ntiles) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
