@@ -294,43 +294,110 @@ __global__ void __launch_bounds__(256, DPZ_DWT_WAVES) dwt_kernel(const float* __
   }
 }
 
-// Inverse: block owns final outputs [c, d) (multiple of IDWT_TILE).
-__device__ __forceinline__ void idwt_tile(const float* __restrict__ coeffs, const Levels& LV,
-                                          float* __restrict__ out, int64_t tile, float* A,
-                                          float* B) {
-  constexpr int SPANI = IDWT_TILE / 2 + 16;
-  (void)SPANI;
-  const int L = LV.level;
-  const int64_t n = LV.len[0];
-  const int64_t c = tile * IDWT_TILE;
-  const int64_t d = (c + IDWT_TILE < n) ? c + IDWT_TILE : n;
+// Inverse: a block owns final outputs [c, d) (a multiple of IDWT_TILE) and needs, per level l,
+// the coefficients [cl[l], dl[l]) of cD_l (and of cA_L at the top).  Persistent blocks stage
+// a tile's whole coefficient footprint (<= 4.2 K floats) into LDS, issue the NEXT tile's loads
+// into registers, then rebuild the levels top-down from LDS (32-bit LDS-relative offsets).
+__host__ __device__ constexpr int idwt_seg_max(int l) { return (IDWT_TILE >> l) + 4; }
+__host__ __device__ constexpr int idwt_iters(int l) { return (idwt_seg_max(l) + 255) / 256; }
+__host__ __device__ constexpr int idwt_doff(int l) {  // LDS offset of cD_l's segment
+  int o = 0;
+  for (int j = 1; j < l; ++j) o += idwt_seg_max(j);
+  return o;
+}
+template <int LEV>
+__host__ __device__ constexpr int idwt_npv() {
+  int s = idwt_iters(LEV);
+  for (int l = 1; l <= LEV; ++l) s += idwt_iters(l);
+  return s;
+}
+constexpr int IDWT_SPAN = IDWT_TILE / 2 + 16;
+constexpr int IDWT_DALL = idwt_doff(DWT_MAX_LEVEL + 1);
+
+struct IdwtRanges {
   int64_t cl[DWT_MAX_LEVEL + 1], dl[DWT_MAX_LEVEL + 1];
-  cl[0] = c;
-  dl[0] = d;
-  for (int l = 1; l <= L; ++l) {
-    cl[l] = cl[l - 1] >> 1;
-    dl[l] = ((dl[l - 1] - 1) >> 1) + 2;
-    if (dl[l] > LV.len[l]) dl[l] = LV.len[l];
+};
+
+template <int LEV>
+__device__ __forceinline__ IdwtRanges idwt_ranges(const Levels& LV, int64_t tile) {
+  IdwtRanges R;
+  const int64_t n = LV.len[0];
+  R.cl[0] = tile * IDWT_TILE;
+  R.dl[0] = (R.cl[0] + IDWT_TILE < n) ? R.cl[0] + IDWT_TILE : n;
+#pragma unroll
+  for (int l = 1; l <= LEV; ++l) {
+    R.cl[l] = R.cl[l - 1] >> 1;
+    R.dl[l] = ((R.dl[l - 1] - 1) >> 1) + 2;
+    if (R.dl[l] > LV.len[l]) R.dl[l] = LV.len[l];
   }
-  // level L approximation
-  for (int64_t p = cl[L] + threadIdx.x; p < dl[L]; p += 256) A[p - cl[L]] = coeffs[p];
-  __syncthreads();
+  return R;
+}
+
+// the tile's coefficients into registers (cA_L first, then cD_1 .. cD_LEV); all loads issued
+// before any is used
+template <int LEV>
+__device__ __forceinline__ void idwt_load(const float* __restrict__ coeffs, const Levels& LV,
+                                          const IdwtRanges& R, float (&pv)[idwt_npv<LEV>()]) {
+  const int t = threadIdx.x;
+  int k = 0;
+#pragma unroll
+  for (int u = 0; u < idwt_iters(LEV); ++u, ++k) {
+    const int64_t p = R.cl[LEV] + t + 256 * u;
+    pv[k] = p < R.dl[LEV] ? coeffs[p] : 0.0f;
+  }
+#pragma unroll
+  for (int l = 1; l <= LEV; ++l) {
+#pragma unroll
+    for (int u = 0; u < idwt_iters(l); ++u, ++k) {
+      const int64_t p = R.cl[l] + t + 256 * u;
+      pv[k] = p < R.dl[l] ? coeffs[LV.doff[l] + p] : 0.0f;
+    }
+  }
+}
+
+template <int LEV>
+__device__ __forceinline__ void idwt_stage(const IdwtRanges& R, const float (&pv)[idwt_npv<LEV>()],
+                                           float* A, float* D) {
+  const int t = threadIdx.x;
+  int k = 0;
+  const int na = (int)(R.dl[LEV] - R.cl[LEV]);
+#pragma unroll
+  for (int u = 0; u < idwt_iters(LEV); ++u, ++k) {
+    const int r = t + 256 * u;
+    if (r < na) A[r] = pv[k];
+  }
+#pragma unroll
+  for (int l = 1; l <= LEV; ++l) {
+    const int nd = (int)(R.dl[l] - R.cl[l]);
+#pragma unroll
+    for (int u = 0; u < idwt_iters(l); ++u, ++k) {
+      const int r = t + 256 * u;
+      if (r < nd) D[idwt_doff(l) + r] = pv[k];
+    }
+  }
+}
+
+template <int LEV>
+__device__ __forceinline__ void idwt_levels(const Levels& LV, const IdwtRanges& R,
+                                            float* __restrict__ out, float* A, float* B,
+                                            const float* D) {
   float* a = A;
   float* bnext = B;
   const float r0 = c_rec_lo[0], r1 = c_rec_lo[1], r2 = c_rec_lo[2], r3 = c_rec_lo[3];
   const float h0 = c_rec_hi[0], h1 = c_rec_hi[1], h2 = c_rec_hi[2], h3 = c_rec_hi[3];
-  for (int l = L; l >= 1; --l) {
-    const float* dd = coeffs + LV.doff[l];
-    const int64_t ca = cl[l];
-    const int64_t q_lo = cl[l - 1];
-    int64_t q_hi = dl[l - 1];
+#pragma unroll
+  for (int l = LEV; l >= 1; --l) {
+    const float* dd = D + idwt_doff(l);
+    int64_t q_hi = R.dl[l - 1];
     if (q_hi > LV.len[l - 1]) q_hi = LV.len[l - 1];
-    for (int64_t q = q_lo + threadIdx.x; q < q_hi; q += 256) {
-      const int64_t m = q >> 1;
-      const float am = a[m - ca], am1 = a[m + 1 - ca];
-      const float dm = dd[m], dm1 = dd[m + 1];
+    const int nq = (int)(q_hi - R.cl[l - 1]);  // cl[l - 1] is even: m - cl[l] = qr >> 1
+    float* const o1 = out + R.cl[0];
+    for (int qr = threadIdx.x; qr < nq; qr += 256) {
+      const int mr = qr >> 1;
+      const float am = a[mr], am1 = a[mr + 1];
+      const float dm = dd[mr], dm1 = dd[mr + 1];
       float ya, yd;
-      if ((q & 1) == 0) {
+      if ((qr & 1) == 0) {
         ya = r0 * am1; ya = ya + r2 * am;
         yd = h0 * dm1; yd = yd + h2 * dm;
       } else {
@@ -338,22 +405,38 @@ __device__ __forceinline__ void idwt_tile(const float* __restrict__ coeffs, cons
         yd = h1 * dm1; yd = yd + h3 * dm;
       }
       const float y = ya + yd;
-      if (l == 1) out[q] = y; else bnext[q - q_lo] = y;
+      if (l == 1) o1[qr] = y; else bnext[qr] = y;
     }
     if (l == 1) break;
     __syncthreads();
-    float* t = a; a = bnext; bnext = t;
+    float* tsw = a; a = bnext; bnext = tsw;
   }
 }
 
+template <int LEV>
 __global__ void __launch_bounds__(256) idwt_kernel(const float* __restrict__ coeffs, Levels LV,
                                                    float* __restrict__ out, int64_t ntiles) {
-  constexpr int SPANI = IDWT_TILE / 2 + 16;
-  __shared__ __attribute__((aligned(16))) float A[SPANI];
-  __shared__ __attribute__((aligned(16))) float B[SPANI];
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    idwt_tile(coeffs, LV, out, tile, A, B);
+  __shared__ __attribute__((aligned(16))) float A[IDWT_SPAN];
+  __shared__ __attribute__((aligned(16))) float B[IDWT_SPAN];
+  __shared__ __attribute__((aligned(16))) float D[IDWT_DALL];
+  int64_t tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  float pv[idwt_npv<LEV>()];
+  IdwtRanges R = idwt_ranges<LEV>(LV, tile);
+  idwt_load<LEV>(coeffs, LV, R, pv);
+  for (;;) {
+    idwt_stage<LEV>(R, pv, A, D);
     __syncthreads();
+    const IdwtRanges Rc = R;
+    const int64_t next = tile + gridDim.x;
+    if (next < ntiles) {  // the next tile's loads are in flight while this one is rebuilt
+      R = idwt_ranges<LEV>(LV, next);
+      idwt_load<LEV>(coeffs, LV, R, pv);
+    }
+    idwt_levels<LEV>(LV, Rc, out, A, B, D);
+    __syncthreads();  // the next tile reuses A / B / D
+    if (next >= ntiles) break;
+    tile = next;
   }
 }
 
@@ -428,6 +511,17 @@ extern "C" int dpz_idwt_sym2(const float* coeffs, int64_t n, int level, float* o
   if (!dwt_levels_ok(n, level)) return DPZ_ERR_UNSUPPORTED;
   const Levels LV = make_levels(n, level);
   const int64_t ntiles = (n + IDWT_TILE - 1) / IDWT_TILE;
-  DPZ_TIMED(DPZ_KT_IDWT, st, idwt_kernel<<<persistent_grid(idwt_kernel, 0, ntiles), 256, 0, st>>>(coeffs, LV, out, ntiles));
+  switch (level) {
+#define DPZ_IDWT_CASE(LEVN)                                                                       \
+  case LEVN:                                                                                      \
+    DPZ_TIMED(DPZ_KT_IDWT, st, idwt_kernel<LEVN><<<persistent_grid(idwt_kernel<LEVN>, 0, ntiles), \
+                                                  256, 0, st>>>(coeffs, LV, out, ntiles));         \
+    break;
+    DPZ_IDWT_CASE(1) DPZ_IDWT_CASE(2) DPZ_IDWT_CASE(3) DPZ_IDWT_CASE(4)
+    DPZ_IDWT_CASE(5) DPZ_IDWT_CASE(6) DPZ_IDWT_CASE(7) DPZ_IDWT_CASE(8)
+#undef DPZ_IDWT_CASE
+    default:
+      return DPZ_ERR_UNSUPPORTED;
+  }
   return DPZ_OK;
 }

@@ -318,6 +318,21 @@ def test_wavedec_waverec_bit_exact(dev, n):
     np.testing.assert_array_equal(_bits(rec), _bits(owav.waverec_array(owav.wavedec_array(x), n)))
 
 
+@pytest.mark.parametrize("level", [1, 2, 3, 5, 6, 8])
+@pytest.mark.parametrize("n", [301, 4096, 100_003, 1_000_001])
+def test_waverec_levels_bit_exact(dev, n, level):
+    """The staged IDWT is instantiated per level (1..8); the forward transform supports <= 4."""
+    codec = _codec()
+    rng = np.random.default_rng(n + level)
+    x = rng.standard_normal(n).astype(np.float32)
+    coeffs = owav.wavedec_array(x, level)
+    if level <= 4:
+        wx, _ = codec.wavedec(torch.from_numpy(x).to(dev), level)
+        np.testing.assert_array_equal(_bits(wx.cpu().numpy()), _bits(coeffs))
+    rec = codec.waverec(torch.from_numpy(coeffs).to(dev), n, level).cpu().numpy()
+    np.testing.assert_array_equal(_bits(rec), _bits(owav.waverec_array(coeffs, n, level)))
+
+
 def test_fp16_pack_roundtrip(dev):
     codec = _codec()
     for n in [1, 7, 8, 9, 1_000_003]:
