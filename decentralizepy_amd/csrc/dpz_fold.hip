@@ -36,6 +36,7 @@ constexpr int FOLD_MAXP = 16;  // payloads per launch (longer lists are chained)
 constexpr int FOLD_THREADS = DPZ_FOLD_THREADS;
 constexpr int FOLD_GROUPS = FOLD_TILE / (4 * FOLD_THREADS);  // float4 groups per thread
 constexpr int FOLD_EQ = 4;  // payload entries per thread preloaded at tile start
+constexpr int FOLD_NB = 4;  // phase path: next payload's extra entries per thread prefetched
 // hit-chain path: per-element chain head (u32) + per-entry value and (next | payload << 16),
 // the tile's local values and the distinct-hit list: 61 KB of LDS at 2816 entries (2 blocks of
 // 512 threads per CU, as the registers allow)
@@ -363,6 +364,28 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
     }
   } else {
   for (int j = t * 4; j < FOLD_TILE; j += 4 * FOLD_THREADS) *reinterpret_cast<uint32_t*>(&htag[j]) = 0xFFFFFFFFu;
+  // entries of a payload past the preloaded ones (dense ranges, e.g. JWINS alpha 0.1-0.4):
+  // the next payload's first FOLD_NB per thread are loaded while the current payload folds
+  int32_t nbi[FOLD_NB];
+  float nbv[FOLD_NB];
+  auto prefetch = [&](int pp) {
+#pragma unroll
+    for (int u = 0; u < FOLD_NB; ++u) nbi[u] = -1;
+    if (pp < a.np && !((a.dense_mask >> pp) & 1u)) {
+      const int64_t first = (int64_t)FOLD_EQ * FOLD_THREADS - pre[pp];
+      const int64_t j0 = rng[pp][0] + (first > 0 ? first : 0) + t;
+      const int64_t e = rng[pp][1];
+#pragma unroll
+      for (int u = 0; u < FOLD_NB; ++u) {
+        const int64_t j = j0 + (int64_t)u * FOLD_THREADS;
+        if (j < e) {
+          nbi[u] = s_idx[pp][j];
+          nbv[u] = s_val[pp][j];
+        }
+      }
+    }
+  };
+  prefetch(0);
   for (int p = 0; p < a.np; ++p) {
     const FoldPayload& P = a.p[p];
     __syncthreads();  // previous payload's reads of hv/htag done
@@ -377,10 +400,19 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
           }
         }
       }
-      // entries past the preloaded ones (dense payload ranges): loaded here
+#pragma unroll
+      for (int u = 0; u < FOLD_NB; ++u) {
+        const int64_t pos = (int64_t)nbi[u] - tlo;
+        if (pos >= 0 && pos < FOLD_TILE) {
+          hv[pos] = nbv[u];
+          htag[pos] = (uint8_t)p;
+        }
+      }
+      // entries past the preloaded and prefetched ones: loaded here
       const int64_t b = rng[p][0], e = rng[p][1];
       const int64_t first = (int64_t)FOLD_EQ * FOLD_THREADS - pre[p];  // relative to b
-      for (int64_t j = b + (first > 0 ? first : 0) + t; j < e; j += FOLD_THREADS) {
+      for (int64_t j = b + (first > 0 ? first : 0) + (int64_t)FOLD_NB * FOLD_THREADS + t; j < e;
+           j += FOLD_THREADS) {
         const int64_t pos = (int64_t)P.idx[j] - tlo;
         if (pos >= 0 && pos < FOLD_TILE) {
           hv[pos] = P.val[j];
@@ -389,6 +421,7 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
       }
     }
     __syncthreads();
+    prefetch(p + 1);
     const float w = P.w;
 #pragma unroll
     for (int q = 0; q < FOLD_GROUPS; ++q) {

@@ -238,7 +238,8 @@ def test_fold_matches_oracle(dev, n, npay):
 
 @pytest.mark.parametrize("n,alpha,npay", [(1_000_003, 0.01, 16), (1_000_003, 0.05, 16),
                                           (4_000_037, 0.01, 20), (300_001, 0.2, 3),
-                                          (300_001, 0.04, 5)])
+                                          (300_001, 0.04, 5), (100_003, 0.99, 2),
+                                          (200_003, 0.4, 3)])
 def test_fold_all_sparse_overlapping(dev, n, alpha, npay):
     """All-sparse payload groups take the one-phase hit-chain fold (tiles with more than its LDS
     capacity of entries fall back to the per-payload phases inside the same launch); payloads

@@ -12,7 +12,7 @@ from decentralizepy_amd import codec  # noqa: E402
 def main():
     dev = torch.device("cuda:0")
     m = 25_000_009
-    for alpha, npay in ((0.01, 16), (0.01, 4), (0.04, 16)):
+    for alpha, npay in ((0.01, 16), (0.01, 4), (0.1, 16), (0.25, 3), (0.4, 3)):
         k = round(alpha * m)
         g = torch.Generator(device=dev).manual_seed(1)
         pays = []
