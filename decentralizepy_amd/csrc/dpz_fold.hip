@@ -7,15 +7,21 @@
 //   sharing/JWINS/Wavelet.py:269-309 the same fold on wavelet coefficients
 //
 // Two launches per group of <= 16 payloads:
-//  * fold_offsets_kernel: one thread per payload entry writes, for every 4096-element output tile
-//    that starts after the previous entry, the first entry index inside that tile
+//  * fold_offsets_kernel: four payload entries per thread write, for every 4096-element output
+//    tile that starts after the previous entry, the first entry index inside that tile
 //    (start[p][t] = lower_bound(idx_p, t*4096)).  Coalesced over idx; replaces a dependent
 //    binary search per tile.
-//  * fold_kernel: one block per output tile.  For each payload in payload order the block
-//    scatters the tile's hits into an LDS value tile tagged with the payload number, and every
-//    thread folds its 16 elements:
-//      t = (tag == p) ? hit : local;  total = (p == 0) ? t*w : total + t*w
-//    in exactly the reference's fp32 order (library compiled with -ffp-contract=off).
+//  * fold_kernel: persistent blocks walk 4096-element tiles (the next tile's entry ranges
+//    prefetched).  Every payload's entries of the tile are loaded up front, flattened.  Then
+//    - hit-chain path (no dense payload, <= FOLD_CAP entries in the tile): entries are pushed on
+//      per-element hit chains in LDS in one pass; every element folds its base value alone
+//      (packed fp32 pairs), and the tile's distinct hit elements, compacted to a list, are
+//      folded exactly with their payload values (one thread each) and replace that result;
+//    - phase path (dense payloads / dense alpha): per payload the block scatters the tile's hits
+//      into an LDS value tile tagged with the payload number (the next payload's extra entries
+//      prefetched meanwhile), and every thread folds its 8 elements:
+//        t = (tag == p) ? hit : local;  total = (p == 0) ? t*w : total + t*w
+//    Both follow the reference's fp32 order exactly (library compiled with -ffp-contract=off).
 // Algorithmic bytes: read local (4N) + write out (4N) + 8 bytes per payload entry.
 #include <cstdlib>
 
@@ -70,21 +76,37 @@ struct FoldArgs {
 };
 
 // grid (ceil((kmax+1)/256), np): thread j of payload p handles entry j (j == k: end sentinel).
+// grid (ceil((kmax + 1) / (4 * 256)), np): thread g of payload p handles entries 4g .. 4g + 3
+// (j == k: the end sentinel); the four indices come in one 16-byte load when aligned.
 __global__ void __launch_bounds__(256) fold_offsets_kernel(FoldArgs a, int32_t* starts) {
   const int p = blockIdx.y;
   const FoldPayload& P = a.p[p];
   if (!P.idx) return;
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t j0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   const int64_t k = P.k;
-  if (j > k) return;
-  int64_t tprev = j == 0 ? -1 : ((int64_t)P.idx[j - 1] >> FOLD_TILE_SHIFT);
-  int64_t tcur = j == k ? a.ntiles : ((int64_t)P.idx[j] >> FOLD_TILE_SHIFT);
-  // an invalid payload (negative / too large / unsorted indices) must not write out of bounds
-  if (tprev < -1) tprev = -1;
-  if (tprev > a.ntiles) tprev = a.ntiles;
-  if (tcur > a.ntiles) tcur = a.ntiles;
+  if (j0 > k) return;
+  int32_t v[5];  // idx[j0 - 1 .. j0 + 3]
+  v[0] = j0 == 0 ? 0 : P.idx[j0 - 1];
+  if (j0 + 4 <= k && (reinterpret_cast<uintptr_t>(P.idx + j0) & 15u) == 0) {
+    const int4 q = *reinterpret_cast<const int4*>(P.idx + j0);
+    v[1] = q.x; v[2] = q.y; v[3] = q.z; v[4] = q.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e + 1] = (j0 + e < k) ? P.idx[j0 + e] : 0;
+  }
   int32_t* st = starts + (int64_t)p * (a.ntiles + 1);
-  for (int64_t t = tprev + 1; t <= tcur; ++t) st[t] = (int32_t)j;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int64_t j = j0 + e;
+    if (j > k) break;
+    int64_t tprev = j == 0 ? -1 : ((int64_t)v[e] >> FOLD_TILE_SHIFT);
+    int64_t tcur = j == k ? a.ntiles : ((int64_t)v[e + 1] >> FOLD_TILE_SHIFT);
+    // an invalid payload (negative / too large / unsorted indices) must not write out of bounds
+    if (tprev < -1) tprev = -1;
+    if (tprev > a.ntiles) tprev = a.ntiles;
+    if (tcur > a.ntiles) tcur = a.ntiles;
+    for (int64_t t = tprev + 1; t <= tcur; ++t) st[t] = (int32_t)j;
+  }
 }
 
 // one payload term of the fold in the reference's fp32 order: the first term of a fresh total is
@@ -600,7 +622,7 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
         fa.dense_mask |= 1u << i;
       }
     if (kmax >= 0) {
-      dim3 og((unsigned)((kmax + 1 + 255) / 256), (unsigned)fa.np);
+      dim3 og((unsigned)((kmax + 1 + 1023) / 1024), (unsigned)fa.np);
       DPZ_TIMED(DPZ_KT_FOLD_OFFSETS, st, fold_offsets_kernel<<<og, 256, 0, st>>>(fa, starts));
     }
     if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<true><<<fold_grid<true>(ntiles), FOLD_THREADS, 0, st>>>(fa));
