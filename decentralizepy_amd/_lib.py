@@ -23,6 +23,7 @@ DPZ_FOLD_REPLACE_ONLY = 0x2
 DPZ_FOLD_ZERO_BASE = 0x4
 DPZ_FOLD_ADD_ONLY = 0x8
 DPZ_FOLD_ACCUMULATE = 0x10
+DPZ_FOLD_ALSO_LOCAL = 0x20
 DPZ_EW_SUB = 1
 DPZ_EW_ADD = 2
 DPZ_EW_CHOCO = 3

@@ -160,7 +160,8 @@ def topk_status(workspace):
 
 
 def decode_average(local, payloads, weights=None, w_self=None, out=None, replace_only=False,
-                   workspace=None, zero_base=False, add_only=False, accumulate=False):
+                   workspace=None, zero_base=False, add_only=False, accumulate=False,
+                   also_local=False):
     """Batched replace + Metro-Hastings fold (reference Sharing.py:156-229, PartialModel.py:257-303).
 
     payloads : list of ``(idx int32 device tensor or None, vals fp32 device tensor)``
@@ -170,6 +171,7 @@ def decode_average(local, payloads, weights=None, w_self=None, out=None, replace
                and the fold starts from +0.0 (DPZ_FOLD_ZERO_BASE)
     add_only : one payload, ``out = local + T`` with T zero-based (DPZ_FOLD_ADD_ONLY)
     accumulate: ``out`` holds a running total the fold continues (DPZ_FOLD_ACCUMULATE)
+    also_local: the result is also written over ``local`` in place (DPZ_FOLD_ALSO_LOCAL)
     """
     _require(local, torch.float32, "local")
     n = local.numel()
@@ -196,7 +198,8 @@ def decode_average(local, payloads, weights=None, w_self=None, out=None, replace
              | (DPZ_FOLD_REPLACE_ONLY if replace_only else 0)
              | (_lib.DPZ_FOLD_ZERO_BASE if zero_base else 0)
              | (_lib.DPZ_FOLD_ADD_ONLY if add_only else 0)
-             | (_lib.DPZ_FOLD_ACCUMULATE if accumulate else 0))
+             | (_lib.DPZ_FOLD_ACCUMULATE if accumulate else 0)
+             | (_lib.DPZ_FOLD_ALSO_LOCAL if also_local else 0))
     ws = (workspace or Workspace(local.device)).get_decode(n, npay)
     rc = _lib.lib().dpz_decode_average(_ptr(local), n, npay, idx_arr, val_arr, k_arr, w_arr,
                                        float(w_self) if w_self is not None else 0.0, flags,

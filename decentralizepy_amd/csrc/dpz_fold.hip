@@ -61,6 +61,7 @@ struct FoldPayload {
 struct FoldArgs {
   const float* local;
   float* out;
+  float* out2;  // DPZ_FOLD_ALSO_LOCAL: the result also over local (in place), else nullptr
   const int32_t* starts;  // [np][ntiles + 1]
   int64_t n;
   int64_t ntiles;
@@ -488,12 +489,17 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
   for (int q = 0; q < FOLD_GROUPS; ++q) {
     const int64_t i0 = tlo + q * 4 * FOLD_THREADS + t * 4;
     if (VEC && i0 + 3 < thi) {
-      *reinterpret_cast<float4*>(a.out + i0) =
-          make_float4(acc[q * 4 + 0], acc[q * 4 + 1], acc[q * 4 + 2], acc[q * 4 + 3]);
+      const float4 r4 = make_float4(acc[q * 4 + 0], acc[q * 4 + 1], acc[q * 4 + 2], acc[q * 4 + 3]);
+      *reinterpret_cast<float4*>(a.out + i0) = r4;
+      // in place over local: every local read of this tile happened before (registers / LDS)
+      if (a.out2) *reinterpret_cast<float4*>(a.out2 + i0) = r4;
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        if (i0 + e < thi) a.out[i0 + e] = acc[q * 4 + e];
+        if (i0 + e < thi) {
+          a.out[i0 + e] = acc[q * 4 + e];
+          if (a.out2) a.out2[i0 + e] = acc[q * 4 + e];
+        }
     }
   }
   __syncthreads();  // the next tile reuses rng / pre / the LDS tile
@@ -553,6 +559,9 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
   const bool add_only = (flags & DPZ_FOLD_ADD_ONLY) != 0;
   const bool zero_base = (flags & DPZ_FOLD_ZERO_BASE) != 0;
   if ((replace_only || add_only) && n_payloads != 1) return DPZ_ERR_ARG;
+  const bool also_local = (flags & DPZ_FOLD_ALSO_LOCAL) != 0;
+  if (also_local && (replace_only || add_only)) return DPZ_ERR_ARG;
+  float* const out2 = also_local ? const_cast<float*>(local) : nullptr;
   if (replace_only && add_only) return DPZ_ERR_ARG;
   if (n_payloads > 0 && (!vals || !k || (!replace_only && !add_only && !w))) return DPZ_ERR_ARG;
   // payload i is dense (a full model) iff idx[i] == NULL and k[i] == n
@@ -571,7 +580,7 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
   if (n_payloads == 0) {
     // no payloads: out = w_self * local (self term only) or zeros
     FoldArgs fa{};
-    fa.local = local; fa.out = out; fa.starts = starts; fa.n = n; fa.ntiles = ntiles;
+    fa.local = local; fa.out = out; fa.out2 = out2; fa.starts = starts; fa.n = n; fa.ntiles = ntiles;
     fa.np = 0; fa.first = 0;
     fa.add_self = (flags & DPZ_FOLD_SELF) ? 1 : 0; fa.w_self = w_self;
     if (!(flags & DPZ_FOLD_ACCUMULATE)) DPZ_HIP_TRY(hipMemsetAsync(out, 0, n * sizeof(float), st));
@@ -595,10 +604,12 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
   }
   for (int base = 0; base < n_payloads; base += FOLD_MAXP) {
     FoldArgs fa{};
-    fa.local = local; fa.out = out; fa.starts = starts; fa.n = n; fa.ntiles = ntiles;
+    fa.local = local; fa.out = out; fa.out2 = out2; fa.starts = starts; fa.n = n; fa.ntiles = ntiles;
     fa.np = (n_payloads - base) < FOLD_MAXP ? (n_payloads - base) : FOLD_MAXP;
     fa.first = (base == 0 && !(flags & DPZ_FOLD_ACCUMULATE)) ? 1 : 0;
     fa.add_self = (base + fa.np == n_payloads && ((flags & DPZ_FOLD_SELF) || add_only)) ? 1 : 0;
+    // over local only with the last group: the earlier groups' launches still read local
+    if (base + fa.np != n_payloads) fa.out2 = nullptr;
     fa.replace_only = replace_only ? 1 : 0;
     fa.zero_base = (zero_base || add_only) ? 1 : 0;
     fa.w_self = add_only ? 1.0f : w_self;

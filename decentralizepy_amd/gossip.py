@@ -183,7 +183,7 @@ class GossipRound:
         nodes = range(self.hi - self.lo)
         if self._hip:
             from . import _lib
-            from ._lib import DPZ_FOLD_SELF
+            from ._lib import DPZ_FOLD_ALSO_LOCAL, DPZ_FOLD_SELF
             tab = getattr(self, "_tab", None)
             if tab is None or tab["key"] != (self.recv_idx.data_ptr(), self.recv_val.data_ptr()):
                 tab = self._tab = self._fold_tables()
@@ -196,7 +196,8 @@ class GossipRound:
                 st.wait_stream(cur)
             rc = _lib.lib().dpz_decode_average_batch(
                 m, self._ptrs(self.x[:m]), self._ptrs(self.out[:m]), self.N, tab["np"],
-                tab["idx"], tab["val"], tab["k"], tab["w"], tab["w_self"], DPZ_FOLD_SELF,
+                tab["idx"], tab["val"], tab["k"], tab["w"], tab["w_self"],
+                DPZ_FOLD_SELF | DPZ_FOLD_ALSO_LOCAL,
                 self._ptrs(dws), min(d.numel() for d in dws), len(self.streams), streams)
             _lib.check(rc, "dpz_decode_average_batch")
             for st in self.streams:
@@ -209,9 +210,11 @@ class GossipRound:
                 self._fold(self.x[j], payloads, w, w_self, self.out[j])
         # post step: the averaged model becomes both the model and init_model (reference
         # Sharing._averaging load_state_dict + PartialModel._post_step): init_model takes the
-        # fold output buffer (swap, no copy), the model gets one copy of it
+        # fold output buffer (swap, no copy); the HIP fold also wrote the result over the model
+        # in place (DPZ_FOLD_ALSO_LOCAL), the injected CPU fold gets one copy
         self.x0, self.out = self.out, self.x0
-        self.x.copy_(self.x0)
+        if not self._hip:
+            self.x.copy_(self.x0)
 
     def _slot(self, node):
         r = node // self.per

@@ -64,6 +64,11 @@ typedef void* dpz_stream_t; /* hipStream_t */
                                      s += w * T_i; s += (1 - sum w) * q)                      */
 #define DPZ_FOLD_ADD_ONLY 0x8     /* n_payloads == 1: out = local + T_0 with T_0 zero-based
                                      (reference STC.py:290-303 process_received)              */
+#define DPZ_FOLD_ALSO_LOCAL 0x20  /* the result is ALSO written over local, in place (the
+                                     reference's load_state_dict of the averaged model while
+                                     _post_step makes it init_model, Sharing.py:186-190,
+                                     PartialModel.py:333-353): saves a model copy per round.
+                                     Not with REPLACE_ONLY / ADD_ONLY.                       */
 
 int dpz_abi_version(void);
 const char* dpz_error_string(int code);

@@ -268,6 +268,28 @@ def test_fold_all_sparse_overlapping(dev, n, alpha, npay):
     np.testing.assert_array_equal(_bits(out2), _bits(ref2))
 
 
+@pytest.mark.parametrize("npay", [0, 3, 20])
+def test_fold_also_local_in_place(dev, npay):
+    """DPZ_FOLD_ALSO_LOCAL: out and local both end as the fold (local read before overwritten,
+    also across chained payload groups)."""
+    codec = _codec()
+    n = 1_000_003
+    rng = np.random.default_rng(npay + 7)
+    local = rng.standard_normal(n).astype(np.float32)
+    pays, tpays = [], []
+    for i in range(npay):
+        idx, vals = _payload(n, n // 100, seed=100 + i, local=local)
+        pays.append((idx, vals))
+        tpays.append((torch.from_numpy(idx).to(dev), torch.from_numpy(vals).to(dev)))
+    weights = [1 / (npay + 1)] * npay
+    w_self = 1 - sum(weights)
+    ref = ofold.fold(local, pays, weights, w_self)
+    tl = torch.from_numpy(local).to(dev)
+    out = codec.decode_average(tl, tpays, weights, w_self, also_local=True)
+    np.testing.assert_array_equal(_bits(out.cpu().numpy()), _bits(ref))
+    np.testing.assert_array_equal(_bits(tl.cpu().numpy()), _bits(ref))
+
+
 @pytest.mark.parametrize("n,k", [(1000, 10), (1000, 0), (1000, 1000), (11_000_000, 110_000)])
 def test_replace_matches_oracle(dev, n, k):
     codec = _codec()
