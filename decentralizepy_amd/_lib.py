@@ -70,6 +70,11 @@ SIGNATURES = {
     "dpz_wavedec_len": (_i64, [_i64, _int]),
     "dpz_dwt_sym2": (_int, [_c_void_p, _c_void_p, _i64, _int, _c_void_p, _c_void_p, _int,
                             _c_void_p]),
+    "dpz_dwt_tile_width": (_i64, []),
+    "dpz_idwt_tile_width": (_i64, []),
+    "dpz_dwt_sym2_tiles": (_int, [_c_void_p, _c_void_p, _i64, _int, _i64, _i64, _c_void_p,
+                                  _c_void_p, _int, _c_void_p]),
+    "dpz_idwt_sym2_tiles": (_int, [_c_void_p, _i64, _int, _i64, _i64, _c_void_p, _c_void_p]),
     "dpz_idwt_sym2": (_int, [_c_void_p, _i64, _int, _c_void_p, _c_void_p]),
     "dpz_scatter_fill": (_int, [_c_void_p, _i64, _c_void_p, _i64, ctypes.c_float, _c_void_p]),
     "dpz_pack_fp16": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),

@@ -270,10 +270,11 @@ __device__ __forceinline__ void dwt_levels(const Levels& LV, float* cx, float* c
 template <bool WX, bool WD, bool ACCUM>
 __global__ void __launch_bounds__(256, DPZ_DWT_WAVES) dwt_kernel(const float* __restrict__ x,
                                                   const float* __restrict__ x0, Levels LV,
-                                                  float* cx, float* cd, int64_t ntiles) {
+                                                  float* cx, float* cd, int64_t tile0,
+                                                  int64_t ntiles) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int64_t n = LV.len[0];
-  int64_t tile = blockIdx.x;
+  int64_t tile = tile0 + blockIdx.x;  // tiles [tile0, ntiles): a rank's share when sharded
   if (tile >= ntiles) return;
   float4 va[DWT_NG], vb[DWT_NG];
   int64_t s0, e0;
@@ -415,11 +416,12 @@ __device__ __forceinline__ void idwt_levels(const Levels& LV, const IdwtRanges& 
 
 template <int LEV>
 __global__ void __launch_bounds__(256) idwt_kernel(const float* __restrict__ coeffs, Levels LV,
-                                                   float* __restrict__ out, int64_t ntiles) {
+                                                   float* __restrict__ out, int64_t tile0,
+                                                   int64_t ntiles) {
   __shared__ __attribute__((aligned(16))) float A[IDWT_SPAN];
   __shared__ __attribute__((aligned(16))) float B[IDWT_SPAN];
   __shared__ __attribute__((aligned(16))) float D[IDWT_DALL];
-  int64_t tile = blockIdx.x;
+  int64_t tile = tile0 + blockIdx.x;
   if (tile >= ntiles) return;
   float pv[idwt_npv<LEV>()];
   IdwtRanges R = idwt_ranges<LEV>(LV, tile);
@@ -476,46 +478,66 @@ extern "C" int64_t dpz_wavedec_len(int64_t n, int level) {
   return make_levels(n, level).total;
 }
 
-extern "C" int dpz_dwt_sym2(const float* x, const float* x0, int64_t n, int level,
-                            float* coeffs_x, float* coeffs_diff, int accumulate,
-                            dpz_stream_t stream) {
+extern "C" int64_t dpz_dwt_tile_width(void) { return DWT_TL; }
+extern "C" int64_t dpz_idwt_tile_width(void) { return IDWT_TILE; }
+
+extern "C" int dpz_dwt_sym2_tiles(const float* x, const float* x0, int64_t n, int level,
+                                  int64_t tile_lo, int64_t tile_hi, float* coeffs_x,
+                                  float* coeffs_diff, int accumulate, dpz_stream_t stream) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (!x || n <= 0) return DPZ_ERR_ARG;
   if (!dwt_levels_ok(n, level) || level > 4) return DPZ_ERR_UNSUPPORTED;
   if (coeffs_diff && !x0) return DPZ_ERR_ARG;
-  if (!coeffs_x && !coeffs_diff) return DPZ_OK;
   const Levels LV = make_levels(n, level);
   const int64_t ntiles = (LV.len[level] + DWT_TL - 1) / DWT_TL;
+  if (tile_lo < 0 || tile_hi > ntiles || tile_lo > tile_hi) return DPZ_ERR_ARG;
+  if ((!coeffs_x && !coeffs_diff) || tile_lo == tile_hi) return DPZ_OK;
   constexpr int SPAN0 = 16 * DWT_TL + 64, SPAN1 = 8 * DWT_TL + 32;
   const size_t shm = 2 * (SPAN0 + SPAN1) * sizeof(float);
   const bool wx = coeffs_x != nullptr, wd = coeffs_diff != nullptr;
+  const int64_t nt = tile_hi - tile_lo;
   const int tslot = timing_begin(DPZ_KT_DWT, st);
   if (wx && wd) {
-    if (accumulate) dwt_kernel<true, true, true><<<persistent_grid(dwt_kernel<true, true, true>, shm, ntiles), 256, shm, st>>>(x, x0, LV, coeffs_x, coeffs_diff, ntiles);
-    else dwt_kernel<true, true, false><<<persistent_grid(dwt_kernel<true, true, false>, shm, ntiles), 256, shm, st>>>(x, x0, LV, coeffs_x, coeffs_diff, ntiles);
+    if (accumulate) dwt_kernel<true, true, true><<<persistent_grid(dwt_kernel<true, true, true>, shm, nt), 256, shm, st>>>(x, x0, LV, coeffs_x, coeffs_diff, tile_lo, tile_hi);
+    else dwt_kernel<true, true, false><<<persistent_grid(dwt_kernel<true, true, false>, shm, nt), 256, shm, st>>>(x, x0, LV, coeffs_x, coeffs_diff, tile_lo, tile_hi);
   } else if (wx) {
-    dwt_kernel<true, false, false><<<persistent_grid(dwt_kernel<true, false, false>, shm, ntiles), 256, shm, st>>>(x, x0, LV, coeffs_x, nullptr, ntiles);
+    dwt_kernel<true, false, false><<<persistent_grid(dwt_kernel<true, false, false>, shm, nt), 256, shm, st>>>(x, x0, LV, coeffs_x, nullptr, tile_lo, tile_hi);
   } else {
-    if (accumulate) dwt_kernel<false, true, true><<<persistent_grid(dwt_kernel<false, true, true>, shm, ntiles), 256, shm, st>>>(x, x0, LV, nullptr, coeffs_diff, ntiles);
-    else dwt_kernel<false, true, false><<<persistent_grid(dwt_kernel<false, true, false>, shm, ntiles), 256, shm, st>>>(x, x0, LV, nullptr, coeffs_diff, ntiles);
+    if (accumulate) dwt_kernel<false, true, true><<<persistent_grid(dwt_kernel<false, true, true>, shm, nt), 256, shm, st>>>(x, x0, LV, nullptr, coeffs_diff, tile_lo, tile_hi);
+    else dwt_kernel<false, true, false><<<persistent_grid(dwt_kernel<false, true, false>, shm, nt), 256, shm, st>>>(x, x0, LV, nullptr, coeffs_diff, tile_lo, tile_hi);
   }
   DPZ_LAUNCH_CHECK();
   timing_end(tslot, st);
   return DPZ_OK;
 }
 
-extern "C" int dpz_idwt_sym2(const float* coeffs, int64_t n, int level, float* out,
-                             dpz_stream_t stream) {
+extern "C" int dpz_dwt_sym2(const float* x, const float* x0, int64_t n, int level,
+                            float* coeffs_x, float* coeffs_diff, int accumulate,
+                            dpz_stream_t stream) {
+  if (!x || n <= 0) return DPZ_ERR_ARG;
+  if (!dwt_levels_ok(n, level) || level > 4) return DPZ_ERR_UNSUPPORTED;
+  const Levels LV = make_levels(n, level);
+  const int64_t ntiles = (LV.len[level] + DWT_TL - 1) / DWT_TL;
+  return dpz_dwt_sym2_tiles(x, x0, n, level, 0, ntiles, coeffs_x, coeffs_diff, accumulate,
+                            stream);
+}
+
+extern "C" int dpz_idwt_sym2_tiles(const float* coeffs, int64_t n, int level, int64_t tile_lo,
+                                   int64_t tile_hi, float* out, dpz_stream_t stream) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (!coeffs || !out || n <= 0) return DPZ_ERR_ARG;
   if (!dwt_levels_ok(n, level)) return DPZ_ERR_UNSUPPORTED;
   const Levels LV = make_levels(n, level);
   const int64_t ntiles = (n + IDWT_TILE - 1) / IDWT_TILE;
+  if (tile_lo < 0 || tile_hi > ntiles || tile_lo > tile_hi) return DPZ_ERR_ARG;
+  if (tile_lo == tile_hi) return DPZ_OK;
+  const int64_t nt = tile_hi - tile_lo;
   switch (level) {
-#define DPZ_IDWT_CASE(LEVN)                                                                       \
-  case LEVN:                                                                                      \
-    DPZ_TIMED(DPZ_KT_IDWT, st, idwt_kernel<LEVN><<<persistent_grid(idwt_kernel<LEVN>, 0, ntiles), \
-                                                  256, 0, st>>>(coeffs, LV, out, ntiles));         \
+#define DPZ_IDWT_CASE(LEVN)                                                                    \
+  case LEVN:                                                                                   \
+    DPZ_TIMED(DPZ_KT_IDWT, st, idwt_kernel<LEVN><<<persistent_grid(idwt_kernel<LEVN>, 0, nt), \
+                                                  256, 0, st>>>(coeffs, LV, out, tile_lo,      \
+                                                                tile_hi));                     \
     break;
     DPZ_IDWT_CASE(1) DPZ_IDWT_CASE(2) DPZ_IDWT_CASE(3) DPZ_IDWT_CASE(4)
     DPZ_IDWT_CASE(5) DPZ_IDWT_CASE(6) DPZ_IDWT_CASE(7) DPZ_IDWT_CASE(8)
@@ -524,4 +546,10 @@ extern "C" int dpz_idwt_sym2(const float* coeffs, int64_t n, int level, float* o
       return DPZ_ERR_UNSUPPORTED;
   }
   return DPZ_OK;
+}
+
+extern "C" int dpz_idwt_sym2(const float* coeffs, int64_t n, int level, float* out,
+                             dpz_stream_t stream) {
+  if (n <= 0) return DPZ_ERR_ARG;
+  return dpz_idwt_sym2_tiles(coeffs, n, level, 0, (n + IDWT_TILE - 1) / IDWT_TILE, out, stream);
 }

@@ -117,3 +117,164 @@ def sharded_topk_encode(x, x0, k, offset, counter=None, group=None, ops=None):
     if counter is not None:
         ops.count(counter, widx, offset)
     return widx, wval
+
+
+# ---------------------------------------------------------------------------------------------
+# One tensor's sym2 DWT / IDWT over ranks (SURVEY.md §8e "wavelet DWT/IDWT: yes, with a halo").
+#
+# The model is cut into IDWT tiles of V = 4096 outputs; rank r owns the contiguous tiles
+# [u_lo, u_hi) = its model slice [lo, hi).  The forward tiles (W = 128 level-L outputs, 2^L * W
+# inputs) of that slice start at t_lo = lo / (2^L W): a rank's forward tiles read only its own
+# slice plus a LEFT halo of 2 (2^L - 1) inputs (30 at level 4; 32 kept, see halo_len), the tail
+# of rank r - 1's slice,
+# exchanged with one small all-gather.  Every rank writes the coefficients its tiles own (one
+# range per level) and one all-gather of those owned ranges gives every rank the whole
+# [cA_L, cD_L, ..., cD_1] array (what the fold and the IDWT read).  The inverse needs no exchange
+# once the coefficients are whole: each rank rebuilds its own slice.  Bit-identical to the
+# one-GPU transform (tests/test_gpu_shard.py; the exchange logic: tests/test_cpu_shard.py).
+
+def _level_lengths(n, level):
+    lens = [n]
+    for _ in range(level):
+        lens.append((lens[-1] + 3) // 2)
+    return lens
+
+
+def wavelet_slice(n, level, world, rank, dwt_tile=128, idwt_tile=4096):
+    """Rank `rank`'s model slice [lo, hi) and its forward / inverse tile ranges."""
+    span = (1 << level) * dwt_tile
+    if idwt_tile % span:
+        raise ValueError("level too deep for the shared tiling (needs 2^level * 128 | 4096)")
+    lens = _level_lengths(n, level)
+    n_fwd = -(-lens[level] // dwt_tile)
+    n_inv = -(-n // idwt_tile)
+    per = -(-n_inv // world)
+    u_lo, u_hi = min(rank * per, n_inv), min((rank + 1) * per, n_inv)
+    lo, hi = min(u_lo * idwt_tile, n), min(u_hi * idwt_tile, n)
+    t_lo = min(lo // span, n_fwd)
+    t_hi = n_fwd if rank == world - 1 else min(hi // span, n_fwd)
+    return dict(lo=lo, hi=hi, t_lo=t_lo, t_hi=t_hi, u_lo=u_lo, u_hi=u_hi)
+
+
+def owned_coeff_ranges(n, level, t_lo, t_hi, last, dwt_tile=128):
+    """[start, end) ranges of the coefficient array written by forward tiles [t_lo, t_hi)."""
+    lens = _level_lengths(n, level)
+    out = [(t_lo * dwt_tile, min(t_hi * dwt_tile, lens[level]))]  # cA_L
+    off = lens[level]
+    for lv in range(level, 0, -1):
+        s = t_lo * dwt_tile << (level - lv)
+        e = lens[lv] if last else min(t_hi * dwt_tile << (level - lv), lens[lv])
+        out.append((off + min(s, lens[lv]), off + e))
+        off += lens[lv]
+    return out
+
+
+def halo_len(level):
+    """Left halo a forward slice needs: 2 (2^L - 1) inputs, rounded up to 4 so that the halo'd
+    buffer keeps the kernel's float4 groups (which start at a multiple of 4) aligned and inside
+    the buffer."""
+    return (2 * ((1 << level) - 1) + 3) // 4 * 4
+
+
+def _virtual(t, first_index):
+    """Address of global element 0 for a buffer holding elements from `first_index` on."""
+    return t.data_ptr() - int(first_index) * t.element_size()
+
+
+def dwt_rank_part(xbuf, x0buf, buf_first, n, level, t_lo, t_hi, cx, cd, accumulate=False):
+    """Forward tiles [t_lo, t_hi) from a halo'd slice buffer whose element 0 is global element
+    `buf_first`; writes the owned coefficients into the full-length cx / cd (may be None)."""
+    dev = xbuf.device
+    rc = _lib.lib().dpz_dwt_sym2_tiles(
+        _virtual(xbuf, buf_first), _virtual(x0buf, buf_first) if x0buf is not None else None,
+        n, level, t_lo, t_hi, _ptr(cx) if cx is not None else None,
+        _ptr(cd) if cd is not None else None, 1 if accumulate else 0, _stream(dev))
+    _lib.check(rc, "dpz_dwt_sym2_tiles")
+
+
+def _exchange_owned(arrs, n, level, world, rank, group, dist):
+    """All-gather every rank's owned coefficient ranges of each array in `arrs` (in place)."""
+    parts = [owned_coeff_ranges(n, level, **{k: wavelet_slice(n, level, world, r)[k]
+                                             for k in ("t_lo", "t_hi")}, last=(r == world - 1))
+             for r in range(world)]
+    sizes = [sum(e - s for s, e in p) for p in parts]
+    cap = max(sizes)
+    dev = arrs[0].device
+    send = torch.zeros(len(arrs) * cap, dtype=torch.float32, device=dev)
+    o = 0
+    for s, e in parts[rank]:
+        for a_i, a in enumerate(arrs):
+            send[a_i * cap + o:a_i * cap + o + (e - s)] = a[s:e]
+        o += e - s
+    recv = torch.empty(world * len(arrs) * cap, dtype=torch.float32, device=dev)
+    dist.all_gather_into_tensor(recv, send, group=group)
+    recv = recv.view(world, len(arrs), cap)
+    for r in range(world):
+        if r == rank:
+            continue
+        o = 0
+        for s, e in parts[r]:
+            for a_i, a in enumerate(arrs):
+                a[s:e] = recv[r, a_i, o:o + (e - s)]
+            o += e - s
+
+
+def sharded_wavedec(x_slice, x0_slice, n, level, group=None, accumulate_into=None):
+    """W(x) and W(x - x0) of a tensor sharded over the ranks of `group` (rank r holds its
+    wavelet_slice [lo, hi) of x and x0).  Returns the whole coefficient arrays on every rank
+    (W(x), W(x - x0) — or, with ``accumulate_into``, that array += W(x - x0) and W(x))."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    sl = wavelet_slice(n, level, world, rank, int(_lib.lib().dpz_dwt_tile_width()),
+                       int(_lib.lib().dpz_idwt_tile_width()))
+    if x_slice.numel() != sl["hi"] - sl["lo"]:
+        raise ValueError("x_slice must be this rank's wavelet_slice of the tensor")
+    H = halo_len(level)
+    for r in range(world - 1):
+        s = wavelet_slice(n, level, world, r)
+        if s["hi"] - s["lo"] < H:
+            raise ValueError("tensor too small for this many ranks (a slice is shorter than the halo)")
+    dev = x_slice.device
+    xb, x0b, first = x_slice, x0_slice, sl["lo"]
+    if world > 1:
+        # the left halo: the last H elements of rank r - 1's slice (x and x0), one all-gather
+        tail = torch.zeros(2 * H, dtype=torch.float32, device=dev)
+        m = min(H, x_slice.numel())
+        tail[H - m:H] = x_slice[x_slice.numel() - m:]
+        tail[2 * H - m:] = x0_slice[x0_slice.numel() - m:]
+        tails = torch.empty(world * 2 * H, dtype=torch.float32, device=dev)
+        dist.all_gather_into_tensor(tails, tail, group=group)
+        if rank > 0:
+            prev = tails.view(world, 2 * H)[rank - 1]
+            xb = torch.cat([prev[:H], x_slice])
+            x0b = torch.cat([prev[H:], x0_slice])
+            first = sl["lo"] - H
+    m_len = codec.wavedec_len(n, level)
+    cx = torch.zeros(m_len, dtype=torch.float32, device=dev)
+    cd = accumulate_into if accumulate_into is not None else torch.zeros_like(cx)
+    dwt_rank_part(xb, x0b, first, n, level, sl["t_lo"], sl["t_hi"], cx, cd,
+                  accumulate=accumulate_into is not None)
+    if world > 1:
+        _exchange_owned([cx, cd], n, level, world, rank, group, dist)
+    return cx, cd
+
+
+def idwt_rank_part(coeffs, n, level, u_lo, u_hi, out_slice, lo):
+    """Inverse tiles [u_lo, u_hi) of the whole coefficient array into out_slice (global [lo, ..))."""
+    rc = _lib.lib().dpz_idwt_sym2_tiles(_ptr(coeffs), n, level, u_lo, u_hi,
+                                        _virtual(out_slice, lo), _stream(coeffs.device))
+    _lib.check(rc, "dpz_idwt_sym2_tiles")
+
+
+def sharded_waverec(coeffs, n, level, group=None):
+    """This rank's slice [lo, hi) of the inverse transform of the whole coefficient array."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    sl = wavelet_slice(n, level, world, rank, int(_lib.lib().dpz_dwt_tile_width()),
+                       int(_lib.lib().dpz_idwt_tile_width()))
+    out = torch.empty(sl["hi"] - sl["lo"], dtype=torch.float32, device=coeffs.device)
+    if out.numel():
+        idwt_rank_part(coeffs, n, level, sl["u_lo"], sl["u_hi"], out, sl["lo"])
+    return out

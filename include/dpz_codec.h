@@ -203,6 +203,22 @@ int dpz_dwt_sym2(const float* x, const float* x0, int64_t n, int level, float* c
  * Replaces reference sharing/JWINS/Wavelet.py:311-316.                                        */
 int dpz_idwt_sym2(const float* coeffs, int64_t n, int level, float* out, dpz_stream_t stream);
 
+/* Tile ranges of the two transforms, for one tensor sharded over ranks (SURVEY §8e "wavelet
+ * DWT/IDWT: yes, with a halo"; decentralizepy_amd/shard.py sharded_wavedec / sharded_waverec).
+ * The forward tile t owns level-L outputs [t*W, (t+1)*W) (W = dpz_dwt_tile_width()) and the
+ * matching 2^(L-l)*W outputs of every detail level; it reads inputs [2^L*W*t - 2(2^L - 1),
+ * 2^L*W*(t+1)) of x / x0 (clipped to [0, n)).  The inverse tile u writes outputs
+ * [u*V, (u+1)*V) (V = dpz_idwt_tile_width()).  x, x0, coeffs and out are VIRTUAL bases: element i
+ * of the global array is at base + i, and only the elements the tiles [tile_lo, tile_hi) touch
+ * are dereferenced (a rank passes its halo'd slice buffer minus its first global index).        */
+int64_t dpz_dwt_tile_width(void);
+int64_t dpz_idwt_tile_width(void);
+int dpz_dwt_sym2_tiles(const float* x, const float* x0, int64_t n, int level, int64_t tile_lo,
+                       int64_t tile_hi, float* coeffs_x, float* coeffs_diff, int accumulate,
+                       dpz_stream_t stream);
+int dpz_idwt_sym2_tiles(const float* coeffs, int64_t n, int level, int64_t tile_lo,
+                        int64_t tile_hi, float* out, dpz_stream_t stream);
+
 /* dst[idx[j]] = value for j < k (indices outside [0, n) are ignored).
  * Replaces reference models/Model.py:53-64 (rewind_accumulation: acc[idx] = 0) where the rewind
  * is not fused into dpz_topk_encode (Wavelet with change_based_selection = False).             */

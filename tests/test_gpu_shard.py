@@ -63,3 +63,60 @@ def test_sharded_topk_encode_one_rank_api(dev):
     cnt = torch.zeros(n, dtype=torch.int32, device=dev)
     idx, val = sharded_topk_encode(x, x0, k, 0, counter=cnt)
     assert torch.equal(idx, ref_idx) and torch.equal(val, ref_val) and torch.equal(cnt, cnt_ref)
+
+
+@pytest.mark.parametrize("n,world", [(1_000_003, 2), (1_000_003, 3), (25_000_000, 8),
+                                     (100_000, 5)])
+def test_sharded_wavelet_equals_whole_tensor(dev, n, world):
+    """SURVEY §8e wavelet row: per-rank forward tiles from halo'd slice buffers (the halo being
+    the previous slice's tail) and per-rank inverse tiles, emulated in one process, equal the
+    one-GPU transforms bit-exactly (plain and accumulate)."""
+    from decentralizepy_amd import codec
+    from decentralizepy_amd.shard import (dwt_rank_part, halo_len, idwt_rank_part,
+                                          wavelet_slice)
+    level = 4
+    g = torch.Generator(device=dev).manual_seed(n + world)
+    x = torch.randn(n, device=dev, generator=g)
+    x0 = x - 0.01 * torch.randn(n, device=dev, generator=g)
+    ref_x, ref_d = codec.wavedec(x, level, x0=x0)
+    m = ref_x.numel()
+    acc0 = 0.01 * torch.randn(m, device=dev, generator=g)
+    ref_acc = acc0.clone()
+    codec.wavedec(x, level, x0=x0, want_x=False, coeffs_diff=ref_acc, accumulate=True)
+    cx = torch.full((m,), float("nan"), device=dev)
+    cd = torch.full((m,), float("nan"), device=dev)
+    acc = acc0.clone()
+    H = halo_len(level)
+    rec = torch.full((n,), float("nan"), device=dev)
+    for r in range(world):
+        sl = wavelet_slice(n, level, world, r)
+        first = max(0, sl["lo"] - H) if r > 0 else 0
+        # the rank's buffer: a COPY of its halo + slice (nothing else of x is reachable)
+        xb = x[first:sl["hi"]].clone()
+        x0b = x0[first:sl["hi"]].clone()
+        dwt_rank_part(xb, x0b, first, n, level, sl["t_lo"], sl["t_hi"], cx, cd)
+        dwt_rank_part(xb, x0b, first, n, level, sl["t_lo"], sl["t_hi"], None, acc,
+                      accumulate=True)
+        out = torch.empty(sl["hi"] - sl["lo"], device=dev)
+        if out.numel():
+            idwt_rank_part(ref_x, n, level, sl["u_lo"], sl["u_hi"], out, sl["lo"])
+            rec[sl["lo"]:sl["hi"]] = out
+    torch.cuda.synchronize()
+    assert torch.equal(cx.view(torch.int32), ref_x.view(torch.int32))
+    assert torch.equal(cd.view(torch.int32), ref_d.view(torch.int32))
+    assert torch.equal(acc.view(torch.int32), ref_acc.view(torch.int32))
+    ref_rec = codec.waverec(ref_x, n, level)
+    assert torch.equal(rec.view(torch.int32), ref_rec.view(torch.int32))
+
+
+def test_sharded_wavelet_one_rank_api(dev):
+    from decentralizepy_amd import codec
+    from decentralizepy_amd.shard import sharded_wavedec, sharded_waverec
+    n = 3_000_017
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(n, device=dev, generator=g)
+    x0 = x - 0.01 * torch.randn(n, device=dev, generator=g)
+    ref_x, ref_d = codec.wavedec(x, 4, x0=x0)
+    cx, cd = sharded_wavedec(x, x0, n, 4)
+    assert torch.equal(cx, ref_x) and torch.equal(cd, ref_d)
+    assert torch.equal(sharded_waverec(cx, n, 4), codec.waverec(ref_x, n, 4))
