@@ -78,3 +78,66 @@ def test_sharded_topk_equals_whole_tensor_encode(world, ties):
         np.testing.assert_array_equal(val.view(np.uint32), ov.view(np.uint32))
         full_cnt[lo:lo + cnt.shape[0]] = cnt
     np.testing.assert_array_equal(full_cnt, o_cnt)
+
+
+# ---------------------------------------------------------------------------------------------
+# sharded wavelet: halo exchange + owned-range all-gather over gloo, the per-rank
+# forward tiles emulated with the oracle on a NaN-padded copy of the rank's halo'd buffer (any
+# input a rank's owned coefficients need but it does not hold turns them into NaN)
+
+def _fake_dwt_rank_part(xb, x0b, first, n, level, t_lo, t_hi, cx, cd, accumulate=False):
+    from oracle import wavelet as owav
+    from decentralizepy_amd.shard import owned_coeff_ranges, _level_lengths
+    full = np.full(n, np.nan, dtype=np.float32)
+    full0 = np.full(n, np.nan, dtype=np.float32)
+    full[first:first + xb.numel()] = xb.numpy()
+    full0[first:first + x0b.numel()] = x0b.numpy()
+    wx = owav.wavedec_array(full, level)
+    wd = owav.wavedec_array(full - full0, level)
+    last = t_hi == -(-_level_lengths(n, level)[level] // 128)
+    for s, e in owned_coeff_ranges(n, level, t_lo, t_hi, last):
+        if cx is not None:
+            cx[s:e] = torch.from_numpy(wx[s:e])
+        if cd is not None:
+            cd[s:e] = (cd[s:e] + torch.from_numpy(wd[s:e])) if accumulate else torch.from_numpy(wd[s:e])
+
+
+def _wavelet_worker(rank, world, port, n, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from decentralizepy_amd import shard
+        shard.dwt_rank_part = _fake_dwt_rank_part
+        g = torch.Generator().manual_seed(n)
+        x = torch.randn(n, generator=g)
+        x0 = x - 0.01 * torch.randn(n, generator=g)
+        sl = shard.wavelet_slice(n, 4, world, rank)
+        cx, cd = shard.sharded_wavedec(x[sl["lo"]:sl["hi"]].contiguous(),
+                                       x0[sl["lo"]:sl["hi"]].contiguous(), n, 4)
+        out_q.put((rank, cx.numpy(), cd.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_wavedec_exchange(world):
+    from oracle import wavelet as owav
+    n = 100_003
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29710 + world
+    procs = [ctx.Process(target=_wavelet_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    g = torch.Generator().manual_seed(n)
+    x = torch.randn(n, generator=g)
+    x0 = x - 0.01 * torch.randn(n, generator=g)
+    ref_x = owav.wavedec_array(x.numpy(), 4)
+    ref_d = owav.wavedec_array(x.numpy() - x0.numpy(), 4)
+    for rank, cx, cd in res:
+        np.testing.assert_array_equal(cx.view(np.uint32), ref_x.view(np.uint32))
+        np.testing.assert_array_equal(cd.view(np.uint32), ref_d.view(np.uint32))
