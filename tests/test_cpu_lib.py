@@ -53,6 +53,20 @@ def test_argument_validation_without_gpu():
     assert rc == 1001
     rc = L.dpz_decode_average(None, 10, 0, None, None, None, None, 0.0, 0, None, None, 0, None)
     assert rc == 1001
+    # sharded wavelet tile ranges: out-of-range / inverted tiles are rejected before any launch
+    # (the pointers are never dereferenced: the checks come first)
+    dummy = 4096
+    nt = -(-L.dpz_wavedec_len(100_000, 4) // L.dpz_dwt_tile_width())  # >= the level-4 tiles
+    assert L.dpz_dwt_tile_width() == 128 and L.dpz_idwt_tile_width() == 4096
+    assert L.dpz_dwt_sym2_tiles(dummy, None, 100_000, 4, 5, 3, dummy, None, 0, None) == 1001
+    assert L.dpz_dwt_sym2_tiles(dummy, None, 100_000, 4, 0, nt + 1, dummy, None, 0, None) == 1001
+    assert L.dpz_dwt_sym2_tiles(dummy, None, 100_000, 4, -1, 2, dummy, None, 0, None) == 1001
+    assert L.dpz_dwt_sym2_tiles(dummy, None, 100_000, 5, 0, 1, dummy, None, 0, None) == 1003
+    assert L.dpz_idwt_sym2_tiles(dummy, 100_000, 4, 0, 26, dummy, None) == 1001
+    assert L.dpz_idwt_sym2_tiles(dummy, 100_000, 4, 3, 3, dummy, None) == 0  # empty range
+    # the fold's in-place flag is refused with the replace-only / add-only modes
+    assert L.dpz_decode_average(dummy, 10, 1, None, None, None, None, 0.0, 0x20 | 0x2, dummy,
+                                None, 0, None) == 1001
 
 
 def test_missing_library_fails_loudly(monkeypatch, tmp_path):
