@@ -46,17 +46,10 @@ def parse():
                         "(bench_workloads.py)")
     p.add_argument("--rotate", type=int, default=None,
                    help="independent node states cycled per step (default: enough for > 2x L3)")
-    p.add_argument("--serial", action="store_true",
-                   help="one stream, each decode consumes the same step's payload (dependent "
-                        "encode -> decode) instead of the pipelined step (decode of the previous "
-                        "step's payload co-scheduled inside the encode)")
     p.add_argument("--streams", type=int, default=3,
                    help="S > 1: S independent node codecs share the GPU on S streams (as "
-                        "decentralizepy runs procs_per_machine nodes per machine); 1: one node")
-    p.add_argument("--graph", action="store_true",
-                   help="replay the steps as a captured hipGraph instead of eager launches (on "
-                        "ROCm 7.2 the graph replay measured ~3 us per step slower than eager "
-                        "launches of these >= 6 us kernels, which the host keeps ahead of)")
+                        "decentralizepy runs procs_per_machine nodes per machine); the one-node "
+                        "(one stream) rate is always measured beside it")
     return p.parse_args()
 
 
@@ -76,17 +69,26 @@ def timed_loop(fn, reps, stream):
 L3_BYTES = 256 * 2 ** 20  # MI355X Infinity Cache (MI355X_MICROARCH.md § Infinity Cache)
 
 
-def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True, rotate=None,
-             pipeline=True, streams=1):
+def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, streams=3):
     """Time `steps` encode+decode steps.  Consecutive steps rotate over R independent node states
     (x, x0, counter, payload, output) so the timed working set is > 2x the 256 MiB Infinity
-    Cache: every step streams its inputs from HBM, as a real round does after training."""
+    Cache: every step streams its inputs from HBM, as a real round does after training.
+
+    Step i = node state i's round: top-k encode of its model (change vs x0, counter update) and
+    the replace decode of that payload over x0 (reference PartialModel.serialized_model +
+    deserialized_model).  The host loop over steps is native (dpz_encode_replace_batch, one
+    ctypes call per R steps).  With S streams, S node codecs share the GPU (state i on stream
+    i % S, its own workspace), as decentralizepy runs procs_per_machine nodes per machine; the
+    one-stream (one node) rate is measured beside it and the faster of the two is the line's
+    value.  Every timed encode's sampled-path status is OR-ed into its workspace's sticky word
+    and checked after the loop (fell_back)."""
     from decentralizepy_amd import codec
+    from decentralizepy_amd._lib import DPZ_BATCH_DECODE, DPZ_BATCH_ENCODE
     k = round(alpha * n)
     per_set = 4 * n * 4 + 8 * k          # x, x0, counter, out + payload
     R = rotate or max(1, math.ceil(2 * L3_BYTES / per_set) + 1)
-    if streams > 1:  # a state is only ever reused by the same stream
-        R = -(-R // streams) * streams
+    S = max(1, streams)
+    R = -(-R // S) * S                   # a state is only ever reused by the same stream
     g = torch.Generator(device=dev).manual_seed(seed)
     sets = []
     for _ in range(R):
@@ -96,153 +98,91 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, use_graph=True, ro
                          idx=torch.empty(k, dtype=torch.int32, device=dev),
                          val=torch.empty(k, dtype=torch.float32, device=dev),
                          out=torch.empty(n, dtype=torch.float32, device=dev)))
-    ws = codec.Workspace(dev)
+    s_list = [torch.cuda.Stream(dev) for _ in range(S)]
+    ws_list = [codec.Workspace(dev) for _ in range(S)]
+    multi = codec.NodeStepBatch(sets, n, k, s_list, ws_list)
+    one = codec.NodeStepBatch(sets, n, k, s_list[:1], ws_list[:1])
 
-    def encode(d):
-        codec.topk_encode(d["x"], k, x0=d["x0"], counter=d["counter"], idx_out=d["idx"],
-                          val_out=d["val"], workspace=ws, asynchronous=True)
+    def run_steps(batch, count, what=DPZ_BATCH_ENCODE | DPZ_BATCH_DECODE):
+        for _ in range(count // R):
+            batch.run(what)
+        if count % R:
+            batch.run(what, m=count % R)
 
-    def decode(d):
-        codec.replace(d["x0"], d["idx"], d["val"], out=d["out"], workspace=ws)
-
-    def step(i):
-        d = sets[i % R]
-        encode(d)
-        decode(d)
-
-    # Pipelined step (default): step i encodes node state i and decodes the payload encoded in
-    # step i-1 (node state i-1) — a node's round is exactly this pair of independent operations
-    # (encode its own model, decode a neighbour's payload).  One call (dpz_topk_encode_replace)
-    # runs the decode's chunks in blocks appended to the encoder's latency-bound selection
-    # launches, on one stream.  Every step still does one full encode and one full decode inside
-    # the timed region.  (Two streams instead measured slower on ROCm 7.2: a cross-stream event
-    # wait costs ~15 us, tools/diag/streams_probe.py.)
-    def step_pipe(i):
-        d, p = sets[i % R], sets[(i - 1) % R]
-        codec.topk_encode(d["x"], k, x0=d["x0"], counter=d["counter"], idx_out=d["idx"],
-                          val_out=d["val"], workspace=ws, asynchronous=True,
-                          co_replace=(p["x0"], p["idx"], p["val"], p["out"]))
-
-    for i in range(max(warmup, R)):
-        step(i)
-    fell_back = False
-    for d in sets:  # completes the last async encode of every state (exact re-run on a miss)
-        fell_back |= codec.topk_complete(d["x"], k, d["idx"], d["val"], ws, x0=d["x0"],
-                                         counter=d["counter"])
     torch.cuda.synchronize()
-
-    # Concurrent node codecs (--streams S > 1): step i runs the dependent encode -> decode of
-    # state i on stream i % S with a workspace of its own, so S nodes' codecs share the GPU the
-    # way decentralizepy runs procs_per_machine node processes per machine.  No cross-stream
-    # dependency (state i is reused only S*ceil(R/S) steps later on the same stream).
-    s_list = [torch.cuda.Stream(dev) for _ in range(max(1, streams))]
-    ws_list = [ws] + [codec.Workspace(dev) for _ in range(max(1, streams) - 1)]
-
-    def step_multi(i):
-        q = i % len(s_list)
-        d = sets[i % R]
-        with torch.cuda.stream(s_list[q]):
-            codec.topk_encode(d["x"], k, x0=d["x0"], counter=d["counter"], idx_out=d["idx"],
-                              val_out=d["val"], workspace=ws_list[q], asynchronous=True)
-            codec.replace(d["x0"], d["idx"], d["val"], out=d["out"], workspace=ws_list[q])
-
-    def make_graph(m, fn):
-        # m consecutive steps captured once and replayed (hipGraph), so the timed loop is not
-        # bound by per-kernel host launch cost; every kernel still runs every step
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            for i in range(m):
-                fn(i)
-        return graph
-
-    if use_graph:
-        f = step_pipe if pipeline else step
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            f(0)
-        torch.cuda.current_stream(dev).wait_stream(side)
-        full = make_graph(R, f)
-        tail = make_graph(steps % R, f) if steps % R else None
-        torch.cuda.synchronize()
-
-        def run_all():
-            for _ in range(steps // R):
-                full.replay()
-            if tail is not None:
-                tail.replay()
-    elif streams > 1:
-        for i in range(2 * R):
-            step_multi(i)
-        torch.cuda.synchronize()
-
-        def run_all():
-            for i in range(steps):
-                step_multi(i)
-    elif pipeline:
-        def run_all():
-            for i in range(steps):
-                step_pipe(i)
-    else:
-        def run_all():
-            for i in range(steps):
-                step(i)
-    if dist is not None:
-        dist.barrier()
+    run_steps(multi, max(warmup, 2 * R))
+    run_steps(one, max(warmup, R))
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run_all()
-    t_host = time.perf_counter() - t0  # host enqueue time (host-bound if close to t)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t = time.perf_counter() - t0
-    if dist is not None:
-        tt = torch.tensor([t], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t = float(tt.item())
-    s_step = t / steps
-    # the dependent (encode -> decode of the same payload, one stream) step, for reference
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(steps):
-        step(i)
-    torch.cuda.synchronize()
-    s_serial = (time.perf_counter() - t0) / steps
-    # one node alone on the GPU, pipelined (decode of the previous payload co-scheduled inside
-    # the encode's latency-bound launches), one stream (skipped with --serial, the profiling run)
-    s_cosched = None
-    if pipeline:
+    multi.sticky_status(clear=True)
+
+    def timed(batch, count):
+        if dist is not None:
+            dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for i in range(steps):
-            step_pipe(i)
+        run_steps(batch, count)
+        t_host = time.perf_counter() - t0  # host enqueue time (host-bound if close to t)
         torch.cuda.synchronize()
-        s_cosched = (time.perf_counter() - t0) / steps
-    # per-stage device time with events on the launch stream
-    stream = torch.cuda.current_stream(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter() - t0
+        if dist is not None:
+            tt = torch.tensor([t], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t = float(tt.item())
+        return t / count, t_host / count
+
+    s_multi, h_multi = timed(multi, steps)
+    s_serial, h_serial = timed(one, steps)
+    status = multi.sticky_status(clear=True)  # every timed encode of both loops
+    fell_back = status != 0
+    if dist is not None:
+        st = torch.tensor([status], device=dev, dtype=torch.int32)
+        dist.all_reduce(st, op=dist.ReduceOp.MAX)
+        fell_back = int(st.item()) != 0
+    if S > 1 and s_multi <= s_serial:
+        s_step, s_host, mode = s_multi, h_multi, "multi"
+    else:
+        s_step, s_host, mode = s_serial, h_serial, "serial"
+    # per-stage device time with events on the one launch stream (encodes only, decodes only)
+    stream = s_list[0]
     reps = max(2 * R, steps // 2)
-    cnt = iter(range(10 ** 9))
-    t_enc = timed_loop(lambda: encode(sets[next(cnt) % R]), reps, stream)
-    cnt = iter(range(10 ** 9))
-    t_dec = timed_loop(lambda: decode(sets[next(cnt) % R]), reps, stream)
+
+    t_enc = _stage_time(one, DPZ_BATCH_ENCODE, reps, run_steps, stream)
+    t_dec = _stage_time(one, DPZ_BATCH_DECODE, reps, run_steps, stream)
     # per-kernel device time: the library brackets every launch with a HIP event pair on the
     # stream it launches on.  A GPU-side spin first lets the host queue all `reps` steps, so the
-    # kernels then run back-to-back as in the graph replay (no host-launch gaps inside a pair).
+    # kernels then run back-to-back (no host-launch gaps inside a pair).
     with codec.KernelTimer() as kt:
-        torch.cuda._sleep(int(200e6))  # ~0.1 s of GPU cycles while the steps are enqueued
-        for i in range(reps):
-            step(i)  # kernels alone (no co-scheduled or concurrent work) for the roofline
+        with torch.cuda.stream(stream):
+            torch.cuda._sleep(int(200e6))  # ~0.1 s of GPU cycles while the steps are enqueued
+        run_steps(one, reps)
         torch.cuda.synchronize()
     kernels = {name: {"avg_us": ms / c * 1e3, "launches_per_step": c / reps}
                for name, (ms, c) in kt.result.items()}
     b_enc = 8 * n + 8 * k + 8 * k      # read x, x0; write idx, val; counter[idx] += 1 (r+w)
     b_dec = 8 * n + 8 * k              # read local, payload; write out
-    fell_back |= codec.topk_status(ws) != 0  # the timed steps' last encode
-    return dict(n=n, k=k, s_step=s_step, s_serial=s_serial, s_cosched=s_cosched, s_host=t_host / steps, fell_back=fell_back, t_enc=t_enc, t_dec=t_dec,
+    fell_back |= multi.sticky_status(clear=True) != 0
+    return dict(n=n, k=k, s_step=s_step, s_multi=s_multi, s_serial=s_serial, s_host=s_host,
+                mode=mode, streams=S, fell_back=fell_back, t_enc=t_enc, t_dec=t_dec,
                 b_enc=b_enc, b_dec=b_dec, kernels=kernels, rotate=R,
                 value=world * 4 * n / s_step / 2 ** 30)
+
+
+def _stage_time(batch, what, reps, run_steps, stream):
+    """Average device time of one step's `what` part (encode or decode), back to back on the
+    batch's single stream, HIP events around the loop on that stream."""
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(int(50e6))  # the host queues the loop while the GPU spins
+        ev0.record(stream)
+    run_steps(batch, reps, what)
+    ev1.record(stream)
+    ev1.synchronize()
+    return ev0.elapsed_time(ev1) / reps * 1e-3
 
 
 def gossip_case(n, alpha, dev, rank, world, dist, rounds, warmup):
@@ -393,17 +333,18 @@ def main():
             dist.destroy_process_group()
         return
     r = gpu_case(args.n, args.alpha, dev, 1234 + rank, args.steps, args.warmup, world, dist,
-                 use_graph=args.graph, rotate=args.rotate, pipeline=not args.serial,
-                 streams=args.streams)
+                 rotate=args.rotate, streams=args.streams)
     extra = None
     if not args.no_extra and world == 1:
         e = gpu_case(16_777_216, 0.01, dev, 99, max(20, args.steps // 2), args.warmup, 1, None,
-                     use_graph=args.graph, pipeline=not args.serial, streams=args.streams)
+                     streams=args.streams)
         extra = {"workload": "north-star target: 64 MiB fp32 tensor (N=16,777,216), 1% top-k",
                  "value": round(e["value"], 2), "ms_per_step": round(e["s_step"] * 1e3, 4),
                  "frac_of_hbm_peak": round((e["b_enc"] + e["b_dec"]) / e["s_step"] / 1e9 / HBM_PEAK_GBS, 4),
+                 "launch": e["mode"],
                  "one_node_serial_ms_per_step": round(e["s_serial"] * 1e3, 4),
-                 "one_node_cosched_ms_per_step": (round(e["s_cosched"] * 1e3, 4) if e["s_cosched"] else None),
+                 "one_node_frac_of_hbm_peak": round((e["b_enc"] + e["b_dec"]) / e["s_serial"] / 1e9 / HBM_PEAK_GBS, 4),
+                 f"{e['streams']}_node_ms_per_step": round(e["s_multi"] * 1e3, 4),
                  "host_enqueue_ms_per_step": round(e["s_host"] * 1e3, 4),
                  "fell_back": e["fell_back"]}
 
@@ -459,15 +400,14 @@ def main():
             "config": {
                 "workload": "C2: PartialModel top-k encode + decode of one 11M-fp32 flattened tensor",
                 "n": r["n"], "k": r["k"], "alpha": args.alpha,
-                "parallelism": (f"{world} GPU(s) x {args.streams} concurrent node codecs (one "
-                                f"stream each), no collective" if args.streams > 1 else
+                "parallelism": (f"{world} GPU(s) x {r['streams']} concurrent node codecs (one "
+                                f"stream each), no collective" if r["mode"] == "multi" else
                                 f"{world} GPU(s) x 1 node codec, no collective"),
-                "launch": ("hipGraph replay of the whole step, one stream" if args.graph else
-                           f"eager; step i = dependent encode -> decode of node state i on stream "
-                           f"i % {args.streams}" if args.streams > 1 else
-                           "eager, one stream (encode -> decode of its payload)" if args.serial else
-                           "eager, one stream, pipelined: encode of state i with the decode of "
-                           "state i-1's payload co-scheduled in its selection launches"),
+                "launch": ("native batched enqueue (dpz_encode_replace_batch); step i = encode -> "
+                           f"replace decode of node state i on stream i % {r['streams']}"
+                           if r["mode"] == "multi" else
+                           "native batched enqueue (dpz_encode_replace_batch), one stream; "
+                           "step i = encode -> replace decode of node state i"),
                 "rotated_states": r["rotate"],
             },
             "roofline": {
@@ -490,7 +430,7 @@ def main():
                            "GBps": round(dec_gbs, 1), "frac": round(dec_gbs / HBM_PEAK_GBS, 4)},
                 "step_frac_of_hbm_peak": round(step_gbs / HBM_PEAK_GBS, 4),
                 "one_node_serial_ms_per_step": round(r["s_serial"] * 1e3, 5),
-                "one_node_cosched_ms_per_step": (round(r["s_cosched"] * 1e3, 5) if r["s_cosched"] else None),
+                f"{r['streams']}_node_ms_per_step": round(r["s_multi"] * 1e3, 5),
                 "host_enqueue_ms_per_step": round(r["s_host"] * 1e3, 5),
                 "kernels": kern,
                 "torch_copy_GBps_256MiB": copy_gbs,

@@ -5,6 +5,8 @@ The shared library is built in-tree (``decentralizepy_amd/libdpzcodec.so``, see
 every codec entry point raises.
 """
 import ctypes
+import glob
+import hashlib
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -24,6 +26,8 @@ DPZ_FOLD_ZERO_BASE = 0x4
 DPZ_FOLD_ADD_ONLY = 0x8
 DPZ_FOLD_ACCUMULATE = 0x10
 DPZ_FOLD_ALSO_LOCAL = 0x20
+DPZ_BATCH_ENCODE = 0x1
+DPZ_BATCH_DECODE = 0x2
 DPZ_EW_SUB = 1
 DPZ_EW_ADD = 2
 DPZ_EW_CHOCO = 3
@@ -41,6 +45,7 @@ _size = ctypes.c_size_t
 # name -> (restype, argtypes); must match include/dpz_codec.h
 SIGNATURES = {
     "dpz_abi_version": (_int, []),
+    "dpz_build_id": (ctypes.c_char_p, []),
     "dpz_error_string": (ctypes.c_char_p, [_int]),
     "dpz_topk_workspace_bytes": (_size, [_i64, _i64]),
     "dpz_topk_encode": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64, _i64,
@@ -88,6 +93,12 @@ SIGNATURES = {
     "dpz_decode_average_batch": (_int, [_int, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
                                         _c_void_p, _c_void_p, _c_void_p, _c_void_p, _int,
                                         _c_void_p, _size, _int, _c_void_p]),
+    "dpz_encode_replace_batch": (_int, [_int, _int, _c_void_p, _c_void_p, _i64, _i64, _c_void_p,
+                                        _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                        _i64, _c_void_p, _c_void_p, _size, _c_void_p, _size,
+                                        _int, _c_void_p]),
+    "dpz_topk_sticky_status": (_int, [_c_void_p, _size, _int, ctypes.POINTER(ctypes.c_int32),
+                                      _c_void_p]),
     "dpz_elias_max_bytes": (_i64, [_i64]),
     "dpz_elias_workspace_bytes": (_size, [_i64, _i64]),
     "dpz_elias_encode": (_int, [_c_void_p, _i64, _c_void_p, _i64, ctypes.POINTER(_i64),
@@ -97,6 +108,21 @@ SIGNATURES = {
 }
 
 _lib = None
+
+
+def source_build_id():
+    """The build id the checked-out sources would produce (csrc/Makefile's BUILD_ID: sha256 of
+    csrc/*.cpp, *.h, *.hip in name order, csrc/Makefile, include/dpz_codec.h; 16 hex digits)."""
+    csrc = os.path.join(_HERE, "csrc")
+    files = sorted(os.path.basename(p) for pat in ("*.cpp", "*.h", "*.hip")
+                   for p in glob.glob(os.path.join(csrc, pat)))
+    h = hashlib.sha256()
+    for f in [os.path.join(csrc, f) for f in files] + [
+            os.path.join(csrc, "Makefile"),
+            os.path.join(os.path.dirname(_HERE), "include", "dpz_codec.h")]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def lib():
@@ -113,6 +139,16 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        # a library built from other sources than the checked-out ones is refused (diagnostic
+        # builds selected with DPZ_CODEC_LIB are exempt)
+        if not os.environ.get("DPZ_CODEC_LIB"):
+            built = handle.dpz_build_id().decode()
+            want = source_build_id()
+            if built != want:
+                raise RuntimeError(
+                    f"decentralizepy_amd: {LIB_PATH} was built from other sources (build id "
+                    f"{built}, checked-out sources {want}); rebuild it with "
+                    "`make -C decentralizepy_amd/csrc`")
         _lib = handle
     return _lib
 

@@ -19,7 +19,7 @@ __all__ = ["DPZ_ACC_NONE", "DPZ_ACC_ACCUMULATE", "DPZ_ACC_ADD", "DPZ_EW_SUB", "D
            "topk_threshold", "mask_below_threshold", "elementwise",
            "topk_complete", "decode_average", "replace", "wavedec_len", "wavedec", "waverec",
            "pack_fp16", "unpack_fp16", "elias_encode", "elias_decode",
-           "KernelTimer"]
+           "KernelTimer", "NodeStepBatch", "topk_sticky_status"]
 
 
 def _ptr(t):
@@ -157,6 +157,83 @@ def topk_status(workspace):
     if workspace.buf is None:
         return 0
     return int(workspace.buf[8:12].view(torch.int32).item())
+
+
+def topk_sticky_status(workspace, clear=False):
+    """OR of the final status of every sampled-path encode on ``workspace`` since the last clear
+    (0 = all final).  Synchronises the current stream (dpz_topk_sticky_status)."""
+    if workspace.buf is None:
+        return 0
+    torch.cuda.synchronize(workspace.device)  # encodes may be pending on other streams
+    v = ctypes.c_int32(0)
+    rc = _lib.lib().dpz_topk_sticky_status(_ptr(workspace.buf), workspace.buf.numel(),
+                                           1 if clear else 0, ctypes.byref(v),
+                                           _stream(workspace.device))
+    check(rc, "dpz_topk_sticky_status")
+    return int(v.value)
+
+
+class NodeStepBatch:
+    """A prepared native enqueue of m node codec steps (dpz_encode_replace_batch): node j encodes
+    ``nodes[j]["x"]`` (change vs ``x0``, counter update) into its payload ``idx``/``val`` and
+    replace-decodes ``decode_src(j)``'s payload over ``x0`` into ``out``, on
+    ``streams[j % len(streams)]`` with that stream's workspace.  The pointer arrays are built
+    once; :meth:`run` is one ctypes call whatever m is (the host loop is native)."""
+
+    def __init__(self, nodes, n, k, streams, workspaces, decode_src=None):
+        m = len(nodes)
+        self.m, self.n, self.k = m, int(n), int(k)
+        for d in nodes:
+            for key in ("x", "x0", "out"):
+                _require(d[key], torch.float32, key)
+                if d[key].numel() != n:
+                    raise ValueError(f"node tensor {key} must hold n elements")
+            _require(d["idx"], torch.int32, "idx")
+            _require(d["val"], torch.float32, "val")
+            _require(d.get("counter"), torch.int32, "counter")
+            if d["idx"].numel() != k or d["val"].numel() != k:
+                raise ValueError("payload buffers must hold k entries")
+        src = decode_src or (lambda j: j)
+        P = ctypes.c_void_p * max(m, 1)
+        self._x = P(*[d["x"].data_ptr() for d in nodes])
+        self._x0 = P(*[d["x0"].data_ptr() for d in nodes])
+        self._cnt = P(*[(d["counter"].data_ptr() if d.get("counter") is not None else 0)
+                        for d in nodes])
+        self._idx = P(*[d["idx"].data_ptr() for d in nodes])
+        self._val = P(*[d["val"].data_ptr() for d in nodes])
+        self._rl = P(*[d["x0"].data_ptr() for d in nodes])
+        self._ri = P(*[nodes[src(j)]["idx"].data_ptr() for j in range(m)])
+        self._rv = P(*[nodes[src(j)]["val"].data_ptr() for j in range(m)])
+        self._ro = P(*[d["out"].data_ptr() for d in nodes])
+        S = len(streams)
+        if len(workspaces) != S:
+            raise ValueError("one workspace per stream")
+        wbufs = [w.get(n, k) for w in workspaces]
+        dbufs = [w.get_decode(n, 1) for w in workspaces]
+        Q = ctypes.c_void_p * S
+        self._ws = Q(*[b.data_ptr() for b in wbufs])
+        self._dws = Q(*[b.data_ptr() for b in dbufs])
+        self._ws_bytes = min(b.numel() for b in wbufs)
+        self._dws_bytes = min(b.numel() for b in dbufs)
+        self._streams = Q(*[s.cuda_stream for s in streams])
+        self._S = S
+        self.workspaces = workspaces
+        self._keep = (nodes, wbufs, dbufs, streams)
+
+    def run(self, what=_lib.DPZ_BATCH_ENCODE | _lib.DPZ_BATCH_DECODE, m=None):
+        m = self.m if m is None else int(m)
+        rc = _lib.lib().dpz_encode_replace_batch(
+            m, int(what), self._x, self._x0, self.n, self.k, self._cnt, self._idx, self._val,
+            self._rl, self._ri, self._rv, self.k, self._ro, self._ws, self._ws_bytes, self._dws,
+            self._dws_bytes, self._S, self._streams)
+        check(rc, "dpz_encode_replace_batch")
+
+    def sticky_status(self, clear=False):
+        """OR of every encode's final status on these workspaces since the last clear."""
+        v = 0
+        for w in self.workspaces:
+            v |= topk_sticky_status(w, clear)
+        return v
 
 
 def decode_average(local, payloads, weights=None, w_self=None, out=None, replace_only=False,

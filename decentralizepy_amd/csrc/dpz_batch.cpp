@@ -52,3 +52,40 @@ extern "C" int dpz_decode_average_batch(int m, const float* const* local, float*
   }
   return DPZ_OK;
 }
+
+// One codec step per node: encode node j's model (as dpz_topk_encode_batch) and/or replace-decode
+// the payload (r_idx[j], r_val[j]) into r_out[j] from r_local[j] (dpz_decode_average with
+// DPZ_FOLD_REPLACE_ONLY), node j on streams[j % n_streams].  Host cost: the launches only.
+extern "C" int dpz_encode_replace_batch(int m, int what, const float* const* x,
+                                        const float* const* x0, int64_t n, int64_t k,
+                                        int32_t* const* counter, int32_t* const* idx_out,
+                                        float* const* val_out, const float* const* r_local,
+                                        const int32_t* const* r_idx, const float* const* r_val,
+                                        int64_t r_k, float* const* r_out, void* const* ws,
+                                        size_t ws_bytes, void* const* dws, size_t dws_bytes,
+                                        int n_streams, const dpz_stream_t* streams) {
+  if (m < 0 || n_streams < 1 || !streams || !(what & (DPZ_BATCH_ENCODE | DPZ_BATCH_DECODE)) ||
+      (what & ~(DPZ_BATCH_ENCODE | DPZ_BATCH_DECODE)))
+    return DPZ_ERR_ARG;
+  if ((what & DPZ_BATCH_ENCODE) && (!x || !idx_out || !val_out || !ws)) return DPZ_ERR_ARG;
+  if ((what & DPZ_BATCH_DECODE) && (!r_local || !r_idx || !r_val || !r_out || !dws))
+    return DPZ_ERR_ARG;
+  for (int j = 0; j < m; ++j) {
+    const int q = j % n_streams;
+    if (what & DPZ_BATCH_ENCODE) {
+      int rc = dpz_topk_encode(x[j], x0 ? x0[j] : nullptr, nullptr, DPZ_ACC_NONE, x[j], n, k,
+                               idx_out[j], val_out[j], counter ? counter[j] : nullptr, ws[q],
+                               ws_bytes, DPZ_TOPK_ASYNC, streams[q]);
+      if (rc != DPZ_OK) return rc;
+    }
+    if (what & DPZ_BATCH_DECODE) {
+      const int32_t* ip = r_idx[j];
+      const float* vp = r_val[j];
+      const int64_t kk = r_k;
+      int rc = dpz_decode_average(r_local[j], n, 1, &ip, &vp, &kk, nullptr, 0.0f,
+                                  DPZ_FOLD_REPLACE_ONLY, r_out[j], dws[q], dws_bytes, streams[q]);
+      if (rc != DPZ_OK) return rc;
+    }
+  }
+  return DPZ_OK;
+}

@@ -206,11 +206,7 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
   int ep[FOLD_EQ];
   int32_t ei[FOLD_EQ];
   float evl[FOLD_EQ];
-#if defined(DPZ_FOLD_SKIP) && DPZ_FOLD_SKIP == 1
-  const int32_t etot = 0;  // ablation: no entries (timing only)
-#else
   const int32_t etot = pre[a.np];
-#endif
 #pragma unroll
   for (int q = 0; q < FOLD_EQ; ++q) {
     const int32_t j = t + q * FOLD_THREADS;
@@ -329,11 +325,7 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
     }
     __syncthreads();  // every owner has read its hit flags before B overwrites head[]
     // B) exact fold of the hit elements, one per thread; the result replaces head[pos]
-#if defined(DPZ_FOLD_SKIP) && DPZ_FOLD_SKIP == 3
-    const uint32_t nhit = 0;  // ablation: no exact fold of the hit elements (timing only)
-#else
     const uint32_t nhit = s_nhit;
-#endif
     for (uint32_t s = t; s < nhit; s += FOLD_THREADS) {
       const int pos = hitl[s];
       const float b = a.zero_base ? 0.0f : lv[pos];

@@ -63,7 +63,15 @@ static unsigned grid_for(int64_t n8) {
 
 using namespace dpz;
 
-extern "C" int dpz_abi_version(void) { return 1; }
+extern "C" int dpz_abi_version(void) { return 2; }
+
+// Hash of the sources this library was built from (Makefile: sha256 of csrc/*.{cpp,h,hip}, the
+// Makefile and include/dpz_codec.h, first 16 hex digits); decentralizepy_amd/_lib.py recomputes
+// it from the checked-out tree so a stale binary fails loudly instead of being tested.
+#ifndef DPZ_BUILD_ID
+#define DPZ_BUILD_ID "unknown"
+#endif
+extern "C" const char* dpz_build_id(void) { return DPZ_BUILD_ID; }
 
 extern "C" const char* dpz_error_string(int code) {
   switch (code) {

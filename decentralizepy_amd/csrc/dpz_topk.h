@@ -114,7 +114,9 @@ struct TopkCtrl {
   uint32_t lo, hi, shift;  // sampled path key window and fine-bin shift
   uint32_t bstar, need;    // threshold bin, entries to take from it
   uint32_t T, icut;        // final threshold key / last selected index among key == T
-  uint32_t pad[53];
+  uint32_t sticky;         // OR of every sampled call's final status since the caller cleared it
+                           // (dpz_topk_sticky_status): misses of ASYNC calls never completed
+  uint32_t pad[52];
 };
 static_assert(sizeof(TopkCtrl) == 256, "ctrl size");
 

@@ -206,3 +206,19 @@ extern "C" int dpz_topk_complete(const float* x, const float* x0, float* acc, in
   DPZ_HIP_TRY(hipStreamSynchronize(a.st));
   return DPZ_OK;
 }
+
+extern "C" int dpz_topk_sticky_status(void* ws, size_t ws_bytes, int clear, int32_t* out,
+                                      dpz_stream_t stream) {
+  if (!ws || ws_bytes < sizeof(TopkCtrl)) return DPZ_ERR_ARG;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  char* p = static_cast<char*>(ws) + offsetof(TopkCtrl, sticky);
+  uint32_t v = 0;
+  DPZ_HIP_TRY(hipMemcpyAsync(&v, p, sizeof(v), hipMemcpyDeviceToHost, st));
+  DPZ_HIP_TRY(hipStreamSynchronize(st));
+  if (clear && v) {
+    DPZ_HIP_TRY(hipMemsetAsync(p, 0, sizeof(uint32_t), st));
+    DPZ_HIP_TRY(hipStreamSynchronize(st));
+  }
+  if (out) *out = (int32_t)v;
+  return DPZ_OK;
+}

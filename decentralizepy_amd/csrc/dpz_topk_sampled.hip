@@ -876,7 +876,10 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   if (blockIdx.x == 0) {  // leave the sample histogram zeroed for the next call
     for (int b = t; b < CB; b += 256) chist[b] = 0;
   }
-  if (status) return;  // select reported a miss: the host runs the exact path
+  if (status) {  // select reported a miss: the host runs the exact path
+    if (blockIdx.x == 0 && t == 0) atomicOr(&ctrl->sticky, status);
+    return;
+  }
   if (t < 64) {
     uint32_t tot;
     const uint32_t ex = wave_excl_scan(sc, &tot);
@@ -889,7 +892,10 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   }
   __syncthreads();
   if (flag) {  // identical in every block
-    if (blockIdx.x == 0 && t == 0) ctrl->status = 1;
+    if (blockIdx.x == 0 && t == 0) {
+      ctrl->status = 1;
+      atomicOr(&ctrl->sticky, 1u);
+    }
     return;
   }
   STAMP_T0(1);
@@ -912,7 +918,10 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   if (blockIdx.x == 0 && t == 0) {
     ctrl->T = T;
     ctrl->icut = icut;
-    if (grand != (uint32_t)k) ctrl->status = 2;  // internal inconsistency
+    if (grand != (uint32_t)k) {  // internal inconsistency
+      ctrl->status = 2;
+      atomicOr(&ctrl->sticky, 2u);
+    }
   }
   if (grand != (uint32_t)k) return;  // identical in every block: nothing is written
   // chunks 1 .. PFC-1 of every segment with more than 64 candidates: all issued together

@@ -71,6 +71,10 @@ typedef void* dpz_stream_t; /* hipStream_t */
                                      Not with REPLACE_ONLY / ADD_ONLY.                       */
 
 int dpz_abi_version(void);
+/* First 16 hex digits of the SHA-256 of the sources the library was built from (csrc/ *.cpp, *.h,
+ * *.hip in name order, then csrc/Makefile, then this header): the Python binding compares it
+ * with the checked-out tree and refuses a stale binary.                                        */
+const char* dpz_build_id(void);
 const char* dpz_error_string(int code);
 
 /* Top-k magnitude encode.
@@ -187,6 +191,31 @@ int dpz_decode_average_batch(int m, const float* const* local, float* const* out
                              const float* const* vals, const int64_t* k, const float* w,
                              const float* w_self, int flags, void* const* ws, size_t ws_bytes,
                              int n_streams, const dpz_stream_t* streams);
+
+/* One codec step per node for m nodes of equal size (n, k): with DPZ_BATCH_ENCODE, node j's
+ * dpz_topk_encode(x[j], x0[j], NULL, DPZ_ACC_NONE, x[j], n, k, idx_out[j], val_out[j],
+ * counter[j], ws[q], ws_bytes, DPZ_TOPK_ASYNC, streams[q]); with DPZ_BATCH_DECODE, then the replace
+ * decode dpz_decode_average(r_local[j], n, 1, &r_idx[j], &r_val[j], &r_k, NULL, 0,
+ * DPZ_FOLD_REPLACE_ONLY, r_out[j], dws[q], dws_bytes, streams[q]); q = j % n_streams.  Arrays are
+ * HOST arrays of device pointers.  A node's round (reference sharing/PartialModel.py:188-303:
+ * serialized_model of its own model, deserialized_model of a received payload) with the host
+ * loop in native code.  The encodes are asynchronous: a sampled-path miss is recorded in the
+ * workspace's sticky status word (dpz_topk_sticky_status), never silently.                     */
+#define DPZ_BATCH_ENCODE 0x1
+#define DPZ_BATCH_DECODE 0x2
+int dpz_encode_replace_batch(int m, int what, const float* const* x, const float* const* x0,
+                             int64_t n, int64_t k, int32_t* const* counter,
+                             int32_t* const* idx_out, float* const* val_out,
+                             const float* const* r_local, const int32_t* const* r_idx,
+                             const float* const* r_val, int64_t r_k, float* const* r_out,
+                             void* const* ws, size_t ws_bytes, void* const* dws, size_t dws_bytes,
+                             int n_streams, const dpz_stream_t* streams);
+/* OR of the final status of every sampled-path encode run on this top-k workspace since the
+ * last clear (0 = every one was final; nonzero = at least one missed and, if it was ASYNC and
+ * not completed by dpz_topk_complete, published unverified output).  Synchronises `stream`;
+ * clear != 0 resets the word afterwards.  *out is a HOST pointer.                              */
+int dpz_topk_sticky_status(void* ws, size_t ws_bytes, int clear, int32_t* out,
+                           dpz_stream_t stream);
 
 /* Multilevel sym2 DWT, mode "symmetric", fp32, pywt-1.1.1-exact summation order.
  * Replaces reference sharing/JWINS/Wavelet.py:12-32 (pywt.wavedec + coeffs_to_array).

@@ -30,10 +30,36 @@ def test_library_exports_every_declared_symbol():
     assert set(_lib.SIGNATURES) == declared
 
 
+def test_build_id_matches_checked_out_sources():
+    """The loaded library was built from exactly these sources (a stale .so is refused)."""
+    from decentralizepy_amd import _lib
+    L = _lib.lib()
+    assert L.dpz_build_id().decode() == _lib.source_build_id()
+
+
+def test_batch_entry_validates_arguments():
+    from decentralizepy_amd import _lib
+    L = _lib.lib()
+    st = (ctypes.c_void_p * 1)(None)
+    # no operation bit / unknown bits / zero streams
+    assert L.dpz_encode_replace_batch(1, 0, None, None, 10, 1, None, None, None, None, None,
+                                      None, 1, None, None, 0, None, 0, 1, st) == 1001
+    assert L.dpz_encode_replace_batch(1, 4, None, None, 10, 1, None, None, None, None, None,
+                                      None, 1, None, None, 0, None, 0, 1, st) == 1001
+    assert L.dpz_encode_replace_batch(1, 1, None, None, 10, 1, None, None, None, None, None,
+                                      None, 1, None, None, 0, None, 0, 0, st) == 1001
+    # encode without buffers / decode without buffers
+    assert L.dpz_encode_replace_batch(1, 1, None, None, 10, 1, None, None, None, None, None,
+                                      None, 1, None, None, 0, None, 0, 1, st) == 1001
+    assert L.dpz_encode_replace_batch(1, 2, None, None, 10, 1, None, None, None, None, None,
+                                      None, 1, None, None, 0, None, 0, 1, st) == 1001
+    assert L.dpz_topk_sticky_status(None, 0, 0, None, None) == 1001
+
+
 def test_host_only_entry_points():
     from decentralizepy_amd import _lib
     L = _lib.lib()
-    assert L.dpz_abi_version() == 1
+    assert L.dpz_abi_version() == 2
     assert L.dpz_error_string(1001) == b"invalid argument"
     assert L.dpz_topk_workspace_bytes(11_000_000, 110_000) > 0
     # wavedec length = pywt coeffs_to_array length (sym2, level 4)

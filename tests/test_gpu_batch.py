@@ -1,0 +1,105 @@
+"""GPU tests of the native per-node step enqueue (dpz_encode_replace_batch) and the sticky status
+word that makes an asynchronous encode's sampled-path miss visible (bench.py's timed region)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import fold as ofold
+from oracle import topk as otopk
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def _node(dev, n, k, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, generator=g)
+    x0 = x - 0.01 * torch.randn(n, generator=g)
+    return dict(x=x.to(dev), x0=x0.to(dev), counter=torch.zeros(n, dtype=torch.int32, device=dev),
+                idx=torch.empty(k, dtype=torch.int32, device=dev),
+                val=torch.empty(k, dtype=torch.float32, device=dev),
+                out=torch.empty(n, dtype=torch.float32, device=dev))
+
+
+@pytest.mark.parametrize("streams", [1, 2, 3])
+def test_node_step_batch_matches_oracle(dev, streams):
+    from decentralizepy_amd import codec
+    n, k, m = 1_000_003, 10_000, 5
+    nodes = [_node(dev, n, k, 40 + j) for j in range(m)]
+    ss = [torch.cuda.Stream(dev) for _ in range(streams)]
+    ws = [codec.Workspace(dev) for _ in range(streams)]
+    # node j decodes node (j+1) % m's payload: independent of its own encode only across nodes
+    # handled earlier on the same stream, so decode the node's own payload (the bench's step)
+    b = codec.NodeStepBatch(nodes, n, k, ss, ws)
+    b.sticky_status(clear=True)
+    for _ in range(2):  # twice: counters accumulate, workspaces are reused
+        b.run()
+    torch.cuda.synchronize()
+    assert b.sticky_status() == 0
+    for j, d in enumerate(nodes):
+        x = d["x"].cpu().numpy()
+        x0 = d["x0"].cpu().numpy()
+        cnt = np.zeros(n, dtype=np.int32)
+        oi, ov = otopk.encode(x, x0, None, 0, k, counter=cnt)
+        otopk.encode(x, x0, None, 0, k, counter=cnt)
+        np.testing.assert_array_equal(d["idx"].cpu().numpy(), oi)
+        np.testing.assert_array_equal(_bits(d["val"].cpu().numpy()), _bits(ov))
+        np.testing.assert_array_equal(d["counter"].cpu().numpy(), cnt)
+        ref = ofold.replace(x0, oi, ov)
+        np.testing.assert_array_equal(_bits(d["out"].cpu().numpy()), _bits(ref))
+
+
+def test_node_step_batch_encode_only_and_decode_only(dev):
+    from decentralizepy_amd import codec
+    from decentralizepy_amd._lib import DPZ_BATCH_DECODE, DPZ_BATCH_ENCODE
+    n, k = 600_001, 6000
+    nodes = [_node(dev, n, k, 7), _node(dev, n, k, 8)]
+    s = [torch.cuda.Stream(dev)]
+    b = codec.NodeStepBatch(nodes, n, k, s, [codec.Workspace(dev)])
+    for d in nodes:
+        d["out"].fill_(7.0)
+    torch.cuda.synchronize()
+    b.run(DPZ_BATCH_ENCODE)
+    torch.cuda.synchronize()
+    assert all(float(d["out"][0]) == 7.0 for d in nodes), "encode-only must not decode"
+    b.run(DPZ_BATCH_DECODE, m=1)  # first node only
+    torch.cuda.synchronize()
+    assert float(nodes[1]["out"][0]) == 7.0
+    x = nodes[0]["x"].cpu().numpy()
+    x0 = nodes[0]["x0"].cpu().numpy()
+    oi, ov = otopk.encode(x, x0, None, 0, k)
+    np.testing.assert_array_equal(_bits(nodes[0]["out"].cpu().numpy()),
+                                  _bits(ofold.replace(x0, oi, ov)))
+
+
+def test_sticky_status_records_an_uncompleted_miss(dev):
+    """An ASYNC encode whose sampled window misses (adversarial layout, as in
+    test_gpu_codec.test_topk_sampled_miss_falls_back) is never completed: the sticky word must
+    say so, and a clear must reset it."""
+    from decentralizepy_amd import codec
+    n = 1 << 20
+    k = round(0.01 * n)
+    x = np.zeros(n, dtype=np.float32)
+    rng = np.random.default_rng(11)
+    big = []
+    for c in range(1023):
+        s = (c * (n - 64)) // 1023 + 64
+        e = ((c + 1) * (n - 64)) // 1023
+        big.extend(range(s + 100, min(e - 100, s + 100 + 12)))
+    big = np.array(big)
+    x[:] = 1e-6 * rng.standard_normal(n).astype(np.float32)
+    x[big] = rng.uniform(1.0, 2.0, big.shape[0]).astype(np.float32)
+    tx = torch.from_numpy(x).to(dev)
+    tx0 = torch.zeros(n, device=dev)
+    ws = codec.Workspace(dev)
+    good = _node(dev, n, k, 3)
+    codec.topk_encode(good["x"], k, x0=good["x0"], workspace=ws)  # a normal call first
+    assert codec.topk_sticky_status(ws, clear=True) == 0
+    codec.topk_encode(tx, k, x0=tx0, workspace=ws, asynchronous=True)
+    codec.topk_encode(good["x"], k, x0=good["x0"], workspace=ws, asynchronous=True)
+    assert codec.topk_sticky_status(ws) != 0, "the missed async encode must stay recorded"
+    assert codec.topk_sticky_status(ws, clear=True) != 0
+    assert codec.topk_sticky_status(ws) == 0

@@ -1,5 +1,5 @@
 """Diagnostic: per-kernel device time of the sampled top-k encode on HBM-rotated inputs.
-Pick the library build with DPZ_CODEC_LIB (e.g. the ablation builds of `make ablate`)."""
+Pick the library build with DPZ_CODEC_LIB."""
 import sys
 
 import torch

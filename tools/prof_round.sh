@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-CMD="python3 bench.py --steps ${STEPS:-100} --warmup 10 --no-cpu --no-extra --streams 1 --serial"
+CMD="python3 bench.py --steps ${STEPS:-100} --warmup 10 --no-cpu --no-extra --streams 1"
 rm -rf gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- $CMD > gpurun_out/prof.log 2>&1 || { echo "trace rc=$?"; tail -5 gpurun_out/prof.log; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- $CMD > gpurun_out/pmc_fetch.log 2>&1 || { echo "fetch rc=$?"; tail -5 gpurun_out/pmc_fetch.log; exit 1; }
