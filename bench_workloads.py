@@ -218,7 +218,7 @@ def shard_case(dev, rank, world, dist, n=67_108_864, alpha=0.001, steps=20, warm
     each rank decodes the global payload into its own slice (replace; indices outside the slice
     fall outside [0, n_r) and are skipped).  Strong scaling: N fixed, value = N params / time."""
     from decentralizepy_amd import codec
-    from decentralizepy_amd.shard import HipShardOps, sharded_topk_encode
+    from decentralizepy_amd.shard import HipShardOps, sharded_replace, sharded_topk_encode
     k = round(alpha * n)
     lo = n * rank // world
     hi = n * (rank + 1) // world
@@ -237,7 +237,7 @@ def shard_case(dev, rank, world, dist, n=67_108_864, alpha=0.001, steps=20, warm
     def step(i):
         d = sets[i % R]
         idx, val = sharded_topk_encode(d["x"], d["x0"], k, lo, counter=d["cnt"], ops=ops)
-        codec.replace(d["x0"], idx - lo, val, out=d["out"], workspace=ws)
+        sharded_replace(d["x0"], lo, idx, val, out=d["out"], ops=ops)
 
     for i in range(warmup):
         step(i)

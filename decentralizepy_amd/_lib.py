@@ -87,6 +87,8 @@ SIGNATURES = {
     "dpz_timing_enable": (_int, [_int]),
     "dpz_timing_read": (_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64), _int]),
     "dpz_kernel_name": (ctypes.c_char_p, [_int]),
+    "dpz_replace_slice": (_int, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _i64, _c_void_p,
+                                 _c_void_p]),
     "dpz_topk_encode_batch": (_int, [_int, _c_void_p, _c_void_p, _i64, _i64, _c_void_p,
                                      _c_void_p, _c_void_p, _c_void_p, _size, _int, _c_void_p,
                                      _c_void_p]),

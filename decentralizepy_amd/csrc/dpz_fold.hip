@@ -633,3 +633,18 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
   }
   return DPZ_OK;
 }
+
+extern "C" int dpz_replace_slice(const float* local, int64_t n, int64_t offset,
+                                 const int32_t* idx, const float* vals, int64_t k, float* out,
+                                 dpz_stream_t stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (n < 0 || k < 0 || offset < 0) return DPZ_ERR_ARG;
+  if (n == 0) return DPZ_OK;
+  if (!local || !out || local == out || (k > 0 && (!idx || !vals))) return DPZ_ERR_ARG;
+  if (!aligned16(local) || !aligned16(out)) return DPZ_ERR_ARG;
+  if (k == 0) {
+    DPZ_HIP_TRY(hipMemcpyAsync(out, local, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, st));
+    return DPZ_OK;
+  }
+  return launch_replace(ReplaceJob{local, idx, vals, k, n, out, 0, replace_chunks(k), 0, offset}, st);
+}

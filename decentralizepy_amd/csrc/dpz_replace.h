@@ -39,6 +39,8 @@ struct ReplaceJob {
   float* out;
   int64_t c0, c1;  // chunks [c0, c1) of this launch
   int add;         // 0: out = local with entries replaced; 1: out = local + T (T zero-based)
+  int64_t off;     // payload indices are global; element i of local / out is global off + i
+                   // (a rank's slice of a sharded model; entries outside [0, n) are skipped)
 };
 
 static inline int64_t replace_chunks(int64_t k) { return (k + RP_E - 1) / RP_E; }
@@ -54,13 +56,13 @@ __device__ __forceinline__ void replace_chunk(const ReplaceJob& j, int64_t c, bo
     const int64_t k = j.k, n = j.n;
     const int64_t e0 = c * RP_E;
     const int64_t e1 = (e0 + RP_E < k) ? e0 + RP_E : k;
-    int64_t a = c == 0 ? 0 : (int64_t)j.idx[e0];
-    int64_t b = e1 >= k ? n : (int64_t)j.idx[e1];
+    int64_t a = c == 0 ? 0 : (int64_t)j.idx[e0] - j.off;
+    int64_t b = e1 >= k ? n : (int64_t)j.idx[e1] - j.off;
     // an invalid payload (indices outside [0, n)) must not fault: clamp the range
     a = a < 0 ? 0 : (a > n ? n : a);
     b = b < 0 ? 0 : (b > n ? n : b);
     if (t < e1 - e0) {
-      my_i = j.idx[e0 + t];
+      my_i = (int64_t)j.idx[e0 + t] - j.off;
       my_v = j.val[e0 + t];
     }
     if (a < b) {

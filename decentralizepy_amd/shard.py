@@ -77,6 +77,12 @@ class HipShardOps:
     def count(self, counter, idx, offset):
         _scatter_add(counter, idx, offset)
 
+    def replace_slice(self, local_slice, offset, idx, vals, out):
+        rc = _lib.lib().dpz_replace_slice(_ptr(local_slice), local_slice.numel(), int(offset),
+                                          _ptr(idx), _ptr(vals), idx.numel(), _ptr(out),
+                                          _stream(local_slice.device))
+        _lib.check(rc, "dpz_replace_slice")
+
 
 def sharded_topk_encode(x, x0, k, offset, counter=None, group=None, ops=None):
     """Global top-k of a tensor sharded over the ranks of `group`.
@@ -141,32 +147,49 @@ def _level_lengths(n, level):
 
 
 def wavelet_slice(n, level, world, rank, dwt_tile=128, idwt_tile=4096):
-    """Rank `rank`'s model slice [lo, hi) and its forward / inverse tile ranges."""
+    """Rank `rank`'s model slice [lo, hi) and its forward / inverse tile ranges.
+
+    The forward tiles past the last whole span (the model's tail) belong to the rank whose slice
+    holds element n - 1; a rank with an empty slice (more ranks than inverse tiles) owns no tile
+    of either kind."""
     span = (1 << level) * dwt_tile
     if idwt_tile % span:
-        raise ValueError("level too deep for the shared tiling (needs 2^level * 128 | 4096)")
+        raise ValueError("level too deep for the shared tiling (needs 2^level * dwt_tile | "
+                         "idwt_tile)")
     lens = _level_lengths(n, level)
     n_fwd = -(-lens[level] // dwt_tile)
     n_inv = -(-n // idwt_tile)
     per = -(-n_inv // world)
     u_lo, u_hi = min(rank * per, n_inv), min((rank + 1) * per, n_inv)
     lo, hi = min(u_lo * idwt_tile, n), min(u_hi * idwt_tile, n)
+    if lo >= hi:  # empty slice
+        return dict(lo=lo, hi=lo, t_lo=n_fwd, t_hi=n_fwd, u_lo=u_hi, u_hi=u_hi)
     t_lo = min(lo // span, n_fwd)
-    t_hi = n_fwd if rank == world - 1 else min(hi // span, n_fwd)
+    t_hi = n_fwd if hi == n else min(hi // span, n_fwd)
     return dict(lo=lo, hi=hi, t_lo=t_lo, t_hi=t_hi, u_lo=u_lo, u_hi=u_hi)
 
 
-def owned_coeff_ranges(n, level, t_lo, t_hi, last, dwt_tile=128):
-    """[start, end) ranges of the coefficient array written by forward tiles [t_lo, t_hi)."""
+def owned_coeff_ranges(n, level, t_lo, t_hi, dwt_tile=128):
+    """[start, end) ranges of the coefficient array written by forward tiles [t_lo, t_hi) (the
+    last tile, t_hi == the tile count, also owns each detail level's tail)."""
     lens = _level_lengths(n, level)
-    out = [(t_lo * dwt_tile, min(t_hi * dwt_tile, lens[level]))]  # cA_L
+    n_fwd = -(-lens[level] // dwt_tile)
+    last = t_hi == n_fwd and t_lo < t_hi
+    out = [(min(t_lo * dwt_tile, lens[level]), min(t_hi * dwt_tile, lens[level]))]  # cA_L
     off = lens[level]
     for lv in range(level, 0, -1):
-        s = t_lo * dwt_tile << (level - lv)
+        s = min(t_lo * dwt_tile << (level - lv), lens[lv])
         e = lens[lv] if last else min(t_hi * dwt_tile << (level - lv), lens[lv])
-        out.append((off + min(s, lens[lv]), off + e))
+        out.append((off + s, off + max(s, e)))
         off += lens[lv]
     return out
+
+
+def tile_widths():
+    """(forward, inverse) tile widths of the built kernels (dpz_dwt_tile_width /
+    dpz_idwt_tile_width): every slice and owned-range computation uses these."""
+    L = _lib.lib()
+    return int(L.dpz_dwt_tile_width()), int(L.dpz_idwt_tile_width())
 
 
 def halo_len(level):
@@ -192,13 +215,15 @@ def dwt_rank_part(xbuf, x0buf, buf_first, n, level, t_lo, t_hi, cx, cd, accumula
     _lib.check(rc, "dpz_dwt_sym2_tiles")
 
 
-def _exchange_owned(arrs, n, level, world, rank, group, dist):
+def _exchange_owned(arrs, n, level, world, rank, group, dist, widths):
     """All-gather every rank's owned coefficient ranges of each array in `arrs` (in place)."""
-    parts = [owned_coeff_ranges(n, level, **{k: wavelet_slice(n, level, world, r)[k]
-                                             for k in ("t_lo", "t_hi")}, last=(r == world - 1))
-             for r in range(world)]
+    dw, iw = widths
+    parts = []
+    for r in range(world):
+        sl = wavelet_slice(n, level, world, r, dw, iw)
+        parts.append(owned_coeff_ranges(n, level, sl["t_lo"], sl["t_hi"], dw))
     sizes = [sum(e - s for s, e in p) for p in parts]
-    cap = max(sizes)
+    cap = max(1, max(sizes))
     dev = arrs[0].device
     send = torch.zeros(len(arrs) * cap, dtype=torch.float32, device=dev)
     o = 0
@@ -219,44 +244,93 @@ def _exchange_owned(arrs, n, level, world, rank, group, dist):
             o += e - s
 
 
+# the per-rank transforms (dwt_rank_part) are module attributes so the CPU exchange tests can
+# replace them with the oracle; those tests also lift the device requirement below
+_DEVICE_ONLY = True
+
+
+def _check_f32(t, name, numel=None, device=None):
+    if _DEVICE_ONLY if device is None else device:
+        codec._require(t, torch.float32, name)
+    elif t.dtype != torch.float32 or not t.is_contiguous():
+        raise ValueError(f"{name} must be a contiguous float32 tensor")
+    if numel is not None and t.numel() != numel:
+        raise ValueError(f"{name} must hold {numel} elements, got {t.numel()}")
+
+
+def _halo_buffer(t, H):
+    """A (buffer, first-offset) pair holding H elements before `t`'s first element and then `t`:
+    `t` itself viewed with its headroom when it came from alloc_wavelet_slice (no copy; only
+    that buffer's reserved headroom is ever written), otherwise a fresh copy."""
+    so = t.storage_offset()
+    if getattr(t, "_dpz_halo", 0) >= H and so >= H:
+        buf = torch.empty(0, dtype=t.dtype, device=t.device)
+        buf.set_(t.untyped_storage(), so - H, (H + t.numel(),), (1,))
+        return buf, False
+    return torch.cat([torch.empty(H, dtype=t.dtype, device=t.device), t]), True
+
+
+def alloc_wavelet_slice(n, level, world, rank, device):
+    """This rank's x (or x0) slice buffer for sharded_wavedec: a view of a buffer with room for
+    the left halo in front, so the halo exchange writes halo_len(level) elements, not a copy of
+    the whole slice."""
+    dw, iw = tile_widths()
+    sl = wavelet_slice(n, level, world, rank, dw, iw)
+    H = halo_len(level)
+    base = torch.empty(H + sl["hi"] - sl["lo"], dtype=torch.float32, device=device)
+    view = base[H:]
+    view._dpz_halo = H  # the H elements in front are this buffer's own, free for the halo
+    return view
+
+
 def sharded_wavedec(x_slice, x0_slice, n, level, group=None, accumulate_into=None):
     """W(x) and W(x - x0) of a tensor sharded over the ranks of `group` (rank r holds its
     wavelet_slice [lo, hi) of x and x0).  Returns the whole coefficient arrays on every rank
-    (W(x), W(x - x0) — or, with ``accumulate_into``, that array += W(x - x0) and W(x))."""
+    (W(x), W(x - x0) — or, with ``accumulate_into``, that array += W(x - x0) and W(x)).
+    Slices from alloc_wavelet_slice get their halo written in place (no slice copy)."""
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    sl = wavelet_slice(n, level, world, rank, int(_lib.lib().dpz_dwt_tile_width()),
-                       int(_lib.lib().dpz_idwt_tile_width()))
-    if x_slice.numel() != sl["hi"] - sl["lo"]:
-        raise ValueError("x_slice must be this rank's wavelet_slice of the tensor")
+    widths = tile_widths()
+    sl = wavelet_slice(n, level, world, rank, *widths)
+    # every check happens before the first collective, so every rank fails the same way
+    m_len = codec.wavedec_len(n, level)
+    _check_f32(x_slice, "x_slice", sl["hi"] - sl["lo"])
+    _check_f32(x0_slice, "x0_slice", sl["hi"] - sl["lo"])
+    if accumulate_into is not None:
+        _check_f32(accumulate_into, "accumulate_into", m_len)
     H = halo_len(level)
-    for r in range(world - 1):
-        s = wavelet_slice(n, level, world, r)
-        if s["hi"] - s["lo"] < H:
-            raise ValueError("tensor too small for this many ranks (a slice is shorter than the halo)")
+    for r in range(world):
+        s = wavelet_slice(n, level, world, r, *widths)
+        if 0 < s["hi"] - s["lo"] < H:
+            raise ValueError("tensor too small for this many ranks (a slice is shorter than the "
+                             "halo)")
     dev = x_slice.device
     xb, x0b, first = x_slice, x0_slice, sl["lo"]
     if world > 1:
-        # the left halo: the last H elements of rank r - 1's slice (x and x0), one all-gather
+        # the left halo: the last H elements of the previous non-empty slice (x and x0), one
+        # all-gather; an empty slice sends nothing useful and receives nothing
         tail = torch.zeros(2 * H, dtype=torch.float32, device=dev)
         m = min(H, x_slice.numel())
-        tail[H - m:H] = x_slice[x_slice.numel() - m:]
-        tail[2 * H - m:] = x0_slice[x0_slice.numel() - m:]
+        if m:
+            tail[H - m:H] = x_slice[x_slice.numel() - m:]
+            tail[2 * H - m:] = x0_slice[x0_slice.numel() - m:]
         tails = torch.empty(world * 2 * H, dtype=torch.float32, device=dev)
         dist.all_gather_into_tensor(tails, tail, group=group)
-        if rank > 0:
+        if rank > 0 and sl["lo"] < sl["hi"]:
             prev = tails.view(world, 2 * H)[rank - 1]
-            xb = torch.cat([prev[:H], x_slice])
-            x0b = torch.cat([prev[H:], x0_slice])
+            xb, _ = _halo_buffer(x_slice, H)
+            x0b, _ = _halo_buffer(x0_slice, H)
+            xb[:H] = prev[:H]
+            x0b[:H] = prev[H:]
             first = sl["lo"] - H
-    m_len = codec.wavedec_len(n, level)
     cx = torch.zeros(m_len, dtype=torch.float32, device=dev)
     cd = accumulate_into if accumulate_into is not None else torch.zeros_like(cx)
-    dwt_rank_part(xb, x0b, first, n, level, sl["t_lo"], sl["t_hi"], cx, cd,
-                  accumulate=accumulate_into is not None)
+    if sl["t_lo"] < sl["t_hi"]:
+        dwt_rank_part(xb, x0b, first, n, level, sl["t_lo"], sl["t_hi"], cx, cd,
+                      accumulate=accumulate_into is not None)
     if world > 1:
-        _exchange_owned([cx, cd], n, level, world, rank, group, dist)
+        _exchange_owned([cx, cd], n, level, world, rank, group, dist, widths)
     return cx, cd
 
 
@@ -272,9 +346,35 @@ def sharded_waverec(coeffs, n, level, group=None):
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    sl = wavelet_slice(n, level, world, rank, int(_lib.lib().dpz_dwt_tile_width()),
-                       int(_lib.lib().dpz_idwt_tile_width()))
+    _check_f32(coeffs, "coeffs", codec.wavedec_len(n, level))
+    sl = wavelet_slice(n, level, world, rank, *tile_widths())
     out = torch.empty(sl["hi"] - sl["lo"], dtype=torch.float32, device=coeffs.device)
     if out.numel():
         idwt_rank_part(coeffs, n, level, sl["u_lo"], sl["u_hi"], out, sl["lo"])
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# One tensor's decode over ranks (SURVEY.md §8e "one tensor, decode: yes, no collective"): the
+# payload's indices are global and sorted; each rank replaces the entries that fall inside its
+# slice [offset, offset + n) and skips the rest, in one launch (dpz_replace_slice).
+
+def sharded_replace(local_slice, offset, idx, vals, out=None, ops=None):
+    """``T = local.clone(); T[idx] = vals`` (reference PartialModel.py:292-295) restricted to this
+    rank's slice: local_slice holds global elements [offset, offset + len); idx / vals is the
+    WHOLE payload (global ascending indices, e.g. from sharded_topk_encode).  No collective."""
+    ops = ops or HipShardOps(local_slice.device)
+    hip = isinstance(ops, HipShardOps)  # the device kernel needs device tensors
+    _check_f32(local_slice, "local_slice", device=hip)
+    if hip:
+        codec._require(idx, torch.int32, "idx")
+    if idx.dtype != torch.int32 or idx.dim() != 1:
+        raise ValueError("idx must be a 1-D int32 tensor")
+    _check_f32(vals, "vals", idx.numel(), device=hip)
+    if out is None:
+        out = torch.empty_like(local_slice)
+    _check_f32(out, "out", local_slice.numel(), device=hip)
+    if int(offset) < 0:
+        raise ValueError("offset must be >= 0")
+    ops.replace_slice(local_slice, int(offset), idx, vals, out)
     return out

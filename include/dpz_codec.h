@@ -171,6 +171,15 @@ int dpz_decode_average(const float* local, int64_t n, int n_payloads, const int3
                        const float* const* vals, const int64_t* k, const float* w, float w_self,
                        int flags, float* out, void* ws, size_t ws_bytes, dpz_stream_t stream);
 
+/* Replace decode of a GLOBAL payload into one rank's slice of a model sharded over ranks
+ * (SURVEY §8e "one tensor, decode: no collective"; reference sharing/PartialModel.py:292-295
+ * `T[idx] = params` restricted to the slice): local / out hold global elements
+ * [offset, offset + n); out[i] = local[i], then out[idx[j] - offset] = vals[j] for every entry
+ * inside the slice (entries outside are skipped).  idx: k strictly ascending global indices.
+ * local and out 16-byte aligned, out may not alias local.                                      */
+int dpz_replace_slice(const float* local, int64_t n, int64_t offset, const int32_t* idx,
+                      const float* vals, int64_t k, float* out, dpz_stream_t stream);
+
 /* Batched enqueue for a simulated gossip round (decentralizepy_amd/gossip.py): m node codecs,
  * node j on streams[j % n_streams] with workspace ws[j % n_streams].
  * dpz_topk_encode_batch == for each j: dpz_topk_encode(x[j], x0[j], NULL, DPZ_ACC_NONE, x[j], n,

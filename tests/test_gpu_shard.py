@@ -66,14 +66,14 @@ def test_sharded_topk_encode_one_rank_api(dev):
 
 
 @pytest.mark.parametrize("n,world", [(1_000_003, 2), (1_000_003, 3), (25_000_000, 8),
-                                     (100_000, 5)])
+                                     (100_000, 5), (16_484, 4), (28_572, 8)])
 def test_sharded_wavelet_equals_whole_tensor(dev, n, world):
     """SURVEY §8e wavelet row: per-rank forward tiles from halo'd slice buffers (the halo being
     the previous slice's tail) and per-rank inverse tiles, emulated in one process, equal the
     one-GPU transforms bit-exactly (plain and accumulate)."""
     from decentralizepy_amd import codec
     from decentralizepy_amd.shard import (dwt_rank_part, halo_len, idwt_rank_part,
-                                          wavelet_slice)
+                                          tile_widths, wavelet_slice)
     level = 4
     g = torch.Generator(device=dev).manual_seed(n + world)
     x = torch.randn(n, device=dev, generator=g)
@@ -89,14 +89,16 @@ def test_sharded_wavelet_equals_whole_tensor(dev, n, world):
     H = halo_len(level)
     rec = torch.full((n,), float("nan"), device=dev)
     for r in range(world):
-        sl = wavelet_slice(n, level, world, r)
+        sl = wavelet_slice(n, level, world, r, *tile_widths())
         first = max(0, sl["lo"] - H) if r > 0 else 0
         # the rank's buffer: a COPY of its halo + slice (nothing else of x is reachable)
         xb = x[first:sl["hi"]].clone()
         x0b = x0[first:sl["hi"]].clone()
-        dwt_rank_part(xb, x0b, first, n, level, sl["t_lo"], sl["t_hi"], cx, cd)
-        dwt_rank_part(xb, x0b, first, n, level, sl["t_lo"], sl["t_hi"], None, acc,
-                      accumulate=True)
+        if sl["t_lo"] < sl["t_hi"]:
+            assert sl["lo"] < sl["hi"], "an empty slice must own no forward tile"
+            dwt_rank_part(xb, x0b, first, n, level, sl["t_lo"], sl["t_hi"], cx, cd)
+            dwt_rank_part(xb, x0b, first, n, level, sl["t_lo"], sl["t_hi"], None, acc,
+                          accumulate=True)
         out = torch.empty(sl["hi"] - sl["lo"], device=dev)
         if out.numel():
             idwt_rank_part(ref_x, n, level, sl["u_lo"], sl["u_hi"], out, sl["lo"])
@@ -120,3 +122,50 @@ def test_sharded_wavelet_one_rank_api(dev):
     cx, cd = sharded_wavedec(x, x0, n, 4)
     assert torch.equal(cx, ref_x) and torch.equal(cd, ref_d)
     assert torch.equal(sharded_waverec(cx, n, 4), codec.waverec(ref_x, n, 4))
+
+
+def test_sharded_wavedec_headroom_slices(dev):
+    """Slices from alloc_wavelet_slice get the halo written into their own headroom (no copy of
+    the slice); the result equals the one-GPU transform (one rank: no exchange needed)."""
+    from decentralizepy_amd import codec
+    from decentralizepy_amd.shard import alloc_wavelet_slice, sharded_wavedec
+    n = 2_000_003
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(n, device=dev, generator=g)
+    x0 = x - 0.01 * torch.randn(n, device=dev, generator=g)
+    xs = alloc_wavelet_slice(n, 4, 1, 0, dev)
+    x0s = alloc_wavelet_slice(n, 4, 1, 0, dev)
+    xs.copy_(x)
+    x0s.copy_(x0)
+    cx, cd = sharded_wavedec(xs, x0s, n, 4)
+    rx, rd = codec.wavedec(x, 4, x0=x0)
+    assert torch.equal(cx, rx) and torch.equal(cd, rd)
+
+
+@pytest.mark.parametrize("n,world,alpha", [(1_000_003, 3, 0.01), (4_000_000, 8, 0.001),
+                                           (100_001, 5, 0.3)])
+def test_sharded_replace_equals_whole_tensor(dev, n, world, alpha):
+    """SURVEY §8e "one tensor, decode": every rank replaces the GLOBAL payload into its own slice
+    (most entries fall outside it, some slices hold none); the slices assemble the one-GPU
+    replace bit-exactly."""
+    from decentralizepy_amd import codec
+    from decentralizepy_amd.shard import sharded_replace
+    g = torch.Generator(device=dev).manual_seed(n + world)
+    x = torch.randn(n, device=dev, generator=g)
+    x0 = x - 0.01 * torch.randn(n, device=dev, generator=g)
+    k = round(alpha * n)
+    idx, val = codec.topk_encode(x, k, x0=x0)
+    ref = codec.replace(x0, idx, val)
+    bounds = [0, 3, n // 3] + [n // 3 + (j * (n - n // 3)) // (world - 2) for j in range(1, world - 2)] + [n]
+    bounds = sorted(set(bounds))
+    rec = torch.full((n,), float("nan"), device=dev)
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        loc = x0[lo:hi].clone()  # the rank's own (aligned) slice buffer
+        rec[lo:hi] = sharded_replace(loc, lo, idx, val)
+    # a slice no payload entry falls into
+    empty_lo = int(idx[0].item()) - 2 if int(idx[0].item()) >= 2 else None
+    torch.cuda.synchronize()
+    assert torch.equal(rec.view(torch.int32), ref.view(torch.int32))
+    if empty_lo is not None:
+        loc = x0[:empty_lo].clone()
+        assert torch.equal(sharded_replace(loc, 0, idx, val), loc)
