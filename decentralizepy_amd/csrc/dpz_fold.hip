@@ -522,11 +522,14 @@ static inline int64_t fold_ntiles(int64_t n) { return (n + FOLD_TILE - 1) / FOLD
 
 // Replace-only decode of ONE sparse payload (reference PartialModel.py:257-303, T[idx] = params):
 // one 256-thread block per chunk of RP_E payload entries (dpz_replace.h).
+// Standalone replace: one wave per chunk of RP_E entries (~1,600 elements at 1 %), a grid of
+// many short blocks (measured on MI355X: shorter than persistent waves walking the chunks with
+// the next chunk's entries prefetched, and than 64-entry chunks per 256-thread block).
 __global__ void __launch_bounds__(256) replace_kernel(ReplaceJob j) { replace_block(j, blockIdx.x); }
 
 int launch_replace(const ReplaceJob& j, hipStream_t st) {
   if (j.c1 > j.c0)
-    DPZ_TIMED(DPZ_KT_FOLD, st, replace_kernel<<<(unsigned)(j.c1 - j.c0), 256, 0, st>>>(j));
+    DPZ_TIMED(DPZ_KT_FOLD, st, replace_kernel<<<(unsigned)((j.c1 - j.c0 + 3) / 4), 256, 0, st>>>(j));
   return DPZ_OK;
 }
 

@@ -859,6 +859,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   constexpr int PFC = 4;
   uint32_t cnt[2], kk[2][PFC], ii[2][PFC];
   float vv[2][PFC];
+  int32_t cc[2][PFC];  // counter[idx] of the candidates in registers, read ahead of the writes
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int64_t seg = seg0 + u;
@@ -868,6 +869,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
       kk[u][c] = 0u;
       ii[u][c] = 0u;
       vv[u][c] = 0.f;
+      cc[u][c] = 0;
     }
     kk[u][0] = seg < W ? ckey[seg * CAP + lane] : 0u;
     ii[u][0] = seg < W ? cidx[seg * CAP + lane] : 0u;
@@ -879,6 +881,18 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   if (status) {  // select reported a miss: the host runs the exact path
     if (blockIdx.x == 0 && t == 0) atomicOr(&ctrl->sticky, status);
     return;
+  }
+  // Every candidate of chunk 0 reads its counter word (and, when the values are not carried,
+  // its value) now, while the threshold is resolved: the selected ones then update the counter
+  // with a plain store (top-k indices are unique, nothing else writes these words) instead of a
+  // memory-side atomic per index (~64 lines per wave-instruction, the slowest access shape).
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int64_t seg = seg0 + u;
+    if (seg < W && cnt[u] != DENSE && (uint32_t)lane < cnt[u]) {
+      if (counter) cc[u][0] = counter[ii[u][0]];
+      if (!cval) vv[u][0] = vals_src[ii[u][0]];
+    }
   }
   if (t < 64) {
     uint32_t tot;
@@ -938,6 +952,14 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
           if (cval) vv[u][c] = cval[seg * CAP + j];
         }
       }
+#pragma unroll
+      for (int c = 1; c < PFC; ++c) {
+        const uint32_t j = c * 64u + lane;
+        if (j < cnt[u]) {
+          if (counter) cc[u][c] = counter[ii[u][c]];
+          if (!cval) vv[u][c] = vals_src[ii[u][c]];
+        }
+      }
     }
   }
   // count pass (the first PFC chunks from registers), in-block offsets, write pass
@@ -972,14 +994,18 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     const int64_t seg = seg0 + u;
     if (seg >= W) break;
     if (cnt[u] != DENSE) {
-      auto emit = [&](bool sel, uint32_t idx, float v) {
+      // pre: the value and counter word were read ahead (v, cw valid); otherwise gathered here
+      auto emit = [&](bool sel, uint32_t idx, float v, bool pre, int32_t cw) {
         const uint64_t m = __ballot(sel);
         if (sel) {
           const uint32_t pos = run + mbcnt64(m);
           if (pos < (uint64_t)k) {
             idx_out[pos] = (int32_t)idx;
-            val_out[pos] = cval ? v : vals_src[idx];
-            if (counter) atomicAdd(&counter[idx], 1);  // non-returning: no round trip to wait on
+            val_out[pos] = (cval || pre) ? v : vals_src[idx];
+            if (counter) {
+              if (pre) counter[idx] = cw + 1;
+              else atomicAdd(&counter[idx], 1);  // non-returning: no round trip to wait on
+            }
             if (rewind) rewind[idx] = 0.0f;
           }
         }
@@ -988,7 +1014,8 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
 #pragma unroll
       for (int c = 0; c < PFC; ++c) {
         const uint32_t j = c * 64u + lane;
-        if (c * 64u < cnt[u]) emit(j < cnt[u] && is_sel(kk[u][c], ii[u][c]), ii[u][c], vv[u][c]);
+        if (c * 64u < cnt[u])
+          emit(j < cnt[u] && is_sel(kk[u][c], ii[u][c]), ii[u][c], vv[u][c], true, cc[u][c]);
       }
       for (uint32_t j0 = PFC * 64u; j0 < cnt[u]; j0 += 64) {
         const uint32_t j = j0 + lane;
@@ -1001,7 +1028,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
           if (cval) v = cval[seg * CAP + j];
           sel = is_sel(key, idx);
         }
-        emit(sel, idx, v);
+        emit(sel, idx, v, false, 0);
       }
     } else {
       dense_write<VEC>(s, seg, R, n, k, lo, T, icut, run, vals_src, idx_out, val_out, counter,
@@ -1054,7 +1081,7 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
     const int64_t C = a.job->c1 - a.job->c0;
     double f[3];
     cosched_shares(f);
-    const int per[3] = {1, 4, 1};  // chunks per appended block (256- / 1024-thread blocks)
+    const int per[3] = {4, 16, 4};  // chunks per appended block (one per wave)
     int64_t c = a.job->c0;
     double acc_f = 0.0;
     for (int i = 0; i < 3; ++i) {
