@@ -259,7 +259,13 @@ __global__ void __launch_bounds__(256, ACC ? 4 : FOCC) sampled_filter_kernel(
   }
   Raw4 raw[G];
   load_groups<VEC, ACC, G>(s, beg, end, lane, raw);
+#ifdef DPZ_DIAG_FIXED_WINDOW
+  if (threadIdx.x == 0) { win[0] = 0x3CCB295Fu; win[1] = 0x80000000u; win[2] = 21; }
+  __syncthreads();
+  (void)cv;
+#else
   block_window(cv, r_lo, r_hi, win, wsum);
+#endif
   STAMP_W(1);
   STAMP_W(2);
   const uint32_t lo = win[0], hi = win[1], shift = win[2];
@@ -859,7 +865,6 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   constexpr int PFC = 4;
   uint32_t cnt[2], kk[2][PFC], ii[2][PFC];
   float vv[2][PFC];
-  int32_t cc[2][PFC];  // counter[idx] of the candidates in registers, read ahead of the writes
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int64_t seg = seg0 + u;
@@ -869,7 +874,6 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
       kk[u][c] = 0u;
       ii[u][c] = 0u;
       vv[u][c] = 0.f;
-      cc[u][c] = 0;
     }
     kk[u][0] = seg < W ? ckey[seg * CAP + lane] : 0u;
     ii[u][0] = seg < W ? cidx[seg * CAP + lane] : 0u;
@@ -882,17 +886,15 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     if (blockIdx.x == 0 && t == 0) atomicOr(&ctrl->sticky, status);
     return;
   }
-  // Every candidate of chunk 0 reads its counter word (and, when the values are not carried,
-  // its value) now, while the threshold is resolved: the selected ones then update the counter
-  // with a plain store (top-k indices are unique, nothing else writes these words) instead of a
-  // memory-side atomic per index (~64 lines per wave-instruction, the slowest access shape).
+  // When the values are not carried from the filter (vals_src != x), every candidate of chunk 0
+  // gathers its value now, while the threshold is resolved, not at write time.  (Reading the
+  // counter words ahead the same way, for plain-store updates, measured ~1 us SLOWER than the
+  // memory-side atomics at C2: it reads every candidate's line.)
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int64_t seg = seg0 + u;
-    if (seg < W && cnt[u] != DENSE && (uint32_t)lane < cnt[u]) {
-      if (counter) cc[u][0] = counter[ii[u][0]];
-      if (!cval) vv[u][0] = vals_src[ii[u][0]];
-    }
+    if (!cval && seg < W && cnt[u] != DENSE && (uint32_t)lane < cnt[u])
+      vv[u][0] = vals_src[ii[u][0]];
   }
   if (t < 64) {
     uint32_t tot;
@@ -955,10 +957,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
 #pragma unroll
       for (int c = 1; c < PFC; ++c) {
         const uint32_t j = c * 64u + lane;
-        if (j < cnt[u]) {
-          if (counter) cc[u][c] = counter[ii[u][c]];
-          if (!cval) vv[u][c] = vals_src[ii[u][c]];
-        }
+        if (j < cnt[u] && !cval) vv[u][c] = vals_src[ii[u][c]];
       }
     }
   }
@@ -994,18 +993,15 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     const int64_t seg = seg0 + u;
     if (seg >= W) break;
     if (cnt[u] != DENSE) {
-      // pre: the value and counter word were read ahead (v, cw valid); otherwise gathered here
-      auto emit = [&](bool sel, uint32_t idx, float v, bool pre, int32_t cw) {
+      // pre: the value was read ahead (v valid); otherwise gathered here
+      auto emit = [&](bool sel, uint32_t idx, float v, bool pre) {
         const uint64_t m = __ballot(sel);
         if (sel) {
           const uint32_t pos = run + mbcnt64(m);
           if (pos < (uint64_t)k) {
             idx_out[pos] = (int32_t)idx;
             val_out[pos] = (cval || pre) ? v : vals_src[idx];
-            if (counter) {
-              if (pre) counter[idx] = cw + 1;
-              else atomicAdd(&counter[idx], 1);  // non-returning: no round trip to wait on
-            }
+            if (counter) atomicAdd(&counter[idx], 1);  // non-returning: no round trip to wait on
             if (rewind) rewind[idx] = 0.0f;
           }
         }
@@ -1015,7 +1011,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
       for (int c = 0; c < PFC; ++c) {
         const uint32_t j = c * 64u + lane;
         if (c * 64u < cnt[u])
-          emit(j < cnt[u] && is_sel(kk[u][c], ii[u][c]), ii[u][c], vv[u][c], true, cc[u][c]);
+          emit(j < cnt[u] && is_sel(kk[u][c], ii[u][c]), ii[u][c], vv[u][c], true);
       }
       for (uint32_t j0 = PFC * 64u; j0 < cnt[u]; j0 += 64) {
         const uint32_t j = j0 + lane;
@@ -1028,7 +1024,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
           if (cval) v = cval[seg * CAP + j];
           sel = is_sel(key, idx);
         }
-        emit(sel, idx, v, false, 0);
+        emit(sel, idx, v, false);
       }
     } else {
       dense_write<VEC>(s, seg, R, n, k, lo, T, icut, run, vals_src, idx_out, val_out, counter,

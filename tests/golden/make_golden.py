@@ -156,12 +156,15 @@ class TieError(RuntimeError):
     pass
 
 
-def run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed, wavelet=False, nbr_kinds=None):
-    """Replay; on a tie at the k-th key (fp32 differences are quantised) retry with the next seed."""
+def run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed, wavelet=False, nbr_kinds=None,
+                 averaging="_averaging"):
+    """Replay; on a tie at the k-th key (fp32 differences are quantised) retry with the next seed.
+    ``averaging`` names the reference method the node calls on receive (``_averaging``, or the
+    federated server's ``_averaging_server``)."""
     for attempt in range(40):
         try:
             meta = _run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed + 1000 * attempt,
-                                 wavelet, nbr_kinds)
+                                 wavelet, nbr_kinds, averaging)
             meta["seed"] = seed + 1000 * attempt
             return meta
         except TieError as e:
@@ -169,7 +172,8 @@ def run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed, wavelet=False,
     raise RuntimeError(f"{name}: no tie-free seed found")
 
 
-def _run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed, wavelet, nbr_kinds):
+def _run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed, wavelet, nbr_kinds,
+                  averaging="_averaging", on_send=None):
     rng = np.random.default_rng(seed)
     n = rows * cols + nb
     model = Net(rows, cols, nb)
@@ -182,6 +186,8 @@ def _run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed, wavelet, nbr_
     arrays = {"x0": x0}
     meta = {"name": name, "class": cls.__name__, "kwargs": kwargs, "shape": [rows, cols, nb],
             "n": n, "rounds": []}
+    if averaging != "_averaging":
+        meta["averaging"] = averaging
     length = n
     for r in range(rounds):
         cur = get_flat(model)
@@ -190,6 +196,8 @@ def _run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed, wavelet, nbr_
         set_flat(model, x_r)
         arrays[f"r{r}_x"] = x_r
         data = plugin.get_data_to_send(degree=len(uid_nbrs))
+        if on_send is not None:  # wire_main: records the payload and ends the replay
+            on_send(r, data)
         change = plugin.model.model_change
         rmeta = {"alpha": float(plugin.alpha), "partial": "send_partial" in data}
         if wavelet:
@@ -211,7 +219,7 @@ def _run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed, wavelet, nbr_
         msgs = neighbour_payloads(rng, length, kinds, len(uid_nbrs), r, 0.05)
         rmeta["neighbours"] = record_msgs(f"r{r}", msgs, arrays)
         peer = {uid: deque([m]) for uid, m in zip(uid_nbrs, msgs)}
-        plugin._averaging(peer)
+        getattr(plugin, averaging)(peer)
         arrays[f"r{r}_model_after"] = get_flat(model)
         if plugin.model.accumulated_changes is not None:
             arrays[f"r{r}_acc_after_avg"] = plugin.model.accumulated_changes.numpy().copy()
@@ -220,8 +228,8 @@ def _run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed, wavelet, nbr_
     return meta
 
 
-def sharing_scenario():
-    rng = np.random.default_rng(5)
+def sharing_scenario(averaging="_averaging", name="sharing_full", seed=5):
+    rng = np.random.default_rng(seed)
     rows, cols, nb = 31, 33, 7
     n = rows * cols + nb
     model = Net(rows, cols, nb)
@@ -232,12 +240,43 @@ def sharing_scenario():
     data = plugin.get_data_to_send(degree=3)
     msgs = neighbour_payloads(rng, n, ["full"] * 3, 3, 0, 1.0)
     arrays = {"x0": x0, "sent_params": np.asarray(data["params"])}
-    meta = {"name": "sharing_full", "class": "Sharing", "n": n, "shape": [rows, cols, nb],
+    meta = {"name": name, "class": "Sharing", "n": n, "shape": [rows, cols, nb],
             "neighbours": record_msgs("r0", msgs, arrays)}
-    plugin._averaging({uid: deque([m]) for uid, m in zip([1, 2, 3], msgs)})
+    if averaging != "_averaging":
+        meta["averaging"] = averaging
+    getattr(plugin, averaging)({uid: deque([m]) for uid, m in zip([1, 2, 3], msgs)})
     arrays["r0_model_after"] = get_flat(model)
-    np.savez_compressed(os.path.join(OUT, "sharing_full.npz"), **arrays)
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **arrays)
     return meta
+
+
+def server_main():
+    """The federated server's plain average (reference Sharing.py:200-229 and
+    sharing/JWINS/Wavelet.py:331-385, weight 1 / n, no self term) on Sharing, PartialModel and
+    Wavelet, two rounds each with mixed sparse / full neighbour payloads ->
+    tests/golden/server_*.npz + server_scenarios.json (the _averaging fixtures are untouched)."""
+    torch.set_num_threads(4)
+    srv = "_averaging_server"
+    mixed = [["partial", "full", "partial"], ["full", "partial", "partial"]]
+    scen = [
+        run_scenario("server_pm", PartialModel, {"dict_ordered": True, "alpha": 0.1}, 40, 100,
+                     99, 2, seed=51, nbr_kinds=mixed, averaging=srv),
+        run_scenario("server_pm_acc", PartialModel,
+                     {"dict_ordered": True, "alpha": 0.05, "accumulation": True,
+                      "accumulate_averaging_changes": True}, 40, 100, 99, 2, seed=52,
+                     averaging=srv),
+        run_scenario("server_wv", Wavelet,
+                     {"wavelet": "sym2", "level": 4, "alpha": 0.1, "metadata_cap": 0.5,
+                      "accumulation": True}, 40, 100, 99, 2, seed=53, wavelet=True,
+                     nbr_kinds=mixed, averaging=srv),
+        sharing_scenario(averaging=srv, name="server_sharing", seed=54),
+    ]
+    with open(os.path.join(OUT, "server_scenarios.json"), "w") as f:
+        json.dump({"scenarios": scen, "generator": "tests/golden/make_golden.py --server",
+                   "reference": "sacs-epfl/decentralizepy v1 (/root/reference/src)",
+                   "pywavelets": "1.1.1 (python3.9 bridge)", "torch": torch.__version__}, f,
+                  indent=1)
+    print("wrote", len(scen), "server scenarios")
 
 
 def elias_vectors():
@@ -323,5 +362,59 @@ def main():
     print("wrote", len(scen), "scenarios")
 
 
+class _WireDone(Exception):
+    pass
+
+
+def wire_main():
+    """What the reference's TCP layer puts on the wire for a node's first outgoing message
+    (communication/TCP.py:110-131, 215-232: pickle.dumps of the dict after DPSGDNode adds
+    CHANNEL; total_data += len(pickle.dumps(params)), total_meta += the rest, total_bytes += the
+    message length): for PartialModel, Wavelet and JWINS payloads, plain and with the reference
+    Elias index compression -> tests/golden/wire.json (sha256 + lengths of the pickled dict)."""
+    import hashlib
+    torch.set_num_threads(4)
+    with open(os.path.join(OUT, "scenarios.json")) as f:
+        metas = {m["name"]: m for m in json.load(f)["scenarios"]}
+    classes = {"PartialModel": PartialModel, "Wavelet": Wavelet, "JWINS": JWINS}
+    cases = []
+    for name, compression in [("pm_a01_plain", None), ("pm_a01_plain", "Elias"),
+                              ("wv_plain", None), ("wv_acc", "Elias"),
+                              ("jwins_tutorial", "Elias"), ("pm_fullshare", None)]:
+        m = metas[name]
+        kwargs = dict(m["kwargs"])
+        if compression:
+            kwargs.update(compress=True, compression_package="decentralizepy.compression." +
+                          compression, compression_class=compression)
+        rec = {}
+
+        def on_send(r, data, rec=rec):
+            msg = dict(data)
+            msg["CHANNEL"] = "DPSGD"  # node/DPSGDNode.py adds the channel before send
+            out = pickle.dumps(msg)
+            data_len = len(pickle.dumps(msg["params"])) if "params" in msg else 0
+            rec.update(keys=list(msg), pickle_len=len(out), data_len=data_len,
+                       meta_len=len(out) - data_len, sha256=hashlib.sha256(out).hexdigest())
+            raise _WireDone()
+
+        rows, cols, nb = m["shape"]
+        try:
+            _run_scenario(name, classes[m["class"]], kwargs, rows, cols, nb, 1, m["seed"],
+                          m["class"] != "PartialModel", None, on_send=on_send)
+        except _WireDone:
+            pass
+        cases.append({"scenario": name, "compression": compression, **rec})
+    with open(os.path.join(OUT, "wire.json"), "w") as f:
+        json.dump({"cases": cases, "generator": "tests/golden/make_golden.py --wire",
+                   "python": sys.version.split()[0], "numpy": np.__version__,
+                   "pickle_protocol": pickle.DEFAULT_PROTOCOL}, f, indent=1)
+    print("wrote", len(cases), "wire cases")
+
+
 if __name__ == "__main__":
-    main()
+    if "--wire" in sys.argv:
+        wire_main()
+    elif "--server" in sys.argv:
+        server_main()
+    else:
+        main()

@@ -21,8 +21,12 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def load_meta():
+    """scenarios.json plus the federated-server scenarios (server_scenarios.json), merged."""
     with open(os.path.join(GOLDEN, "scenarios.json")) as f:
-        return json.load(f)
+        meta = json.load(f)
+    with open(os.path.join(GOLDEN, "server_scenarios.json")) as f:
+        meta["scenarios"] = meta["scenarios"] + json.load(f)["scenarios"]
+    return meta
 
 
 def scenario_names(cls_filter=None):
@@ -109,17 +113,22 @@ class OracleNode:
                                     counter=self.counter)
         return {"alpha": self.alpha, "indices": idx, "params": val, "send_partial": True}
 
-    def averaging(self, msgs):
+    def averaging(self, msgs, server=False):
+        """Metro-Hastings fold (reference Sharing.py:156-190); ``server``: the plain 1/n average
+        with no self term of _averaging_server (Sharing.py:200-229, Wavelet.py:331-385)."""
         pays, degs = [], []
         for m in msgs:
             pays.append((m["indices"], m["params"]) if "send_partial" in m else (None, m["params"]))
             degs.append(m["degree"])
-        w = [ofold.mh_weight(len(msgs), d) for d in degs]
-        wt = 0
-        for v in w:
-            wt += v
         local = self.xT if self.wavelet else self.model
-        total = ofold.fold(local, pays, w, 1 - wt)
+        if server:
+            total = ofold.fold(local, pays, [1 / len(msgs)] * len(msgs), None)
+        else:
+            w = [ofold.mh_weight(len(msgs), d) for d in degs]
+            wt = 0
+            for v in w:
+                wt += v
+            total = ofold.fold(local, pays, w, 1 - wt)
         self.model = owav.waverec_array(total, self.n, self.level) if self.wavelet else total
         # post step
         new = self.model.copy()
@@ -158,7 +167,8 @@ def replay_oracle(name):
         pay = node.get_data_to_send()
         got = {"payload": pay, "counter_enc": node.counter.copy(),
                "acc_enc": None if node.acc is None else node.acc.copy()}
-        node.averaging(neighbour_msgs(mr, arrays, r))
+        node.averaging(neighbour_msgs(mr, arrays, r),
+                       server=meta.get("averaging") == "_averaging_server")
         got["model"] = node.model
         got["acc_avg"] = None if node.acc is None else node.acc.copy()
         check_round(got, arrays, r, mr)
@@ -227,10 +237,12 @@ def _elias_wire(msgs, check_cls):
     return out
 
 
-def replay_plugin(name, tmpdir, compression_class=None):
+def replay_plugin(name, tmpdir, compression_class=None, config=None):
     """Drive the device plugin through the scenario; with ``compression_class`` ("Elias" or
     "EliasFpzip" of decentralizepy_amd.compression) the wire payloads are compressed and the
-    outgoing index stream is checked against the oracle's reference-pinned Elias bytes."""
+    outgoing index stream is checked against the oracle's reference-pinned Elias bytes.
+    ``config`` = (package, class, kwargs) from sharing_section(): the plugin is built the way
+    Node.init_sharing builds it (importlib, keyword arguments from the config file)."""
     import torch  # noqa: F401
     from oracle import elias as oelias
 
@@ -245,8 +257,14 @@ def replay_plugin(name, tmpdir, compression_class=None):
     if compression_class:
         kwargs.update(compress=True, compression_class=compression_class,
                       compression_package=f"decentralizepy_amd.compression.{compression_class}")
-    plugin = classes[meta["class"]](0, 0, None, _Mapping(), _Graph([1, 2, 3]), model, None,
-                                    str(tmpdir), **kwargs)
+    if config is not None:
+        import importlib
+        package, cls_name, kwargs = config
+        cls = getattr(importlib.import_module(package), cls_name)
+        compression_class = kwargs.get("compression_class") if kwargs.get("compress") else None
+    else:
+        cls = classes[meta["class"]]
+    plugin = cls(0, 0, None, _Mapping(), _Graph([1, 2, 3]), model, None, str(tmpdir), **kwargs)
     for r, mr in enumerate(meta["rounds"]):
         set_flat(model, arrays[f"r{r}_x"])
         data = plugin.get_data_to_send(degree=3)
@@ -264,9 +282,46 @@ def replay_plugin(name, tmpdir, compression_class=None):
         if compression_class:
             msgs = _elias_wire(msgs, compression_class)
         peer = {uid: deque([m]) for uid, m in zip([1, 2, 3], msgs)}
-        plugin._averaging(peer)
+        getattr(plugin, meta.get("averaging", "_averaging"))(peer)
         got["model"] = get_flat(model)
         acc = getattr(model, "accumulated_changes", None)
         got["acc_avg"] = None if acc is None else acc.cpu().numpy().copy()
         check_round(got, arrays, r, mr)
     return plugin
+
+
+# ---- config.ini drop-in ---------------------------------------------------------------------------
+def localconfig_value(v):
+    """The scalar coercion the reference's config reader (the absent ``localconfig`` package)
+    applies, as inferred from its call sites (JWINS.py:88 evals alpha_list, so
+    lists stay strings): int, then float, then booleans / None, else the string."""
+    s = v.strip()
+    for conv in (int, float):
+        try:
+            return conv(s)
+        except ValueError:
+            pass
+    low = s.lower()
+    if low in ("true", "yes", "on"):
+        return True
+    if low in ("false", "no", "off"):
+        return False
+    if low == "none":
+        return None
+    return s
+
+
+def sharing_section(path, to_build=True):
+    """[SHARING] of a reference config.ini as Node.init_sharing sees it (node/Node.py:303-328):
+    package, class and the remaining keyword arguments; with ``to_build`` the reference's
+    package paths point at this build (decentralizepy. -> decentralizepy_amd.), nothing else."""
+    import configparser
+    cp = configparser.ConfigParser()
+    cp.read(path)
+    sec = {k: localconfig_value(v) for k, v in cp.items("SHARING")}
+    if to_build:
+        for key in ("sharing_package", "compression_package"):
+            if key in sec and str(sec[key]).startswith("decentralizepy."):
+                sec[key] = "decentralizepy_amd." + sec[key][len("decentralizepy."):]
+    package, cls = sec.pop("sharing_package"), sec.pop("sharing_class")
+    return package, cls, sec

@@ -109,3 +109,29 @@ def test_choco_constructor_keyword_surface_matches_reference():
     params = list(inspect.signature(Choco.__init__).parameters)
     assert params[9:] == ["step_size", "alpha", "compress", "compression_package",
                           "compression_class", "float_precision"]
+
+
+def test_tutorial_jwins_config_binds_unchanged():
+    """The reference's tutorial/JWINS/config.ini (copied as data: tests/golden/
+    jwins_tutorial_config.ini) with only the package paths swapped: its [SHARING] section binds
+    to the build's JWINS exactly as Node.init_sharing passes it (node/Node.py:303-328)."""
+    import importlib
+    import os
+    path = os.path.join(scenario.GOLDEN, "jwins_tutorial_config.ini")
+    package, cls_name, kwargs = scenario.sharing_section(path)
+    assert package == "decentralizepy_amd.sharing.JWINS.JWINS" and cls_name == "JWINS"
+    assert kwargs["compression_package"] == "decentralizepy_amd.compression.EliasFpzip"
+    assert kwargs["level"] == 4 and kwargs["metadata_cap"] == 0.5
+    assert kwargs["accumulation"] is True and kwargs["alpha_list"].startswith("[")
+    cls = getattr(importlib.import_module(package), cls_name)
+    inspect.signature(cls.__init__).bind(None, 0, 0, None, None, None, None, None, "/tmp",
+                                         **kwargs)
+    # the compressor the config names is importable and built the way Sharing loads it
+    comp = getattr(importlib.import_module(kwargs["compression_package"]),
+                   kwargs["compression_class"])
+    comp(float_precision=None)
+    # and the reference's own package paths name the same classes
+    ref_pkg, ref_cls, ref_kwargs = scenario.sharing_section(path, to_build=False)
+    assert ref_pkg == "decentralizepy.sharing.JWINS.JWINS" and ref_cls == cls_name
+    assert {k: v for k, v in ref_kwargs.items() if k != "compression_package"} == \
+        {k: v for k, v in kwargs.items() if k != "compression_package"}

@@ -31,8 +31,7 @@ def test_node_step_batch_matches_oracle(dev, streams):
     nodes = [_node(dev, n, k, 40 + j) for j in range(m)]
     ss = [torch.cuda.Stream(dev) for _ in range(streams)]
     ws = [codec.Workspace(dev) for _ in range(streams)]
-    # node j decodes node (j+1) % m's payload: independent of its own encode only across nodes
-    # handled earlier on the same stream, so decode the node's own payload (the bench's step)
+    # every node decodes its own payload after its encode (the bench's step)
     b = codec.NodeStepBatch(nodes, n, k, ss, ws)
     b.sticky_status(clear=True)
     for _ in range(2):  # twice: counters accumulate, workspaces are reused
@@ -76,22 +75,14 @@ def test_node_step_batch_encode_only_and_decode_only(dev):
 
 
 def test_sticky_status_records_an_uncompleted_miss(dev):
-    """An ASYNC encode whose sampled window misses (adversarial layout, as in
+    """An ASYNC encode whose sampled window misses (tests/layouts.py, as in
     test_gpu_codec.test_topk_sampled_miss_falls_back) is never completed: the sticky word must
     say so, and a clear must reset it."""
     from decentralizepy_amd import codec
     n = 1 << 20
     k = round(0.01 * n)
-    x = np.zeros(n, dtype=np.float32)
-    rng = np.random.default_rng(11)
-    big = []
-    for c in range(1023):
-        s = (c * (n - 64)) // 1023 + 64
-        e = ((c + 1) * (n - 64)) // 1023
-        big.extend(range(s + 100, min(e - 100, s + 100 + 12)))
-    big = np.array(big)
-    x[:] = 1e-6 * rng.standard_normal(n).astype(np.float32)
-    x[big] = rng.uniform(1.0, 2.0, big.shape[0]).astype(np.float32)
+    from tests.layouts import miss_layout
+    x, _ = miss_layout(n, k)
     tx = torch.from_numpy(x).to(dev)
     tx0 = torch.zeros(n, device=dev)
     ws = codec.Workspace(dev)

@@ -145,21 +145,11 @@ def test_topk_unaligned_views(dev):
 def test_topk_sampled_miss_falls_back(dev):
     """Adversarial layout: the large changes sit between the sample chunks, so the sampled window
     misses the k-th key; the device flags it and the exact path must still give the oracle's set."""
+    from tests.layouts import miss_layout
     codec = _codec()
     n = 1 << 20
     k = round(0.01 * n)
-    x = np.zeros(n, dtype=np.float32)
-    x0 = np.zeros(n, dtype=np.float32)
-    rng = np.random.default_rng(11)
-    # sample chunk c covers [c*(n-64)/1023, +64): put big changes in the middle of the gaps
-    big = []
-    for c in range(1023):
-        s = (c * (n - 64)) // 1023 + 64
-        e = ((c + 1) * (n - 64)) // 1023
-        big.extend(range(s + 100, min(e - 100, s + 100 + 12)))
-    big = np.array(big)
-    x[:] = 1e-6 * rng.standard_normal(n).astype(np.float32)
-    x[big] = rng.uniform(1.0, 2.0, big.shape[0]).astype(np.float32)
+    x, x0 = miss_layout(n, k)
     tx = torch.from_numpy(x).to(dev)
     tx0 = torch.from_numpy(x0).to(dev)
     ws = codec.Workspace(dev)

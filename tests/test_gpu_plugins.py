@@ -16,10 +16,13 @@ def test_plugin_replays_reference_scenario(name, dev, tmp_path):
     scenario.replay_plugin(name, tmp_path)
 
 
-def test_sharing_full_model_fold(dev, tmp_path):
+@pytest.mark.parametrize("name", ["sharing_full", "server_sharing"])
+def test_sharing_full_model_fold(dev, tmp_path, name):
+    """Full-model Sharing: _averaging (Metro-Hastings) and the federated server's
+    _averaging_server (1/n, no self term) against the reference's recorded outputs."""
     from decentralizepy_amd.sharing.Sharing import Sharing
-    meta = next(s for s in scenario.load_meta()["scenarios"] if s["name"] == "sharing_full")
-    a = dict(np.load(os.path.join(scenario.GOLDEN, "sharing_full.npz")))
+    meta = next(s for s in scenario.load_meta()["scenarios"] if s["name"] == name)
+    a = dict(np.load(os.path.join(scenario.GOLDEN, f"{name}.npz")))
     model = scenario.make_model(meta["shape"])
     scenario.set_flat(model, a["x0"])
     plugin = Sharing(0, 0, None, scenario._Mapping(), scenario._Graph([1, 2, 3]), model, None,
@@ -30,7 +33,8 @@ def test_sharing_full_model_fold(dev, tmp_path):
     for i, nb in enumerate(meta["neighbours"]):
         msgs.append({"params": a[f"r0_nbr{i}_params"], "degree": nb["degree"], "iteration": 0,
                      "CHANNEL": "DPSGD"})
-    plugin._averaging({uid: deque([m]) for uid, m in zip([1, 2, 3], msgs)})
+    getattr(plugin, meta.get("averaging", "_averaging"))(
+        {uid: deque([m]) for uid, m in zip([1, 2, 3], msgs)})
     np.testing.assert_array_equal(scenario.get_flat(model).view(np.uint32),
                                   a["r0_model_after"].view(np.uint32))
 
@@ -40,3 +44,55 @@ def test_counter_dump_like_the_node(dev, tmp_path):
     plugin = scenario.replay_plugin("pm_a01_plain", tmp_path)
     counts = plugin.model.shared_parameters_counter.numpy().tolist()
     assert isinstance(counts, list) and sum(counts) == 2 * 410
+
+
+def test_jwins_built_from_tutorial_config_replays_reference(dev, tmp_path):
+    """JWINS built from the UNCHANGED tutorial/JWINS/config.ini [SHARING] section (package paths
+    swapped), the way Node.init_sharing builds it, with the EliasFpzip wire compression the
+    config names: the tutorial scenario replays bit-exactly, the outgoing index streams match
+    the reference-pinned Elias bytes."""
+    cfg = scenario.sharing_section(os.path.join(scenario.GOLDEN, "jwins_tutorial_config.ini"))
+    meta = next(s for s in scenario.load_meta()["scenarios"] if s["name"] == "jwins_tutorial")
+    # the fixture was generated with the config's algorithm keywords (no compression)
+    for key, v in meta["kwargs"].items():
+        assert cfg[2][key] == v, key
+    scenario.replay_plugin("jwins_tutorial", tmp_path, config=cfg)
+
+
+def _wire_cases():
+    import json
+    with open(os.path.join(scenario.GOLDEN, "wire.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("case", _wire_cases(), ids=lambda c: f"{c['scenario']}-{c['compression']}")
+def test_outgoing_message_pickles_like_the_reference(dev, tmp_path, case):
+    """TCP wire (communication/TCP.py:110-131, 215-232): the node's first outgoing dict, with the
+    CHANNEL key DPSGDNode adds, pickles to the reference's exact bytes (same keys, order, dtypes
+    and values), so total_bytes / total_data / total_meta count the same."""
+    import hashlib
+    import pickle
+
+    from decentralizepy_amd.sharing.JWINS.JWINS import JWINS
+    from decentralizepy_amd.sharing.JWINS.Wavelet import Wavelet
+    from decentralizepy_amd.sharing.PartialModel import PartialModel
+    classes = {"PartialModel": PartialModel, "Wavelet": Wavelet, "JWINS": JWINS}
+    meta, arrays = scenario.load(case["scenario"])
+    kwargs = dict(meta["kwargs"])
+    if case["compression"]:
+        c = case["compression"]
+        kwargs.update(compress=True, compression_class=c,
+                      compression_package=f"decentralizepy_amd.compression.{c}")
+    model = scenario.make_model(meta["shape"])
+    scenario.set_flat(model, arrays["x0"])
+    plugin = classes[meta["class"]](0, 0, None, scenario._Mapping(), scenario._Graph([1, 2, 3]),
+                                    model, None, str(tmp_path), **kwargs)
+    scenario.set_flat(model, arrays["r0_x"])
+    msg = dict(plugin.get_data_to_send(degree=3))
+    msg["CHANNEL"] = "DPSGD"
+    out = pickle.dumps(msg)
+    data_len = len(pickle.dumps(msg["params"])) if "params" in msg else 0
+    assert list(msg) == case["keys"]
+    assert (len(out), data_len, len(out) - data_len) == (
+        case["pickle_len"], case["data_len"], case["meta_len"])
+    assert hashlib.sha256(out).hexdigest() == case["sha256"]

@@ -18,15 +18,19 @@ def test_oracle_replays_reference_scenario(name):
     scenario.replay_oracle(name)
 
 
-def test_oracle_full_model_sharing_fold():
-    meta = next(s for s in scenario.load_meta()["scenarios"] if s["name"] == "sharing_full")
-    a = dict(np.load(os.path.join(GOLDEN, "sharing_full.npz")))
+@pytest.mark.parametrize("name", ["sharing_full", "server_sharing"])
+def test_oracle_full_model_sharing_fold(name):
+    meta = next(s for s in scenario.load_meta()["scenarios"] if s["name"] == name)
+    a = dict(np.load(os.path.join(GOLDEN, f"{name}.npz")))
     pays = [(None, a[f"r0_nbr{i}_params"]) for i in range(3)]
-    w = [ofold.mh_weight(3, nb["degree"]) for nb in meta["neighbours"]]
-    wt = 0
-    for v in w:
-        wt += v
-    out = ofold.fold(a["x0"], pays, w, 1 - wt)
+    if meta.get("averaging") == "_averaging_server":  # reference Sharing.py:200-229
+        out = ofold.fold(a["x0"], pays, [1 / 3] * 3, None)
+    else:
+        w = [ofold.mh_weight(3, nb["degree"]) for nb in meta["neighbours"]]
+        wt = 0
+        for v in w:
+            wt += v
+        out = ofold.fold(a["x0"], pays, w, 1 - wt)
     np.testing.assert_array_equal(out.view(np.uint32), a["r0_model_after"].view(np.uint32))
     np.testing.assert_array_equal(a["sent_params"], a["x0"])
 
