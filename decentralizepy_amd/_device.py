@@ -106,7 +106,13 @@ class DeviceCounter:
         return self.device_tensor.numel()
 
     def __getitem__(self, item):
-        return self.device_tensor.cpu()[item]
+        """Index on the device and copy only the selection (a CPU tensor, as indexing the
+        reference's CPU counter returns); host index arrays are moved to the device first."""
+        if isinstance(item, (np.ndarray, list)):
+            item = torch.as_tensor(np.asarray(item), device=self.device_tensor.device)
+        elif isinstance(item, torch.Tensor):
+            item = item.to(self.device_tensor.device)
+        return self.device_tensor[item].cpu()
 
     def __array__(self, dtype=None):
         a = self.numpy()

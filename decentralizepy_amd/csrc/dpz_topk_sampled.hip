@@ -259,13 +259,7 @@ __global__ void __launch_bounds__(256, ACC ? 4 : FOCC) sampled_filter_kernel(
   }
   Raw4 raw[G];
   load_groups<VEC, ACC, G>(s, beg, end, lane, raw);
-#ifdef DPZ_DIAG_FIXED_WINDOW
-  if (threadIdx.x == 0) { win[0] = 0x3CCB295Fu; win[1] = 0x80000000u; win[2] = 21; }
-  __syncthreads();
-  (void)cv;
-#else
   block_window(cv, r_lo, r_hi, win, wsum);
-#endif
   STAMP_W(1);
   STAMP_W(2);
   const uint32_t lo = win[0], hi = win[1], shift = win[2];

