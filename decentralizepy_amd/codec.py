@@ -449,6 +449,52 @@ def elias_decode(buf, nbytes, nbits, first, count, dtype=torch.int64, workspace=
     return out[:n.value]
 
 
+def fpz_encode(x, precision=0, out=None, workspace=None):
+    """Block-floating stream of a device fp32 vector (csrc/dpz_fpz.hip; the float leg of
+    compression/EliasFpzip.py:19-51 at precision 0 and EliasFpzipLossy.py:14-58 at precision p).
+    Returns a device uint8 view of exactly the stream's bytes."""
+    _require(x, torch.float32, "x")
+    n = x.numel()
+    cap = int(_lib.lib().dpz_fpz_max_bytes(n))
+    if out is None or out.numel() < cap:
+        out = torch.empty(cap, dtype=torch.uint8, device=x.device)
+    need = int(_lib.lib().dpz_fpz_workspace_bytes(n))
+    workspace = workspace or Workspace(x.device)
+    if workspace.ebuf is None or workspace.ebuf.numel() < need:
+        workspace.ebuf = torch.empty(max(need, 256), dtype=torch.uint8, device=x.device)
+    ws = workspace.ebuf
+    nbytes = ctypes.c_int64(0)
+    rc = _lib.lib().dpz_fpz_encode(_ptr(x), n, int(precision), _ptr(out), out.numel(),
+                                   ctypes.byref(nbytes), _ptr(ws), ws.numel(), _stream(x.device))
+    if rc == _lib.DPZ_ERR_UNSUPPORTED:
+        raise ValueError("float precision must be 0 (lossless) or 10..32")
+    check(rc, "dpz_fpz_encode")
+    return out[:nbytes.value]
+
+
+def fpz_decode(buf, n, precision, out=None, check_status=True):
+    """Values of a block-floating stream held on the device (a uint8 tensor of the whole stream,
+    4-byte aligned); ``n`` and ``precision`` come from its header.  With ``check_status`` the
+    call synchronises and raises ValueError on a malformed stream."""
+    _require(buf, torch.uint8, "buf")
+    if out is None:
+        out = torch.empty(max(n, 1), dtype=torch.float32, device=buf.device)
+    _require(out, torch.float32, "out")
+    if out.numel() < n:
+        raise ValueError("out holds fewer than n values")
+    status = torch.zeros(1, dtype=torch.int32, device=buf.device)
+    rc = _lib.lib().dpz_fpz_decode(_ptr(buf), buf.numel(), n, int(precision), _ptr(out),
+                                   _ptr(status), _stream(buf.device))
+    if rc == _lib.DPZ_ERR_ARG:
+        raise ValueError("malformed float stream")
+    if rc == _lib.DPZ_ERR_UNSUPPORTED:
+        raise ValueError("float precision must be 0 (lossless) or 10..32")
+    check(rc, "dpz_fpz_decode")
+    if check_status and int(status.item()) != 0:
+        raise ValueError("malformed float stream")
+    return out[:n]
+
+
 class KernelTimer:
     """Per-kernel device time measured by the library with HIP event pairs on each launch's own
     stream (``dpz_timing_*``).  Launches into a capturing stream are not timed.

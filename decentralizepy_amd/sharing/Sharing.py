@@ -59,7 +59,7 @@ class Sharing:
         self.device = pick_device(rank)
         self.staging = Staging()
         self.workspace = codec.Workspace(self.device)
-        if hasattr(getattr(self, "compressor", None), "compress_device"):
+        if hasattr(getattr(self, "compressor", None), "_dev"):
             self.compressor.device = self.device  # device compressors run on this node's GPU
 
     # ---- wire format -----------------------------------------------------------------------
@@ -73,7 +73,10 @@ class Sharing:
     def decompress_data(self, data, device=False):
         if self.compress:
             if "params" in data:
-                data["params"] = self.compressor.decompress_float(data["params"])
+                if device and hasattr(self.compressor, "decompress_float_device"):
+                    data["params"] = self.compressor.decompress_float_device(data["params"])
+                else:
+                    data["params"] = self.compressor.decompress_float(data["params"])
         return data
 
     def serialized_model(self):
@@ -122,7 +125,10 @@ class Sharing:
 
     def _device_payload(self, data):
         """Received (decompressed) payload dict -> (idx int32 device or None, vals fp32 device)."""
-        vals = torch.from_numpy(np.ascontiguousarray(data["params"], dtype=np.float32))
+        vals = data["params"]
+        if isinstance(vals, torch.Tensor):  # decoded on the device by the compressor
+            return None, vals.to(self.device, torch.float32).reshape(-1)
+        vals = torch.from_numpy(np.ascontiguousarray(vals, dtype=np.float32))
         return None, vals.to(self.device, non_blocking=True)
 
     def _pop_payloads(self, peer_deques):

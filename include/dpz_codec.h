@@ -280,7 +280,8 @@ enum {
   DPZ_KT_EXACT_WRITE, DPZ_KT_ACCUMULATE,
   DPZ_KT_FOLD_OFFSETS, DPZ_KT_FOLD, DPZ_KT_DWT, DPZ_KT_IDWT, DPZ_KT_ELIAS_COUNT,
   DPZ_KT_ELIAS_SCAN, DPZ_KT_ELIAS_PACK, DPZ_KT_ELIAS_SPEC, DPZ_KT_ELIAS_RESOLVE,
-  DPZ_KT_ELIAS_WRITE, DPZ_KT_FP16, DPZ_KT_SCATTER, DPZ_KT_COUNT
+  DPZ_KT_ELIAS_WRITE, DPZ_KT_FP16, DPZ_KT_SCATTER, DPZ_KT_FPZ_SIZE, DPZ_KT_FPZ_SCAN,
+  DPZ_KT_FPZ_PACK, DPZ_KT_FPZ_DECODE, DPZ_KT_COUNT
 };
 int dpz_timing_enable(int on);  /* also clears the accumulators */
 int dpz_timing_read(double* ms_sum, int64_t* count, int max_ids);
@@ -310,6 +311,29 @@ int dpz_elias_encode(const int32_t* idx, int64_t k, uint8_t* out, int64_t out_ca
 int dpz_elias_decode(const uint8_t* in, int64_t nbytes, int64_t nbits, int64_t first,
                      int64_t* out64, int32_t* out32, int64_t out_cap, int64_t* count_host,
                      void* ws, size_t ws_bytes, dpz_stream_t stream);
+
+/* ---- Block-floating fp32 value coding (the float leg of EliasFpzip / EliasFpzipLossy) --------
+ * Replaces compression/EliasFpzip.py:19-51 (fpzip.compress, precision 0) and
+ * compression/EliasFpzipLossy.py:14-58 (precision p).  fpzip is absent, so the bytes are this
+ * build's own format (csrc/dpz_fpz.hip): precision 0 (or >= 32) is lossless for every bit pattern;
+ * 1 <= p < 32 keeps the top p bits of each value's bit pattern (the rest truncated; from p = 10 on
+ * a NaN stays a NaN); p < 0 returns DPZ_ERR_UNSUPPORTED.  Stream: 16-byte header ('DPFZ', n, precision, nblk), a table of
+ * nblk + 1 block offsets, then per 256 values a meta word and sign / exponent / mantissa planes. */
+
+/* Upper bound of the stream size for n values (every block at full exponent width). */
+int64_t dpz_fpz_max_bytes(int64_t n);
+/* Device workspace for an encode of n values. */
+size_t dpz_fpz_workspace_bytes(int64_t n);
+/* x: device fp32[n] (n <= 2^30); out: device buffer, 4-byte aligned, out_cap >=
+ * dpz_fpz_max_bytes(n).  Writes the stream, its length to *nbytes_host (host; synchronises).   */
+int dpz_fpz_encode(const float* x, int64_t n, int precision, uint8_t* out, int64_t out_cap,
+                   int64_t* nbytes_host, void* ws, size_t ws_bytes, dpz_stream_t stream);
+/* in: device copy of a stream of nbytes (a multiple of 4, 4-byte aligned); n and precision from
+ * its header (the caller holds the bytes).  Writes out[n]; asynchronous.  Every block is checked
+ * against the header, the offset table and the buffer bounds: a malformed block is not decoded
+ * and sets *status (device uint32, OR-ed) to nonzero; the caller reads it after the stream.   */
+int dpz_fpz_decode(const uint8_t* in, int64_t nbytes, int64_t n, int precision, float* out,
+                   uint32_t* status, dpz_stream_t stream);
 
 #ifdef __cplusplus
 }

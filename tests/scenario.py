@@ -226,13 +226,14 @@ def get_flat(model):
 def _elias_wire(msgs, check_cls):
     """Neighbour messages as an Elias(-Fpzip) sender puts them on the wire (oracle encoder)."""
     from oracle import elias as oelias
+    from oracle import fpz as ofpz
     out = []
     for m in msgs:
         m = dict(m)
         if "indices" in m:
             m["indices"] = oelias.encode(m["indices"])
         if check_cls == "EliasFpzip" and "params" in m:
-            m["params"] = np.ascontiguousarray(m["params"], np.float32).view(np.uint8).copy()
+            m["params"] = ofpz.encode(m["params"], 0)
         out.append(m)
     return out
 
@@ -273,6 +274,10 @@ def replay_plugin(name, tmpdir, compression_class=None, config=None):
             if "indices" in data:
                 np.testing.assert_array_equal(np.asarray(data["indices"]),
                                               oelias.encode(arrays[f"r{r}_indices"]))
+            if compression_class == "EliasFpzip" and "params" in data:
+                from oracle import fpz as ofpz
+                np.testing.assert_array_equal(np.asarray(data["params"]),
+                                              ofpz.encode(arrays[f"r{r}_params"], 0))
             data = plugin.decompress_data(data)
         acc = getattr(model, "accumulated_changes", None)
         got = {"payload": data, "counter_enc": model.shared_parameters_counter.numpy().copy(),

@@ -76,12 +76,46 @@ def test_compression_surface_and_trailer():
     # trailer of the SURVEY.md §8a known-answer stream
     kat = bytes.fromhex("520003000000000000008900000000000000")
     assert parse_trailer(kat) == (137, 3)
-    x = np.random.default_rng(0).standard_normal(33).astype(np.float32)
-    f = EliasFpzip(float_precision=None)
-    np.testing.assert_array_equal(f.decompress_float(f.compress_float(x)).view(np.uint32),
-                                  x.view(np.uint32))
     for cls in (Elias, EliasFpzip):
         assert issubclass(cls, Compression)
+
+
+def test_float_compressor_surface():
+    """EliasFpzip / EliasFpzipLossy constructor surface (reference compression/EliasFpzip.py:14,
+    EliasFpzipLossy.py:14: float_precision=16 default; the plugins pass None when a config names
+    none) and the host-side header parse, on an oracle-made stream (no GPU needed)."""
+    import numpy as np
+
+    from decentralizepy_amd.compression.EliasFpzip import EliasFpzip, parse_float_header
+    from decentralizepy_amd.compression.EliasFpzipLossy import EliasFpzipLossy
+    from oracle import fpz as ofpz
+    assert EliasFpzip(float_precision=None).precision == 0
+    assert EliasFpzipLossy().precision == 16
+    assert EliasFpzipLossy(float_precision=None).precision == 16
+    assert EliasFpzipLossy(float_precision=8).float_precision == 8
+    with pytest.raises(ValueError):
+        EliasFpzipLossy(float_precision=-1)
+    x = np.random.default_rng(0).standard_normal(1000).astype(np.float32)
+    assert parse_float_header(ofpz.encode(x, 16)) == (1000, 16)
+    assert parse_float_header(ofpz.encode(x, 0)) == (1000, 32)
+    with pytest.raises(ValueError):
+        parse_float_header(ofpz.encode(x, 0)[:-8][:20])
+    with pytest.raises(ValueError):
+        parse_float_header(x.view(np.uint8))
+    import inspect
+
+    from decentralizepy_amd.sharing.STC import STC
+    assert inspect.signature(STC).parameters["compression_package"].default == \
+        "decentralizepy_amd.compression.EliasFpzipLossy"
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure mode")
+def test_float_compressor_fails_loudly_without_gpu():
+    import numpy as np
+
+    from decentralizepy_amd.compression.EliasFpzip import EliasFpzip
+    with pytest.raises(RuntimeError, match="no CPU path|CPU fallback"):
+        EliasFpzip().compress_float(np.ones(4, np.float32))
 
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure mode")
