@@ -31,6 +31,7 @@ DPZ_BATCH_DECODE = 0x2
 DPZ_EW_SUB = 1
 DPZ_EW_ADD = 2
 DPZ_EW_CHOCO = 3
+DPZ_EW_MHCOMBINE = 4
 DPZ_OK = 0
 DPZ_ERR_ARG = 1001
 DPZ_ERR_WORKSPACE = 1002

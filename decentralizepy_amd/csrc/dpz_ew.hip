@@ -5,6 +5,8 @@
 //   :73-97    self_add_state_dict             x_hat += 1.0 * q
 //   :117-140  topk_sparsification_tensor      q[|q| < T] = 0   (T from dpz_topk_threshold)
 //   :441-447  x = x + step_size * (s - x_hat)
+// and the owner-side combine of the over-HBM gossip round (decentralizepy_amd/gossip.py,
+// reduce-scatter exchange): x_new = x * (c - B) + A.
 // One fp32 rounding per operation (-ffp-contract=off), grid-stride, float4 where aligned.
 #include "dpz_common.h"
 #include "dpz_topk.h"
@@ -15,6 +17,11 @@ template <int OP>
 __device__ __forceinline__ float ew(float a, float b, float d, float c) {
   if (OP == DPZ_EW_SUB) return a - b;
   if (OP == DPZ_EW_ADD) return a + b;
+  if (OP == DPZ_EW_MHCOMBINE) {  // x * (c - hit weight) + weighted hit sum
+    const float keep = c - b;
+    const float base = a * keep;
+    return base + d;
+  }
   const float diff = b - d;  // s - x_hat
   const float step = c * diff;
   return a + step;
@@ -30,16 +37,16 @@ __global__ void __launch_bounds__(256) ew_kernel(const float* a, const float* b,
       const float4 av = reinterpret_cast<const float4*>(a)[g];
       const float4 bv = reinterpret_cast<const float4*>(b)[g];
       float4 dv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (OP == DPZ_EW_CHOCO) dv = reinterpret_cast<const float4*>(d)[g];
+      if (OP == DPZ_EW_CHOCO || OP == DPZ_EW_MHCOMBINE) dv = reinterpret_cast<const float4*>(d)[g];
       reinterpret_cast<float4*>(out)[g] =
           make_float4(ew<OP>(av.x, bv.x, dv.x, c), ew<OP>(av.y, bv.y, dv.y, c),
                       ew<OP>(av.z, bv.z, dv.z, c), ew<OP>(av.w, bv.w, dv.w, c));
     }
     for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
-      out[i] = ew<OP>(a[i], b[i], OP == DPZ_EW_CHOCO ? d[i] : 0.f, c);
+      out[i] = ew<OP>(a[i], b[i], (OP == DPZ_EW_CHOCO || OP == DPZ_EW_MHCOMBINE) ? d[i] : 0.f, c);
   } else {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
-      out[i] = ew<OP>(a[i], b[i], OP == DPZ_EW_CHOCO ? d[i] : 0.f, c);
+      out[i] = ew<OP>(a[i], b[i], (OP == DPZ_EW_CHOCO || OP == DPZ_EW_MHCOMBINE) ? d[i] : 0.f, c);
   }
 }
 
@@ -68,13 +75,15 @@ extern "C" int dpz_elementwise(int op, const float* a, const float* b, const flo
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (n < 0) return DPZ_ERR_ARG;
   if (n == 0) return DPZ_OK;
-  if (!a || !b || !out || (op == DPZ_EW_CHOCO && !d)) return DPZ_ERR_ARG;
-  const int vec = aligned16(a) && aligned16(b) && aligned16(out) && (op != DPZ_EW_CHOCO || aligned16(d));
+  const bool use_d = op == DPZ_EW_CHOCO || op == DPZ_EW_MHCOMBINE;
+  if (!a || !b || !out || (use_d && !d)) return DPZ_ERR_ARG;
+  const int vec = aligned16(a) && aligned16(b) && aligned16(out) && (!use_d || aligned16(d));
   const unsigned g = ew_grid(n);
   switch (op) {
     case DPZ_EW_SUB: ew_kernel<DPZ_EW_SUB><<<g, 256, 0, st>>>(a, b, d, c, n, out, vec); break;
     case DPZ_EW_ADD: ew_kernel<DPZ_EW_ADD><<<g, 256, 0, st>>>(a, b, d, c, n, out, vec); break;
     case DPZ_EW_CHOCO: ew_kernel<DPZ_EW_CHOCO><<<g, 256, 0, st>>>(a, b, d, c, n, out, vec); break;
+    case DPZ_EW_MHCOMBINE: ew_kernel<DPZ_EW_MHCOMBINE><<<g, 256, 0, st>>>(a, b, d, c, n, out, vec); break;
     default: return DPZ_ERR_ARG;
   }
   DPZ_LAUNCH_CHECK();

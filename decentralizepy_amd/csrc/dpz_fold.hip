@@ -42,6 +42,7 @@ constexpr int FOLD_MAXP = 16;  // payloads per launch (longer lists are chained)
 constexpr int FOLD_THREADS = DPZ_FOLD_THREADS;
 constexpr int FOLD_GROUPS = FOLD_TILE / (4 * FOLD_THREADS);  // float4 groups per thread
 constexpr int FOLD_EQ = 4;  // payload entries per thread preloaded at tile start
+constexpr int FOLD_POOL = 64;  // hit-chain path: elements hit by >= 3 payloads folded from LDS rows
 constexpr int FOLD_NB = 4;  // phase path: next payload's extra entries per thread prefetched
 // hit-chain path: per-element chain head (u32) + per-entry value and (next | payload << 16),
 // the tile's local values and the distinct-hit list: 61 KB of LDS at 2816 entries (2 blocks of
@@ -122,6 +123,17 @@ __device__ __forceinline__ void fold_term(float& acc, float tv, float w, bool fi
   }
 }
 
+#ifdef DPZ_STAMPS  // diagnostic build only: per (block, tile iteration) phase stamps
+__device__ unsigned long long g_fold_st[6][8192];
+#define FSTAMP(i)                                                    \
+  do {                                                               \
+    if (threadIdx.x == 0 && it_ < 16 && blockIdx.x < 512)            \
+      g_fold_st[i][blockIdx.x * 16 + it_] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define FSTAMP(i) do {} while (0)
+#endif
+
 template <bool VEC>
 __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
   // phase path: hv (value tile) + htag (payload tag); hit-mask path: msk + epos + ev
@@ -136,6 +148,8 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
   __shared__ const int32_t* s_idx[FOLD_MAXP];
   __shared__ const float* s_val[FOLD_MAXP];
   __shared__ uint32_t s_nhit;
+  __shared__ uint32_t s_pool_n;                // rows of s_pool taken in this tile
+  __shared__ float s_pool[FOLD_POOL][FOLD_MAXP];  // payload values of elements hit >= 3 times
   __shared__ float s_w[FOLD_MAXP];
   if (t == 0) {
     for (int p = 0; p < a.np; ++p) {
@@ -153,7 +167,30 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
     nr0 = st[blockIdx.x];
     nr1 = st[blockIdx.x + 1];
   }
+  float L[4 * FOLD_GROUPS];
+  // local values of tile `tl` into L: issued early, consumed a phase later (loads stay in
+  // flight across the plain barriers in between)
+  auto load_local = [&](int64_t tl) {
+    const int64_t lo_ = tl * FOLD_TILE;
+    const int64_t hi_ = (lo_ + FOLD_TILE < a.n) ? lo_ + FOLD_TILE : a.n;
+#pragma unroll
+    for (int q = 0; q < FOLD_GROUPS; ++q) {
+      const int64_t i0 = lo_ + q * 4 * FOLD_THREADS + t * 4;
+      if (VEC && i0 + 3 < hi_) {
+        float4 v = *reinterpret_cast<const float4*>(a.local + i0);
+        L[q * 4 + 0] = v.x; L[q * 4 + 1] = v.y; L[q * 4 + 2] = v.z; L[q * 4 + 3] = v.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) L[q * 4 + e] = i0 + e < hi_ ? a.local[i0 + e] : 0.0f;
+      }
+    }
+  };
+  if ((int64_t)blockIdx.x < a.ntiles) load_local(blockIdx.x);
+  int it_ = -1;
+  (void)it_;
   for (int64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+  ++it_;
+  FSTAMP(0);
   const int64_t tlo = tile * FOLD_TILE;
   const int64_t thi = (tlo + FOLD_TILE < a.n) ? tlo + FOLD_TILE : a.n;
   if (t < 64) {
@@ -178,29 +215,26 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
     nr1 = st[tile + gridDim.x + 1];
   }
 
-  // this thread's elements: q-th group = tlo + q*1024 + 4t .. +3
-  float L[4 * FOLD_GROUPS], acc[4 * FOLD_GROUPS];
+  // this thread's elements: q-th group = tlo + q*1024 + 4t .. +3; L (the local values) was
+  // loaded ahead (prologue, or behind the previous tile's hit fold)
+  float acc[4 * FOLD_GROUPS];
+  if (!a.first) {
 #pragma unroll
-  for (int q = 0; q < FOLD_GROUPS; ++q) {
-    const int64_t i0 = tlo + q * 4 * FOLD_THREADS + t * 4;
-    if (VEC && i0 + 3 < thi) {
-      float4 v = *reinterpret_cast<const float4*>(a.local + i0);
-      L[q * 4 + 0] = v.x; L[q * 4 + 1] = v.y; L[q * 4 + 2] = v.z; L[q * 4 + 3] = v.w;
-      if (!a.first) {
+    for (int q = 0; q < FOLD_GROUPS; ++q) {
+      const int64_t i0 = tlo + q * 4 * FOLD_THREADS + t * 4;
+      if (VEC && i0 + 3 < thi) {
         float4 o = *reinterpret_cast<const float4*>(a.out + i0);
         acc[q * 4 + 0] = o.x; acc[q * 4 + 1] = o.y; acc[q * 4 + 2] = o.z; acc[q * 4 + 3] = o.w;
-      }
-    } else {
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int64_t i = i0 + e;
-        L[q * 4 + e] = i < thi ? a.local[i] : 0.0f;
-        if (!a.first) acc[q * 4 + e] = i < thi ? a.out[i] : 0.0f;
+        for (int e = 0; e < 4; ++e) acc[q * 4 + e] = i0 + e < thi ? a.out[i0 + e] : 0.0f;
       }
     }
   }
+  bool l_ahead = false;  // L already holds the next tile's values
 
   __syncthreads();  // rng / pre visible
+  FSTAMP(1);
   // every payload's entries of this tile (flattened, the first FOLD_EQ * FOLD_THREADS of them)
   // are loaded before any is used: one memory latency per tile instead of one per payload
   int ep[FOLD_EQ];
@@ -244,7 +278,10 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
     for (int q = 0; q < FOLD_GROUPS; ++q)
       *reinterpret_cast<float4*>(&lv[q * 4 * FOLD_THREADS + t * 4]) =
           make_float4(L[q * 4 + 0], L[q * 4 + 1], L[q * 4 + 2], L[q * 4 + 3]);
-    if (t == 0) s_nhit = 0;
+    if (t == 0) {
+      s_nhit = 0;
+      s_pool_n = 0;
+    }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < FOLD_EQ; ++q) {
@@ -275,6 +312,7 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
       }
     }
     __syncthreads();
+    FSTAMP(2);
     // A) base fold of this thread's elements; remember which of them carry hits
     uint32_t hitbits = 0;
 #pragma unroll
@@ -323,52 +361,94 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
         acc[2 * h + 1] = a2[h].y;
       }
     }
+    // L is dead from here on (B and add_self read the LDS copy lv): the next tile's local
+    // values load behind the hit fold and the stores
+    if (tile + gridDim.x < a.ntiles) {
+      load_local(tile + gridDim.x);
+      l_ahead = true;
+    }
     __syncthreads();  // every owner has read its hit flags before B overwrites head[]
-    // B) exact fold of the hit elements, one per thread; the result replaces head[pos]
+    FSTAMP(3);
+    // B) exact fold of the hit elements, two per thread with their chain walks interleaved
+    //    (the walks are dependent LDS reads: one latency for both); the result replaces
+    //    head[pos].  The usual one or two hits of an element fold branch-free; an element with
+    //    three or more (rare) is refolded by the general chain walk.
     const uint32_t nhit = s_nhit;
-    for (uint32_t s = t; s < nhit; s += FOLD_THREADS) {
-      const int pos = hitl[s];
-      const float b = a.zero_base ? 0.0f : lv[pos];
-      float av = a.first ? 0.0f : a.out[tlo + pos];
-      uint32_t p1 = 0xFFFFu, p2 = 0xFFFFu, more = 0xFFFFu;
-      float v1 = 0.0f, v2 = 0.0f;
-      const uint32_t c1 = head[pos] & 0xFFFFu;
-      {
-        const uint32_t m1 = meta[c1];
-        p1 = m1 >> 16;
-        v1 = ev[c1];
-        const uint32_t c2 = m1 & 0xFFFFu;
-        if (c2 != 0xFFFFu) {
-          const uint32_t m2 = meta[c2];
-          p2 = m2 >> 16;
-          v2 = ev[c2];
-          more = m2 & 0xFFFFu;
-        }
-      }
-      // unrolled over the 16 payload slots with the weights read from LDS up front: a rolled
-      // loop waited on one LDS read per payload for every hit element
-      float wr[FOLD_MAXP];
+    float wr[FOLD_MAXP];
 #pragma unroll
-      for (int p = 0; p < FOLD_MAXP; ++p) wr[p] = s_w[p];
+    for (int p = 0; p < FOLD_MAXP; ++p) wr[p] = s_w[p];
+    for (uint32_t s0 = t; s0 < nhit; s0 += 2 * FOLD_THREADS) {
+      const uint32_t s1 = s0 + FOLD_THREADS;
+      const bool two = s1 < nhit;
+      int pos[2];
+      pos[0] = hitl[s0];
+      pos[1] = two ? hitl[s1] : pos[0];
+      float bb[2], av[2], v1[2], v2[2];
+      uint32_t p1[2], p2[2], more[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bb[h] = a.zero_base ? 0.0f : lv[pos[h]];
+        av[h] = a.first ? 0.0f : a.out[tlo + pos[h]];
+        const uint32_t c1 = head[pos[h]] & 0xFFFFu;
+        const uint32_t m1 = meta[c1];
+        p1[h] = m1 >> 16;
+        v1[h] = ev[c1];
+        const uint32_t c2 = m1 & 0xFFFFu;
+        const uint32_t m2 = meta[c2 != 0xFFFFu ? c2 : c1];
+        p2[h] = c2 != 0xFFFFu ? (m2 >> 16) : 0xFFFFu;
+        v2[h] = ev[c2 != 0xFFFFu ? c2 : c1];
+        more[h] = c2 != 0xFFFFu ? (m2 & 0xFFFFu) : 0xFFFFu;
+      }
 #pragma unroll
       for (int p = 0; p < FOLD_MAXP; ++p) {
         if (p >= a.np) break;
-        float tv = ((uint32_t)p == p1) ? v1 : (((uint32_t)p == p2) ? v2 : b);
-        if (more != 0xFFFFu && (uint32_t)p != p1 && (uint32_t)p != p2) {
-          for (uint32_t c = more; c != 0xFFFFu;) {  // a third hit or more (rare)
-            const uint32_t m = meta[c];
-            if ((m >> 16) == (uint32_t)p) {
-              tv = ev[c];
-              break;
-            }
-            c = m & 0xFFFFu;
-          }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float tv = ((uint32_t)p == p1[h]) ? v1[h] : (((uint32_t)p == p2[h]) ? v2[h] : bb[h]);
+          fold_term(av[h], tv, wr[p], a.first && p == 0, a.replace_only, a.zero_base);
         }
-        fold_term(av, tv, wr[p], a.first && p == 0, a.replace_only, a.zero_base);
       }
-      head[pos] = __float_as_uint(av);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (more[h] != 0xFFFFu) {  // three or more hits (rare): walk the chain once into a row
+          float acc = a.first ? 0.0f : a.out[tlo + pos[h]];
+          const uint32_t row = atomicAdd(&s_pool_n, 1u);
+          if (row < FOLD_POOL) {
+            uint32_t mask = 0;
+            for (uint32_t c = head[pos[h]] & 0xFFFFu; c != 0xFFFFu;) {
+              const uint32_t m = meta[c];
+              s_pool[row][m >> 16] = ev[c];
+              mask |= 1u << (m >> 16);
+              c = m & 0xFFFFu;
+            }
+            for (int p = 0; p < a.np; ++p) {
+              const float tv = ((mask >> p) & 1u) ? s_pool[row][p] : bb[h];
+              fold_term(acc, tv, wr[p], a.first && p == 0, a.replace_only, a.zero_base);
+            }
+          } else {  // the pool is full: a walk per payload
+            for (int p = 0; p < a.np; ++p) {
+              float tv = bb[h];
+              for (uint32_t c = head[pos[h]] & 0xFFFFu; c != 0xFFFFu;) {
+                const uint32_t m = meta[c];
+                if ((m >> 16) == (uint32_t)p) {
+                  tv = ev[c];
+                  break;
+                }
+                c = m & 0xFFFFu;
+              }
+              fold_term(acc, tv, wr[p], a.first && p == 0, a.replace_only, a.zero_base);
+            }
+          }
+          av[h] = acc;
+        }
+      }
+      // every hit element's chain head is read above before any result overwrites it: each
+      // element belongs to exactly one (thread, h), and only its own head[pos] is written
+      head[pos[0]] = __float_as_uint(av[0]);
+      if (two) head[pos[1]] = __float_as_uint(av[1]);
     }
     __syncthreads();
+    FSTAMP(4);
     if (hitbits) {
 #pragma unroll
       for (int q = 0; q < FOLD_GROUPS; ++q)
@@ -474,8 +554,20 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
   }
   }  // phase path
   if (a.add_self) {
+    if (l_ahead) {  // hit-chain path: this tile's local values from the LDS copy
+      const float* lv = reinterpret_cast<const float*>(lds_raw) + FOLD_TILE + 2 * FOLD_CAP;
 #pragma unroll
-    for (int e = 0; e < 4 * FOLD_GROUPS; ++e) acc[e] = acc[e] + L[e] * a.w_self;
+      for (int q = 0; q < FOLD_GROUPS; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(&lv[q * 4 * FOLD_THREADS + t * 4]);
+        acc[q * 4 + 0] = acc[q * 4 + 0] + v.x * a.w_self;
+        acc[q * 4 + 1] = acc[q * 4 + 1] + v.y * a.w_self;
+        acc[q * 4 + 2] = acc[q * 4 + 2] + v.z * a.w_self;
+        acc[q * 4 + 3] = acc[q * 4 + 3] + v.w * a.w_self;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4 * FOLD_GROUPS; ++e) acc[e] = acc[e] + L[e] * a.w_self;
+    }
   }
 #pragma unroll
   for (int q = 0; q < FOLD_GROUPS; ++q) {
@@ -494,7 +586,9 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
         }
     }
   }
+  if (!l_ahead && tile + gridDim.x < a.ntiles) load_local(tile + gridDim.x);
   __syncthreads();  // the next tile reuses rng / pre / the LDS tile
+  FSTAMP(5);
   }  // tile loop
 }
 
@@ -536,6 +630,17 @@ int launch_replace(const ReplaceJob& j, hipStream_t st) {
 }  // namespace dpz
 
 using namespace dpz;
+
+#ifdef DPZ_STAMPS
+extern "C" int dpz_debug_fold_stamps(unsigned long long* host_out, int reset) {
+  if (host_out) DPZ_HIP_TRY(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_fold_st), sizeof(g_fold_st)));
+  if (reset) {
+    static unsigned long long zero[6][8192];
+    DPZ_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_fold_st), zero, sizeof(zero)));
+  }
+  return 0;
+}
+#endif
 
 extern "C" size_t dpz_decode_workspace_bytes(int64_t n, int n_payloads) {
   const int64_t np = n_payloads < FOLD_MAXP ? (n_payloads > 0 ? n_payloads : 1) : FOLD_MAXP;

@@ -8,8 +8,19 @@ encode, ``sharing/PartialModel.py:188-255``), sends the dict to each neighbour o
 shards the nodes over the ranks (one process per GPU), and replaces the per-edge sends by ONE
 all-gather of the fixed-size payloads (every node sends the same k): each rank encodes its own
 nodes, ``all_gather_into_tensor`` over RCCL gives every rank every payload (96 x 8k bytes: 84 MB
-at N = 11M), and each rank folds its own nodes' neighbourhoods locally.  No reduce-scatter: the
-96 models fit one GPU's HBM.
+at N = 11M), and each rank folds its own nodes' neighbourhoods locally — bit-exact with the
+reference's per-node fold.
+
+Over-HBM regime (BASELINE.json C4: "RCCL reduce-scatter ... only when a simulated topology's
+payloads exceed one GPU's HBM"): when the all-gathered payload buffers would not fit the rank's
+budget, the payloads are never replicated.  The fold is split by linearity,
+``x_d' = x_d * (w_self + sum_s w_s - B_d) + A_d`` with ``A_d = sum_s w_s * v_s`` and
+``B_d = sum_s w_s`` over the entries of each neighbour payload (zero elsewhere): every rank folds
+the contributions of the payloads it owns into dense (A, B) rows for every destination node
+(batched HIP fold, zero base), one ``reduce_scatter_tensor`` per destination group sums them on
+the owning rank, which combines them with its model (``DPZ_EW_MHCOMBINE``).  Destination groups
+are sized to the budget.  This path reassociates the fp32 sums (RCCL's reduction order), so it
+matches the reference within fp32 tolerance, not bit for bit.
 
 The encode / fold callables are injectable so the sharding and exchange logic can be tested with
 the CPU gloo backend; the defaults are the HIP codec (no CPU fallback).
@@ -59,9 +70,16 @@ class GossipRound:
     """Nodes [lo, hi) of a topology on this rank; ``step()`` runs one full round."""
 
     def __init__(self, adj, x_init, alpha, rank=0, world=1, group=None, encode=None, fold=None,
-                 device=None, streams=3):
+                 device=None, streams=3, exchange="auto", hbm_budget=None, partial=None,
+                 combine=None):
         """adj: adjacency sets of all nodes; x_init: (hi - lo, N) fp32 tensor with this rank's
-        nodes' flat models (device tensor for the HIP codec)."""
+        nodes' flat models (device tensor for the HIP codec).
+
+        exchange: "allgather" (bit-exact), "reduce_scatter" (over-HBM) or "auto" (reduce-scatter
+        when world > 1 and the all-gathered payloads exceed ``hbm_budget`` bytes; default budget:
+        half of the device's free memory at construction).  ``partial(payloads, weights, out)``
+        (zero-based weighted sum of sparse payloads) and ``combine(x, B, A, c, out)`` are
+        injectable like encode / fold (CPU tests); the defaults are the HIP codec."""
         self.adj = adj
         self.n_nodes = len(adj)
         self.rank, self.world, self.group = rank, world, group
@@ -75,10 +93,34 @@ class GossipRound:
         self.counter = torch.zeros_like(self.x, dtype=torch.int32)
         self.send_idx = torch.zeros(self.per, self.k, dtype=torch.int32, device=self.device)
         self.send_val = torch.zeros(self.per, self.k, dtype=torch.float32, device=self.device)
-        self.recv_idx = torch.empty(self.per * world, self.k, dtype=torch.int32,
-                                    device=self.device)
-        self.recv_val = torch.empty(self.per * world, self.k, dtype=torch.float32,
-                                    device=self.device)
+        gathered = self.per * world * self.k * 8
+        if hbm_budget is None:
+            if self.device.type == "cuda":
+                hbm_budget = torch.cuda.mem_get_info(self.device)[0] // 2
+            else:
+                hbm_budget = float("inf")
+        self.hbm_budget = hbm_budget
+        if exchange == "auto":
+            exchange = "reduce_scatter" if world > 1 and gathered > hbm_budget else "allgather"
+        if exchange not in ("allgather", "reduce_scatter"):
+            raise ValueError(f"unknown exchange {exchange!r}")
+        self.exchange_mode = exchange
+        if exchange == "allgather":
+            self.recv_idx = torch.empty(self.per * world, self.k, dtype=torch.int32,
+                                        device=self.device)
+            self.recv_val = torch.empty(self.per * world, self.k, dtype=torch.float32,
+                                        device=self.device)
+        else:
+            self.recv_idx = self.recv_val = None
+            self._partial = partial or self._hip_partial
+            self._combine = combine or self._hip_combine
+            self._ones = torch.ones(self.k, dtype=torch.float32, device=self.device)
+            self._zero_local = torch.zeros(self.N, dtype=torch.float32, device=self.device)
+            # destination nodes per reduce-scatter: send (A, B) rows for `world` ranks plus the
+            # received pair, within the budget
+            row = 4 * self.N
+            g = int(hbm_budget // (2 * row * (world + 1))) if hbm_budget != float("inf") else self.per
+            self.rs_group = max(1, min(self.per, g))
         self.out = torch.empty_like(self.x)
         self.weights = [mh_weights(adj, i) for i in range(self.lo, self.hi)]
         self._encode = encode or self._hip_encode
@@ -151,7 +193,64 @@ class GossipRound:
                               idx_out=self.send_idx[j], val_out=self.send_val[j],
                               workspace=self.wss[0], exact=True)
 
+    def _hip_partial(self, payloads, weights, out):
+        from . import codec
+        # zero base: the local operand only shapes the call (its values never enter the sum)
+        codec.decode_average(self._zero_local, payloads, weights, None, out=out,
+                             workspace=self.wss[0], zero_base=True)
+
+    def _hip_combine(self, x, b, a, c, out):
+        from . import codec
+        from ._lib import DPZ_EW_MHCOMBINE
+        codec.elementwise(DPZ_EW_MHCOMBINE, x, b, a, c, out=out)
+
+    def fold_reduce_scatter(self):
+        """Over-HBM exchange + fold: see the module docstring.  Destination node d of rank r in
+        group [g0, g0 + G) is row r * G + (d - r*per - g0) of this rank's (A, B) send buffers."""
+        import torch.distributed as dist
+        W, per, G, N = self.world, self.per, self.rs_group, self.N
+        mine = set(range(self.lo, self.hi))
+        for g0 in range(0, per, G):
+            gsz = min(G, per - g0)
+            send_a = torch.zeros(W * gsz, N, dtype=torch.float32, device=self.device)
+            send_b = torch.zeros_like(send_a)
+            for r in range(W):
+                for j in range(gsz):
+                    d = r * per + g0 + j
+                    if d >= self.n_nodes:
+                        continue
+                    nbrs, w, _ = mh_weights(self.adj, d)
+                    own = [(q, wq) for q, wq in zip(nbrs, w) if q in mine]
+                    if not own:
+                        continue
+                    row = r * gsz + j
+                    pays = [(self.send_idx[q - self.lo], self.send_val[q - self.lo]) for q, _ in own]
+                    ones = [(self.send_idx[q - self.lo], self._ones) for q, _ in own]
+                    ws_ = [wq for _, wq in own]
+                    self._partial(pays, ws_, send_a[row])
+                    self._partial(ones, ws_, send_b[row])
+            recv_a = torch.empty(gsz, N, dtype=torch.float32, device=self.device)
+            recv_b = torch.empty_like(recv_a)
+            if W > 1:
+                dist.reduce_scatter_tensor(recv_a, send_a, group=self.group)
+                dist.reduce_scatter_tensor(recv_b, send_b, group=self.group)
+            else:
+                recv_a.copy_(send_a)
+                recv_b.copy_(send_b)
+            del send_a, send_b
+            for j in range(gsz):
+                d = self.lo + g0 + j
+                if d >= self.hi:
+                    continue
+                nbrs, w, w_self = self.weights[d - self.lo]
+                c = w_self + sum(w)
+                self._combine(self.x[d - self.lo], recv_b[j], recv_a[j], c, self.out[d - self.lo])
+        self.x0, self.out = self.out, self.x0
+        self.x.copy_(self.x0)
+
     def exchange(self):
+        if self.exchange_mode == "reduce_scatter":
+            return  # folded into fold_reduce_scatter
         if self.world == 1:
             self.recv_idx, self.recv_val = self.send_idx, self.send_val  # no copy on one rank
             return
@@ -222,5 +321,8 @@ class GossipRound:
 
     def step(self):
         self.encode_all()
+        if self.exchange_mode == "reduce_scatter":
+            self.fold_reduce_scatter()
+            return
         self.exchange()
         self.fold_all()

@@ -128,10 +128,13 @@ int dpz_mask_below_threshold(const float* x, int64_t n, const void* ws, float* o
  *   DPZ_EW_SUB   out = a - b
  *   DPZ_EW_ADD   out = a + b
  *   DPZ_EW_CHOCO out = a + c * (b - d)      (x + gamma * (s - x_hat))
+ *   DPZ_EW_MHCOMBINE out = a * (c - b) + d  (the reduce-scatter gossip round's owner combine:
+ *                x * (weight total - hit weights) + weighted hit values, decentralizepy_amd/gossip.py)
  * out may alias a.  c is rounded to fp32 like a torch scalar multiply.                        */
 #define DPZ_EW_SUB 1
 #define DPZ_EW_ADD 2
 #define DPZ_EW_CHOCO 3
+#define DPZ_EW_MHCOMBINE 4
 int dpz_elementwise(int op, const float* a, const float* b, const float* d, float c, int64_t n,
                     float* out, dpz_stream_t stream);
 /* Helpers of the sharded top-k (one tensor split over ranks, decentralizepy_amd/shard.py,

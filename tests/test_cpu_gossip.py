@@ -125,3 +125,71 @@ def test_two_rank_round_equals_single_rank(path, n):
     for rank, lo, xs in got:
         np.testing.assert_array_equal(xs.view(np.uint32),
                                       single.x.numpy()[lo:lo + xs.shape[0]].view(np.uint32))
+
+
+def _torch_partial(payloads, weights, out):
+    out.zero_()
+    for (idx, val), w in zip(payloads, weights):
+        out.index_add_(0, idx.long(), val * torch.tensor(w, dtype=torch.float32))
+
+
+def _torch_combine(x, b, a, c, out):
+    out.copy_(x * (torch.tensor(c, dtype=torch.float32) - b) + a)
+
+
+def _rs_worker(rank, world, port, n, path, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from decentralizepy_amd.gossip import GossipRound, read_edges, shard
+        adj = read_edges(path)
+        x = _models(len(adj), n)
+        lo, hi, per = shard(len(adj), world, rank)
+        k = round(0.05 * n)
+        # an emulated budget one byte below the all-gathered payloads: auto picks the
+        # reduce-scatter, one destination node per group
+        budget = per * world * k * 8 - 1
+        eng = GossipRound(adj, x[lo:hi], 0.05, rank=rank, world=world, encode=_oracle_encode,
+                          fold=_oracle_fold, hbm_budget=budget, partial=_torch_partial,
+                          combine=_torch_combine)
+        assert eng.exchange_mode == "reduce_scatter" and eng.recv_idx is None
+        assert eng.rs_group == 1
+        for r in range(2):
+            _train(eng, r)
+            eng.step()
+        q.put((rank, lo, eng.x.numpy().copy()))
+    except Exception as e:  # noqa: BLE001 - reported to the parent instead of a queue timeout
+        q.put((rank, None, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("path,n", [(EDGES16, 1500), (EDGES96, 600)])
+def test_reduce_scatter_round_matches_within_tolerance(path, n):
+    """The over-HBM exchange (payloads never replicated; dense (A, B) contributions
+    reduce-scattered to the owning rank) reproduces the bit-exact all-gather round within fp32
+    reassociation tolerance, over two rounds (BASELINE.json C4)."""
+    from decentralizepy_amd.gossip import GossipRound, read_edges
+    adj = read_edges(path)
+    x = _models(len(adj), n)
+    single = GossipRound(adj, x, 0.05, encode=_oracle_encode, fold=_oracle_fold)
+    assert single.exchange_mode == "allgather"
+    for r in range(2):
+        _train(single, r)
+        single.step()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_rs_worker, args=(r, 2, port, n, path, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, lo, xs in got:
+        assert lo is not None, xs
+        ref = single.x.numpy()[lo:lo + xs.shape[0]]
+        np.testing.assert_allclose(xs, ref, rtol=1e-5, atol=1e-6)

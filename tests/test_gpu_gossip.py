@@ -26,3 +26,28 @@ def test_gossip_round_device_matches_oracle(dev, path, n, alpha):
         np.testing.assert_array_equal(eng.x.cpu().numpy().view(np.uint32),
                                       ref.x.numpy().view(np.uint32))
         np.testing.assert_array_equal(eng.counter.cpu().numpy(), ref.counter.numpy())
+
+
+@pytest.mark.parametrize("path,n,alpha", [(EDGES16, 200_003, 0.01), (EDGES96, 30_000, 0.05)])
+def test_reduce_scatter_exchange_device_within_tolerance(dev, path, n, alpha):
+    """The over-HBM exchange's device legs — the zero-based batched fold of the owned payloads
+    into dense (A, B) rows and the DPZ_EW_MHCOMBINE owner combine — on one rank (forced mode,
+    budget of one destination node per group), against the bit-exact all-gather round within
+    fp32 reassociation tolerance."""
+    from decentralizepy_amd.gossip import GossipRound, read_edges
+    adj = read_edges(path)
+    x = _models(len(adj), n)
+    exact = GossipRound(adj, x.to(dev), alpha)
+    rs = GossipRound(adj, x.to(dev), alpha, exchange="reduce_scatter", hbm_budget=1)
+    assert rs.exchange_mode == "reduce_scatter" and rs.rs_group == 1
+    for r in range(2):
+        g = torch.Generator().manual_seed(100 + r)
+        noise = (0.01 * torch.randn(len(adj), n, generator=g)).to(dev)
+        exact.x += noise
+        rs.x += noise
+        exact.step()
+        rs.step()
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(rs.x.cpu().numpy(), exact.x.cpu().numpy(), rtol=1e-5,
+                                   atol=1e-6)
+        np.testing.assert_array_equal(rs.counter.cpu().numpy(), exact.counter.cpu().numpy())
