@@ -9,7 +9,8 @@ reference's PartialModel.serialized_model + deserialized_model pair (SURVEY.md ย
 Workload (BASELINE.json configs[1]): N = 11,000,000 (ResNet-18-sized), alpha = 0.01 -> k = 110,000.
 Multi-GPU (torchrun): each rank encodes+decodes its own node's tensor (the gossip round is a set
 of independent per-node codecs: no data-path collective) -> weak scaling; value = all ranks'
-params / max-over-ranks time.
+params / max-over-ranks time.  Beside it, every run times one C4 gossip round of the 96-node
+topology sharded over the ranks, whose payload exchange is an RCCL all-gather ("gossip_round").
 
 Prints ONE JSON line (rank 0).
 """
@@ -37,7 +38,8 @@ def parse():
     p.add_argument("--alpha", type=float, default=0.01)
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--no-extra", action="store_true", help="skip the 64 MiB secondary line")
+    p.add_argument("--no-extra", action="store_true",
+                   help="skip the 64 MiB secondary line and the C4 gossip-round object")
     p.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "e2e", "shard"], default="c2",
                    help="c2: one node's 11M tensor per GPU (default); c4: the 96-node gossip "
                         "round of eval/96_regular.edges sharded over the GPUs; c3: JWINS wavelet "
@@ -251,26 +253,46 @@ def load_pmc(kernel):
     return ent.get("hbm_bytes_per_launch")
 
 
-def cpu_baseline(n, alpha, seconds):
+def _cpu_steps(n, alpha, seconds, threads):
     from oracle import ref_ops
-    g = torch.Generator().manual_seed(0)
-    x = torch.randn(n, generator=g)
-    x0 = x - 0.01 * torch.randn(n, generator=g)
-    counter = torch.zeros(n, dtype=torch.int32)
-    times = []
-    t_start = time.perf_counter()
-    while True:
-        t0 = time.perf_counter()
-        idx, vals = ref_ops.encode(x, x0, alpha, counter)
-        ref_ops.decode(x0, idx, vals)
-        times.append(time.perf_counter() - t0)
-        if len(times) >= 3 and time.perf_counter() - t_start > seconds:
-            break
-    t = sorted(times)[len(times) // 2]
-    return dict(value=4 * n / t / 2 ** 30, unit="GiB/s", cores=torch.get_num_threads(),
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        g = torch.Generator().manual_seed(0)
+        x = torch.randn(n, generator=g)
+        x0 = x - 0.01 * torch.randn(n, generator=g)
+        counter = torch.zeros(n, dtype=torch.int32)
+        times = []
+        t_start = time.perf_counter()
+        while True:
+            t0 = time.perf_counter()
+            idx, vals = ref_ops.encode(x, x0, alpha, counter)
+            ref_ops.decode(x0, idx, vals)
+            times.append(time.perf_counter() - t0)
+            if len(times) >= 3 and time.perf_counter() - t_start > seconds:
+                break
+    finally:
+        torch.set_num_threads(prev)
+    return sorted(times)[len(times) // 2], times
+
+
+def cpu_baseline(n, alpha, seconds):
+    """The reference's CPU op sequence on this box's host cores (SURVEY.md ยง8d): at the process's
+    thread budget (OMP_NUM_THREADS / torch's default: the cores this job may use), and at the
+    per-node share floor(cores / 16) a 16-node machine gives each node process
+    (node/DPSGDNode.py:434-439 sets floor(cores / procs_per_machine))."""
+    cores = torch.get_num_threads()
+    t, times = _cpu_steps(n, alpha, seconds, cores)
+    share = max(1, cores // 16)
+    t1, times1 = _cpu_steps(n, alpha, max(3.0, seconds / 2), share)
+    return dict(value=4 * n / t / 2 ** 30, unit="GiB/s", cores=cores,
                 kind="port",
                 sample=f"reference ATen-CPU op sequence (oracle/ref_ops.py), N={n}, k={round(alpha*n)}, "
-                       f"median of {len(times)} encode+decode steps ({sum(times):.1f} s)")
+                       f"median of {len(times)} encode+decode steps ({sum(times):.1f} s) at "
+                       f"{cores} threads (torch.get_num_threads(), the job's CPU share)",
+                per_node_share={"threads": share, "value": round(4 * n / t1 / 2 ** 30, 4),
+                                "unit": "GiB/s", "steps": len(times1),
+                                "note": "floor(cores / 16): one of 16 node processes per machine"})
 
 
 def main():
@@ -347,6 +369,25 @@ def main():
                  f"{e['streams']}_node_ms_per_step": round(e["s_multi"] * 1e3, 4),
                  "host_enqueue_ms_per_step": round(e["s_host"] * 1e3, 4),
                  "fell_back": e["fell_back"]}
+
+    # the gossip round of BASELINE.json C4 (eval/96_regular.edges) at every N: the nodes are
+    # sharded over the ranks and each round's payloads cross ranks in one RCCL all-gather, so a
+    # multi-GPU run of this bench also times the collective path (strong scaling, 96 nodes fixed)
+    gossip = None
+    if not args.no_extra:
+        gr = gossip_case(args.n, args.alpha, dev, rank, world, dist, rounds=5, warmup=2)
+        gossip = {"workload": "C4: one gossip round of eval/96_regular.edges (96 nodes, 190 "
+                              "edges): every node top-k encodes, payloads all-gathered over RCCL, "
+                              "every node MH-folds its neighbours' payloads",
+                  "value": round(gr["value"], 3), "unit": "GiB/s",
+                  "ms_per_round": round(gr["s_step"] * 1e3, 4), "scaling": "strong",
+                  "parallelism": f"{gr['nodes']} nodes sharded over {world} GPU(s), "
+                                 + ("one RCCL all-gather of the payloads per round" if world > 1
+                                    else "no collective on one GPU"),
+                  "round_alg_bytes": gr["alg_bytes"],
+                  "round_frac_of_hbm_peak": round(gr["alg_bytes"] / gr["s_step"] / 1e9
+                                                  / HBM_PEAK_GBS / world, 4)}
+        torch.cuda.empty_cache()
 
     copy_gbs = None
     if rank == 0:  # context: what a plain device-to-device copy reaches on this box
@@ -437,6 +478,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "secondary": extra,
+            "gossip_round": gossip,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
