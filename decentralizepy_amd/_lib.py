@@ -113,6 +113,17 @@ SIGNATURES = {
     "dpz_fpz_encode": (_int, [_c_void_p, _i64, _int, _c_void_p, _i64, ctypes.POINTER(_i64),
                               _c_void_p, _size, _c_void_p]),
     "dpz_fpz_decode": (_int, [_c_void_p, _i64, _i64, _int, _c_void_p, _c_void_p, _c_void_p]),
+    "dpz_fft_workspace_bytes": (_i64, [_i64]),
+    "dpz_rfft": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p, _size, _c_void_p]),
+    "dpz_irfft": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p, _size, _c_void_p]),
+    "dpz_cplx_key": (_int, [_c_void_p, _c_void_p, _int, _i64, _c_void_p, _c_void_p]),
+    "dpz_cplx_gather": (_int, [_c_void_p, _i64, _c_void_p, _i64, _c_void_p, _c_void_p,
+                               _c_void_p]),
+    "dpz_cplx_pair_indices": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
+    "dpz_haar_wavedec_len": (_i64, [_i64, _int]),
+    "dpz_dwt_haar": (_int, [_c_void_p, _c_void_p, _i64, _int, _c_void_p, _c_void_p, _int,
+                            _c_void_p]),
+    "dpz_idwt_haar": (_int, [_c_void_p, _i64, _int, _c_void_p, _c_void_p]),
 }
 
 _lib = None

@@ -19,7 +19,8 @@ __all__ = ["DPZ_ACC_NONE", "DPZ_ACC_ACCUMULATE", "DPZ_ACC_ADD", "DPZ_EW_SUB", "D
            "topk_threshold", "mask_below_threshold", "elementwise",
            "topk_complete", "decode_average", "replace", "wavedec_len", "wavedec", "waverec",
            "pack_fp16", "unpack_fp16", "elias_encode", "elias_decode",
-           "KernelTimer", "NodeStepBatch", "topk_sticky_status"]
+           "KernelTimer", "NodeStepBatch", "topk_sticky_status", "rfft", "irfft", "cplx_key",
+           "cplx_gather", "cplx_pair_indices"]
 
 
 def _ptr(t):
@@ -330,15 +331,27 @@ def replace(local, idx, vals, out=None, workspace=None):
     return decode_average(local, [(idx, vals)], out=out, replace_only=True, workspace=workspace)
 
 
-def wavedec_len(n, level=4):
-    m = int(_lib.lib().dpz_wavedec_len(int(n), int(level)))
+WAVELETS = ("sym2", "haar")
+
+
+def _check_wavelet(wavelet):
+    if wavelet not in WAVELETS:
+        raise NotImplementedError(f"wavelet '{wavelet}': the device kernels implement {WAVELETS}")
+
+
+def wavedec_len(n, level=4, wavelet="sym2"):
+    _check_wavelet(wavelet)
+    fn = _lib.lib().dpz_wavedec_len if wavelet == "sym2" else _lib.lib().dpz_haar_wavedec_len
+    m = int(fn(int(n), int(level)))
     if m < 0:
-        raise ValueError(f"sym2 level-{level} wavedec unsupported for n={n}")
+        raise ValueError(f"{wavelet} level-{level} wavedec unsupported for n={n}")
     return m
 
 
-def wavedec(x, level=4, x0=None, want_x=True, coeffs_x=None, coeffs_diff=None, accumulate=False):
-    """sym2 multilevel DWT as one ``coeffs_to_array`` vector (reference Wavelet.py:12-32).
+def wavedec(x, level=4, x0=None, want_x=True, coeffs_x=None, coeffs_diff=None, accumulate=False,
+            wavelet="sym2"):
+    """Multilevel DWT (``wavelet`` "sym2" or "haar", mode "symmetric") as one
+    ``coeffs_to_array`` vector (reference Wavelet.py:12-32).
 
     Returns ``(W(x) or None, W(x - x0) or None)``; with ``accumulate=True`` adds W(x - x0) into
     ``coeffs_diff`` instead of overwriting it.
@@ -346,28 +359,41 @@ def wavedec(x, level=4, x0=None, want_x=True, coeffs_x=None, coeffs_diff=None, a
     _require(x, torch.float32, "x")
     _require(x0, torch.float32, "x0")
     n = x.numel()
-    m = wavedec_len(n, level)
+    m = wavedec_len(n, level, wavelet)
     if want_x and coeffs_x is None:
         coeffs_x = torch.empty(m, dtype=torch.float32, device=x.device)
     if x0 is not None and coeffs_diff is None:
         if accumulate:
             raise ValueError("accumulate needs coeffs_diff")
         coeffs_diff = torch.empty(m, dtype=torch.float32, device=x.device)
-    rc = _lib.lib().dpz_dwt_sym2(_ptr(x), _ptr(x0), n, int(level),
-                                 _ptr(coeffs_x if want_x else None),
-                                 _ptr(coeffs_diff if x0 is not None else None),
-                                 1 if accumulate else 0, _stream(x.device))
-    check(rc, "dpz_dwt_sym2")
+    for t, nm in ((coeffs_x if want_x else None, "coeffs_x"),
+                  (coeffs_diff if x0 is not None else None, "coeffs_diff")):
+        _require(t, torch.float32, nm)
+        if t is not None and t.numel() != m:
+            raise ValueError(f"{nm} must hold wavedec_len(n, level) = {m} values")
+    if x0 is not None and x0.numel() != n:
+        raise ValueError("x0 must match x")
+    fn = _lib.lib().dpz_dwt_sym2 if wavelet == "sym2" else _lib.lib().dpz_dwt_haar
+    rc = fn(_ptr(x), _ptr(x0), n, int(level), _ptr(coeffs_x if want_x else None),
+            _ptr(coeffs_diff if x0 is not None else None), 1 if accumulate else 0,
+            _stream(x.device))
+    check(rc, f"dpz_dwt_{wavelet}")
     return (coeffs_x if want_x else None), (coeffs_diff if x0 is not None else None)
 
 
-def waverec(coeffs, n, level=4, out=None):
-    """sym2 multilevel IDWT, first n outputs (reference Wavelet.py:311-316)."""
+def waverec(coeffs, n, level=4, out=None, wavelet="sym2"):
+    """Multilevel IDWT ("sym2" or "haar"), first n outputs (reference Wavelet.py:311-316)."""
     _require(coeffs, torch.float32, "coeffs")
+    if coeffs.numel() != wavedec_len(n, level, wavelet):
+        raise ValueError("coeffs must hold wavedec_len(n, level) values")
     if out is None:
         out = torch.empty(int(n), dtype=torch.float32, device=coeffs.device)
-    rc = _lib.lib().dpz_idwt_sym2(_ptr(coeffs), int(n), int(level), _ptr(out), _stream(coeffs.device))
-    check(rc, "dpz_idwt_sym2")
+    _require(out, torch.float32, "out")
+    if out.numel() < int(n):
+        raise ValueError("out must hold n values")
+    fn = _lib.lib().dpz_idwt_sym2 if wavelet == "sym2" else _lib.lib().dpz_idwt_haar
+    rc = fn(_ptr(coeffs), int(n), int(level), _ptr(out), _stream(coeffs.device))
+    check(rc, f"dpz_idwt_{wavelet}")
     return out
 
 
@@ -493,6 +519,93 @@ def fpz_decode(buf, n, precision, out=None, check_status=True):
     if check_status and int(status.item()) != 0:
         raise ValueError("malformed float stream")
     return out[:n]
+
+
+def _fft_ws(n, workspace, device):
+    need = int(_lib.lib().dpz_fft_workspace_bytes(int(n)))
+    if need < 0:
+        raise ValueError(f"real FFT of n={n} unsupported (2 <= n < 2**31)")
+    workspace = workspace or Workspace(device)
+    buf = getattr(workspace, "fbuf", None)
+    if buf is None or buf.numel() < max(need, 256):
+        buf = workspace.fbuf = torch.empty(max(need, 256), dtype=torch.uint8, device=device)
+    return buf
+
+
+def rfft(x, out=None, workspace=None):
+    """``torch.fft.rfft(x)`` of a device fp32 vector through hipFFT (reference
+    sharing/JWINS/FFT.py:12-25); returns complex64[n // 2 + 1]."""
+    _require(x, torch.float32, "x")
+    n = x.numel()
+    if out is None:
+        out = torch.empty(n // 2 + 1, dtype=torch.complex64, device=x.device)
+    _require(out, torch.complex64, "out")
+    if out.numel() != n // 2 + 1:
+        raise ValueError("out must hold n // 2 + 1 complex values")
+    ws = _fft_ws(n, workspace, x.device)
+    rc = _lib.lib().dpz_rfft(_ptr(x), n, _ptr(out), _ptr(ws), ws.numel(), _stream(x.device))
+    check(rc, "dpz_rfft")
+    return out
+
+
+def irfft(coeffs, n, out=None, workspace=None):
+    """``torch.fft.irfft(coeffs, n)`` (1/n normalisation; reference sharing/JWINS/FFT.py:301).
+    ``coeffs`` (complex64[n // 2 + 1]) is overwritten."""
+    _require(coeffs, torch.complex64, "coeffs")
+    n = int(n)
+    if coeffs.numel() != n // 2 + 1:
+        raise ValueError("coeffs must hold n // 2 + 1 complex values")
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=coeffs.device)
+    _require(out, torch.float32, "out")
+    ws = _fft_ws(n, workspace, coeffs.device)
+    rc = _lib.lib().dpz_irfft(_ptr(coeffs), n, _ptr(out), _ptr(ws), ws.numel(),
+                              _stream(coeffs.device))
+    check(rc, "dpz_irfft")
+    return out
+
+
+def cplx_key(change, acc=None, acc_mode=DPZ_ACC_NONE, out=None):
+    """fp32 |change| of a complex64 change vector after the DPZ_ACC_* accumulation step
+    (reference PartialModel.py:315-329 + FFT.py:143-149)."""
+    _require(change, torch.complex64, "change")
+    _require(acc, torch.complex64, "acc")
+    m = change.numel()
+    if acc is not None and acc.numel() != m:
+        raise ValueError("acc must match the change length")
+    if out is None:
+        out = torch.empty(m, dtype=torch.float32, device=change.device)
+    _require(out, torch.float32, "out")
+    rc = _lib.lib().dpz_cplx_key(_ptr(change), _ptr(acc), int(acc_mode), m, _ptr(out),
+                                 _stream(change.device))
+    check(rc, "dpz_cplx_key")
+    return out
+
+
+def cplx_gather(src, idx, acc=None, out=None):
+    """``src[idx]`` of a complex64 vector; zeroes ``acc[idx]`` when given (Model.py:53-64)."""
+    _require(src, torch.complex64, "src")
+    _require(idx, torch.int32, "idx")
+    _require(acc, torch.complex64, "acc")
+    if out is None:
+        out = torch.empty(idx.numel(), dtype=torch.complex64, device=src.device)
+    _require(out, torch.complex64, "out")
+    rc = _lib.lib().dpz_cplx_gather(_ptr(src), src.numel(), _ptr(idx), idx.numel(), _ptr(out),
+                                    _ptr(acc), _stream(src.device))
+    check(rc, "dpz_cplx_gather")
+    return out
+
+
+def cplx_pair_indices(idx, out=None):
+    """int32[2k] ``(2 i, 2 i + 1)`` per index: a complex payload as a payload of the float view."""
+    _require(idx, torch.int32, "idx")
+    k = idx.numel()
+    if out is None:
+        out = torch.empty(2 * k, dtype=torch.int32, device=idx.device)
+    _require(out, torch.int32, "out")
+    rc = _lib.lib().dpz_cplx_pair_indices(_ptr(idx), k, _ptr(out), _stream(idx.device))
+    check(rc, "dpz_cplx_pair_indices")
+    return out
 
 
 class KernelTimer:

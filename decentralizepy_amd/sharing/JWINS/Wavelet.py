@@ -14,8 +14,9 @@ Device path per round (all HIP kernels, fp32, pywt-1.1.1-exact summation order):
              multilevel IDWT launch (Wavelet.py:269-329)
   post-step  acc += W(x_new - prev) as one accumulating DWT launch (PartialModel.py:346-349)
 
-Only ``wavelet="sym2"`` and ``level <= 4`` (the configuration of every shipped JWINS config,
-e.g. tutorial/JWINS/config.ini) have device kernels; other wavelets raise NotImplementedError.
+Device kernels exist for ``wavelet="sym2"`` with ``level <= 4`` (every shipped JWINS config, e.g.
+tutorial/JWINS/config.ini) and for the reference's default ``wavelet="haar"`` with ``level <= 8``;
+other wavelets raise NotImplementedError.
 """
 import numpy as np
 import torch
@@ -25,14 +26,18 @@ from ..._device import to_host
 from ...utils import identity
 from ..PartialModel import PartialModel
 
-SUPPORTED_WAVELETS = ("sym2",)
+SUPPORTED_WAVELETS = ("sym2", "haar")
+MAX_LEVEL = {"sym2": 4, "haar": 8}
+FILTER_LEN = {"sym2": 4, "haar": 2}
 
 
-def coeff_slices(n, level):
-    """``pywt.coeffs_to_array`` slices of a 1-D ``wavedec`` (array layout [cA_L, cD_L..cD_1])."""
+def coeff_slices(n, level, wavelet="sym2"):
+    """``pywt.coeffs_to_array`` slices of a 1-D ``wavedec`` (array layout [cA_L, cD_L..cD_1]);
+    level lengths floor((len + filter_len - 1) / 2) (pywt.dwt_coeff_len, mode symmetric)."""
+    f = FILTER_LEN[wavelet]
     lens = [int(n)]
     for _ in range(level):
-        lens.append((lens[-1] + 3) // 2)
+        lens.append((lens[-1] + f - 1) // 2)
     slices = [slice(0, lens[level])]
     pos = lens[level]
     for lvl in range(level, 0, -1):
@@ -54,14 +59,15 @@ class Wavelet(PartialModel):
         if wavelet not in SUPPORTED_WAVELETS:
             raise NotImplementedError(
                 f"wavelet '{wavelet}': the device DWT kernels implement {SUPPORTED_WAVELETS}")
-        if not 1 <= self.level <= 4:
-            raise NotImplementedError("the device DWT kernels implement levels 1..4")
+        if not 1 <= self.level <= MAX_LEVEL[wavelet]:
+            raise NotImplementedError(
+                f"the device {wavelet} DWT kernels implement levels 1..{MAX_LEVEL[wavelet]}")
         super().__init__(rank, machine_id, communication, mapping, graph, model, dataset, log_dir,
                          alpha, dict_ordered, save_shared, metadata_cap, accumulation,
                          save_accumulated, identity, accumulate_averaging_changes, compress,
                          compression_package, compression_class)
         self.change_based_selection = change_based_selection
-        slices, m = coeff_slices(self.number_of_params, self.level)
+        slices, m = coeff_slices(self.number_of_params, self.level, self.wavelet)
         self.wt_shape = (m,)
         self.coeff_slices = slices
 
@@ -70,11 +76,11 @@ class Wavelet(PartialModel):
         pass
 
     def _transformed_len(self):
-        return codec.wavedec_len(self.number_of_params, self.level)
+        return codec.wavedec_len(self.number_of_params, self.level, self.wavelet)
 
     def _transform_pre_step(self, x):
         """W(x), W(x - init) in one DWT launch."""
-        return codec.wavedec(x, self.level, x0=self.init_model)
+        return codec.wavedec(x, self.level, x0=self.init_model, wavelet=self.wavelet)
 
     def _encode(self, k):
         acc = self.model.accumulated_changes if self.accumulation else None
@@ -110,7 +116,8 @@ class Wavelet(PartialModel):
     def _accumulate_change(self, new, prev):
         """acc += W(new - prev) (reference PartialModel.py:346-349 with T = wavelet)."""
         codec.wavedec(new, self.level, x0=prev, want_x=False,
-                      coeffs_diff=self.model.accumulated_changes, accumulate=True)
+                      coeffs_diff=self.model.accumulated_changes, accumulate=True,
+                      wavelet=self.wavelet)
 
     # ---- receive side -------------------------------------------------------------------------
     def deserialized_model(self, m):
@@ -139,7 +146,7 @@ class Wavelet(PartialModel):
                 weight_total += w
             w_self = 1 - weight_total
         total = self._fold(self.pre_share_model_transformed, payloads, weights, w_self)
-        return codec.waverec(total, self.number_of_params, self.level)
+        return codec.waverec(total, self.number_of_params, self.level, wavelet=self.wavelet)
 
     def _averaging(self, peer_deques):
         """reference Wavelet.py:269-329: fold in the wavelet domain, then waverec."""

@@ -51,10 +51,11 @@ class PartialModel(Sharing):
         self.save_accumulated = conditional_value(save_accumulated, "", False)
         self.change_transformer = change_transformer
         self.accumulate_averaging_changes = accumulate_averaging_changes
-        if self.save_accumulated:
-            raise NotImplementedError(
-                "save_accumulated (per-round JSON dumps of the full change vector) is not "
-                "supported by the device codec")
+        if self.save_accumulated:  # reference PartialModel.py:122-131
+            self.model_change_path = os.path.join(self.log_dir, "model_change/{}".format(self.rank))
+            Path(self.model_change_path).mkdir(parents=True, exist_ok=True)
+            self.model_val_path = os.path.join(self.log_dir, "model_val/{}".format(self.rank))
+            Path(self.model_val_path).mkdir(parents=True, exist_ok=True)
         self._check_transformer()
 
         with torch.no_grad():
@@ -242,6 +243,23 @@ class PartialModel(Sharing):
                     self._accumulate_change(self.init_model, self.prev)
                 self.prev = self.init_model
             self.model.model_change = None
+        if self.save_accumulated:
+            self.save_change()
+
+    def save_vector(self, v, s):
+        """reference PartialModel.py:355-383: {order, shapes, tensor} as JSON per round."""
+        output_dict = dict()
+        output_dict["order"] = list(self.model.state_dict().keys())
+        output_dict["shapes"] = {k: list(v1.shape) for k, v1 in self.model.state_dict().items()}
+        output_dict["tensor"] = v.tolist()
+        with open(os.path.join(s, "{}.json".format(self.communication_round + 1)), "w") as of:
+            json.dump(output_dict, of)
+
+    def save_change(self):
+        """reference PartialModel.py:385-390.  As in the reference, _post_step has already cleared
+        model.model_change, so this raises AttributeError on None (the reference's behaviour
+        with save_accumulated set, kept for drop-in fidelity)."""
+        self.save_vector(self.model.model_change, self.model_change_path)
 
     def _accumulate_change(self, new, prev):
         """acc += T(new - prev) (identity: the encoder's accumulate-only kernel)."""

@@ -260,6 +260,15 @@ int dpz_dwt_sym2_tiles(const float* x, const float* x0, int64_t n, int level, in
 int dpz_idwt_sym2_tiles(const float* coeffs, int64_t n, int level, int64_t tile_lo,
                         int64_t tile_hi, float* out, dpz_stream_t stream);
 
+/* ---- Haar DWT / IDWT (pywt "haar", mode "symmetric": the reference Wavelet's DEFAULT wavelet,
+ * sharing/JWINS/Wavelet.py:56).  Same contracts as the sym2 entries above, levels 1..8; level
+ * lengths len_l = ceil(len_{l-1} / 2), layout [cA_L, cD_L, ..., cD_1] (pywt.coeffs_to_array).
+ * Bit-exact with PyWavelets 1.1.1 (csrc/dpz_haar.hip gives the summation order).              */
+int64_t dpz_haar_wavedec_len(int64_t n, int level);
+int dpz_dwt_haar(const float* x, const float* x0, int64_t n, int level, float* coeffs_x,
+                 float* coeffs_diff, int accumulate, dpz_stream_t stream);
+int dpz_idwt_haar(const float* coeffs, int64_t n, int level, float* out, dpz_stream_t stream);
+
 /* dst[idx[j]] = value for j < k (indices outside [0, n) are ignored).
  * Replaces reference models/Model.py:53-64 (rewind_accumulation: acc[idx] = 0) where the rewind
  * is not fused into dpz_topk_encode (Wavelet with change_based_selection = False).             */
@@ -284,7 +293,7 @@ enum {
   DPZ_KT_FOLD_OFFSETS, DPZ_KT_FOLD, DPZ_KT_DWT, DPZ_KT_IDWT, DPZ_KT_ELIAS_COUNT,
   DPZ_KT_ELIAS_SCAN, DPZ_KT_ELIAS_PACK, DPZ_KT_ELIAS_SPEC, DPZ_KT_ELIAS_RESOLVE,
   DPZ_KT_ELIAS_WRITE, DPZ_KT_FP16, DPZ_KT_SCATTER, DPZ_KT_FPZ_SIZE, DPZ_KT_FPZ_SCAN,
-  DPZ_KT_FPZ_PACK, DPZ_KT_FPZ_DECODE, DPZ_KT_COUNT
+  DPZ_KT_FPZ_PACK, DPZ_KT_FPZ_DECODE, DPZ_KT_CPLX, DPZ_KT_FFT_SCALE, DPZ_KT_HAAR, DPZ_KT_COUNT
 };
 int dpz_timing_enable(int on);  /* also clears the accumulators */
 int dpz_timing_read(double* ms_sum, int64_t* count, int max_ids);
@@ -337,6 +346,32 @@ int dpz_fpz_encode(const float* x, int64_t n, int precision, uint8_t* out, int64
  * and sets *status (device uint32, OR-ed) to nonzero; the caller reads it after the stream.   */
 int dpz_fpz_decode(const uint8_t* in, int64_t nbytes, int64_t n, int precision, float* out,
                    uint32_t* status, dpz_stream_t stream);
+
+/* ---- FFT sharing plugin: real FFTs and complex coefficients (decentralizepy_amd/sharing/JWINS/FFT.py)
+ * Replaces sharing/JWINS/FFT.py:12-25 (torch.fft.rfft), :301 (torch.fft.irfft, 1/n on the
+ * inverse), :143-156 (top-k over |complex change|, flat_fft[index]), PartialModel.py:315-329 on
+ * the complex change, Model.py:53-64 (complex rewind).  Complex = interleaved fp32 (re, im), the
+ * torch.complex64 layout; m = n / 2 + 1 coefficients for n reals.  The transforms run in hipFFT
+ * (rocFFT; plans cached per device / n / direction, the library's only device allocation is
+ * rocFFT's twiddle tables); the work area is the caller's.                                      */
+/* Work area for dpz_rfft / dpz_irfft of n reals (the max of both directions); -1 if unsupported
+ * (n < 2 or n > 2^31 - 1).  Creates (and caches) the plans.                                      */
+int64_t dpz_fft_workspace_bytes(int64_t n);
+/* out[m complex] = rfft(x[n]).  Asynchronous on stream.                                          */
+int dpz_rfft(const float* x, int64_t n, float* out, void* ws, size_t ws_bytes, dpz_stream_t stream);
+/* out[n] = irfft(coeffs[m complex], n) with torch's "backward" normalisation (1/n).  coeffs is
+ * OVERWRITTEN (C2R works in place on its input).                                                  */
+int dpz_irfft(float* coeffs, int64_t n, float* out, void* ws, size_t ws_bytes, dpz_stream_t stream);
+/* key[i] = |c[i]| (fp32 sqrt(re^2 + im^2)) of the complex change after the DPZ_ACC_* step
+ * (ACCUMULATE: acc += change, key = |acc|; ADD: key = |change + acc|, acc unchanged).          */
+int dpz_cplx_key(const float* change, float* acc, int acc_mode, int64_t m, float* key,
+                 dpz_stream_t stream);
+/* out[j] = src[idx[j]] (complex); acc[idx[j]] = 0 when acc is not NULL.                          */
+int dpz_cplx_gather(const float* src, int64_t m, const int32_t* idx, int64_t k, float* out,
+                    float* acc, dpz_stream_t stream);
+/* pair[2j] = 2 idx[j], pair[2j+1] = 2 idx[j] + 1 (8-byte aligned pair): a complex payload as a
+ * float payload of the interleaved view, for dpz_decode_average.                                  */
+int dpz_cplx_pair_indices(const int32_t* idx, int64_t k, int32_t* pair, dpz_stream_t stream);
 
 #ifdef __cplusplus
 }

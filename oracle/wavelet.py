@@ -1,4 +1,4 @@
-"""Oracle: pywt-exact fp32 sym2 multilevel DWT / IDWT — TEST INFRASTRUCTURE ONLY.
+"""Oracle: pywt-exact fp32 sym2 and haar multilevel DWT / IDWT — TEST INFRASTRUCTURE ONLY.
 
 The reference calls PyWavelets (third-party, not vendored):
 
@@ -29,6 +29,13 @@ inverse (valid part, F/2 = 2 taps per phase), for m in [0, n-1)::
     y[2m+p] = (r[p]*a[m+1] + r[p+2]*a[m]) + (h[p]*d[m+1] + h[p+2]*d[m])
 
 (approximation branch summed first into the zeroed output, detail branch added after).
+
+haar (the reference Wavelet's default, ``Wavelet.py:56``), F = 2: no left overhang, so::
+
+    out[o] = f0*x~[2o+1] + f1*x~[2o]          x~[n] = x[n-1] for odd n
+    y[2m+p] = r[p]*a[m] + h[p]*d[m]            (output length 2 len(a))
+
+verified bit-for-bit against pywt 1.1.1 (fixtures ``tests/golden/wavelet_haar_pywt.npz``).
 """
 import numpy as np
 
@@ -42,19 +49,46 @@ REC_HI = DEC_HI[::-1].copy()
 
 F = 4
 
+# haar filter bank (pywt 1.1.1 ``Wavelet('haar')``), fp32 casts
+H = np.float32(0.7071067811865476)
+HAAR_DEC_LO = np.array([H, H], dtype=np.float32)
+HAAR_DEC_HI = np.array([-H, H], dtype=np.float32)
+HAAR_REC_LO = np.array([H, H], dtype=np.float32)
+HAAR_REC_HI = np.array([H, -H], dtype=np.float32)
+FILTER_LEN = {"sym2": 4, "haar": 2}
 
-def level_lengths(n, level):
+
+def level_lengths(n, level, wavelet="sym2"):
     """[n_0=n, n_1, ..., n_L] with n_l = floor((n_{l-1} + F - 1) / 2)."""
+    f = FILTER_LEN[wavelet]
     lens = [int(n)]
     for _ in range(level):
-        lens.append((lens[-1] + F - 1) // 2)
+        lens.append((lens[-1] + f - 1) // 2)
     return lens
 
 
-def coeff_len(n, level):
+def coeff_len(n, level, wavelet="sym2"):
     """Length M of ``coeffs_to_array(wavedec(x))`` for a length-n input."""
-    lens = level_lengths(n, level)
+    lens = level_lengths(n, level, wavelet)
     return lens[level] + sum(lens[1:])
+
+
+def _dwt1_haar(x, flt):
+    x = np.asarray(x, dtype=np.float32)
+    n = x.shape[0]
+    xe = np.concatenate([x, x[-1:]]) if n % 2 else x
+    f0, f1 = np.float32(flt[0]), np.float32(flt[1])
+    return (f0 * xe[1::2] + f1 * xe[0::2]).astype(np.float32)
+
+
+def _idwt1_haar(a, d):
+    n = d.shape[0]
+    if a.shape[0] == n + 1:
+        a = a[:n]
+    y = np.empty(2 * n, dtype=np.float32)
+    y[0::2] = HAAR_REC_LO[0] * a + HAAR_REC_HI[0] * d
+    y[1::2] = HAAR_REC_LO[1] * a + HAAR_REC_HI[1] * d
+    return y
 
 
 def _dwt1(x, flt):
@@ -75,13 +109,16 @@ def _dwt1(x, flt):
     return out.astype(np.float32)
 
 
-def wavedec_array(x, level=4):
-    """``coeffs_to_array(wavedec(x, 'sym2', level=level))`` as one fp32 vector."""
+def wavedec_array(x, level=4, wavelet="sym2"):
+    """``coeffs_to_array(wavedec(x, wavelet, level=level))`` as one fp32 vector."""
     a = np.asarray(x, dtype=np.float32)
     details = []
     for _ in range(level):
-        d = _dwt1(a, DEC_HI)
-        a = _dwt1(a, DEC_LO)
+        if wavelet == "haar":
+            d, a = _dwt1_haar(a, HAAR_DEC_HI), _dwt1_haar(a, HAAR_DEC_LO)
+        else:
+            d = _dwt1(a, DEC_HI)
+            a = _dwt1(a, DEC_LO)
         details.append(d)
     return np.concatenate([a] + details[::-1]).astype(np.float32)
 
@@ -100,14 +137,14 @@ def _idwt1(a, d):
     return y
 
 
-def waverec_array(coeffs, n, level=4):
+def waverec_array(coeffs, n, level=4, wavelet="sym2"):
     """``waverec(array_to_coeffs(coeffs))`` truncated to the original length n."""
-    lens = level_lengths(n, level)
+    lens = level_lengths(n, level, wavelet)
     c = np.asarray(coeffs, dtype=np.float32)
     pos = lens[level]
     a = c[:pos]
     for lvl in range(level, 0, -1):
         d = c[pos:pos + lens[lvl]]
         pos += lens[lvl]
-        a = _idwt1(a, d)
+        a = _idwt1_haar(a, d) if wavelet == "haar" else _idwt1(a, d)
     return a[:n].copy()

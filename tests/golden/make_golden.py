@@ -483,8 +483,54 @@ def fullsize_main():
     print("wrote", len(cases), "full-size cases")
 
 
+def haar_main():
+    """The reference Wavelet plugin with its DEFAULT wavelet, haar (sharing/JWINS/Wavelet.py:56):
+    pywt 1.1.1 haar wavedec / waverec vectors (odd and even sizes, levels 1-8) and multi-round
+    Wavelet scenarios (plain, accumulation, accumulate-averaging, level 6, mixed full payloads)
+    -> tests/golden/wavelet_haar_pywt.npz, haar_*.npz, haar_scenarios.json."""
+    torch.set_num_threads(4)
+    rng = np.random.default_rng(71)
+    arrays, cases = {}, []
+    for n, level in [(1, 1), (2, 1), (3, 1), (17, 4), (64, 4), (65, 4), (101, 4), (1001, 8),
+                     (4099, 4), (10000, 6), (65537, 8)]:
+        x = rng.standard_normal(n).astype(np.float32)
+        arr, sl = pywt.coeffs_to_array(pywt.wavedec(x, "haar", level=level))
+        rec = pywt.waverec(pywt.array_to_coeffs(arr, sl, output_format="wavedec"), wavelet="haar")
+        key = f"n{n}_l{level}"
+        arrays[f"{key}_x"] = x
+        arrays[f"{key}_coeffs"] = np.asarray(arr, dtype=np.float32)
+        arrays[f"{key}_rec"] = np.asarray(rec, dtype=np.float32)
+        cases.append([n, level])
+    np.savez_compressed(os.path.join(OUT, "wavelet_haar_pywt.npz"), **arrays)
+    wv = {"alpha": 0.1, "metadata_cap": 0.5}  # wavelet / level: the reference defaults
+    mixed = [["partial", "full", "partial"], ["full", "partial", "partial"]]
+    scen = [
+        run_scenario("haar_plain", Wavelet, wv, 20, 50, 1, 2, seed=81, wavelet=True,
+                     nbr_kinds=mixed),
+        run_scenario("haar_acc", Wavelet, {**wv, "accumulation": True}, 40, 100, 99, 2,
+                     seed=82, wavelet=True),
+        run_scenario("haar_accavg", Wavelet,
+                     {**wv, "accumulation": True, "accumulate_averaging_changes": True},
+                     40, 100, 99, 2, seed=83, wavelet=True),
+        run_scenario("haar_l6_nochange", Wavelet,
+                     {**wv, "level": 6, "accumulation": True, "change_based_selection": False},
+                     40, 100, 99, 2, seed=84, wavelet=True),
+        run_scenario("haar_server", Wavelet, {**wv, "accumulation": True}, 40, 100, 99, 2,
+                     seed=85, wavelet=True, nbr_kinds=mixed, averaging="_averaging_server"),
+    ]
+    with open(os.path.join(OUT, "haar_scenarios.json"), "w") as f:
+        json.dump({"scenarios": scen, "pywt_cases": cases,
+                   "generator": "tests/golden/make_golden.py --haar",
+                   "reference": "sacs-epfl/decentralizepy v1 (/root/reference/src)",
+                   "pywavelets": "1.1.1 (python3.9 bridge)", "torch": torch.__version__}, f,
+                  indent=1)
+    print("wrote", len(scen), "haar scenarios,", len(cases), "pywt cases")
+
+
 if __name__ == "__main__":
-    if "--fullsize" in sys.argv:
+    if "--haar" in sys.argv:
+        haar_main()
+    elif "--fullsize" in sys.argv:
         fullsize_main()
     elif "--wire" in sys.argv:
         wire_main()

@@ -17,17 +17,22 @@ def _ref_kwargs():
           "change_based_selection", "save_accumulated", "accumulation",
           "accumulate_averaging_changes", "compress", "compression_package", "compression_class"]
     jw = ["alpha_list"] + wv[1:]
-    return {"PartialModel": pm, "Wavelet": wv, "JWINS": jw}
+    fft = ["alpha", "dict_ordered", "save_shared", "metadata_cap", "change_based_selection",
+           "save_accumulated", "accumulation", "accumulate_averaging_changes", "compress",
+           "compression_package", "compression_class"]
+    return {"PartialModel": pm, "Wavelet": wv, "JWINS": jw, "FFT": fft}
 
 
 def test_constructor_keyword_surface_matches_reference():
+    from decentralizepy_amd.sharing.JWINS.FFT import FFT
     from decentralizepy_amd.sharing.JWINS.JWINS import JWINS
     from decentralizepy_amd.sharing.JWINS.Wavelet import Wavelet
     from decentralizepy_amd.sharing.PartialModel import PartialModel
     from decentralizepy_amd.sharing.Sharing import Sharing
     positional = ["self", "rank", "machine_id", "communication", "mapping", "graph", "model",
                   "dataset", "log_dir"]
-    for cls, names in [(PartialModel, "PartialModel"), (Wavelet, "Wavelet"), (JWINS, "JWINS")]:
+    for cls, names in [(PartialModel, "PartialModel"), (Wavelet, "Wavelet"), (JWINS, "JWINS"),
+                       (FFT, "FFT")]:
         params = list(inspect.signature(cls.__init__).parameters)
         assert params[:9] == positional
         assert params[9:] == _ref_kwargs()[names], cls
@@ -58,9 +63,12 @@ def test_plugin_fails_loudly_without_gpu(tmp_path):
 def test_unsupported_wavelet_is_rejected(tmp_path):
     from decentralizepy_amd.sharing.JWINS.Wavelet import Wavelet
     model = scenario.make_model([4, 4, 2])
-    with pytest.raises(NotImplementedError, match="haar"):
+    with pytest.raises(NotImplementedError, match="db4"):
         Wavelet(0, 0, None, scenario._Mapping(), scenario._Graph([1]), model, None,
-                str(tmp_path), wavelet="haar")
+                str(tmp_path), wavelet="db4")
+    with pytest.raises(NotImplementedError, match="levels 1..4"):
+        Wavelet(0, 0, None, scenario._Mapping(), scenario._Graph([1]), model, None,
+                str(tmp_path), wavelet="sym2", level=5)
 
 
 def test_compression_surface_and_trailer():

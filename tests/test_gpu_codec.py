@@ -346,6 +346,35 @@ def test_waverec_levels_bit_exact(dev, n, level):
     np.testing.assert_array_equal(_bits(rec), _bits(owav.waverec_array(coeffs, n, level)))
 
 
+@pytest.mark.parametrize("level", [1, 2, 3, 4, 6, 8])
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 255, 256, 257, 1001, 65_537, 1_000_003, 25_000_000])
+def test_haar_bit_exact(dev, n, level):
+    """haar DWT pair / accumulate / IDWT (the reference Wavelet's default wavelet) against the
+    pywt-pinned oracle, every level 1-8 (chunk edges at 256, odd lengths at every level)."""
+    if n > 1_000_003 and level not in (4, 8):
+        pytest.skip("full size at two levels")
+    codec = _codec()
+    rng = np.random.default_rng(n * 10 + level)
+    x = rng.standard_normal(n).astype(np.float32)
+    x0 = (x - 0.01 * rng.standard_normal(n)).astype(np.float32)
+    tx, tx0 = torch.from_numpy(x).to(dev), torch.from_numpy(x0).to(dev)
+    wx, wd = codec.wavedec(tx, level, x0=tx0, wavelet="haar")
+    cx = owav.wavedec_array(x, level, "haar")
+    np.testing.assert_array_equal(_bits(wx.cpu().numpy()), _bits(cx))
+    np.testing.assert_array_equal(_bits(wd.cpu().numpy()),
+                                  _bits(owav.wavedec_array(x - x0, level, "haar")))
+    acc = (0.01 * rng.standard_normal(wx.numel())).astype(np.float32)
+    tacc = torch.from_numpy(acc).to(dev)
+    codec.wavedec(tx, level, x0=tx0, want_x=False, coeffs_diff=tacc, accumulate=True,
+                  wavelet="haar")
+    np.testing.assert_array_equal(_bits(tacc.cpu().numpy()),
+                                  _bits(acc + owav.wavedec_array(x - x0, level, "haar")))
+    wxo, _ = codec.wavedec(tx, level, wavelet="haar")
+    np.testing.assert_array_equal(_bits(wxo.cpu().numpy()), _bits(cx))
+    rec = codec.waverec(wx, n, level, wavelet="haar").cpu().numpy()
+    np.testing.assert_array_equal(_bits(rec), _bits(owav.waverec_array(cx, n, level, "haar")))
+
+
 def test_fp16_pack_roundtrip(dev):
     codec = _codec()
     for n in [1, 7, 8, 9, 1_000_003]:

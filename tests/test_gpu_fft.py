@@ -1,0 +1,87 @@
+"""GPU: the FFT plugin (decentralizepy_amd/sharing/JWINS/FFT.py: hipFFT transforms + the HIP
+complex-key / gather / pair-index kernels + the shared top-k and fold kernels) replays the
+reference FFT plugin's recorded rounds: exact indices and counters, complex values, accumulators
+and averaged models within scenario.fft_tol (rocFFT vs torch's CPU pocketfft)."""
+from collections import deque
+
+import numpy as np
+import pytest
+import torch
+
+from tests import scenario
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", scenario.fft_names())
+def test_fft_plugin_replays_reference(name, dev, tmp_path):
+    scenario.replay_fft_plugin(name, tmp_path)
+
+
+def test_fft_full_payload_raises_keyerror_like_reference(dev, tmp_path):
+    """reference FFT.deserialized_model reads m["indices"] for a full payload as well."""
+    from decentralizepy_amd.sharing.JWINS.FFT import FFT
+    meta, arrays = scenario.load_fft("fft_plain")
+    model = scenario.make_model(meta["shape"])
+    scenario.set_flat(model, arrays["x0"])
+    plugin = FFT(0, 0, None, scenario._Mapping(), scenario._Graph([1]), model, None,
+                 str(tmp_path), **meta["kwargs"])
+    plugin.get_data_to_send(degree=1)
+    full = {"params": np.zeros(meta["m"], np.complex64), "degree": 1, "iteration": 0,
+            "CHANNEL": "DPSGD"}
+    with pytest.raises(KeyError):
+        plugin._averaging({1: deque([full])})
+    with pytest.raises(KeyError):
+        plugin.deserialized_model({"params": np.zeros(meta["m"], np.complex64)})
+
+
+@pytest.mark.parametrize("n", [4098, 1 << 20, 11_000_000])
+def test_rfft_irfft_against_numpy(dev, n):
+    """dpz_rfft / dpz_irfft against a float64 numpy FFT (error bound as scenario.fft_tol) and the
+    round trip; sizes include a power of two and the C2 model size (2^6 5^6 11)."""
+    from decentralizepy_amd import codec
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(n, device=dev, generator=g)
+    f = codec.rfft(x)
+    xh = x.cpu().numpy()
+    ref = np.fft.rfft(xh.astype(np.float64))
+    scale = float(np.abs(xh).max())
+    err = np.abs(f.cpu().numpy() - ref).max()
+    assert err <= scenario.fft_tol("params", n, scale), err
+    back = codec.irfft(f.clone(), n)
+    err2 = np.abs(back.cpu().numpy() - xh).max()
+    assert err2 <= scenario.fft_tol("model", n, scale), err2
+
+
+def test_cplx_kernels_exact(dev):
+    """dpz_cplx_key (all accumulation modes), dpz_cplx_gather with the rewind and
+    dpz_cplx_pair_indices against fp32 numpy restatements (bit-exact)."""
+    from decentralizepy_amd import codec
+    from oracle import fft as offt
+    rng = np.random.default_rng(3)
+    m = 100_003
+    c = (rng.standard_normal(m) + 1j * rng.standard_normal(m)).astype(np.complex64)
+    a = (0.1 * (rng.standard_normal(m) + 1j * rng.standard_normal(m))).astype(np.complex64)
+    cd = torch.from_numpy(c).to(dev)
+    for mode in (codec.DPZ_ACC_NONE, codec.DPZ_ACC_ACCUMULATE, codec.DPZ_ACC_ADD):
+        ad = torch.from_numpy(a.copy()).to(dev)
+        key = codec.cplx_key(cd, ad if mode else None, mode).cpu().numpy()
+        if mode == codec.DPZ_ACC_ACCUMULATE:
+            acc_ref = (a.view(np.float32) + c.view(np.float32)).view(np.complex64)
+            np.testing.assert_array_equal(ad.cpu().numpy().view(np.uint32), acc_ref.view(np.uint32))
+            src = acc_ref
+        elif mode == codec.DPZ_ACC_ADD:
+            src = (c.view(np.float32) + a.view(np.float32)).view(np.complex64)
+        else:
+            src = c
+        np.testing.assert_array_equal(key.view(np.uint32), offt.cabs(src).view(np.uint32))
+    idx = np.sort(rng.choice(m, 5000, replace=False)).astype(np.int32)
+    idd = torch.from_numpy(idx).to(dev)
+    ad = torch.from_numpy(a.copy()).to(dev)
+    out = codec.cplx_gather(cd, idd, acc=ad).cpu().numpy()
+    np.testing.assert_array_equal(out.view(np.uint64), c[idx].view(np.uint64))
+    a2 = a.copy()
+    a2[idx] = 0
+    np.testing.assert_array_equal(ad.cpu().numpy().view(np.uint64), a2.view(np.uint64))
+    pair = codec.cplx_pair_indices(idd).cpu().numpy()
+    np.testing.assert_array_equal(pair, offt.pair_indices(idx).astype(np.int32))

@@ -96,3 +96,20 @@ def test_outgoing_message_pickles_like_the_reference(dev, tmp_path, case):
     assert (len(out), data_len, len(out) - data_len) == (
         case["pickle_len"], case["data_len"], case["meta_len"])
     assert hashlib.sha256(out).hexdigest() == case["sha256"]
+
+
+def test_save_accumulated_behaves_like_reference(dev, tmp_path):
+    """save_accumulated (reference PartialModel.py:122-131, 350-390): the constructor creates
+    model_change/<rank> and model_val/<rank>; _post_step clears model.model_change and then
+    save_change() dumps it, i.e. calls None.tolist() -> AttributeError, as the reference does."""
+    from decentralizepy_amd.sharing.PartialModel import PartialModel
+    meta, arrays = scenario.load("pm_a01_plain")
+    model = scenario.make_model(meta["shape"])
+    scenario.set_flat(model, arrays["x0"])
+    plugin = PartialModel(0, 0, None, scenario._Mapping(), scenario._Graph([1, 2, 3]), model,
+                          None, str(tmp_path), alpha=0.1, save_accumulated="yes")
+    assert (tmp_path / "model_change" / "0").is_dir() and (tmp_path / "model_val" / "0").is_dir()
+    plugin.get_data_to_send(degree=3)
+    msgs = scenario.neighbour_msgs(meta["rounds"][0], arrays, 0)
+    with pytest.raises(AttributeError, match="tolist"):
+        plugin._averaging({uid: deque([m]) for uid, m in zip([1, 2, 3], msgs)})

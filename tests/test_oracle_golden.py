@@ -50,6 +50,22 @@ def test_elias_known_answer_vector():
         "520003000000000000008900000000000000"
 
 
+def test_oracle_haar_matches_pywt():
+    """haar (the reference Wavelet's default) wavedec / waverec of PyWavelets 1.1.1, levels 1-8,
+    odd and even sizes (tests/golden/make_golden.py --haar)."""
+    import json
+    a = dict(np.load(os.path.join(GOLDEN, "wavelet_haar_pywt.npz")))
+    with open(os.path.join(GOLDEN, "haar_scenarios.json")) as f:
+        cases = json.load(f)["pywt_cases"]
+    for n, level in cases:
+        key = f"n{n}_l{level}"
+        c = owav.wavedec_array(a[f"{key}_x"], level, "haar")
+        np.testing.assert_array_equal(c.view(np.uint32), a[f"{key}_coeffs"].view(np.uint32))
+        assert c.shape[0] == owav.coeff_len(n, level, "haar")
+        rec = owav.waverec_array(a[f"{key}_coeffs"], n, level, "haar")
+        np.testing.assert_array_equal(rec.view(np.uint32), a[f"{key}_rec"][:n].view(np.uint32))
+
+
 def test_oracle_wavelet_matches_pywt():
     a = dict(np.load(os.path.join(GOLDEN, "wavelet_pywt.npz")))
     for n in scenario.load_meta()["wavelet_sizes"]:

@@ -14,5 +14,5 @@ if [ -n "$ref" ]; then
 fi
 cd "$src/decentralizepy_amd/csrc"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off $flags -shared \
-  -o "$out/lib_$name.so" dpz_*.hip dpz_batch.cpp
+  -o "$out/lib_$name.so" dpz_*.hip dpz_batch.cpp -lhipfft
 echo "built $out/lib_$name.so"
