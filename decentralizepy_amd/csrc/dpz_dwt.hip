@@ -25,7 +25,10 @@ constexpr int DWT_TL = DPZ_DWT_TL;
 // waves per SIMD the forward kernel is register-bounded for (3 without the bound: 150 VGPRs)
 #ifndef DPZ_DWT_WAVES
 #define DPZ_DWT_WAVES 4
-#endif  // level-L outputs per block (forward)
+#endif
+#ifndef DPZ_DWT4_WAVES  // the level-4 kernel (interior path)
+#define DPZ_DWT4_WAVES 4
+#endif
 constexpr int IDWT_TILE = 4096;
 
 // sym2 filters (fp32 casts of pywt's double coefficients)
@@ -264,9 +267,174 @@ __device__ __forceinline__ void dwt_levels(const Levels& LV, float* cx, float* c
   }
 }
 
+// ---- interior tiles at level 4 (no array edge within reach, not the first tile of a sharded
+// range): level 1 is computed straight from the span registers — group G (inputs g0 + 4G .. +3)
+// gives the level-1 outputs 2G, 2G + 1 from its 4 inputs and the 2 before it (the left lane's
+// z, w by a shuffle; lane 0 of each wave loads them) — its details go to global memory and its
+// approximations to LDS as one 8-byte store.  Levels 2-4 read LDS as 8 + 16-byte vectors: a
+// thread computes two adjacent outputs from 6 consecutive inputs (no bank conflicts; the span
+// path reads with a stride of 2).  Same pywt summation order as conv4r (no odd-length tail
+// inside an interior tile).
+constexpr int DWT_IN1 = 8 * DWT_TL + 16;       // level-1 values per pipeline (from 8 TL t - 16)
+constexpr int DWT_IN2 = 4 * DWT_TL + 8;        // level-2 values (from 4 TL t - 8)
+constexpr int DWT_IN3 = 2 * DWT_TL + 4;        // level-3 values (from 2 TL t - 4)
+constexpr int DWT_NGRP = (16 * DWT_TL + 32) / 4;  // float4 groups of an interior span
+
+// interior tiles of a level-4 launch over [tile0, tile_hi): [a, b) with a = max(tile0 + 1, 1)
+// (the first tile of a sharded range has only a 32-input halo) and (t + 2) * 16 TL <= n (no
+// symmetric extension within reach at any level)
+static inline void dwt_interior_range(int64_t n, int64_t tile0, int64_t tile_hi, int64_t* a,
+                                      int64_t* b) {
+  int64_t lo = tile0 + 1 > 1 ? tile0 + 1 : 1;
+  int64_t hi = n / (16 * DWT_TL) - 1;
+  if (hi > tile_hi) hi = tile_hi;
+  if (lo > tile_hi) lo = tile_hi;
+  if (hi < lo) hi = lo;
+  *a = lo;
+  *b = hi;
+}
+
+// the 2 inputs before each wave's first group (lane 0) of an interior span
+template <bool WD>
+__device__ __forceinline__ void dwt_halo_load(const float* __restrict__ x,
+                                              const float* __restrict__ x0, int64_t g0,
+                                              float2 (&hx)[DWT_NG], float2 (&hb)[DWT_NG]) {
+#pragma unroll
+  for (int q = 0; q < DWT_NG; ++q) {
+    const int G = threadIdx.x + 256 * q;
+    hx[q] = make_float2(0.f, 0.f);
+    hb[q] = hx[q];
+    if ((threadIdx.x & 63) == 0 && G < DWT_NGRP) {
+      const int64_t p = g0 + 4 * (int64_t)G - 2;
+      hx[q] = make_float2(x[p], x[p + 1]);
+      if (WD) hb[q] = make_float2(x0[p], x0[p + 1]);
+    }
+  }
+}
+
+__device__ __forceinline__ float conv4v(float i0, float i1, float i2, float i3, const float* f) {
+  // f0 * x~[top] + f1 * x~[top-1] + f2 * x~[top-2] + f3 * x~[top-3]; i3 = top
+  float acc = f[0] * i3;
+  acc = acc + f[1] * i2;
+  acc = acc + f[2] * i1;
+  acc = acc + f[3] * i0;
+  return acc;
+}
+
+template <bool WX, bool WD, bool ACCUM>
+__device__ __forceinline__ void dwt_int_level1(const Levels& LV, float* cx, float* cd, int64_t tile,
+                                               const float4 (&va)[DWT_NG],
+                                               const float4 (&vb)[DWT_NG],
+                                               const float2 (&hx)[DWT_NG],
+                                               const float2 (&hb)[DWT_NG], float* smem) {
+  float* L1[2] = {smem, smem + DWT_IN1};
+  const int64_t s1 = tile * (8 * DWT_TL) - 16;  // level-1 position of LDS index 0
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int q = 0; q < DWT_NG; ++q) {
+    const int G = threadIdx.x + 256 * q;
+    float in[2][6];  // h0, h1, a0..a3 per pipeline
+    in[0][2] = va[q].x; in[0][3] = va[q].y; in[0][4] = va[q].z; in[0][5] = va[q].w;
+    if (WD) {
+      in[1][2] = va[q].x - vb[q].x; in[1][3] = va[q].y - vb[q].y;
+      in[1][4] = va[q].z - vb[q].z; in[1][5] = va[q].w - vb[q].w;
+    }
+    {
+      const float zx = __shfl_up(va[q].z, 1, 64), wx = __shfl_up(va[q].w, 1, 64);
+      in[0][0] = lane == 0 ? hx[q].x : zx;
+      in[0][1] = lane == 0 ? hx[q].y : wx;
+      if (WD) {
+        const float zd = __shfl_up(in[1][4], 1, 64), wd = __shfl_up(in[1][5], 1, 64);
+        in[1][0] = lane == 0 ? hx[q].x - hb[q].x : zd;
+        in[1][1] = lane == 0 ? hx[q].y - hb[q].y : wd;
+      }
+    }
+    if (G >= DWT_NGRP) continue;
+    const int64_t o = s1 + 2 * G;  // level-1 outputs o, o + 1
+    const bool own = G >= 8;        // [8 TL t, 8 TL (t + 1)) is owned
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp) {
+      if (sp == 0 && !WX) continue;
+      if (sp == 1 && !WD) continue;
+      const float* v = in[sp];
+      const float lo0 = conv4v(v[0], v[1], v[2], v[3], c_dec_lo);
+      const float lo1 = conv4v(v[2], v[3], v[4], v[5], c_dec_lo);
+      *reinterpret_cast<float2*>(L1[sp] + 2 * G) = make_float2(lo0, lo1);
+      if (own) {
+        const float hi0 = conv4v(v[0], v[1], v[2], v[3], c_dec_hi);
+        const float hi1 = conv4v(v[2], v[3], v[4], v[5], c_dec_hi);
+        float* dst = (sp == 0 ? cx : cd) + LV.doff[1] + o;
+        if (ACCUM && sp == 1) {
+          dst[0] = dst[0] + hi0;
+          dst[1] = dst[1] + hi1;
+        } else {
+          dst[0] = hi0;
+          dst[1] = hi1;
+        }
+      }
+    }
+  }
+}
+
+// one level from LDS `in` (index 0 = position base_in) into LDS `out` (or cA at the top level):
+// outputs u in [2, nu), u = position - base_out, reading in[2u - 2 .. 2u + 1]; owned details for
+// u >= u_own.
+template <bool WX, bool WD, bool ACCUM, bool TOP>
+__device__ __forceinline__ void dwt_int_level(const Levels& LV, float* cx, float* cd, int l,
+                                              int64_t base_out, int nu, int u_own, float* const* in,
+                                              float* const* out) {
+  const int npairs = nu / 2;  // pairs p = 1 .. npairs - 1 (u = 2p, 2p + 1)
+  for (int p = 1 + (int)threadIdx.x; p < npairs; p += 256) {
+    const int u = 2 * p;
+    const int64_t pos = base_out + u;
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp) {
+      if (sp == 0 && !WX) continue;
+      if (sp == 1 && !WD) continue;
+      const float2 A = *reinterpret_cast<const float2*>(in[sp] + 2 * u - 2);
+      const float4 B = *reinterpret_cast<const float4*>(in[sp] + 2 * u);
+      const float lo0 = conv4v(A.x, A.y, B.x, B.y, c_dec_lo);
+      const float lo1 = conv4v(B.x, B.y, B.z, B.w, c_dec_lo);
+      float* g = sp == 0 ? cx : cd;
+      const bool acc = ACCUM && sp == 1;
+      if (TOP) {
+        if (u >= u_own) {
+          float* dst = g + pos;
+          dst[0] = acc ? dst[0] + lo0 : lo0;
+          dst[1] = acc ? dst[1] + lo1 : lo1;
+        }
+      } else {
+        *reinterpret_cast<float2*>(out[sp] + u) = make_float2(lo0, lo1);
+      }
+      if (u >= u_own) {
+        const float hi0 = conv4v(A.x, A.y, B.x, B.y, c_dec_hi);
+        const float hi1 = conv4v(B.x, B.y, B.z, B.w, c_dec_hi);
+        float* dst = g + LV.doff[l] + pos;
+        dst[0] = acc ? dst[0] + hi0 : hi0;
+        dst[1] = acc ? dst[1] + hi1 : hi1;
+      }
+    }
+  }
+}
+
+template <bool WX, bool WD, bool ACCUM>
+__device__ __forceinline__ void dwt_int_levels234(const Levels& LV, float* cx, float* cd,
+                                                  int64_t tile, float* smem) {
+  float* L1[2] = {smem, smem + DWT_IN1};
+  float* L2[2] = {smem + 2 * DWT_IN1, smem + 2 * DWT_IN1 + DWT_IN2};
+  float* L3[2] = {smem + 2 * DWT_IN1 + 2 * DWT_IN2, smem + 2 * DWT_IN1 + 2 * DWT_IN2 + DWT_IN3};
+  // level 2: positions 4 TL t - 8 + u, owned from u = 8
+  dwt_int_level<WX, WD, ACCUM, false>(LV, cx, cd, 2, tile * (4 * DWT_TL) - 8, DWT_IN2, 8, L1, L2);
+  __syncthreads();
+  dwt_int_level<WX, WD, ACCUM, false>(LV, cx, cd, 3, tile * (2 * DWT_TL) - 4, DWT_IN3, 4, L2, L3);
+  __syncthreads();
+  dwt_int_level<WX, WD, ACCUM, true>(LV, cx, cd, 4, tile * DWT_TL - 2, DWT_TL + 2, 2, L3, nullptr);
+}
+
 // Persistent grid (about as many blocks as the CUs hold at once, each walking tiles with a
 // grid stride): the per-tile blocks were short enough (~2.6 us) that the workgroup dispatcher,
-// not HBM, bounded the launch (SQ_WAVE_CYCLES showed ~21 % of the wave slots in use).
+// not HBM, bounded the launch (SQ_WAVE_CYCLES showed ~21 % of the wave slots in use).  Used for
+// levels other than 4; level 4 runs dwt4_kernel below.
 template <bool WX, bool WD, bool ACCUM>
 __global__ void __launch_bounds__(256, DPZ_DWT_WAVES) dwt_kernel(const float* __restrict__ x,
                                                   const float* __restrict__ x0, Levels LV,
@@ -291,6 +459,55 @@ __global__ void __launch_bounds__(256, DPZ_DWT_WAVES) dwt_kernel(const float* __
     dwt_levels<WX, WD, ACCUM>(LV, cx, cd, tile, smem);
     __syncthreads();  // the next tile reuses the LDS buffers
     if (next >= ntiles) break;
+    tile = next;
+  }
+}
+
+// Level 4 (every shipped JWINS config): blocks [0, n_edge) first take one EDGE tile each — the
+// tiles that touch an array end or start a sharded range ([tile0, a) and [b, tile_hi)) — on the
+// span path above, without prefetch; then every block walks the INTERIOR tiles [a, b) on the
+// register / vector-LDS path with the next tile's loads in flight.  Nothing is live across the
+// two phases, so the span path's registers do not add to the interior loop's (94 VGPRs alone,
+// 194 with both paths in one loop).
+template <bool WX, bool WD, bool ACCUM>
+__global__ void __launch_bounds__(256, DPZ_DWT4_WAVES) dwt4_kernel(const float* __restrict__ x,
+                                                   const float* __restrict__ x0, Levels LV,
+                                                   float* cx, float* cd, int64_t tile0,
+                                                   int64_t a, int64_t b, int64_t tile_hi) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int64_t n = LV.len[0];
+  const int64_t n_lo = a - tile0;
+  if ((int64_t)blockIdx.x < n_lo + (tile_hi - b)) {
+    const int64_t tile = (int64_t)blockIdx.x < n_lo ? tile0 + blockIdx.x : b + (blockIdx.x - n_lo);
+    float4 va[DWT_NG], vb[DWT_NG];
+    int64_t s0, e0;
+    dwt_span(LV, tile, &s0, &e0);
+    dwt_span_load<WD>(x, x0, n, s0, e0, va, vb);
+    dwt_span_store<WX, WD>(va, vb, n, s0, e0, smem);
+    dwt_levels<WX, WD, ACCUM>(LV, cx, cd, tile, smem);
+    __syncthreads();
+  }
+  int64_t tile = a + blockIdx.x;
+  if (tile >= b) return;
+  float4 va[DWT_NG], vb[DWT_NG];
+  float2 hx[DWT_NG], hb[DWT_NG];
+  int64_t s0, e0;
+  dwt_span(LV, tile, &s0, &e0);
+  dwt_span_load<WD>(x, x0, n, s0, e0, va, vb);
+  dwt_halo_load<WD>(x, x0, s0 & ~int64_t(3), hx, hb);
+  for (;;) {
+    dwt_int_level1<WX, WD, ACCUM>(LV, cx, cd, tile, va, vb, hx, hb, smem);
+    // the next tile's loads are in flight while this tile's levels 2-4 are computed
+    const int64_t next = tile + gridDim.x;
+    if (next < b) {
+      dwt_span(LV, next, &s0, &e0);
+      dwt_span_load<WD>(x, x0, n, s0, e0, va, vb);
+      dwt_halo_load<WD>(x, x0, s0 & ~int64_t(3), hx, hb);
+    }
+    __syncthreads();  // level-1 approximations in LDS
+    dwt_int_levels234<WX, WD, ACCUM>(LV, cx, cd, tile, smem);
+    __syncthreads();  // the next tile reuses the LDS buffers
+    if (next >= b) break;
     tile = next;
   }
 }
@@ -497,7 +714,26 @@ extern "C" int dpz_dwt_sym2_tiles(const float* x, const float* x0, int64_t n, in
   const bool wx = coeffs_x != nullptr, wd = coeffs_diff != nullptr;
   const int64_t nt = tile_hi - tile_lo;
   const int tslot = timing_begin(DPZ_KT_DWT, st);
-  if (wx && wd) {
+  if (level == 4) {
+    int64_t a, b;
+    dwt_interior_range(n, tile_lo, tile_hi, &a, &b);
+    const int64_t nedge = (a - tile_lo) + (tile_hi - b);
+#define DPZ_DWT4_LAUNCH(WXV, WDV, ACV)                                                           \
+  {                                                                                              \
+    int64_t g = persistent_grid(dwt4_kernel<WXV, WDV, ACV>, shm, b - a);                          \
+    if (g < nedge) g = nedge;                                                                    \
+    dwt4_kernel<WXV, WDV, ACV><<<(unsigned)g, 256, shm, st>>>(x, x0, LV, coeffs_x, coeffs_diff,  \
+                                                             tile_lo, a, b, tile_hi);            \
+  }
+    if (wx && wd) {
+      if (accumulate) DPZ_DWT4_LAUNCH(true, true, true) else DPZ_DWT4_LAUNCH(true, true, false)
+    } else if (wx) {
+      DPZ_DWT4_LAUNCH(true, false, false)
+    } else {
+      if (accumulate) DPZ_DWT4_LAUNCH(false, true, true) else DPZ_DWT4_LAUNCH(false, true, false)
+    }
+#undef DPZ_DWT4_LAUNCH
+  } else if (wx && wd) {
     if (accumulate) dwt_kernel<true, true, true><<<persistent_grid(dwt_kernel<true, true, true>, shm, nt), 256, shm, st>>>(x, x0, LV, coeffs_x, coeffs_diff, tile_lo, tile_hi);
     else dwt_kernel<true, true, false><<<persistent_grid(dwt_kernel<true, true, false>, shm, nt), 256, shm, st>>>(x, x0, LV, coeffs_x, coeffs_diff, tile_lo, tile_hi);
   } else if (wx) {

@@ -48,7 +48,7 @@ __global__ void __launch_bounds__(256) cplx_key_kernel(const float2* __restrict_
     }
     const float re2 = c.x * c.x;
     const float im2 = c.y * c.y;
-    key[i] = __fsqrt_rn(re2 + im2);
+    key[i] = sqrtf(re2 + im2);  // correctly rounded (llvm.sqrt without afn)
   }
 }
 
