@@ -124,6 +124,19 @@ SIGNATURES = {
     "dpz_dwt_haar": (_int, [_c_void_p, _c_void_p, _i64, _int, _c_void_p, _c_void_p, _int,
                             _c_void_p]),
     "dpz_idwt_haar": (_int, [_c_void_p, _i64, _int, _c_void_p, _c_void_p]),
+    "dpz_lz4_max_bytes": (_i64, [_i64]),
+    "dpz_lz4_workspace_bytes": (_size, [_i64, _i64, _i64]),
+    "dpz_lz4_compress": (_int, [_c_void_p, _i64, _c_void_p, _i64, ctypes.POINTER(_i64),
+                                _c_void_p, _size, _c_void_p]),
+    "dpz_lz4_frame_info": (_int, [ctypes.c_char_p, _i64, ctypes.POINTER(_i64),
+                                  ctypes.POINTER(_i64), ctypes.POINTER(_int),
+                                  ctypes.POINTER(_i64)]),
+    "dpz_lz4_decompress": (_int, [_c_void_p, ctypes.c_char_p, _i64, _c_void_p, _i64,
+                                  ctypes.POINTER(_i64), _c_void_p, _size, _c_void_p]),
+    "dpz_delta_i32": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
+    "dpz_running_sum_workspace_bytes": (_size, [_i64]),
+    "dpz_running_sum_i32": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p, _size,
+                                   _c_void_p]),
 }
 
 _lib = None

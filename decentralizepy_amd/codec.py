@@ -20,7 +20,8 @@ __all__ = ["DPZ_ACC_NONE", "DPZ_ACC_ACCUMULATE", "DPZ_ACC_ADD", "DPZ_EW_SUB", "D
            "topk_complete", "decode_average", "replace", "wavedec_len", "wavedec", "waverec",
            "pack_fp16", "unpack_fp16", "elias_encode", "elias_decode",
            "KernelTimer", "NodeStepBatch", "topk_sticky_status", "rfft", "irfft", "cplx_key",
-           "cplx_gather", "cplx_pair_indices"]
+           "cplx_gather", "cplx_pair_indices", "lz4_compress", "lz4_decompress", "lz4_frame_info",
+           "delta_i32", "running_sum_i32"]
 
 
 def _ptr(t):
@@ -606,6 +607,90 @@ def cplx_pair_indices(idx, out=None):
     rc = _lib.lib().dpz_cplx_pair_indices(_ptr(idx), k, _ptr(out), _stream(idx.device))
     check(rc, "dpz_cplx_pair_indices")
     return out
+
+
+def _lz4_ws(workspace, device, need):
+    workspace = workspace or Workspace(device)
+    buf = getattr(workspace, "lbuf", None)
+    if buf is None or buf.numel() < max(need, 256):
+        buf = workspace.lbuf = torch.empty(max(need, 256), dtype=torch.uint8, device=device)
+    return buf
+
+
+def lz4_compress(data, out=None, workspace=None):
+    """LZ4 frame of a device byte tensor (csrc/dpz_lz4.hip: independent 4 KB blocks, one wave
+    each); returns a device uint8 view of exactly the frame (reference Lz4Wrapper.py:20-98)."""
+    _require(data, torch.uint8, "data")
+    n = data.numel()
+    cap = int(_lib.lib().dpz_lz4_max_bytes(n))
+    if out is None or out.numel() < cap:
+        out = torch.empty(cap, dtype=torch.uint8, device=data.device)
+    ws = _lz4_ws(workspace, data.device, int(_lib.lib().dpz_lz4_workspace_bytes(n, 0, 0)))
+    nbytes = ctypes.c_int64(0)
+    rc = _lib.lib().dpz_lz4_compress(_ptr(data), n, _ptr(out), out.numel(), ctypes.byref(nbytes),
+                                     _ptr(ws), ws.numel(), _stream(data.device))
+    check(rc, "dpz_lz4_compress")
+    return out[:nbytes.value]
+
+
+def lz4_frame_info(frame):
+    """(content_size or -1, blocks, linked, block_max) of a host frame (bytes-like)."""
+    b = bytes(frame)
+    cs, nb, ln, bm = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int(0), ctypes.c_int64(0)
+    rc = _lib.lib().dpz_lz4_frame_info(b, len(b), ctypes.byref(cs), ctypes.byref(nb),
+                                       ctypes.byref(ln), ctypes.byref(bm))
+    if rc == _lib.DPZ_ERR_ARG:
+        raise ValueError("malformed LZ4 frame")
+    check(rc, "dpz_lz4_frame_info")
+    return int(cs.value), int(nb.value), bool(ln.value), int(bm.value)
+
+
+def lz4_decompress(frame, device, out=None, workspace=None, max_size=None):
+    """Content of an LZ4 frame (host bytes-like) decoded on ``device``; returns a device uint8
+    tensor.  Linked frames (python-lz4's default) and independent frames with blocks of at most
+    64 KB are supported."""
+    b = bytes(frame)
+    cs, nb, linked, bmax = lz4_frame_info(b)
+    if cs < 0 and max_size is None:
+        raise ValueError("frame without a content size: pass max_size")
+    size = cs if cs >= 0 else int(max_size)
+    if out is None or out.numel() < size:
+        out = torch.empty(max(size, 1), dtype=torch.uint8, device=device)
+    _require(out, torch.uint8, "out")
+    dframe = torch.frombuffer(bytearray(b), dtype=torch.uint8).to(device) if b else \
+        torch.empty(1, dtype=torch.uint8, device=device)
+    need = int(_lib.lib().dpz_lz4_workspace_bytes(0, nb, 0 if linked else bmax))
+    ws = _lz4_ws(workspace, out.device, need)
+    n = ctypes.c_int64(0)
+    rc = _lib.lib().dpz_lz4_decompress(_ptr(dframe), b, len(b), _ptr(out), out.numel(),
+                                       ctypes.byref(n), _ptr(ws), ws.numel(), _stream(out.device))
+    if rc == _lib.DPZ_ERR_ARG:
+        raise ValueError("malformed LZ4 frame")
+    check(rc, "dpz_lz4_decompress")
+    return out[:n.value]
+
+
+def delta_i32(idx, out=None):
+    """``np.diff(idx, prepend=0).astype(np.int32)`` of a device int32 vector."""
+    _require(idx, torch.int32, "idx")
+    if out is None:
+        out = torch.empty_like(idx)
+    rc = _lib.lib().dpz_delta_i32(_ptr(idx), idx.numel(), _ptr(out), _stream(idx.device))
+    check(rc, "dpz_delta_i32")
+    return out
+
+
+def running_sum_i32(d, dtype=torch.int64, workspace=None):
+    """``np.cumsum`` of a device int32 vector as int64 (or truncated to int32)."""
+    _require(d, torch.int32, "d")
+    k = d.numel()
+    out = torch.empty(max(k, 1), dtype=dtype, device=d.device)
+    ws = _lz4_ws(workspace, d.device, int(_lib.lib().dpz_running_sum_workspace_bytes(k)))
+    rc = _lib.lib().dpz_running_sum_i32(_ptr(d), k, _ptr(out if dtype == torch.int64 else None),
+                                        _ptr(out if dtype == torch.int32 else None), _ptr(ws),
+                                        ws.numel(), _stream(d.device))
+    check(rc, "dpz_running_sum_i32")
+    return out[:k]
 
 
 class KernelTimer:

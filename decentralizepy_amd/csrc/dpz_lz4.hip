@@ -1,0 +1,663 @@
+// LZ4 frame codec on the device: the wire format of the reference's Lz4Wrapper compressor.
+//
+// Replaces (reference sacs-epfl/decentralizepy, src/decentralizepy/):
+//   compression/Lz4Wrapper.py:20-41   lz4.frame.compress(np.diff(sorted idx).tobytes())
+//   compression/Lz4Wrapper.py:43-61   np.cumsum(np.frombuffer(lz4.frame.decompress(b), int32))
+//   compression/Lz4Wrapper.py:63-98   the same frame codec on the fp32 value bytes
+// (python-lz4's lz4.frame, third-party, absent here; its frame format is the LZ4 frame spec and
+// its default preferences are: 64 KB blocks, linked, content size stored, no checksums).
+//
+// Encoder: the input is cut into independent 4 KB blocks, ONE WAVE per block (the frame says
+// B.Indep, so any LZ4 frame decoder — python-lz4 on a reference node included — reads it):
+//   1. the block is staged in LDS; every position i <= len - 12 hashes its 4 bytes (LZ4's
+//      multiplicative hash, 12 bits) 64 positions at a time: the candidate is the table entry
+//      left by earlier chunks, then the chunk publishes itself with LDS atomicMax (so the nearest
+//      earlier occurrence from a previous chunk wins — deterministic);
+//   2. each lane extends its candidate word-wise (min match 4, capped at 1024 and at len - 5) and
+//      sets its bit in a 4096-bit match mask;
+//   3. the greedy parse walks the mask with 64-bit bit scans (literal runs cost one scan, not one
+//      step per byte) and records the sequences in LDS;
+//   4. sequence sizes, a wave scan, and every lane emits its sequences into an LDS output buffer,
+//      copied out coalesced; a block that does not shrink is stored uncompressed (LZ4 frame
+//      high-bit block size).
+// A second launch scans the block sizes and assembles the frame (header, size-prefixed blocks,
+// end mark).  Decoder: the host walks the frame's block headers (it holds the bytes); linked
+// frames (python-lz4's default) decode in ONE workgroup block after block with a 64 KB LDS ring
+// window; independent frames decode one workgroup per block into per-block slots, then a scan
+// and a compaction.  Every read / write is bounds-checked; a malformed block sets *status.
+#include "dpz_common.h"
+
+namespace dpz {
+
+constexpr int LZ_BLK = 4096;        // encoder block (one wave)
+constexpr int LZ_HASH_LOG = 12;
+constexpr int LZ_MAXM = 1024;       // match length cap
+constexpr int LZ_MFLIMIT = 12;      // a match starts at least 12 bytes before the block end
+constexpr int LZ_LASTLIT = 5;       // the last 5 bytes are literals
+constexpr int LZ_BLK_OUT = LZ_BLK + 64;  // per-block encoder output slot (raw fallback fits)
+constexpr int LZ_MAXSEQ = LZ_BLK / 4;
+constexpr uint32_t LZ_MAGIC = 0x184D2204u;
+constexpr int LZ_HDR = 15;          // magic 4 + FLG + BD + content size 8 + HC
+
+// ---- encoder --------------------------------------------------------------------------------
+struct LzEncLds {
+  uint32_t data[LZ_BLK / 4 + 2];      // the block (+8 zero bytes of slack)
+  uint32_t table[1 << LZ_HASH_LOG];   // position + 1 of the latest occurrence (0 = none)
+  uint32_t minfo[LZ_BLK];             // (match length << 16) | offset, per position
+  unsigned long long mask[LZ_BLK / 64];
+  uint2 seq[LZ_MAXSEQ + 1];           // (literal start | literal length << 16, offset | ml << 16)
+  uint32_t nseq;
+};
+
+__device__ __forceinline__ uint32_t lz_read32(const uint32_t* w, int i) {
+  const int q = i >> 2, r = i & 3;
+  if (r == 0) return w[q];
+  return (w[q] >> (8 * r)) | (w[q + 1] << (32 - 8 * r));
+}
+
+__device__ __forceinline__ uint32_t lz_byte(const uint32_t* w, int i) {
+  return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+}
+
+__device__ __forceinline__ int lz_lenext(int L) { return L >= 15 ? (L - 15) / 255 + 1 : 0; }
+
+__device__ __forceinline__ void lz_put(uint8_t* ob, int pos, uint32_t v) { ob[pos] = (uint8_t)v; }
+
+// one wave per 4 KB block; blocks of 64 threads
+__global__ void __launch_bounds__(64) lz4_encode_blocks(const uint8_t* __restrict__ in, int64_t n,
+                                                       uint8_t* __restrict__ slots,
+                                                       uint32_t* __restrict__ bsize) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lz_smem[];
+  LzEncLds& S = *reinterpret_cast<LzEncLds*>(lz_smem);
+  const int lane = threadIdx.x;
+  const int64_t blk = blockIdx.x;
+  const int64_t base = blk * LZ_BLK;
+  const int len = (int)((n - base) < LZ_BLK ? (n - base) : LZ_BLK);
+  // stage the block (bytes -> words), zero the table and the mask
+  for (int w = lane; w < LZ_BLK / 4 + 2; w += 64) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = 4 * w + e;
+      if (i < len) v |= (uint32_t)in[base + i] << (8 * e);
+    }
+    S.data[w] = v;
+  }
+  for (int t = lane; t < (1 << LZ_HASH_LOG); t += 64) S.table[t] = 0;
+  for (int t = lane; t < LZ_BLK / 64; t += 64) S.mask[t] = 0ull;
+  __syncthreads();
+  const int last_start = len - LZ_MFLIMIT;  // match starts i <= last_start
+  const int mend = len - LZ_LASTLIT;        // a match ends at or before mend
+  for (int c0 = 0; c0 <= last_start; c0 += 64) {
+    const int i = c0 + lane;
+    const bool ok = i <= last_start;
+    uint32_t v = 0, h = 0, cand = 0;
+    if (ok) {
+      v = lz_read32(S.data, i);
+      h = (v * 2654435761u) >> (32 - LZ_HASH_LOG);
+      cand = S.table[h];
+    }
+    __syncthreads();
+    if (ok) atomicMax(&S.table[h], (uint32_t)(i + 1));
+    uint32_t info = 0;
+    if (ok && cand != 0) {
+      const int j = (int)cand - 1;
+      if (lz_read32(S.data, j) == v) {
+        int ml = 4;
+        const int cap = (mend - i) < LZ_MAXM ? (mend - i) : LZ_MAXM;
+        while (ml + 4 <= cap) {
+          const uint32_t x = lz_read32(S.data, i + ml) ^ lz_read32(S.data, j + ml);
+          if (x) {
+            ml += __builtin_ctz(x) >> 3;
+            break;
+          }
+          ml += 4;
+        }
+        if (ml + 4 > cap) {  // byte tail (or the capped word loop ran out)
+          while (ml < cap && lz_byte(S.data, i + ml) == lz_byte(S.data, j + ml)) ++ml;
+        }
+        if (ml > cap) ml = cap;
+        if (ml >= 4) info = ((uint32_t)ml << 16) | (uint32_t)(i - j);
+      }
+    }
+    if (ok) S.minfo[i] = info;
+    const unsigned long long bal = __ballot(info != 0);
+    if (lane == 0) S.mask[c0 >> 6] = bal;
+    __syncthreads();
+  }
+  __syncthreads();
+  // greedy parse (wave-uniform): jump from match end to the next match start by bit scans
+  uint32_t nseq = 0;
+  int p = 0, lit = 0;
+  for (;;) {
+    int q = -1;
+    if (p <= last_start) {
+      int wi = p >> 6;
+      unsigned long long w = S.mask[wi] & (~0ull << (p & 63));
+      const int wlast = last_start >> 6;
+      while (w == 0ull && wi < wlast) w = S.mask[++wi];
+      if (w != 0ull) q = (wi << 6) + __builtin_ctzll(w);
+    }
+    if (q < 0) break;
+    const uint32_t info = S.minfo[q];
+    const int ml = (int)(info >> 16), off = (int)(info & 0xFFFFu);
+    if (lane == 0)
+      S.seq[nseq] = make_uint2((uint32_t)lit | ((uint32_t)(q - lit) << 16),
+                               (uint32_t)off | ((uint32_t)ml << 16));
+    ++nseq;
+    p = q + ml;
+    lit = p;
+  }
+  // the last sequence: literals only
+  if (lane == 0) S.seq[nseq] = make_uint2((uint32_t)lit | ((uint32_t)(len - lit) << 16), 0u);
+  __syncthreads();
+  const uint32_t ns = nseq + 1;
+  // sizes and offsets of the sequences (wave scan in chunks of 64)
+  uint8_t* ob = reinterpret_cast<uint8_t*>(S.minfo);  // reuse: 16 KB >= LZ_BLK_OUT
+  uint32_t run = 0;
+  for (uint32_t s0 = 0; s0 < ns; s0 += 64) {
+    const uint32_t s = s0 + lane;
+    int sz = 0;
+    uint2 e = make_uint2(0, 0);
+    if (s < ns) {
+      e = S.seq[s];
+      const int L = (int)(e.x >> 16);
+      sz = 1 + lz_lenext(L) + L;
+      if (s + 1 < ns) sz += 2 + lz_lenext((int)(e.y >> 16) - 4);
+    }
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan((uint32_t)sz, &tot);
+    if (s < ns) {
+      int pos = (int)(run + ex);
+      if (run + ex + sz <= (uint32_t)LZ_BLK) {  // beyond: the block goes out raw anyway
+        const int lstart = (int)(e.x & 0xFFFFu), L = (int)(e.x >> 16);
+        const int M = s + 1 < ns ? (int)(e.y >> 16) - 4 : 0;
+        lz_put(ob, pos++, (uint32_t)((L >= 15 ? 15 : L) << 4) | (uint32_t)(M >= 15 ? 15 : M));
+        if (L >= 15) {
+          int r = L - 15;
+          for (; r >= 255; r -= 255) lz_put(ob, pos++, 255u);
+          lz_put(ob, pos++, (uint32_t)r);
+        }
+        for (int t = 0; t < L; ++t) lz_put(ob, pos++, lz_byte(S.data, lstart + t));
+        if (s + 1 < ns) {
+          const uint32_t off = e.y & 0xFFFFu;
+          lz_put(ob, pos++, off & 0xFFu);
+          lz_put(ob, pos++, off >> 8);
+          if (M >= 15) {
+            int r = M - 15;
+            for (; r >= 255; r -= 255) lz_put(ob, pos++, 255u);
+            lz_put(ob, pos++, (uint32_t)r);
+          }
+        }
+      }
+    }
+    run += tot;
+  }
+  __syncthreads();
+  const bool raw = run >= (uint32_t)len;
+  uint8_t* dst = slots + blk * LZ_BLK_OUT;
+  const int outn = raw ? len : (int)run;
+  for (int t = lane; t < outn; t += 64) dst[t] = raw ? (uint8_t)lz_byte(S.data, t) : ob[t];
+  if (lane == 0) bsize[blk] = (uint32_t)outn | (raw ? 0x80000000u : 0u);
+}
+
+// frame assembly: block offsets (one block scans), header, size-prefixed blocks, end mark
+__global__ void __launch_bounds__(256) lz4_frame_offsets(const uint32_t* __restrict__ bsize,
+                                                         int64_t nblk, uint64_t* __restrict__ boff,
+                                                         uint64_t* __restrict__ total) {
+  __shared__ uint64_t wsum[4];
+  uint64_t run = LZ_HDR;
+  for (int64_t b0 = 0; b0 < nblk; b0 += 256) {
+    const int64_t b = b0 + threadIdx.x;
+    const uint64_t v = b < nblk ? 4ull + (bsize[b] & 0x7FFFFFFFu) : 0ull;
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan64(v, wsum, &tot);
+    if (b < nblk) boff[b] = run + ex;
+    run += tot;
+  }
+  if (threadIdx.x == 0) *total = run + 4;  // + end mark
+}
+
+__global__ void __launch_bounds__(256) lz4_frame_write(const uint8_t* __restrict__ slots,
+                                                       const uint32_t* __restrict__ bsize,
+                                                       const uint64_t* __restrict__ boff,
+                                                       const uint64_t* __restrict__ total,
+                                                       int64_t nblk, uint8_t* __restrict__ out,
+                                                       uint32_t hdr_lo, uint32_t hdr_mid,
+                                                       uint64_t content) {
+  const int64_t b = blockIdx.x;
+  if (b == 0 && threadIdx.x < LZ_HDR) {
+    const int t = threadIdx.x;
+    uint8_t v;
+    if (t < 4) v = (uint8_t)(LZ_MAGIC >> (8 * t));
+    else if (t == 4) v = (uint8_t)(hdr_lo & 0xFF);          // FLG
+    else if (t == 5) v = (uint8_t)((hdr_lo >> 8) & 0xFF);   // BD
+    else if (t < 14) v = (uint8_t)(content >> (8 * (t - 6)));
+    else v = (uint8_t)(hdr_mid & 0xFF);                     // HC
+    out[t] = v;
+  }
+  if (b == 0 && threadIdx.x < 4) out[*total - 4 + threadIdx.x] = 0;  // end mark
+  if (b >= nblk) return;
+  const uint32_t sz = bsize[b];
+  const uint64_t o = boff[b];
+  if (threadIdx.x < 4) out[o + threadIdx.x] = (uint8_t)(sz >> (8 * threadIdx.x));
+  const uint32_t m = sz & 0x7FFFFFFFu;
+  const uint8_t* src = slots + b * LZ_BLK_OUT;
+  for (uint32_t t = threadIdx.x; t < m; t += 256) out[o + 4 + t] = src[t];
+}
+
+// ---- decoder ----------------------------------------------------------------------------------
+// One workgroup (64 threads) decodes the blocks [b0, b1) in order (b1 = b0 + 1 for independent
+// frames) with an LDS ring of the last 64 KB decoded (an LZ4 offset is < 2^16, and a match copy
+// never overwrites a ring slot it still has to read: the slot of position p is rewritten by
+// p + 65536 only).  Output goes to a per-block slot (independent) or out + the running offset
+// (linked).  The compressed block is staged in LDS.
+struct LzBlock {
+  int64_t in_off;   // first byte of the block data (after its 4-byte size)
+  uint32_t csize;   // compressed size
+  uint32_t raw;     // stored uncompressed
+};
+
+__device__ __forceinline__ uint32_t rd_in(const uint8_t* s, uint32_t i) { return s[i]; }
+
+__global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t* __restrict__ in,
+                                                        const LzBlock* __restrict__ blocks,
+                                                        int64_t nblk, int linked, uint32_t bmax,
+                                                        uint32_t win, uint8_t* __restrict__ out,
+                                                        uint64_t out_cap,
+                                                        uint64_t* __restrict__ dsize,
+                                                        uint32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lz_smem[];
+  uint8_t* ring = lz_smem;           // win bytes
+  uint8_t* cb = lz_smem + win;       // staged compressed block (bmax + 16)
+  const int lane = threadIdx.x;
+  const uint32_t wmask = win - 1;
+  int64_t b0 = linked ? 0 : blockIdx.x, b1 = linked ? nblk : blockIdx.x + 1;
+  uint64_t opos = 0;                 // bytes decoded so far by this workgroup (ring position)
+  uint64_t obase = linked ? 0 : (uint64_t)blockIdx.x * bmax;  // output slot
+  bool bad = false;
+  for (int64_t b = b0; b < b1 && !bad; ++b) {
+    const LzBlock B = blocks[b];
+    if (B.csize > bmax + 16 || (B.raw && B.csize > bmax)) { bad = true; break; }
+    for (uint32_t t = lane; t < B.csize; t += 64) cb[t] = in[B.in_off + t];
+    __syncthreads();
+    const uint64_t start = opos;
+    if (B.raw) {
+      for (uint32_t t = lane; t < B.csize; t += 64) {
+        ring[(opos + t) & wmask] = cb[t];
+        if (obase + opos + t < out_cap) out[obase + opos + t] = cb[t];
+      }
+      opos += B.csize;
+      __syncthreads();
+      if (!linked && lane == 0) dsize[b] = opos - start;
+      continue;
+    }
+    uint32_t ip = 0;
+    for (;;) {  // wave-uniform token walk
+      if (ip >= B.csize) { bad = true; break; }
+      const uint32_t tok = cb[ip++];
+      uint32_t L = tok >> 4;
+      if (L == 15) {
+        uint32_t x;
+        do {
+          if (ip >= B.csize) { bad = true; break; }
+          x = cb[ip++];
+          L += x;
+        } while (x == 255);
+        if (bad) break;
+      }
+      if (ip + L > B.csize || opos - start + L > bmax) { bad = true; break; }
+      for (uint32_t t = lane; t < L; t += 64) {
+        const uint8_t v = cb[ip + t];
+        ring[(opos + t) & wmask] = v;
+        if (obase + opos + t < out_cap) out[obase + opos + t] = v;
+      }
+      ip += L;
+      opos += L;
+      if (ip == B.csize) break;  // the last sequence has no match
+      if (ip + 2 > B.csize) { bad = true; break; }
+      const uint32_t off = (uint32_t)cb[ip] | ((uint32_t)cb[ip + 1] << 8);
+      ip += 2;
+      uint32_t M = (tok & 15u);
+      if (M == 15) {
+        uint32_t x;
+        do {
+          if (ip >= B.csize) { bad = true; break; }
+          x = cb[ip++];
+          M += x;
+        } while (x == 255);
+        if (bad) break;
+      }
+      M += 4;
+      const uint64_t hist = linked ? opos : opos - start;  // reachable history
+      if (off == 0 || off > hist || opos - start + M > bmax) { bad = true; break; }
+      __syncthreads();  // literal bytes in the ring before the match reads them
+      // out[opos + t] = out[opos - off + (t mod off)]: each byte independently
+      for (uint32_t t = lane; t < M; t += 64) {
+        const uint8_t v = ring[(opos - off + (t % off)) & wmask];
+        ring[(opos + t) & wmask] = v;
+        if (obase + opos + t < out_cap) out[obase + opos + t] = v;
+      }
+      opos += M;
+      __syncthreads();
+    }
+    __syncthreads();
+    if (!linked && lane == 0) dsize[b] = opos - start;
+  }
+  if (bad && lane == 0) atomicOr(status, 1u);
+  if (linked && lane == 0) dsize[0] = opos;
+}
+
+// independent frames: slot b (dsize[b] bytes at b * bmax) -> out + prefix
+__global__ void __launch_bounds__(256) lz4_gather_kernel(const uint8_t* __restrict__ slots,
+                                                         const uint64_t* __restrict__ dsize,
+                                                         int64_t nblk, uint32_t bmax,
+                                                         uint8_t* __restrict__ out,
+                                                         uint64_t out_cap,
+                                                         uint64_t* __restrict__ total) {
+  __shared__ uint64_t wsum[4];
+  __shared__ uint64_t base_sh;
+  // every block recomputes the prefix of the sizes before its slot range (nblk is small)
+  const int64_t b = blockIdx.x;
+  uint64_t before = 0, all = 0;
+  for (int64_t c0 = 0; c0 < nblk; c0 += 256) {
+    const int64_t c = c0 + threadIdx.x;
+    const uint64_t v = c < nblk ? dsize[c] : 0ull;
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan64(v, wsum, &tot);
+    if (c == b) base_sh = before + ex;
+    before += tot;
+  }
+  all = before;
+  __syncthreads();
+  const uint64_t o = base_sh, m = dsize[b];
+  for (uint64_t t = threadIdx.x; t < m; t += 256)
+    if (o + t < out_cap) out[o + t] = slots[(uint64_t)b * bmax + t];
+  if (b == 0 && threadIdx.x == 0) *total = all;
+}
+
+
+// ---- index deltas (Lz4Wrapper.compress: np.diff(sorted, prepend=0)) and their running sum ----
+__global__ void __launch_bounds__(256) delta_i32_kernel(const int32_t* __restrict__ in, int64_t k,
+                                                        int32_t* __restrict__ out) {
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < k; j += (int64_t)gridDim.x * 256)
+    out[j] = (int32_t)((uint32_t)in[j] - (j ? (uint32_t)in[j - 1] : 0u));  // int32 wrap as numpy
+}
+
+constexpr int PS_TILE = 4096;  // elements per block of the running-sum kernels
+
+__global__ void __launch_bounds__(256) psum_tiles_kernel(const int32_t* __restrict__ in, int64_t k,
+                                                         int64_t* __restrict__ tsum) {
+  __shared__ uint64_t wsum[4];
+  const int64_t t0 = (int64_t)blockIdx.x * PS_TILE;
+  int64_t acc = 0;
+  for (int e = threadIdx.x; e < PS_TILE; e += 256)
+    if (t0 + e < k) acc += in[t0 + e];
+  uint64_t tot;
+  block_excl_scan64((uint64_t)acc, wsum, &tot);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = (int64_t)tot;
+}
+
+__global__ void __launch_bounds__(256) psum_scan_kernel(int64_t* __restrict__ tsum, int64_t nt) {
+  __shared__ uint64_t wsum[4];
+  uint64_t run = 0;
+  for (int64_t b0 = 0; b0 < nt; b0 += 256) {
+    const int64_t b = b0 + threadIdx.x;
+    const uint64_t v = b < nt ? (uint64_t)tsum[b] : 0ull;
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan64(v, wsum, &tot);
+    if (b < nt) tsum[b] = (int64_t)(run + ex);
+    run += tot;
+  }
+}
+
+// inclusive running sum: out64[j] = sum in[0..j] (int64, numpy's cumsum of int32), out32 too
+__global__ void __launch_bounds__(256) psum_write_kernel(const int32_t* __restrict__ in, int64_t k,
+                                                         const int64_t* __restrict__ tsum,
+                                                         int64_t* out64, int32_t* out32) {
+  __shared__ uint64_t wsum[4];
+  const int64_t t0 = (int64_t)blockIdx.x * PS_TILE;
+  constexpr int PER = PS_TILE / 256;
+  int64_t v[PER];
+  int64_t acc = 0;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int64_t j = t0 + (int64_t)threadIdx.x * PER + e;
+    v[e] = j < k ? in[j] : 0;
+    acc += v[e];
+  }
+  uint64_t tot;
+  int64_t run = tsum[blockIdx.x] + (int64_t)block_excl_scan64((uint64_t)acc, wsum, &tot);
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int64_t j = t0 + (int64_t)threadIdx.x * PER + e;
+    run += v[e];
+    if (j < k) {
+      if (out64) out64[j] = run;
+      if (out32) out32[j] = (int32_t)run;
+    }
+  }
+}
+
+// xxHash32 (seed 0) of a short buffer: the frame descriptor checksum
+static uint32_t xxh32_small(const uint8_t* p, int len) {
+  const uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u,
+                 P5 = 374761393u;
+  auto rotl = [](uint32_t x, int r) { return (x << r) | (x >> (32 - r)); };
+  uint32_t h = P5 + (uint32_t)len;
+  int i = 0;
+  for (; i + 4 <= len; i += 4) {
+    const uint32_t v = (uint32_t)p[i] | ((uint32_t)p[i + 1] << 8) | ((uint32_t)p[i + 2] << 16) |
+                       ((uint32_t)p[i + 3] << 24);
+    h += v * P3;
+    h = rotl(h, 17) * P4;
+  }
+  for (; i < len; ++i) {
+    h += p[i] * P5;
+    h = rotl(h, 11) * P1;
+  }
+  h ^= h >> 15;
+  h *= P2;
+  h ^= h >> 13;
+  h *= P3;
+  h ^= h >> 16;
+  return h;
+}
+
+}  // namespace dpz
+
+using namespace dpz;
+
+extern "C" int64_t dpz_lz4_max_bytes(int64_t n) {
+  if (n < 0) return -1;
+  const int64_t nblk = (n + LZ_BLK - 1) / LZ_BLK;
+  return LZ_HDR + nblk * (4 + LZ_BLK) + 4 + 16;
+}
+
+extern "C" size_t dpz_lz4_workspace_bytes(int64_t n, int64_t nblk_in, int64_t bmax) {
+  // encoder: per-block slots + sizes + offsets; decoder: block table + sizes + slots
+  const int64_t nb_e = (n + LZ_BLK - 1) / LZ_BLK + 1;
+  const size_t enc = (size_t)nb_e * LZ_BLK_OUT + (size_t)nb_e * 4 + (size_t)nb_e * 8 + 64;
+  const size_t dec = (size_t)(nblk_in + 1) * (sizeof(LzBlock) + 8) + (size_t)(nblk_in + 1) * bmax + 512;
+  const size_t w = enc > dec ? enc : dec;
+  return (w + 255) & ~(size_t)255;
+}
+
+extern "C" int dpz_lz4_compress(const uint8_t* in, int64_t n, uint8_t* out, int64_t out_cap,
+                                int64_t* nbytes_host, void* ws, size_t ws_bytes,
+                                dpz_stream_t stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (n < 0 || (n > 0 && !in) || !out || !nbytes_host) return DPZ_ERR_ARG;
+  if (out_cap < dpz_lz4_max_bytes(n)) return DPZ_ERR_ARG;
+  const int64_t nblk = (n + LZ_BLK - 1) / LZ_BLK;
+  if (ws_bytes < dpz_lz4_workspace_bytes(n, 0, 0) || !ws) return DPZ_ERR_WORKSPACE;
+  uint8_t* w8 = static_cast<uint8_t*>(ws);
+  uint8_t* slots = w8;
+  uint32_t* bsize = reinterpret_cast<uint32_t*>(w8 + (size_t)(nblk + 1) * LZ_BLK_OUT);
+  uint64_t* boff = reinterpret_cast<uint64_t*>(
+      w8 + (((size_t)(nblk + 1) * LZ_BLK_OUT + (size_t)(nblk + 1) * 4 + 7) & ~(size_t)7));
+  uint64_t* total = boff + nblk + 1;
+  // descriptor: FLG = version 01, B.Indep, C.Size; BD = 64 KB max block
+  uint8_t desc[10];
+  desc[0] = 0x40 | 0x20 | 0x08;
+  desc[1] = 0x40;
+  for (int i = 0; i < 8; ++i) desc[2 + i] = (uint8_t)((uint64_t)n >> (8 * i));
+  const uint32_t hc = (xxh32_small(desc, 10) >> 8) & 0xFF;
+  if (nblk > 0) {
+    DPZ_TIMED(DPZ_KT_LZ4, st, lz4_encode_blocks<<<(unsigned)nblk, 64, sizeof(LzEncLds), st>>>(
+                                  in, n, slots, bsize));
+  }
+  DPZ_TIMED(DPZ_KT_LZ4, st, lz4_frame_offsets<<<1, 256, 0, st>>>(bsize, nblk, boff, total));
+  DPZ_TIMED(DPZ_KT_LZ4, st, lz4_frame_write<<<(unsigned)(nblk > 0 ? nblk : 1), 256, 0, st>>>(
+                                slots, bsize, boff, total, nblk, out,
+                                (uint32_t)desc[0] | ((uint32_t)desc[1] << 8), hc, (uint64_t)n));
+  uint64_t tot = 0;
+  DPZ_HIP_TRY(hipMemcpyAsync(&tot, total, 8, hipMemcpyDeviceToHost, st));
+  DPZ_HIP_TRY(hipStreamSynchronize(st));
+  *nbytes_host = (int64_t)tot;
+  return DPZ_OK;
+}
+
+extern "C" int dpz_lz4_frame_info(const uint8_t* frame_host, int64_t nbytes, int64_t* content_size,
+                                  int64_t* nblk, int* linked, int64_t* block_max) {
+  if (!frame_host || nbytes < 7 || !content_size || !nblk || !linked || !block_max)
+    return DPZ_ERR_ARG;
+  const uint8_t* p = frame_host;
+  const uint32_t magic = p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24);
+  if (magic != LZ_MAGIC) return DPZ_ERR_ARG;
+  const uint8_t flg = p[4], bd = p[5];
+  if ((flg >> 6) != 1 || (flg & 0x02) || (bd & 0x8F)) return DPZ_ERR_ARG;
+  const int bmax_id = (bd >> 4) & 7;
+  if (bmax_id < 4) return DPZ_ERR_ARG;
+  const bool csize = flg & 0x08, dict = flg & 0x01, bsum = flg & 0x10;
+  int64_t pos = 6;
+  int64_t cs = -1;
+  if (csize) {
+    if (nbytes < pos + 8) return DPZ_ERR_ARG;
+    cs = 0;
+    for (int i = 0; i < 8; ++i) cs |= (int64_t)p[pos + i] << (8 * i);
+    pos += 8;
+  }
+  if (dict) pos += 4;
+  if (nbytes < pos + 1) return DPZ_ERR_ARG;
+  if ((uint8_t)((xxh32_small(p + 4, (int)(pos - 4)) >> 8) & 0xFF) != p[pos]) return DPZ_ERR_ARG;
+  pos += 1;
+  int64_t nb = 0;
+  for (;;) {
+    if (nbytes < pos + 4) return DPZ_ERR_ARG;
+    const uint32_t sz = p[pos] | (p[pos + 1] << 8) | (p[pos + 2] << 16) | ((uint32_t)p[pos + 3] << 24);
+    pos += 4;
+    if (sz == 0) break;
+    pos += (sz & 0x7FFFFFFFu) + (bsum ? 4 : 0);
+    if (pos > nbytes) return DPZ_ERR_ARG;
+    ++nb;
+  }
+  *content_size = cs;
+  *nblk = nb;
+  *linked = (flg & 0x20) ? 0 : 1;
+  *block_max = (int64_t)1 << (8 + 2 * bmax_id);
+  return DPZ_OK;
+}
+
+extern "C" int dpz_lz4_decompress(const uint8_t* frame_dev, const uint8_t* frame_host,
+                                  int64_t nbytes, uint8_t* out, int64_t out_cap,
+                                  int64_t* n_host, void* ws, size_t ws_bytes,
+                                  dpz_stream_t stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!frame_dev || !n_host || out_cap < 0 || (out_cap > 0 && !out)) return DPZ_ERR_ARG;
+  int64_t cs, nb, bmax;
+  int linked;
+  int rc = dpz_lz4_frame_info(frame_host, nbytes, &cs, &nb, &linked, &bmax);
+  if (rc != DPZ_OK) return rc;
+  if (ws_bytes < dpz_lz4_workspace_bytes(0, nb, linked ? 0 : bmax) || !ws) return DPZ_ERR_WORKSPACE;
+  const uint8_t flg = frame_host[4];
+  const bool bsum = flg & 0x10;
+  // block table from the host bytes
+  LzBlock* tab_h = static_cast<LzBlock*>(malloc(sizeof(LzBlock) * (size_t)(nb + 1)));
+  if (!tab_h) return DPZ_ERR_INTERNAL;
+  int64_t pos = 6 + ((flg & 0x08) ? 8 : 0) + ((flg & 0x01) ? 4 : 0) + 1;
+  for (int64_t b = 0; b < nb; ++b) {
+    const uint8_t* p = frame_host + pos;
+    const uint32_t sz = p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24);
+    tab_h[b].in_off = pos + 4;
+    tab_h[b].csize = sz & 0x7FFFFFFFu;
+    tab_h[b].raw = sz >> 31;
+    pos += 4 + (sz & 0x7FFFFFFFu) + (bsum ? 4 : 0);
+  }
+  uint8_t* w8 = static_cast<uint8_t*>(ws);
+  LzBlock* tab = reinterpret_cast<LzBlock*>(w8);
+  uint64_t* dsize = reinterpret_cast<uint64_t*>(w8 + sizeof(LzBlock) * (size_t)(nb + 1));
+  uint32_t* status = reinterpret_cast<uint32_t*>(dsize + nb + 1);
+  uint64_t* total = reinterpret_cast<uint64_t*>(status + 2);
+  uint8_t* slots = reinterpret_cast<uint8_t*>(total + 1);
+  slots = reinterpret_cast<uint8_t*>(((uintptr_t)slots + 255) & ~(uintptr_t)255);
+  uint32_t maxc_all = 0;
+  for (int64_t b = 0; b < nb; ++b) maxc_all = maxc_all > tab_h[b].csize ? maxc_all : tab_h[b].csize;
+  const uint32_t* csz = &maxc_all;
+  hipError_t e = hipMemcpyAsync(tab, tab_h, sizeof(LzBlock) * (size_t)(nb > 0 ? nb : 1),
+                                hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemsetAsync(status, 0, 16, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);  // tab_h is freed below
+  free(tab_h);
+  if (e != hipSuccess) return (int)e;
+  uint64_t tot = 0;
+  uint32_t bad = 0;
+  if (nb > 0) {
+    // ring of 64 KB (smaller when every block is: independent frames whose block max is
+    // smaller) + the largest compressed block
+    const uint32_t maxc = *csz;
+    const uint32_t win = 65536;
+    const size_t shm = (size_t)win + (size_t)maxc + 16;
+    if (bmax > 65536 || shm > 160 * 1024) return DPZ_ERR_UNSUPPORTED;
+    DPZ_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(lz4_decode_kernel),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    if (linked) {
+      DPZ_TIMED(DPZ_KT_LZ4, st, lz4_decode_kernel<<<1, 64, shm, st>>>(
+                                    frame_dev, tab, nb, 1, (uint32_t)bmax, win, out,
+                                    (uint64_t)out_cap, total, status));
+    } else {
+      DPZ_TIMED(DPZ_KT_LZ4, st, lz4_decode_kernel<<<(unsigned)nb, 64, shm, st>>>(
+                                    frame_dev, tab, nb, 0, (uint32_t)bmax, win, slots,
+                                    (uint64_t)nb * bmax, dsize, status));
+      DPZ_TIMED(DPZ_KT_LZ4, st, lz4_gather_kernel<<<(unsigned)nb, 256, 0, st>>>(
+                                    slots, dsize, nb, (uint32_t)bmax, out, (uint64_t)out_cap,
+                                    total));
+    }
+    DPZ_HIP_TRY(hipMemcpyAsync(&tot, total, 8, hipMemcpyDeviceToHost, st));
+    DPZ_HIP_TRY(hipMemcpyAsync(&bad, status, 4, hipMemcpyDeviceToHost, st));
+    DPZ_HIP_TRY(hipStreamSynchronize(st));
+  }
+  if (bad) return DPZ_ERR_ARG;
+  if (cs >= 0 && (int64_t)tot != cs) return DPZ_ERR_ARG;
+  if ((int64_t)tot > out_cap) return DPZ_ERR_WORKSPACE;
+  *n_host = (int64_t)tot;
+  return DPZ_OK;
+}
+
+extern "C" int dpz_delta_i32(const int32_t* in, int64_t k, int32_t* out, dpz_stream_t stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (k < 0 || (k > 0 && (!in || !out)) || in == out) return DPZ_ERR_ARG;
+  if (k == 0) return DPZ_OK;
+  int64_t g = (k + 255) / 256;
+  if (g > 4096) g = 4096;
+  DPZ_TIMED(DPZ_KT_LZ4, st, delta_i32_kernel<<<(unsigned)g, 256, 0, st>>>(in, k, out));
+  return DPZ_OK;
+}
+
+extern "C" size_t dpz_running_sum_workspace_bytes(int64_t k) {
+  return (size_t)(((k + PS_TILE - 1) / PS_TILE) + 1) * 8 + 256;
+}
+
+extern "C" int dpz_running_sum_i32(const int32_t* in, int64_t k, int64_t* out64, int32_t* out32,
+                                   void* ws, size_t ws_bytes, dpz_stream_t stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (k < 0 || (k > 0 && (!in || (!out64 && !out32)))) return DPZ_ERR_ARG;
+  if (k == 0) return DPZ_OK;
+  if (!ws || ws_bytes < dpz_running_sum_workspace_bytes(k)) return DPZ_ERR_WORKSPACE;
+  const int64_t nt = (k + PS_TILE - 1) / PS_TILE;
+  int64_t* tsum = static_cast<int64_t*>(ws);
+  DPZ_TIMED(DPZ_KT_LZ4, st, psum_tiles_kernel<<<(unsigned)nt, 256, 0, st>>>(in, k, tsum));
+  DPZ_TIMED(DPZ_KT_LZ4, st, psum_scan_kernel<<<1, 256, 0, st>>>(tsum, nt));
+  DPZ_TIMED(DPZ_KT_LZ4, st, psum_write_kernel<<<(unsigned)nt, 256, 0, st>>>(in, k, tsum, out64, out32));
+  return DPZ_OK;
+}

@@ -293,7 +293,7 @@ enum {
   DPZ_KT_FOLD_OFFSETS, DPZ_KT_FOLD, DPZ_KT_DWT, DPZ_KT_IDWT, DPZ_KT_ELIAS_COUNT,
   DPZ_KT_ELIAS_SCAN, DPZ_KT_ELIAS_PACK, DPZ_KT_ELIAS_SPEC, DPZ_KT_ELIAS_RESOLVE,
   DPZ_KT_ELIAS_WRITE, DPZ_KT_FP16, DPZ_KT_SCATTER, DPZ_KT_FPZ_SIZE, DPZ_KT_FPZ_SCAN,
-  DPZ_KT_FPZ_PACK, DPZ_KT_FPZ_DECODE, DPZ_KT_CPLX, DPZ_KT_FFT_SCALE, DPZ_KT_HAAR, DPZ_KT_COUNT
+  DPZ_KT_FPZ_PACK, DPZ_KT_FPZ_DECODE, DPZ_KT_CPLX, DPZ_KT_FFT_SCALE, DPZ_KT_HAAR, DPZ_KT_LZ4, DPZ_KT_COUNT
 };
 int dpz_timing_enable(int on);  /* also clears the accumulators */
 int dpz_timing_read(double* ms_sum, int64_t* count, int max_ids);
@@ -372,6 +372,43 @@ int dpz_cplx_gather(const float* src, int64_t m, const int32_t* idx, int64_t k, 
 /* pair[2j] = 2 idx[j], pair[2j+1] = 2 idx[j] + 1 (8-byte aligned pair): a complex payload as a
  * float payload of the interleaved view, for dpz_decode_average.                                  */
 int dpz_cplx_pair_indices(const int32_t* idx, int64_t k, int32_t* pair, dpz_stream_t stream);
+
+/* ---- LZ4 frames (the wire format of compression/Lz4Wrapper.py:20-98, lz4.frame) -------------
+ * Encoder: independent 4 KB blocks, one wave each (B.Indep, BD = 64 KB, content size stored, no
+ * checksums): a valid LZ4 frame any decoder reads; the bytes are this build's (greedy parse over a
+ * 12-bit hash of 4-byte words; python-lz4's match finder is not reproduced, so byte parity is
+ * unpinned).  Decoder: any LZ4 frame with 64 KB (or smaller) blocks, linked (python-lz4's
+ * default, decoded by one workgroup) or independent (one workgroup per block); content and
+ * block checksums are skipped, dictionary IDs rejected.                                         */
+/* Upper bound of the frame size for n input bytes. */
+int64_t dpz_lz4_max_bytes(int64_t n);
+/* Device workspace for an encode of n bytes (nblk = bmax = 0) or a decode of a frame of nblk
+ * blocks of at most bmax bytes (n = 0); the max of what the calls ask is always enough.       */
+size_t dpz_lz4_workspace_bytes(int64_t n, int64_t nblk, int64_t bmax);
+/* in: device bytes[n]; out: device, out_cap >= dpz_lz4_max_bytes(n).  The frame length goes to
+ * *nbytes_host (host; synchronises).                                                            */
+int dpz_lz4_compress(const uint8_t* in, int64_t n, uint8_t* out, int64_t out_cap,
+                     int64_t* nbytes_host, void* ws, size_t ws_bytes, dpz_stream_t stream);
+/* Frame header and block walk of a HOST copy of a frame: content size (-1 if absent), block
+ * count, linked flag, block max.  DPZ_ERR_ARG on a malformed frame (bad magic, version, header
+ * checksum, truncated blocks).                                                                  */
+int dpz_lz4_frame_info(const uint8_t* frame_host, int64_t nbytes, int64_t* content_size,
+                       int64_t* nblk, int* linked, int64_t* block_max);
+/* frame_dev / frame_host: the same nbytes of frame on the device and on the host (the host walks
+ * the block headers).  Writes the content to out (device) and its length to *n_host (host;
+ * synchronises).  DPZ_ERR_ARG on a malformed block or a content-size mismatch,
+ * DPZ_ERR_WORKSPACE if the content exceeds out_cap, DPZ_ERR_UNSUPPORTED above 64 KB blocks.   */
+int dpz_lz4_decompress(const uint8_t* frame_dev, const uint8_t* frame_host, int64_t nbytes,
+                       uint8_t* out, int64_t out_cap, int64_t* n_host, void* ws, size_t ws_bytes,
+                       dpz_stream_t stream);
+/* out[j] = in[j] - in[j-1] (in[-1] = 0), int32 wrap-around: np.diff(a, prepend=0).astype(int32)
+ * (Lz4Wrapper.py:35-37).  in and out must not alias.                                           */
+int dpz_delta_i32(const int32_t* in, int64_t k, int32_t* out, dpz_stream_t stream);
+/* Inclusive running sum of int32 values as int64 (np.cumsum, Lz4Wrapper.py:58-59) into out64
+ * and / or its int32 truncation into out32 (either may be NULL).                                */
+size_t dpz_running_sum_workspace_bytes(int64_t k);
+int dpz_running_sum_i32(const int32_t* in, int64_t k, int64_t* out64, int32_t* out32, void* ws,
+                        size_t ws_bytes, dpz_stream_t stream);
 
 #ifdef __cplusplus
 }

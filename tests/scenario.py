@@ -233,6 +233,12 @@ def _elias_wire(msgs, check_cls):
     out = []
     for m in msgs:
         m = dict(m)
+        if check_cls == "Lz4Wrapper":  # liblz4 frames, as a reference node's lz4.frame sends
+            from oracle import lz4 as olz4
+            if "indices" in m:
+                m["indices"] = olz4.wrapper_compress(np.array(m["indices"], dtype=np.int32))
+            out.append(m)
+            continue
         if "indices" in m:
             m["indices"] = oelias.encode(m["indices"])
         if check_cls == "EliasFpzip" and "params" in m:
@@ -242,9 +248,11 @@ def _elias_wire(msgs, check_cls):
 
 
 def replay_plugin(name, tmpdir, compression_class=None, config=None):
-    """Drive the device plugin through the scenario; with ``compression_class`` ("Elias" or
-    "EliasFpzip" of decentralizepy_amd.compression) the wire payloads are compressed and the
-    outgoing index stream is checked against the oracle's reference-pinned Elias bytes.
+    """Drive the device plugin through the scenario; with ``compression_class`` ("Elias",
+    "EliasFpzip" or "Lz4Wrapper" of decentralizepy_amd.compression) the wire payloads are
+    compressed and the outgoing index stream is checked against the oracle's reference-pinned
+    Elias bytes (Lz4Wrapper: decoded by liblz4 and by the oracle's frame decoder; the neighbour
+    messages arrive as liblz4 frames).
     ``config`` = (package, class, kwargs) from sharing_section(): the plugin is built the way
     Node.init_sharing builds it (importlib, keyword arguments from the config file)."""
     import torch  # noqa: F401
@@ -274,7 +282,12 @@ def replay_plugin(name, tmpdir, compression_class=None, config=None):
         data = plugin.get_data_to_send(degree=3)
         if compression_class:
             data = dict(data)
-            if "indices" in data:
+            if "indices" in data and compression_class == "Lz4Wrapper":
+                from oracle import lz4 as olz4
+                np.testing.assert_array_equal(olz4.wrapper_decompress(data["indices"]),
+                                              arrays[f"r{r}_indices"])
+                assert olz4.ref_decompress(data["indices"]) == olz4.decode_frame(data["indices"])
+            elif "indices" in data:
                 np.testing.assert_array_equal(np.asarray(data["indices"]),
                                               oelias.encode(arrays[f"r{r}_indices"]))
             if compression_class == "EliasFpzip" and "params" in data:
