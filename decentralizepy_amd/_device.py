@@ -70,6 +70,35 @@ def to_device_flat(flat_cpu, device, staging, name):
     return out
 
 
+def h2d_array(arr, dtype, device, staging, name):
+    """H2D of a host numpy array (a received payload leg) through the pinned buffer ``name``:
+    the host copy into pinned memory, then an asynchronous DMA on the current stream, so the
+    caller's host work on the next payload (unpickled dict, decompression) overlaps this DMA
+    (reference wire boundary: node/DPSGDNode.py receive -> Sharing._averaging).  The buffer is
+    not reused before its DMA has completed (Staging events)."""
+    a = np.ascontiguousarray(arr, dtype=dtype)
+    tdt = torch.from_numpy(a[:0]).dtype
+    host = staging.get(name, a.size, tdt)
+    host.numpy()[...] = a.reshape(-1)
+    out = host.to(device, non_blocking=True)
+    staging.mark(name, tdt, torch.cuda.current_stream(device))
+    return out
+
+
+class PayloadNames:
+    """Pinned-buffer names for received payload legs: a ring of ``slots`` names, so consecutive
+    legs use distinct buffers and a reused buffer waits only for its own earlier DMA (Staging);
+    the pinned memory stays bounded."""
+
+    def __init__(self, slots=64):
+        self.i = 0
+        self.slots = slots
+
+    def __call__(self, leg):
+        self.i = (self.i + 1) % self.slots
+        return f"pay{self.i}_{leg}"
+
+
 def to_host(t, staging, name):
     """D2H into a pinned buffer; returns a numpy array that owns its memory."""
     host = staging.get(name, t.numel(), t.dtype)

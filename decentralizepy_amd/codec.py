@@ -651,9 +651,8 @@ def lz4_decompress(frame, device, out=None, workspace=None, max_size=None):
     64 KB are supported."""
     b = bytes(frame)
     cs, nb, linked, bmax = lz4_frame_info(b)
-    if cs < 0 and max_size is None:
-        raise ValueError("frame without a content size: pass max_size")
-    size = cs if cs >= 0 else int(max_size)
+    # without a stored content size the blocks bound it (each decodes to at most bmax bytes)
+    size = cs if cs >= 0 else (int(max_size) if max_size is not None else nb * bmax)
     if out is None or out.numel() < size:
         out = torch.empty(max(size, 1), dtype=torch.uint8, device=device)
     _require(out, torch.uint8, "out")

@@ -126,15 +126,10 @@ class Choco(Sharing):
 
     def _device_message(self, data):
         data = self.decompress_data(data)
-        vals = torch.from_numpy(np.ascontiguousarray(data["params"], dtype=np.float32))
+        vals = self._h2d(data["params"], np.float32, "vals")
         if "send_partial" not in data:  # a full model (Sharing.deserialized_model)
-            return None, vals.to(self.device)
-        idx = data["indices"]
-        if isinstance(idx, torch.Tensor):
-            idx = idx.to(self.device, torch.int32)
-        else:
-            idx = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int32)).to(self.device)
-        return idx, vals.to(self.device)
+            return None, vals
+        return self._h2d(data["indices"], np.int32, "idx"), vals
 
     def _averaging(self, peer_deques):
         """reference Choco.py:412-447"""

@@ -137,17 +137,9 @@ class FFT(PartialModel):
     # ---- receive side ---------------------------------------------------------------------------
     def _device_payload(self, data):
         """Complex payload -> (float-pair idx int32[2k] or None, fp32 view of the values)."""
-        vals = data["params"]
-        if not isinstance(vals, torch.Tensor):
-            vals = torch.from_numpy(np.ascontiguousarray(vals, dtype=np.complex64))
-        vals = vals.to(self.device, torch.complex64, non_blocking=True).reshape(-1)
+        vals = self._h2d(data["params"], np.complex64, "vals")
         idx = data["indices"]  # a full payload raises KeyError, as in the reference (FFT.py:234)
-        if isinstance(idx, torch.Tensor):
-            idx = idx.to(self.device, torch.int32)
-        else:
-            idx = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int32))
-            idx = idx.to(self.device, non_blocking=True)
-        return codec.cplx_pair_indices(idx), vals.view(torch.float32)
+        return codec.cplx_pair_indices(self._h2d(idx, np.int32, "idx")), vals.view(torch.float32)
 
     def _averaging(self, peer_deques):
         """reference FFT.py:252-302: Metro-Hastings fold of the coefficients, then irfft."""

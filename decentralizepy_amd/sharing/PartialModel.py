@@ -205,16 +205,8 @@ class PartialModel(Sharing):
     def _device_payload(self, data):
         if "send_partial" not in data:
             return super()._device_payload(data)
-        vals = data["params"]
-        if not isinstance(vals, torch.Tensor):  # decoded on the device by the compressor
-            vals = torch.from_numpy(np.ascontiguousarray(vals, dtype=np.float32))
-        idx = data["indices"]
-        if isinstance(idx, torch.Tensor):  # decoded on the device by the compressor
-            idx = idx.to(self.device, torch.int32)
-        else:
-            idx = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int32))
-            idx = idx.to(self.device, non_blocking=True)
-        return idx, vals.to(self.device, non_blocking=True)
+        return self._h2d(data["indices"], np.int32, "idx"), self._h2d(data["params"], np.float32,
+                                                                        "vals")
 
     def deserialized_model(self, m):
         """Received dict -> state_dict: ``T = cat(local); T[idx] = params`` on the device

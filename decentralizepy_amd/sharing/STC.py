@@ -106,13 +106,7 @@ class STC(Sharing):
 
     def _device_sparse(self, m):
         """(idx int32 device, vals fp32 device) of a received, decompressed message."""
-        idx = m["indices"]
-        if isinstance(idx, torch.Tensor):
-            idx = idx.to(self.device, torch.int32)
-        else:
-            idx = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int32)).to(self.device)
-        vals = torch.from_numpy(np.ascontiguousarray(m["params"], dtype=np.float32))
-        return idx, vals.to(self.device)
+        return self._h2d(m["indices"], np.int32, "idx"), self._h2d(m["params"], np.float32, "vals")
 
     def _encode_change(self):
         """top-k of model_change (STC.py:158-174): (idx, vals) device tensors."""

@@ -18,7 +18,8 @@ import numpy as np
 import torch
 
 from .. import codec
-from .._device import Staging, flatten_state, pick_device, to_device_flat, to_host
+from .._device import (PayloadNames, Staging, flatten_state, h2d_array, pick_device,
+                       to_device_flat, to_host)
 
 
 class Sharing:
@@ -58,6 +59,7 @@ class Sharing:
 
         self.device = pick_device(rank)
         self.staging = Staging()
+        self._pay_names = PayloadNames()
         self.workspace = codec.Workspace(self.device)
         if hasattr(getattr(self, "compressor", None), "_dev"):
             self.compressor.device = self.device  # device compressors run on this node's GPU
@@ -123,13 +125,16 @@ class Sharing:
             flat = flatten_state(self.model.state_dict())
         return to_device_flat(flat, self.device, self.staging, "local")
 
+    def _h2d(self, arr, dtype, leg):
+        """A host payload leg to the device through a pinned buffer (async DMA, overlapping the
+        host work on the next payload); device tensors (decoded by a device compressor) stay."""
+        if isinstance(arr, torch.Tensor):
+            return arr.to(self.device, torch.from_numpy(np.zeros(0, dtype)).dtype).reshape(-1)
+        return h2d_array(arr, dtype, self.device, self.staging, self._pay_names(leg))
+
     def _device_payload(self, data):
         """Received (decompressed) payload dict -> (idx int32 device or None, vals fp32 device)."""
-        vals = data["params"]
-        if isinstance(vals, torch.Tensor):  # decoded on the device by the compressor
-            return None, vals.to(self.device, torch.float32).reshape(-1)
-        vals = torch.from_numpy(np.ascontiguousarray(vals, dtype=np.float32))
-        return None, vals.to(self.device, non_blocking=True)
+        return None, self._h2d(data["params"], np.float32, "params")
 
     def _pop_payloads(self, peer_deques):
         payloads, degrees = [], []
