@@ -40,7 +40,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-extra", action="store_true",
                    help="skip the 64 MiB secondary line and the C4 gossip-round object")
-    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "e2e", "shard"], default="c2",
+    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "e2e", "shard", "fft", "wire"],
+                   default="c2",
                    help="c2: one node's 11M tensor per GPU (default); c4: the 96-node gossip "
                         "round of eval/96_regular.edges sharded over the GPUs; c3: JWINS wavelet "
                         "25M + 16-payload decode; c5: 256 MiB, 0.1%%, fp16 values; e2e: "
@@ -333,12 +334,17 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         return
-    if args.workload in ("c3", "c5", "e2e", "shard"):
+    if args.workload in ("c3", "c5", "e2e", "shard", "fft", "wire"):
         import bench_workloads as bw
-        if args.workload == "shard":
+        if args.workload == "fft":
+            r = bw.fft_case(dev, steps=min(args.steps, 30))
+        elif args.workload == "wire":
+            r = bw.wire_case(dev)
+        elif args.workload == "shard":
             r = bw.shard_case(dev, rank, world, dist, steps=min(args.steps, 40))
         elif args.workload == "c3":
             r = [bw.c3_case(dev, alpha=a, steps=min(args.steps, 40)) for a in (0.01, 0.1)]
+            r.append(bw.c3_case(dev, alpha=0.01, steps=min(args.steps, 40), wavelet="haar"))
         elif args.workload == "c5":
             r = bw.c5_case(dev, steps=min(args.steps, 40), streams=args.streams)
         else:

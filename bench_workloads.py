@@ -24,7 +24,7 @@ def _sync_time(fn, steps):
     return (time.perf_counter() - t0) / steps
 
 
-def c3_case(dev, n=25_000_000, alpha=0.01, npay=16, steps=40, warmup=5, seed=3):
+def c3_case(dev, n=25_000_000, alpha=0.01, npay=16, steps=40, warmup=5, seed=3, wavelet="sym2"):
     """C3: one JWINS receiver round on an N-parameter model (reference Wavelet.py:142-329 with
     the tutorial/JWINS/config.ini settings change_based_selection, accumulation and
     accumulate_averaging_changes on): encode = W(x), W(x - x0) in one DWT launch, top-k of
@@ -36,7 +36,7 @@ def c3_case(dev, n=25_000_000, alpha=0.01, npay=16, steps=40, warmup=5, seed=3):
     4M + 4N + 8 n k."""
     from decentralizepy_amd import codec
     level = 4
-    m = codec.wavedec_len(n, level)
+    m = codec.wavedec_len(n, level, wavelet)
     k = round(alpha * m)
     per_set = 4 * (2 * n + 4 * m) + 8 * k
     R = max(2, math.ceil(2 * L3_BYTES / per_set) + 1)
@@ -64,14 +64,15 @@ def c3_case(dev, n=25_000_000, alpha=0.01, npay=16, steps=40, warmup=5, seed=3):
     ws = codec.Workspace(dev)
 
     def encode(d):
-        codec.wavedec(d["x"], level, x0=d["x0"], coeffs_x=d["wx"], coeffs_diff=d["wc"])
+        codec.wavedec(d["x"], level, x0=d["x0"], coeffs_x=d["wx"], coeffs_diff=d["wc"],
+                      wavelet=wavelet)
         codec.topk_encode(d["wc"], k, acc=d["acc"], acc_mode=codec.DPZ_ACC_ADD,
                           vals_src=d["wx"], counter=d["cnt"], idx_out=d["idx"],
                           val_out=d["val"], workspace=ws, asynchronous=True)
 
     def decode(d):
         codec.decode_average(d["wx"], pays, w, w_self, out=d["tot"], workspace=ws)
-        codec.waverec(d["tot"], n, level, out=d["out"])
+        codec.waverec(d["tot"], n, level, out=d["out"], wavelet=wavelet)
 
     def step(i):
         d = sets[i % R]
@@ -92,7 +93,7 @@ def c3_case(dev, n=25_000_000, alpha=0.01, npay=16, steps=40, warmup=5, seed=3):
     kern = {nm: round(ms / c * 1e3, 2) for nm, (ms, c) in kt.result.items()}
     b_enc = 8 * n + 8 * m + 8 * m + 12 * k  # x, x0 -> W(x), W(dx); read W(dx), acc; k triples
     b_dec = 4 * m + 4 * n + 8 * npay * k + 8 * m
-    return dict(workload=f"C3: JWINS sym2 level-4 wavelet + top-k (accumulation) of an "
+    return dict(workload=f"C3: JWINS {wavelet} level-4 wavelet + top-k (accumulation) of an "
                          f"N={n} tensor (M={m} coefficients), {npay}-payload batched decode + "
                          f"MH average + IDWT", n=n, m=m, k=k, alpha=alpha, rotated_states=R,
                 value=4 * n / t_step / 2 ** 30, ms_per_step=t_step * 1e3,
@@ -259,3 +260,117 @@ def shard_case(dev, rank, world, dist, n=67_108_864, alpha=0.001, steps=20, warm
                          f"top-k (one all-gather of {world} x {k} candidates) + slice decode",
                 n=n, k=k, world=world, value=4 * n / t / 2 ** 30, ms_per_step=t * 1e3,
                 scaling="strong")
+
+
+def fft_case(dev, n=11_000_000, alpha=0.01, npay=3, steps=30, warmup=5, seed=9):
+    """The FFT sharing plugin's device round (reference sharing/JWINS/FFT.py:132-302) on an
+    N-parameter model: encode = x - x0, rfft(x) and rfft(x - x0) (hipFFT), |change| (complex, HIP),
+    top-k on it with the counter, complex values gathered from rfft(x); decode = npay complex
+    payloads folded (Metro-Hastings) over the (re, im) pairs, irfft (hipFFT) + 1/n.  The step
+    rate is reported on the GiB/s metric (4N bytes of model per step) with the HIP kernels'
+    average durations; the hipFFT kernels are library launches outside the per-kernel table."""
+    from decentralizepy_amd import codec
+    m = n // 2 + 1
+    k = round(alpha * m)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    R = 3
+    sets = []
+    for _ in range(R):
+        x = torch.randn(n, device=dev, generator=g)
+        sets.append(dict(x=x, x0=x - 0.01 * torch.randn(n, device=dev, generator=g),
+                         d=torch.empty(n, device=dev),
+                         cnt=torch.zeros(m, dtype=torch.int32, device=dev),
+                         out=torch.empty(n, device=dev)))
+    pays = []
+    for j in range(npay):
+        idx = torch.sort(torch.randperm(m, device=dev, generator=g)[:k])[0].to(torch.int32)
+        vals = torch.randn(2 * k, device=dev, generator=g)
+        pays.append((codec.cplx_pair_indices(idx), vals))
+    w = [1 / (npay + 1)] * npay
+    wt = 0.0
+    for v in w:
+        wt += v
+    ws = codec.Workspace(dev)
+
+    def step(i):
+        d = sets[i % R]
+        codec.elementwise(codec.DPZ_EW_SUB, d["x"], d["x0"], out=d["d"])
+        fx = codec.rfft(d["x"], workspace=ws)
+        ch = codec.rfft(d["d"], workspace=ws)
+        key = codec.cplx_key(ch)
+        idx, _ = codec.topk_encode(key, k, counter=d["cnt"], workspace=ws, asynchronous=True)
+        codec.cplx_gather(fx, idx)
+        tot = codec.decode_average(fx.view(torch.float32), pays, w, 1 - wt, workspace=ws)
+        codec.irfft(tot.view(torch.complex64), n, out=d["out"], workspace=ws)
+
+    for i in range(warmup):
+        step(i)
+    t = _sync_time(step, steps)
+    with codec.KernelTimer() as kt:
+        for i in range(R):
+            step(i)
+        torch.cuda.synchronize()
+    kern = {nm: round(ms / c * 1e3, 2) for nm, (ms, c) in kt.result.items()}
+    return dict(workload=f"FFT plugin round: rfft top-k encode + {npay}-payload complex fold + "
+                         f"irfft of an N={n} model (M={m} coefficients)",
+                n=n, m=m, k=k, alpha=alpha, value=4 * n / t / 2 ** 30, ms_per_step=t * 1e3,
+                note="hipFFT transforms are not in the per-kernel table (library kernels)",
+                kernels_avg_us=kern)
+
+
+def wire_case(dev, n=11_000_000, alpha=0.01, reps=30, seed=13):
+    """Device wire codecs on a C2 payload (k = 110,000 indices of an 11M model, fp32 values):
+    Elias-gamma (the reference's byte format), LZ4 frames of the int32 gaps (Lz4Wrapper's index
+    leg) and of the fp32 values, and the block-floating fp32 codec (EliasFpzip's value leg).
+    Encode and decode are timed device-to-device (each call ends with its size read-back) and
+    the wire bytes are reported against the raw int32 / fp32 legs.  cpu_baseline: liblz4 1.9.3
+    (what python-lz4 wraps) on the same gaps, one host thread."""
+    import numpy as np
+
+    from decentralizepy_amd import codec
+    k = round(alpha * n)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    idx = torch.sort(torch.randperm(n, device=dev, generator=g)[:k])[0].to(torch.int32)
+    vals = 0.01 * torch.randn(k, device=dev, generator=g)
+    ws = codec.Workspace(dev)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            out = fn()
+        torch.cuda.synchronize()
+        return out, (time.perf_counter() - t0) / reps * 1e6
+
+    res = {"k": k, "raw_idx_bytes": 4 * k, "raw_val_bytes": 4 * k}
+    el, t = timed(lambda: codec.elias_encode(idx, workspace=ws))
+    res["elias"] = {"bytes": int(el.numel()), "encode_us": round(t, 1)}
+    gaps = codec.delta_i32(idx)
+    fr, t = timed(lambda: codec.lz4_compress(gaps.view(torch.uint8), workspace=ws))
+    frame = fr.cpu().numpy().tobytes()
+    _, td = timed(lambda: codec.running_sum_i32(
+        codec.lz4_decompress(frame, dev, workspace=ws).view(torch.int32), dtype=torch.int32,
+        workspace=ws))
+    res["lz4_idx"] = {"bytes": len(frame), "encode_us": round(t, 1), "decode_us": round(td, 1)}
+    fv, t = timed(lambda: codec.lz4_compress(vals.view(torch.uint8), workspace=ws))
+    res["lz4_vals"] = {"bytes": int(fv.numel()), "encode_us": round(t, 1)}
+    fz, t = timed(lambda: codec.fpz_encode(vals, 0, workspace=ws))
+    res["fpz_vals"] = {"bytes": int(fz.numel()), "encode_us": round(t, 1)}
+    try:  # cpu_baseline leg (test infrastructure: liblz4 through the oracle's ctypes binding)
+        from oracle import lz4 as olz4
+        gh = np.diff(idx.cpu().numpy(), prepend=0).astype(np.int32).tobytes()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            cf = olz4.ref_compress(gh)
+        te = (time.perf_counter() - t0) / reps * 1e6
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            olz4.ref_decompress(cf)
+        tdc = (time.perf_counter() - t0) / reps * 1e6
+        res["cpu_baseline"] = {"kind": "liblz4 1.9.3 (python-lz4 default preferences)",
+                               "cores": 1, "bytes": len(cf), "encode_us": round(te, 1),
+                               "decode_us": round(tdc, 1)}
+    except OSError:
+        pass
+    return res

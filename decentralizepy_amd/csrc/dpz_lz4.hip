@@ -258,7 +258,30 @@ struct LzBlock {
   uint32_t raw;     // stored uncompressed
 };
 
-__device__ __forceinline__ uint32_t rd_in(const uint8_t* s, uint32_t i) { return s[i]; }
+// the block just decoded, ring positions [a, b) (b - a <= ring size), to out[a .. b): bytes up to
+// a 16-byte boundary of the output, then 16-byte stores of bytes gathered from the ring
+__device__ __forceinline__ void lz4_ring_out(const uint8_t* ring, uint32_t wmask, uint64_t a,
+                                             uint64_t b, uint8_t* out, uint64_t cap) {
+  const int lane = threadIdx.x;
+  if (b > cap) b = cap;
+  if (a >= b) return;
+  const uint64_t head = ((16 - ((uintptr_t)(out + a) & 15)) & 15);
+  const uint64_t a16 = a + head < b ? a + head : b;
+  for (uint64_t p = a + lane; p < a16; p += 64) out[p] = ring[p & wmask];
+  const uint64_t nv = (b - a16) / 16;
+  for (uint64_t v = lane; v < nv; v += 64) {
+    const uint64_t p = a16 + 16 * v;
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint64_t pq = p + 4 * q;
+      w[q] = (uint32_t)ring[pq & wmask] | ((uint32_t)ring[(pq + 1) & wmask] << 8) |
+             ((uint32_t)ring[(pq + 2) & wmask] << 16) | ((uint32_t)ring[(pq + 3) & wmask] << 24);
+    }
+    *reinterpret_cast<uint4*>(out + p) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  for (uint64_t p = a16 + 16 * nv + lane; p < b; p += 64) out[p] = ring[p & wmask];
+}
 
 __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t* __restrict__ in,
                                                         const LzBlock* __restrict__ blocks,
@@ -285,10 +308,10 @@ __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t* __restric
     if (B.raw) {
       for (uint32_t t = lane; t < B.csize; t += 64) {
         ring[(opos + t) & wmask] = cb[t];
-        if (obase + opos + t < out_cap) out[obase + opos + t] = cb[t];
       }
       opos += B.csize;
       __syncthreads();
+      lz4_ring_out(ring, wmask, start, opos, out + obase, out_cap > obase ? out_cap - obase : 0);
       if (!linked && lane == 0) dsize[b] = opos - start;
       continue;
     }
@@ -308,9 +331,7 @@ __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t* __restric
       }
       if (ip + L > B.csize || opos - start + L > bmax) { bad = true; break; }
       for (uint32_t t = lane; t < L; t += 64) {
-        const uint8_t v = cb[ip + t];
-        ring[(opos + t) & wmask] = v;
-        if (obase + opos + t < out_cap) out[obase + opos + t] = v;
+        ring[(opos + t) & wmask] = cb[ip + t];
       }
       ip += L;
       opos += L;
@@ -334,14 +355,13 @@ __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t* __restric
       __syncthreads();  // literal bytes in the ring before the match reads them
       // out[opos + t] = out[opos - off + (t mod off)]: each byte independently
       for (uint32_t t = lane; t < M; t += 64) {
-        const uint8_t v = ring[(opos - off + (t % off)) & wmask];
-        ring[(opos + t) & wmask] = v;
-        if (obase + opos + t < out_cap) out[obase + opos + t] = v;
+        ring[(opos + t) & wmask] = ring[(opos - off + (t % off)) & wmask];
       }
       opos += M;
       __syncthreads();
     }
     __syncthreads();
+    if (!bad) lz4_ring_out(ring, wmask, start, opos, out + obase, out_cap > obase ? out_cap - obase : 0);
     if (!linked && lane == 0) dsize[b] = opos - start;
   }
   if (bad && lane == 0) atomicOr(status, 1u);

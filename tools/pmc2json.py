@@ -2,7 +2,7 @@
 
 FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide
 coalesced reads (MI355X_MICROARCH.md § HBM), so traffic = 2 * FETCH_SIZE + WRITE_SIZE.
-Usage: pmc2json.py fetch.csv write.csv out.json
+Usage: pmc2json.py fetch.csv write.csv out.json ["source description"]
 """
 import collections
 import csv
@@ -12,7 +12,8 @@ import sys
 NAMES = {"sampled_sample_kernel": "topk_sample", "sampled_filter_kernel": "topk_filter",
          "sampled_select_kernel": "topk_select", "sampled_resolve_kernel": "topk_resolve",
          "sampled_compact_kernel": "topk_compact", "fold_offsets_kernel": "fold_offsets",
-         "fold_kernel": "fold", "replace_kernel": "fold", "dwt_kernel": "dwt",
+         "fold_kernel": "fold", "replace_kernel": "fold", "dwt_kernel": "dwt", "dwt4_kernel": "dwt",
+         "haar_dwt_kernel": "haar_dwt", "haar_idwt_kernel": "haar_idwt",
          "idwt_kernel": "idwt"}
 
 
@@ -39,9 +40,10 @@ def main(fetch, write, out):
         fk, wk = f.get(k, 0.0), w.get(k, 0.0)
         kernels[k] = {"FETCH_SIZE_KiB": round(fk, 2), "WRITE_SIZE_KiB": round(wk, 2),
                       "hbm_bytes_per_launch": int(round((2 * fk + wk) * 1024))}
+    src = sys.argv[4] if len(sys.argv) > 4 else (
+        "`python3 bench.py --steps 100 --warmup 10 --no-cpu --no-extra --streams 1 --serial`")
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
-                     "`python3 bench.py --steps 100 --warmup 10 --no-cpu --no-extra --streams 1 --serial`; "
-                     "traffic = 2*FETCH_SIZE (gfx950 half-count correction) + WRITE_SIZE",
+                     f"{src}; traffic = 2*FETCH_SIZE (gfx950 half-count correction) + WRITE_SIZE",
            "kernels": kernels}
     with open(out, "w") as fh:
         json.dump(doc, fh, indent=1)
