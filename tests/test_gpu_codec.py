@@ -229,11 +229,13 @@ def test_fold_matches_oracle(dev, n, npay):
 @pytest.mark.parametrize("n,alpha,npay", [(1_000_003, 0.01, 16), (1_000_003, 0.05, 16),
                                           (4_000_037, 0.01, 20), (300_001, 0.2, 3),
                                           (300_001, 0.04, 5), (100_003, 0.99, 2),
-                                          (200_003, 0.4, 3)])
+                                          (200_003, 0.4, 3), (1_000_003, 0.1, 16),
+                                          (1_000_003, 0.15, 16), (1_000_003, 0.2, 16),
+                                          (2_000_003, 0.1, 20)])
 def test_fold_all_sparse_overlapping(dev, n, alpha, npay):
-    """All-sparse payload groups take the one-phase hit-chain fold (tiles with more than its LDS
-    capacity of entries fall back to the per-payload phases inside the same launch); payloads
-    share many indices so elements carry 2, 3 and more hits."""
+    """All-sparse payload groups: tiles with at most 2,816 entries take the one-phase hit-chain
+    fold, denser tiles (JWINS alpha 0.1-0.2 x 16 payloads) the per-payload phases, inside the
+    same launch; payloads share many indices so elements carry 2, 3 and more hits."""
     codec = _codec()
     rng = np.random.default_rng(int(n * alpha) + npay)
     local = rng.standard_normal(n).astype(np.float32)
@@ -256,6 +258,38 @@ def test_fold_all_sparse_overlapping(dev, n, alpha, npay):
     ref2 = ofold.fold(local, pays, [1 / npay] * npay, None)
     out2 = codec.decode_average(tl, tpays, [1 / npay] * npay, None).cpu().numpy()
     np.testing.assert_array_equal(_bits(out2), _bits(ref2))
+
+
+@pytest.mark.parametrize("alpha", [0.01, 0.1])
+def test_fold_zero_base_and_accumulate_dense(dev, alpha):
+    """DPZ_FOLD_ZERO_BASE (STC's server total: sparse payloads are zero off their entries, the
+    total starts from +0.0) and DPZ_FOLD_ACCUMULATE (Choco: continue a running total) on the
+    hit-chain (alpha 0.01) and phase (alpha 0.1 x 16) paths, bit-exact."""
+    codec = _codec()
+    n, npay = 1_000_003, 16
+    rng = np.random.default_rng(int(alpha * 1000))
+    k = round(alpha * n)
+    pays, tpays = [], []
+    for i in range(npay):
+        idx = np.sort(rng.choice(n, size=k, replace=False)).astype(np.int32)
+        vals = rng.standard_normal(k).astype(np.float32)
+        pays.append((idx, vals))
+        tpays.append((torch.from_numpy(idx).to(dev), torch.from_numpy(vals).to(dev)))
+    w = [1.0 / (npay + 1)] * npay
+    zeros = np.zeros(n, np.float32)
+    ref = zeros.copy()
+    for (idx, vals), wi in zip(pays, w):
+        ref = ref + ofold.replace(zeros, idx, vals) * np.float32(wi)
+    tl = torch.zeros(n, device=dev)
+    out = codec.decode_average(tl, tpays, w, None, zero_base=True).cpu().numpy()
+    np.testing.assert_array_equal(_bits(out), _bits(ref))
+    start = rng.standard_normal(n).astype(np.float32)
+    ref2 = start.copy()
+    for (idx, vals), wi in zip(pays, w):
+        ref2 = ref2 + ofold.replace(zeros, idx, vals) * np.float32(wi)
+    tout = torch.from_numpy(start).to(dev)
+    codec.decode_average(tl, tpays, w, None, zero_base=True, accumulate=True, out=tout)
+    np.testing.assert_array_equal(_bits(tout.cpu().numpy()), _bits(ref2))
 
 
 @pytest.mark.parametrize("npay", [0, 3, 20])
