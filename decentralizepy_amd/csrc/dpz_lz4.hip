@@ -7,14 +7,14 @@
 // (python-lz4's lz4.frame, third-party, absent here; its frame format is the LZ4 frame spec and
 // its default preferences are: 64 KB blocks, linked, content size stored, no checksums).
 //
-// Encoder: the input is cut into independent 4 KB blocks, ONE WAVE per block (the frame says
+// Encoder: the input is cut into independent 2 KB blocks (DPZ_LZ_BLK), ONE WAVE per block (the frame says
 // B.Indep, so any LZ4 frame decoder — python-lz4 on a reference node included — reads it):
 //   1. the block is staged in LDS; every position i <= len - 12 hashes its 4 bytes (LZ4's
-//      multiplicative hash, 12 bits) 64 positions at a time: the candidate is the table entry
+//      multiplicative hash, 11 bits) 64 positions at a time: the candidate is the table entry
 //      left by earlier chunks, then the chunk publishes itself with LDS atomicMax (so the nearest
 //      earlier occurrence from a previous chunk wins — deterministic);
 //   2. each lane extends its candidate word-wise (min match 4, capped at 1024 and at len - 5) and
-//      sets its bit in a 4096-bit match mask;
+//      sets its bit in a per-position match mask;
 //   3. the greedy parse walks the mask with 64-bit bit scans (literal runs cost one scan, not one
 //      step per byte) and records the sequences in LDS;
 //   4. sequence sizes, a wave scan, and every lane emits its sequences into an LDS output buffer,
@@ -29,8 +29,15 @@
 
 namespace dpz {
 
-constexpr int LZ_BLK = 4096;        // encoder block (one wave)
-constexpr int LZ_HASH_LOG = 12;
+#ifndef DPZ_LZ_BLK
+#define DPZ_LZ_BLK 2048
+#endif
+#ifndef DPZ_LZ_HASH_LOG
+#define DPZ_LZ_HASH_LOG 11
+#endif
+constexpr int LZ_BLK = DPZ_LZ_BLK;  // encoder block (one wave)
+constexpr int LZ_HASH_LOG = DPZ_LZ_HASH_LOG;
+static_assert(LZ_BLK >= 256 && LZ_BLK <= 65536 && (LZ_BLK & 63) == 0, "encoder block size");
 constexpr int LZ_MAXM = 1024;       // match length cap
 constexpr int LZ_MFLIMIT = 12;      // a match starts at least 12 bytes before the block end
 constexpr int LZ_LASTLIT = 5;       // the last 5 bytes are literals
@@ -63,6 +70,44 @@ __device__ __forceinline__ int lz_lenext(int L) { return L >= 15 ? (L - 15) / 25
 
 __device__ __forceinline__ void lz_put(uint8_t* ob, int pos, uint32_t v) { ob[pos] = (uint8_t)v; }
 
+// Global bytes -> LDS, one wave: every load of a round issued before its LDS writes (a loop of
+// load -> wait -> write per byte is one memory round trip per 64 bytes).  16-byte loads when the
+// source is aligned, else 16 independent byte loads per lane per round.
+__device__ __forceinline__ void lz_stage(uint8_t* dst, const uint8_t* __restrict__ src, uint32_t n) {
+  const int lane = threadIdx.x & 63;
+  if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
+    const uint32_t nv = n / 16;
+    for (uint32_t v0 = 0; v0 < nv; v0 += 4 * 64) {
+      uint4 r[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t v = v0 + u * 64 + lane;
+        if (v < nv) r[u] = reinterpret_cast<const uint4*>(src)[v];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t v = v0 + u * 64 + lane;
+        if (v < nv) *reinterpret_cast<uint4*>(dst + 16 * v) = r[u];
+      }
+    }
+    for (uint32_t t = nv * 16 + lane; t < n; t += 64) dst[t] = src[t];
+    return;
+  }
+  for (uint32_t t0 = 0; t0 < n; t0 += 16 * 64) {
+    uint8_t r[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const uint32_t t = t0 + u * 64 + lane;
+      r[u] = t < n ? src[t] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const uint32_t t = t0 + u * 64 + lane;
+      if (t < n) dst[t] = r[u];
+    }
+  }
+}
+
 // one wave per 4 KB block; blocks of 64 threads
 __global__ void __launch_bounds__(64) lz4_encode_blocks(const uint8_t* __restrict__ in, int64_t n,
                                                        uint8_t* __restrict__ slots,
@@ -73,16 +118,10 @@ __global__ void __launch_bounds__(64) lz4_encode_blocks(const uint8_t* __restric
   const int64_t blk = blockIdx.x;
   const int64_t base = blk * LZ_BLK;
   const int len = (int)((n - base) < LZ_BLK ? (n - base) : LZ_BLK);
-  // stage the block (bytes -> words), zero the table and the mask
-  for (int w = lane; w < LZ_BLK / 4 + 2; w += 64) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int i = 4 * w + e;
-      if (i < len) v |= (uint32_t)in[base + i] << (8 * e);
-    }
-    S.data[w] = v;
-  }
+  // stage the block (zero slack after it), zero the table and the mask
+  for (int w = lane; w < LZ_BLK / 4 + 2; w += 64) S.data[w] = 0;
+  __syncthreads();
+  lz_stage(reinterpret_cast<uint8_t*>(S.data), in + base, (uint32_t)len);
   for (int t = lane; t < (1 << LZ_HASH_LOG); t += 64) S.table[t] = 0;
   for (int t = lane; t < LZ_BLK / 64; t += 64) S.mask[t] = 0ull;
   __syncthreads();
@@ -153,7 +192,7 @@ __global__ void __launch_bounds__(64) lz4_encode_blocks(const uint8_t* __restric
   __syncthreads();
   const uint32_t ns = nseq + 1;
   // sizes and offsets of the sequences (wave scan in chunks of 64)
-  uint8_t* ob = reinterpret_cast<uint8_t*>(S.minfo);  // reuse: 16 KB >= LZ_BLK_OUT
+  uint8_t* ob = reinterpret_cast<uint8_t*>(S.minfo);  // reuse: 4 LZ_BLK bytes >= LZ_BLK_OUT
   uint32_t run = 0;
   for (uint32_t s0 = 0; s0 < ns; s0 += 64) {
     const uint32_t s = s0 + lane;
@@ -283,6 +322,25 @@ __device__ __forceinline__ void lz4_ring_out(const uint8_t* ring, uint32_t wmask
   for (uint64_t p = a16 + 16 * nv + lane; p < b; p += 64) out[p] = ring[p & wmask];
 }
 
+// The token walk is wave-uniform scalar work: the next 256 bytes of the staged block sit one
+// word per lane in a register window (refilled with one LDS read when the walk passes its end),
+// and a byte is a v_readlane away — no LDS round trip per token / length / offset byte.  Literal
+// and match bytes are copied by the whole wave inside the LDS ring (one wave per workgroup, so
+// its LDS accesses stay in program order without barriers).
+struct LzWin {
+  uint32_t wv;     // this lane's word: staged bytes [base + 4 lane, +4)
+  uint32_t base;   // window start (a multiple of 4)
+};
+
+__device__ __forceinline__ uint32_t lz_win_byte(LzWin& w, const uint32_t* cb32, uint32_t p) {
+  if (p - w.base >= 252u) {  // (unsigned: also p < base, which never happens)
+    w.base = p & ~3u;
+    w.wv = cb32[(w.base >> 2) + threadIdx.x];
+  }
+  const uint32_t r = p - w.base;
+  return (__builtin_amdgcn_readlane(w.wv, (int)(r >> 2)) >> (8 * (r & 3))) & 0xFFu;
+}
+
 __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t* __restrict__ in,
                                                         const LzBlock* __restrict__ blocks,
                                                         int64_t nblk, int linked, uint32_t bmax,
@@ -292,7 +350,8 @@ __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t* __restric
                                                         uint32_t* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lz_smem[];
   uint8_t* ring = lz_smem;           // win bytes
-  uint8_t* cb = lz_smem + win;       // staged compressed block (bmax + 16)
+  uint8_t* cb = lz_smem + win;       // staged compressed block (+ 256 bytes of window slack)
+  const uint32_t* cb32 = reinterpret_cast<const uint32_t*>(cb);
   const int lane = threadIdx.x;
   const uint32_t wmask = win - 1;
   int64_t b0 = linked ? 0 : blockIdx.x, b1 = linked ? nblk : blockIdx.x + 1;
@@ -302,49 +361,48 @@ __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t* __restric
   for (int64_t b = b0; b < b1 && !bad; ++b) {
     const LzBlock B = blocks[b];
     if (B.csize > bmax + 16 || (B.raw && B.csize > bmax)) { bad = true; break; }
-    for (uint32_t t = lane; t < B.csize; t += 64) cb[t] = in[B.in_off + t];
+    lz_stage(cb, in + B.in_off, B.csize);
+    for (uint32_t t = B.csize + lane; t < B.csize + 256; t += 64) cb[t] = 0;
     __syncthreads();
     const uint64_t start = opos;
     if (B.raw) {
-      for (uint32_t t = lane; t < B.csize; t += 64) {
-        ring[(opos + t) & wmask] = cb[t];
-      }
+      for (uint32_t t = lane; t < B.csize; t += 64) ring[(opos + t) & wmask] = cb[t];
       opos += B.csize;
       __syncthreads();
       lz4_ring_out(ring, wmask, start, opos, out + obase, out_cap > obase ? out_cap - obase : 0);
       if (!linked && lane == 0) dsize[b] = opos - start;
       continue;
     }
+    LzWin w{cb32[lane], 0u};
     uint32_t ip = 0;
+    const uint32_t cs = B.csize;
     for (;;) {  // wave-uniform token walk
-      if (ip >= B.csize) { bad = true; break; }
-      const uint32_t tok = cb[ip++];
+      if (ip >= cs) { bad = true; break; }
+      const uint32_t tok = lz_win_byte(w, cb32, ip++);
       uint32_t L = tok >> 4;
       if (L == 15) {
         uint32_t x;
         do {
-          if (ip >= B.csize) { bad = true; break; }
-          x = cb[ip++];
+          if (ip >= cs) { bad = true; break; }
+          x = lz_win_byte(w, cb32, ip++);
           L += x;
         } while (x == 255);
         if (bad) break;
       }
-      if (ip + L > B.csize || opos - start + L > bmax) { bad = true; break; }
-      for (uint32_t t = lane; t < L; t += 64) {
-        ring[(opos + t) & wmask] = cb[ip + t];
-      }
+      if (ip + L > cs || opos - start + L > bmax) { bad = true; break; }
+      for (uint32_t t = lane; t < L; t += 64) ring[(opos + t) & wmask] = cb[ip + t];
       ip += L;
       opos += L;
-      if (ip == B.csize) break;  // the last sequence has no match
-      if (ip + 2 > B.csize) { bad = true; break; }
-      const uint32_t off = (uint32_t)cb[ip] | ((uint32_t)cb[ip + 1] << 8);
+      if (ip == cs) break;  // the last sequence has no match
+      if (ip + 2 > cs) { bad = true; break; }
+      const uint32_t off = lz_win_byte(w, cb32, ip) | (lz_win_byte(w, cb32, ip + 1) << 8);
       ip += 2;
       uint32_t M = (tok & 15u);
       if (M == 15) {
         uint32_t x;
         do {
-          if (ip >= B.csize) { bad = true; break; }
-          x = cb[ip++];
+          if (ip >= cs) { bad = true; break; }
+          x = lz_win_byte(w, cb32, ip++);
           M += x;
         } while (x == 255);
         if (bad) break;
@@ -352,13 +410,15 @@ __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t* __restric
       M += 4;
       const uint64_t hist = linked ? opos : opos - start;  // reachable history
       if (off == 0 || off > hist || opos - start + M > bmax) { bad = true; break; }
-      __syncthreads();  // literal bytes in the ring before the match reads them
       // out[opos + t] = out[opos - off + (t mod off)]: each byte independently
-      for (uint32_t t = lane; t < M; t += 64) {
-        ring[(opos + t) & wmask] = ring[(opos - off + (t % off)) & wmask];
+      if (off >= M) {
+        for (uint32_t t = lane; t < M; t += 64)
+          ring[(opos + t) & wmask] = ring[(opos - off + t) & wmask];
+      } else {
+        for (uint32_t t = lane; t < M; t += 64)
+          ring[(opos + t) & wmask] = ring[(opos - off + (t % off)) & wmask];
       }
       opos += M;
-      __syncthreads();
     }
     __syncthreads();
     if (!bad) lz4_ring_out(ring, wmask, start, opos, out + obase, out_cap > obase ? out_cap - obase : 0);
@@ -627,7 +687,7 @@ extern "C" int dpz_lz4_decompress(const uint8_t* frame_dev, const uint8_t* frame
     // smaller) + the largest compressed block
     const uint32_t maxc = *csz;
     const uint32_t win = 65536;
-    const size_t shm = (size_t)win + (size_t)maxc + 16;
+    const size_t shm = (size_t)win + (size_t)maxc + 16 + 256;
     if (bmax > 65536 || shm > 160 * 1024) return DPZ_ERR_UNSUPPORTED;
     DPZ_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(lz4_decode_kernel),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));

@@ -374,9 +374,9 @@ int dpz_cplx_gather(const float* src, int64_t m, const int32_t* idx, int64_t k, 
 int dpz_cplx_pair_indices(const int32_t* idx, int64_t k, int32_t* pair, dpz_stream_t stream);
 
 /* ---- LZ4 frames (the wire format of compression/Lz4Wrapper.py:20-98, lz4.frame) -------------
- * Encoder: independent 4 KB blocks, one wave each (B.Indep, BD = 64 KB, content size stored, no
+ * Encoder: independent 2 KB blocks, one wave each (B.Indep, BD = 64 KB, content size stored, no
  * checksums): a valid LZ4 frame any decoder reads; the bytes are this build's (greedy parse over a
- * 12-bit hash of 4-byte words; python-lz4's match finder is not reproduced, so byte parity is
+ * 11-bit hash of 4-byte words; python-lz4's match finder is not reproduced, so byte parity is
  * unpinned).  Decoder: any LZ4 frame with 64 KB (or smaller) blocks, linked (python-lz4's
  * default, decoded by one workgroup) or independent (one workgroup per block); content and
  * block checksums are skipped, dictionary IDs rejected.                                         */
