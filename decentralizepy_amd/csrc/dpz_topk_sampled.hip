@@ -819,7 +819,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     int32_t* idx_out, float* val_out, int32_t* counter, float* rewind, ReplaceJob pj) {
   __shared__ uint32_t wcnt[CSEG];
   __shared__ uint32_t subbase[NSUB + 1];
-  __shared__ uint32_t flag;
+  __shared__ uint32_t flag, spec;
   __shared__ uint64_t wsum64[4];
   __shared__ ResolveLds RL;
   __shared__ uint32_t bsk[BLDS], bsi[BLDS];
@@ -836,6 +836,13 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   const uint32_t status = ctrl->status;
   const uint32_t need = ctrl->need, lo = ctrl->lo, shift = ctrl->shift, bstar = ctrl->bstar;
   const uint32_t sc = t < NSUB ? blcnt[t] : 0u;
+  // the first SPEC entries of every boundary sub-list, loaded with the counts (thread t: sub-list
+  // t / SPEC, slot t % SPEC) instead of after them: when no sub-list holds more (the usual case,
+  // ~k/1000 boundary entries over 16 sub-lists), the boundary set needs no dependent load
+  constexpr uint32_t SPEC = 256 / NSUB;
+  static_assert(NSUB * SPEC == 256 && SPEC <= SUBCAP, "one speculative entry per thread");
+  const uint32_t sp_sub = (uint32_t)t / SPEC, sp_slot = (uint32_t)t % SPEC;
+  const uint32_t spk = blkey[sp_sub * SUBCAP + sp_slot], spi = blidx[sp_sub * SUBCAP + sp_slot];
   static_assert(B_MAX <= 256 * 8, "above counts: 8 per thread");
   uint32_t abv_before = 0, abv_all = 0;
   {
@@ -894,10 +901,12 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     uint32_t tot;
     const uint32_t ex = wave_excl_scan(sc, &tot);
     const bool over = __ballot(sc > (uint32_t)SUBCAP) != 0;
+    const bool spec_ok = __ballot(sc > SPEC) == 0;
     if (t < NSUB) subbase[t] = ex;
     if (t == 0) {
       subbase[NSUB] = tot;
       flag = (over || tot > (uint32_t)BCAP || need == 0 || need > tot) ? 1u : 0u;
+      spec = spec_ok ? 1u : 0u;
     }
   }
   __syncthreads();
@@ -910,7 +919,15 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   }
   STAMP_T0(1);
   Bound bd{blkey, blidx, subbase, bsk, bsi, subbase[NSUB]};
-  bd.load();
+  if (spec) {  // every boundary entry is in a speculative register (nb <= 256 <= BLDS)
+    if (sp_slot < subbase[sp_sub + 1] - subbase[sp_sub]) {
+      bsk[subbase[sp_sub] + sp_slot] = spk;
+      bsi[subbase[sp_sub] + sp_slot] = spi;
+    }
+    __syncthreads();
+  } else {
+    bd.load();
+  }
   uint32_t T, icut;
   block_resolve(bd, need, lo + (bstar << shift), shift, RL, &T, &icut);
   STAMP_T0(2);
