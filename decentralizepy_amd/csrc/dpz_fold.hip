@@ -21,7 +21,10 @@
 //      into an LDS value tile tagged with the payload number (the next payload's extra entries
 //      prefetched meanwhile), and every thread folds its 8 elements:
 //        t = (tag == p) ? hit : local;  total = (p == 0) ? t*w : total + t*w
-//    Both follow the reference's fp32 order exactly (library compiled with -ffp-contract=off).
+//  * fold_group_kernel instead, for all-sparse groups of >= 8 payloads at moderate density
+//    (JWINS alpha 0.03-0.1 x 16): every entry of the tile loaded at tile start, payloads folded
+//    four at a time from their own LDS value slots (two barriers per four payloads).
+//    All follow the reference's fp32 order exactly (library compiled with -ffp-contract=off).
 // Algorithmic bytes: read local (4N) + write out (4N) + 8 bytes per payload entry.
 #include <cstdlib>
 
@@ -592,23 +595,265 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
   }  // tile loop
 }
 
+// ------------------------------------------------------------------------------------------------
+// Slotted fold for dense all-sparse groups (JWINS alpha 0.1-0.4: thousands of entries per tile).
+// The phase path pays a global load latency per payload (the next payload's entries arrive while
+// only a short fold runs) and two barriers per payload.  Here every entry of the tile (up to
+// FG_CAP per round) is loaded at tile start, into registers, and the payloads are folded
+// FG_SLOTS at a time: each payload of a phase scatters into its own LDS value tile with a hit bit,
+// then every thread folds its 8 elements over the phase's payloads in the reference's order
+//   t = hit ? value : local;  total = (p == 0) ? t*w : total + t*w
+// Hit flags are one byte per element (bit s: slot s hit), so the entries of a payload, sorted and
+// spread over consecutive lanes, rarely collide in an LDS atomic; each thread clears its own
+// elements' flags right after folding them, so a phase costs two barriers and no global round
+// trip.
+constexpr int FG_SLOTS = 4;                    // payloads per phase
+constexpr int FG_CAP = 6144;                   // entries held per round (>= one payload's 4096)
+constexpr int FG_EPT = FG_CAP / FOLD_THREADS;  // per thread
+#ifndef DPZ_FG_HALVES
+#define DPZ_FG_HALVES 2
+#endif
+constexpr int FG_HALVES = DPZ_FG_HALVES;  // entry load batches per round (register pressure)
+static_assert(FG_CAP >= FOLD_TILE && FOLD_TILE <= 65536, "a round holds one payload's tile");
+static_assert(FG_SLOTS <= 8, "slot flags are the bits of one byte per element");
+#ifndef DPZ_FOLD_GROUP_MIN
+#define DPZ_FOLD_GROUP_MIN 1536
+#endif
+constexpr int64_t FOLD_GROUP_MIN = DPZ_FOLD_GROUP_MIN;  // average entries per tile
+
+template <bool VEC>
+__global__ void __launch_bounds__(FOLD_THREADS, 4) fold_group_kernel(FoldArgs a) {
+  __shared__ __attribute__((aligned(16))) float hv[FG_SLOTS][FOLD_TILE];
+  __shared__ uint32_t hf[FOLD_TILE / 4];  // hit flags: byte e of word w = element 4w + e
+  __shared__ int32_t rng[FOLD_MAXP][2];
+  __shared__ int32_t pre[FOLD_MAXP + 1];
+  __shared__ const int32_t* s_idx[FOLD_MAXP];
+  __shared__ const float* s_val[FOLD_MAXP];
+  __shared__ float s_w[FOLD_MAXP];
+  const int t = threadIdx.x;
+  if (t == 0) {
+    for (int p = 0; p < a.np; ++p) {
+      s_idx[p] = a.p[p].idx;
+      s_val[p] = a.p[p].val;
+      s_w[p] = a.p[p].w;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < FOLD_GROUPS; ++q) hf[q * FOLD_THREADS + t] = 0;
+  int32_t nr0 = 0, nr1 = 0;
+  const bool rng_lane = t < a.np;
+  if (rng_lane && (int64_t)blockIdx.x < a.ntiles) {
+    const int32_t* st = a.starts + (int64_t)t * (a.ntiles + 1);
+    nr0 = st[blockIdx.x];
+    nr1 = st[blockIdx.x + 1];
+  }
+  float L[4 * FOLD_GROUPS];
+  auto load_local = [&](int64_t tl) {
+    const int64_t lo_ = tl * FOLD_TILE;
+    const int64_t hi_ = (lo_ + FOLD_TILE < a.n) ? lo_ + FOLD_TILE : a.n;
+#pragma unroll
+    for (int q = 0; q < FOLD_GROUPS; ++q) {
+      const int64_t i0 = lo_ + q * 4 * FOLD_THREADS + t * 4;
+      if (VEC && i0 + 3 < hi_) {
+        float4 v = *reinterpret_cast<const float4*>(a.local + i0);
+        L[q * 4 + 0] = v.x; L[q * 4 + 1] = v.y; L[q * 4 + 2] = v.z; L[q * 4 + 3] = v.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) L[q * 4 + e] = i0 + e < hi_ ? a.local[i0 + e] : 0.0f;
+      }
+    }
+  };
+  if ((int64_t)blockIdx.x < a.ntiles) load_local(blockIdx.x);
+  for (int64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    const int64_t tlo = tile * FOLD_TILE;
+    const int64_t thi = (tlo + FOLD_TILE < a.n) ? tlo + FOLD_TILE : a.n;
+    if (t < 64) {
+      const int32_t c = (t < a.np && nr1 > nr0) ? nr1 - nr0 : 0;
+      if (t < a.np) {
+        rng[t][0] = nr0;
+        rng[t][1] = nr1;
+      }
+      int32_t incl = c;
+#pragma unroll
+      for (int d = 1; d < FOLD_MAXP; d <<= 1) {
+        const int32_t v = __shfl_up(incl, d, 64);
+        if (t >= d) incl += v;
+      }
+      if (t < FOLD_MAXP) pre[t + 1] = incl;
+      if (t == 0) pre[0] = 0;
+    }
+    if (rng_lane && tile + gridDim.x < a.ntiles) {
+      const int32_t* st = a.starts + (int64_t)t * (a.ntiles + 1);
+      nr0 = st[tile + gridDim.x];
+      nr1 = st[tile + gridDim.x + 1];
+    }
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    f2v acc2[2 * FOLD_GROUPS];  // this thread's 8 running totals as packed pairs
+    float base[4 * FOLD_GROUPS];  // a payload's value off its entries: local, or 0 (zero base)
+#pragma unroll
+    for (int e = 0; e < 4 * FOLD_GROUPS; ++e) base[e] = a.zero_base ? 0.0f : L[e];
+#pragma unroll
+    for (int h = 0; h < 2 * FOLD_GROUPS; ++h) acc2[h] = f2v{0.0f, 0.0f};
+    if (!a.first) {
+#pragma unroll
+      for (int q = 0; q < FOLD_GROUPS; ++q) {
+        const int64_t i0 = tlo + q * 4 * FOLD_THREADS + t * 4;
+        float o[4];
+        if (VEC && i0 + 3 < thi) {
+          const float4 v = *reinterpret_cast<const float4*>(a.out + i0);
+          o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = i0 + e < thi ? a.out[i0 + e] : 0.0f;
+        }
+        acc2[2 * q] = f2v{o[0], o[1]};
+        acc2[2 * q + 1] = f2v{o[2], o[3]};
+      }
+    }
+    __syncthreads();  // rng / pre visible; the previous tile's last phase is done
+    for (int pa = 0; pa < a.np;) {
+      // the round: payloads [pa, pb) whose entries of this tile fit FG_CAP (at least one)
+      int pb = pa + 1;
+      while (pb < a.np && pre[pb + 1] - pre[pa] <= FG_CAP) ++pb;
+      const int32_t j0 = pre[pa], jn = pre[pb] - pre[pa];
+      // entry u of this thread: ei = (position in the tile | payload << 16) or ~0 (absent /
+      // outside the tile: an invalid payload cannot write out of bounds), ev = its value.
+      // Loaded in FG_HALVES batches (fewer address registers live at once).
+      uint32_t ei[FG_EPT];
+      float ev[FG_EPT];
+#pragma unroll
+      for (int h = 0; h < FG_HALVES; ++h) {
+        constexpr int HU = FG_EPT / FG_HALVES;
+#pragma unroll
+        for (int u = h * HU; u < (h + 1) * HU; ++u) {
+          const int32_t j = t + u * FOLD_THREADS;
+          ei[u] = 0;
+          ev[u] = 0.0f;
+          if (j < jn) {
+            const int32_t jj = j0 + j;
+            int p = 0;
+#pragma unroll
+            for (int s = FOLD_MAXP / 2; s >= 1; s >>= 1) p += pre[p + s] <= jj ? s : 0;
+            const int64_t src = (int64_t)rng[p][0] + (jj - pre[p]);
+            ei[u] = (uint32_t)s_idx[p][src];
+            ev[u] = s_val[p][src];
+          }
+        }
+#pragma unroll
+        for (int u = h * HU; u < (h + 1) * HU; ++u) {
+          // the entry's payload again (4 LDS reads): cheaper than holding it in registers
+          uint32_t p = 0;
+          {
+            const int32_t jj = j0 + t + u * FOLD_THREADS;
+#pragma unroll
+            for (int s = FOLD_MAXP / 2; s >= 1; s >>= 1) p += pre[p + s] <= jj ? s : 0;
+          }
+          const int64_t pos = (int64_t)(int32_t)ei[u] - tlo;
+          const bool in = t + u * FOLD_THREADS < jn && pos >= 0 && pos < FOLD_TILE;
+          ei[u] = in ? ((uint32_t)pos | (p << 16)) : ~0u;
+        }
+      }
+      for (int pbase = pa; pbase < pb; pbase += FG_SLOTS) {
+        const int ns = (pb - pbase) < FG_SLOTS ? (pb - pbase) : FG_SLOTS;
+        // scatter this phase's payloads into their slots
+#pragma unroll
+        for (int u = 0; u < FG_EPT; ++u) {
+          const uint32_t s = (ei[u] >> 16) - (uint32_t)pbase;  // ~0 entries: s is huge
+          if (s < (uint32_t)ns) {
+            const uint32_t pos = ei[u] & 0xFFFFu;
+            hv[s][pos] = ev[u];
+            atomicOr(&hf[pos >> 2], (1u << s) << (8u * (pos & 3u)));
+          }
+        }
+        __syncthreads();
+        // fold the phase's payloads (this thread's own elements: flag word q * 512 + t)
+        uint32_t fw[FOLD_GROUPS];
+#pragma unroll
+        for (int q = 0; q < FOLD_GROUPS; ++q) {
+          fw[q] = hf[q * FOLD_THREADS + t];
+          hf[q * FOLD_THREADS + t] = 0;  // read: cleared for the next phase (no one else reads it)
+        }
+        // packed fp32 pairs (v_pk_mul / v_pk_add: two elements per instruction, no FMA); the
+        // first term of a fresh total (payload 0) is peeled off the loop
+        for (int s = 0; s < ns; ++s) {
+          const int p = pbase + s;
+          const float w = s_w[p];
+          const f2v w2 = {w, w};
+          const bool first_term = a.first && p == 0;
+#pragma unroll
+          for (int q = 0; q < FOLD_GROUPS; ++q) {
+            const int jt = q * 4 * FOLD_THREADS + t * 4;
+            const uint32_t f = fw[q] >> s;  // bit 8e: element e hit by slot s
+            const float4 h4 = *reinterpret_cast<const float4*>(&hv[s][jt]);
+            const f2v t01 = {(f & 0x1u) ? h4.x : base[q * 4 + 0], (f & 0x100u) ? h4.y : base[q * 4 + 1]};
+            const f2v t23 = {(f & 0x10000u) ? h4.z : base[q * 4 + 2], (f & 0x1000000u) ? h4.w : base[q * 4 + 3]};
+            if (first_term) {
+              const f2v z = {0.0f, 0.0f};
+              acc2[2 * q] = a.zero_base ? z + t01 * w2 : t01 * w2;
+              acc2[2 * q + 1] = a.zero_base ? z + t23 * w2 : t23 * w2;
+            } else {
+              acc2[2 * q] = acc2[2 * q] + t01 * w2;
+              acc2[2 * q + 1] = acc2[2 * q + 1] + t23 * w2;
+            }
+          }
+        }
+        __syncthreads();  // slots and flags free for the next phase
+      }
+      pa = pb;
+    }
+    float acc[4 * FOLD_GROUPS];
+#pragma unroll
+    for (int h = 0; h < 2 * FOLD_GROUPS; ++h) {
+      acc[2 * h] = acc2[h].x;
+      acc[2 * h + 1] = acc2[h].y;
+    }
+    if (a.add_self) {
+#pragma unroll
+      for (int e = 0; e < 4 * FOLD_GROUPS; ++e) acc[e] = acc[e] + L[e] * a.w_self;
+    }
+#pragma unroll
+    for (int q = 0; q < FOLD_GROUPS; ++q) {
+      const int64_t i0 = tlo + q * 4 * FOLD_THREADS + t * 4;
+      if (VEC && i0 + 3 < thi) {
+        const float4 r4 =
+            make_float4(acc[q * 4 + 0], acc[q * 4 + 1], acc[q * 4 + 2], acc[q * 4 + 3]);
+        *reinterpret_cast<float4*>(a.out + i0) = r4;
+        if (a.out2) *reinterpret_cast<float4*>(a.out2 + i0) = r4;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (i0 + e < thi) {
+            a.out[i0 + e] = acc[q * 4 + e];
+            if (a.out2) a.out2[i0 + e] = acc[q * 4 + e];
+          }
+      }
+    }
+    if (tile + gridDim.x < a.ntiles) load_local(tile + gridDim.x);
+    // no barrier here: every read of rng / pre / the slots of this tile happened before the
+    // last phase's barrier (a group with no payload has no phase: np == 0 never reaches here)
+  }  // tile loop
+}
+
 // blocks of the persistent fold grid: what the CUs hold at once (occupancy API)
 template <bool VEC>
-static unsigned fold_grid(int64_t ntiles) {
-  static int slots = 0;
-  if (slots == 0) {
+static unsigned fold_grid(int64_t ntiles, bool group = false) {
+  static int slots[2] = {0, 0};
+  int& sl = slots[group ? 1 : 0];
+  if (sl == 0) {
     int dev = 0, cus = 256, per = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fold_kernel<VEC>, FOLD_THREADS, 0) !=
-            hipSuccess || per < 1)
-      per = 1;
-    slots = cus * per;
+    const hipError_t e =
+        group ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fold_group_kernel<VEC>, FOLD_THREADS, 0)
+              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fold_kernel<VEC>, FOLD_THREADS, 0);
+    if (e != hipSuccess || per < 1) per = 1;
+    sl = cus * per;
   }
+  const int slots_now = sl;
   // DPZ_FOLD_BLOCKS=N caps the grid at N blocks (A/B diagnostics; 0 = the occupancy slots)
   static const int64_t cap = getenv("DPZ_FOLD_BLOCKS") ? atoll(getenv("DPZ_FOLD_BLOCKS")) : 0;
-  const int64_t g = cap > 0 ? cap : slots;
+  const int64_t g = cap > 0 ? cap : slots_now;
   return (unsigned)(ntiles < g ? (ntiles > 0 ? ntiles : 1) : g);
 }
 
@@ -735,6 +980,22 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
     if (kmax >= 0) {
       dim3 og((unsigned)((kmax + 1 + 1023) / 1024), (unsigned)fa.np);
       DPZ_TIMED(DPZ_KT_FOLD_OFFSETS, st, fold_offsets_kernel<<<og, 256, 0, st>>>(fa, starts));
+    }
+    // all-sparse groups of >= 8 payloads with FOLD_GROUP_MIN .. 2 FG_CAP entries per tile on
+    // average take the slotted fold (measured on MI355X at 25 M x 16 payloads: alpha 0.04
+    // 463 -> 193 us, 0.1 345 -> 284 us; the hit-chain path stays faster at alpha 0.01, the
+    // phase path at alpha 0.2 x 16 and for a few dense payloads); DPZ_FOLD_GROUP=0 / 1 forces it
+    if (fa.all_sparse && fa.np > 0 && !fa.replace_only) {
+      int64_t etot = 0;
+      for (int i = 0; i < fa.np; ++i) etot += fa.p[i].k;
+      bool use_group = fa.np >= 8 && etot > FOLD_GROUP_MIN * ntiles &&
+                       etot <= 2 * (int64_t)FG_CAP * ntiles;
+      if (const char* e = getenv("DPZ_FOLD_GROUP")) use_group = atoi(e) != 0;
+      if (use_group) {
+        if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_group_kernel<true><<<fold_grid<true>(ntiles, true), FOLD_THREADS, 0, st>>>(fa));
+        else DPZ_TIMED(DPZ_KT_FOLD, st, fold_group_kernel<false><<<fold_grid<false>(ntiles, true), FOLD_THREADS, 0, st>>>(fa));
+        continue;
+      }
     }
     if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<true><<<fold_grid<true>(ntiles), FOLD_THREADS, 0, st>>>(fa));
     else DPZ_TIMED(DPZ_KT_FOLD, st, fold_kernel<false><<<fold_grid<false>(ntiles), FOLD_THREADS, 0, st>>>(fa));

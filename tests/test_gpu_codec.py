@@ -260,6 +260,46 @@ def test_fold_all_sparse_overlapping(dev, n, alpha, npay):
     np.testing.assert_array_equal(_bits(out2), _bits(ref2))
 
 
+@pytest.mark.parametrize("group", ["0", "1"])
+@pytest.mark.parametrize("n,alpha,npay", [(1_000_003, 0.01, 16), (1_000_003, 0.1, 16),
+                                          (200_003, 0.4, 3), (100_003, 0.99, 2),
+                                          (300_001, 0.12, 20)])
+def test_fold_paths_forced(dev, monkeypatch, group, n, alpha, npay):
+    """The slotted fold (DPZ_FOLD_GROUP=1: every all-sparse group, incl. sparse alpha, several
+    rounds per tile at alpha 0.99 x 2) and the hit-chain / phase paths (DPZ_FOLD_GROUP=0, also at
+    dense alpha) are each bit-exact vs the oracle, with and without the self term, and with a
+    zero base and accumulation."""
+    monkeypatch.setenv("DPZ_FOLD_GROUP", group)
+    codec = _codec()
+    rng = np.random.default_rng(int(n * alpha) + npay + 17)
+    local = rng.standard_normal(n).astype(np.float32)
+    k = max(1, round(alpha * n))
+    pays, tpays = [], []
+    for i in range(npay):
+        idx = np.sort(rng.choice(n, size=k, replace=False)).astype(np.int32)
+        vals = rng.standard_normal(k).astype(np.float32)
+        pays.append((idx, vals))
+        tpays.append((torch.from_numpy(idx).to(dev), torch.from_numpy(vals).to(dev)))
+    weights = [ofold.mh_weight(npay, int(d)) for d in rng.integers(1, 20, size=npay)]
+    w_self = 1 - sum(weights)
+    tl = torch.from_numpy(local).to(dev)
+    ref = ofold.fold(local, pays, weights, w_self)
+    out = codec.decode_average(tl, tpays, weights, w_self).cpu().numpy()
+    np.testing.assert_array_equal(_bits(out), _bits(ref))
+    ref2 = ofold.fold(local, pays, [1 / npay] * npay, None)
+    out2 = codec.decode_average(tl, tpays, [1 / npay] * npay, None).cpu().numpy()
+    np.testing.assert_array_equal(_bits(out2), _bits(ref2))
+    zeros = np.zeros(n, np.float32)
+    start = rng.standard_normal(n).astype(np.float32)
+    ref3 = start.copy()
+    for (idx, vals), wi in zip(pays, weights):
+        ref3 = ref3 + ofold.replace(zeros, idx, vals) * np.float32(wi)
+    tout = torch.from_numpy(start).to(dev)
+    codec.decode_average(torch.zeros(n, device=dev), tpays, weights, None, zero_base=True,
+                         accumulate=True, out=tout)
+    np.testing.assert_array_equal(_bits(tout.cpu().numpy()), _bits(ref3))
+
+
 @pytest.mark.parametrize("alpha", [0.01, 0.1])
 def test_fold_zero_base_and_accumulate_dense(dev, alpha):
     """DPZ_FOLD_ZERO_BASE (STC's server total: sparse payloads are zero off their entries, the

@@ -12,7 +12,7 @@ from decentralizepy_amd import codec  # noqa: E402
 def main():
     dev = torch.device("cuda:0")
     m = 25_000_009
-    for alpha, npay in ((0.01, 16), (0.01, 4), (0.1, 16), (0.25, 3), (0.4, 3)):
+    for alpha, npay in ((0.01, 16), (0.02, 16), (0.03, 16), (0.04, 16), (0.1, 16), (0.2, 16), (0.4, 3)):
         k = round(alpha * m)
         g = torch.Generator(device=dev).manual_seed(1)
         pays = []
@@ -32,7 +32,7 @@ def main():
                                      workspace=ws)
             torch.cuda.synchronize()
         res = {nm: round(ms / c * 1e3, 2) for nm, (ms, c) in kt.result.items()}
-        print(f"phases={os.environ.get('DPZ_FOLD_PHASES', '0')} alpha={alpha} npay={npay} {res}",
+        print(f"group={os.environ.get('DPZ_FOLD_GROUP', 'auto')} alpha={alpha} npay={npay} {res}",
               flush=True)
 
 
