@@ -104,7 +104,10 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     s_list = [torch.cuda.Stream(dev) for _ in range(S)]
     ws_list = [codec.Workspace(dev) for _ in range(S)]
     multi = codec.NodeStepBatch(sets, n, k, s_list, ws_list)
-    one = codec.NodeStepBatch(sets, n, k, s_list[:1], ws_list[:1])
+    # one node on one stream decodes a neighbour's payload (the previous state's, encoded in the
+    # previous step on the same stream), so its decode is co-scheduled in its encode's launches
+    one = codec.NodeStepBatch(sets, n, k, s_list[:1], ws_list[:1],
+                              decode_src=lambda j: (j - 1) % len(sets))
 
     def run_steps(batch, count, what=DPZ_BATCH_ENCODE | DPZ_BATCH_DECODE):
         for _ in range(count // R):
@@ -156,11 +159,14 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     t_dec = _stage_time(one, DPZ_BATCH_DECODE, reps, run_steps, stream)
     # per-kernel device time: the library brackets every launch with a HIP event pair on the
     # stream it launches on.  A GPU-side spin first lets the host queue all `reps` steps, so the
-    # kernels then run back-to-back (no host-launch gaps inside a pair).
+    # kernels then run back-to-back (no host-launch gaps inside a pair).  Encodes and decodes are
+    # queued as separate loops: a one-stream step co-schedules the decode inside the encoder's
+    # launches (dpz_encode_replace_batch), which would hide the replace kernel's own duration.
     with codec.KernelTimer() as kt:
         with torch.cuda.stream(stream):
             torch.cuda._sleep(int(200e6))  # ~0.1 s of GPU cycles while the steps are enqueued
-        run_steps(one, reps)
+        run_steps(one, reps, DPZ_BATCH_ENCODE)
+        run_steps(one, reps, DPZ_BATCH_DECODE)
         torch.cuda.synchronize()
     kernels = {name: {"avg_us": ms / c * 1e3, "launches_per_step": c / reps}
                for name, (ms, c) in kt.result.items()}
@@ -454,7 +460,8 @@ def main():
                            f"replace decode of node state i on stream i % {r['streams']}"
                            if r["mode"] == "multi" else
                            "native batched enqueue (dpz_encode_replace_batch), one stream; "
-                           "step i = encode -> replace decode of node state i"),
+                           "step i = encode of node state i with the replace decode of state "
+                           "i - 1's payload co-scheduled in the encoder's launches"),
                 "rotated_states": r["rotate"],
             },
             "roofline": {

@@ -6,6 +6,7 @@
 // Python enqueue (~30-50 us) exceeds the kernels' device time, so the loop over nodes lives here:
 // node j goes to stream j % n_streams (one workspace per stream), and its sampled-path status
 // word is copied to status[j] (device) on the same stream so the caller reads all of them once.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include "../../include/dpz_codec.h"
@@ -70,8 +71,25 @@ extern "C" int dpz_encode_replace_batch(int m, int what, const float* const* x,
   if ((what & DPZ_BATCH_ENCODE) && (!x || !idx_out || !val_out || !ws)) return DPZ_ERR_ARG;
   if ((what & DPZ_BATCH_DECODE) && (!r_local || !r_idx || !r_val || !r_out || !dws))
     return DPZ_ERR_ARG;
+  // On ONE stream, a node whose decoded payload is not the one it is encoding (a neighbour's)
+  // runs its encode and decode as one co-scheduled call (dpz_topk_encode_replace: the decode's
+  // chunks ride in the encoder's latency-bound launches; C2 serial step 61.8 -> 59.4 us on
+  // MI355X).  On several streams the other nodes' streaming already fills the tails, and the
+  // plain launches measured faster (C2 3 streams: 41.9 vs 42.7 us).  DPZ_BATCH_COSCHED=0 / 1
+  // forces the stream rule (never the independence rule).
+  static const int cs_env = getenv("DPZ_BATCH_COSCHED") ? atoi(getenv("DPZ_BATCH_COSCHED")) : -1;
+  const bool cosched = cs_env >= 0 ? cs_env != 0 : n_streams == 1;
   for (int j = 0; j < m; ++j) {
     const int q = j % n_streams;
+    if (cosched && (what & DPZ_BATCH_ENCODE) && (what & DPZ_BATCH_DECODE) &&
+        r_idx[j] != idx_out[j] && r_val[j] != val_out[j]) {
+      int rc = dpz_topk_encode_replace(x[j], x0 ? x0[j] : nullptr, nullptr, DPZ_ACC_NONE, x[j], n,
+                                       k, idx_out[j], val_out[j], counter ? counter[j] : nullptr,
+                                       ws[q], ws_bytes, DPZ_TOPK_ASYNC, r_local[j], r_idx[j],
+                                       r_val[j], r_k, n, r_out[j], dws[q], dws_bytes, streams[q]);
+      if (rc != DPZ_OK) return rc;
+      continue;
+    }
     if (what & DPZ_BATCH_ENCODE) {
       int rc = dpz_topk_encode(x[j], x0 ? x0[j] : nullptr, nullptr, DPZ_ACC_NONE, x[j], n, k,
                                idx_out[j], val_out[j], counter ? counter[j] : nullptr, ws[q],

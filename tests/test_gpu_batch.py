@@ -51,6 +51,30 @@ def test_node_step_batch_matches_oracle(dev, streams):
         np.testing.assert_array_equal(_bits(d["out"].cpu().numpy()), _bits(ref))
 
 
+def test_node_step_batch_one_stream_neighbour_decode(dev):
+    """One stream, node j decoding node j - 1's payload: the decode is co-scheduled inside the
+    encode's launches (dpz_encode_replace_batch) and still equals encode + replace."""
+    from decentralizepy_amd import codec
+    n, k, m = 1_000_003, 10_000, 4
+    nodes = [_node(dev, n, k, 60 + j) for j in range(m)]
+    b = codec.NodeStepBatch(nodes, n, k, [torch.cuda.Stream(dev)], [codec.Workspace(dev)],
+                            decode_src=lambda j: (j - 1) % m)
+    b.sticky_status(clear=True)
+    for _ in range(2):  # node 0 reads node m-1's payload of the previous run
+        b.run()
+    torch.cuda.synchronize()
+    assert b.sticky_status() == 0
+    ref = []
+    for d in nodes:
+        oi, ov = otopk.encode(d["x"].cpu().numpy(), d["x0"].cpu().numpy(), None, 0, k)
+        ref.append((oi, ov))
+    for j, d in enumerate(nodes):
+        oi, ov = ref[(j - 1) % m]
+        np.testing.assert_array_equal(_bits(d["out"].cpu().numpy()),
+                                      _bits(ofold.replace(d["x0"].cpu().numpy(), oi, ov)))
+        np.testing.assert_array_equal(d["idx"].cpu().numpy(), ref[j][0])
+
+
 def test_node_step_batch_encode_only_and_decode_only(dev):
     from decentralizepy_amd import codec
     from decentralizepy_amd._lib import DPZ_BATCH_DECODE, DPZ_BATCH_ENCODE
