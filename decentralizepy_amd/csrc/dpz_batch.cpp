@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/dpz_codec.h"
+#include "dpz_topk.h"
 
 extern "C" int dpz_topk_encode_batch(int m, const float* const* x, const float* const* x0,
                                      int64_t n, int64_t k, int32_t* const* counter,
@@ -19,16 +20,13 @@ extern "C" int dpz_topk_encode_batch(int m, const float* const* x, const float* 
   if (m < 0 || n_streams < 1 || !x || !idx_out || !val_out || !ws || !streams) return DPZ_ERR_ARG;
   for (int j = 0; j < m; ++j) {
     const int q = j % n_streams;
-    int rc = dpz_topk_encode(x[j], x0 ? x0[j] : nullptr, nullptr, DPZ_ACC_NONE, x[j], n, k,
-                             idx_out[j], val_out[j], counter ? counter[j] : nullptr, ws[q],
-                             ws_bytes, DPZ_TOPK_ASYNC, streams[q]);
+    // the sampled path's compact writes node j's final status word to status[j] itself (a
+    // separate 4-byte device copy per node cost a blit launch of ~8 us on its stream)
+    int rc = dpz::topk_encode_status(x[j], x0 ? x0[j] : nullptr, x[j], n, k, idx_out[j],
+                                     val_out[j], counter ? counter[j] : nullptr, ws[q], ws_bytes,
+                                     static_cast<hipStream_t>(streams[q]),
+                                     status ? status + j : nullptr);
     if (rc != DPZ_OK) return rc;
-    if (status) {
-      // TopkCtrl.status is the third 32-bit word of the workspace (dpz_topk.h)
-      hipError_t e = hipMemcpyAsync(status + j, static_cast<char*>(ws[q]) + 8, sizeof(int32_t),
-                                    hipMemcpyDeviceToDevice, static_cast<hipStream_t>(streams[q]));
-      if (e != hipSuccess) return (int)e;
-    }
   }
   return DPZ_OK;
 }

@@ -244,6 +244,8 @@ struct EncodeArgs {
   int64_t n, k; int32_t* idx_out; float* val_out; int32_t* counter; char* ws;
   hipStream_t st;
   const ReplaceJob* job;  // co-scheduled replace decode (sampled path only), or nullptr
+  int32_t* status_out;    // sampled path, ASYNC: compact's block 0 also writes the call's final
+                          // status word here (device), or nullptr
 };
 
 // dpz_topk_exact.hip / dpz_topk_sampled.hip
@@ -253,6 +255,11 @@ int run_exact(const EncodeArgs& a, const WsLayout& L, int rekey, bool vec, int k
               int64_t cap = 0);
 // phases: bit 0 = streaming pass (sample, filter), bit 1 = selection tail (select .. compact)
 int run_sampled(const EncodeArgs& a, const WsLayout& L, bool vec, int phases = 3);
+// dpz_topk_encode with the final sampled-path status word also written to status_out (device)
+// on the stream, as the call's last write: no separate copy (dpz_topk_encode_batch)
+int topk_encode_status(const float* x, const float* x0, const float* vals_src, int64_t n,
+                       int64_t k, int32_t* idx_out, float* val_out, int32_t* counter, void* ws,
+                       size_t ws_bytes, hipStream_t st, int32_t* status_out);
 static inline bool use_sampled(int64_t n, int64_t k) {
   return n >= (1 << 18) && k >= 1 && k <= n / 2;
 }

@@ -114,6 +114,25 @@ extern "C" int dpz_topk_encode(const float* x, const float* x0, float* acc, int 
   return dpz_topk_dispatch(a, flags);
 }
 
+namespace dpz {
+int topk_encode_status(const float* x, const float* x0, const float* vals_src, int64_t n,
+                       int64_t k, int32_t* idx_out, float* val_out, int32_t* counter, void* ws,
+                       size_t ws_bytes, hipStream_t st, int32_t* status_out) {
+  EncodeArgs a{x, x0, nullptr, DPZ_ACC_NONE, vals_src, n, k, idx_out, val_out, counter,
+               static_cast<char*>(ws), st};
+  int rc = validate(a, ws_bytes);
+  if (rc != DPZ_OK) return rc;
+  if (n == 0 || k == 0 || !use_sampled(n, k)) {  // no sampled tail writes it: status 0
+    if (n > 0) rc = dpz_topk_dispatch(a, DPZ_TOPK_ASYNC);
+    if (rc != DPZ_OK) return rc;
+    if (status_out) DPZ_HIP_TRY(hipMemsetAsync(status_out, 0, sizeof(int32_t), st));
+    return DPZ_OK;
+  }
+  a.status_out = status_out;
+  return dpz_topk_dispatch(a, DPZ_TOPK_ASYNC);
+}
+}  // namespace dpz
+
 static bool overlaps(const void* p, size_t pb, const void* q, size_t qb) {
   if (!p || !q || pb == 0 || qb == 0) return false;
   const uintptr_t a = reinterpret_cast<uintptr_t>(p), b = reinterpret_cast<uintptr_t>(q);

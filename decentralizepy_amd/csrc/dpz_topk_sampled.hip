@@ -816,7 +816,8 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     const uint32_t* __restrict__ blkey, const uint32_t* __restrict__ blidx,
     const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ cidx,
     const uint32_t* __restrict__ ckey, const float* __restrict__ cval, const float* vals_src,
-    int32_t* idx_out, float* val_out, int32_t* counter, float* rewind, ReplaceJob pj) {
+    int32_t* idx_out, float* val_out, int32_t* counter, float* rewind, int32_t* status_out,
+    ReplaceJob pj) {
   __shared__ uint32_t wcnt[CSEG];
   __shared__ uint32_t subbase[NSUB + 1];
   __shared__ uint32_t flag, spec;
@@ -884,7 +885,10 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     for (int b = t; b < CB; b += 256) chist[b] = 0;
   }
   if (status) {  // select reported a miss: the host runs the exact path
-    if (blockIdx.x == 0 && t == 0) atomicOr(&ctrl->sticky, status);
+    if (blockIdx.x == 0 && t == 0) {
+      atomicOr(&ctrl->sticky, status);
+      if (status_out) *status_out = (int32_t)status;
+    }
     return;
   }
   // When the values are not carried from the filter (vals_src != x), every candidate of chunk 0
@@ -914,6 +918,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     if (blockIdx.x == 0 && t == 0) {
       ctrl->status = 1;
       atomicOr(&ctrl->sticky, 1u);
+      if (status_out) *status_out = 1;
     }
     return;
   }
@@ -949,6 +954,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
       ctrl->status = 2;
       atomicOr(&ctrl->sticky, 2u);
     }
+    if (status_out) *status_out = grand != (uint32_t)k ? 2 : 0;
   }
   if (grand != (uint32_t)k) return;  // identical in every block: nothing is written
   // chunks 1 .. PFC-1 of every segment with more than 64 candidates: all issued together
@@ -1124,7 +1130,7 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
   const unsigned ncmp = (unsigned)((g.W + CSEG - 1) / CSEG);
   DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC><<<ncmp + pb[2], 256, 0, a.st>>>(
       s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, cidx,
-      ckey, cval, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, jb[2]));
+      ckey, cval, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, a.status_out, jb[2]));
   return DPZ_OK;
 }
 
