@@ -300,6 +300,32 @@ def test_fold_paths_forced(dev, monkeypatch, group, n, alpha, npay):
     np.testing.assert_array_equal(_bits(tout.cpu().numpy()), _bits(ref3))
 
 
+@pytest.mark.parametrize("group", ["0", "1"])
+@pytest.mark.parametrize("alpha", [0.01, 0.1])
+def test_fold_unaligned_views(dev, monkeypatch, group, alpha):
+    """local / out 4 bytes off a 16-byte boundary: the scalar-load (VEC = false) builds of the
+    hit-chain, phase and slotted fold kernels, bit-exact."""
+    monkeypatch.setenv("DPZ_FOLD_GROUP", group)
+    codec = _codec()
+    n, npay = 300_001, 16
+    rng = np.random.default_rng(int(alpha * 100) + 5)
+    local = rng.standard_normal(n + 1).astype(np.float32)
+    k = round(alpha * n)
+    pays, tpays = [], []
+    for i in range(npay):
+        idx = np.sort(rng.choice(n, size=k, replace=False)).astype(np.int32)
+        vals = rng.standard_normal(k).astype(np.float32)
+        pays.append((idx, vals))
+        tpays.append((torch.from_numpy(idx).to(dev), torch.from_numpy(vals).to(dev)))
+    weights = [1.0 / (npay + 1)] * npay
+    tl = torch.from_numpy(local).to(dev)[1:]
+    out = torch.empty(n + 1, device=dev)[1:]
+    assert tl.data_ptr() % 16 and out.data_ptr() % 16
+    codec.decode_average(tl, tpays, weights, 1.0 / (npay + 1), out=out)
+    ref = ofold.fold(local[1:], pays, weights, 1.0 / (npay + 1))
+    np.testing.assert_array_equal(_bits(out.cpu().numpy()), _bits(ref))
+
+
 @pytest.mark.parametrize("alpha", [0.01, 0.1])
 def test_fold_zero_base_and_accumulate_dense(dev, alpha):
     """DPZ_FOLD_ZERO_BASE (STC's server total: sparse payloads are zero off their entries, the
