@@ -148,6 +148,16 @@ static_assert(HB % 256 == 0 && HB <= 1024, "fine bins: multiple of 256, at most 
 #define DPZ_FG 2
 #endif
 constexpr int W_MAX = DPZ_WMAX;    // wave segments (one wave streams one contiguous segment)
+// Up to W_SMALL_N elements the filter runs at most W_SMALL segments: measured on MI355X with 3
+// node codecs per GPU (bench default), C2 (11 M) 41.4 -> 38.3 us per step and 64 MiB 59.5 ->
+// 54.5 us — a filter grid that leaves CU slots free lets the other streams' kernels run beside
+// it — with the one-node step unchanged; at 25 M (C3, accumulation) and 67 M (C5) the full
+// W_MAX measured faster (tools/diag/ab_bench.sh, workload_ab.sh).
+#ifndef DPZ_WSMALL
+#define DPZ_WSMALL 3072
+#endif
+constexpr int W_SMALL = DPZ_WSMALL;
+constexpr int64_t W_SMALL_N = (1 << 24) + (1 << 22);
 constexpr int FG = DPZ_FG;         // float4 groups of 256 elements a filter wave loads at once
 #ifndef DPZ_FOCC
 #define DPZ_FOCC 8
@@ -185,7 +195,8 @@ struct FastGeom {
 static inline FastGeom fast_geom(int64_t n, int64_t k = 0) {
   FastGeom g;
   int64_t W = (n + W_MIN_RANGE - 1) / W_MIN_RANGE;
-  if (W > W_MAX) W = W_MAX;
+  const int64_t wmax = n <= W_SMALL_N ? W_SMALL : W_MAX;
+  if (W > wmax) W = wmax;
   if (W < 1) W = 1;
   int64_t R = (n + W - 1) / W;
   R = (R + 3) & ~int64_t(3);
