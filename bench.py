@@ -53,7 +53,42 @@ def parse():
                    help="S > 1: S independent node codecs share the GPU on S streams (as "
                         "decentralizepy runs procs_per_machine nodes per machine); the one-node "
                         "(one stream) rate is always measured beside it")
+    p.add_argument("--repeats", type=int, default=0,
+                   help="timed regions of exactly --steps steps each (0: auto, enough for a "
+                        "stable median at small --steps); the line reports the median region")
     return p.parse_args()
+
+
+def spawn_ranks(args):
+    """``bench.py --gpus N`` (N > 1) started WITHOUT a launcher: run N ranks, one process per
+    GPU, under torch.distributed.run as a child process and exit with its code.  This parent
+    never makes a HIP call (no GPU initialised before the ranks start); it times the CPU
+    baseline first (host cores only) and hands it to rank 0 through a file, so the ranks' GPU
+    work and the CPU sample never overlap."""
+    import socket
+    import subprocess
+    import tempfile
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    path = None
+    if not args.no_cpu and args.workload == "c2":
+        cpu = cpu_baseline(args.n, args.alpha, args.cpu_seconds)
+        fd, path = tempfile.mkstemp(prefix="dpz_cpu_", suffix=".json")
+        with os.fdopen(fd, "w") as f:
+            json.dump(cpu, f)
+        env["DPZ_BENCH_CPU_BASELINE"] = path
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    try:
+        rc = subprocess.call(cmd, env=env)
+    finally:
+        if path:
+            os.unlink(path)
+    return rc
 
 
 def timed_loop(fn, reps, stream):
@@ -72,7 +107,7 @@ def timed_loop(fn, reps, stream):
 L3_BYTES = 256 * 2 ** 20  # MI355X Infinity Cache (MI355X_MICROARCH.md § Infinity Cache)
 
 
-def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, streams=3):
+def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, streams=3, repeats=9):
     """Time `steps` encode+decode steps.  Consecutive steps rotate over R independent node states
     (x, x0, counter, payload, output) so the timed working set is > 2x the 256 MiB Infinity
     Cache: every step streams its inputs from HBM, as a real round does after training.
@@ -121,7 +156,7 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     torch.cuda.synchronize()
     multi.sticky_status(clear=True)
 
-    def timed(batch, count):
+    def timed_once(batch, count):
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
@@ -139,6 +174,15 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
             t = float(tt.item())
         return t / count, t_host / count
 
+    def timed(batch, count):
+        """`repeats` timed regions of exactly `count` steps, each bracketed by barrier +
+        synchronize and max-over-ranks; the median region is the result (a 20-step region is
+        under 1 ms of device time, so one host hiccup would otherwise move the line)."""
+        res = sorted(timed_once(batch, count) for _ in range(repeats))
+        spread.append([res[0][0], res[len(res) // 2][0], res[-1][0]])
+        return res[len(res) // 2]
+
+    spread = []
     s_multi, h_multi = timed(multi, steps)
     s_serial, h_serial = timed(one, steps)
     status = multi.sticky_status(clear=True)  # every timed encode of both loops
@@ -175,7 +219,9 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     fell_back |= multi.sticky_status(clear=True) != 0
     return dict(n=n, k=k, s_step=s_step, s_multi=s_multi, s_serial=s_serial, s_host=s_host,
                 mode=mode, streams=S, fell_back=fell_back, t_enc=t_enc, t_dec=t_dec,
-                b_enc=b_enc, b_dec=b_dec, kernels=kernels, rotate=R,
+                b_enc=b_enc, b_dec=b_dec, kernels=kernels, rotate=R, repeats=repeats,
+                spread_ms={"multi": [round(v * 1e3, 5) for v in spread[0]],
+                           "serial": [round(v * 1e3, 5) for v in spread[1]]},
                 value=world * 4 * n / s_step / 2 ** 30)
 
 
@@ -194,7 +240,7 @@ def _stage_time(batch, what, reps, run_steps, stream):
     return ev0.elapsed_time(ev1) / reps * 1e-3
 
 
-def gossip_case(n, alpha, dev, rank, world, dist, rounds, warmup):
+def gossip_case(n, alpha, dev, rank, world, dist, rounds, warmup, exchange="allgather"):
     """C4: one synchronous gossip round of the 96-node regular topology (reference
     eval/96_regular.edges, copied as data under tests/golden/), nodes sharded over the ranks,
     payloads exchanged by one RCCL all-gather (decentralizepy_amd/gossip.py).  A "training"
@@ -204,7 +250,7 @@ def gossip_case(n, alpha, dev, rank, world, dist, rounds, warmup):
     lo, hi, _ = shard(len(adj), world, rank)
     g = torch.Generator(device=dev).manual_seed(77 + rank)
     x = torch.randn(hi - lo, n, device=dev, generator=g)
-    eng = GossipRound(adj, x, alpha, rank=rank, world=world, device=dev)
+    eng = GossipRound(adj, x, alpha, rank=rank, world=world, device=dev, exchange=exchange)
     del x
     noise = 0.01 * torch.randn(hi - lo, n, device=dev, generator=g)
     total = 0.0
@@ -226,9 +272,18 @@ def gossip_case(n, alpha, dev, rank, world, dist, rounds, warmup):
         if r >= warmup:
             total += dt
     s_round = total / rounds
+    # per-leg times (encode / exchange / fold, or the reduce-scatter legs) from two more rounds
+    # with a synchronize between legs: a breakdown beside the timed rounds, not part of them
+    eng.leg_times = {}
+    for _ in range(2):
+        eng.x += noise
+        eng.step()
+    legs = {nm: round(v / 2 * 1e3, 4) for nm, v in eng.leg_times.items()}
+    eng.leg_times = None
     k = eng.k
     nsum = sum(len(a) for a in adj)
-    return dict(n=n, k=k, s_step=s_round, nodes=len(adj), edges=nsum // 2,
+    return dict(n=n, k=k, s_step=s_round, nodes=len(adj), edges=nsum // 2, legs_ms=legs,
+                rs_group=getattr(eng, "rs_group", None),
                 value=len(adj) * 4 * n / s_round / 2 ** 30,
                 alg_bytes=len(adj) * (8 * n + 16 * k) + len(adj) * 8 * n + nsum * 8 * k)
 
@@ -292,7 +347,15 @@ def cpu_baseline(n, alpha, seconds):
     t, times = _cpu_steps(n, alpha, seconds, cores)
     share = max(1, cores // 16)
     t1, times1 = _cpu_steps(n, alpha, max(3.0, seconds / 2), share)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = None
     return dict(value=4 * n / t / 2 ** 30, unit="GiB/s", cores=cores,
+                host_cpu_count=os.cpu_count(), affinity_cpus=affinity,
+                cores_note=(f"{cores} threads used (torch intra-op threads = this job's CPU "
+                            f"share); the host reports {os.cpu_count()} logical CPUs, "
+                            f"{affinity} in this process's affinity mask"),
                 kind="port",
                 sample=f"reference ATen-CPU op sequence (oracle/ref_ops.py), N={n}, k={round(alpha*n)}, "
                        f"median of {len(times)} encode+decode steps ({sum(times):.1f} s) at "
@@ -302,11 +365,21 @@ def cpu_baseline(n, alpha, seconds):
                                 "note": "floor(cores / 16): one of 16 node processes per machine"})
 
 
+def _finish(dist):
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))  # the parent never touches the GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were started")
     dist = None
     if world > 1:
         import torch.distributed as dist_mod
@@ -315,15 +388,19 @@ def main():
         dist = dist_mod
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
+    repeats = args.repeats or max(5, min(25, math.ceil(4000 / max(1, args.steps))))
 
     if args.workload == "c4":
         rounds = max(3, min(args.steps, 20))
-        r = gossip_case(args.n, args.alpha, dev, rank, world, dist, rounds, max(1, min(args.warmup, 3)))
+        warm = max(1, min(args.warmup, 3))
+        r = gossip_case(args.n, args.alpha, dev, rank, world, dist, rounds, warm)
+        rs = gossip_case(args.n, args.alpha, dev, rank, world, dist, max(3, rounds // 2), warm,
+                         exchange="reduce_scatter")
         if rank == 0:
             print(json.dumps({
                 "metric": "GiB/s fp32 params encoded+decoded (device-resident), 1% top-k",
                 "value": round(r["value"], 3), "unit": "GiB/s", "n_gpus": world,
-                "steps": rounds, "warmup": max(1, min(args.warmup, 3)),
+                "steps": rounds, "warmup": warm,
                 "ms_per_step": round(r["s_step"] * 1e3, 4), "higher_is_better": True,
                 "scaling": "strong", "vs_baseline": None, "dtype": "f32",
                 "data": "synthetic (x ~ N(0,1), +0.01*N(0,1) per round), device-generated",
@@ -335,10 +412,18 @@ def main():
                                           "RCCL all-gather of the payloads per round"},
                 "round_alg_bytes": r["alg_bytes"],
                 "round_frac_of_hbm_peak": round(r["alg_bytes"] / r["s_step"] / 1e9 / HBM_PEAK_GBS / world, 4),
+                "legs_ms": r["legs_ms"],
+                "reduce_scatter_mode": {
+                    "note": "the over-HBM exchange forced (exchange='reduce_scatter'): payloads "
+                            "never replicated; per destination group one batched zero-base fold "
+                            "of the owned (A, B) rows, one packed RCCL reduce-scatter, the "
+                            "owner's combine" + ("" if world > 1 else
+                                                 " (1 GPU: no collective, the legs still run)"),
+                    "ms_per_round": round(rs["s_step"] * 1e3, 4),
+                    "value": round(rs["value"], 3), "legs_ms": rs["legs_ms"],
+                    "rs_group": rs["rs_group"]},
             }), flush=True)
-        if dist is not None:
-            dist.barrier()
-            dist.destroy_process_group()
+        _finish(dist)
         return
     if args.workload in ("c3", "c5", "e2e", "shard", "fft", "wire"):
         import bench_workloads as bw
@@ -351,6 +436,7 @@ def main():
         elif args.workload == "c3":
             r = [bw.c3_case(dev, alpha=a, steps=min(args.steps, 40)) for a in (0.01, 0.1)]
             r.append(bw.c3_case(dev, alpha=0.01, steps=min(args.steps, 40), wavelet="haar"))
+            r.append(bw.c3_round_case(dev, rank, world, dist, rounds=min(args.steps, 10)))
         elif args.workload == "c5":
             r = bw.c5_case(dev, steps=min(args.steps, 40), streams=args.streams)
         else:
@@ -362,30 +448,32 @@ def main():
             print(json.dumps({"metric": "GiB/s fp32 params encoded+decoded", "unit": "GiB/s",
                               "workload": args.workload, "n_gpus": world, "result": r}),
                   flush=True)
-        if dist is not None:
-            dist.barrier()
-            dist.destroy_process_group()
+        _finish(dist)
         return
     r = gpu_case(args.n, args.alpha, dev, 1234 + rank, args.steps, args.warmup, world, dist,
-                 rotate=args.rotate, streams=args.streams)
+                 rotate=args.rotate, streams=args.streams, repeats=repeats)
     extra = None
-    if not args.no_extra and world == 1:
-        e = gpu_case(16_777_216, 0.01, dev, 99, max(20, args.steps // 2), args.warmup, 1, None,
-                     streams=args.streams)
-        extra = {"workload": "north-star target: 64 MiB fp32 tensor (N=16,777,216), 1% top-k",
+    if not args.no_extra:
+        # the north-star tensor, every rank its own node's 64 MiB model (weak, like the headline)
+        e = gpu_case(16_777_216, 0.01, dev, 99 + rank, max(20, args.steps // 2), args.warmup,
+                     world, dist, streams=args.streams, repeats=repeats)
+        b = (e["b_enc"] + e["b_dec"]) * world
+        extra = {"workload": "north-star target: 64 MiB fp32 tensor (N=16,777,216), 1% top-k, "
+                             "one per GPU",
                  "value": round(e["value"], 2), "ms_per_step": round(e["s_step"] * 1e3, 4),
-                 "frac_of_hbm_peak": round((e["b_enc"] + e["b_dec"]) / e["s_step"] / 1e9 / HBM_PEAK_GBS, 4),
+                 "frac_of_hbm_peak": round(b / e["s_step"] / 1e9 / HBM_PEAK_GBS / world, 4),
                  "launch": e["mode"],
                  "one_node_serial_ms_per_step": round(e["s_serial"] * 1e3, 4),
-                 "one_node_frac_of_hbm_peak": round((e["b_enc"] + e["b_dec"]) / e["s_serial"] / 1e9 / HBM_PEAK_GBS, 4),
+                 "one_node_frac_of_hbm_peak": round(b / e["s_serial"] / 1e9 / HBM_PEAK_GBS / world, 4),
                  f"{e['streams']}_node_ms_per_step": round(e["s_multi"] * 1e3, 4),
                  "host_enqueue_ms_per_step": round(e["s_host"] * 1e3, 4),
+                 "spread_ms": e["spread_ms"],
                  "fell_back": e["fell_back"]}
 
     # the gossip round of BASELINE.json C4 (eval/96_regular.edges) at every N: the nodes are
     # sharded over the ranks and each round's payloads cross ranks in one RCCL all-gather, so a
     # multi-GPU run of this bench also times the collective path (strong scaling, 96 nodes fixed)
-    gossip = None
+    gossip = shard_line = None
     if not args.no_extra:
         gr = gossip_case(args.n, args.alpha, dev, rank, world, dist, rounds=5, warmup=2)
         gossip = {"workload": "C4: one gossip round of eval/96_regular.edges (96 nodes, 190 "
@@ -396,9 +484,16 @@ def main():
                   "parallelism": f"{gr['nodes']} nodes sharded over {world} GPU(s), "
                                  + ("one RCCL all-gather of the payloads per round" if world > 1
                                     else "no collective on one GPU"),
+                  "legs_ms": gr["legs_ms"],
                   "round_alg_bytes": gr["alg_bytes"],
                   "round_frac_of_hbm_peak": round(gr["alg_bytes"] / gr["s_step"] / 1e9
                                                   / HBM_PEAK_GBS / world, 4)}
+        torch.cuda.empty_cache()
+        # one C5 tensor (256 MiB, alpha 0.001) sharded over the ranks: the sharded top-k's
+        # candidate all-gather is the collective (strong scaling)
+        import bench_workloads as bw
+        sh = bw.shard_case(dev, rank, world, dist, steps=20)
+        shard_line = {k_: (round(v, 4) if isinstance(v, float) else v) for k_, v in sh.items()}
         torch.cuda.empty_cache()
 
     copy_gbs = None
@@ -412,8 +507,17 @@ def main():
         del a, b
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.n, args.alpha, args.cpu_seconds)
+    if rank == 0 and not args.no_cpu:
+        path = os.environ.get("DPZ_BENCH_CPU_BASELINE")
+        if path and os.path.exists(path):  # timed by the spawning parent before the ranks
+            with open(path) as f:
+                cpu = json.load(f)
+            cpu["timed_by"] = "the bench.py parent process before the GPU ranks started"
+        else:
+            cpu = cpu_baseline(args.n, args.alpha,
+                               args.cpu_seconds if world == 1 else min(args.cpu_seconds, 8.0))
+            if world > 1:
+                cpu["timed_by"] = "rank 0 after the GPU legs (the other ranks wait at a barrier)"
 
     if rank == 0:
         t_enc, t_dec = r["t_enc"], r["t_dec"]
@@ -473,7 +577,10 @@ def main():
                            "step i = encode of node state i with the replace decode of state "
                            "i - 1's payload co-scheduled in the encoder's launches"),
                 "rotated_states": r["rotate"],
+                "timing": (f"median of {r['repeats']} timed regions of exactly {args.steps} "
+                           f"steps (each: barrier + synchronize on both sides, max over ranks)"),
             },
+            "spread_ms_per_step": r["spread_ms"],
             "roofline": {
                 "bound": "hbm",
                 "kernel": dom,
@@ -502,11 +609,10 @@ def main():
             "cpu_baseline": cpu,
             "secondary": extra,
             "gossip_round": gossip,
+            "shard": shard_line,
         }
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    _finish(dist)
 
 
 if __name__ == "__main__":

@@ -103,6 +103,70 @@ def c3_case(dev, n=25_000_000, alpha=0.01, npay=16, steps=40, warmup=5, seed=3, 
                 kernels_avg_us=kern)
 
 
+def c3_round_case(dev, rank, world, dist, n=25_000_000, rounds=10, warmup=2, seed=21,
+                  wavelet="sym2"):
+    """C3 shape (b): the topology-faithful JWINS round of tutorial/JWINS/regular_16.txt (16 nodes
+    of degree 3, copied under tests/golden/) with the tutorial config (sym2 level 4, alpha_list
+    [0.1, 0.15, 0.2, 0.25, 0.3, 0.4, 1.0] drawn per node from random.seed(uid), metadata_cap
+    0.5, accumulation + accumulate_averaging_changes): every node encodes (DWT pair, top-k with
+    ADD accumulation, or a full share), payloads all-gathered over RCCL when world > 1, every
+    node folds its 3 neighbours in the wavelet domain, IDWT, accumulating post-step
+    (decentralizepy_amd/gossip_jwins.py).  The alpha draws are deterministic, so the timed rounds
+    are the same sequence on every run.  Algorithmic bytes per node: DWT pair 8N + 8M; encode
+    read W(dx), acc 8M + 20k (idx, val, counter r+w, acc rewind), or a 4M acc zeroing; fold 4M +
+    payloads + 4M; IDWT 4M + 4N; post-step 8N + 8M; init_model copy 8N."""
+    import os
+
+    from decentralizepy_amd.gossip import read_edges, shard
+    from decentralizepy_amd.gossip_jwins import JwinsRound
+    here = os.path.dirname(os.path.abspath(__file__))
+    adj = read_edges(os.path.join(here, "tests", "golden", "regular_16.edges"))
+    lo, hi, _ = shard(len(adj), world, rank)
+    g = torch.Generator(device=dev).manual_seed(seed + rank)
+    x = torch.randn(hi - lo, n, device=dev, generator=g)
+    eng = JwinsRound(adj, x, "[0.1,0.15,0.2,0.25,0.3,0.4,1.0]", rank=rank, world=world,
+                     wavelet=wavelet, metadata_cap=0.5, device=dev)
+    del x
+    noise = 0.01 * torch.randn(hi - lo, n, device=dev, generator=g)
+    m = eng.M
+    times, alg = [], []
+    for r in range(warmup + rounds):
+        eng.x += noise
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        eng.step()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if dist is not None:
+            tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        if r >= warmup:
+            times.append(dt)
+            b = 0
+            for i in range(len(adj)):
+                a = eng.alphas[i]
+                k = round(a * m) if a < 0.5 else 0
+                b += 8 * n + 8 * m + (8 * m + 20 * k if k else 4 * m)
+                b += 8 * m + sum((8 * round(eng.alphas[q] * m) if eng.alphas[q] < 0.5 else 4 * m)
+                                 for q in adj[i])
+                b += 4 * m + 4 * n + 8 * n + 8 * m + 8 * n
+            alg.append(b)
+    t = sum(times) / len(times)
+    b = sum(alg) / len(alg)
+    return dict(workload=f"C3 shape (b): JWINS round of regular_16 (16 nodes x degree 3), "
+                         f"N={n} per node, {wavelet} level 4, tutorial alpha_list",
+                n=n, m=m, nodes=len(adj), world=world, rounds=rounds,
+                ms_per_round=t * 1e3, ms_per_round_min=min(times) * 1e3,
+                value=len(adj) * 4 * n / t / 2 ** 30,
+                alg_bytes_per_round=b, round_frac_of_hbm_peak=b / t / 8e12 / world,
+                scaling="strong (16 nodes fixed)")
+
+
 def c5_case(dev, n=67_108_864, alpha=0.001, steps=40, warmup=5, seed=5, streams=3):
     """C5: 256 MiB fp32 tensor, 0.1 % top-k, payload values packed to fp16 (RNE, torch.half
     semantics): encode = top-k + fp16 pack; decode = fp16 unpack + replace.  B = 16N + 12k."""

@@ -21,15 +21,26 @@ def pick_device(rank):
     return torch.device("cuda", int(rank) % torch.cuda.device_count())
 
 
+def _pinned_cap():
+    """Pinned host bytes one plugin may hold (DPZ_PINNED_MB, default 1024 MiB).  decentralizepy
+    runs procs_per_machine node processes per host (16 in the tutorial), each with its own
+    staging, so the cap bounds the page-locked total per machine."""
+    return int(float(os.environ.get("DPZ_PINNED_MB", "1024")) * 2 ** 20)
+
+
 class Staging:
-    """Reusable pinned host buffers keyed by (name, dtype); grown on demand.
+    """Reusable pinned host buffers keyed by (name, dtype); grown on demand, within a byte cap.
 
     A buffer handed out again waits for the last asynchronous copy that read it (``mark``),
-    so a pinned source is never overwritten while its DMA is in flight."""
+    so a pinned source is never overwritten while its DMA is in flight.  ``get`` returns None
+    when a buffer would take the total past ``cap_bytes``: the caller then copies through
+    pageable memory (synchronous, correct, slower)."""
 
-    def __init__(self):
+    def __init__(self, cap_bytes=None):
         self._bufs = {}
         self._events = {}
+        self.cap = _pinned_cap() if cap_bytes is None else int(cap_bytes)
+        self.total = 0
 
     def get(self, name, n, dtype):
         key = (name, dtype)
@@ -38,8 +49,15 @@ class Staging:
             ev.synchronize()
         buf = self._bufs.get(key)
         if buf is None or buf.numel() < n:
+            size = max(int(n), 1) * torch.empty(0, dtype=dtype).element_size()
+            old = 0 if buf is None else buf.numel() * buf.element_size()
+            if self.total - old + size > self.cap:
+                return None
+            self._bufs.pop(key, None)
+            del buf
             buf = torch.empty(max(int(n), 1), dtype=dtype, pin_memory=True)
             self._bufs[key] = buf
+            self.total += size - old
         return buf[:n]
 
     def mark(self, name, dtype, stream):
@@ -64,6 +82,8 @@ def to_device_flat(flat_cpu, device, staging, name):
         raise NotImplementedError(
             f"the flattened model is {flat_cpu.dtype}; the HIP codec handles fp32 models only")
     host = staging.get(name, flat_cpu.numel(), torch.float32)
+    if host is None:  # over the pinned cap: pageable copy
+        return flat_cpu.to(device)
     host.copy_(flat_cpu)
     out = host.to(device, non_blocking=True)
     staging.mark(name, torch.float32, torch.cuda.current_stream(device))
@@ -79,6 +99,8 @@ def h2d_array(arr, dtype, device, staging, name):
     a = np.ascontiguousarray(arr, dtype=dtype)
     tdt = torch.from_numpy(a[:0]).dtype
     host = staging.get(name, a.size, tdt)
+    if host is None:  # over the pinned cap: pageable copy
+        return torch.from_numpy(a.reshape(-1)).to(device)
     host.numpy()[...] = a.reshape(-1)
     out = host.to(device, non_blocking=True)
     staging.mark(name, tdt, torch.cuda.current_stream(device))
@@ -87,10 +109,12 @@ def h2d_array(arr, dtype, device, staging, name):
 
 class PayloadNames:
     """Pinned-buffer names for received payload legs: a ring of ``slots`` names, so consecutive
-    legs use distinct buffers and a reused buffer waits only for its own earlier DMA (Staging);
-    the pinned memory stays bounded."""
+    legs use distinct buffers and a reused buffer waits only for its own earlier DMA (Staging).
+    A few slots cover the legs in flight (the next payload's host work overlaps the previous
+    DMA); more would only pin more memory: a full-model payload (Sharing, Choco) pins 4N bytes
+    per slot, within the Staging cap."""
 
-    def __init__(self, slots=64):
+    def __init__(self, slots=8):
         self.i = 0
         self.slots = slots
 
@@ -102,6 +126,8 @@ class PayloadNames:
 def to_host(t, staging, name):
     """D2H into a pinned buffer; returns a numpy array that owns its memory."""
     host = staging.get(name, t.numel(), t.dtype)
+    if host is None:  # over the pinned cap: pageable copy
+        return t.cpu().numpy().copy()
     host.copy_(t, non_blocking=True)
     torch.cuda.current_stream(t.device).synchronize()
     return host.numpy().copy()

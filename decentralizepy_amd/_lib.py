@@ -20,6 +20,7 @@ DPZ_TOPK_EXACT = 0x1
 DPZ_TOPK_ASYNC = 0x2
 DPZ_TOPK_STREAM = 0x4
 DPZ_TOPK_TAIL = 0x8
+DPZ_TOPK_SHARED = 0x10
 DPZ_FOLD_SELF = 0x1
 DPZ_FOLD_REPLACE_ONLY = 0x2
 DPZ_FOLD_ZERO_BASE = 0x4
@@ -51,6 +52,9 @@ SIGNATURES = {
     "dpz_topk_workspace_bytes": (_size, [_i64, _i64]),
     "dpz_topk_encode": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64, _i64,
                                _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size, _int, _c_void_p]),
+    "dpz_topk_encode_status": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64,
+                                      _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
+                                      _c_void_p, _c_void_p]),
     "dpz_topk_encode_replace": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64,
                                        _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
                                        _int, _c_void_p, _c_void_p, _c_void_p, _i64, _i64,

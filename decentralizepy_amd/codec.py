@@ -81,7 +81,7 @@ class Workspace:
 
 def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, counter=None,
                 idx_out=None, val_out=None, workspace=None, exact=False, asynchronous=False,
-                phase=None, co_replace=None):
+                phase=None, co_replace=None, status_out=None, shared=False):
     """Top-k magnitude encode (reference PartialModel.py:164-255 / Wavelet.py:142-197).
 
     Returns ``(idx int32[k], val fp32[k])`` in ascending index order.  Mutates ``acc`` and
@@ -93,7 +93,10 @@ def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, c
     ``co_replace=(local, idx, vals, out)`` also performs the independent decode
     ``replace(local, idx, vals, out=out)`` of a received payload inside the encoder's
     latency-bound selection launches (dpz_topk_encode_replace); it is complete when the encode's
-    stream work is.
+    stream work is.  ``status_out`` (a 1-element int32 device tensor or view): asynchronous
+    encode whose final status word (0 = final, else re-run with ``exact=True``) is written there
+    on the device (dpz_topk_encode_status).  ``shared``: several codecs run concurrently on the
+    GPU (DPZ_TOPK_SHARED: the smaller filter grid); identical results.
     """
     _require(x, torch.float32, "x")
     _require(x0, torch.float32, "x0")
@@ -109,9 +112,20 @@ def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, c
     if val_out is None:
         val_out = torch.empty(k, dtype=torch.float32, device=x.device)
     ws = (workspace or Workspace(x.device)).get(n, k)
-    flags = (DPZ_TOPK_EXACT if exact else 0) | (DPZ_TOPK_ASYNC if asynchronous else 0)
+    flags = ((DPZ_TOPK_EXACT if exact else 0) | (DPZ_TOPK_ASYNC if asynchronous else 0)
+             | (_lib.DPZ_TOPK_SHARED if shared else 0))
     if phase is not None:
         flags |= {"stream": DPZ_TOPK_STREAM, "tail": DPZ_TOPK_TAIL}[phase]
+    if status_out is not None:
+        _require(status_out, torch.int32, "status_out")
+        if co_replace is not None or phase is not None or exact:
+            raise ValueError("status_out: a plain sampled-path encode only")
+        rc = _lib.lib().dpz_topk_encode_status(_ptr(x), _ptr(x0), _ptr(acc), int(acc_mode),
+                                               _ptr(vals_src), n, k, _ptr(idx_out), _ptr(val_out),
+                                               _ptr(counter), _ptr(ws), ws.numel(),
+                                               _ptr(status_out), _stream(x.device))
+        check(rc, "dpz_topk_encode_status")
+        return idx_out, val_out
     if co_replace is None:
         rc = _lib.lib().dpz_topk_encode(_ptr(x), _ptr(x0), _ptr(acc), int(acc_mode),
                                         _ptr(vals_src), n, k, _ptr(idx_out), _ptr(val_out),
@@ -648,11 +662,20 @@ def lz4_frame_info(frame):
 def lz4_decompress(frame, device, out=None, workspace=None, max_size=None):
     """Content of an LZ4 frame (host bytes-like) decoded on ``device``; returns a device uint8
     tensor.  Linked frames (python-lz4's default) and independent frames with blocks of at most
-    64 KB are supported."""
+    64 KB are supported.  The frame comes from a peer, so its header is untrusted: a stored
+    content size is checked against what the blocks can hold (each decodes to at most bmax
+    bytes) and against ``max_size`` BEFORE anything is allocated.  Block / content xxh32
+    checksums, when the frame carries them, are skipped, not verified (the transport —
+    ZeroMQ over TCP — already guarantees integrity; every decoder read and write is
+    bounds-checked, so a corrupt frame cannot fault or overrun)."""
     b = bytes(frame)
     cs, nb, linked, bmax = lz4_frame_info(b)
-    # without a stored content size the blocks bound it (each decodes to at most bmax bytes)
-    size = cs if cs >= 0 else (int(max_size) if max_size is not None else nb * bmax)
+    bound = nb * bmax
+    if cs > bound or (max_size is not None and cs > int(max_size)):
+        raise ValueError(f"malformed LZ4 frame: content size {cs} exceeds what its {nb} "
+                         f"blocks can hold ({bound} bytes) or max_size")
+    # without a stored content size the blocks bound it
+    size = cs if cs >= 0 else (min(bound, int(max_size)) if max_size is not None else bound)
     if out is None or out.numel() < size:
         out = torch.empty(max(size, 1), dtype=torch.uint8, device=device)
     _require(out, torch.uint8, "out")

@@ -22,10 +22,11 @@ extern "C" int dpz_topk_encode_batch(int m, const float* const* x, const float* 
     const int q = j % n_streams;
     // the sampled path's compact writes node j's final status word to status[j] itself (a
     // separate 4-byte device copy per node cost a blit launch of ~8 us on its stream)
-    int rc = dpz::topk_encode_status(x[j], x0 ? x0[j] : nullptr, x[j], n, k, idx_out[j],
+    int rc = dpz::topk_encode_status(x[j], x0 ? x0[j] : nullptr, nullptr, DPZ_ACC_NONE, x[j],
+                                     n, k, idx_out[j],
                                      val_out[j], counter ? counter[j] : nullptr, ws[q], ws_bytes,
                                      static_cast<hipStream_t>(streams[q]),
-                                     status ? status + j : nullptr);
+                                     status ? status + j : nullptr, n_streams > 1);
     if (rc != DPZ_OK) return rc;
   }
   return DPZ_OK;
@@ -89,9 +90,11 @@ extern "C" int dpz_encode_replace_batch(int m, int what, const float* const* x,
       continue;
     }
     if (what & DPZ_BATCH_ENCODE) {
+      // several streams: several codecs share the GPU, the smaller filter grid (DPZ_TOPK_SHARED)
+      const int fl = DPZ_TOPK_ASYNC | (n_streams > 1 ? DPZ_TOPK_SHARED : 0);
       int rc = dpz_topk_encode(x[j], x0 ? x0[j] : nullptr, nullptr, DPZ_ACC_NONE, x[j], n, k,
                                idx_out[j], val_out[j], counter ? counter[j] : nullptr, ws[q],
-                               ws_bytes, DPZ_TOPK_ASYNC, streams[q]);
+                               ws_bytes, fl, streams[q]);
       if (rc != DPZ_OK) return rc;
     }
     if (what & DPZ_BATCH_DECODE) {

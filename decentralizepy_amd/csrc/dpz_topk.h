@@ -192,10 +192,14 @@ struct FastGeom {
 
 // k > 0: the candidate capacity per segment grows with alpha = k / n (the key window holds
 // about alpha + a few percent of the elements; a segment over capacity turns DENSE, still exact)
-static inline FastGeom fast_geom(int64_t n, int64_t k = 0) {
+// shared: several node codecs share the GPU (a batch enqueue on several streams): up to
+// W_SMALL_N elements the filter grid is capped at W_SMALL segments so the other streams' kernels
+// find free CU slots; a lone codec (one stream) takes the full W_MAX grid, the faster one alone
+// (C2 filter 18.8 vs 20.6 us).
+static inline FastGeom fast_geom(int64_t n, int64_t k = 0, bool shared = false) {
   FastGeom g;
   int64_t W = (n + W_MIN_RANGE - 1) / W_MIN_RANGE;
-  const int64_t wmax = n <= W_SMALL_N ? W_SMALL : W_MAX;
+  const int64_t wmax = (shared && n <= W_SMALL_N) ? W_SMALL : W_MAX;
   if (W > wmax) W = wmax;
   if (W < 1) W = 1;
   int64_t R = (n + W - 1) / W;
@@ -223,12 +227,12 @@ struct WsLayout {
   FastGeom fg;
 };
 
-static inline WsLayout ws_layout(int64_t n, int64_t k = 0) {
+static inline WsLayout ws_layout(int64_t n, int64_t k = 0, bool shared = false) {
   WsLayout L;
   size_t o = 0;
   L.ex_nblk = (n + EX_CHUNK - 1) / EX_CHUNK;
   if (L.ex_nblk < 1) L.ex_nblk = 1;
-  L.fg = fast_geom(n > 0 ? n : 1, k);
+  L.fg = fast_geom(n > 0 ? n : 1, k, shared);
   L.ctrl = o; o += align256(sizeof(TopkCtrl));
   L.chist = o; o += align256(CB * 4);  // must be zero before the first sampled call (self-cleaning)
   L.ex_hist = o; o += align256(4096 * 4);
@@ -250,6 +254,12 @@ static inline WsLayout ws_layout(int64_t n, int64_t k = 0) {
   return L;
 }
 
+// Workspace bytes a caller must provide: enough for either grid (the flags choose per call).
+static inline size_t ws_bytes_needed(int64_t n, int64_t k) {
+  const size_t a = ws_layout(n, k, false).total, b = ws_layout(n, k, true).total;
+  return a > b ? a : b;
+}
+
 struct EncodeArgs {
   const float* x; const float* x0; float* acc; int acc_mode; const float* vals_src;
   int64_t n, k; int32_t* idx_out; float* val_out; int32_t* counter; char* ws;
@@ -257,6 +267,7 @@ struct EncodeArgs {
   const ReplaceJob* job;  // co-scheduled replace decode (sampled path only), or nullptr
   int32_t* status_out;    // sampled path, ASYNC: compact's block 0 also writes the call's final
                           // status word here (device), or nullptr
+  bool shared;            // DPZ_TOPK_SHARED: the filter grid for several codecs per GPU
 };
 
 // dpz_topk_exact.hip / dpz_topk_sampled.hip
@@ -268,9 +279,10 @@ int run_exact(const EncodeArgs& a, const WsLayout& L, int rekey, bool vec, int k
 int run_sampled(const EncodeArgs& a, const WsLayout& L, bool vec, int phases = 3);
 // dpz_topk_encode with the final sampled-path status word also written to status_out (device)
 // on the stream, as the call's last write: no separate copy (dpz_topk_encode_batch)
-int topk_encode_status(const float* x, const float* x0, const float* vals_src, int64_t n,
-                       int64_t k, int32_t* idx_out, float* val_out, int32_t* counter, void* ws,
-                       size_t ws_bytes, hipStream_t st, int32_t* status_out);
+int topk_encode_status(const float* x, const float* x0, float* acc, int acc_mode,
+                       const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
+                       float* val_out, int32_t* counter, void* ws, size_t ws_bytes,
+                       hipStream_t st, int32_t* status_out, bool shared = false);
 static inline bool use_sampled(int64_t n, int64_t k) {
   return n >= (1 << 18) && k >= 1 && k <= n / 2;
 }

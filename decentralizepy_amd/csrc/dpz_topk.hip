@@ -64,7 +64,7 @@ static int validate(const EncodeArgs& a, size_t ws_bytes) {
   if (a.n > 0 && !a.x) return DPZ_ERR_ARG;
   if (a.acc_mode != DPZ_ACC_NONE && !a.acc) return DPZ_ERR_ARG;
   if (a.k > 0 && (!a.idx_out || !a.val_out || !a.vals_src)) return DPZ_ERR_ARG;
-  if (a.n > 0 && (!a.ws || ws_bytes < ws_layout(a.n, a.k).total)) return DPZ_ERR_WORKSPACE;
+  if (a.n > 0 && (!a.ws || ws_bytes < ws_bytes_needed(a.n, a.k))) return DPZ_ERR_WORKSPACE;
   return DPZ_OK;
 }
 
@@ -74,11 +74,12 @@ using namespace dpz;
 
 extern "C" size_t dpz_topk_workspace_bytes(int64_t n, int64_t k) {
   (void)k;
-  return ws_layout(n > 0 ? n : 1, k).total;
+  return ws_bytes_needed(n > 0 ? n : 1, k);
 }
 
-static int dpz_topk_dispatch(const EncodeArgs& a, int flags) {
-  const WsLayout L = ws_layout(a.n, a.k);
+static int dpz_topk_dispatch(EncodeArgs a, int flags) {
+  if (flags & DPZ_TOPK_SHARED) a.shared = true;
+  const WsLayout L = ws_layout(a.n, a.k, a.shared);
   const bool vec = all_aligned(a);
   if (a.k == 0) {
     if (a.acc_mode == DPZ_ACC_ACCUMULATE && a.n > 0)
@@ -115,11 +116,13 @@ extern "C" int dpz_topk_encode(const float* x, const float* x0, float* acc, int 
 }
 
 namespace dpz {
-int topk_encode_status(const float* x, const float* x0, const float* vals_src, int64_t n,
-                       int64_t k, int32_t* idx_out, float* val_out, int32_t* counter, void* ws,
-                       size_t ws_bytes, hipStream_t st, int32_t* status_out) {
-  EncodeArgs a{x, x0, nullptr, DPZ_ACC_NONE, vals_src, n, k, idx_out, val_out, counter,
+int topk_encode_status(const float* x, const float* x0, float* acc, int acc_mode,
+                       const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
+                       float* val_out, int32_t* counter, void* ws, size_t ws_bytes,
+                       hipStream_t st, int32_t* status_out, bool shared) {
+  EncodeArgs a{x, x0, acc, acc_mode, vals_src, n, k, idx_out, val_out, counter,
                static_cast<char*>(ws), st};
+  a.shared = shared;
   int rc = validate(a, ws_bytes);
   if (rc != DPZ_OK) return rc;
   if (n == 0 || k == 0 || !use_sampled(n, k)) {  // no sampled tail writes it: status 0
@@ -132,6 +135,16 @@ int topk_encode_status(const float* x, const float* x0, const float* vals_src, i
   return dpz_topk_dispatch(a, DPZ_TOPK_ASYNC);
 }
 }  // namespace dpz
+
+extern "C" int dpz_topk_encode_status(const float* x, const float* x0, float* acc, int acc_mode,
+                                      const float* vals_src, int64_t n, int64_t k,
+                                      int32_t* idx_out, float* val_out, int32_t* counter,
+                                      void* ws, size_t ws_bytes, int32_t* status_out,
+                                      dpz_stream_t stream) {
+  if (!status_out) return DPZ_ERR_ARG;
+  return topk_encode_status(x, x0, acc, acc_mode, vals_src, n, k, idx_out, val_out, counter, ws,
+                            ws_bytes, static_cast<hipStream_t>(stream), status_out);
+}
 
 static bool overlaps(const void* p, size_t pb, const void* q, size_t qb) {
   if (!p || !q || pb == 0 || qb == 0) return false;

@@ -48,9 +48,14 @@ def read_edges(path):
 
 
 def mh_weights(adj, i):
-    """Metro-Hastings weights of node i's neighbours, in ascending neighbour order, and the self
-    weight, rounded exactly like the reference (Python doubles, ``Sharing.py:165-185``)."""
-    nbrs = sorted(adj[i])
+    """Metro-Hastings weights of node i's neighbours and the self weight, rounded exactly like
+    the reference (Python doubles, ``Sharing.py:165-185``), in the reference's FOLD ORDER: the
+    node folds ``peer_deques`` in the iteration order of its neighbour set
+    (``node/DPSGDNode.py:111-115`` builds the averaging dict from ``graph.neighbors(uid)``, a
+    ``set`` filled by ``graphs/Graph.py:57-103``).  ``read_edges`` fills the same sets in the same
+    insertion order, so ``list(adj[i])`` is that order; it is NOT ascending for most nodes of
+    96_regular.edges, and the fp32 fold is order-sensitive."""
+    nbrs = list(adj[i])
     w = [1 / (max(len(nbrs), len(adj[j])) + 1) for j in nbrs]
     total = 0
     for v in w:
@@ -99,6 +104,15 @@ class GossipRound:
                 hbm_budget = torch.cuda.mem_get_info(self.device)[0] // 2
             else:
                 hbm_budget = float("inf")
+        if world > 1:
+            # the exchange mode and the reduce-scatter group size decide which collectives every
+            # rank issues: all ranks must derive them from ONE budget (the smallest), or ranks
+            # with slightly different free memory issue mismatched collectives and hang
+            import torch.distributed as dist
+            dev = self.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+            b = torch.tensor([float(hbm_budget)], dtype=torch.float64, device=dev)
+            dist.all_reduce(b, op=dist.ReduceOp.MIN, group=group)
+            hbm_budget = float(b.item())
         self.hbm_budget = hbm_budget
         if exchange == "auto":
             exchange = "reduce_scatter" if world > 1 and gathered > hbm_budget else "allgather"
@@ -122,6 +136,7 @@ class GossipRound:
             g = int(hbm_budget // (2 * row * (world + 1))) if hbm_budget != float("inf") else self.per
             self.rs_group = max(1, min(self.per, g))
         self.out = torch.empty_like(self.x)
+        self.leg_times = None
         self.weights = [mh_weights(adj, i) for i in range(self.lo, self.hi)]
         self._encode = encode or self._hip_encode
         self._fold = fold or self._hip_fold
@@ -204,49 +219,129 @@ class GossipRound:
         from ._lib import DPZ_EW_MHCOMBINE
         codec.elementwise(DPZ_EW_MHCOMBINE, x, b, a, c, out=out)
 
-    def fold_reduce_scatter(self):
-        """Over-HBM exchange + fold: see the module docstring.  Destination node d of rank r in
-        group [g0, g0 + G) is row r * G + (d - r*per - g0) of this rank's (A, B) send buffers."""
-        import torch.distributed as dist
-        W, per, G, N = self.world, self.per, self.rs_group, self.N
+    def _rs_tables(self):
+        """Per destination group [g0, g0 + gsz): the (A, B) contribution rows this rank owns.
+        Row layout of the packed send buffer (W, gsz, 2, N): destination node d = r*per + g0 + j
+        of rank r is block r, row j; plane 0 = A_d, plane 1 = B_d.  Each job is (r, j, own
+        payloads as (local node, weight)); rows without a job stay zero.  Built once: the
+        topology and the node sharding do not change between rounds."""
+        per, G = self.per, self.rs_group
         mine = set(range(self.lo, self.hi))
+        groups = []
         for g0 in range(0, per, G):
             gsz = min(G, per - g0)
-            send_a = torch.zeros(W * gsz, N, dtype=torch.float32, device=self.device)
-            send_b = torch.zeros_like(send_a)
-            for r in range(W):
+            jobs, empty = [], []
+            for r in range(self.world):
                 for j in range(gsz):
                     d = r * per + g0 + j
-                    if d >= self.n_nodes:
-                        continue
-                    nbrs, w, _ = mh_weights(self.adj, d)
-                    own = [(q, wq) for q, wq in zip(nbrs, w) if q in mine]
-                    if not own:
-                        continue
-                    row = r * gsz + j
-                    pays = [(self.send_idx[q - self.lo], self.send_val[q - self.lo]) for q, _ in own]
-                    ones = [(self.send_idx[q - self.lo], self._ones) for q, _ in own]
-                    ws_ = [wq for _, wq in own]
-                    self._partial(pays, ws_, send_a[row])
-                    self._partial(ones, ws_, send_b[row])
-            recv_a = torch.empty(gsz, N, dtype=torch.float32, device=self.device)
-            recv_b = torch.empty_like(recv_a)
-            if W > 1:
-                dist.reduce_scatter_tensor(recv_a, send_a, group=self.group)
-                dist.reduce_scatter_tensor(recv_b, send_b, group=self.group)
+                    own = []
+                    if d < self.n_nodes:
+                        nbrs, w, _ = mh_weights(self.adj, d)
+                        own = [(q - self.lo, wq) for q, wq in zip(nbrs, w) if q in mine]
+                    (jobs.append((r, j, own)) if own else empty.append((r, j)))
+            groups.append((g0, gsz, jobs, empty))
+        return groups
+
+    def _rs_batch_args(self, send, jobs):
+        """Host tables of ONE dpz_decode_average_batch call that writes every A and B row of a
+        group (zero base: A_d = sum_s w_s * v_s, B_d = sum_s w_s * 1 on the payload entries)."""
+        outs, counts, idx, val, kk, w = [], [], [], [], [], []
+        for plane in (0, 1):
+            for r, j, own in jobs:
+                outs.append(send[r, j, plane].data_ptr())
+                counts.append(len(own))
+                for q, wq in own:
+                    idx.append(self.send_idx[q].data_ptr())
+                    val.append(self.send_val[q].data_ptr() if plane == 0 else self._ones.data_ptr())
+                    kk.append(self.k)
+                    w.append(wq)
+        m, tot = len(outs), max(1, len(idx))
+        loc = (ctypes.c_void_p * max(1, m))(*([self._zero_local.data_ptr()] * m))
+        return dict(m=m, local=loc, out=(ctypes.c_void_p * max(1, m))(*outs),
+                    np=(ctypes.c_int * max(1, m))(*counts), idx=(ctypes.c_void_p * tot)(*idx),
+                    val=(ctypes.c_void_p * tot)(*val), k=(ctypes.c_int64 * tot)(*kk),
+                    w=(ctypes.c_float * tot)(*w))
+
+    def fold_reduce_scatter(self):
+        """Over-HBM exchange + fold: see the module docstring.  Per destination group: ONE batched
+        zero-base fold writes this rank's (A, B) rows into one packed send buffer, ONE
+        reduce-scatter sums them on the owning ranks, and each owner combines its nodes."""
+        import torch.distributed as dist
+        W, N = self.world, self.N
+        if getattr(self, "_rs", None) is None:
+            G = self.rs_group
+            self._rs = self._rs_tables()
+            # persistent packed buffers sized for the largest group (within the budget)
+            self._rs_send = torch.zeros(W, G, 2, N, dtype=torch.float32, device=self.device)
+            self._rs_recv = (torch.empty(G, 2, N, dtype=torch.float32, device=self.device)
+                             if W > 1 else None)
+            self._rs_args = {}
+        t_mark = self._leg_mark(None)  # per-leg timing (bench only, self.leg_times)
+        for g0, gsz, jobs, empty in self._rs:
+            send = self._rs_send[:, :gsz]
+            if self._hip and jobs:
+                from . import _lib
+                from ._lib import DPZ_FOLD_ZERO_BASE
+                key = (g0, send.data_ptr())
+                a = self._rs_args.get(key)
+                if a is None:
+                    a = self._rs_args[key] = self._rs_batch_args(send, jobs)
+                streams = (ctypes.c_void_p * len(self.streams))(
+                    *[s.cuda_stream for s in self.streams])
+                maxp = max(len(own) for _, _, own in jobs)
+                dws = [w_.get_decode(N, maxp) for w_ in self.wss]
+                cur = torch.cuda.current_stream(self.device)
+                for st in self.streams:
+                    st.wait_stream(cur)
+                rc = _lib.lib().dpz_decode_average_batch(
+                    a["m"], a["local"], a["out"], N, a["np"], a["idx"], a["val"], a["k"], a["w"],
+                    None, DPZ_FOLD_ZERO_BASE, self._ptrs(dws), min(d.numel() for d in dws),
+                    len(self.streams), streams)
+                _lib.check(rc, "dpz_decode_average_batch")
+                for st in self.streams:
+                    cur.wait_stream(st)
             else:
-                recv_a.copy_(send_a)
-                recv_b.copy_(send_b)
-            del send_a, send_b
+                for r, j, own in jobs:
+                    pays = [(self.send_idx[q], self.send_val[q]) for q, _ in own]
+                    ones = [(self.send_idx[q], self._ones) for q, _ in own]
+                    ws_ = [wq for _, wq in own]
+                    self._partial(pays, ws_, send[r, j, 0])
+                    self._partial(ones, ws_, send[r, j, 1])
+            for r, j in empty:  # rows of destinations with no neighbour on this rank
+                send[r, j].zero_()
+            t_mark = self._leg_mark(t_mark, "rs_partial")
+            if W > 1:
+                # the slice [:, :gsz] of a (W, G, 2, N) buffer is contiguous only when gsz == G
+                src = send if send.is_contiguous() else send.contiguous()
+                recv = self._rs_recv[:gsz]
+                dist.reduce_scatter_tensor(recv.view(-1), src.view(-1), group=self.group)
+            else:
+                recv = send[0]
+            t_mark = self._leg_mark(t_mark, "rs_collective")
             for j in range(gsz):
                 d = self.lo + g0 + j
                 if d >= self.hi:
                     continue
                 nbrs, w, w_self = self.weights[d - self.lo]
                 c = w_self + sum(w)
-                self._combine(self.x[d - self.lo], recv_b[j], recv_a[j], c, self.out[d - self.lo])
+                self._combine(self.x[d - self.lo], recv[j, 1], recv[j, 0], c,
+                              self.out[d - self.lo])
+            t_mark = self._leg_mark(t_mark, "rs_combine")
         self.x0, self.out = self.out, self.x0
         self.x.copy_(self.x0)
+
+    def _leg_mark(self, t_prev, name=None):
+        """With ``self.leg_times`` a dict: synchronize, add the time since t_prev to leg `name`
+        and return the new mark (bench only; a no-op otherwise)."""
+        if self.leg_times is None:
+            return None
+        import time
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        now = time.perf_counter()
+        if name is not None and t_prev is not None:
+            self.leg_times[name] = self.leg_times.get(name, 0.0) + (now - t_prev)
+        return now
 
     def exchange(self):
         if self.exchange_mode == "reduce_scatter":
@@ -320,9 +415,13 @@ class GossipRound:
         return r * self.per + (node - r * self.per)
 
     def step(self):
+        t = self._leg_mark(None)
         self.encode_all()
+        t = self._leg_mark(t, "encode")
         if self.exchange_mode == "reduce_scatter":
             self.fold_reduce_scatter()
             return
         self.exchange()
+        t = self._leg_mark(t, "exchange")
         self.fold_all()
+        self._leg_mark(t, "fold")

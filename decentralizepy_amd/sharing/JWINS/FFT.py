@@ -96,7 +96,19 @@ class FFT(PartialModel):
     # ---- wire format ------------------------------------------------------------------------------
     def compress_data(self, data, idx_dev=None, val_dev=None):
         """Indices may take the device index codec; complex values go through the compressor's
-        host ``compress_float`` as in the reference (FFT.py:211 -> PartialModel.py:147-154)."""
+        host ``compress_float`` as in the reference (FFT.py:211 -> PartialModel.py:147-154).
+        Only a pass-through value leg (Compression / Elias: ``compress_float`` is the identity)
+        can carry complex64: the float codecs (fpzip-class, LZ4, fp16) are fp32 codecs, and the
+        reference's fail on or silently reinterpret complex input (fpzip.compress rejects it,
+        EliasFpzip.py:34; Lz4Wrapper decodes the bytes as float32, Lz4Wrapper.py:94-98), so this
+        raises instead of corrupting the average."""
+        from ...compression.Compression import Compression
+        if (self.compress and "params" in data and np.iscomplexobj(data["params"])
+                and type(self.compressor).compress_float is not Compression.compress_float):
+            raise NotImplementedError(
+                f"FFT: complex64 payload values cannot go through "
+                f"{type(self.compressor).__name__}.compress_float (an fp32 codec); use "
+                "compression_class Elias (indices only) or compress = False")
         return super().compress_data(data, idx_dev=idx_dev, val_dev=None)
 
     def _full_share(self):

@@ -146,6 +146,24 @@ class PartialModel(Sharing):
             self._pre_version = state_version(sd)
             self.pre_share_model_transformed, self._change_dev = \
                 self._transform_pre_step(self.pre_share_model)
+            self.model.model_change = self._model_change()
+
+    def _model_change(self):
+        """``model.model_change`` as the reference sets it (PartialModel.py:317-331): T(x - init),
+        and with accumulation the accumulated change before the rewind (acc + change, the value
+        the encode forms in registers; fp32 addition commutes, so it is the same bits as the
+        reference's ``acc += change`` / ``change += acc``).  A device tensor; the selection
+        itself never reads it (the encode fuses the change), so it costs one elementwise pass."""
+        acc = self.model.accumulated_changes if self.accumulation else None
+        change = self._change_dev
+        if change is None:
+            change = codec.elementwise(codec.DPZ_EW_SUB, self.pre_share_model, self.init_model)
+        if acc is None:
+            return change
+        out = torch.empty_like(change)
+        codec.elementwise(codec.DPZ_EW_ADD, acc.view(torch.float32), change.view(torch.float32),
+                          out=out.view(torch.float32))
+        return out
 
     def _encode(self, k):
         """Top-k encode; returns device (idx int32[k], val fp32[k])."""

@@ -52,6 +52,11 @@ typedef void* dpz_stream_t; /* hipStream_t */
  * enqueues everything and TAIL nothing.                                                       */
 #define DPZ_TOPK_STREAM 0x4
 #define DPZ_TOPK_TAIL 0x8
+/* Several codecs share the GPU (concurrent streams): up to ~2^24 elements the sampled path's
+ * filter uses a smaller grid that leaves CU slots to the other streams' kernels; a lone codec
+ * (the default) takes the larger, faster-alone grid.  Results are identical either way; STREAM
+ * and TAIL calls of one encode must pass the same choice.                                     */
+#define DPZ_TOPK_SHARED 0x10
 
 /* ---- fold flags ---- */
 #define DPZ_FOLD_SELF 0x1         /* add the local term w_self*local after the payloads        */
@@ -153,6 +158,17 @@ int dpz_topk_complete(const float* x, const float* x0, float* acc, int acc_mode,
                       const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
                       float* val_out, int32_t* counter, void* ws, size_t ws_bytes,
                       int* used_fallback, dpz_stream_t stream);
+
+/* dpz_topk_encode with DPZ_TOPK_ASYNC (same arguments, any acc_mode) that also writes the call's
+ * final status word to status_out (DEVICE int32, on `stream`, as the encode's last write): 0 =
+ * the result is final; otherwise the sampled path missed, nothing was written or updated, and the
+ * caller re-runs the encode with DPZ_TOPK_EXACT.  Lets a caller enqueue many encodes that share
+ * one workspace (a gossip round's nodes, decentralizepy_amd/gossip_jwins.py) and read every
+ * status once; replaces the same reference lines as dpz_topk_encode.                          */
+int dpz_topk_encode_status(const float* x, const float* x0, float* acc, int acc_mode,
+                           const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
+                           float* val_out, int32_t* counter, void* ws, size_t ws_bytes,
+                           int32_t* status_out, dpz_stream_t stream);
 
 /* Batched decode + Metro-Hastings fold over n_payloads neighbour payloads.
  * Replaces reference sharing/PartialModel.py:257-303 (T = cat(local); T[idx] = params),

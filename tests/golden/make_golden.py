@@ -157,14 +157,14 @@ class TieError(RuntimeError):
 
 
 def run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed, wavelet=False, nbr_kinds=None,
-                 averaging="_averaging"):
+                 averaging="_averaging", record_change=False):
     """Replay; on a tie at the k-th key (fp32 differences are quantised) retry with the next seed.
     ``averaging`` names the reference method the node calls on receive (``_averaging``, or the
     federated server's ``_averaging_server``)."""
     for attempt in range(40):
         try:
             meta = _run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed + 1000 * attempt,
-                                 wavelet, nbr_kinds, averaging)
+                                 wavelet, nbr_kinds, averaging, record_change=record_change)
             meta["seed"] = seed + 1000 * attempt
             return meta
         except TieError as e:
@@ -173,7 +173,7 @@ def run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed, wavelet=False,
 
 
 def _run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed, wavelet, nbr_kinds,
-                  averaging="_averaging", on_send=None):
+                  averaging="_averaging", on_send=None, record_change=False):
     rng = np.random.default_rng(seed)
     n = rows * cols + nb
     model = Net(rows, cols, nb)
@@ -199,6 +199,8 @@ def _run_scenario(name, cls, kwargs, rows, cols, nb, rounds, seed, wavelet, nbr_
         if on_send is not None:  # wire_main: records the payload and ends the replay
             on_send(r, data)
         change = plugin.model.model_change
+        if record_change:  # PartialModel.py:331 (the reference's model.model_change after send)
+            arrays[f"r{r}_model_change"] = change.numpy().copy()
         rmeta = {"alpha": float(plugin.alpha), "partial": "send_partial" in data}
         if wavelet:
             length = int(plugin.wt_shape[0])
@@ -527,8 +529,40 @@ def haar_main():
     print("wrote", len(scen), "haar scenarios,", len(cases), "pywt cases")
 
 
+def model_change_main():
+    """``model.model_change`` as the reference leaves it after get_data_to_send
+    (PartialModel.py:317-331: T(x - init), with accumulation the accumulated change before the
+    rewind) for PartialModel plain / accumulation / accumulate_averaging_changes and Wavelet
+    with accumulate_averaging_changes -> tests/golden/mc_*.npz + model_change_scenarios.json
+    (the other fixtures are untouched)."""
+    torch.set_num_threads(4)
+    pm = {"dict_ordered": True}
+    wv = {"wavelet": "sym2", "level": 4, "alpha": 0.1, "metadata_cap": 0.5}
+    scen = [
+        run_scenario("mc_pm_plain", PartialModel, {**pm, "alpha": 0.1}, 40, 100, 99, 2, seed=61,
+                     record_change=True),
+        run_scenario("mc_pm_acc", PartialModel, {**pm, "alpha": 0.1, "accumulation": True},
+                     40, 100, 99, 2, seed=62, record_change=True),
+        run_scenario("mc_pm_accavg", PartialModel,
+                     {**pm, "alpha": 0.2, "accumulation": True,
+                      "accumulate_averaging_changes": True}, 40, 100, 99, 2, seed=63,
+                     record_change=True),
+        run_scenario("mc_wv_accavg", Wavelet,
+                     {**wv, "accumulation": True, "accumulate_averaging_changes": True},
+                     40, 100, 99, 2, seed=64, wavelet=True, record_change=True),
+    ]
+    with open(os.path.join(OUT, "model_change_scenarios.json"), "w") as f:
+        json.dump({"scenarios": scen, "generator": "tests/golden/make_golden.py --model-change",
+                   "reference": "sacs-epfl/decentralizepy v1 (/root/reference/src)",
+                   "pywavelets": "1.1.1 (python3.9 bridge)", "torch": torch.__version__}, f,
+                  indent=1)
+    print("wrote", len(scen), "model_change scenarios")
+
+
 if __name__ == "__main__":
-    if "--haar" in sys.argv:
+    if "--model-change" in sys.argv:
+        model_change_main()
+    elif "--haar" in sys.argv:
         haar_main()
     elif "--fullsize" in sys.argv:
         fullsize_main()

@@ -24,7 +24,7 @@ def load_meta():
     """scenarios.json plus the federated-server scenarios (server_scenarios.json), merged."""
     with open(os.path.join(GOLDEN, "scenarios.json")) as f:
         meta = json.load(f)
-    for extra in ("server_scenarios.json", "haar_scenarios.json"):
+    for extra in ("server_scenarios.json", "haar_scenarios.json", "model_change_scenarios.json"):
         with open(os.path.join(GOLDEN, extra)) as f:
             meta["scenarios"] = meta["scenarios"] + json.load(f)["scenarios"]
     return meta
@@ -96,6 +96,14 @@ class OracleNode:
         mode = otopk.ACC_NONE
         if self.accumulation:
             mode = otopk.ACC_ADD if self.aac else otopk.ACC_ACCUMULATE
+        # model.model_change (PartialModel.py:317-331): the change, with accumulation the
+        # accumulated change before the rewind
+        if mode == otopk.ACC_ACCUMULATE:
+            self.model_change = self.acc + ((change - x0) if x0 is not None else change)
+        elif mode == otopk.ACC_ADD:
+            self.model_change = ((change - x0) if x0 is not None else change) + self.acc
+        else:
+            self.model_change = (change - x0) if x0 is not None else change.copy()
         if self.alpha >= self.cap:
             if self.accumulation:
                 if mode == otopk.ACC_ACCUMULATE:  # pre-step accumulation happens before the zeroing
@@ -160,6 +168,9 @@ def check_round(got, arrays, r, meta_round, bits=True):
     if f"r{r}_acc_after_avg" in arrays:
         np.testing.assert_array_equal(np.asarray(got["acc_avg"]).view(np.uint32),
                                       arrays[f"r{r}_acc_after_avg"].view(np.uint32))
+    if f"r{r}_model_change" in arrays:
+        np.testing.assert_array_equal(np.asarray(got["model_change"]).view(np.uint32),
+                                      arrays[f"r{r}_model_change"].view(np.uint32))
 
 
 def replay_oracle(name):
@@ -169,7 +180,8 @@ def replay_oracle(name):
         node.model = arrays[f"r{r}_x"].copy()
         pay = node.get_data_to_send()
         got = {"payload": pay, "counter_enc": node.counter.copy(),
-               "acc_enc": None if node.acc is None else node.acc.copy()}
+               "acc_enc": None if node.acc is None else node.acc.copy(),
+               "model_change": node.model_change}
         node.averaging(neighbour_msgs(mr, arrays, r),
                        server=meta.get("averaging") == "_averaging_server")
         got["model"] = node.model
@@ -296,8 +308,10 @@ def replay_plugin(name, tmpdir, compression_class=None, config=None):
                                               ofpz.encode(arrays[f"r{r}_params"], 0))
             data = plugin.decompress_data(data)
         acc = getattr(model, "accumulated_changes", None)
+        mc = getattr(model, "model_change", None)
         got = {"payload": data, "counter_enc": model.shared_parameters_counter.numpy().copy(),
-               "acc_enc": None if acc is None else acc.cpu().numpy().copy()}
+               "acc_enc": None if acc is None else acc.cpu().numpy().copy(),
+               "model_change": None if mc is None else mc.cpu().numpy().copy()}
         assert data["degree"] == mr["degree"]
         msgs = neighbour_msgs(mr, arrays, r)
         if compression_class:
@@ -425,8 +439,10 @@ def replay_fft_plugin(name, tmpdir):
                               if mr["partial"] else ["params", "degree", "iteration"])
         assert data["params"].dtype == np.complex64
         acc = getattr(model, "accumulated_changes", None)
+        mc = getattr(model, "model_change", None)
         got = {"payload": data, "counter_enc": model.shared_parameters_counter.numpy().copy(),
-               "acc_enc": None if acc is None else acc.cpu().numpy().copy()}
+               "acc_enc": None if acc is None else acc.cpu().numpy().copy(),
+               "model_change": None if mc is None else mc.cpu().numpy().copy()}
         peer = {uid: deque([m]) for uid, m in zip([1, 2, 3], neighbour_msgs(mr, arrays, r))}
         plugin._averaging(peer)
         got["model"] = get_flat(model)

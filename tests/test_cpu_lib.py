@@ -101,3 +101,15 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         _lib.lib()
+
+
+def test_staging_pinned_cap_refuses_before_pinning():
+    """Pinned staging is bounded: a buffer that would take the total past the cap
+    is refused (None -> the caller copies through pageable memory), nothing pinned."""
+    import torch
+
+    from decentralizepy_amd._device import PayloadNames, Staging
+    st = Staging(cap_bytes=1024)
+    assert st.get("local", 1000, torch.float32) is None and st.total == 0
+    names = PayloadNames()
+    assert len({names("idx") for _ in range(3 * names.slots)}) == names.slots <= 8

@@ -643,3 +643,23 @@ def test_topk_c3_wavelet_rounds_stay_on_sampled_path(dev):
     np.testing.assert_array_equal(idx.cpu().numpy(), oi)
     np.testing.assert_array_equal(_bits(val.cpu().numpy()), _bits(ov))
     np.testing.assert_array_equal(_bits(acc.cpu().numpy()), _bits(o_acc))
+
+
+@pytest.mark.parametrize("n,alpha", [(11_000_000, 0.01), (16_777_216, 0.01), (3_000_017, 0.1)])
+def test_shared_and_lone_filter_grids_agree(dev, n, alpha):
+    """DPZ_TOPK_SHARED (the smaller filter grid for several codecs per GPU) and the lone-codec
+    grid select the same payload and make the same counter update, bit for bit."""
+    from decentralizepy_amd import codec
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(n, device=dev, generator=g)
+    x0 = x - 0.01 * torch.randn(n, device=dev, generator=g)
+    k = round(alpha * n)
+    res = []
+    for shared in (False, True):
+        cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+        ws = codec.Workspace(dev)
+        idx, val = codec.topk_encode(x, k, x0=x0, counter=cnt, workspace=ws, shared=shared)
+        assert codec.topk_status(ws) == 0  # the sampled path, no fallback
+        res.append((idx.cpu(), val.cpu(), cnt.cpu()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

@@ -35,6 +35,28 @@ def test_fft_full_payload_raises_keyerror_like_reference(dev, tmp_path):
         plugin.deserialized_model({"params": np.zeros(meta["m"], np.complex64)})
 
 
+@pytest.mark.parametrize("cls,ok", [("Elias", True), ("EliasFpzip", False),
+                                    ("Lz4Wrapper", False), ("EliasFp16", False)])
+def test_fft_complex_values_only_through_pass_through_float_leg(dev, tmp_path, cls, ok):
+    """Complex64 values may not go through an fp32 float codec (it would drop the imaginary
+    part): Elias (indices only) works, the float codecs raise."""
+    from decentralizepy_amd.sharing.JWINS.FFT import FFT
+    meta, arrays = scenario.load_fft("fft_plain")
+    model = scenario.make_model(meta["shape"])
+    scenario.set_flat(model, arrays["x0"])
+    kw = dict(meta["kwargs"], compress=True, compression_class=cls,
+              compression_package=f"decentralizepy_amd.compression.{cls}")
+    plugin = FFT(0, 0, None, scenario._Mapping(), scenario._Graph([1]), model, None,
+                 str(tmp_path), **kw)
+    scenario.set_flat(model, arrays["r0_x"])
+    if ok:
+        data = plugin.get_data_to_send(degree=1)
+        assert np.iscomplexobj(data["params"])
+    else:
+        with pytest.raises(NotImplementedError):
+            plugin.get_data_to_send(degree=1)
+
+
 @pytest.mark.parametrize("n", [4098, 1 << 20, 11_000_000])
 def test_rfft_irfft_against_numpy(dev, n):
     """dpz_rfft / dpz_irfft against a float64 numpy FFT (error bound as scenario.fft_tol) and the

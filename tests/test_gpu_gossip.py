@@ -28,8 +28,10 @@ def test_gossip_round_device_matches_oracle(dev, path, n, alpha):
         np.testing.assert_array_equal(eng.counter.cpu().numpy(), ref.counter.numpy())
 
 
-@pytest.mark.parametrize("path,n,alpha", [(EDGES16, 200_003, 0.01), (EDGES96, 30_000, 0.05)])
-def test_reduce_scatter_exchange_device_within_tolerance(dev, path, n, alpha):
+@pytest.mark.parametrize("path,n,alpha,budget", [(EDGES16, 200_003, 0.01, 1),
+                                                  (EDGES96, 30_000, 0.05, 1),
+                                                  (EDGES96, 30_000, 0.05, None)])
+def test_reduce_scatter_exchange_device_within_tolerance(dev, path, n, alpha, budget):
     """The over-HBM exchange's device legs — the zero-based batched fold of the owned payloads
     into dense (A, B) rows and the DPZ_EW_MHCOMBINE owner combine — on one rank (forced mode,
     budget of one destination node per group), against the bit-exact all-gather round within
@@ -38,8 +40,9 @@ def test_reduce_scatter_exchange_device_within_tolerance(dev, path, n, alpha):
     adj = read_edges(path)
     x = _models(len(adj), n)
     exact = GossipRound(adj, x.to(dev), alpha)
-    rs = GossipRound(adj, x.to(dev), alpha, exchange="reduce_scatter", hbm_budget=1)
-    assert rs.exchange_mode == "reduce_scatter" and rs.rs_group == 1
+    rs = GossipRound(adj, x.to(dev), alpha, exchange="reduce_scatter", hbm_budget=budget)
+    # budget 1: one destination node per group; None: the whole rank in one batched group
+    assert rs.exchange_mode == "reduce_scatter" and rs.rs_group == (1 if budget else len(adj))
     for r in range(2):
         g = torch.Generator().manual_seed(100 + r)
         noise = (0.01 * torch.randn(len(adj), n, generator=g)).to(dev)
@@ -51,3 +54,37 @@ def test_reduce_scatter_exchange_device_within_tolerance(dev, path, n, alpha):
         np.testing.assert_allclose(rs.x.cpu().numpy(), exact.x.cpu().numpy(), rtol=1e-5,
                                    atol=1e-6)
         np.testing.assert_array_equal(rs.counter.cpu().numpy(), exact.counter.cpu().numpy())
+
+
+@pytest.mark.parametrize("wavelet", ["sym2", "haar"])
+def test_jwins_round_device_matches_oracle(dev, wavelet):
+    """C3 shape (b): the JWINS round of tutorial/JWINS/regular_16.txt with the tutorial alpha
+    list (uid-seeded draws, full shares included) — DWT pair, ADD-accumulation top-k, batched
+    coefficient-domain fold, IDWT, accumulating post-step — bit-exact against the same engine
+    driven by the oracle, over 2 rounds.  M >= 2^18 keeps the encodes on the sampled path."""
+    from decentralizepy_amd.gossip import read_edges
+    from decentralizepy_amd.gossip_jwins import JwinsRound
+    from tests.jwins_ops import OracleJwinsOps, coeff_len
+    from tests.test_cpu_gossip_jwins import EDGES16, TUTORIAL_ALPHAS, _noise
+    adj = read_edges(EDGES16)
+    n = 300_001
+    x = torch.randn(16, n, generator=torch.Generator().manual_seed(11))
+    ref = JwinsRound(adj, x, TUTORIAL_ALPHAS, wavelet=wavelet, ops=OracleJwinsOps(wavelet),
+                     device=torch.device("cpu"), m_len=coeff_len(n, 4, wavelet))
+    eng = JwinsRound(adj, x.to(dev), TUTORIAL_ALPHAS, wavelet=wavelet)
+    assert eng.M == ref.M
+    kinds = set()
+    for r in range(2):
+        for j in range(16):
+            nz = torch.from_numpy(_noise(r, j, n))
+            ref.x[j] += nz
+            eng.x[j] += nz.to(dev)
+        ref.step()
+        eng.step()
+        kinds |= {a >= 0.5 for a in eng.alphas}
+        torch.cuda.synchronize()
+        for name in ("x", "x0", "acc"):
+            np.testing.assert_array_equal(getattr(eng, name).cpu().numpy().view(np.uint32),
+                                          getattr(ref, name).numpy().view(np.uint32), err_msg=name)
+        np.testing.assert_array_equal(eng.counter.cpu().numpy(), ref.counter.numpy())
+    assert kinds == {True, False}

@@ -68,6 +68,27 @@ def test_malformed_frames_are_rejected(dev):
         codec.lz4_decompress(bytes(frame[:-10]), dev)
 
 
+def test_untrusted_content_size_is_bounded_before_allocation(dev):
+    """A peer frame whose header claims 2^40 content bytes (header checksum recomputed, so the
+    header itself is well-formed) is rejected from the block bound, before any allocation."""
+    import struct
+
+    import xxhash
+
+    from decentralizepy_amd import codec
+    frame = bytearray(olz4.ref_compress(_cases()["idx_gaps_c2"]))
+    assert frame[4] & 0x08  # content size present (python-lz4's default store_size=True)
+    frame[6:14] = struct.pack("<Q", 1 << 40)
+    frame[14] = (xxhash.xxh32(bytes(frame[4:14])).intdigest() >> 8) & 0xFF
+    cs, nb, _, bmax = codec.lz4_frame_info(bytes(frame))
+    assert cs == 1 << 40 and cs > nb * bmax
+    with pytest.raises(ValueError):
+        codec.lz4_decompress(bytes(frame), dev)
+    good = olz4.ref_compress(_cases()["idx_gaps_c2"])
+    with pytest.raises(ValueError):  # a caller's max_size below the stored size
+        codec.lz4_decompress(good, dev, max_size=16)
+
+
 def test_lz4wrapper_index_and_value_legs(dev):
     from decentralizepy_amd.compression.Lz4Wrapper import Lz4Wrapper
     rng = np.random.default_rng(11)

@@ -113,3 +113,18 @@ def test_save_accumulated_behaves_like_reference(dev, tmp_path):
     msgs = scenario.neighbour_msgs(meta["rounds"][0], arrays, 0)
     with pytest.raises(AttributeError, match="tolist"):
         plugin._averaging({uid: deque([m]) for uid, m in zip([1, 2, 3], msgs)})
+
+
+def test_staging_over_cap_falls_back_to_pageable_copies(dev):
+    import numpy as np
+    import torch
+
+    from decentralizepy_amd._device import Staging, h2d_array, to_device_flat, to_host
+    st = Staging(cap_bytes=4096)
+    x = torch.randn(100_000)
+    assert torch.equal(to_device_flat(x, dev, st, "local").cpu(), x)
+    a = np.arange(50_000, dtype=np.int32)
+    assert np.array_equal(h2d_array(a, np.int32, dev, st, "idx").cpu().numpy(), a)
+    assert np.array_equal(to_host(torch.from_numpy(a).to(dev), st, "out"), a)
+    small = to_device_flat(torch.ones(100), dev, st, "small")  # within the cap: pinned
+    assert st.total == 400 and torch.equal(small.cpu(), torch.ones(100))

@@ -11,7 +11,7 @@ ok_or_stop() {  # rc 0 = pass, 1 = test failures (still safe to continue); anyth
 }
 STAGE=${1:-all}
 if [ "$STAGE" = all ] || [ "$STAGE" = test ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-900} python -m pytest tests -m gpu -x -q ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
   ok_or_stop $? pytest
   tail -5 gpurun_out/pytest_gpu.log
 fi
