@@ -83,7 +83,9 @@ struct FoldArgs {
 // grid (ceil((kmax+1)/256), np): thread j of payload p handles entry j (j == k: end sentinel).
 // grid (ceil((kmax + 1) / (4 * 256)), np): thread g of payload p handles entries 4g .. 4g + 3
 // (j == k: the end sentinel); the four indices come in one 16-byte load when aligned.
-__global__ void __launch_bounds__(256) fold_offsets_kernel(FoldArgs a, int32_t* starts) {
+template <int SHIFT>
+__global__ void __launch_bounds__(256) fold_offsets_kernel(FoldArgs a, int32_t* starts,
+                                                           int64_t ntiles) {
   const int p = blockIdx.y;
   const FoldPayload& P = a.p[p];
   if (!P.idx) return;
@@ -99,17 +101,17 @@ __global__ void __launch_bounds__(256) fold_offsets_kernel(FoldArgs a, int32_t* 
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e + 1] = (j0 + e < k) ? P.idx[j0 + e] : 0;
   }
-  int32_t* st = starts + (int64_t)p * (a.ntiles + 1);
+  int32_t* st = starts + (int64_t)p * (ntiles + 1);
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int64_t j = j0 + e;
     if (j > k) break;
-    int64_t tprev = j == 0 ? -1 : ((int64_t)v[e] >> FOLD_TILE_SHIFT);
-    int64_t tcur = j == k ? a.ntiles : ((int64_t)v[e + 1] >> FOLD_TILE_SHIFT);
+    int64_t tprev = j == 0 ? -1 : ((int64_t)v[e] >> SHIFT);
+    int64_t tcur = j == k ? ntiles : ((int64_t)v[e + 1] >> SHIFT);
     // an invalid payload (negative / too large / unsorted indices) must not write out of bounds
     if (tprev < -1) tprev = -1;
-    if (tprev > a.ntiles) tprev = a.ntiles;
-    if (tcur > a.ntiles) tcur = a.ntiles;
+    if (tprev > ntiles) tprev = ntiles;
+    if (tcur > ntiles) tcur = ntiles;
     for (int64_t t = tprev + 1; t <= tcur; ++t) st[t] = (int32_t)j;
   }
 }
@@ -834,6 +836,215 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_group_kernel(FoldArgs a)
   }  // tile loop
 }
 
+// ---- the slot fold: every payload of a group in ONE phase per 1024-element tile -------------
+// For dense groups (JWINS alpha 0.03-0.4 x 16 payloads; a node's 3 neighbours with full-share
+// payloads among them) the hit-chain / phase / 4-slot kernels pay a global round trip per tile
+// (or per payload) for the entries at 2 blocks per CU.  Here the tile is 1024 elements and every
+// payload has its own LDS value slot (np x 4 KB + a 16-bit hit mask per element), so one tile is
+//   scatter (entries already in registers) -> barrier -> issue the NEXT tile's entries, local
+//   values and dense payload values -> fold the 4 elements of this thread over all payloads ->
+//   store -> barrier
+// and every global load of a tile is in flight while the previous tile folds.  Dense payloads
+// (idx == NULL) are loaded per element like local (4 values per thread) and written into their
+// slot; their mask bit is implied.  Order per element: the reference's
+//   t = hit ? value : local;  total = t_0*w_0 (+0 first with a zero base); total += t_p*w_p;
+//   total += w_self * local
+// packed fp32 pairs, no FMA (-ffp-contract=off).
+constexpr int FS_SHIFT = 10;
+constexpr int FS_TILE = 1 << FS_SHIFT;
+constexpr int FS_THREADS = 256;          // 4 elements (one float4) per thread
+constexpr int FS_EPT = 16;               // entries per thread held per round
+constexpr int FS_CAP = FS_EPT * FS_THREADS;
+constexpr int FS_DMAX = 4;               // dense payloads per group on this path
+static_assert(FS_TILE == 4 * FS_THREADS, "one float4 per thread");
+
+static inline int64_t fs_ntiles(int64_t n) { return (n + FS_TILE - 1) / FS_TILE; }
+static inline size_t fs_smem(int np) { return (size_t)np * FS_TILE * 4 + FS_TILE * 2; }
+
+template <bool VEC, bool DENSE>
+__global__ void __launch_bounds__(FS_THREADS) fold_slots_kernel(FoldArgs a, int64_t nt,
+                                                                int nd, uint32_t dpk) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char fs_smem_[];
+  float* hv = reinterpret_cast<float*>(fs_smem_);                           // [np][FS_TILE]
+  uint32_t* hm = reinterpret_cast<uint32_t*>(fs_smem_ + (size_t)a.np * FS_TILE * 4);  // masks
+  __shared__ int32_t s_pre[2][FOLD_MAXP + 1];  // tile entry prefix, double-buffered
+  __shared__ int32_t s_rng[2][FOLD_MAXP];      // first entry of the tile per payload
+  __shared__ const int32_t* s_idx[FOLD_MAXP];
+  __shared__ const float* s_val[FOLD_MAXP];
+  const int t = threadIdx.x;
+  const int np = a.np;
+  if (t < np) {
+    s_idx[t] = a.p[t].idx;
+    s_val[t] = a.p[t].val;
+  }
+  hm[2 * t] = 0;
+  hm[2 * t + 1] = 0;
+  const int32_t* starts = a.starts;
+  // thread p < np: the entry range of payload p over a tile (dense payloads: empty)
+  auto range_of = [&](int64_t tl, int32_t& r0, int32_t& r1) {
+    r0 = r1 = 0;
+    if (t < np && tl < nt && a.p[t].idx) {
+      const int32_t* sp = starts + (int64_t)t * (nt + 1);
+      r0 = sp[tl];
+      r1 = sp[tl + 1];
+    }
+  };
+  // wave 0 turns the per-payload ranges into the prefix of the flattened entry list
+  auto publish = [&](int buf, int32_t r0, int32_t r1) {
+    if (t < 64) {
+      const int32_t c = (t < np && r1 > r0) ? r1 - r0 : 0;
+      int32_t incl = c;
+#pragma unroll
+      for (int d = 1; d < FOLD_MAXP; d <<= 1) {
+        const int32_t v = __shfl_up(incl, d, 64);
+        if (t >= d) incl += v;
+      }
+      if (t < FOLD_MAXP) {
+        s_pre[buf][t + 1] = incl;
+        s_rng[buf][t] = r0;
+      }
+      if (t == 0) s_pre[buf][0] = 0;
+    }
+  };
+  // entries [j0, j0 + FS_CAP) of a tile's flattened list: (position | payload << 16) or ~0
+  uint32_t ei[FS_EPT];
+  float ev[FS_EPT];
+  auto load_entries = [&](int buf, int64_t tlo, int32_t j0) {
+    const int32_t tot = s_pre[buf][np];
+#pragma unroll
+    for (int u = 0; u < FS_EPT; ++u) {
+      const int32_t j = j0 + t + u * FS_THREADS;
+      ei[u] = ~0u;
+      ev[u] = 0.0f;
+      if (j < tot) {
+        int p = 0;
+#pragma unroll
+        for (int sb = FOLD_MAXP / 2; sb >= 1; sb >>= 1) p += s_pre[buf][p + sb] <= j ? sb : 0;
+        const int32_t src = s_rng[buf][p] + (j - s_pre[buf][p]);
+        const int64_t pos = (int64_t)s_idx[p][src] - tlo;
+        ev[u] = s_val[p][src];
+        // an invalid payload (unsorted / out of range) is dropped, never written out of bounds
+        ei[u] = (pos >= 0 && pos < FS_TILE) ? ((uint32_t)pos | ((uint32_t)p << 16)) : ~0u;
+      }
+    }
+  };
+  float4 L, Ln;
+  float4 dv[DENSE ? FS_DMAX : 1], dn[DENSE ? FS_DMAX : 1];
+  auto load_elems = [&](int64_t tl, float4& l4, float4 (&d4)[DENSE ? FS_DMAX : 1]) {
+    const int64_t i0 = tl * FS_TILE + 4 * t;
+    auto ld = [&](const float* src) {
+      if (VEC && i0 + 3 < a.n) return *reinterpret_cast<const float4*>(src + i0);
+      float e[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) e[q] = i0 + q < a.n ? src[i0 + q] : 0.0f;
+      return make_float4(e[0], e[1], e[2], e[3]);
+    };
+    if (tl >= nt) return;
+    l4 = ld(a.local);
+    if (DENSE) {
+#pragma unroll
+      for (int d = 0; d < FS_DMAX; ++d)
+        if (d < nd) d4[d] = ld(a.p[(dpk >> (4 * d)) & 15u].val);
+    }
+  };
+  // prologue: ranges of the first two tiles, the first tile's entries and elements
+  int64_t tile = blockIdx.x;
+  int32_t r0, r1;
+  range_of(tile, r0, r1);
+  publish(0, r0, r1);
+  range_of(tile + gridDim.x, r0, r1);  // held for the next tile's publish
+  __syncthreads();
+  load_entries(0, tile * FS_TILE, 0);
+  load_elems(tile, L, dv);
+  int buf = 0;
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  for (; tile < nt; tile += gridDim.x) {
+    const int64_t tlo = tile * FS_TILE;
+    // scatter this tile's entries (the first FS_CAP; the rest in extra rounds, synchronously)
+    const int32_t tot = s_pre[buf][np];
+    for (int32_t j0 = 0;;) {
+#pragma unroll
+      for (int u = 0; u < FS_EPT; ++u) {
+        if (ei[u] != ~0u) {
+          const uint32_t pos = ei[u] & 0xFFFFu, p = ei[u] >> 16;
+          hv[p * FS_TILE + pos] = ev[u];
+          atomicOr(&hm[pos >> 1], (1u << p) << (16u * (pos & 1u)));
+        }
+      }
+      j0 += FS_CAP;
+      if (j0 >= tot) break;
+      load_entries(buf, tlo, j0);
+    }
+    if (DENSE) {
+#pragma unroll
+      for (int d = 0; d < FS_DMAX; ++d)
+        if (d < nd)
+          *reinterpret_cast<float4*>(&hv[((dpk >> (4 * d)) & 15u) * FS_TILE + 4 * t]) = dv[d];
+    }
+    // the next tile's prefix (its ranges were loaded one tile ago)
+    publish(buf ^ 1, r0, r1);
+    __syncthreads();  // B1: slots, masks and the next prefix visible
+    const int64_t nx = tile + gridDim.x;
+    range_of(nx + gridDim.x, r0, r1);  // two tiles ahead
+    if (nx < nt) {
+      load_entries(buf ^ 1, nx * FS_TILE, 0);
+      load_elems(nx, Ln, dn);
+    }
+    // fold this thread's 4 elements over every payload
+    const uint2 mw = *reinterpret_cast<const uint2*>(&hm[2 * t]);
+    *reinterpret_cast<uint2*>(&hm[2 * t]) = make_uint2(0u, 0u);
+    const uint32_t dm = a.dense_mask;
+    const uint32_t m0 = (mw.x & 0xFFFFu) | dm, m1 = (mw.x >> 16) | dm;
+    const uint32_t m2 = (mw.y & 0xFFFFu) | dm, m3 = (mw.y >> 16) | dm;
+    const f2v base01 = a.zero_base ? f2v{0.0f, 0.0f} : f2v{L.x, L.y};
+    const f2v base23 = a.zero_base ? f2v{0.0f, 0.0f} : f2v{L.z, L.w};
+    f2v acc01 = {0.0f, 0.0f}, acc23 = {0.0f, 0.0f};
+#pragma unroll
+    for (int p = 0; p < FOLD_MAXP; ++p) {
+      if (p >= np) break;
+      const float w = a.p[p].w;
+      const f2v w2 = {w, w};
+      const float4 h4 = *reinterpret_cast<const float4*>(&hv[p * FS_TILE + 4 * t]);
+      const f2v t01 = {((m0 >> p) & 1u) ? h4.x : base01.x, ((m1 >> p) & 1u) ? h4.y : base01.y};
+      const f2v t23 = {((m2 >> p) & 1u) ? h4.z : base23.x, ((m3 >> p) & 1u) ? h4.w : base23.y};
+      if (p == 0) {
+        const f2v z = {0.0f, 0.0f};
+        acc01 = a.zero_base ? z + t01 * w2 : t01 * w2;
+        acc23 = a.zero_base ? z + t23 * w2 : t23 * w2;
+      } else {
+        acc01 = acc01 + t01 * w2;
+        acc23 = acc23 + t23 * w2;
+      }
+    }
+    float r[4] = {acc01.x, acc01.y, acc23.x, acc23.y};
+    if (a.add_self) {
+      const float lv[4] = {L.x, L.y, L.z, L.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = r[e] + lv[e] * a.w_self;
+    }
+    const int64_t i0 = tlo + 4 * t;
+    if (VEC && i0 + 3 < a.n) {
+      const float4 r4 = make_float4(r[0], r[1], r[2], r[3]);
+      *reinterpret_cast<float4*>(a.out + i0) = r4;
+      if (a.out2) *reinterpret_cast<float4*>(a.out2 + i0) = r4;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (i0 + e < a.n) {
+          a.out[i0 + e] = r[e];
+          if (a.out2) a.out2[i0 + e] = r[e];
+        }
+    }
+    L = Ln;
+    if (DENSE) {
+#pragma unroll
+      for (int d = 0; d < FS_DMAX; ++d) dv[d] = dn[d];
+    }
+    buf ^= 1;
+    __syncthreads();  // B2: every fold read of the slots / masks / prefix is done
+  }
+}
+
 // blocks of the persistent fold grid: what the CUs hold at once (occupancy API)
 template <bool VEC>
 static unsigned fold_grid(int64_t ntiles, bool group = false) {
@@ -858,6 +1069,28 @@ static unsigned fold_grid(int64_t ntiles, bool group = false) {
 }
 
 static inline int64_t fold_ntiles(int64_t n) { return (n + FOLD_TILE - 1) / FOLD_TILE; }
+
+// blocks of the slot fold: what the CUs hold at once with np slots of dynamic LDS
+template <bool VEC, bool DENSE>
+static unsigned fs_grid(int64_t nt, int np) {
+  static int per_np[FOLD_MAXP + 1] = {};
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  int& per = per_np[np];
+  if (per == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fold_slots_kernel<VEC, DENSE>,
+                                                     FS_THREADS, fs_smem(np)) != hipSuccess ||
+        per < 1)
+      per = 1;
+  }
+  const int64_t g = (int64_t)cus * per;
+  return (unsigned)(nt < g ? (nt > 0 ? nt : 1) : g);
+}
 
 // Replace-only decode of ONE sparse payload (reference PartialModel.py:257-303, T[idx] = params):
 // one 256-thread block per chunk of RP_E payload entries (dpz_replace.h).
@@ -889,7 +1122,8 @@ extern "C" int dpz_debug_fold_stamps(unsigned long long* host_out, int reset) {
 
 extern "C" size_t dpz_decode_workspace_bytes(int64_t n, int n_payloads) {
   const int64_t np = n_payloads < FOLD_MAXP ? (n_payloads > 0 ? n_payloads : 1) : FOLD_MAXP;
-  return (size_t)np * (size_t)(fold_ntiles(n > 0 ? n : 1) + 1) * sizeof(int32_t);
+  // tile starts at the slot fold's 1024-element granularity (the coarser 4096 fit inside)
+  return (size_t)np * (size_t)(fs_ntiles(n > 0 ? n : 1) + 1) * sizeof(int32_t);
 }
 
 extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
@@ -977,20 +1211,57 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
         fa.all_sparse = 0;
         fa.dense_mask |= 1u << i;
       }
+    // The slot fold (fold_slots_kernel) takes dense-alpha groups: entries per 4096 elements on
+    // average >= DPZ_FOLD_SLOTS_MIN (default below), at most FS_DMAX dense payloads, a fresh
+    // total.  DPZ_FOLD_KIND=1 / 2 / 3 forces the classic / 4-slot group / slot fold (A/B
+    // diagnostics; a forced kind that cannot take the group falls back to the classic kernel).
+    int64_t etot = 0;
+    int nd = 0;
+    uint32_t dpk = 0;
+    for (int i = 0; i < fa.np; ++i) {
+      if (fa.p[i].idx) {
+        etot += fa.p[i].k;
+      } else {
+        if (nd < FS_DMAX) dpk |= (uint32_t)i << (4 * nd);
+        ++nd;
+      }
+    }
+    const int kind = getenv("DPZ_FOLD_KIND") ? atoi(getenv("DPZ_FOLD_KIND")) : 0;
+    const int64_t slots_min =
+        getenv("DPZ_FOLD_SLOTS_MIN") ? atoll(getenv("DPZ_FOLD_SLOTS_MIN")) : 600;
+    const bool slots_ok = !fa.replace_only && fa.first && nd <= FS_DMAX && fa.np > 0;
+    bool use_slots = slots_ok && (etot + (int64_t)nd * n > slots_min * ntiles);
+    if (kind) use_slots = slots_ok && kind == 3;
+    if (use_slots) {
+      const int64_t nt = fs_ntiles(n);
+      fa.starts = starts;
+      if (kmax >= 0) {
+        dim3 og((unsigned)((kmax + 1 + 1023) / 1024), (unsigned)fa.np);
+        DPZ_TIMED(DPZ_KT_FOLD_OFFSETS, st, fold_offsets_kernel<FS_SHIFT><<<og, 256, 0, st>>>(fa, starts, nt));
+      }
+      const size_t sm = fs_smem(fa.np);
+      if (nd) {
+        if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_slots_kernel<true, true><<<fs_grid<true, true>(nt, fa.np), FS_THREADS, sm, st>>>(fa, nt, nd, dpk));
+        else DPZ_TIMED(DPZ_KT_FOLD, st, fold_slots_kernel<false, true><<<fs_grid<false, true>(nt, fa.np), FS_THREADS, sm, st>>>(fa, nt, nd, dpk));
+      } else {
+        if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_slots_kernel<true, false><<<fs_grid<true, false>(nt, fa.np), FS_THREADS, sm, st>>>(fa, nt, 0, 0u));
+        else DPZ_TIMED(DPZ_KT_FOLD, st, fold_slots_kernel<false, false><<<fs_grid<false, false>(nt, fa.np), FS_THREADS, sm, st>>>(fa, nt, 0, 0u));
+      }
+      continue;
+    }
     if (kmax >= 0) {
       dim3 og((unsigned)((kmax + 1 + 1023) / 1024), (unsigned)fa.np);
-      DPZ_TIMED(DPZ_KT_FOLD_OFFSETS, st, fold_offsets_kernel<<<og, 256, 0, st>>>(fa, starts));
+      DPZ_TIMED(DPZ_KT_FOLD_OFFSETS, st, fold_offsets_kernel<FOLD_TILE_SHIFT><<<og, 256, 0, st>>>(fa, starts, ntiles));
     }
     // all-sparse groups of >= 8 payloads with FOLD_GROUP_MIN .. 2 FG_CAP entries per tile on
     // average take the slotted fold (measured on MI355X at 25 M x 16 payloads: alpha 0.04
     // 463 -> 193 us, 0.1 345 -> 284 us; the hit-chain path stays faster at alpha 0.01, the
     // phase path at alpha 0.2 x 16 and for a few dense payloads); DPZ_FOLD_GROUP=0 / 1 forces it
     if (fa.all_sparse && fa.np > 0 && !fa.replace_only) {
-      int64_t etot = 0;
-      for (int i = 0; i < fa.np; ++i) etot += fa.p[i].k;
       bool use_group = fa.np >= 8 && etot > FOLD_GROUP_MIN * ntiles &&
                        etot <= 2 * (int64_t)FG_CAP * ntiles;
       if (const char* e = getenv("DPZ_FOLD_GROUP")) use_group = atoi(e) != 0;
+      if (kind) use_group = kind == 2;
       if (use_group) {
         if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_group_kernel<true><<<fold_grid<true>(ntiles, true), FOLD_THREADS, 0, st>>>(fa));
         else DPZ_TIMED(DPZ_KT_FOLD, st, fold_group_kernel<false><<<fold_grid<false>(ntiles, true), FOLD_THREADS, 0, st>>>(fa));

@@ -300,6 +300,83 @@ def test_fold_paths_forced(dev, monkeypatch, group, n, alpha, npay):
     np.testing.assert_array_equal(_bits(tout.cpu().numpy()), _bits(ref3))
 
 
+@pytest.mark.parametrize("kind", ["1", "2", "3"])
+@pytest.mark.parametrize("n,alpha,npay,ndense", [(1_000_003, 0.01, 16, 0), (1_000_003, 0.1, 16, 0),
+                                                 (2_000_001, 0.25, 16, 0), (300_001, 0.3, 3, 1),
+                                                 (300_001, 0.1, 3, 3), (100_003, 0.99, 2, 0),
+                                                 (50_000, 0.05, 7, 4), (4097, 0.2, 5, 2)])
+def test_fold_kinds_forced(dev, monkeypatch, kind, n, alpha, npay, ndense):
+    """Every fold kernel forced in turn (DPZ_FOLD_KIND 1: classic hit-chain / phase, 2: 4-slot
+    group, 3: the one-phase slot fold) on sparse groups and on groups with dense (full-share)
+    payloads, bit-exact vs the oracle with and without the self term and with a zero base; a
+    kind that cannot take a group (dense payloads on the 4-slot path, more than 4 dense on the
+    slot fold) runs the classic kernel.  alpha 0.25 x 16 needs two entry rounds per slot tile."""
+    monkeypatch.setenv("DPZ_FOLD_KIND", kind)
+    codec = _codec()
+    rng = np.random.default_rng(int(n * alpha) + npay + 31 * ndense)
+    local = rng.standard_normal(n).astype(np.float32)
+    k = max(1, round(alpha * n))
+    pays, tpays = [], []
+    dense_at = set(rng.choice(npay, size=ndense, replace=False).tolist())
+    for i in range(npay):
+        if i in dense_at:
+            vals = rng.standard_normal(n).astype(np.float32)
+            pays.append((None, vals))
+            tpays.append((None, torch.from_numpy(vals).to(dev)))
+            continue
+        idx = np.sort(rng.choice(n, size=k, replace=False)).astype(np.int32)
+        vals = rng.standard_normal(k).astype(np.float32)
+        pays.append((idx, vals))
+        tpays.append((torch.from_numpy(idx).to(dev), torch.from_numpy(vals).to(dev)))
+    weights = [ofold.mh_weight(npay, int(d)) for d in rng.integers(1, 20, size=npay)]
+    w_self = 1 - sum(weights)
+    tl = torch.from_numpy(local).to(dev)
+    ref = ofold.fold(local, pays, weights, w_self)
+    out = codec.decode_average(tl, tpays, weights, w_self).cpu().numpy()
+    np.testing.assert_array_equal(_bits(out), _bits(ref))
+    ref2 = ofold.fold(local, pays, [1 / npay] * npay, None)
+    out2 = codec.decode_average(tl, tpays, [1 / npay] * npay, None).cpu().numpy()
+    np.testing.assert_array_equal(_bits(out2), _bits(ref2))
+    if ndense == 0:
+        zeros = np.zeros(n, np.float32)
+        ref3 = np.zeros(n, np.float32)
+        for j, ((idx, vals), wi) in enumerate(zip(pays, weights)):
+            term = ofold.replace(zeros, idx, vals) * np.float32(wi)
+            ref3 = (np.float32(0) + term) if j == 0 else ref3 + term
+        out3 = codec.decode_average(torch.zeros(n, device=dev), tpays, weights, None,
+                                    zero_base=True).cpu().numpy()
+        np.testing.assert_array_equal(_bits(out3), _bits(ref3))
+    # in place over local (DPZ_FOLD_ALSO_LOCAL)
+    tl2 = torch.from_numpy(local).to(dev)
+    out4 = codec.decode_average(tl2, tpays, weights, w_self, also_local=True)
+    np.testing.assert_array_equal(_bits(out4.cpu().numpy()), _bits(ref))
+    np.testing.assert_array_equal(_bits(tl2.cpu().numpy()), _bits(ref))
+
+
+@pytest.mark.parametrize("kind", ["3"])
+@pytest.mark.parametrize("alpha", [0.1, 0.3])
+def test_slot_fold_unaligned_views(dev, monkeypatch, kind, alpha):
+    """The slot fold's scalar-load build (local / out 4 bytes off a 16-byte boundary)."""
+    monkeypatch.setenv("DPZ_FOLD_KIND", kind)
+    codec = _codec()
+    n, npay = 300_001, 16
+    rng = np.random.default_rng(int(alpha * 100) + 9)
+    local = rng.standard_normal(n + 1).astype(np.float32)
+    k = round(alpha * n)
+    pays, tpays = [], []
+    for _ in range(npay):
+        idx = np.sort(rng.choice(n, size=k, replace=False)).astype(np.int32)
+        vals = rng.standard_normal(k).astype(np.float32)
+        pays.append((idx, vals))
+        tpays.append((torch.from_numpy(idx).to(dev), torch.from_numpy(vals).to(dev)))
+    w = [1 / (npay + 1)] * npay
+    tl = torch.from_numpy(local).to(dev)[1:]
+    out = torch.empty(n + 1, device=dev)[1:]
+    codec.decode_average(tl, tpays, w, 1 - sum(w), out=out)
+    ref = ofold.fold(local[1:], pays, w, 1 - sum(w))
+    np.testing.assert_array_equal(_bits(out.cpu().numpy()), _bits(ref))
+
+
 @pytest.mark.parametrize("group", ["0", "1"])
 @pytest.mark.parametrize("alpha", [0.01, 0.1])
 def test_fold_unaligned_views(dev, monkeypatch, group, alpha):
