@@ -94,7 +94,7 @@ static int dpz_topk_dispatch(EncodeArgs a, int flags) {
     if (flags & DPZ_TOPK_ASYNC) return DPZ_OK;
     int fb = 0;
     return dpz_topk_complete(a.x, a.x0, a.acc, a.acc_mode, a.vals_src, a.n, a.k, a.idx_out,
-                             a.val_out, a.counter, a.ws, L.total, &fb, a.st);
+                             a.val_out, a.counter, a.ws, ws_bytes_needed(a.n, a.k), &fb, a.st);
   }
   if (phases == 2) return DPZ_OK;  // the exact path ran whole in the STREAM call
   int rc = run_exact(a, L, 0, vec);
