@@ -1045,6 +1045,291 @@ __global__ void __launch_bounds__(FS_THREADS) fold_slots_kernel(FoldArgs a, int6
   }
 }
 
+// ---- the walk fold: one wave per contiguous element range, payload cursors, no barriers -----
+// Every other fold kernel needs the tile-offsets pre-pass (fold_offsets_kernel reads every
+// payload index once more: 35-100 us of 25 M x 16 payloads at JWINS alphas) and block barriers
+// per tile or per payload.  Here each wave owns a contiguous run of tiles of TE = 64 * EPL
+// elements and walks every payload's sorted entries with a cursor:
+//  * start: a 64-ary search (64 probes per step, one wave-wide load) finds each payload's first
+//    entry of the wave's range: <= 6 dependent steps for any k, all payloads' probes in flight;
+//  * per tile: a 64-entry window per payload (idx, val; one coalesced load each) is already in
+//    registers; the entries inside the tile are its leading lanes (sorted), their count advances
+//    the cursor, and the NEXT tile's windows, local values and dense payload values are issued
+//    before this tile is folded;
+//  * payload by payload, in the reference's order, the window's lanes write their values with a
+//    (tile, payload) tag into the wave's own LDS row, and every lane folds its EPL elements
+//      t = (tag == mine) ? value : local;  total = t_0*w_0 (+0 first with a zero base);
+//      total += t_p*w_p;  total += w_self * local
+//    (no block barrier: the row is the wave's own, LDS ops of one wave run in order).
+// A window whose 64 entries all fall inside the tile (dense tiles) is followed by synchronous
+// extra windows (correct, slower); EPL is chosen so a tile holds ~32 entries per payload on
+// average.  Invalid payloads (unsorted / out of range) cannot write out of bounds.
+constexpr int FW_WAVES = 4;  // waves per block (256 threads)
+constexpr int FW_DMAX = 4;   // dense payloads per group on this path
+
+template <int EPL>
+struct FwV {
+  float v[EPL];
+};
+
+template <bool VEC, int EPL>
+__device__ __forceinline__ FwV<EPL> fw_load(const float* p, int64_t i0, int64_t n) {
+  FwV<EPL> r;
+  if (VEC && i0 + EPL <= n) {
+    if constexpr (EPL == 4) {
+      const float4 v = *reinterpret_cast<const float4*>(p + i0);
+      r.v[0] = v.x; r.v[1] = v.y; r.v[2] = v.z; r.v[3] = v.w;
+      return r;
+    } else if constexpr (EPL == 2) {
+      const float2 v = *reinterpret_cast<const float2*>(p + i0);
+      r.v[0] = v.x; r.v[1] = v.y;
+      return r;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) r.v[e] = i0 + e < n ? p[i0 + e] : 0.0f;
+  return r;
+}
+
+template <bool VEC, int EPL>
+__device__ __forceinline__ void fw_store(float* p, int64_t i0, int64_t n, const float (&r)[EPL]) {
+  if (VEC && i0 + EPL <= n) {
+    if constexpr (EPL == 4) {
+      *reinterpret_cast<float4*>(p + i0) = make_float4(r[0], r[1], r[2], r[3]);
+      return;
+    } else if constexpr (EPL == 2) {
+      *reinterpret_cast<float2*>(p + i0) = make_float2(r[0], r[1]);
+      return;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EPL; ++e)
+    if (i0 + e < n) p[i0 + e] = r[e];
+}
+
+// the leading lanes whose index lies below `hi` (a sorted window): 0..64
+__device__ __forceinline__ int fw_lead(bool in) {
+  const uint64_t b = __ballot(in);
+  return ~b == 0 ? 64 : (int)__builtin_ctzll(~b);
+}
+
+__device__ __forceinline__ int32_t fw_uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+template <bool VEC, int EPL, int NPMAX, bool DENSE>
+__global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw, int nd,
+                                                        uint32_t dpk) {
+  constexpr int TE = 64 * EPL;
+  __shared__ float s_val[FW_WAVES][TE];
+  __shared__ uint32_t s_tag[FW_WAVES][TE];
+  __shared__ float s_dense[DENSE ? FW_WAVES : 1][DENSE ? FW_DMAX : 1][DENSE ? TE : 1];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float* wv = s_val[wid];
+  uint32_t* wt = s_tag[wid];
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) wt[lane + 64 * e] = 0xFFFFFFFFu;
+  const int64_t n = a.n;
+  const int64_t ntl = (n + TE - 1) / TE;
+  const int64_t gw = (int64_t)blockIdx.x * FW_WAVES + wid;
+  const int64_t t0 = gw * tpw;
+  const int64_t t1 = (t0 + tpw < ntl) ? t0 + tpw : ntl;
+  if (t0 >= t1) return;  // no block barrier anywhere: a wave may leave alone
+  const int np = a.np;
+  // ---- start cursors: 64-ary lower_bound(idx_p, t0 * TE) of every sparse payload (k < 2^31,
+  // n < 2^31: 32-bit positions) ----
+  int32_t cur[NPMAX];
+  {
+    int32_t lo[NPMAX], hi[NPMAX];
+    const int32_t e0 = (int32_t)(t0 * TE);
+#pragma unroll
+    for (int p = 0; p < NPMAX; ++p) {
+      lo[p] = 0;
+      hi[p] = (p < np && a.p[p].idx) ? (int32_t)a.p[p].k : 0;
+    }
+    for (int step = 0; step < 7; ++step) {
+      int32_t v[NPMAX], stride[NPMAX];
+#pragma unroll
+      for (int p = 0; p < NPMAX; ++p) {  // every payload's probes in flight together
+        const int32_t len = hi[p] - lo[p];
+        stride[p] = len <= 64 ? 1 : (len + 63) / 64;
+        const int64_t q = (int64_t)lo[p] + (int64_t)lane * stride[p];
+        v[p] = (len > 0 && q < hi[p]) ? a.p[p].idx[q] : INT32_MAX;
+      }
+      bool more = false;
+#pragma unroll
+      for (int p = 0; p < NPMAX; ++p) {
+        const int32_t len = hi[p] - lo[p];
+        if (len <= 0) continue;
+        const int32_t c = (int32_t)__popcll(__ballot(v[p] < e0));  // probes below e0: a prefix
+        if (stride[p] == 1) {
+          lo[p] = fw_uni(lo[p] + c);
+          hi[p] = lo[p];
+        } else {
+          const int32_t nlo = c > 0 ? lo[p] + (c - 1) * stride[p] + 1 : lo[p];
+          const int64_t nhi = (int64_t)lo[p] + (int64_t)c * stride[p];
+          lo[p] = fw_uni(nlo);
+          hi[p] = fw_uni(nhi < hi[p] ? (int32_t)nhi : hi[p]);
+          more = true;
+        }
+      }
+      if (!more) break;
+    }
+#pragma unroll
+    for (int p = 0; p < NPMAX; ++p) cur[p] = lo[p];
+  }
+  // ---- one 64-entry window per sparse payload: (idx, val) at cur + lane ----
+  int32_t wi[NPMAX], wn[NPMAX];
+  float wvv[NPMAX], wvn[NPMAX];
+  auto load_windows = [&](int32_t (&ix)[NPMAX], float (&vx)[NPMAX]) {
+#pragma unroll
+    for (int p = 0; p < NPMAX; ++p) {
+      ix[p] = INT32_MAX;
+      vx[p] = 0.0f;
+      if (p < np && a.p[p].idx) {
+        const int64_t j = (int64_t)cur[p] + lane;
+        if (j < a.p[p].k) {
+          ix[p] = a.p[p].idx[j];
+          vx[p] = a.p[p].val[j];
+        }
+      }
+    }
+  };
+  FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE + lane * EPL, n), Ln;
+  FwV<EPL> O, On;  // a running total continued from out (DPZ_FOLD_ACCUMULATE)
+  if (!a.first) O = fw_load<VEC, EPL>(a.out, t0 * TE + lane * EPL, n);
+  FwV<EPL> D[DENSE ? FW_DMAX : 1], Dn[DENSE ? FW_DMAX : 1];
+  if (DENSE) {
+#pragma unroll
+    for (int d = 0; d < FW_DMAX; ++d)
+      if (d < nd) D[d] = fw_load<VEC, EPL>(a.p[(dpk >> (4 * d)) & 15u].val, t0 * TE + lane * EPL, n);
+  }
+  load_windows(wi, wvv);
+  uint32_t seq = 0;
+  for (int64_t tile = t0; tile < t1; ++tile, ++seq) {
+    const int64_t tlo = tile * TE, thi = tlo + TE;
+    // entries of this tile per payload = the window's leading lanes below thi
+    int cnt[NPMAX];
+    bool full = false;
+#pragma unroll
+    for (int p = 0; p < NPMAX; ++p) {
+      cnt[p] = fw_lead((int64_t)wi[p] < thi);
+      full |= cnt[p] == 64;
+    }
+    const bool has_next = tile + 1 < t1;
+    // usual case: every cursor advances now and the next tile's windows, local values and dense
+    // values go in flight before this tile folds; a full window (a dense tile) defers that to
+    // after the fold, its payload's further windows read synchronously in its phase
+    if (!full) {
+#pragma unroll
+      for (int p = 0; p < NPMAX; ++p) cur[p] = fw_uni(cur[p] + cnt[p]);
+      if (has_next) load_windows(wn, wvn);
+    }
+    if (has_next) {
+      Ln = fw_load<VEC, EPL>(a.local, thi + lane * EPL, n);
+      if (!a.first) On = fw_load<VEC, EPL>(a.out, thi + lane * EPL, n);
+      if (DENSE) {
+#pragma unroll
+        for (int d = 0; d < FW_DMAX; ++d)
+          if (d < nd) Dn[d] = fw_load<VEC, EPL>(a.p[(dpk >> (4 * d)) & 15u].val, thi + lane * EPL, n);
+      }
+    }
+    if (DENSE) {  // this tile's dense values: this lane's own elements, read back by it only
+#pragma unroll
+      for (int d = 0; d < FW_DMAX; ++d)
+        if (d < nd) {
+#pragma unroll
+          for (int e = 0; e < EPL; ++e) s_dense[wid][d][lane * EPL + e] = D[d].v[e];
+        }
+    }
+    float acc[EPL], base[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      base[e] = a.zero_base ? 0.0f : L.v[e];
+      acc[e] = a.first ? 0.0f : O.v[e];
+    }
+    int dord = 0;
+#pragma unroll
+    for (int p = 0; p < NPMAX; ++p) {
+      if (p >= np) break;
+      const float w = a.p[p].w;
+      const bool first_term = a.first && p == 0;
+      float tv[EPL];
+      if (!a.p[p].idx) {  // dense: its own value everywhere
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) tv[e] = DENSE ? s_dense[wid][dord][lane * EPL + e] : base[e];
+        ++dord;
+      } else {
+        const uint32_t tag = (seq << 4) | (uint32_t)p;
+        {
+          const int64_t pos = (int64_t)wi[p] - tlo;
+          if (lane < cnt[p] && pos >= 0 && pos < TE) {
+            wv[pos] = wvv[p];
+            wt[pos] = tag;
+          }
+        }
+        if (full) {
+          // this payload's further entries in the tile (cnt == 64), then its cursor
+          int32_t c = cnt[p];
+          if (c == 64) {
+            for (int32_t j0 = cur[p] + 64;; j0 += 64) {
+              const int64_t j = (int64_t)j0 + lane;
+              const int32_t iv = j < a.p[p].k ? a.p[p].idx[j] : INT32_MAX;
+              const bool in = (int64_t)iv < thi;
+              const int cc = fw_lead(in);
+              const int64_t pos = (int64_t)iv - tlo;
+              if (lane < cc && pos >= 0 && pos < TE) {
+                wv[pos] = a.p[p].val[j];
+                wt[pos] = tag;
+              }
+              c += cc;
+              if (cc < 64) break;
+            }
+          }
+          cur[p] = fw_uni(cur[p] + c);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+          const int q = lane * EPL + e;
+          tv[e] = wt[q] == tag ? wv[q] : base[e];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        const float term = tv[e] * w;
+        acc[e] = first_term ? (a.zero_base ? 0.0f + term : term) : acc[e] + term;
+      }
+    }
+    if (full) {  // every cursor now final (payloads past np / dense advanced by 0)
+#pragma unroll
+      for (int p = 0; p < NPMAX; ++p)
+        if (p >= np || !a.p[p].idx) cur[p] = fw_uni(cur[p] + cnt[p]);
+      if (has_next) load_windows(wn, wvn);
+    }
+    if (a.add_self) {
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) acc[e] = acc[e] + L.v[e] * a.w_self;
+    }
+    fw_store<VEC, EPL>(a.out, tlo + lane * EPL, n, acc);
+    if (a.out2) fw_store<VEC, EPL>(a.out2, tlo + lane * EPL, n, acc);
+    if (has_next) {
+#pragma unroll
+      for (int p = 0; p < NPMAX; ++p) {
+        wi[p] = wn[p];
+        wvv[p] = wvn[p];
+      }
+      L = Ln;
+      if (!a.first) O = On;
+      if (DENSE) {
+#pragma unroll
+        for (int d = 0; d < FW_DMAX; ++d) D[d] = Dn[d];
+      }
+    }
+  }
+}
+
 // blocks of the persistent fold grid: what the CUs hold at once (occupancy API)
 template <bool VEC>
 static unsigned fold_grid(int64_t ntiles, bool group = false) {
@@ -1090,6 +1375,54 @@ static unsigned fs_grid(int64_t nt, int np) {
   }
   const int64_t g = (int64_t)cus * per;
   return (unsigned)(nt < g ? (nt > 0 ? nt : 1) : g);
+}
+
+// The walk fold's launch: EPL from the densest sparse payload (~32 entries per payload per
+// tile on average), NPMAX 4 or 16, dense payloads staged per wave; a persistent grid of what
+// the CUs hold, each wave a contiguous run of tiles.
+template <bool VEC, int EPL, int NPMAX, bool DENSE>
+static int launch_walk_t(const FoldArgs& fa, int nd, uint32_t dpk, hipStream_t st) {
+  static int per = 0, cus = 0;
+  if (per == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fold_walk_kernel<VEC, EPL, NPMAX, DENSE>,
+                                                     256, 0) != hipSuccess || per < 1)
+      per = 1;
+  }
+  constexpr int TE = 64 * EPL;
+  const int64_t ntl = (fa.n + TE - 1) / TE;
+  int64_t blocks = (int64_t)cus * per;
+  const int64_t need = (ntl + FW_WAVES - 1) / FW_WAVES;
+  if (blocks > need) blocks = need;
+  if (blocks < 1) blocks = 1;
+  const int64_t tpw = (ntl + blocks * FW_WAVES - 1) / (blocks * FW_WAVES);
+  DPZ_TIMED(DPZ_KT_FOLD, st, fold_walk_kernel<VEC, EPL, NPMAX, DENSE><<<(unsigned)blocks, 256, 0, st>>>(fa, tpw, nd, dpk));
+  return DPZ_OK;
+}
+
+template <bool VEC, int EPL>
+static int launch_walk_e(const FoldArgs& fa, int nd, uint32_t dpk, hipStream_t st) {
+  if (fa.np <= 4)
+    return nd ? launch_walk_t<VEC, EPL, 4, true>(fa, nd, dpk, st)
+              : launch_walk_t<VEC, EPL, 4, false>(fa, nd, dpk, st);
+  return nd ? launch_walk_t<VEC, EPL, 16, true>(fa, nd, dpk, st)
+            : launch_walk_t<VEC, EPL, 16, false>(fa, nd, dpk, st);
+}
+
+static int launch_walk(const FoldArgs& fa, bool vec, double dens, int nd, uint32_t dpk,
+                       hipStream_t st) {
+  const int epl = dens <= 0.125 ? 4 : (dens <= 0.25 ? 2 : 1);
+  if (vec) {
+    if (epl == 4) return launch_walk_e<true, 4>(fa, nd, dpk, st);
+    if (epl == 2) return launch_walk_e<true, 2>(fa, nd, dpk, st);
+    return launch_walk_e<true, 1>(fa, nd, dpk, st);
+  }
+  if (epl == 4) return launch_walk_e<false, 4>(fa, nd, dpk, st);
+  if (epl == 2) return launch_walk_e<false, 2>(fa, nd, dpk, st);
+  return launch_walk_e<false, 1>(fa, nd, dpk, st);
 }
 
 // Replace-only decode of ONE sparse payload (reference PartialModel.py:257-303, T[idx] = params):
@@ -1229,6 +1562,15 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
     const int kind = getenv("DPZ_FOLD_KIND") ? atoi(getenv("DPZ_FOLD_KIND")) : 0;
     const int64_t slots_min =
         getenv("DPZ_FOLD_SLOTS_MIN") ? atoll(getenv("DPZ_FOLD_SLOTS_MIN")) : 600;
+    // DPZ_FOLD_KIND=4 forces the walk fold (no offsets pre-pass)
+    if (kind == 4 && !fa.replace_only && nd <= FW_DMAX && fa.np > 0) {
+      double dens = 0.0;
+      for (int i = 0; i < fa.np; ++i)
+        if (fa.p[i].idx && (double)fa.p[i].k / (double)n > dens) dens = (double)fa.p[i].k / (double)n;
+      const int rc = launch_walk(fa, vec, dens, nd, dpk, st);
+      if (rc != DPZ_OK) return rc;
+      continue;
+    }
     const bool slots_ok = !fa.replace_only && fa.first && nd <= FS_DMAX && fa.np > 0;
     bool use_slots = slots_ok && (etot + (int64_t)nd * n > slots_min * ntiles);
     if (kind) use_slots = slots_ok && kind == 3;

@@ -59,7 +59,7 @@ def case(dev, m, alpha, npay, ndense, kinds, reps=20):
 def main():
     dev = torch.device("cuda:0")
     m = 25_000_009
-    kinds = sys.argv[1:] or ["0", "1", "2", "3"]
+    kinds = sys.argv[1:] or ["0", "1", "2", "4"]
     for alpha, npay, nd in ((0.01, 16, 0), (0.03, 16, 0), (0.1, 16, 0), (0.2, 16, 0),
                             (0.3, 16, 0), (0.1, 3, 0), (0.3, 3, 0), (0.1, 3, 1), (0.3, 3, 2),
                             (0.2, 3, 3)):
