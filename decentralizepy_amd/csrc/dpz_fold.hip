@@ -27,6 +27,7 @@
 //    All follow the reference's fp32 order exactly (library compiled with -ffp-contract=off).
 // Algorithmic bytes: read local (4N) + write out (4N) + 8 bytes per payload entry.
 #include <cstdlib>
+#include <type_traits>
 
 #include "dpz_common.h"
 #include "dpz_replace.h"
@@ -1072,28 +1073,40 @@ struct FwV {
   float v[EPL];
 };
 
+// Loads are branch-free (addresses clamped into [0, n), results past n unused: their elements
+// are never stored), so the compiler can count them and wait only for the tile it folds, never
+// for the next tile's loads in flight (a load under a branch makes it wait for all: vmcnt(0)).
+// VEC kernels run only for n >= 4 and 16-byte aligned operands.
+// Loads are branch-free (addresses clamped into [0, n); results past n are never stored), so
+// the compiler counts them and waits only for the tile it folds, never for the next tile's loads
+// in flight (a load under a branch makes it wait for everything: vmcnt(0)).  VEC kernels run
+// only when n is a multiple of 4 and the operands are 16-byte aligned.
 template <bool VEC, int EPL>
 __device__ __forceinline__ FwV<EPL> fw_load(const float* p, int64_t i0, int64_t n) {
   FwV<EPL> r;
-  if (VEC && i0 + EPL <= n) {
+  if constexpr (VEC && EPL > 1) {
+    const int64_t q = i0 < n ? i0 : n - EPL;
     if constexpr (EPL == 4) {
-      const float4 v = *reinterpret_cast<const float4*>(p + i0);
+      const float4 v = *reinterpret_cast<const float4*>(p + q);
       r.v[0] = v.x; r.v[1] = v.y; r.v[2] = v.z; r.v[3] = v.w;
-      return r;
-    } else if constexpr (EPL == 2) {
-      const float2 v = *reinterpret_cast<const float2*>(p + i0);
+    } else {
+      const float2 v = *reinterpret_cast<const float2*>(p + q);
       r.v[0] = v.x; r.v[1] = v.y;
-      return r;
     }
+    return r;
   }
 #pragma unroll
-  for (int e = 0; e < EPL; ++e) r.v[e] = i0 + e < n ? p[i0 + e] : 0.0f;
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t q = i0 + e < n ? i0 + e : n - 1;
+    r.v[e] = p[q];
+  }
   return r;
 }
 
-template <bool VEC, int EPL>
+// GUARD: the ragged last tile (elements past n are not stored)
+template <bool VEC, int EPL, bool GUARD>
 __device__ __forceinline__ void fw_store(float* p, int64_t i0, int64_t n, const float (&r)[EPL]) {
-  if (VEC && i0 + EPL <= n) {
+  if (VEC && EPL > 1 && (!GUARD || i0 < n)) {
     if constexpr (EPL == 4) {
       *reinterpret_cast<float4*>(p + i0) = make_float4(r[0], r[1], r[2], r[3]);
       return;
@@ -1102,9 +1115,10 @@ __device__ __forceinline__ void fw_store(float* p, int64_t i0, int64_t n, const 
       return;
     }
   }
+  if (VEC && EPL > 1) return;
 #pragma unroll
   for (int e = 0; e < EPL; ++e)
-    if (i0 + e < n) p[i0 + e] = r[e];
+    if (!GUARD || i0 + e < n) p[i0 + e] = r[e];
 }
 
 // the leading lanes whose index lies below `hi` (a sorted window): 0..64
@@ -1115,6 +1129,8 @@ __device__ __forceinline__ int fw_lead(bool in) {
 
 __device__ __forceinline__ int32_t fw_uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// requires a fresh total (a.first); DENSE: up to FW_DMAX dense payloads (their payload numbers
+// packed 4 bits each in dpk)
 template <bool VEC, int EPL, int NPMAX, bool DENSE>
 __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw, int nd,
                                                         uint32_t dpk) {
@@ -1134,8 +1150,23 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw,
   const int64_t t1 = (t0 + tpw < ntl) ? t0 + tpw : ntl;
   if (t0 >= t1) return;  // no block barrier anywhere: a wave may leave alone
   const int np = a.np;
-  // ---- start cursors: 64-ary lower_bound(idx_p, t0 * TE) of every sparse payload (k < 2^31,
-  // n < 2^31: 32-bit positions) ----
+  // per payload slot: a sparse payload's arrays, or a harmless valid address (local) with k = 0
+  const int32_t* ip[NPMAX];
+  const float* vp[NPMAX];
+  int32_t kk[NPMAX];
+#pragma unroll
+  for (int p = 0; p < NPMAX; ++p) {
+    const bool sp = p < np && a.p[p].idx != nullptr;
+    ip[p] = sp ? a.p[p].idx : reinterpret_cast<const int32_t*>(a.local);
+    vp[p] = sp ? a.p[p].val : a.local;
+    kk[p] = sp ? (int32_t)a.p[p].k : 0;
+  }
+  const float* dp[DENSE ? FW_DMAX : 1];
+  if (DENSE) {
+#pragma unroll
+    for (int d = 0; d < FW_DMAX; ++d) dp[d] = d < nd ? a.p[(dpk >> (4 * d)) & 15u].val : a.local;
+  }
+  // ---- start cursors: 64-ary lower_bound(idx_p, t0 * TE) (k, n < 2^31) ----
   int32_t cur[NPMAX];
   {
     int32_t lo[NPMAX], hi[NPMAX];
@@ -1143,7 +1174,7 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw,
 #pragma unroll
     for (int p = 0; p < NPMAX; ++p) {
       lo[p] = 0;
-      hi[p] = (p < np && a.p[p].idx) ? (int32_t)a.p[p].k : 0;
+      hi[p] = kk[p];
     }
     for (int step = 0; step < 7; ++step) {
       int32_t v[NPMAX], stride[NPMAX];
@@ -1152,7 +1183,9 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw,
         const int32_t len = hi[p] - lo[p];
         stride[p] = len <= 64 ? 1 : (len + 63) / 64;
         const int64_t q = (int64_t)lo[p] + (int64_t)lane * stride[p];
-        v[p] = (len > 0 && q < hi[p]) ? a.p[p].idx[q] : INT32_MAX;
+        const bool ok = len > 0 && q < hi[p];
+        const int32_t x = ip[p][ok ? q : 0];
+        v[p] = ok ? x : INT32_MAX;
       }
       bool more = false;
 #pragma unroll
@@ -1176,82 +1209,69 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw,
 #pragma unroll
     for (int p = 0; p < NPMAX; ++p) cur[p] = lo[p];
   }
-  // ---- one 64-entry window per sparse payload: (idx, val) at cur + lane ----
+  // ---- one 64-entry window per payload slot at cur + lane: branch-free loads of raw values
+  // (lanes past k read entry 0 and are masked when the window is used, at the next tile: a
+  // select here would wait for the load at once) ----
   int32_t wi[NPMAX], wn[NPMAX];
   float wvv[NPMAX], wvn[NPMAX];
   auto load_windows = [&](int32_t (&ix)[NPMAX], float (&vx)[NPMAX]) {
 #pragma unroll
     for (int p = 0; p < NPMAX; ++p) {
-      ix[p] = INT32_MAX;
-      vx[p] = 0.0f;
-      if (p < np && a.p[p].idx) {
-        const int64_t j = (int64_t)cur[p] + lane;
-        if (j < a.p[p].k) {
-          ix[p] = a.p[p].idx[j];
-          vx[p] = a.p[p].val[j];
-        }
-      }
+      const int32_t j = cur[p] + lane;
+      const int32_t jc = j < kk[p] ? j : 0;
+      ix[p] = ip[p][jc];
+      vx[p] = vp[p][jc];
     }
   };
   FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE + lane * EPL, n), Ln;
-  FwV<EPL> O, On;  // a running total continued from out (DPZ_FOLD_ACCUMULATE)
-  if (!a.first) O = fw_load<VEC, EPL>(a.out, t0 * TE + lane * EPL, n);
   FwV<EPL> D[DENSE ? FW_DMAX : 1], Dn[DENSE ? FW_DMAX : 1];
   if (DENSE) {
 #pragma unroll
-    for (int d = 0; d < FW_DMAX; ++d)
-      if (d < nd) D[d] = fw_load<VEC, EPL>(a.p[(dpk >> (4 * d)) & 15u].val, t0 * TE + lane * EPL, n);
+    for (int d = 0; d < FW_DMAX; ++d) D[d] = fw_load<VEC, EPL>(dp[d], t0 * TE + lane * EPL, n);
   }
   load_windows(wi, wvv);
   uint32_t seq = 0;
-  for (int64_t tile = t0; tile < t1; ++tile, ++seq) {
+  auto tile_body = [&](int64_t tile, auto guard) {
+    constexpr bool GUARD = decltype(guard)::value;
     const int64_t tlo = tile * TE, thi = tlo + TE;
     // entries of this tile per payload = the window's leading lanes below thi
     int cnt[NPMAX];
     bool full = false;
 #pragma unroll
-    for (int p = 0; p < NPMAX; ++p) {
-      cnt[p] = fw_lead((int64_t)wi[p] < thi);
+    for (int p = 0; p < NPMAX; ++p) {  // cur[p] is the window's first entry
+      cnt[p] = fw_lead(cur[p] + lane < kk[p] && (int64_t)wi[p] < thi);
       full |= cnt[p] == 64;
     }
     const bool has_next = tile + 1 < t1;
-    // usual case: every cursor advances now and the next tile's windows, local values and dense
-    // values go in flight before this tile folds; a full window (a dense tile) defers that to
-    // after the fold, its payload's further windows read synchronously in its phase
+    // the usual case: every cursor advances now and the next tile's windows and elements go in
+    // flight before this tile folds (unconditionally: clamped addresses past the end); a full
+    // window (a dense tile) reads its payload's further windows in its phase and defers the
+    // next windows to after the fold
     if (!full) {
 #pragma unroll
       for (int p = 0; p < NPMAX; ++p) cur[p] = fw_uni(cur[p] + cnt[p]);
-      if (has_next) load_windows(wn, wvn);
+      load_windows(wn, wvn);
     }
-    if (has_next) {
-      Ln = fw_load<VEC, EPL>(a.local, thi + lane * EPL, n);
-      if (!a.first) On = fw_load<VEC, EPL>(a.out, thi + lane * EPL, n);
-      if (DENSE) {
+    Ln = fw_load<VEC, EPL>(a.local, thi + lane * EPL, n);
+    if (DENSE) {
 #pragma unroll
-        for (int d = 0; d < FW_DMAX; ++d)
-          if (d < nd) Dn[d] = fw_load<VEC, EPL>(a.p[(dpk >> (4 * d)) & 15u].val, thi + lane * EPL, n);
-      }
-    }
-    if (DENSE) {  // this tile's dense values: this lane's own elements, read back by it only
+      for (int d = 0; d < FW_DMAX; ++d) Dn[d] = fw_load<VEC, EPL>(dp[d], thi + lane * EPL, n);
 #pragma unroll
-      for (int d = 0; d < FW_DMAX; ++d)
-        if (d < nd) {
+      for (int d = 0; d < FW_DMAX; ++d)  // this lane's own elements, read back by it only
 #pragma unroll
-          for (int e = 0; e < EPL; ++e) s_dense[wid][d][lane * EPL + e] = D[d].v[e];
-        }
+        for (int e = 0; e < EPL; ++e) s_dense[wid][d][lane * EPL + e] = D[d].v[e];
     }
     float acc[EPL], base[EPL];
 #pragma unroll
     for (int e = 0; e < EPL; ++e) {
       base[e] = a.zero_base ? 0.0f : L.v[e];
-      acc[e] = a.first ? 0.0f : O.v[e];
+      acc[e] = 0.0f;
     }
     int dord = 0;
 #pragma unroll
     for (int p = 0; p < NPMAX; ++p) {
       if (p >= np) break;
       const float w = a.p[p].w;
-      const bool first_term = a.first && p == 0;
       float tv[EPL];
       if (!a.p[p].idx) {  // dense: its own value everywhere
 #pragma unroll
@@ -1266,18 +1286,16 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw,
             wt[pos] = tag;
           }
         }
-        if (full) {
-          // this payload's further entries in the tile (cnt == 64), then its cursor
+        if (full) {  // this payload's further entries in the tile (cnt == 64), then its cursor
           int32_t c = cnt[p];
           if (c == 64) {
             for (int32_t j0 = cur[p] + 64;; j0 += 64) {
-              const int64_t j = (int64_t)j0 + lane;
-              const int32_t iv = j < a.p[p].k ? a.p[p].idx[j] : INT32_MAX;
-              const bool in = (int64_t)iv < thi;
-              const int cc = fw_lead(in);
+              const int32_t j = j0 + lane;
+              const int32_t iv = j < kk[p] ? ip[p][j] : INT32_MAX;
+              const int cc = fw_lead((int64_t)iv < thi);
               const int64_t pos = (int64_t)iv - tlo;
               if (lane < cc && pos >= 0 && pos < TE) {
-                wv[pos] = a.p[p].val[j];
+                wv[pos] = vp[p][j];
                 wt[pos] = tag;
               }
               c += cc;
@@ -1286,48 +1304,61 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw,
           }
           cur[p] = fw_uni(cur[p] + c);
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        // the row is this wave's own and one wave's LDS instructions execute in order, so the
+        // lanes' writes above are seen by the reads below with no wait; the scheduling barriers
+        // only keep the compiler from moving LDS accesses across (no memory fence: a fence
+        // would also wait for the next tile's global loads in flight)
         __builtin_amdgcn_wave_barrier();
+        uint32_t tg[EPL];
+        float hv[EPL];
+        if constexpr (EPL == 4) {
+          const uint4 t4 = *reinterpret_cast<const uint4*>(&wt[lane * 4]);
+          const float4 h4 = *reinterpret_cast<const float4*>(&wv[lane * 4]);
+          tg[0] = t4.x; tg[1] = t4.y; tg[2] = t4.z; tg[3] = t4.w;
+          hv[0] = h4.x; hv[1] = h4.y; hv[2] = h4.z; hv[3] = h4.w;
+        } else {
 #pragma unroll
-        for (int e = 0; e < EPL; ++e) {
-          const int q = lane * EPL + e;
-          tv[e] = wt[q] == tag ? wv[q] : base[e];
+          for (int e = 0; e < EPL; ++e) {
+            tg[e] = wt[lane * EPL + e];
+            hv[e] = wv[lane * EPL + e];
+          }
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) tv[e] = tg[e] == tag ? hv[e] : base[e];
         __builtin_amdgcn_wave_barrier();
       }
 #pragma unroll
       for (int e = 0; e < EPL; ++e) {
         const float term = tv[e] * w;
-        acc[e] = first_term ? (a.zero_base ? 0.0f + term : term) : acc[e] + term;
+        acc[e] = p == 0 ? (a.zero_base ? 0.0f + term : term) : acc[e] + term;
       }
     }
-    if (full) {  // every cursor now final (payloads past np / dense advanced by 0)
-#pragma unroll
-      for (int p = 0; p < NPMAX; ++p)
-        if (p >= np || !a.p[p].idx) cur[p] = fw_uni(cur[p] + cnt[p]);
-      if (has_next) load_windows(wn, wvn);
+    if (full) {  // every cursor is final now (empty slots advance by 0)
+      load_windows(wn, wvn);
     }
     if (a.add_self) {
 #pragma unroll
       for (int e = 0; e < EPL; ++e) acc[e] = acc[e] + L.v[e] * a.w_self;
     }
-    fw_store<VEC, EPL>(a.out, tlo + lane * EPL, n, acc);
-    if (a.out2) fw_store<VEC, EPL>(a.out2, tlo + lane * EPL, n, acc);
-    if (has_next) {
+    fw_store<VEC, EPL, GUARD>(a.out, tlo + lane * EPL, n, acc);
+    if (a.out2) fw_store<VEC, EPL, GUARD>(a.out2, tlo + lane * EPL, n, acc);
+    (void)has_next;
 #pragma unroll
-      for (int p = 0; p < NPMAX; ++p) {
-        wi[p] = wn[p];
-        wvv[p] = wvn[p];
-      }
-      L = Ln;
-      if (!a.first) O = On;
-      if (DENSE) {
-#pragma unroll
-        for (int d = 0; d < FW_DMAX; ++d) D[d] = Dn[d];
-      }
+    for (int p = 0; p < NPMAX; ++p) {
+      wi[p] = wn[p];
+      wvv[p] = wvn[p];
     }
-  }
+    L = Ln;
+    if (DENSE) {
+#pragma unroll
+      for (int d = 0; d < FW_DMAX; ++d) D[d] = Dn[d];
+    }
+    ++seq;
+  };
+  const int64_t tfull = n / TE;  // tiles wholly inside [0, n)
+  const int64_t tf = t1 < tfull ? t1 : (tfull > t0 ? tfull : t0);
+  for (int64_t tile = t0; tile < tf; ++tile) tile_body(tile, std::false_type{});
+  if (tf < t1) tile_body(tf, std::true_type{});  // the global last tile, ragged
 }
 
 // blocks of the persistent fold grid: what the CUs hold at once (occupancy API)
@@ -1403,26 +1434,30 @@ static int launch_walk_t(const FoldArgs& fa, int nd, uint32_t dpk, hipStream_t s
   return DPZ_OK;
 }
 
+// dense payloads only with at most 4 payloads (walk_ok): the 16-payload kernel's registers
 template <bool VEC, int EPL>
 static int launch_walk_e(const FoldArgs& fa, int nd, uint32_t dpk, hipStream_t st) {
   if (fa.np <= 4)
     return nd ? launch_walk_t<VEC, EPL, 4, true>(fa, nd, dpk, st)
               : launch_walk_t<VEC, EPL, 4, false>(fa, nd, dpk, st);
-  return nd ? launch_walk_t<VEC, EPL, 16, true>(fa, nd, dpk, st)
-            : launch_walk_t<VEC, EPL, 16, false>(fa, nd, dpk, st);
+  return launch_walk_t<VEC, EPL, 16, false>(fa, 0, 0u, st);
+}
+
+static bool walk_ok(const FoldArgs& fa, int nd) {
+  return !fa.replace_only && fa.first && fa.np > 0 && (fa.np <= 4 ? nd <= FW_DMAX : nd == 0);
 }
 
 static int launch_walk(const FoldArgs& fa, bool vec, double dens, int nd, uint32_t dpk,
                        hipStream_t st) {
-  const int epl = dens <= 0.125 ? 4 : (dens <= 0.25 ? 2 : 1);
+  // ~32 entries per payload per tile on average at dens <= 0.125 (256-element tiles); denser
+  // payloads take 128-element tiles (~26-51 entries at 0.2-0.4; rare full windows)
+  const int epl = dens <= 0.125 ? 4 : 2;
   if (vec) {
     if (epl == 4) return launch_walk_e<true, 4>(fa, nd, dpk, st);
-    if (epl == 2) return launch_walk_e<true, 2>(fa, nd, dpk, st);
-    return launch_walk_e<true, 1>(fa, nd, dpk, st);
+    return launch_walk_e<true, 2>(fa, nd, dpk, st);
   }
   if (epl == 4) return launch_walk_e<false, 4>(fa, nd, dpk, st);
-  if (epl == 2) return launch_walk_e<false, 2>(fa, nd, dpk, st);
-  return launch_walk_e<false, 1>(fa, nd, dpk, st);
+  return launch_walk_e<false, 2>(fa, nd, dpk, st);
 }
 
 // Replace-only decode of ONE sparse payload (reference PartialModel.py:257-303, T[idx] = params):
@@ -1563,11 +1598,11 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
     const int64_t slots_min =
         getenv("DPZ_FOLD_SLOTS_MIN") ? atoll(getenv("DPZ_FOLD_SLOTS_MIN")) : 600;
     // DPZ_FOLD_KIND=4 forces the walk fold (no offsets pre-pass)
-    if (kind == 4 && !fa.replace_only && nd <= FW_DMAX && fa.np > 0) {
+    if (kind == 4 && walk_ok(fa, nd)) {
       double dens = 0.0;
       for (int i = 0; i < fa.np; ++i)
         if (fa.p[i].idx && (double)fa.p[i].k / (double)n > dens) dens = (double)fa.p[i].k / (double)n;
-      const int rc = launch_walk(fa, vec, dens, nd, dpk, st);
+      const int rc = launch_walk(fa, vec && n % 4 == 0, dens, nd, dpk, st);
       if (rc != DPZ_OK) return rc;
       continue;
     }

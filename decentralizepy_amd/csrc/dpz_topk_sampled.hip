@@ -809,7 +809,14 @@ __device__ __forceinline__ void dense_write(const KeySrc s, int64_t seg, int64_t
 // offsets, and the ordered write of (idx, vals_src[idx]) with counter / rewind updates.  Block 0
 // re-zeroes the sample histogram and publishes T / icut / status.
 constexpr int CSEG = 8;
-template <bool VEC>
+// PLAIN (dense alpha, k > n/32): counter[idx] += 1 as a gathered read + plain store instead of a
+// memory-side atomic.  The selected indices are unique, so no two lanes update one word; a wave
+// instruction of atomics whose 64 lanes hit ~40 different lines runs at ~1/13 of the streaming
+// rate (MI355X_MICROARCH.md, Global float atomics: "64 lanes in 64 different rows"), which made
+// the C3 compact (k = 2.5 M) atomic-bound; scattered plain stores run at the streaming rate, and
+// the gathers are issued while the threshold is being resolved.  At sparse alpha the atomics stay
+// (reading every candidate's counter ahead measured slower at C2).
+template <bool VEC, bool PLAIN>
 __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl,
     uint32_t* chist, const uint32_t* __restrict__ blkabove, const uint32_t* __restrict__ blcnt,
@@ -894,12 +901,19 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   // When the values are not carried from the filter (vals_src != x), every candidate of chunk 0
   // gathers its value now, while the threshold is resolved, not at write time.  (Reading the
   // counter words ahead the same way, for plain-store updates, measured ~1 us SLOWER than the
-  // memory-side atomics at C2: it reads every candidate's line.)
+  // memory-side atomics at C2: it reads every candidate's line; PLAIN does it at dense alpha.)
+  uint32_t cc[2][PFC];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int c = 0; c < PFC; ++c) cc[u][c] = 0u;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int64_t seg = seg0 + u;
-    if (!cval && seg < W && cnt[u] != DENSE && (uint32_t)lane < cnt[u])
-      vv[u][0] = vals_src[ii[u][0]];
+    if (seg < W && cnt[u] != DENSE && (uint32_t)lane < cnt[u]) {
+      if (!cval) vv[u][0] = vals_src[ii[u][0]];
+      if (PLAIN && counter) cc[u][0] = (uint32_t)counter[ii[u][0]];
+    }
   }
   if (t < 64) {
     uint32_t tot;
@@ -975,6 +989,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
       for (int c = 1; c < PFC; ++c) {
         const uint32_t j = c * 64u + lane;
         if (j < cnt[u] && !cval) vv[u][c] = vals_src[ii[u][c]];
+        if (PLAIN && counter && j < cnt[u]) cc[u][c] = (uint32_t)counter[ii[u][c]];
       }
     }
   }
@@ -1010,15 +1025,19 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     const int64_t seg = seg0 + u;
     if (seg >= W) break;
     if (cnt[u] != DENSE) {
-      // pre: the value was read ahead (v valid); otherwise gathered here
-      auto emit = [&](bool sel, uint32_t idx, float v, bool pre) {
+      // pre: the value was read ahead (v valid); otherwise gathered here.  cw: the counter word
+      // read ahead (PLAIN)
+      auto emit = [&](bool sel, uint32_t idx, float v, bool pre, uint32_t cw) {
         const uint64_t m = __ballot(sel);
         if (sel) {
           const uint32_t pos = run + mbcnt64(m);
           if (pos < (uint64_t)k) {
             idx_out[pos] = (int32_t)idx;
             val_out[pos] = (cval || pre) ? v : vals_src[idx];
-            if (counter) atomicAdd(&counter[idx], 1);  // non-returning: no round trip to wait on
+            if (counter) {
+              if (PLAIN) counter[idx] = (int32_t)(cw + 1u);  // unique indices: no race
+              else atomicAdd(&counter[idx], 1);  // non-returning: no round trip to wait on
+            }
             if (rewind) rewind[idx] = 0.0f;
           }
         }
@@ -1028,20 +1047,21 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
       for (int c = 0; c < PFC; ++c) {
         const uint32_t j = c * 64u + lane;
         if (c * 64u < cnt[u])
-          emit(j < cnt[u] && is_sel(kk[u][c], ii[u][c]), ii[u][c], vv[u][c], true);
+          emit(j < cnt[u] && is_sel(kk[u][c], ii[u][c]), ii[u][c], vv[u][c], true, cc[u][c]);
       }
       for (uint32_t j0 = PFC * 64u; j0 < cnt[u]; j0 += 64) {
         const uint32_t j = j0 + lane;
         bool sel = false;
-        uint32_t idx = 0;
+        uint32_t idx = 0, cw = 0;
         float v = 0.f;
         if (j < cnt[u]) {
           const uint32_t key = ckey[seg * CAP + j];
           idx = cidx[seg * CAP + j];
           if (cval) v = cval[seg * CAP + j];
           sel = is_sel(key, idx);
+          if (PLAIN && counter && sel) cw = (uint32_t)counter[idx];
         }
-        emit(sel, idx, v, false);
+        emit(sel, idx, v, false, cw);
       }
     } else {
       dense_write<VEC>(s, seg, R, n, k, lo, T, icut, run, vals_src, idx_out, val_out, counter,
@@ -1128,9 +1148,17 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
       blidx, jb[1]));
   float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE) ? a.acc : nullptr;
   const unsigned ncmp = (unsigned)((g.W + CSEG - 1) / CSEG);
-  DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC><<<ncmp + pb[2], 256, 0, a.st>>>(
-      s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, cidx,
-      ckey, cval, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, a.status_out, jb[2]));
+  // DPZ_COUNTER_PLAIN=0 / 1 forces the counter update form (A/B diagnostics)
+  bool plain = a.k > a.n / 32;
+  if (const char* e = getenv("DPZ_COUNTER_PLAIN")) plain = atoi(e) != 0;
+  if (plain)
+    DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC, true><<<ncmp + pb[2], 256, 0, a.st>>>(
+        s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, cidx,
+        ckey, cval, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, a.status_out, jb[2]));
+  else
+    DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC, false><<<ncmp + pb[2], 256, 0, a.st>>>(
+        s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, cidx,
+        ckey, cval, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, a.status_out, jb[2]));
   return DPZ_OK;
 }
 

@@ -742,3 +742,33 @@ def test_shared_and_lone_filter_grids_agree(dev, n, alpha):
         res.append((idx.cpu(), val.cpu(), cnt.cpu()))
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("plain", ["0", "1"])
+@pytest.mark.parametrize("n,alpha,mode", [(3_000_017, 0.01, otopk.ACC_NONE),
+                                          (3_000_017, 0.1, otopk.ACC_ADD),
+                                          (1_000_003, 0.3, otopk.ACC_ACCUMULATE)])
+def test_counter_update_forms_agree(dev, monkeypatch, plain, n, alpha, mode):
+    """The compact's counter update as memory-side atomics (DPZ_COUNTER_PLAIN=0) and as gathered
+    read + plain store (=1, the dense-alpha default) both give counter[idx] += 1 on a counter
+    that already holds counts, with the accumulator rewound, bit-exact vs the oracle."""
+    monkeypatch.setenv("DPZ_COUNTER_PLAIN", plain)
+    from decentralizepy_amd import codec
+    x, x0 = _inputs(n, seed=n % 89 + int(alpha * 100))
+    rng = np.random.default_rng(3)
+    cnt0 = rng.integers(0, 50, size=n).astype(np.int32)
+    acc = (0.01 * rng.standard_normal(n)).astype(np.float32) if mode != otopk.ACC_NONE else None
+    k = round(alpha * n)
+    o_cnt, o_acc = cnt0.copy(), (acc.copy() if acc is not None else None)
+    oi, ov = otopk.encode(x, x0, o_acc, mode, k, counter=o_cnt)
+    tcnt = torch.from_numpy(cnt0.copy()).to(dev)
+    tacc = torch.from_numpy(acc.copy()).to(dev) if acc is not None else None
+    ws = codec.Workspace(dev)
+    idx, val = codec.topk_encode(torch.from_numpy(x).to(dev), k, x0=torch.from_numpy(x0).to(dev),
+                                 acc=tacc, acc_mode=mode, counter=tcnt, workspace=ws)
+    assert codec.topk_status(ws) == 0
+    np.testing.assert_array_equal(idx.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(val.cpu().numpy()), _bits(ov))
+    np.testing.assert_array_equal(tcnt.cpu().numpy(), o_cnt)
+    if acc is not None:
+        np.testing.assert_array_equal(_bits(tacc.cpu().numpy()), _bits(o_acc))
