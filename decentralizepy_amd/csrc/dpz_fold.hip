@@ -837,215 +837,6 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_group_kernel(FoldArgs a)
   }  // tile loop
 }
 
-// ---- the slot fold: every payload of a group in ONE phase per 1024-element tile -------------
-// For dense groups (JWINS alpha 0.03-0.4 x 16 payloads; a node's 3 neighbours with full-share
-// payloads among them) the hit-chain / phase / 4-slot kernels pay a global round trip per tile
-// (or per payload) for the entries at 2 blocks per CU.  Here the tile is 1024 elements and every
-// payload has its own LDS value slot (np x 4 KB + a 16-bit hit mask per element), so one tile is
-//   scatter (entries already in registers) -> barrier -> issue the NEXT tile's entries, local
-//   values and dense payload values -> fold the 4 elements of this thread over all payloads ->
-//   store -> barrier
-// and every global load of a tile is in flight while the previous tile folds.  Dense payloads
-// (idx == NULL) are loaded per element like local (4 values per thread) and written into their
-// slot; their mask bit is implied.  Order per element: the reference's
-//   t = hit ? value : local;  total = t_0*w_0 (+0 first with a zero base); total += t_p*w_p;
-//   total += w_self * local
-// packed fp32 pairs, no FMA (-ffp-contract=off).
-constexpr int FS_SHIFT = 10;
-constexpr int FS_TILE = 1 << FS_SHIFT;
-constexpr int FS_THREADS = 256;          // 4 elements (one float4) per thread
-constexpr int FS_EPT = 16;               // entries per thread held per round
-constexpr int FS_CAP = FS_EPT * FS_THREADS;
-constexpr int FS_DMAX = 4;               // dense payloads per group on this path
-static_assert(FS_TILE == 4 * FS_THREADS, "one float4 per thread");
-
-static inline int64_t fs_ntiles(int64_t n) { return (n + FS_TILE - 1) / FS_TILE; }
-static inline size_t fs_smem(int np) { return (size_t)np * FS_TILE * 4 + FS_TILE * 2; }
-
-template <bool VEC, bool DENSE>
-__global__ void __launch_bounds__(FS_THREADS) fold_slots_kernel(FoldArgs a, int64_t nt,
-                                                                int nd, uint32_t dpk) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char fs_smem_[];
-  float* hv = reinterpret_cast<float*>(fs_smem_);                           // [np][FS_TILE]
-  uint32_t* hm = reinterpret_cast<uint32_t*>(fs_smem_ + (size_t)a.np * FS_TILE * 4);  // masks
-  __shared__ int32_t s_pre[2][FOLD_MAXP + 1];  // tile entry prefix, double-buffered
-  __shared__ int32_t s_rng[2][FOLD_MAXP];      // first entry of the tile per payload
-  __shared__ const int32_t* s_idx[FOLD_MAXP];
-  __shared__ const float* s_val[FOLD_MAXP];
-  const int t = threadIdx.x;
-  const int np = a.np;
-  if (t < np) {
-    s_idx[t] = a.p[t].idx;
-    s_val[t] = a.p[t].val;
-  }
-  hm[2 * t] = 0;
-  hm[2 * t + 1] = 0;
-  const int32_t* starts = a.starts;
-  // thread p < np: the entry range of payload p over a tile (dense payloads: empty)
-  auto range_of = [&](int64_t tl, int32_t& r0, int32_t& r1) {
-    r0 = r1 = 0;
-    if (t < np && tl < nt && a.p[t].idx) {
-      const int32_t* sp = starts + (int64_t)t * (nt + 1);
-      r0 = sp[tl];
-      r1 = sp[tl + 1];
-    }
-  };
-  // wave 0 turns the per-payload ranges into the prefix of the flattened entry list
-  auto publish = [&](int buf, int32_t r0, int32_t r1) {
-    if (t < 64) {
-      const int32_t c = (t < np && r1 > r0) ? r1 - r0 : 0;
-      int32_t incl = c;
-#pragma unroll
-      for (int d = 1; d < FOLD_MAXP; d <<= 1) {
-        const int32_t v = __shfl_up(incl, d, 64);
-        if (t >= d) incl += v;
-      }
-      if (t < FOLD_MAXP) {
-        s_pre[buf][t + 1] = incl;
-        s_rng[buf][t] = r0;
-      }
-      if (t == 0) s_pre[buf][0] = 0;
-    }
-  };
-  // entries [j0, j0 + FS_CAP) of a tile's flattened list: (position | payload << 16) or ~0
-  uint32_t ei[FS_EPT];
-  float ev[FS_EPT];
-  auto load_entries = [&](int buf, int64_t tlo, int32_t j0) {
-    const int32_t tot = s_pre[buf][np];
-#pragma unroll
-    for (int u = 0; u < FS_EPT; ++u) {
-      const int32_t j = j0 + t + u * FS_THREADS;
-      ei[u] = ~0u;
-      ev[u] = 0.0f;
-      if (j < tot) {
-        int p = 0;
-#pragma unroll
-        for (int sb = FOLD_MAXP / 2; sb >= 1; sb >>= 1) p += s_pre[buf][p + sb] <= j ? sb : 0;
-        const int32_t src = s_rng[buf][p] + (j - s_pre[buf][p]);
-        const int64_t pos = (int64_t)s_idx[p][src] - tlo;
-        ev[u] = s_val[p][src];
-        // an invalid payload (unsorted / out of range) is dropped, never written out of bounds
-        ei[u] = (pos >= 0 && pos < FS_TILE) ? ((uint32_t)pos | ((uint32_t)p << 16)) : ~0u;
-      }
-    }
-  };
-  float4 L, Ln;
-  float4 dv[DENSE ? FS_DMAX : 1], dn[DENSE ? FS_DMAX : 1];
-  auto load_elems = [&](int64_t tl, float4& l4, float4 (&d4)[DENSE ? FS_DMAX : 1]) {
-    const int64_t i0 = tl * FS_TILE + 4 * t;
-    auto ld = [&](const float* src) {
-      if (VEC && i0 + 3 < a.n) return *reinterpret_cast<const float4*>(src + i0);
-      float e[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) e[q] = i0 + q < a.n ? src[i0 + q] : 0.0f;
-      return make_float4(e[0], e[1], e[2], e[3]);
-    };
-    if (tl >= nt) return;
-    l4 = ld(a.local);
-    if (DENSE) {
-#pragma unroll
-      for (int d = 0; d < FS_DMAX; ++d)
-        if (d < nd) d4[d] = ld(a.p[(dpk >> (4 * d)) & 15u].val);
-    }
-  };
-  // prologue: ranges of the first two tiles, the first tile's entries and elements
-  int64_t tile = blockIdx.x;
-  int32_t r0, r1;
-  range_of(tile, r0, r1);
-  publish(0, r0, r1);
-  range_of(tile + gridDim.x, r0, r1);  // held for the next tile's publish
-  __syncthreads();
-  load_entries(0, tile * FS_TILE, 0);
-  load_elems(tile, L, dv);
-  int buf = 0;
-  typedef float f2v __attribute__((ext_vector_type(2)));
-  for (; tile < nt; tile += gridDim.x) {
-    const int64_t tlo = tile * FS_TILE;
-    // scatter this tile's entries (the first FS_CAP; the rest in extra rounds, synchronously)
-    const int32_t tot = s_pre[buf][np];
-    for (int32_t j0 = 0;;) {
-#pragma unroll
-      for (int u = 0; u < FS_EPT; ++u) {
-        if (ei[u] != ~0u) {
-          const uint32_t pos = ei[u] & 0xFFFFu, p = ei[u] >> 16;
-          hv[p * FS_TILE + pos] = ev[u];
-          atomicOr(&hm[pos >> 1], (1u << p) << (16u * (pos & 1u)));
-        }
-      }
-      j0 += FS_CAP;
-      if (j0 >= tot) break;
-      load_entries(buf, tlo, j0);
-    }
-    if (DENSE) {
-#pragma unroll
-      for (int d = 0; d < FS_DMAX; ++d)
-        if (d < nd)
-          *reinterpret_cast<float4*>(&hv[((dpk >> (4 * d)) & 15u) * FS_TILE + 4 * t]) = dv[d];
-    }
-    // the next tile's prefix (its ranges were loaded one tile ago)
-    publish(buf ^ 1, r0, r1);
-    __syncthreads();  // B1: slots, masks and the next prefix visible
-    const int64_t nx = tile + gridDim.x;
-    range_of(nx + gridDim.x, r0, r1);  // two tiles ahead
-    if (nx < nt) {
-      load_entries(buf ^ 1, nx * FS_TILE, 0);
-      load_elems(nx, Ln, dn);
-    }
-    // fold this thread's 4 elements over every payload
-    const uint2 mw = *reinterpret_cast<const uint2*>(&hm[2 * t]);
-    *reinterpret_cast<uint2*>(&hm[2 * t]) = make_uint2(0u, 0u);
-    const uint32_t dm = a.dense_mask;
-    const uint32_t m0 = (mw.x & 0xFFFFu) | dm, m1 = (mw.x >> 16) | dm;
-    const uint32_t m2 = (mw.y & 0xFFFFu) | dm, m3 = (mw.y >> 16) | dm;
-    const f2v base01 = a.zero_base ? f2v{0.0f, 0.0f} : f2v{L.x, L.y};
-    const f2v base23 = a.zero_base ? f2v{0.0f, 0.0f} : f2v{L.z, L.w};
-    f2v acc01 = {0.0f, 0.0f}, acc23 = {0.0f, 0.0f};
-#pragma unroll
-    for (int p = 0; p < FOLD_MAXP; ++p) {
-      if (p >= np) break;
-      const float w = a.p[p].w;
-      const f2v w2 = {w, w};
-      const float4 h4 = *reinterpret_cast<const float4*>(&hv[p * FS_TILE + 4 * t]);
-      const f2v t01 = {((m0 >> p) & 1u) ? h4.x : base01.x, ((m1 >> p) & 1u) ? h4.y : base01.y};
-      const f2v t23 = {((m2 >> p) & 1u) ? h4.z : base23.x, ((m3 >> p) & 1u) ? h4.w : base23.y};
-      if (p == 0) {
-        const f2v z = {0.0f, 0.0f};
-        acc01 = a.zero_base ? z + t01 * w2 : t01 * w2;
-        acc23 = a.zero_base ? z + t23 * w2 : t23 * w2;
-      } else {
-        acc01 = acc01 + t01 * w2;
-        acc23 = acc23 + t23 * w2;
-      }
-    }
-    float r[4] = {acc01.x, acc01.y, acc23.x, acc23.y};
-    if (a.add_self) {
-      const float lv[4] = {L.x, L.y, L.z, L.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) r[e] = r[e] + lv[e] * a.w_self;
-    }
-    const int64_t i0 = tlo + 4 * t;
-    if (VEC && i0 + 3 < a.n) {
-      const float4 r4 = make_float4(r[0], r[1], r[2], r[3]);
-      *reinterpret_cast<float4*>(a.out + i0) = r4;
-      if (a.out2) *reinterpret_cast<float4*>(a.out2 + i0) = r4;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (i0 + e < a.n) {
-          a.out[i0 + e] = r[e];
-          if (a.out2) a.out2[i0 + e] = r[e];
-        }
-    }
-    L = Ln;
-    if (DENSE) {
-#pragma unroll
-      for (int d = 0; d < FS_DMAX; ++d) dv[d] = dn[d];
-    }
-    buf ^= 1;
-    __syncthreads();  // B2: every fold read of the slots / masks / prefix is done
-  }
-}
-
 // ---- the walk fold: one wave per contiguous element range, payload cursors, no barriers -----
 // Every other fold kernel needs the tile-offsets pre-pass (fold_offsets_kernel reads every
 // payload index once more: 35-100 us of 25 M x 16 payloads at JWINS alphas) and block barriers
@@ -1129,15 +920,19 @@ __device__ __forceinline__ int fw_lead(bool in) {
 
 __device__ __forceinline__ int32_t fw_uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// requires a fresh total (a.first); DENSE: up to FW_DMAX dense payloads (their payload numbers
-// packed 4 bits each in dpk)
-template <bool VEC, int EPL, int NPMAX, bool DENSE>
-__global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw, int nd,
-                                                        uint32_t dpk) {
+constexpr int FW_G = 4;  // payloads per group: the windows of one group are in registers
+
+// Sparse payloads only (dense ones take the classic kernels), a fresh total (a.first),
+// n < 2^31 - 1024 (walk_ok).  The payloads are walked in groups of FW_G: the windows of the
+// group being folded and of the next group (of this tile, or group 0 of the next tile) are in
+// registers, so every window load is in flight while the group before it folds, with 16
+// registers of windows whatever the payload count.  Cursors live one per lane (lane p: payload
+// p) in one register.
+template <bool VEC, int EPL>
+__global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw) {
   constexpr int TE = 64 * EPL;
   __shared__ float s_val[FW_WAVES][TE];
   __shared__ uint32_t s_tag[FW_WAVES][TE];
-  __shared__ float s_dense[DENSE ? FW_WAVES : 1][DENSE ? FW_DMAX : 1][DENSE ? TE : 1];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float* wv = s_val[wid];
   uint32_t* wt = s_tag[wid];
@@ -1150,167 +945,120 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw,
   const int64_t t1 = (t0 + tpw < ntl) ? t0 + tpw : ntl;
   if (t0 >= t1) return;  // no block barrier anywhere: a wave may leave alone
   const int np = a.np;
-  // per payload slot: a sparse payload's arrays, or a harmless valid address (local) with k = 0
-  const int32_t* ip[NPMAX];
-  const float* vp[NPMAX];
-  int32_t kk[NPMAX];
-#pragma unroll
-  for (int p = 0; p < NPMAX; ++p) {
-    const bool sp = p < np && a.p[p].idx != nullptr;
-    ip[p] = sp ? a.p[p].idx : reinterpret_cast<const int32_t*>(a.local);
-    vp[p] = sp ? a.p[p].val : a.local;
-    kk[p] = sp ? (int32_t)a.p[p].k : 0;
-  }
-  const float* dp[DENSE ? FW_DMAX : 1];
-  if (DENSE) {
-#pragma unroll
-    for (int d = 0; d < FW_DMAX; ++d) dp[d] = d < nd ? a.p[(dpk >> (4 * d)) & 15u].val : a.local;
-  }
-  // ---- start cursors: 64-ary lower_bound(idx_p, t0 * TE) (k, n < 2^31) ----
-  int32_t cur[NPMAX];
+  const int ng = (np + FW_G - 1) / FW_G;
+  // lane p < np: payload p's entry count, its cursor (the next window's first entry)
+  const int32_t kl = lane < np ? (int32_t)a.p[lane < FOLD_MAXP ? lane : 0].k : 0;
+  // ---- start cursors: 64-ary lower_bound(idx_p, t0 * TE), payload by payload ----
+  int32_t curv = 0;
   {
-    int32_t lo[NPMAX], hi[NPMAX];
     const int32_t e0 = (int32_t)(t0 * TE);
-#pragma unroll
-    for (int p = 0; p < NPMAX; ++p) {
-      lo[p] = 0;
-      hi[p] = kk[p];
-    }
-    for (int step = 0; step < 7; ++step) {
-      int32_t v[NPMAX], stride[NPMAX];
-#pragma unroll
-      for (int p = 0; p < NPMAX; ++p) {  // every payload's probes in flight together
-        const int32_t len = hi[p] - lo[p];
-        stride[p] = len <= 64 ? 1 : (len + 63) / 64;
-        const int64_t q = (int64_t)lo[p] + (int64_t)lane * stride[p];
-        const bool ok = len > 0 && q < hi[p];
-        const int32_t x = ip[p][ok ? q : 0];
-        v[p] = ok ? x : INT32_MAX;
-      }
-      bool more = false;
-#pragma unroll
-      for (int p = 0; p < NPMAX; ++p) {
-        const int32_t len = hi[p] - lo[p];
-        if (len <= 0) continue;
-        const int32_t c = (int32_t)__popcll(__ballot(v[p] < e0));  // probes below e0: a prefix
-        if (stride[p] == 1) {
-          lo[p] = fw_uni(lo[p] + c);
-          hi[p] = lo[p];
-        } else {
-          const int32_t nlo = c > 0 ? lo[p] + (c - 1) * stride[p] + 1 : lo[p];
-          const int64_t nhi = (int64_t)lo[p] + (int64_t)c * stride[p];
-          lo[p] = fw_uni(nlo);
-          hi[p] = fw_uni(nhi < hi[p] ? (int32_t)nhi : hi[p]);
-          more = true;
+    for (int p = 0; p < np; ++p) {
+      const int32_t* ip = a.p[p].idx;
+      int32_t lo = 0, hi = fw_uni(__builtin_amdgcn_readlane(kl, p));
+      while (hi > lo) {
+        const int32_t len = hi - lo;
+        const int32_t stride = len <= 64 ? 1 : (len + 63) / 64;
+        const int64_t q = (int64_t)lo + (int64_t)lane * stride;
+        const bool ok = q < hi;
+        const int32_t x = ip[ok ? q : lo];
+        const int32_t c = (int32_t)__popcll(__ballot(ok && x < e0));  // a prefix
+        if (stride == 1) {
+          lo += c;
+          break;
         }
+        const int32_t nlo = c > 0 ? lo + (c - 1) * stride + 1 : lo;
+        const int64_t nhi = (int64_t)lo + (int64_t)c * stride;
+        hi = nhi < hi ? (int32_t)nhi : hi;
+        lo = nlo;
       }
-      if (!more) break;
+      curv = lane == p ? lo : curv;
     }
-#pragma unroll
-    for (int p = 0; p < NPMAX; ++p) cur[p] = lo[p];
   }
-  // ---- one 64-entry window per payload slot at cur + lane: branch-free loads of raw values
-  // (lanes past k read entry 0 and are masked when the window is used, at the next tile: a
-  // select here would wait for the load at once) ----
-  int32_t wi[NPMAX], wn[NPMAX];
-  float wvv[NPMAX], wvn[NPMAX];
-  auto load_windows = [&](int32_t (&ix)[NPMAX], float (&vx)[NPMAX]) {
+  auto cur_of = [&](int p) { return fw_uni(__builtin_amdgcn_readlane(curv, p)); };
+  // ---- the windows of one group: (idx, val) at cur + lane, branch-free loads of raw values
+  // (lanes past k read entry 0 and are masked when the window is used) ----
+  int32_t wi[FW_G], wn[FW_G];
+  float wvv[FW_G], wvn[FW_G];
+  auto load_group = [&](int g, int32_t (&ix)[FW_G], float (&vx)[FW_G]) {
 #pragma unroll
-    for (int p = 0; p < NPMAX; ++p) {
-      const int32_t j = cur[p] + lane;
-      const int32_t jc = j < kk[p] ? j : 0;
-      ix[p] = ip[p][jc];
-      vx[p] = vp[p][jc];
+    for (int q = 0; q < FW_G; ++q) {
+      const int p = g * FW_G + q;
+      const bool live = p < np;
+      const int pc = live ? p : 0;
+      const int32_t j = (live ? cur_of(pc) : 0) + lane;
+      const int32_t k = live ? (int32_t)a.p[pc].k : 0;
+      const int32_t jc = j < k ? j : 0;
+      ix[q] = a.p[pc].idx[jc];
+      vx[q] = a.p[pc].val[jc];
     }
   };
   FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE + lane * EPL, n), Ln;
-  FwV<EPL> D[DENSE ? FW_DMAX : 1], Dn[DENSE ? FW_DMAX : 1];
-  if (DENSE) {
-#pragma unroll
-    for (int d = 0; d < FW_DMAX; ++d) D[d] = fw_load<VEC, EPL>(dp[d], t0 * TE + lane * EPL, n);
-  }
-  load_windows(wi, wvv);
+  load_group(0, wi, wvv);
   uint32_t seq = 0;
   auto tile_body = [&](int64_t tile, auto guard) {
     constexpr bool GUARD = decltype(guard)::value;
-    const int64_t tlo = tile * TE, thi = tlo + TE;
-    // entries of this tile per payload = the window's leading lanes below thi
-    int cnt[NPMAX];
-    bool full = false;
-#pragma unroll
-    for (int p = 0; p < NPMAX; ++p) {  // cur[p] is the window's first entry
-      cnt[p] = fw_lead(cur[p] + lane < kk[p] && (int64_t)wi[p] < thi);
-      full |= cnt[p] == 64;
-    }
-    const bool has_next = tile + 1 < t1;
-    // the usual case: every cursor advances now and the next tile's windows and elements go in
-    // flight before this tile folds (unconditionally: clamped addresses past the end); a full
-    // window (a dense tile) reads its payload's further windows in its phase and defers the
-    // next windows to after the fold
-    if (!full) {
-#pragma unroll
-      for (int p = 0; p < NPMAX; ++p) cur[p] = fw_uni(cur[p] + cnt[p]);
-      load_windows(wn, wvn);
-    }
-    Ln = fw_load<VEC, EPL>(a.local, thi + lane * EPL, n);
-    if (DENSE) {
-#pragma unroll
-      for (int d = 0; d < FW_DMAX; ++d) Dn[d] = fw_load<VEC, EPL>(dp[d], thi + lane * EPL, n);
-#pragma unroll
-      for (int d = 0; d < FW_DMAX; ++d)  // this lane's own elements, read back by it only
-#pragma unroll
-        for (int e = 0; e < EPL; ++e) s_dense[wid][d][lane * EPL + e] = D[d].v[e];
-    }
+    const int64_t tlo = tile * TE;
+    const int32_t tlo32 = (int32_t)tlo, thi32 = tlo32 + TE;
+    Ln = fw_load<VEC, EPL>(a.local, tlo + TE + lane * EPL, n);  // clamped past the end
     float acc[EPL], base[EPL];
 #pragma unroll
     for (int e = 0; e < EPL; ++e) {
       base[e] = a.zero_base ? 0.0f : L.v[e];
       acc[e] = 0.0f;
     }
-    int dord = 0;
+    for (int g = 0; g < ng; ++g) {
+      // this group's window starts; the entries of the tile are the leading lanes below thi
+      int32_t c0[FW_G], cnt[FW_G];
 #pragma unroll
-    for (int p = 0; p < NPMAX; ++p) {
-      if (p >= np) break;
-      const float w = a.p[p].w;
-      float tv[EPL];
-      if (!a.p[p].idx) {  // dense: its own value everywhere
+      for (int q = 0; q < FW_G; ++q) {
+        const int p = g * FW_G + q;
+        const bool live = p < np;
+        c0[q] = live ? cur_of(p) : 0;
+        const int32_t k = live ? (int32_t)a.p[p].k : 0;
+        cnt[q] = fw_lead(c0[q] + lane < k && wi[q] < thi32);
+        // the next tile's window start of this payload (a full window is finished in its phase)
+        if (live) curv = lane == p ? c0[q] + cnt[q] : curv;
+      }
+      // the next group's windows (this tile's next group, or group 0 of the next tile)
+      load_group(g + 1 < ng ? g + 1 : 0, wn, wvn);
 #pragma unroll
-        for (int e = 0; e < EPL; ++e) tv[e] = DENSE ? s_dense[wid][dord][lane * EPL + e] : base[e];
-        ++dord;
-      } else {
+      for (int q = 0; q < FW_G; ++q) {
+        const int p = g * FW_G + q;
+        if (p >= np) break;
+        const float w = a.p[p].w;
         const uint32_t tag = (seq << 4) | (uint32_t)p;
         {
-          const int64_t pos = (int64_t)wi[p] - tlo;
-          if (lane < cnt[p] && pos >= 0 && pos < TE) {
-            wv[pos] = wvv[p];
+          const uint32_t pos = (uint32_t)(wi[q] - tlo32);  // < TE: inside the tile
+          if (lane < cnt[q] && pos < (uint32_t)TE) {
+            wv[pos] = wvv[q];
             wt[pos] = tag;
           }
         }
-        if (full) {  // this payload's further entries in the tile (cnt == 64), then its cursor
-          int32_t c = cnt[p];
-          if (c == 64) {
-            for (int32_t j0 = cur[p] + 64;; j0 += 64) {
-              const int32_t j = j0 + lane;
-              const int32_t iv = j < kk[p] ? ip[p][j] : INT32_MAX;
-              const int cc = fw_lead((int64_t)iv < thi);
-              const int64_t pos = (int64_t)iv - tlo;
-              if (lane < cc && pos >= 0 && pos < TE) {
-                wv[pos] = vp[p][j];
-                wt[pos] = tag;
-              }
-              c += cc;
-              if (cc < 64) break;
+        if (cnt[q] == 64) {  // a dense tile: this payload's further windows, synchronously
+          const int32_t k = (int32_t)a.p[p].k;
+          int32_t c = 64;
+          for (int32_t j0 = c0[q] + 64;; j0 += 64) {
+            const int32_t j = j0 + lane;
+            const int32_t iv = j < k ? a.p[p].idx[j] : INT32_MAX;
+            const int cc = fw_lead(iv < thi32);
+            const uint32_t pos = (uint32_t)(iv - tlo32);
+            if (lane < cc && pos < (uint32_t)TE) {
+              wv[pos] = a.p[p].val[j];
+              wt[pos] = tag;
             }
+            c += cc;
+            if (cc < 64) break;
           }
-          cur[p] = fw_uni(cur[p] + c);
+          curv = lane == p ? c0[q] + c : curv;
+          if (ng == 1) load_group(0, wn, wvn);  // the next tile's window of this group moved
         }
         // the row is this wave's own and one wave's LDS instructions execute in order, so the
         // lanes' writes above are seen by the reads below with no wait; the scheduling barriers
         // only keep the compiler from moving LDS accesses across (no memory fence: a fence
-        // would also wait for the next tile's global loads in flight)
+        // would also wait for the next windows in flight)
         __builtin_amdgcn_wave_barrier();
         uint32_t tg[EPL];
-        float hv[EPL];
+        float hv[EPL], tv[EPL];
         if constexpr (EPL == 4) {
           const uint4 t4 = *reinterpret_cast<const uint4*>(&wt[lane * 4]);
           const float4 h4 = *reinterpret_cast<const float4*>(&wv[lane * 4]);
@@ -1323,18 +1071,19 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw,
             hv[e] = wv[lane * EPL + e];
           }
         }
-#pragma unroll
-        for (int e = 0; e < EPL; ++e) tv[e] = tg[e] == tag ? hv[e] : base[e];
         __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+          tv[e] = tg[e] == tag ? hv[e] : base[e];
+          const float term = tv[e] * w;
+          acc[e] = p == 0 ? (a.zero_base ? 0.0f + term : term) : acc[e] + term;
+        }
       }
 #pragma unroll
-      for (int e = 0; e < EPL; ++e) {
-        const float term = tv[e] * w;
-        acc[e] = p == 0 ? (a.zero_base ? 0.0f + term : term) : acc[e] + term;
+      for (int q = 0; q < FW_G; ++q) {
+        wi[q] = wn[q];
+        wvv[q] = wvn[q];
       }
-    }
-    if (full) {  // every cursor is final now (empty slots advance by 0)
-      load_windows(wn, wvn);
     }
     if (a.add_self) {
 #pragma unroll
@@ -1342,17 +1091,7 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw,
     }
     fw_store<VEC, EPL, GUARD>(a.out, tlo + lane * EPL, n, acc);
     if (a.out2) fw_store<VEC, EPL, GUARD>(a.out2, tlo + lane * EPL, n, acc);
-    (void)has_next;
-#pragma unroll
-    for (int p = 0; p < NPMAX; ++p) {
-      wi[p] = wn[p];
-      wvv[p] = wvn[p];
-    }
     L = Ln;
-    if (DENSE) {
-#pragma unroll
-      for (int d = 0; d < FW_DMAX; ++d) D[d] = Dn[d];
-    }
     ++seq;
   };
   const int64_t tfull = n / TE;  // tiles wholly inside [0, n)
@@ -1386,41 +1125,19 @@ static unsigned fold_grid(int64_t ntiles, bool group = false) {
 
 static inline int64_t fold_ntiles(int64_t n) { return (n + FOLD_TILE - 1) / FOLD_TILE; }
 
-// blocks of the slot fold: what the CUs hold at once with np slots of dynamic LDS
-template <bool VEC, bool DENSE>
-static unsigned fs_grid(int64_t nt, int np) {
-  static int per_np[FOLD_MAXP + 1] = {};
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-  }
-  int& per = per_np[np];
-  if (per == 0) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fold_slots_kernel<VEC, DENSE>,
-                                                     FS_THREADS, fs_smem(np)) != hipSuccess ||
-        per < 1)
-      per = 1;
-  }
-  const int64_t g = (int64_t)cus * per;
-  return (unsigned)(nt < g ? (nt > 0 ? nt : 1) : g);
-}
-
-// The walk fold's launch: EPL from the densest sparse payload (~32 entries per payload per
-// tile on average), NPMAX 4 or 16, dense payloads staged per wave; a persistent grid of what
-// the CUs hold, each wave a contiguous run of tiles.
-template <bool VEC, int EPL, int NPMAX, bool DENSE>
-static int launch_walk_t(const FoldArgs& fa, int nd, uint32_t dpk, hipStream_t st) {
+// The walk fold's launch: EPL from the densest payload (~32 entries per payload per tile on
+// average at dens <= 0.125: 256-element tiles; denser payloads 128-element tiles); a
+// persistent grid of what the CUs hold, each wave a contiguous run of tiles.
+template <bool VEC, int EPL>
+static int launch_walk_t(const FoldArgs& fa, hipStream_t st) {
   static int per = 0, cus = 0;
   if (per == 0) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fold_walk_kernel<VEC, EPL, NPMAX, DENSE>,
-                                                     256, 0) != hipSuccess || per < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fold_walk_kernel<VEC, EPL>, 256, 0) !=
+            hipSuccess || per < 1)
       per = 1;
   }
   constexpr int TE = 64 * EPL;
@@ -1430,34 +1147,19 @@ static int launch_walk_t(const FoldArgs& fa, int nd, uint32_t dpk, hipStream_t s
   if (blocks > need) blocks = need;
   if (blocks < 1) blocks = 1;
   const int64_t tpw = (ntl + blocks * FW_WAVES - 1) / (blocks * FW_WAVES);
-  DPZ_TIMED(DPZ_KT_FOLD, st, fold_walk_kernel<VEC, EPL, NPMAX, DENSE><<<(unsigned)blocks, 256, 0, st>>>(fa, tpw, nd, dpk));
+  DPZ_TIMED(DPZ_KT_FOLD, st, fold_walk_kernel<VEC, EPL><<<(unsigned)blocks, 256, 0, st>>>(fa, tpw));
   return DPZ_OK;
 }
 
-// dense payloads only with at most 4 payloads (walk_ok): the 16-payload kernel's registers
-template <bool VEC, int EPL>
-static int launch_walk_e(const FoldArgs& fa, int nd, uint32_t dpk, hipStream_t st) {
-  if (fa.np <= 4)
-    return nd ? launch_walk_t<VEC, EPL, 4, true>(fa, nd, dpk, st)
-              : launch_walk_t<VEC, EPL, 4, false>(fa, nd, dpk, st);
-  return launch_walk_t<VEC, EPL, 16, false>(fa, 0, 0u, st);
+static bool walk_ok(const FoldArgs& fa) {
+  return !fa.replace_only && fa.first && fa.all_sparse && fa.np > 0 &&
+         fa.n < (int64_t(1) << 31) - 1024;
 }
 
-static bool walk_ok(const FoldArgs& fa, int nd) {
-  return !fa.replace_only && fa.first && fa.np > 0 && (fa.np <= 4 ? nd <= FW_DMAX : nd == 0);
-}
-
-static int launch_walk(const FoldArgs& fa, bool vec, double dens, int nd, uint32_t dpk,
-                       hipStream_t st) {
-  // ~32 entries per payload per tile on average at dens <= 0.125 (256-element tiles); denser
-  // payloads take 128-element tiles (~26-51 entries at 0.2-0.4; rare full windows)
+static int launch_walk(const FoldArgs& fa, bool vec, double dens, hipStream_t st) {
   const int epl = dens <= 0.125 ? 4 : 2;
-  if (vec) {
-    if (epl == 4) return launch_walk_e<true, 4>(fa, nd, dpk, st);
-    return launch_walk_e<true, 2>(fa, nd, dpk, st);
-  }
-  if (epl == 4) return launch_walk_e<false, 4>(fa, nd, dpk, st);
-  return launch_walk_e<false, 2>(fa, nd, dpk, st);
+  if (vec) return epl == 4 ? launch_walk_t<true, 4>(fa, st) : launch_walk_t<true, 2>(fa, st);
+  return epl == 4 ? launch_walk_t<false, 4>(fa, st) : launch_walk_t<false, 2>(fa, st);
 }
 
 // Replace-only decode of ONE sparse payload (reference PartialModel.py:257-303, T[idx] = params):
@@ -1490,8 +1192,7 @@ extern "C" int dpz_debug_fold_stamps(unsigned long long* host_out, int reset) {
 
 extern "C" size_t dpz_decode_workspace_bytes(int64_t n, int n_payloads) {
   const int64_t np = n_payloads < FOLD_MAXP ? (n_payloads > 0 ? n_payloads : 1) : FOLD_MAXP;
-  // tile starts at the slot fold's 1024-element granularity (the coarser 4096 fit inside)
-  return (size_t)np * (size_t)(fs_ntiles(n > 0 ? n : 1) + 1) * sizeof(int32_t);
+  return (size_t)np * (size_t)(fold_ntiles(n > 0 ? n : 1) + 1) * sizeof(int32_t);
 }
 
 extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
@@ -1579,51 +1280,24 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
         fa.all_sparse = 0;
         fa.dense_mask |= 1u << i;
       }
-    // The slot fold (fold_slots_kernel) takes dense-alpha groups: entries per 4096 elements on
-    // average >= DPZ_FOLD_SLOTS_MIN (default below), at most FS_DMAX dense payloads, a fresh
-    // total.  DPZ_FOLD_KIND=1 / 2 / 3 forces the classic / 4-slot group / slot fold (A/B
-    // diagnostics; a forced kind that cannot take the group falls back to the classic kernel).
+    // The walk fold (no offsets pre-pass) takes all-sparse groups of a fresh total where it
+    // measured faster on MI355X (M = 25 M, tools/diag/fold_kinds.py): a node's few neighbours
+    // at any alpha, many payloads at dense alpha.  DPZ_FOLD_KIND=1 / 2 / 4 forces the classic /
+    // 4-slot group / walk fold (A/B diagnostics; a forced kind that cannot take the group runs
+    // the classic kernel).
     int64_t etot = 0;
-    int nd = 0;
-    uint32_t dpk = 0;
-    for (int i = 0; i < fa.np; ++i) {
+    double dens = 0.0;
+    for (int i = 0; i < fa.np; ++i)
       if (fa.p[i].idx) {
         etot += fa.p[i].k;
-      } else {
-        if (nd < FS_DMAX) dpk |= (uint32_t)i << (4 * nd);
-        ++nd;
+        if ((double)fa.p[i].k / (double)n > dens) dens = (double)fa.p[i].k / (double)n;
       }
-    }
     const int kind = getenv("DPZ_FOLD_KIND") ? atoi(getenv("DPZ_FOLD_KIND")) : 0;
-    const int64_t slots_min =
-        getenv("DPZ_FOLD_SLOTS_MIN") ? atoll(getenv("DPZ_FOLD_SLOTS_MIN")) : 600;
-    // DPZ_FOLD_KIND=4 forces the walk fold (no offsets pre-pass)
-    if (kind == 4 && walk_ok(fa, nd)) {
-      double dens = 0.0;
-      for (int i = 0; i < fa.np; ++i)
-        if (fa.p[i].idx && (double)fa.p[i].k / (double)n > dens) dens = (double)fa.p[i].k / (double)n;
-      const int rc = launch_walk(fa, vec && n % 4 == 0, dens, nd, dpk, st);
+    bool use_walk = walk_ok(fa) && (fa.np <= 4 || (double)etot / (double)fa.np >= 0.05 * (double)n);
+    if (kind) use_walk = walk_ok(fa) && kind == 4;
+    if (use_walk) {
+      const int rc = launch_walk(fa, vec && n % 4 == 0, dens, st);
       if (rc != DPZ_OK) return rc;
-      continue;
-    }
-    const bool slots_ok = !fa.replace_only && fa.first && nd <= FS_DMAX && fa.np > 0;
-    bool use_slots = slots_ok && (etot + (int64_t)nd * n > slots_min * ntiles);
-    if (kind) use_slots = slots_ok && kind == 3;
-    if (use_slots) {
-      const int64_t nt = fs_ntiles(n);
-      fa.starts = starts;
-      if (kmax >= 0) {
-        dim3 og((unsigned)((kmax + 1 + 1023) / 1024), (unsigned)fa.np);
-        DPZ_TIMED(DPZ_KT_FOLD_OFFSETS, st, fold_offsets_kernel<FS_SHIFT><<<og, 256, 0, st>>>(fa, starts, nt));
-      }
-      const size_t sm = fs_smem(fa.np);
-      if (nd) {
-        if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_slots_kernel<true, true><<<fs_grid<true, true>(nt, fa.np), FS_THREADS, sm, st>>>(fa, nt, nd, dpk));
-        else DPZ_TIMED(DPZ_KT_FOLD, st, fold_slots_kernel<false, true><<<fs_grid<false, true>(nt, fa.np), FS_THREADS, sm, st>>>(fa, nt, nd, dpk));
-      } else {
-        if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_slots_kernel<true, false><<<fs_grid<true, false>(nt, fa.np), FS_THREADS, sm, st>>>(fa, nt, 0, 0u));
-        else DPZ_TIMED(DPZ_KT_FOLD, st, fold_slots_kernel<false, false><<<fs_grid<false, false>(nt, fa.np), FS_THREADS, sm, st>>>(fa, nt, 0, 0u));
-      }
       continue;
     }
     if (kmax >= 0) {

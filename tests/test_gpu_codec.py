@@ -300,7 +300,7 @@ def test_fold_paths_forced(dev, monkeypatch, group, n, alpha, npay):
     np.testing.assert_array_equal(_bits(tout.cpu().numpy()), _bits(ref3))
 
 
-@pytest.mark.parametrize("kind", ["1", "2", "3", "4"])
+@pytest.mark.parametrize("kind", ["1", "2", "4"])
 @pytest.mark.parametrize("n,alpha,npay,ndense", [(1_000_003, 0.01, 16, 0), (1_000_003, 0.1, 16, 0),
                                                  (2_000_001, 0.25, 16, 0), (300_001, 0.3, 3, 1),
                                                  (300_001, 0.1, 3, 3), (100_003, 0.99, 2, 0),
@@ -308,11 +308,11 @@ def test_fold_paths_forced(dev, monkeypatch, group, n, alpha, npay):
                                                  (300_001, 0.6, 4, 0), (1_000_003, 0.45, 16, 1)])
 def test_fold_kinds_forced(dev, monkeypatch, kind, n, alpha, npay, ndense):
     """Every fold kernel forced in turn (DPZ_FOLD_KIND 1: classic hit-chain / phase, 2: 4-slot
-    group, 3: the one-phase slot fold, 4: the walk fold) on sparse groups and on groups with dense (full-share)
-    payloads, bit-exact vs the oracle with and without the self term and with a zero base; a
-    kind that cannot take a group (dense payloads on the 4-slot path, more than 4 dense on the
-    slot fold) runs the classic kernel.  alpha 0.25 x 16 needs two entry rounds per slot tile;
-    alpha 0.45 / 0.6 overflow the walk fold's 64-entry windows (its synchronous dense-tile path)."""
+    group, 4: the walk fold) on sparse groups and on groups with dense (full-share) payloads,
+    bit-exact vs the oracle with and without the self term and with a zero base; a kind that
+    cannot take a group (dense payloads on the 4-slot and walk paths) runs the classic kernel.
+    alpha 0.45 / 0.6 overflow the walk fold's 64-entry windows (its synchronous dense-tile
+    path); 7 and 16 payloads walk in groups of four."""
     monkeypatch.setenv("DPZ_FOLD_KIND", kind)
     codec = _codec()
     rng = np.random.default_rng(int(n * alpha) + npay + 31 * ndense)
@@ -355,10 +355,10 @@ def test_fold_kinds_forced(dev, monkeypatch, kind, n, alpha, npay, ndense):
     np.testing.assert_array_equal(_bits(tl2.cpu().numpy()), _bits(ref))
 
 
-@pytest.mark.parametrize("kind", ["3", "4"])
+@pytest.mark.parametrize("kind", ["4"])
 @pytest.mark.parametrize("alpha", [0.1, 0.3])
-def test_slot_fold_unaligned_views(dev, monkeypatch, kind, alpha):
-    """The slot fold's scalar-load build (local / out 4 bytes off a 16-byte boundary)."""
+def test_walk_fold_unaligned_views(dev, monkeypatch, kind, alpha):
+    """The walk fold's scalar-load build (local / out 4 bytes off a 16-byte boundary)."""
     monkeypatch.setenv("DPZ_FOLD_KIND", kind)
     codec = _codec()
     n, npay = 300_001, 16

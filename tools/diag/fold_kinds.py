@@ -60,11 +60,13 @@ def main():
     dev = torch.device("cuda:0")
     m = 25_000_009
     kinds = sys.argv[1:] or ["0", "1", "2", "4"]
-    for alpha, npay, nd in ((0.01, 16, 0), (0.03, 16, 0), (0.1, 16, 0), (0.2, 16, 0),
-                            (0.3, 16, 0), (0.1, 3, 0), (0.3, 3, 0), (0.1, 3, 1), (0.3, 3, 2),
-                            (0.2, 3, 3)):
-        r = case(dev, m, alpha, npay, nd, kinds)
-        print(json.dumps({"m": m, "alpha": alpha, "npay": npay, "dense": nd, "kinds": r}),
+    for mm, alpha, npay, nd in ((m, 0.01, 16, 0), (m, 0.03, 16, 0), (m, 0.05, 16, 0),
+                                (m, 0.1, 16, 0), (m, 0.2, 16, 0), (m, 0.3, 16, 0),
+                                (m, 0.01, 3, 0), (m, 0.1, 3, 0), (m, 0.3, 3, 0), (m, 0.4, 3, 0),
+                                (m, 0.1, 3, 1), (11_000_000, 0.01, 3, 0),
+                                (11_000_000, 0.01, 4, 0), (11_000_000, 0.01, 1, 0)):
+        r = case(dev, mm, alpha, npay, nd, kinds)
+        print(json.dumps({"m": mm, "alpha": alpha, "npay": npay, "dense": nd, "kinds": r}),
               flush=True)
 
 
