@@ -988,8 +988,10 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw)
       const int32_t j = (live ? cur_of(pc) : 0) + lane;
       const int32_t k = live ? (int32_t)a.p[pc].k : 0;
       const int32_t jc = j < k ? j : 0;
-      ix[q] = a.p[pc].idx[jc];
-      vx[q] = a.p[pc].val[jc];
+      // an empty payload's arrays may be null: read a valid address instead (masked at use)
+      const bool has = a.p[pc].k > 0;
+      ix[q] = (has ? a.p[pc].idx : reinterpret_cast<const int32_t*>(a.local))[jc];
+      vx[q] = (has ? a.p[pc].val : a.local)[jc];
     }
   };
   FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE + lane * EPL, n), Ln;
