@@ -928,7 +928,7 @@ constexpr int FW_G = 4;  // payloads per group: the windows of one group are in 
 // registers, so every window load is in flight while the group before it folds, with 16
 // registers of windows whatever the payload count.  Cursors live one per lane (lane p: payload
 // p) in one register.
-template <bool VEC, int EPL>
+template <bool VEC, int EPL, bool ONE>
 __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw) {
   constexpr int TE = 64 * EPL;
   __shared__ float s_val[FW_WAVES][TE];
@@ -945,9 +945,12 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw)
   const int64_t t1 = (t0 + tpw < ntl) ? t0 + tpw : ntl;
   if (t0 >= t1) return;  // no block barrier anywhere: a wave may leave alone
   const int np = a.np;
-  const int ng = (np + FW_G - 1) / FW_G;
-  // lane p < np: payload p's entry count, its cursor (the next window's first entry)
+  // ONE (np <= FW_G): one group, its payload numbers compile-time constants, so their
+  // pointers / sizes / weights and cursors stay in scalar registers; otherwise the group loop is
+  // dynamic and the cursors live one per lane (lane p: payload p) in one register
+  const int ng = ONE ? 1 : (np + FW_G - 1) / FW_G;
   const int32_t kl = lane < np ? (int32_t)a.p[lane < FOLD_MAXP ? lane : 0].k : 0;
+  int32_t cs[FW_G];  // ONE: the cursors
   // ---- start cursors: 64-ary lower_bound(idx_p, t0 * TE), payload by payload ----
   int32_t curv = 0;
   {
@@ -974,7 +977,17 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw)
       curv = lane == p ? lo : curv;
     }
   }
-  auto cur_of = [&](int p) { return fw_uni(__builtin_amdgcn_readlane(curv, p)); };
+  if (ONE) {
+#pragma unroll
+    for (int q = 0; q < FW_G; ++q) cs[q] = fw_uni(__builtin_amdgcn_readlane(curv, q));
+  }
+  auto cur_of = [&](int p) {
+    return ONE ? cs[p & (FW_G - 1)] : fw_uni(__builtin_amdgcn_readlane(curv, p));
+  };
+  auto set_cur = [&](int p, int32_t v) {
+    if (ONE) cs[p & (FW_G - 1)] = fw_uni(v);
+    else curv = lane == p ? v : curv;
+  };
   // ---- the windows of one group: (idx, val) at cur + lane, branch-free loads of raw values
   // (lanes past k read entry 0 and are masked when the window is used) ----
   int32_t wi[FW_G], wn[FW_G];
@@ -1008,7 +1021,8 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw)
       base[e] = a.zero_base ? 0.0f : L.v[e];
       acc[e] = 0.0f;
     }
-    for (int g = 0; g < ng; ++g) {
+    for (int gg = 0; gg < ng; ++gg) {
+      const int g = ONE ? 0 : gg;
       // this group's window starts; the entries of the tile are the leading lanes below thi
       int32_t c0[FW_G], cnt[FW_G];
 #pragma unroll
@@ -1019,7 +1033,7 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw)
         const int32_t k = live ? (int32_t)a.p[p].k : 0;
         cnt[q] = fw_lead(c0[q] + lane < k && wi[q] < thi32);
         // the next tile's window start of this payload (a full window is finished in its phase)
-        if (live) curv = lane == p ? c0[q] + cnt[q] : curv;
+        if (live) set_cur(p, c0[q] + cnt[q]);
       }
       // the next group's windows (this tile's next group, or group 0 of the next tile)
       load_group(g + 1 < ng ? g + 1 : 0, wn, wvn);
@@ -1051,7 +1065,7 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw)
             c += cc;
             if (cc < 64) break;
           }
-          curv = lane == p ? c0[q] + c : curv;
+          set_cur(p, c0[q] + c);
           if (ng == 1) load_group(0, wn, wvn);  // the next tile's window of this group moved
         }
         // the row is this wave's own and one wave's LDS instructions execute in order, so the
@@ -1130,7 +1144,7 @@ static inline int64_t fold_ntiles(int64_t n) { return (n + FOLD_TILE - 1) / FOLD
 // The walk fold's launch: EPL from the densest payload (~32 entries per payload per tile on
 // average at dens <= 0.125: 256-element tiles; denser payloads 128-element tiles); a
 // persistent grid of what the CUs hold, each wave a contiguous run of tiles.
-template <bool VEC, int EPL>
+template <bool VEC, int EPL, bool ONE>
 static int launch_walk_t(const FoldArgs& fa, hipStream_t st) {
   static int per = 0, cus = 0;
   if (per == 0) {
@@ -1138,7 +1152,7 @@ static int launch_walk_t(const FoldArgs& fa, hipStream_t st) {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fold_walk_kernel<VEC, EPL>, 256, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fold_walk_kernel<VEC, EPL, ONE>, 256, 0) !=
             hipSuccess || per < 1)
       per = 1;
   }
@@ -1149,7 +1163,7 @@ static int launch_walk_t(const FoldArgs& fa, hipStream_t st) {
   if (blocks > need) blocks = need;
   if (blocks < 1) blocks = 1;
   const int64_t tpw = (ntl + blocks * FW_WAVES - 1) / (blocks * FW_WAVES);
-  DPZ_TIMED(DPZ_KT_FOLD, st, fold_walk_kernel<VEC, EPL><<<(unsigned)blocks, 256, 0, st>>>(fa, tpw));
+  DPZ_TIMED(DPZ_KT_FOLD, st, fold_walk_kernel<VEC, EPL, ONE><<<(unsigned)blocks, 256, 0, st>>>(fa, tpw));
   return DPZ_OK;
 }
 
@@ -1158,10 +1172,15 @@ static bool walk_ok(const FoldArgs& fa) {
          fa.n < (int64_t(1) << 31) - 1024;
 }
 
+template <bool ONE>
+static int launch_walk_o(const FoldArgs& fa, bool vec, int epl, hipStream_t st) {
+  if (vec) return epl == 4 ? launch_walk_t<true, 4, ONE>(fa, st) : launch_walk_t<true, 2, ONE>(fa, st);
+  return epl == 4 ? launch_walk_t<false, 4, ONE>(fa, st) : launch_walk_t<false, 2, ONE>(fa, st);
+}
+
 static int launch_walk(const FoldArgs& fa, bool vec, double dens, hipStream_t st) {
   const int epl = dens <= 0.125 ? 4 : 2;
-  if (vec) return epl == 4 ? launch_walk_t<true, 4>(fa, st) : launch_walk_t<true, 2>(fa, st);
-  return epl == 4 ? launch_walk_t<false, 4>(fa, st) : launch_walk_t<false, 2>(fa, st);
+  return fa.np <= FW_G ? launch_walk_o<true>(fa, vec, epl, st) : launch_walk_o<false>(fa, vec, epl, st);
 }
 
 // Replace-only decode of ONE sparse payload (reference PartialModel.py:257-303, T[idx] = params):

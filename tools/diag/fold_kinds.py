@@ -59,7 +59,7 @@ def case(dev, m, alpha, npay, ndense, kinds, reps=20):
 def main():
     dev = torch.device("cuda:0")
     m = 25_000_009
-    kinds = sys.argv[1:] or ["0", "1", "2", "4"]
+    kinds = os.environ.get("FOLD_KINDS", "0 1 2 4").split()
     for mm, alpha, npay, nd in ((m, 0.01, 16, 0), (m, 0.03, 16, 0), (m, 0.05, 16, 0),
                                 (m, 0.1, 16, 0), (m, 0.2, 16, 0), (m, 0.3, 16, 0),
                                 (m, 0.01, 3, 0), (m, 0.1, 3, 0), (m, 0.3, 3, 0), (m, 0.4, 3, 0),
