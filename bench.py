@@ -53,6 +53,9 @@ def parse():
                    help="S > 1: S independent node codecs share the GPU on S streams (as "
                         "decentralizepy runs procs_per_machine nodes per machine); the one-node "
                         "(one stream) rate is always measured beside it")
+    p.add_argument("--selftest-spawn", action="store_true",
+                   help="(tests) each started rank reports RANK / WORLD_SIZE / LOCAL_RANK and "
+                        "exits before any GPU call")
     p.add_argument("--repeats", type=int, default=0,
                    help="timed regions of exactly --steps steps each (0: auto, enough for a "
                         "stable median at small --steps); the line reports the median region")
@@ -378,6 +381,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.selftest_spawn:
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank,
+                          "cpu_baseline_file": bool(os.environ.get("DPZ_BENCH_CPU_BASELINE"))}),
+              flush=True)
+        return
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were started")
     dist = None

@@ -22,6 +22,7 @@ position without exchanging them.  The per-node work is the HIP codec (DWT pair,
 with ADD accumulation, batched coefficient-domain fold, IDWT, accumulating DWT); ``ops`` is
 injectable so the round logic is tested against the numpy oracle on the CPU (gloo, world 2).
 """
+import contextlib
 import ctypes
 import random
 
@@ -37,30 +38,52 @@ def _al(v):
 
 
 class HipJwinsOps:
-    """The HIP codec behind the round (no CPU path)."""
+    """The HIP codec behind the round (no CPU path).  The rank's nodes run as ``streams``
+    concurrent codecs (node j on stream j % S, one top-k workspace each), as decentralizepy runs
+    several node processes per GPU: one node's latency-bound selection tail overlaps another's
+    streaming kernels.  ``fork`` / ``join`` order the streams against the caller's stream around
+    each phase of the round (the fold needs every neighbour's payload)."""
 
-    def __init__(self, device, wavelet, level):
+    def __init__(self, device, wavelet, level, streams=3):
         from . import codec
         self.codec = codec
         self.device = device
         self.wavelet, self.level = wavelet, level
-        self.ws = codec.Workspace(device)
+        self.streams = [torch.cuda.Stream(device) for _ in range(max(1, streams))]
+        self.wss = [codec.Workspace(device) for _ in self.streams]
+        self.ws = self.wss[0]
 
     def reserve(self, m_len, ks):
-        """Size the shared top-k workspace for every k a round can draw, once (a workspace that
-        grows mid-round would be reallocated between asynchronous encodes)."""
-        for k in ks:
-            self.ws.get(m_len, k)
+        """Size every top-k workspace for every k a round can draw, once (a workspace that grows
+        mid-round would be reallocated between asynchronous encodes)."""
+        for ws in self.wss:
+            for k in ks:
+                ws.get(m_len, k)
+
+    def fork(self):
+        cur = torch.cuda.current_stream(self.device)
+        for st in self.streams:
+            st.wait_stream(cur)
+
+    def join(self):
+        cur = torch.cuda.current_stream(self.device)
+        for st in self.streams:
+            cur.wait_stream(st)
+
+    def on(self, j):
+        """Context: node j's work goes to its stream."""
+        return torch.cuda.stream(self.streams[j % len(self.streams)])
 
     def transform_pair(self, x, x0, wx, wc):
         self.codec.wavedec(x, self.level, x0=x0, coeffs_x=wx, coeffs_diff=wc,
                            wavelet=self.wavelet)
 
-    def encode(self, wc, k, acc, wx, counter, idx_out, val_out, status):
+    def encode(self, wc, k, acc, wx, counter, idx_out, val_out, status, j=0):
         """Asynchronous: the final status word goes to ``status`` on the device."""
         self.codec.topk_encode(wc, k, acc=acc, acc_mode=self.codec.DPZ_ACC_ADD, vals_src=wx,
                                counter=counter, idx_out=idx_out, val_out=val_out,
-                               workspace=self.ws, status_out=status)
+                               workspace=self.wss[j % len(self.wss)], status_out=status,
+                               shared=len(self.streams) > 1)
 
     def encode_exact(self, wc, k, acc, wx, counter, idx_out, val_out):
         self.codec.topk_encode(wc, k, acc=acc, acc_mode=self.codec.DPZ_ACC_ADD, vals_src=wx,
@@ -88,15 +111,15 @@ class HipJwinsOps:
                 w.append(wq)
             ws_.append(w_self)
         m, tot = len(jobs), max(1, len(idx))
-        dws = self.ws.get_decode(m_len, max(counts) if counts else 1)
-        stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-        rc = _lib.lib().dpz_decode_average_batch(
+        dws = [w_.get_decode(m_len, max(counts) if counts else 1) for w_ in self.wss]
+        S = len(self.streams)
+        rc = _lib.lib().dpz_decode_average_batch(  # node j on stream j % S (the streams' order)
             m, (ctypes.c_void_p * max(1, m))(*locs), (ctypes.c_void_p * max(1, m))(*outs),
             m_len, (ctypes.c_int * max(1, m))(*counts), (ctypes.c_void_p * tot)(*idx),
             (ctypes.c_void_p * tot)(*val), (ctypes.c_int64 * tot)(*kk),
             (ctypes.c_float * tot)(*w), (ctypes.c_float * max(1, m))(*ws_), DPZ_FOLD_SELF,
-            (ctypes.c_void_p * 1)(dws.data_ptr()), dws.numel(), 1,
-            (ctypes.c_void_p * 1)(stream))
+            (ctypes.c_void_p * S)(*[d.data_ptr() for d in dws]), min(d.numel() for d in dws), S,
+            (ctypes.c_void_p * S)(*[st.cuda_stream for st in self.streams]))
         _lib.check(rc, "dpz_decode_average_batch")
 
     def inverse(self, tot, n, out):
@@ -200,21 +223,37 @@ class JwinsRound:
         return None, bv[ov:ov + self.M]
 
     # ---- one round ---------------------------------------------------------------------------
+    def _on(self, j):
+        on = getattr(self.ops, "on", None)
+        return on(j) if on is not None else contextlib.nullcontext()
+
+    def _fork(self):
+        if hasattr(self.ops, "fork"):
+            self.ops.fork()
+
+    def _join(self):
+        if hasattr(self.ops, "join"):
+            self.ops.join()
+
     def encode_all(self, lay):
         m = self.hi - self.lo
+        self._fork()
         for j in range(m):
             q = self.lo + j
-            self.ops.transform_pair(self.x[j], self.x0[j], self.wx[j], self.wc[j])
-            partial, k, oi, ov = lay[q]
-            if partial:
-                self.ops.encode(self.wc[j], k, self.acc[j], self.wx[j], self.counter[j],
-                                self.send_idx[oi:oi + k], self.send_val[ov:ov + k],
-                                self.status[j:j + 1])
-            else:  # Wavelet.py:185-192: all of W(x), accumulated changes zeroed
-                self.acc[j].zero_()
-                self.status[j:j + 1].zero_()
-                if self.world > 1:
-                    self.send_val[ov:ov + self.M].copy_(self.wx[j])
+            with self._on(j):
+                self.ops.transform_pair(self.x[j], self.x0[j], self.wx[j], self.wc[j])
+                partial, k, oi, ov = lay[q]
+                if partial:
+                    kw = {"j": j} if hasattr(self.ops, "on") else {}
+                    self.ops.encode(self.wc[j], k, self.acc[j], self.wx[j], self.counter[j],
+                                    self.send_idx[oi:oi + k], self.send_val[ov:ov + k],
+                                    self.status[j:j + 1], **kw)
+                else:  # Wavelet.py:185-192: all of W(x), accumulated changes zeroed
+                    self.acc[j].zero_()
+                    self.status[j:j + 1].zero_()
+                    if self.world > 1:
+                        self.send_val[ov:ov + self.M].copy_(self.wx[j])
+        self._join()
         # a sampled-path miss (rare) left that node's payload and bookkeeping untouched: redo it
         for j in self.ops.missed(self.status[:m]):
             partial, k, oi, ov = lay[self.lo + j]
@@ -236,11 +275,14 @@ class JwinsRound:
             nbrs, w, w_self = self.weights[self.lo + j]
             pays = [self._payload(q, lay, s_idx, s_val) for q in nbrs]
             jobs.append((self.wx[j], pays, w, w_self, self.wc[j]))
-        self.ops.fold_all(jobs, self.M)
+        self._fork()
+        self.ops.fold_all(jobs, self.M)  # node j on stream j % S
         for j in range(self.hi - self.lo):
-            self.ops.inverse(self.wc[j], self.N, self.x[j])        # model <- waverec(total)
-            self.ops.accumulate(self.acc[j], self.x[j], self.x0[j])  # acc += W(x_new - prev)
-        self.x0.copy_(self.x)                                       # init_model = prev = x_new
+            with self._on(j):
+                self.ops.inverse(self.wc[j], self.N, self.x[j])        # model <- waverec(total)
+                self.ops.accumulate(self.acc[j], self.x[j], self.x0[j])  # acc += W(x_new - prev)
+                self.x0[j].copy_(self.x[j])                              # init = prev = x_new
+        self._join()
 
     def step(self):
         alphas = [rng.choice(self.alpha_list) for rng in self.rngs]
