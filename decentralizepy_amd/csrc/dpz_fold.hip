@@ -864,52 +864,67 @@ struct FwV {
   float v[EPL];
 };
 
-// Loads are branch-free (addresses clamped into [0, n), results past n unused: their elements
-// are never stored), so the compiler can count them and wait only for the tile it folds, never
-// for the next tile's loads in flight (a load under a branch makes it wait for all: vmcnt(0)).
-// VEC kernels run only for n >= 4 and 16-byte aligned operands.
+// A lane's EPL elements of a tile: contiguous for EPL <= 4; for EPL = 4C > 4, chunk c holds the
+// lane's 4 elements at 256 c + 4 lane (every float4 wave-instruction reads 1 KB contiguous).
+template <int EPL>
+__device__ __forceinline__ int fw_elem(int lane, int e) {
+  return EPL <= 4 ? lane * EPL + e : 256 * (e >> 2) + 4 * lane + (e & 3);
+}
+
 // Loads are branch-free (addresses clamped into [0, n); results past n are never stored), so
 // the compiler counts them and waits only for the tile it folds, never for the next tile's loads
 // in flight (a load under a branch makes it wait for everything: vmcnt(0)).  VEC kernels run
 // only when n is a multiple of 4 and the operands are 16-byte aligned.
 template <bool VEC, int EPL>
-__device__ __forceinline__ FwV<EPL> fw_load(const float* p, int64_t i0, int64_t n) {
+__device__ __forceinline__ FwV<EPL> fw_load(const float* p, int64_t tlo, int lane, int64_t n) {
   FwV<EPL> r;
-  if constexpr (VEC && EPL > 1) {
-    const int64_t q = i0 < n ? i0 : n - EPL;
-    if constexpr (EPL == 4) {
+  if constexpr (VEC && EPL >= 4) {
+#pragma unroll
+    for (int c = 0; c < EPL / 4; ++c) {
+      const int64_t i0 = tlo + fw_elem<EPL>(lane, 4 * c);
+      const int64_t q = i0 < n ? i0 : n - 4;
       const float4 v = *reinterpret_cast<const float4*>(p + q);
-      r.v[0] = v.x; r.v[1] = v.y; r.v[2] = v.z; r.v[3] = v.w;
-    } else {
-      const float2 v = *reinterpret_cast<const float2*>(p + q);
-      r.v[0] = v.x; r.v[1] = v.y;
+      r.v[4 * c] = v.x; r.v[4 * c + 1] = v.y; r.v[4 * c + 2] = v.z; r.v[4 * c + 3] = v.w;
     }
+    return r;
+  } else if constexpr (VEC && EPL == 2) {
+    const int64_t i0 = tlo + 2 * lane;
+    const int64_t q = i0 < n ? i0 : n - 2;
+    const float2 v = *reinterpret_cast<const float2*>(p + q);
+    r.v[0] = v.x; r.v[1] = v.y;
     return r;
   }
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
-    const int64_t q = i0 + e < n ? i0 + e : n - 1;
-    r.v[e] = p[q];
+    const int64_t i = tlo + fw_elem<EPL>(lane, e);
+    r.v[e] = p[i < n ? i : n - 1];
   }
   return r;
 }
 
 // GUARD: the ragged last tile (elements past n are not stored)
 template <bool VEC, int EPL, bool GUARD>
-__device__ __forceinline__ void fw_store(float* p, int64_t i0, int64_t n, const float (&r)[EPL]) {
-  if (VEC && EPL > 1 && (!GUARD || i0 < n)) {
-    if constexpr (EPL == 4) {
-      *reinterpret_cast<float4*>(p + i0) = make_float4(r[0], r[1], r[2], r[3]);
-      return;
-    } else if constexpr (EPL == 2) {
-      *reinterpret_cast<float2*>(p + i0) = make_float2(r[0], r[1]);
-      return;
-    }
-  }
-  if (VEC && EPL > 1) return;
+__device__ __forceinline__ void fw_store(float* p, int64_t tlo, int lane, int64_t n,
+                                         const float (&r)[EPL]) {
+  if constexpr (VEC && EPL >= 4) {
 #pragma unroll
-  for (int e = 0; e < EPL; ++e)
-    if (!GUARD || i0 + e < n) p[i0 + e] = r[e];
+    for (int c = 0; c < EPL / 4; ++c) {
+      const int64_t i0 = tlo + fw_elem<EPL>(lane, 4 * c);
+      if (!GUARD || i0 < n)
+        *reinterpret_cast<float4*>(p + i0) =
+            make_float4(r[4 * c], r[4 * c + 1], r[4 * c + 2], r[4 * c + 3]);
+    }
+    return;
+  } else if constexpr (VEC && EPL == 2) {
+    const int64_t i0 = tlo + 2 * lane;
+    if (!GUARD || i0 < n) *reinterpret_cast<float2*>(p + i0) = make_float2(r[0], r[1]);
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const int64_t i = tlo + fw_elem<EPL>(lane, e);
+    if (!GUARD || i < n) p[i] = r[e];
+  }
 }
 
 // the leading lanes whose index lies below `hi` (a sorted window): 0..64
@@ -1007,14 +1022,14 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw)
       vx[q] = (has ? a.p[pc].val : a.local)[jc];
     }
   };
-  FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE + lane * EPL, n), Ln;
+  FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n), Ln;
   load_group(0, wi, wvv);
   uint32_t seq = 0;
   auto tile_body = [&](int64_t tile, auto guard) {
     constexpr bool GUARD = decltype(guard)::value;
     const int64_t tlo = tile * TE;
     const int32_t tlo32 = (int32_t)tlo, thi32 = tlo32 + TE;
-    Ln = fw_load<VEC, EPL>(a.local, tlo + TE + lane * EPL, n);  // clamped past the end
+    Ln = fw_load<VEC, EPL>(a.local, tlo + TE, lane, n);  // clamped past the end
     float acc[EPL], base[EPL];
 #pragma unroll
     for (int e = 0; e < EPL; ++e) {
@@ -1075,11 +1090,15 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw)
         __builtin_amdgcn_wave_barrier();
         uint32_t tg[EPL];
         float hv[EPL], tv[EPL];
-        if constexpr (EPL == 4) {
-          const uint4 t4 = *reinterpret_cast<const uint4*>(&wt[lane * 4]);
-          const float4 h4 = *reinterpret_cast<const float4*>(&wv[lane * 4]);
-          tg[0] = t4.x; tg[1] = t4.y; tg[2] = t4.z; tg[3] = t4.w;
-          hv[0] = h4.x; hv[1] = h4.y; hv[2] = h4.z; hv[3] = h4.w;
+        if constexpr (EPL >= 4) {
+#pragma unroll
+          for (int c = 0; c < EPL / 4; ++c) {
+            const int o = fw_elem<EPL>(lane, 4 * c);
+            const uint4 t4 = *reinterpret_cast<const uint4*>(&wt[o]);
+            const float4 h4 = *reinterpret_cast<const float4*>(&wv[o]);
+            tg[4 * c] = t4.x; tg[4 * c + 1] = t4.y; tg[4 * c + 2] = t4.z; tg[4 * c + 3] = t4.w;
+            hv[4 * c] = h4.x; hv[4 * c + 1] = h4.y; hv[4 * c + 2] = h4.z; hv[4 * c + 3] = h4.w;
+          }
         } else {
 #pragma unroll
           for (int e = 0; e < EPL; ++e) {
@@ -1105,8 +1124,8 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw)
 #pragma unroll
       for (int e = 0; e < EPL; ++e) acc[e] = acc[e] + L.v[e] * a.w_self;
     }
-    fw_store<VEC, EPL, GUARD>(a.out, tlo + lane * EPL, n, acc);
-    if (a.out2) fw_store<VEC, EPL, GUARD>(a.out2, tlo + lane * EPL, n, acc);
+    fw_store<VEC, EPL, GUARD>(a.out, tlo, lane, n, acc);
+    if (a.out2) fw_store<VEC, EPL, GUARD>(a.out2, tlo, lane, n, acc);
     L = Ln;
     ++seq;
   };
@@ -1174,12 +1193,22 @@ static bool walk_ok(const FoldArgs& fa) {
 
 template <bool ONE>
 static int launch_walk_o(const FoldArgs& fa, bool vec, int epl, hipStream_t st) {
-  if (vec) return epl == 4 ? launch_walk_t<true, 4, ONE>(fa, st) : launch_walk_t<true, 2, ONE>(fa, st);
+  if (vec) {
+    if (epl == 16) return launch_walk_t<true, 16, ONE>(fa, st);
+    return epl == 4 ? launch_walk_t<true, 4, ONE>(fa, st) : launch_walk_t<true, 2, ONE>(fa, st);
+  }
+  if (epl == 16) return launch_walk_t<false, 16, ONE>(fa, st);
   return epl == 4 ? launch_walk_t<false, 4, ONE>(fa, st) : launch_walk_t<false, 2, ONE>(fa, st);
 }
 
+// ~10-32 entries per payload per tile on average: 1024-element tiles up to dens 0.03, 256 up to
+// 0.125, 128 beyond (full windows then rare; DPZ_FOLD_WALK_EPL forces 16 / 4 / 2)
 static int launch_walk(const FoldArgs& fa, bool vec, double dens, hipStream_t st) {
-  const int epl = dens <= 0.125 ? 4 : 2;
+  int epl = dens <= 0.03 ? 16 : (dens <= 0.125 ? 4 : 2);
+  if (const char* e = getenv("DPZ_FOLD_WALK_EPL")) {
+    const int v = atoi(e);
+    if (v == 16 || v == 4 || v == 2) epl = v;
+  }
   return fa.np <= FW_G ? launch_walk_o<true>(fa, vec, epl, st) : launch_walk_o<false>(fa, vec, epl, st);
 }
 
