@@ -964,14 +964,35 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw)
   // pointers / sizes / weights and cursors stay in scalar registers; otherwise the group loop is
   // dynamic and the cursors live one per lane (lane p: payload p) in one register
   const int ng = ONE ? 1 : (np + FW_G - 1) / FW_G;
-  const int32_t kl = lane < np ? (int32_t)a.p[lane < FOLD_MAXP ? lane : 0].k : 0;
+  const int lp = lane < np && lane < FOLD_MAXP ? lane : 0;
+  const int32_t kl = lane < np ? (int32_t)a.p[lp].k : 0;
+  // !ONE: payload p's pointers and weight held by lane p, read back with readlane (no scalar
+  // loads of the kernel arguments with a run-time payload number inside the loop)
+  const uint64_t ipl = reinterpret_cast<uint64_t>(a.p[lp].idx);
+  const uint64_t vpl = reinterpret_cast<uint64_t>(a.p[lp].val);
+  const float wl = a.p[lp].w;
+  auto rl64 = [](uint64_t v, int p) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, p);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), p);
+    return ((uint64_t)hi << 32) | lo;
+  };
+  auto P_idx = [&](int p) {
+    return ONE ? a.p[p].idx : reinterpret_cast<const int32_t*>(rl64(ipl, p));
+  };
+  auto P_val = [&](int p) {
+    return ONE ? a.p[p].val : reinterpret_cast<const float*>(rl64(vpl, p));
+  };
+  auto P_k = [&](int p) { return ONE ? (int32_t)a.p[p].k : fw_uni(__builtin_amdgcn_readlane(kl, p)); };
+  auto P_w = [&](int p) {
+    return ONE ? a.p[p].w : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl), p));
+  };
   int32_t cs[FW_G];  // ONE: the cursors
   // ---- start cursors: 64-ary lower_bound(idx_p, t0 * TE), payload by payload ----
   int32_t curv = 0;
   {
     const int32_t e0 = (int32_t)(t0 * TE);
     for (int p = 0; p < np; ++p) {
-      const int32_t* ip = a.p[p].idx;
+      const int32_t* ip = P_idx(p);
       int32_t lo = 0, hi = fw_uni(__builtin_amdgcn_readlane(kl, p));
       while (hi > lo) {
         const int32_t len = hi - lo;
@@ -1014,12 +1035,13 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw)
       const bool live = p < np;
       const int pc = live ? p : 0;
       const int32_t j = (live ? cur_of(pc) : 0) + lane;
-      const int32_t k = live ? (int32_t)a.p[pc].k : 0;
+      const int32_t kp = P_k(pc);
+      const int32_t k = live ? kp : 0;
       const int32_t jc = j < k ? j : 0;
       // an empty payload's arrays may be null: read a valid address instead (masked at use)
-      const bool has = a.p[pc].k > 0;
-      ix[q] = (has ? a.p[pc].idx : reinterpret_cast<const int32_t*>(a.local))[jc];
-      vx[q] = (has ? a.p[pc].val : a.local)[jc];
+      const bool has = kp > 0;
+      ix[q] = (has ? P_idx(pc) : reinterpret_cast<const int32_t*>(a.local))[jc];
+      vx[q] = (has ? P_val(pc) : a.local)[jc];
     }
   };
   FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n), Ln;
@@ -1045,7 +1067,7 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw)
         const int p = g * FW_G + q;
         const bool live = p < np;
         c0[q] = live ? cur_of(p) : 0;
-        const int32_t k = live ? (int32_t)a.p[p].k : 0;
+        const int32_t k = live ? P_k(p) : 0;
         cnt[q] = fw_lead(c0[q] + lane < k && wi[q] < thi32);
         // the next tile's window start of this payload (a full window is finished in its phase)
         if (live) set_cur(p, c0[q] + cnt[q]);
@@ -1056,7 +1078,7 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw)
       for (int q = 0; q < FW_G; ++q) {
         const int p = g * FW_G + q;
         if (p >= np) break;
-        const float w = a.p[p].w;
+        const float w = P_w(p);
         const uint32_t tag = (seq << 4) | (uint32_t)p;
         {
           const uint32_t pos = (uint32_t)(wi[q] - tlo32);  // < TE: inside the tile
@@ -1066,15 +1088,17 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw)
           }
         }
         if (cnt[q] == 64) {  // a dense tile: this payload's further windows, synchronously
-          const int32_t k = (int32_t)a.p[p].k;
+          const int32_t k = P_k(p);
+          const int32_t* pi = P_idx(p);
+          const float* pv = P_val(p);
           int32_t c = 64;
           for (int32_t j0 = c0[q] + 64;; j0 += 64) {
             const int32_t j = j0 + lane;
-            const int32_t iv = j < k ? a.p[p].idx[j] : INT32_MAX;
+            const int32_t iv = j < k ? pi[j] : INT32_MAX;
             const int cc = fw_lead(iv < thi32);
             const uint32_t pos = (uint32_t)(iv - tlo32);
             if (lane < cc && pos < (uint32_t)TE) {
-              wv[pos] = a.p[p].val[j];
+              wv[pos] = pv[j];
               wt[pos] = tag;
             }
             c += cc;
