@@ -935,16 +935,226 @@ __device__ __forceinline__ int fw_lead(bool in) {
 
 __device__ __forceinline__ int32_t fw_uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Sparse payloads only (dense ones take the classic kernels), a fresh total (a.first),
+// n < 2^31 - 1024 (walk_ok), np <= NS.  NS payload slots, all compile-time: every slot's window
+// of the NEXT tile is issued at the start of this tile (branch-free loads), so the loads are in
+// flight while all of this tile's payloads fold.  NS = 4: the payloads' pointers, sizes, weights
+// and cursors in scalar registers (a generic path holds them one per lane and reads them back
+// with readlane; measured slower than fold_walk_groups_kernel at 16 payloads, which is used there).
+template <bool VEC, int EPL, int NS>
+__global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw) {
+  constexpr bool ONE = NS <= 4;
+  constexpr int TE = 64 * EPL;
+  __shared__ float s_val[FW_WAVES][TE];
+  __shared__ uint32_t s_tag[FW_WAVES][TE];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float* wv = s_val[wid];
+  uint32_t* wt = s_tag[wid];
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) wt[lane + 64 * e] = 0xFFFFFFFFu;
+  const int64_t n = a.n;
+  const int64_t ntl = (n + TE - 1) / TE;
+  const int64_t gw = (int64_t)blockIdx.x * FW_WAVES + wid;
+  const int64_t t0 = gw * tpw;
+  const int64_t t1 = (t0 + tpw < ntl) ? t0 + tpw : ntl;
+  if (t0 >= t1) return;  // no block barrier anywhere: a wave may leave alone
+  const int np = a.np;
+  const int lp = lane < np && lane < FOLD_MAXP ? lane : 0;
+  const int32_t kl = lane < np ? (int32_t)a.p[lp].k : 0;
+  const uint64_t ipl = ONE ? 0 : reinterpret_cast<uint64_t>(a.p[lp].idx);
+  const uint64_t vpl = ONE ? 0 : reinterpret_cast<uint64_t>(a.p[lp].val);
+  const float wl = ONE ? 0.0f : a.p[lp].w;
+  auto rl64 = [](uint64_t v, int p) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, p);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), p);
+    return ((uint64_t)hi << 32) | lo;
+  };
+  auto P_idx = [&](int p) {
+    return ONE ? a.p[p].idx : reinterpret_cast<const int32_t*>(rl64(ipl, p));
+  };
+  auto P_val = [&](int p) {
+    return ONE ? a.p[p].val : reinterpret_cast<const float*>(rl64(vpl, p));
+  };
+  auto P_k = [&](int p) { return ONE ? (int32_t)a.p[p].k : fw_uni(__builtin_amdgcn_readlane(kl, p)); };
+  auto P_w = [&](int p) {
+    return ONE ? a.p[p].w : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl), p));
+  };
+  // ---- start cursors: 64-ary lower_bound(idx_p, t0 * TE), payload by payload ----
+  int32_t curv = 0;  // lane p: payload p's cursor (the next window's first entry)
+  {
+    const int32_t e0 = (int32_t)(t0 * TE);
+    for (int p = 0; p < np; ++p) {
+      const int32_t* ip = a.p[p].idx;
+      int32_t lo = 0, hi = fw_uni(__builtin_amdgcn_readlane(kl, p));
+      while (hi > lo) {
+        const int32_t len = hi - lo;
+        const int32_t stride = len <= 64 ? 1 : (len + 63) / 64;
+        const int64_t q = (int64_t)lo + (int64_t)lane * stride;
+        const bool ok = q < hi;
+        const int32_t x = ip[ok ? q : lo];
+        const int32_t c = (int32_t)__popcll(__ballot(ok && x < e0));  // a prefix
+        if (stride == 1) {
+          lo += c;
+          break;
+        }
+        const int32_t nlo = c > 0 ? lo + (c - 1) * stride + 1 : lo;
+        const int64_t nhi = (int64_t)lo + (int64_t)c * stride;
+        hi = nhi < hi ? (int32_t)nhi : hi;
+        lo = nlo;
+      }
+      curv = lane == p ? lo : curv;
+    }
+  }
+  int32_t cs[ONE ? NS : 1];
+  if constexpr (ONE) {
+#pragma unroll
+    for (int p = 0; p < NS; ++p) cs[p] = fw_uni(__builtin_amdgcn_readlane(curv, p));
+  }
+  auto cur_of = [&](int p) {
+    if constexpr (ONE) return cs[p];
+    else return fw_uni(__builtin_amdgcn_readlane(curv, p));
+  };
+  auto set_cur = [&](int p, int32_t v) {
+    if constexpr (ONE) cs[p] = fw_uni(v);
+    else curv = lane == p ? v : curv;
+  };
+  // ---- one 64-entry window per slot: (idx, val) at cur + lane, branch-free loads of raw values
+  // (lanes past k read entry 0 and are masked when the window is used) ----
+  int32_t wi[NS], wn[NS];
+  float wvv[NS], wvn[NS];
+  auto load_window = [&](int p, int32_t& ix, float& vx) {
+    const bool live = p < np;
+    const int pc = live ? p : 0;
+    const int32_t j = (live ? cur_of(p) : 0) + lane;
+    const int32_t kp = P_k(pc);
+    const int32_t k = live ? kp : 0;
+    const int32_t jc = j < k ? j : 0;
+    // an empty payload's arrays may be null: read a valid address instead (masked at use)
+    const bool has = kp > 0;
+    ix = (has ? P_idx(pc) : reinterpret_cast<const int32_t*>(a.local))[jc];
+    vx = (has ? P_val(pc) : a.local)[jc];
+  };
+  FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n), Ln;
+#pragma unroll
+  for (int p = 0; p < NS; ++p) load_window(p, wi[p], wvv[p]);
+  uint32_t seq = 0;
+  auto tile_body = [&](int64_t tile, auto guard) {
+    constexpr bool GUARD = decltype(guard)::value;
+    const int64_t tlo = tile * TE;
+    const int32_t tlo32 = (int32_t)tlo, thi32 = tlo32 + TE;
+    // every slot: this tile's window start and entry count (the leading lanes below thi); the
+    // cursors move to the next tile's windows, which are issued now with the next local values
+    int32_t c0[NS], cnt[NS];
+#pragma unroll
+    for (int p = 0; p < NS; ++p) {
+      const bool live = p < np;
+      c0[p] = live ? cur_of(p) : 0;
+      const int32_t k = live ? P_k(p) : 0;
+      cnt[p] = fw_lead(c0[p] + lane < k && wi[p] < thi32);
+      if (live) set_cur(p, c0[p] + cnt[p]);
+    }
+#pragma unroll
+    for (int p = 0; p < NS; ++p) load_window(p, wn[p], wvn[p]);
+    Ln = fw_load<VEC, EPL>(a.local, tlo + TE, lane, n);  // clamped past the end
+    float acc[EPL], base[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      base[e] = a.zero_base ? 0.0f : L.v[e];
+      acc[e] = 0.0f;
+    }
+#pragma unroll
+    for (int p = 0; p < NS; ++p) {
+      if (p >= np) break;
+      const float w = P_w(p);
+      const uint32_t tag = (seq << 4) | (uint32_t)p;
+      {
+        const uint32_t pos = (uint32_t)(wi[p] - tlo32);  // < TE: inside the tile
+        if (lane < cnt[p] && pos < (uint32_t)TE) {
+          wv[pos] = wvv[p];
+          wt[pos] = tag;
+        }
+      }
+      if (cnt[p] == 64) {  // a dense tile: this payload's further windows, synchronously
+        const int32_t k = P_k(p);
+        const int32_t* pi = P_idx(p);
+        const float* pv = P_val(p);
+        int32_t c = 64;
+        for (int32_t j0 = c0[p] + 64;; j0 += 64) {
+          const int32_t j = j0 + lane;
+          const int32_t iv = j < k ? pi[j] : INT32_MAX;
+          const int cc = fw_lead(iv < thi32);
+          const uint32_t pos = (uint32_t)(iv - tlo32);
+          if (lane < cc && pos < (uint32_t)TE) {
+            wv[pos] = pv[j];
+            wt[pos] = tag;
+          }
+          c += cc;
+          if (cc < 64) break;
+        }
+        set_cur(p, c0[p] + c);
+        load_window(p, wn[p], wvn[p]);  // the next tile's window of this payload moved
+      }
+      // the row is this wave's own and one wave's LDS instructions execute in order, so the
+      // lanes' writes above are seen by the reads below with no wait; the scheduling barriers
+      // only keep the compiler from moving LDS accesses across (no memory fence: a fence would
+      // also wait for the next tile's loads in flight)
+      __builtin_amdgcn_wave_barrier();
+      uint32_t tg[EPL];
+      float hv[EPL];
+      if constexpr (EPL >= 4) {
+#pragma unroll
+        for (int c = 0; c < EPL / 4; ++c) {
+          const int o = fw_elem<EPL>(lane, 4 * c);
+          const uint4 t4 = *reinterpret_cast<const uint4*>(&wt[o]);
+          const float4 h4 = *reinterpret_cast<const float4*>(&wv[o]);
+          tg[4 * c] = t4.x; tg[4 * c + 1] = t4.y; tg[4 * c + 2] = t4.z; tg[4 * c + 3] = t4.w;
+          hv[4 * c] = h4.x; hv[4 * c + 1] = h4.y; hv[4 * c + 2] = h4.z; hv[4 * c + 3] = h4.w;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+          tg[e] = wt[lane * EPL + e];
+          hv[e] = wv[lane * EPL + e];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        const float tv = tg[e] == tag ? hv[e] : base[e];
+        const float term = tv * w;
+        acc[e] = p == 0 ? (a.zero_base ? 0.0f + term : term) : acc[e] + term;
+      }
+    }
+    if (a.add_self) {
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) acc[e] = acc[e] + L.v[e] * a.w_self;
+    }
+    fw_store<VEC, EPL, GUARD>(a.out, tlo, lane, n, acc);
+    if (a.out2) fw_store<VEC, EPL, GUARD>(a.out2, tlo, lane, n, acc);
+#pragma unroll
+    for (int p = 0; p < NS; ++p) {
+      wi[p] = wn[p];
+      wvv[p] = wvn[p];
+    }
+    L = Ln;
+    ++seq;
+  };
+  const int64_t tfull = n / TE;  // tiles wholly inside [0, n)
+  const int64_t tf = t1 < tfull ? t1 : (tfull > t0 ? tfull : t0);
+  for (int64_t tile = t0; tile < tf; ++tile) tile_body(tile, std::false_type{});
+  if (tf < t1) tile_body(tf, std::true_type{});  // the global last tile, ragged
+}
+
 constexpr int FW_G = 4;  // payloads per group: the windows of one group are in registers
 
-// Sparse payloads only (dense ones take the classic kernels), a fresh total (a.first),
-// n < 2^31 - 1024 (walk_ok).  The payloads are walked in groups of FW_G: the windows of the
+// 5..16 sparse payloads (fold_walk_kernel's conditions otherwise).  The payloads are walked in
+// groups of FW_G: the windows of the
 // group being folded and of the next group (of this tile, or group 0 of the next tile) are in
 // registers, so every window load is in flight while the group before it folds, with 16
 // registers of windows whatever the payload count.  Cursors live one per lane (lane p: payload
 // p) in one register.
 template <bool VEC, int EPL, bool ONE>
-__global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw) {
+__global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64_t tpw) {
   constexpr int TE = 64 * EPL;
   __shared__ float s_val[FW_WAVES][TE];
   __shared__ uint32_t s_tag[FW_WAVES][TE];
@@ -1187,7 +1397,7 @@ static inline int64_t fold_ntiles(int64_t n) { return (n + FOLD_TILE - 1) / FOLD
 // The walk fold's launch: EPL from the densest payload (~32 entries per payload per tile on
 // average at dens <= 0.125: 256-element tiles; denser payloads 128-element tiles); a
 // persistent grid of what the CUs hold, each wave a contiguous run of tiles.
-template <bool VEC, int EPL, bool ONE>
+template <bool VEC, int EPL, int NS>
 static int launch_walk_t(const FoldArgs& fa, hipStream_t st) {
   static int per = 0, cus = 0;
   if (per == 0) {
@@ -1195,7 +1405,9 @@ static int launch_walk_t(const FoldArgs& fa, hipStream_t st) {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fold_walk_kernel<VEC, EPL, ONE>, 256, 0) !=
+    const void* kf = NS <= 4 ? reinterpret_cast<const void*>(fold_walk_kernel<VEC, EPL, 4>)
+                             : reinterpret_cast<const void*>(fold_walk_groups_kernel<VEC, EPL, false>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kf, 256, 0) !=
             hipSuccess || per < 1)
       per = 1;
   }
@@ -1206,7 +1418,12 @@ static int launch_walk_t(const FoldArgs& fa, hipStream_t st) {
   if (blocks > need) blocks = need;
   if (blocks < 1) blocks = 1;
   const int64_t tpw = (ntl + blocks * FW_WAVES - 1) / (blocks * FW_WAVES);
-  DPZ_TIMED(DPZ_KT_FOLD, st, fold_walk_kernel<VEC, EPL, ONE><<<(unsigned)blocks, 256, 0, st>>>(fa, tpw));
+  if constexpr (NS <= 4) {
+    DPZ_TIMED(DPZ_KT_FOLD, st, fold_walk_kernel<VEC, EPL, NS><<<(unsigned)blocks, 256, 0, st>>>(fa, tpw));
+  } else {
+    DPZ_TIMED(DPZ_KT_FOLD, st,
+              fold_walk_groups_kernel<VEC, EPL, false><<<(unsigned)blocks, 256, 0, st>>>(fa, tpw));
+  }
   return DPZ_OK;
 }
 
@@ -1215,25 +1432,37 @@ static bool walk_ok(const FoldArgs& fa) {
          fa.n < (int64_t(1) << 31) - 1024;
 }
 
-template <bool ONE>
+template <int NS>
 static int launch_walk_o(const FoldArgs& fa, bool vec, int epl, hipStream_t st) {
   if (vec) {
-    if (epl == 16) return launch_walk_t<true, 16, ONE>(fa, st);
-    return epl == 4 ? launch_walk_t<true, 4, ONE>(fa, st) : launch_walk_t<true, 2, ONE>(fa, st);
+    switch (epl) {
+      case 16: return launch_walk_t<true, 16, NS>(fa, st);
+      case 8: return launch_walk_t<true, 8, NS>(fa, st);
+      case 4: return launch_walk_t<true, 4, NS>(fa, st);
+      default: return launch_walk_t<true, 2, NS>(fa, st);
+    }
   }
-  if (epl == 16) return launch_walk_t<false, 16, ONE>(fa, st);
-  return epl == 4 ? launch_walk_t<false, 4, ONE>(fa, st) : launch_walk_t<false, 2, ONE>(fa, st);
+  switch (epl) {
+    case 16: return launch_walk_t<false, 16, NS>(fa, st);
+    case 8: return launch_walk_t<false, 8, NS>(fa, st);
+    case 4: return launch_walk_t<false, 4, NS>(fa, st);
+    default: return launch_walk_t<false, 2, NS>(fa, st);
+  }
 }
 
-// ~10-32 entries per payload per tile on average: 1024-element tiles up to dens 0.03, 256 up to
-// 0.125, 128 beyond (full windows then rare; DPZ_FOLD_WALK_EPL forces 16 / 4 / 2)
+// The largest tile that holds about one 64-entry window per payload on average (the densest
+// payload, `dens`): fewer tiles mean fewer window loads and LDS passes per element, and an
+// overflowing window is re-read synchronously (measured on MI355X, tools/diag/walk_epl.sh).
 static int launch_walk(const FoldArgs& fa, bool vec, double dens, hipStream_t st) {
-  int epl = dens <= 0.03 ? 16 : (dens <= 0.125 ? 4 : 2);
-  if (const char* e = getenv("DPZ_FOLD_WALK_EPL")) {
-    const int v = atoi(e);
-    if (v == 16 || v == 4 || v == 2) epl = v;
+  // about 52 entries or fewer per payload and tile (M = 25 M: 16 x alpha 0.1 at 512-element tiles
+  // 215 us, 1024: 283, 256: 287; 3 x 0.1: 64 / 72 / 77 us)
+  const int epl = dens <= 0.055 ? 16 : (dens <= 0.105 ? 8 : (dens <= 0.21 ? 4 : 2));
+  int e = epl;
+  if (const char* s = getenv("DPZ_FOLD_WALK_EPL")) {
+    const int v = atoi(s);
+    if (v == 16 || v == 8 || v == 4 || v == 2) e = v;
   }
-  return fa.np <= FW_G ? launch_walk_o<true>(fa, vec, epl, st) : launch_walk_o<false>(fa, vec, epl, st);
+  return fa.np <= 4 ? launch_walk_o<4>(fa, vec, e, st) : launch_walk_o<16>(fa, vec, e, st);
 }
 
 // Replace-only decode of ONE sparse payload (reference PartialModel.py:257-303, T[idx] = params):
@@ -1356,7 +1585,8 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
       }
     // The walk fold (no offsets pre-pass) takes all-sparse groups of a fresh total where it
     // measured faster on MI355X (M = 25 M, tools/diag/fold_kinds.py): a node's few neighbours
-    // at any alpha, many payloads at dense alpha.  DPZ_FOLD_KIND=1 / 2 / 4 forces the classic /
+    // at any alpha; 16 payloads at alpha 0.02 .. 0.2 (the hit-chain fold below that, the phase
+    // fold above).  DPZ_FOLD_KIND=1 / 2 / 4 forces the classic /
     // 4-slot group / walk fold (A/B diagnostics; a forced kind that cannot take the group runs
     // the classic kernel).
     int64_t etot = 0;
@@ -1367,7 +1597,8 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
         if ((double)fa.p[i].k / (double)n > dens) dens = (double)fa.p[i].k / (double)n;
       }
     const int kind = getenv("DPZ_FOLD_KIND") ? atoi(getenv("DPZ_FOLD_KIND")) : 0;
-    bool use_walk = walk_ok(fa) && (fa.np <= 4 || (double)etot / (double)fa.np >= 0.05 * (double)n);
+    const double avg = fa.np > 0 ? (double)etot / (double)fa.np / (double)n : 0.0;
+    bool use_walk = walk_ok(fa) && (fa.np <= 4 || (avg >= 0.02 && avg <= 0.21));
     if (kind) use_walk = walk_ok(fa) && kind == 4;
     if (use_walk) {
       const int rc = launch_walk(fa, vec && n % 4 == 0, dens, st);

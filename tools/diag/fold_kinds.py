@@ -60,13 +60,17 @@ def main():
     dev = torch.device("cuda:0")
     m = 25_000_009
     kinds = os.environ.get("FOLD_KINDS", "0 1 2 4").split()
-    for mm, alpha, npay, nd in ((m, 0.01, 16, 0), (m, 0.03, 16, 0), (m, 0.05, 16, 0),
+    # FOLD_CASES="m:alpha:npay:ndense ..." replaces the default list
+    cases = [tuple(t(v) for t, v in zip((int, float, int, int), c.split(":")))
+             for c in os.environ.get("FOLD_CASES", "").split()]
+    for mm, alpha, npay, nd in cases or ((m, 0.01, 16, 0), (m, 0.03, 16, 0), (m, 0.05, 16, 0),
                                 (m, 0.1, 16, 0), (m, 0.2, 16, 0), (m, 0.3, 16, 0),
                                 (m, 0.01, 3, 0), (m, 0.1, 3, 0), (m, 0.3, 3, 0), (m, 0.4, 3, 0),
                                 (m, 0.1, 3, 1), (11_000_000, 0.01, 3, 0),
                                 (11_000_000, 0.01, 4, 0), (11_000_000, 0.01, 1, 0)):
         r = case(dev, mm, alpha, npay, nd, kinds)
-        print(json.dumps({"m": mm, "alpha": alpha, "npay": npay, "dense": nd, "kinds": r}),
+        print(json.dumps({"m": mm, "alpha": alpha, "npay": npay, "dense": nd,
+                          "walk_epl": os.environ.get("DPZ_FOLD_WALK_EPL"), "kinds": r}),
               flush=True)
 
 
