@@ -115,9 +115,13 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     (x, x0, counter, payload, output) so the timed working set is > 2x the 256 MiB Infinity
     Cache: every step streams its inputs from HBM, as a real round does after training.
 
-    Step i = node state i's round: top-k encode of its model (change vs x0, counter update) and
-    the replace decode of that payload over x0 (reference PartialModel.serialized_model +
-    deserialized_model).  The host loop over steps is native (dpz_encode_replace_batch, one
+    Step i = node state i's round: top-k encode of its model x (change vs x0, counter update)
+    and the replace decode of a neighbour's payload over x (reference
+    PartialModel.serialized_model + deserialized_model, whose base is the receiver's current
+    state_dict): the neighbour is the state encoded S steps earlier on the same stream.  The
+    decode's copy of x is written by the encoder's filter as it streams x (fused), so the step
+    moves 12N + 24k bytes; the line's frac_of_hbm_peak keeps SURVEY §8(d)'s unfused B = 16N + 16k
+    (decode materialised as in the reference) and the PMC traffic beside it is what moved.  The host loop over steps is native (dpz_encode_replace_batch, one
     ctypes call per R steps).  With S streams, S node codecs share the GPU (state i on stream
     i % S, its own workspace), as decentralizepy runs procs_per_machine nodes per machine; the
     one-stream (one node) rate is measured beside it and the faster of the two is the line's
@@ -130,6 +134,8 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     R = rotate or max(1, math.ceil(2 * L3_BYTES / per_set) + 1)
     S = max(1, streams)
     R = -(-R // S) * S                   # a state is only ever reused by the same stream
+    if S > 1:
+        R = max(R, 2 * S)                # a neighbour's payload is another state's
     g = torch.Generator(device=dev).manual_seed(seed)
     sets = []
     for _ in range(R):
@@ -141,7 +147,7 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
                          out=torch.empty(n, dtype=torch.float32, device=dev)))
     s_list = [torch.cuda.Stream(dev) for _ in range(S)]
     ws_list = [codec.Workspace(dev) for _ in range(S)]
-    multi = codec.NodeStepBatch(sets, n, k, s_list, ws_list)
+    multi = codec.NodeStepBatch(sets, n, k, s_list, ws_list, decode_src=lambda j: (j - S) % len(sets))
     # one node on one stream decodes a neighbour's payload (the previous state's, encoded in the
     # previous step on the same stream), so its decode is co-scheduled in its encode's launches
     one = codec.NodeStepBatch(sets, n, k, s_list[:1], ws_list[:1],
@@ -209,14 +215,19 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     # kernels then run back-to-back (no host-launch gaps inside a pair).  Encodes and decodes are
     # queued as separate loops: a one-stream step co-schedules the decode inside the encoder's
     # launches (dpz_encode_replace_batch), which would hide the replace kernel's own duration.
+    # The kernels of the one-node step as it runs (fused: the filter also writes the decode's
+    # copy of x, the select launch scatters the entries), then the standalone replace decode
+    # (the "fold" kernel, for the event-pair overhead below and the decode stage).
     with codec.KernelTimer() as kt:
         with torch.cuda.stream(stream):
             torch.cuda._sleep(int(200e6))  # ~0.1 s of GPU cycles while the steps are enqueued
-        run_steps(one, reps, DPZ_BATCH_ENCODE)
+        run_steps(one, reps)
         run_steps(one, reps, DPZ_BATCH_DECODE)
         torch.cuda.synchronize()
     kernels = {name: {"avg_us": ms / c * 1e3, "launches_per_step": c / reps}
                for name, (ms, c) in kt.result.items()}
+    if "fold" in kernels:  # the standalone decode's launches are not part of the step
+        kernels["fold"]["launches_per_step"] = 0.0 if fused_copy() else 1.0
     b_enc = 8 * n + 8 * k + 8 * k      # read x, x0; write idx, val; counter[idx] += 1 (r+w)
     b_dec = 8 * n + 8 * k              # read local, payload; write out
     fell_back |= multi.sticky_status(clear=True) != 0
@@ -291,12 +302,20 @@ def gossip_case(n, alpha, dev, rank, world, dist, rounds, warmup, exchange="allg
                 alg_bytes=len(adj) * (8 * n + 16 * k) + len(adj) * 8 * n + nsum * 8 * k)
 
 
+def fused_copy():
+    """The one-node step's decode copy is written by the encoder's filter (dpz_topk.hip
+    dpz_topk_encode_replace) unless disabled by the A/B switches."""
+    return os.environ.get("DPZ_FUSED_COPY", "1") != "0" and \
+        os.environ.get("DPZ_BATCH_COSCHED", "1") != "0"
+
+
 def kernel_alg_bytes(name, n, k):
     """Algorithmic HBM bytes of one launch: the bytes the operation must move,
     not what the implementation happens to move (candidate lists, histograms are excluded)."""
     return {
         "topk_sample": 8 * 65536,          # x, x0 at the 65,536 sampled positions
-        "topk_filter": 8 * n,              # read x, x0 once
+        # read x, x0 once (+ write the decode's copy of x when fused)
+        "topk_filter": 12 * n if fused_copy() else 8 * n,
         "topk_select": 0,                  # works on the ~1.9k candidates only
         "topk_resolve": 0,                 # works on the ~k/256 boundary entries only
         "topk_compact": 8 * k + 4 * k + 8 * k,  # write idx, val; gather vals; counter r+w
@@ -538,7 +557,7 @@ def main():
         # back-to-back average) and subtracted from every kernel's event-pair average, so the
         # averages are what rocprofv3 --kernel-trace reports (profiles/)
         bias = 0.0
-        if "fold" in kern and kern["fold"]["launches_per_step"] == 1.0:
+        if "fold" in kern:
             bias = max(0.0, kern["fold"]["avg_us"] - t_dec * 1e6)
         for name, kv in kern.items():
             b = kernel_alg_bytes(name, r["n"], r["k"])
@@ -578,12 +597,14 @@ def main():
                 "parallelism": (f"{world} GPU(s) x {r['streams']} concurrent node codecs (one "
                                 f"stream each), no collective" if r["mode"] == "multi" else
                                 f"{world} GPU(s) x 1 node codec, no collective"),
-                "launch": ("native batched enqueue (dpz_encode_replace_batch); step i = encode -> "
-                           f"replace decode of node state i on stream i % {r['streams']}"
+                "launch": ("native batched enqueue (dpz_encode_replace_batch); step i = encode "
+                           f"of node state i with the replace decode of state i - {r['streams']}'s "
+                           f"payload over its x fused in, on stream i % {r['streams']}"
                            if r["mode"] == "multi" else
                            "native batched enqueue (dpz_encode_replace_batch), one stream; "
                            "step i = encode of node state i with the replace decode of state "
-                           "i - 1's payload co-scheduled in the encoder's launches"),
+                           "i - 1's payload over state i's x fused into the encoder's launches "
+                           "(filter writes the copy of x, select scatters the entries)"),
                 "rotated_states": r["rotate"],
                 "timing": (f"median of {r['repeats']} timed regions of exactly {args.steps} "
                            f"steps (each: barrier + synchronize on both sides, max over ranks)"),

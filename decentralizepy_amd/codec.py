@@ -192,7 +192,9 @@ def topk_sticky_status(workspace, clear=False):
 class NodeStepBatch:
     """A prepared native enqueue of m node codec steps (dpz_encode_replace_batch): node j encodes
     ``nodes[j]["x"]`` (change vs ``x0``, counter update) into its payload ``idx``/``val`` and
-    replace-decodes ``decode_src(j)``'s payload over ``x0`` into ``out``, on
+    replace-decodes ``decode_src(j)``'s payload over its current model ``x`` into ``out`` (the
+    reference's deserialized_model starts from the receiver's state_dict, PartialModel.py:278-295;
+    with ``decode_src(j) != j`` the encoder's filter writes the copy of ``x``), on
     ``streams[j % len(streams)]`` with that stream's workspace.  The pointer arrays are built
     once; :meth:`run` is one ctypes call whatever m is (the host loop is native)."""
 
@@ -217,7 +219,7 @@ class NodeStepBatch:
                         for d in nodes])
         self._idx = P(*[d["idx"].data_ptr() for d in nodes])
         self._val = P(*[d["val"].data_ptr() for d in nodes])
-        self._rl = P(*[d["x0"].data_ptr() for d in nodes])
+        self._rl = P(*[d["x"].data_ptr() for d in nodes])
         self._ri = P(*[nodes[src(j)]["idx"].data_ptr() for j in range(m)])
         self._rv = P(*[nodes[src(j)]["val"].data_ptr() for j in range(m)])
         self._ro = P(*[d["out"].data_ptr() for d in nodes])

@@ -76,15 +76,21 @@ extern "C" int dpz_encode_replace_batch(int m, int what, const float* const* x,
   // MI355X).  On several streams the other nodes' streaming already fills the tails, and the
   // plain launches measured faster (C2 3 streams: 41.9 vs 42.7 us).  DPZ_BATCH_COSCHED=0 / 1
   // forces the stream rule (never the independence rule).
+  // A node decoding over the model it encodes (r_local[j] == x[j], the reference's
+  // deserialized_model base) takes the fused call on any stream count: the encoder's filter
+  // writes the decode's copy of x as it streams x (dpz_topk_encode_replace).
   static const int cs_env = getenv("DPZ_BATCH_COSCHED") ? atoi(getenv("DPZ_BATCH_COSCHED")) : -1;
   const bool cosched = cs_env >= 0 ? cs_env != 0 : n_streams == 1;
   for (int j = 0; j < m; ++j) {
     const int q = j % n_streams;
-    if (cosched && (what & DPZ_BATCH_ENCODE) && (what & DPZ_BATCH_DECODE) &&
-        r_idx[j] != idx_out[j] && r_val[j] != val_out[j]) {
+    const bool both = (what & DPZ_BATCH_ENCODE) && (what & DPZ_BATCH_DECODE) &&
+                      r_idx[j] != idx_out[j] && r_val[j] != val_out[j];
+    const bool fused = both && r_local[j] == x[j] && cs_env != 0;
+    if (both && (cosched || fused)) {
+      const int fl = DPZ_TOPK_ASYNC | (n_streams > 1 ? DPZ_TOPK_SHARED : 0);
       int rc = dpz_topk_encode_replace(x[j], x0 ? x0[j] : nullptr, nullptr, DPZ_ACC_NONE, x[j], n,
                                        k, idx_out[j], val_out[j], counter ? counter[j] : nullptr,
-                                       ws[q], ws_bytes, DPZ_TOPK_ASYNC, r_local[j], r_idx[j],
+                                       ws[q], ws_bytes, fl, r_local[j], r_idx[j],
                                        r_val[j], r_k, n, r_out[j], dws[q], dws_bytes, streams[q]);
       if (rc != DPZ_OK) return rc;
       continue;

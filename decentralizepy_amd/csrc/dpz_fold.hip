@@ -854,10 +854,10 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_group_kernel(FoldArgs a)
 //      total += t_p*w_p;  total += w_self * local
 //    (no block barrier: the row is the wave's own, LDS ops of one wave run in order).
 // A window whose 64 entries all fall inside the tile (dense tiles) is followed by synchronous
-// extra windows (correct, slower); EPL is chosen so a tile holds ~32 entries per payload on
-// average.  Invalid payloads (unsorted / out of range) cannot write out of bounds.
+// extra windows (correct, slower); EPL is chosen so a tile holds ~52 entries or fewer per
+// payload on average (launch_walk).  Invalid payloads (unsorted / out of range) cannot write out
+// of bounds.
 constexpr int FW_WAVES = 4;  // waves per block (256 threads)
-constexpr int FW_DMAX = 4;   // dense payloads per group on this path
 
 template <int EPL>
 struct FwV {

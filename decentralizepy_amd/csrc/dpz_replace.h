@@ -42,9 +42,12 @@ struct ReplaceJob {
   int add;         // 0: out = local with entries replaced; 1: out = local + T (T zero-based)
   int64_t off;     // payload indices are global; element i of local / out is global off + i
                    // (a rank's slice of a sharded model; entries outside [0, n) are skipped)
+  int scatter;     // 1: out already holds local (the encoder's filter copied it while streaming
+                   // the same tensor): only the entries are written, 64 per chunk (replace only)
 };
 
 static inline int64_t replace_chunks(int64_t k) { return (k + RP_E - 1) / RP_E; }
+static inline int64_t scatter_chunks(int64_t k) { return (k + 63) / 64; }
 
 // A chunk's entries, one per lane: rel = index relative to the slice, clamped to [-1, n] (lanes
 // past the chunk's end hold INT32_MAX), ev = value; bnext = the next chunk's first index (the
@@ -180,6 +183,17 @@ __device__ __forceinline__ void replace_block(const ReplaceJob& j, int64_t p) {
   const int64_t c = j.c0 + p * per + (threadIdx.x >> 6);
   if (c >= j.c1) return;
   const int lane = threadIdx.x & 63;
+  if (j.scatter) {
+    // out[idx[e]] = val[e] for the chunk's 64 entries; of equal (adjacent, the indices are
+    // sorted) indices the last entry wins, as in the sequential `T[idx] = params`
+    const int64_t e = c * 64 + lane;
+    if (e < j.k) {
+      const int64_t i = (int64_t)j.idx[e] - j.off;
+      const bool last = e + 1 >= j.k || j.idx[e + 1] != j.idx[e];
+      if (last && i >= 0 && i < j.n) j.out[i] = j.val[e];
+    }
+    return;
+  }
   const RpChunk ch = rp_load(j, c, lane);
   rp_stream(j, c, lane, ch);
 }

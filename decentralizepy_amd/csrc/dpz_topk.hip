@@ -174,10 +174,19 @@ extern "C" int dpz_topk_encode_replace(const float* x, const float* x0, float* a
       overlaps(r_out, ob, idx_out, (size_t)k * 4) || overlaps(r_out, ob, val_out, (size_t)k * 4) ||
       overlaps(r_out, ob, ws, ws_bytes) || overlaps(r_out, ob, r_ws, r_ws_bytes))
     return DPZ_ERR_ARG;
-  const ReplaceJob job{r_local, r_idx, r_val, r_k, r_n, r_out, 0, replace_chunks(r_k), 0};
+  ReplaceJob job{r_local, r_idx, r_val, r_k, r_n, r_out, 0, replace_chunks(r_k), 0};
   const bool r_vec = ((reinterpret_cast<uintptr_t>(r_local) | reinterpret_cast<uintptr_t>(r_out)) & 15u) == 0;
   const bool carried = n > 0 && k > 0 && r_k > 0 && r_vec && !(flags & DPZ_TOPK_EXACT) &&
                        use_sampled(n, k);
+  // Decoding over the very tensor being encoded (reference: deserialized_model starts from the
+  // node's current state_dict, the model its serialized_model just encoded): the filter, which
+  // streams x anyway, writes out = x, and only the payload entries are scattered afterwards —
+  // 4n bytes of reads fewer than an independent replace (DPZ_FUSED_COPY=0 disables, A/B).
+  const char* fe = getenv("DPZ_FUSED_COPY");
+  if (carried && (!fe || atoi(fe) != 0) && r_local == x && r_n == n && acc_mode == DPZ_ACC_NONE) {
+    job.scatter = 1;
+    job.c1 = scatter_chunks(r_k);
+  }
   if (!carried) {  // run it on its own first (same stream), then the plain encode
     const float* vp = r_val;
     const int32_t* ip = r_idx;

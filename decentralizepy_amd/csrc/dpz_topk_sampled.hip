@@ -236,7 +236,7 @@ template <bool VEC, bool ACC, int G>
 __global__ void __launch_bounds__(256, ACC ? 4 : FOCC) sampled_filter_kernel(
     KeySrc s, int64_t n, uint32_t r_lo, uint32_t r_hi, int64_t W, int64_t R, int64_t CAP,
     TopkCtrl* ctrl, const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt,
-    uint32_t* cidx, uint32_t* ckey, float* cval) {
+    uint32_t* cidx, uint32_t* ckey, float* cval, float* __restrict__ copy_out) {
   __shared__ uint32_t h[HBR];
   __shared__ uint32_t win[4];
   __shared__ uint32_t wsum[16];
@@ -278,6 +278,19 @@ __global__ void __launch_bounds__(256, ACC ? 4 : FOCC) sampled_filter_kernel(
     for (int q = 0; q < G; ++q) {
       uint32_t kq[4];
       const int cq = raw[q].cnt;
+      if (copy_out) {  // fused replace decode over this same tensor: out = x while x streams by
+        const int64_t i0 = base + q * 256 + lane * 4;
+        if (VEC && cq == 4) {
+          typedef float v4f __attribute__((ext_vector_type(4)));
+          const v4f v = {raw[q].a.x, raw[q].a.y, raw[q].a.z, raw[q].a.w};
+          __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(copy_out + i0));
+        } else {
+          const float xv[4] = {raw[q].a.x, raw[q].a.y, raw[q].a.z, raw[q].a.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (e < cq) copy_out[i0 + e] = xv[e];
+        }
+      }
       if (cq) finish_keys4<VEC, ACC>(s, base + q * 256 + lane * 4, store_acc, raw[q], kq);
       bool f[4];
       uint32_t pre = 0, tot = 0;
@@ -1110,10 +1123,18 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
   // (sample, select, resolve, compact) and run in blocks appended after each launch's own
   ReplaceJob jb[3] = {};
   unsigned pb[3] = {0, 0, 0};
+  // a scatter job (dpz_topk_encode_replace over the tensor being encoded): the filter writes
+  // out = x as it streams x, and the entries are scattered in the select launch (after it)
+  float* copy_out = (a.job && phases == 3 && a.job->scatter) ? a.job->out : nullptr;
   if (a.job && phases == 3) {
     const int64_t C = a.job->c1 - a.job->c0;
     double f[3];
     cosched_shares(f);
+    if (copy_out) {
+      f[0] = 0.0;
+      f[1] = 1.0;
+      f[2] = 0.0;
+    }
     const int per[3] = {4, 16, 4};  // chunks per appended block (one per wave)
     int64_t c = a.job->c0;
     double acc_f = 0.0;
@@ -1136,10 +1157,12 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
     window_ranks(a.n, a.k, &r_lo, &r_hi);
     if (a.acc_mode == DPZ_ACC_NONE)
       DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC, false, FG><<<nb, 256, 0, a.st>>>(
-          s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval));
+          s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval,
+          copy_out));
     else
       DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC, true, 3><<<nb, 256, 0, a.st>>>(
-          s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval));
+          s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval,
+          copy_out));
   }
   if (!(phases & 2)) return DPZ_OK;
   s.rekey = 1;

@@ -31,7 +31,8 @@ def test_node_step_batch_matches_oracle(dev, streams):
     nodes = [_node(dev, n, k, 40 + j) for j in range(m)]
     ss = [torch.cuda.Stream(dev) for _ in range(streams)]
     ws = [codec.Workspace(dev) for _ in range(streams)]
-    # every node decodes its own payload after its encode (the bench's step)
+    # every node decodes its own payload after its encode (not fused: the payload is the
+    # encode's own output)
     b = codec.NodeStepBatch(nodes, n, k, ss, ws)
     b.sticky_status(clear=True)
     for _ in range(2):  # twice: counters accumulate, workspaces are reused
@@ -47,18 +48,22 @@ def test_node_step_batch_matches_oracle(dev, streams):
         np.testing.assert_array_equal(d["idx"].cpu().numpy(), oi)
         np.testing.assert_array_equal(_bits(d["val"].cpu().numpy()), _bits(ov))
         np.testing.assert_array_equal(d["counter"].cpu().numpy(), cnt)
-        ref = ofold.replace(x0, oi, ov)
+        ref = ofold.replace(x, oi, ov)
         np.testing.assert_array_equal(_bits(d["out"].cpu().numpy()), _bits(ref))
 
 
-def test_node_step_batch_one_stream_neighbour_decode(dev):
-    """One stream, node j decoding node j - 1's payload: the decode is co-scheduled inside the
-    encode's launches (dpz_encode_replace_batch) and still equals encode + replace."""
+@pytest.mark.parametrize("streams", [1, 3])
+def test_node_step_batch_neighbour_decode(dev, streams):
+    """Node j decoding node j - S's payload over its own x (S streams): the decode is fused
+    into the encode (the filter writes the copy of x, select scatters the entries;
+    dpz_encode_replace_batch) and still equals encode + replace."""
     from decentralizepy_amd import codec
-    n, k, m = 1_000_003, 10_000, 4
+    n, k, m = 1_000_003, 10_000, 2 * streams if streams > 1 else 4
+    S = streams
     nodes = [_node(dev, n, k, 60 + j) for j in range(m)]
-    b = codec.NodeStepBatch(nodes, n, k, [torch.cuda.Stream(dev)], [codec.Workspace(dev)],
-                            decode_src=lambda j: (j - 1) % m)
+    b = codec.NodeStepBatch(nodes, n, k, [torch.cuda.Stream(dev) for _ in range(S)],
+                            [codec.Workspace(dev) for _ in range(S)],
+                            decode_src=lambda j: (j - S) % m)
     b.sticky_status(clear=True)
     for _ in range(2):  # node 0 reads node m-1's payload of the previous run
         b.run()
@@ -69,9 +74,9 @@ def test_node_step_batch_one_stream_neighbour_decode(dev):
         oi, ov = otopk.encode(d["x"].cpu().numpy(), d["x0"].cpu().numpy(), None, 0, k)
         ref.append((oi, ov))
     for j, d in enumerate(nodes):
-        oi, ov = ref[(j - 1) % m]
+        oi, ov = ref[(j - S) % m]
         np.testing.assert_array_equal(_bits(d["out"].cpu().numpy()),
-                                      _bits(ofold.replace(d["x0"].cpu().numpy(), oi, ov)))
+                                      _bits(ofold.replace(d["x"].cpu().numpy(), oi, ov)))
         np.testing.assert_array_equal(d["idx"].cpu().numpy(), ref[j][0])
 
 
@@ -95,7 +100,7 @@ def test_node_step_batch_encode_only_and_decode_only(dev):
     x0 = nodes[0]["x0"].cpu().numpy()
     oi, ov = otopk.encode(x, x0, None, 0, k)
     np.testing.assert_array_equal(_bits(nodes[0]["out"].cpu().numpy()),
-                                  _bits(ofold.replace(x0, oi, ov)))
+                                  _bits(ofold.replace(x, oi, ov)))
 
 
 def test_sticky_status_records_an_uncompleted_miss(dev):

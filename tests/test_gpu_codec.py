@@ -671,6 +671,47 @@ def test_coscheduled_replace_rejects_aliasing(dev):
         codec.topk_encode(tx, 10_000, x0=tx0, co_replace=(tx0.clone(), p_idx, p_val, tx))
 
 
+@pytest.mark.parametrize("n,alpha,rk,dup,layout", [
+    (11_000_000, 0.01, 110_000, False, None),      # C2: the bench's one-node step
+    (16_777_216, 0.01, 167_772, False, None),      # 64 MiB
+    (1_000_001, 0.01, 7_000, True, None),          # ragged n; adjacent duplicate indices
+    (1_000_003, 0.01, 0, False, None),             # empty payload: the copy only
+    (1 << 20, 0.01, 9_000, False, "miss"),         # sampled window misses: exact re-run
+])
+def test_encode_with_fused_replace(dev, n, alpha, rk, dup, layout):
+    """Decoding over the tensor being encoded (co_replace local is x): the encoder's filter
+    writes out = x as it streams x and the select launch scatters the entries
+    (dpz_topk_encode_replace); equals encode + T = x.copy(); T[idx] = vals, bit-exact."""
+    codec = _codec()
+    k = round(alpha * n)
+    if layout == "miss":
+        from tests.layouts import miss_layout
+        x, _ = miss_layout(n, k)
+        x0 = None
+    else:
+        x, x0 = _inputs(n, 9)
+    o_cnt = np.zeros(n, dtype=np.int32)
+    oi, ov = otopk.encode(x, x0, None, 0, k, counter=o_cnt)
+    ridx, rvals = _payload(n, rk, seed=4, local=x)
+    if dup and rk > 2:  # entries j and j + 1 share an index: the later value wins
+        ridx[rk // 2 + 1] = ridx[rk // 2]
+        ridx[-1] = ridx[-2]
+    ref = ofold.replace(x, ridx, rvals)
+    tx = torch.from_numpy(x).to(dev)
+    tx0 = torch.from_numpy(x0).to(dev) if x0 is not None else None
+    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    out = torch.full_like(tx, float("nan"))
+    ws = codec.Workspace(dev)
+    idx, val = codec.topk_encode(tx, k, x0=tx0, counter=cnt, workspace=ws,
+                                 co_replace=(tx, torch.from_numpy(ridx).to(dev),
+                                             torch.from_numpy(rvals).to(dev), out))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(idx.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(val.cpu().numpy()), _bits(ov))
+    np.testing.assert_array_equal(cnt.cpu().numpy(), o_cnt)
+    np.testing.assert_array_equal(_bits(out.cpu().numpy()), _bits(ref))
+
+
 def _sampled_status(ws):
     return int(ws.buf[8:12].view(torch.int32).item())
 

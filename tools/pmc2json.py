@@ -12,7 +12,8 @@ import sys
 NAMES = {"sampled_sample_kernel": "topk_sample", "sampled_filter_kernel": "topk_filter",
          "sampled_select_kernel": "topk_select", "sampled_resolve_kernel": "topk_resolve",
          "sampled_compact_kernel": "topk_compact", "fold_offsets_kernel": "fold_offsets",
-         "fold_kernel": "fold", "fold_group_kernel": "fold_group", "fold_slots_kernel": "fold_slots", "replace_kernel": "fold", "dwt_kernel": "dwt", "dwt4_kernel": "dwt",
+         "fold_kernel": "fold", "fold_group_kernel": "fold_group", "fold_slots_kernel": "fold_slots",
+         "fold_walk_kernel": "fold_walk", "fold_walk_groups_kernel": "fold_walk", "replace_kernel": "fold", "dwt_kernel": "dwt", "dwt4_kernel": "dwt",
          "haar_dwt_kernel": "haar_dwt", "haar_idwt_kernel": "haar_idwt",
          "idwt_kernel": "idwt"}
 
