@@ -347,6 +347,149 @@ __global__ void __launch_bounds__(256, ACC ? 4 : FOCC) sampled_filter_kernel(
   STAMP_W(5);
 }
 
+// One float4 group's keys kq (valid elements e < cq, index i0 + e, values xv) into the wave's
+// candidate list: keys >= lo are staged in index order (ballot + mbcnt), or counted into the
+// window histogram once the segment is DENSE.
+__device__ __forceinline__ void stage_group(WaveList& L, uint32_t* h, const uint32_t (&kq)[4],
+                                            const float (&xv)[4], int cq, uint32_t i0, int lane,
+                                            uint32_t lo, uint32_t hi, uint32_t shift, int64_t CAP,
+                                            uint32_t& run, bool& dense) {
+  bool f[4];
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    f[e] = e < cq && kq[e] >= lo;
+    const uint64_t m = __ballot(f[e]);
+    pre += mbcnt64(m);
+    tot += (uint32_t)__popcll(m);
+  }
+  if (!tot) return;
+  if (!dense && run + tot <= (uint32_t)CAP && tot <= (uint32_t)STAGE) {
+    if (L.staged + tot > STAGE) L.flush(lane, true, h, lo, hi, shift);
+    uint32_t p = L.staged + pre;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (f[e]) {
+        L.stg[p] = i0 + e;
+        L.stg[STAGE + p] = kq[e];
+        L.stg[2 * STAGE + p] = __float_as_uint(xv[e]);
+        ++p;
+      }
+    }
+    L.staged += tot;
+  } else {
+    if (!dense) L.flush(lane, false, h, lo, hi, shift);
+    dense = true;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (f[e]) atomicAdd(&h[fine_bin(kq[e], lo, hi, shift)], 1u);
+  }
+  run += tot;
+}
+
+// Software-pipelined filter for the PartialModel step (16-byte aligned operands, no
+// accumulation; with or without the fused copy): every stream load is branch-free — lanes past
+// the segment's last whole float4 read element 0 and are masked — so the compiler's wait counts
+// track them, and the NEXT groups' loads are in flight while this group is copied, keyed and
+// staged.  (sampled_filter_kernel loads G groups, then waits for all of them — vmcnt(0) under
+// its ragged-element branches — and has nothing in flight while it processes them.)  The < 4
+// elements past the last whole float4 of [0, n) are handled after the loop, by the last segment.
+template <bool X0, bool COPY, int G>
+__global__ void __launch_bounds__(256, FOCC) sampled_filter_pipe_kernel(
+    KeySrc s, int64_t n, uint32_t r_lo, uint32_t r_hi, int64_t W, int64_t R, int64_t CAP,
+    TopkCtrl* ctrl, const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt,
+    uint32_t* cidx, uint32_t* ckey, float* cval, float* __restrict__ copy_out) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  __shared__ uint32_t h[HBR];
+  __shared__ uint32_t win[4];
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t st[4][3 * STAGE];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int b = threadIdx.x; b < HBR; b += 256) h[b] = 0;
+  const int64_t seg = (int64_t)blockIdx.x * 4 + wid;
+  const int64_t beg = seg * R;  // a multiple of 4 (R is); >= n for the grid's spare waves
+  const int64_t end = (beg + R < n) ? beg + R : n;
+  const int64_t end4 = beg < end ? beg + ((end - beg) & ~int64_t(3)) : beg;
+  uint4 cv[2];
+  {
+    const uint4* c4 = reinterpret_cast<const uint4*>(chist) + (510 - 2 * threadIdx.x);
+    cv[0] = c4[0];
+    cv[1] = c4[1];
+  }
+  const v4f* __restrict__ xa = reinterpret_cast<const v4f*>(s.x);
+  const v4f* __restrict__ xb = reinterpret_cast<const v4f*>(s.x0);
+  v4f ca[G], cb[G];
+  auto ld = [&](int64_t base, v4f (&a)[G], v4f (&b)[G]) {
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      const int64_t i0 = base + q * 256 + lane * 4;
+      const int64_t g4 = (i0 < end4 ? i0 : 0) >> 2;
+      a[q] = __builtin_nontemporal_load(xa + g4);
+      if (X0) b[q] = __builtin_nontemporal_load(xb + g4);
+    }
+  };
+  ld(beg, ca, cb);
+  block_window(cv, r_lo, r_hi, win, wsum);
+  const uint32_t lo = win[0], hi = win[1], shift = win[2];
+  if (seg == 0 && lane == 0) {
+    ctrl->lo = lo;
+    ctrl->hi = hi;
+    ctrl->shift = shift;
+  }
+  WaveList L{cidx + seg * CAP, ckey + seg * CAP, cval ? cval + seg * CAP : nullptr, st[wid], 0u,
+             0u};
+  uint32_t run = 0;
+  bool dense = false;
+  auto proc = [&](const v4f (&a)[G], const v4f (&b)[G], int64_t base) {
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      const int64_t i0 = base + q * 256 + lane * 4;
+      const int cq = i0 < end4 ? 4 : 0;
+      if (COPY && cq) __builtin_nontemporal_store(a[q], reinterpret_cast<v4f*>(copy_out) + (i0 >> 2));
+      const float xv[4] = {a[q].x, a[q].y, a[q].z, a[q].w};
+      uint32_t kq[4];
+      if (X0) {
+        const float bv[4] = {b[q].x, b[q].y, b[q].z, b[q].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) kq[e] = key_of(xv[e] - bv[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) kq[e] = key_of(xv[e]);
+      }
+      stage_group(L, h, kq, xv, cq, (uint32_t)i0, lane, lo, hi, shift, CAP, run, dense);
+    }
+  };
+  // ping-pong buffers, unrolled by two so no register copy waits on a load in flight
+  v4f pa[G], pb[G];
+  for (int64_t base = beg; base < end4; base += 2 * G * 256) {
+    ld(base + G * 256, pa, pb);
+    proc(ca, cb, base);
+    ld(base + 2 * G * 256, ca, cb);
+    proc(pa, pb, base + G * 256);
+  }
+  if (end4 < end) {  // the last segment's ragged 1-3 elements
+    const int64_t i = end4 + lane;
+    const bool v = i < end;
+    float xv[4] = {0.f, 0.f, 0.f, 0.f};
+    uint32_t kq[4] = {0u, 0u, 0u, 0u};
+    if (v) {
+      xv[0] = s.x[i];
+      kq[0] = key_of(X0 ? xv[0] - s.x0[i] : xv[0]);
+      if (COPY) copy_out[i] = xv[0];
+    }
+    // one element per lane: lane order is index order
+    stage_group(L, h, kq, xv, v ? 1 : 0, (uint32_t)i, lane, lo, hi, shift, CAP, run, dense);
+  }
+  if (!dense) L.flush(lane, true, h, lo, hi, shift);
+  __syncthreads();
+  uint32_t* gcopy = ghist + (blockIdx.x & (GH_COPIES - 1)) * GH_STRIDE;
+  for (int b = threadIdx.x; b < HBR; b += 256) {
+    const uint32_t v = h[b];
+    if (v) atomicAdd(&gcopy[b], v);
+  }
+  if (lane == 0 && seg < W) segcnt[seg] = dense ? DENSE : run;
+}
+
 // Wave-level threshold bin from the global window histogram gh (LDS, HB fine bins + the
 // above-window count `above`): lane l holds the HB/64 bins [HB - HB/64 (l + 1), HB - HB/64 l).
 __device__ __forceinline__ bool wave_bstar(const uint32_t* gh, uint32_t above, uint32_t k,
@@ -1006,8 +1149,27 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
       }
     }
   }
-  // count pass (the first PFC chunks from registers), in-block offsets, write pass
   auto is_sel = [&](uint32_t key, uint32_t idx) { return key > T || (key == T && idx <= icut); };
+  // counter updates of the register-held candidates first: the kernel cannot retire before its
+  // scattered memory-side atomics (or stores) land, so they drain while the count and write
+  // passes run (the write pass skips them)
+  if (counter) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t seg = seg0 + u;
+      if (seg < W && cnt[u] != DENSE) {
+#pragma unroll
+        for (int c = 0; c < PFC; ++c) {
+          const uint32_t j = c * 64u + lane;
+          if (j < cnt[u] && is_sel(kk[u][c], ii[u][c])) {
+            if (PLAIN) counter[ii[u][c]] = (int32_t)(cc[u][c] + 1u);  // unique indices: no race
+            else atomicAdd(&counter[ii[u][c]], 1);  // non-returning
+          }
+        }
+      }
+    }
+  }
+  // count pass (the first PFC chunks from registers), in-block offsets, write pass
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int64_t seg = seg0 + u;
@@ -1047,7 +1209,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
           if (pos < (uint64_t)k) {
             idx_out[pos] = (int32_t)idx;
             val_out[pos] = (cval || pre) ? v : vals_src[idx];
-            if (counter) {
+            if (counter && !pre) {  // register-held chunks (pre) were counted up front
               if (PLAIN) counter[idx] = (int32_t)(cw + 1u);  // unique indices: no race
               else atomicAdd(&counter[idx], 1);  // non-returning: no round trip to wait on
             }
@@ -1131,9 +1293,14 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
     double f[3];
     cosched_shares(f);
     if (copy_out) {
+      // the scatter must follow the filter's copy: blocks appended to compact (default; the
+      // latency-bound compact leaves most CU slots free: C2 one-node step 57.2 -> 55.6 us on
+      // MI355X vs appended to select) or select (DPZ_SCATTER_AT=select, A/B diagnostics)
+      const char* e = getenv("DPZ_SCATTER_AT");
+      const bool at_compact = !(e && e[0] == 's');
       f[0] = 0.0;
-      f[1] = 1.0;
-      f[2] = 0.0;
+      f[1] = at_compact ? 0.0 : 1.0;
+      f[2] = at_compact ? 1.0 : 0.0;
     }
     const int per[3] = {4, 16, 4};  // chunks per appended block (one per wave)
     int64_t c = a.job->c0;
@@ -1155,7 +1322,27 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
         s, a.n, ctrl, chist, ghist, blcnt, jb[0]));
     uint32_t r_lo, r_hi;
     window_ranks(a.n, a.k, &r_lo, &r_hi);
-    if (a.acc_mode == DPZ_ACC_NONE)
+    // DPZ_FILTER_PIPE=0 / 1 / 2: the batched filter / the pipelined one with 1 / 2 float4 groups
+    // per step (A/B diagnostics)
+    static const int pipe = getenv("DPZ_FILTER_PIPE") ? atoi(getenv("DPZ_FILTER_PIPE")) : 1;
+    if (VEC && a.acc_mode == DPZ_ACC_NONE && pipe > 0) {
+      const bool x0 = a.x0 != nullptr;
+#define DPZ_PIPE(X0_, CP_, G_)                                                                   \
+  DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_pipe_kernel<X0_, CP_, G_><<<nb, 256, 0, a.st>>>( \
+      s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval, copy_out))
+      if (pipe == 2) {
+        if (x0 && copy_out) DPZ_PIPE(true, true, 2);
+        else if (x0) DPZ_PIPE(true, false, 2);
+        else if (copy_out) DPZ_PIPE(false, true, 2);
+        else DPZ_PIPE(false, false, 2);
+      } else {
+        if (x0 && copy_out) DPZ_PIPE(true, true, 1);
+        else if (x0) DPZ_PIPE(true, false, 1);
+        else if (copy_out) DPZ_PIPE(false, true, 1);
+        else DPZ_PIPE(false, false, 1);
+      }
+#undef DPZ_PIPE
+    } else if (a.acc_mode == DPZ_ACC_NONE)
       DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC, false, FG><<<nb, 256, 0, a.st>>>(
           s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval,
           copy_out));

@@ -671,17 +671,22 @@ def test_coscheduled_replace_rejects_aliasing(dev):
         codec.topk_encode(tx, 10_000, x0=tx0, co_replace=(tx0.clone(), p_idx, p_val, tx))
 
 
+@pytest.mark.parametrize("where", ["select", "compact"])
 @pytest.mark.parametrize("n,alpha,rk,dup,layout", [
     (11_000_000, 0.01, 110_000, False, None),      # C2: the bench's one-node step
     (16_777_216, 0.01, 167_772, False, None),      # 64 MiB
     (1_000_001, 0.01, 7_000, True, None),          # ragged n; adjacent duplicate indices
     (1_000_003, 0.01, 0, False, None),             # empty payload: the copy only
     (1 << 20, 0.01, 9_000, False, "miss"),         # sampled window misses: exact re-run
+    (11_000_000, 0.01, 5, True, None),             # far fewer entries than wave segments
+    (11_000_000, 0.01, 110_000, True, "cluster"),  # entries packed at both ends: long gaps
 ])
-def test_encode_with_fused_replace(dev, n, alpha, rk, dup, layout):
+def test_encode_with_fused_replace(dev, n, alpha, rk, dup, layout, where, monkeypatch):
     """Decoding over the tensor being encoded (co_replace local is x): the encoder's filter
-    writes out = x as it streams x and the select launch scatters the entries
-    (dpz_topk_encode_replace); equals encode + T = x.copy(); T[idx] = vals, bit-exact."""
+    writes out = x as it streams x and the select launch (or, DPZ_SCATTER_AT=compact, the
+    compact launch) scatters the entries (dpz_topk_encode_replace); equals encode +
+    T = x.copy(); T[idx] = vals, bit-exact."""
+    monkeypatch.setenv("DPZ_SCATTER_AT", where)
     codec = _codec()
     k = round(alpha * n)
     if layout == "miss":
@@ -693,6 +698,11 @@ def test_encode_with_fused_replace(dev, n, alpha, rk, dup, layout):
     o_cnt = np.zeros(n, dtype=np.int32)
     oi, ov = otopk.encode(x, x0, None, 0, k, counter=o_cnt)
     ridx, rvals = _payload(n, rk, seed=4, local=x)
+    if layout == "cluster":  # most entries in the first 1 %, the rest in the last 0.1 %
+        rng = np.random.default_rng(5)
+        a = rng.choice(n // 100, size=rk - rk // 10, replace=False)
+        b = n - 1 - rng.choice(n // 1000, size=rk // 10, replace=False)
+        ridx = np.sort(np.concatenate([a, b])).astype(np.int32)
     if dup and rk > 2:  # entries j and j + 1 share an index: the later value wins
         ridx[rk // 2 + 1] = ridx[rk // 2]
         ridx[-1] = ridx[-2]
