@@ -1,5 +1,7 @@
 // Shared declarations of the top-k encoder (exact + sampled paths). See dpz_topk.hip.
 #pragma once
+#include <cstdlib>
+
 #include "dpz_common.h"
 #include "dpz_replace.h"
 
@@ -199,7 +201,11 @@ struct FastGeom {
 static inline FastGeom fast_geom(int64_t n, int64_t k = 0, bool shared = false) {
   FastGeom g;
   int64_t W = (n + W_MIN_RANGE - 1) / W_MIN_RANGE;
-  const int64_t wmax = (shared && n <= W_SMALL_N) ? W_SMALL : W_MAX;
+  // DPZ_WLONE=N caps a lone codec's grid at N segments (A/B diagnostics)
+  static const int64_t wlone = getenv("DPZ_WLONE") ? atoll(getenv("DPZ_WLONE")) : 0;
+  const int64_t wmax = (shared && n <= W_SMALL_N)
+                           ? W_SMALL
+                           : ((wlone > 0 && wlone < W_MAX) ? wlone : W_MAX);
   if (W > wmax) W = wmax;
   if (W < 1) W = 1;
   int64_t R = (n + W - 1) / W;

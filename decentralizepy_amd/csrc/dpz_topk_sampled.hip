@@ -390,15 +390,20 @@ __device__ __forceinline__ void stage_group(WaveList& L, uint32_t* h, const uint
 // Software-pipelined filter for the PartialModel step (16-byte aligned operands, no
 // accumulation; with or without the fused copy): every stream load is branch-free — lanes past
 // the segment's last whole float4 read element 0 and are masked — so the compiler's wait counts
-// track them, and the NEXT groups' loads are in flight while this group is copied, keyed and
-// staged.  (sampled_filter_kernel loads G groups, then waits for all of them — vmcnt(0) under
-// its ragged-element branches — and has nothing in flight while it processes them.)  The < 4
-// elements past the last whole float4 of [0, n) are handled after the loop, by the last segment.
-template <bool X0, bool COPY, int G>
-__global__ void __launch_bounds__(256, FOCC) sampled_filter_pipe_kernel(
+// track them, and D - 1 float4 groups (x and x0, 2 KB per wave each) stay in flight while a
+// group is copied, keyed and staged: the loop is unrolled D times over D register buffers, so
+// no register copy ever waits on a load.  (sampled_filter_kernel loads G groups, then waits for
+// all of them — vmcnt(0) under its ragged-element branches — and has nothing in flight while it
+// processes them.)  OCC waves per SIMD: the grid's W segments are all resident at once (8 at
+// 8192 segments with D = 2; 4 at <= 4096 segments, where 128 registers hold deeper pipelines).
+// The < 4 elements past the last whole float4 of [0, n) are handled after the loop, by the last
+// segment.
+template <bool X0, bool COPY, int D, int OCC>
+__global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
     KeySrc s, int64_t n, uint32_t r_lo, uint32_t r_hi, int64_t W, int64_t R, int64_t CAP,
     TopkCtrl* ctrl, const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt,
     uint32_t* cidx, uint32_t* ckey, float* cval, float* __restrict__ copy_out) {
+  static_assert(D >= 2, "at least one group in flight");
   typedef float v4f __attribute__((ext_vector_type(4)));
   __shared__ uint32_t h[HBR];
   __shared__ uint32_t win[4];
@@ -418,17 +423,16 @@ __global__ void __launch_bounds__(256, FOCC) sampled_filter_pipe_kernel(
   }
   const v4f* __restrict__ xa = reinterpret_cast<const v4f*>(s.x);
   const v4f* __restrict__ xb = reinterpret_cast<const v4f*>(s.x0);
-  v4f ca[G], cb[G];
-  auto ld = [&](int64_t base, v4f (&a)[G], v4f (&b)[G]) {
-#pragma unroll
-    for (int q = 0; q < G; ++q) {
-      const int64_t i0 = base + q * 256 + lane * 4;
-      const int64_t g4 = (i0 < end4 ? i0 : 0) >> 2;
-      a[q] = __builtin_nontemporal_load(xa + g4);
-      if (X0) b[q] = __builtin_nontemporal_load(xb + g4);
-    }
+  v4f A[D], B[D];
+  // group j of the segment (256 elements) into buffer slot u
+  auto ld = [&](int64_t j, int u) {
+    const int64_t i0 = beg + j * 256 + lane * 4;
+    const int64_t g4 = (i0 < end4 ? i0 : 0) >> 2;
+    A[u] = __builtin_nontemporal_load(xa + g4);
+    if (X0) B[u] = __builtin_nontemporal_load(xb + g4);
   };
-  ld(beg, ca, cb);
+#pragma unroll
+  for (int u = 0; u < D - 1; ++u) ld(u, u);
   block_window(cv, r_lo, r_hi, win, wsum);
   const uint32_t lo = win[0], hi = win[1], shift = win[2];
   if (seg == 0 && lane == 0) {
@@ -440,32 +444,29 @@ __global__ void __launch_bounds__(256, FOCC) sampled_filter_pipe_kernel(
              0u};
   uint32_t run = 0;
   bool dense = false;
-  auto proc = [&](const v4f (&a)[G], const v4f (&b)[G], int64_t base) {
+  auto proc = [&](int64_t j, int u) {
+    const int64_t i0 = beg + j * 256 + lane * 4;
+    const int cq = i0 < end4 ? 4 : 0;
+    if (COPY && cq) __builtin_nontemporal_store(A[u], reinterpret_cast<v4f*>(copy_out) + (i0 >> 2));
+    const float xv[4] = {A[u].x, A[u].y, A[u].z, A[u].w};
+    uint32_t kq[4];
+    if (X0) {
+      const float bv[4] = {B[u].x, B[u].y, B[u].z, B[u].w};
 #pragma unroll
-    for (int q = 0; q < G; ++q) {
-      const int64_t i0 = base + q * 256 + lane * 4;
-      const int cq = i0 < end4 ? 4 : 0;
-      if (COPY && cq) __builtin_nontemporal_store(a[q], reinterpret_cast<v4f*>(copy_out) + (i0 >> 2));
-      const float xv[4] = {a[q].x, a[q].y, a[q].z, a[q].w};
-      uint32_t kq[4];
-      if (X0) {
-        const float bv[4] = {b[q].x, b[q].y, b[q].z, b[q].w};
+      for (int e = 0; e < 4; ++e) kq[e] = key_of(xv[e] - bv[e]);
+    } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) kq[e] = key_of(xv[e] - bv[e]);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) kq[e] = key_of(xv[e]);
-      }
-      stage_group(L, h, kq, xv, cq, (uint32_t)i0, lane, lo, hi, shift, CAP, run, dense);
+      for (int e = 0; e < 4; ++e) kq[e] = key_of(xv[e]);
     }
+    stage_group(L, h, kq, xv, cq, (uint32_t)i0, lane, lo, hi, shift, CAP, run, dense);
   };
-  // ping-pong buffers, unrolled by two so no register copy waits on a load in flight
-  v4f pa[G], pb[G];
-  for (int64_t base = beg; base < end4; base += 2 * G * 256) {
-    ld(base + G * 256, pa, pb);
-    proc(ca, cb, base);
-    ld(base + 2 * G * 256, ca, cb);
-    proc(pa, pb, base + G * 256);
+  const int64_t ng = (end4 - beg + 255) >> 8;  // groups holding whole float4s
+  for (int64_t j0 = 0; j0 < ng; j0 += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      ld(j0 + u + D - 1, (u + D - 1) % D);  // the group D - 1 ahead, into the slot just freed
+      proc(j0 + u, u);
+    }
   }
   if (end4 < end) {  // the last segment's ragged 1-3 elements
     const int64_t i = end4 + lane;
@@ -1322,25 +1323,31 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
         s, a.n, ctrl, chist, ghist, blcnt, jb[0]));
     uint32_t r_lo, r_hi;
     window_ranks(a.n, a.k, &r_lo, &r_hi);
-    // DPZ_FILTER_PIPE=0 / 1 / 2: the batched filter / the pipelined one with 1 / 2 float4 groups
-    // per step (A/B diagnostics)
+    // The pipelined filter (PartialModel: aligned, no accumulation): depth 2 at 8 waves / SIMD
+    // when the grid needs them (more than 4096 segments), else depth DPZ_FILTER_DEPTH (default
+    // 4) at 4 waves / SIMD.  DPZ_FILTER_PIPE=0 selects the batched filter (A/B diagnostics).
     static const int pipe = getenv("DPZ_FILTER_PIPE") ? atoi(getenv("DPZ_FILTER_PIPE")) : 1;
+    static const int depth = getenv("DPZ_FILTER_DEPTH") ? atoi(getenv("DPZ_FILTER_DEPTH")) : 4;
     if (VEC && a.acc_mode == DPZ_ACC_NONE && pipe > 0) {
       const bool x0 = a.x0 != nullptr;
-#define DPZ_PIPE(X0_, CP_, G_)                                                                   \
-  DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_pipe_kernel<X0_, CP_, G_><<<nb, 256, 0, a.st>>>( \
+      const int dsel = g.W > 4096 ? 2 : (depth >= 8 ? 8 : (depth >= 6 ? 6 : 4));
+#define DPZ_PIPE(D_, O_)                                                                      \
+  do {                                                                                        \
+    if (x0 && copy_out) DPZ_PIPE1(true, true, D_, O_);                                        \
+    else if (x0) DPZ_PIPE1(true, false, D_, O_);                                              \
+    else if (copy_out) DPZ_PIPE1(false, true, D_, O_);                                        \
+    else DPZ_PIPE1(false, false, D_, O_);                                                     \
+  } while (0)
+#define DPZ_PIPE1(X0_, CP_, D_, O_)                                                           \
+  DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_pipe_kernel<X0_, CP_, D_, O_><<<nb, 256, 0, a.st>>>( \
       s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval, copy_out))
-      if (pipe == 2) {
-        if (x0 && copy_out) DPZ_PIPE(true, true, 2);
-        else if (x0) DPZ_PIPE(true, false, 2);
-        else if (copy_out) DPZ_PIPE(false, true, 2);
-        else DPZ_PIPE(false, false, 2);
-      } else {
-        if (x0 && copy_out) DPZ_PIPE(true, true, 1);
-        else if (x0) DPZ_PIPE(true, false, 1);
-        else if (copy_out) DPZ_PIPE(false, true, 1);
-        else DPZ_PIPE(false, false, 1);
+      switch (dsel) {
+        case 2: DPZ_PIPE(2, 8); break;
+        case 8: DPZ_PIPE(8, 4); break;
+        case 6: DPZ_PIPE(6, 4); break;
+        default: DPZ_PIPE(4, 4); break;
       }
+#undef DPZ_PIPE1
 #undef DPZ_PIPE
     } else if (a.acc_mode == DPZ_ACC_NONE)
       DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_kernel<VEC, false, FG><<<nb, 256, 0, a.st>>>(
