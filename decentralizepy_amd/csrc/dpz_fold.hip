@@ -858,6 +858,11 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_group_kernel(FoldArgs a)
 // payload on average (launch_walk).  Invalid payloads (unsorted / out of range) cannot write out
 // of bounds.
 constexpr int FW_WAVES = 4;  // waves per block (256 threads)
+// fold_walk_kernel's register bound (blocks per CU = waves per SIMD): the walk hides its window
+// loads by occupancy (measured on MI355X, 3 payloads x alpha 0.4 at 128-element tiles: 125 -> 111
+// us at 8 waves / SIMD).  The 4-group kernel is left unbounded: bounding it to 5 waves at
+// 512-element tiles measured slower (16 x 0.1: 233 vs 222 us, profiles/r03_s2_fold_occ_ab.json).
+#define FW_MINB_1(EPL) ((EPL) >= 16 ? 4 : ((EPL) >= 8 ? 5 : ((EPL) >= 4 ? 7 : 8)))
 
 template <int EPL>
 struct FwV {
@@ -874,22 +879,25 @@ __device__ __forceinline__ int fw_elem(int lane, int e) {
 // Loads are branch-free (addresses clamped into [0, n); results past n are never stored), so
 // the compiler counts them and waits only for the tile it folds, never for the next tile's loads
 // in flight (a load under a branch makes it wait for everything: vmcnt(0)).  VEC kernels run
-// only when n is a multiple of 4 and the operands are 16-byte aligned.
+// when the operands are 16-byte aligned and n >= 1024: a vector group reaching past n is clamped
+// to the last whole aligned group, and the ragged last tile reloads its values element-wise
+// (sym2 level-4 coefficient arrays, M = 25,000,009 at C3, are not a multiple of 4).
 template <bool VEC, int EPL>
 __device__ __forceinline__ FwV<EPL> fw_load(const float* p, int64_t tlo, int lane, int64_t n) {
   FwV<EPL> r;
   if constexpr (VEC && EPL >= 4) {
+    const int64_t last = (n & ~int64_t(3)) - 4;  // the last whole float4 group inside [0, n)
 #pragma unroll
     for (int c = 0; c < EPL / 4; ++c) {
       const int64_t i0 = tlo + fw_elem<EPL>(lane, 4 * c);
-      const int64_t q = i0 < n ? i0 : n - 4;
+      const int64_t q = i0 + 4 <= n ? i0 : last;
       const float4 v = *reinterpret_cast<const float4*>(p + q);
       r.v[4 * c] = v.x; r.v[4 * c + 1] = v.y; r.v[4 * c + 2] = v.z; r.v[4 * c + 3] = v.w;
     }
     return r;
   } else if constexpr (VEC && EPL == 2) {
     const int64_t i0 = tlo + 2 * lane;
-    const int64_t q = i0 < n ? i0 : n - 2;
+    const int64_t q = i0 + 2 <= n ? i0 : (n & ~int64_t(1)) - 2;
     const float2 v = *reinterpret_cast<const float2*>(p + q);
     r.v[0] = v.x; r.v[1] = v.y;
     return r;
@@ -910,14 +918,23 @@ __device__ __forceinline__ void fw_store(float* p, int64_t tlo, int lane, int64_
 #pragma unroll
     for (int c = 0; c < EPL / 4; ++c) {
       const int64_t i0 = tlo + fw_elem<EPL>(lane, 4 * c);
-      if (!GUARD || i0 < n)
+      if (!GUARD || i0 + 4 <= n) {
         *reinterpret_cast<float4*>(p + i0) =
             make_float4(r[4 * c], r[4 * c + 1], r[4 * c + 2], r[4 * c + 3]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (i0 + e < n) p[i0 + e] = r[4 * c + e];
+      }
     }
     return;
   } else if constexpr (VEC && EPL == 2) {
     const int64_t i0 = tlo + 2 * lane;
-    if (!GUARD || i0 < n) *reinterpret_cast<float2*>(p + i0) = make_float2(r[0], r[1]);
+    if (!GUARD || i0 + 2 <= n) {
+      *reinterpret_cast<float2*>(p + i0) = make_float2(r[0], r[1]);
+    } else if (i0 < n) {
+      p[i0] = r[0];
+    }
     return;
   }
 #pragma unroll
@@ -942,7 +959,7 @@ __device__ __forceinline__ int32_t fw_uni(int32_t v) { return __builtin_amdgcn_r
 // and cursors in scalar registers (a generic path holds them one per lane and reads them back
 // with readlane; measured slower than fold_walk_groups_kernel at 16 payloads, which is used there).
 template <bool VEC, int EPL, int NS>
-__global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw) {
+__global__ void __launch_bounds__(256, FW_MINB_1(EPL)) fold_walk_kernel(FoldArgs a, int64_t tpw) {
   constexpr bool ONE = NS <= 4;
   constexpr int TE = 64 * EPL;
   __shared__ float s_val[FW_WAVES][TE];
@@ -1042,6 +1059,8 @@ __global__ void __launch_bounds__(256) fold_walk_kernel(FoldArgs a, int64_t tpw)
     constexpr bool GUARD = decltype(guard)::value;
     const int64_t tlo = tile * TE;
     const int32_t tlo32 = (int32_t)tlo, thi32 = tlo32 + TE;
+    // the ragged last tile: its vector groups past the last whole one were clamped on load
+    if constexpr (GUARD && VEC) L = fw_load<false, EPL>(a.local, tlo, lane, n);
     // every slot: this tile's window start and entry count (the leading lanes below thi); the
     // cursors move to the next tile's windows, which are issued now with the next local values
     int32_t c0[NS], cnt[NS];
@@ -1261,6 +1280,8 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
     constexpr bool GUARD = decltype(guard)::value;
     const int64_t tlo = tile * TE;
     const int32_t tlo32 = (int32_t)tlo, thi32 = tlo32 + TE;
+    // the ragged last tile: its vector groups past the last whole one were clamped on load
+    if constexpr (GUARD && VEC) L = fw_load<false, EPL>(a.local, tlo, lane, n);
     Ln = fw_load<VEC, EPL>(a.local, tlo + TE, lane, n);  // clamped past the end
     float acc[EPL], base[EPL];
 #pragma unroll
@@ -1601,7 +1622,7 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
     bool use_walk = walk_ok(fa) && (fa.np <= 4 || (avg >= 0.02 && avg <= 0.21));
     if (kind) use_walk = walk_ok(fa) && kind == 4;
     if (use_walk) {
-      const int rc = launch_walk(fa, vec && n % 4 == 0, dens, st);
+      const int rc = launch_walk(fa, vec && n >= 1024, dens, st);
       if (rc != DPZ_OK) return rc;
       continue;
     }

@@ -398,7 +398,9 @@ __device__ __forceinline__ void stage_group(WaveList& L, uint32_t* h, const uint
 // 8192 segments with D = 2; 4 at <= 4096 segments, where 128 registers hold deeper pipelines).
 // The < 4 elements past the last whole float4 of [0, n) are handled after the loop, by the last
 // segment.
-template <bool X0, bool COPY, int D, int OCC>
+// SRC: the key's operands — 0: |x|, 1: |x - x0|, 2: |acc + x| (DPZ_ACC_ADD without x0: the
+// wavelet encode's W(x - x0) plus the accumulated changes, C3).
+template <int SRC, bool COPY, int D, int OCC>
 __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
     KeySrc s, int64_t n, uint32_t r_lo, uint32_t r_hi, int64_t W, int64_t R, int64_t CAP,
     TopkCtrl* ctrl, const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt,
@@ -422,7 +424,8 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
     cv[1] = c4[1];
   }
   const v4f* __restrict__ xa = reinterpret_cast<const v4f*>(s.x);
-  const v4f* __restrict__ xb = reinterpret_cast<const v4f*>(s.x0);
+  constexpr bool X0 = SRC != 0;  // a second operand stream (x0 or acc) in the B buffers
+  const v4f* __restrict__ xb = reinterpret_cast<const v4f*>(SRC == 2 ? s.acc : s.x0);
   v4f A[D], B[D];
   // group j of the segment (256 elements) into buffer slot u
   auto ld = [&](int64_t j, int u) {
@@ -450,10 +453,14 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
     if (COPY && cq) __builtin_nontemporal_store(A[u], reinterpret_cast<v4f*>(copy_out) + (i0 >> 2));
     const float xv[4] = {A[u].x, A[u].y, A[u].z, A[u].w};
     uint32_t kq[4];
-    if (X0) {
+    if (SRC == 1) {
       const float bv[4] = {B[u].x, B[u].y, B[u].z, B[u].w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) kq[e] = key_of(xv[e] - bv[e]);
+    } else if (SRC == 2) {
+      const float bv[4] = {B[u].x, B[u].y, B[u].z, B[u].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) kq[e] = key_of(bv[e] + xv[e]);  // acc + change
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) kq[e] = key_of(xv[e]);
@@ -475,7 +482,7 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
     uint32_t kq[4] = {0u, 0u, 0u, 0u};
     if (v) {
       xv[0] = s.x[i];
-      kq[0] = key_of(X0 ? xv[0] - s.x0[i] : xv[0]);
+      kq[0] = key_of(SRC == 1 ? xv[0] - s.x0[i] : (SRC == 2 ? s.acc[i] + xv[0] : xv[0]));
       if (COPY) copy_out[i] = xv[0];
     }
     // one element per lane: lane order is index order
@@ -1328,15 +1335,17 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
     // 4) at 4 waves / SIMD.  DPZ_FILTER_PIPE=0 selects the batched filter (A/B diagnostics).
     static const int pipe = getenv("DPZ_FILTER_PIPE") ? atoi(getenv("DPZ_FILTER_PIPE")) : 1;
     static const int depth = getenv("DPZ_FILTER_DEPTH") ? atoi(getenv("DPZ_FILTER_DEPTH")) : 4;
-    if (VEC && a.acc_mode == DPZ_ACC_NONE && pipe > 0) {
+    const bool add_only = a.acc_mode == DPZ_ACC_ADD && !a.x0;
+    if (VEC && (a.acc_mode == DPZ_ACC_NONE || add_only) && pipe > 0) {
       const bool x0 = a.x0 != nullptr;
       const int dsel = g.W > 4096 ? 2 : (depth >= 8 ? 8 : (depth >= 6 ? 6 : 4));
 #define DPZ_PIPE(D_, O_)                                                                      \
   do {                                                                                        \
-    if (x0 && copy_out) DPZ_PIPE1(true, true, D_, O_);                                        \
-    else if (x0) DPZ_PIPE1(true, false, D_, O_);                                              \
-    else if (copy_out) DPZ_PIPE1(false, true, D_, O_);                                        \
-    else DPZ_PIPE1(false, false, D_, O_);                                                     \
+    if (add_only) DPZ_PIPE1(2, false, D_, O_);                                                \
+    else if (x0 && copy_out) DPZ_PIPE1(1, true, D_, O_);                                      \
+    else if (x0) DPZ_PIPE1(1, false, D_, O_);                                                 \
+    else if (copy_out) DPZ_PIPE1(0, true, D_, O_);                                            \
+    else DPZ_PIPE1(0, false, D_, O_);                                                         \
   } while (0)
 #define DPZ_PIPE1(X0_, CP_, D_, O_)                                                           \
   DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_pipe_kernel<X0_, CP_, D_, O_><<<nb, 256, 0, a.st>>>( \

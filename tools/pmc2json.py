@@ -9,7 +9,7 @@ import csv
 import json
 import sys
 
-NAMES = {"sampled_sample_kernel": "topk_sample", "sampled_filter_kernel": "topk_filter",
+NAMES = {"sampled_sample_kernel": "topk_sample", "sampled_filter_kernel": "topk_filter", "sampled_filter_pipe_kernel": "topk_filter",
          "sampled_select_kernel": "topk_select", "sampled_resolve_kernel": "topk_resolve",
          "sampled_compact_kernel": "topk_compact", "fold_offsets_kernel": "fold_offsets",
          "fold_kernel": "fold", "fold_group_kernel": "fold_group", "fold_slots_kernel": "fold_slots",
