@@ -1158,25 +1158,6 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     }
   }
   auto is_sel = [&](uint32_t key, uint32_t idx) { return key > T || (key == T && idx <= icut); };
-  // counter updates of the register-held candidates first: the kernel cannot retire before its
-  // scattered memory-side atomics (or stores) land, so they drain while the count and write
-  // passes run (the write pass skips them)
-  if (counter) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int64_t seg = seg0 + u;
-      if (seg < W && cnt[u] != DENSE) {
-#pragma unroll
-        for (int c = 0; c < PFC; ++c) {
-          const uint32_t j = c * 64u + lane;
-          if (j < cnt[u] && is_sel(kk[u][c], ii[u][c])) {
-            if (PLAIN) counter[ii[u][c]] = (int32_t)(cc[u][c] + 1u);  // unique indices: no race
-            else atomicAdd(&counter[ii[u][c]], 1);  // non-returning
-          }
-        }
-      }
-    }
-  }
   // count pass (the first PFC chunks from registers), in-block offsets, write pass
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -1217,7 +1198,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
           if (pos < (uint64_t)k) {
             idx_out[pos] = (int32_t)idx;
             val_out[pos] = (cval || pre) ? v : vals_src[idx];
-            if (counter && !pre) {  // register-held chunks (pre) were counted up front
+            if (counter) {
               if (PLAIN) counter[idx] = (int32_t)(cw + 1u);  // unique indices: no race
               else atomicAdd(&counter[idx], 1);  // non-returning: no round trip to wait on
             }
@@ -1304,11 +1285,13 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
       // the scatter must follow the filter's copy: blocks appended to compact (default; the
       // latency-bound compact leaves most CU slots free: C2 one-node step 57.2 -> 55.6 us on
       // MI355X vs appended to select) or select (DPZ_SCATTER_AT=select, A/B diagnostics)
+      // (DPZ_SCATTER_AT=split: half in each)
       const char* e = getenv("DPZ_SCATTER_AT");
-      const bool at_compact = !(e && e[0] == 's');
+      const bool at_select = e && e[0] == 's' && e[1] == 'e';
+      const bool split = e && e[0] == 's' && e[1] == 'p';
       f[0] = 0.0;
-      f[1] = at_compact ? 0.0 : 1.0;
-      f[2] = at_compact ? 1.0 : 0.0;
+      f[1] = split ? 0.5 : (at_select ? 1.0 : 0.0);
+      f[2] = split ? 0.5 : (at_select ? 0.0 : 1.0);
     }
     const int per[3] = {4, 16, 4};  // chunks per appended block (one per wave)
     int64_t c = a.job->c0;

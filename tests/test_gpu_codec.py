@@ -671,7 +671,7 @@ def test_coscheduled_replace_rejects_aliasing(dev):
         codec.topk_encode(tx, 10_000, x0=tx0, co_replace=(tx0.clone(), p_idx, p_val, tx))
 
 
-@pytest.mark.parametrize("where", ["select", "compact"])
+@pytest.mark.parametrize("where", ["select", "compact", "split"])
 @pytest.mark.parametrize("n,alpha,rk,dup,layout", [
     (11_000_000, 0.01, 110_000, False, None),      # C2: the bench's one-node step
     (16_777_216, 0.01, 167_772, False, None),      # 64 MiB
