@@ -6,6 +6,7 @@ behind the C ABI (``include/dpz_codec.h``).  Calls are enqueued on the current t
 """
 import ctypes
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -670,7 +671,7 @@ def lz4_decompress(frame, device, out=None, workspace=None, max_size=None):
     checksums, when the frame carries them, are skipped, not verified (the transport —
     ZeroMQ over TCP — already guarantees integrity; every decoder read and write is
     bounds-checked, so a corrupt frame cannot fault or overrun)."""
-    b = bytes(frame)
+    b = frame if isinstance(frame, bytes) else bytes(frame)
     cs, nb, linked, bmax = lz4_frame_info(b)
     bound = nb * bmax
     if cs > bound or (max_size is not None and cs > int(max_size)):
@@ -681,8 +682,16 @@ def lz4_decompress(frame, device, out=None, workspace=None, max_size=None):
     if out is None or out.numel() < size:
         out = torch.empty(max(size, 1), dtype=torch.uint8, device=device)
     _require(out, torch.uint8, "out")
-    dframe = torch.frombuffer(bytearray(b), dtype=torch.uint8).to(device) if b else \
-        torch.empty(1, dtype=torch.uint8, device=device)
+    # the frame goes up through a pinned buffer kept with the workspace (the call synchronizes
+    # its stream before returning, so the buffer is free again when the next call starts)
+    wsp = workspace or Workspace(out.device)
+    pin = getattr(wsp, "lz4_pin", None)
+    if pin is None or pin.numel() < max(len(b), 1):
+        pin = wsp.lz4_pin = torch.empty(max(len(b), 4096), dtype=torch.uint8, pin_memory=True)
+    if b:
+        pin.numpy()[:len(b)] = np.frombuffer(b, dtype=np.uint8)
+    dframe = pin[:max(len(b), 1)].to(out.device, non_blocking=True)
+    workspace = wsp
     need = int(_lib.lib().dpz_lz4_workspace_bytes(0, nb, 0 if linked else bmax))
     ws = _lz4_ws(workspace, out.device, need)
     n = ctypes.c_int64(0)

@@ -341,13 +341,19 @@ __device__ __forceinline__ uint32_t lz_win_byte(LzWin& w, const uint32_t* cb32, 
   return (__builtin_amdgcn_readlane(w.wv, (int)(r >> 2)) >> (8 * (r & 3))) & 0xFFu;
 }
 
+// flagged_only (independent frames): decode only the blocks lz4_decode_par_kernel left to it
+// (dsize[b] == LZ_PAR_FALLBACK); the other workgroups leave at once.
+constexpr uint64_t LZ_PAR_FALLBACK = ~0ull;
+
 __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t* __restrict__ in,
                                                         const LzBlock* __restrict__ blocks,
                                                         int64_t nblk, int linked, uint32_t bmax,
                                                         uint32_t win, uint8_t* __restrict__ out,
                                                         uint64_t out_cap,
                                                         uint64_t* __restrict__ dsize,
-                                                        uint32_t* __restrict__ status) {
+                                                        uint32_t* __restrict__ status,
+                                                        int flagged_only) {
+  if (flagged_only && !linked && dsize[blockIdx.x] != LZ_PAR_FALLBACK) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lz_smem[];
   uint8_t* ring = lz_smem;           // win bytes
   uint8_t* cb = lz_smem + win;       // staged compressed block (+ 256 bytes of window slack)
@@ -426,6 +432,281 @@ __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t* __restric
   }
   if (bad && lane == 0) atomicOr(status, 1u);
   if (linked && lane == 0) dsize[0] = opos;
+}
+
+// ---- parallel decode of a small independent block (this codec's frames: 2 KB blocks) --------
+// The sequential decoder walks ≈ 500 sequences per 2 KB block of index gaps one after another,
+// each costing a few dependent LDS / readlane steps (≈ 115 us per frame measured).  Here a
+// 256-thread workgroup decodes the block with no sequential walk longer than a 64-byte chunk:
+//  1. every byte position p is parsed AS IF a token started there: nxt[p] = the position after
+//     its sequence (literal length and its extension bytes, literals, offset, match extension);
+//  2. from every p, a walk along nxt until it leaves p's 64-byte chunk: exit[p];
+//  3. one thread chains the chunks: 0 -> exit[0] -> exit[exit[0]] ... (one step per chunk),
+//     which gives every chunk's true entry token;
+//  4. each chunk re-walks from its entry and flags its true tokens;
+//  5. a block scan of the tokens' decoded lengths gives each sequence's output offset;
+//  6. every output byte gets its source: src = a compressed position (literal) or an earlier
+//     output position (match byte at distance off); pointer jumping (src[p] = src[src[p]], in
+//     place, <= log2(LZ_PAR_MAX) + 1 rounds) leaves every byte on a literal;
+//  7. the bytes are read from the staged block and stored 4 at a time.
+// A block that decodes past LZ_PAR_MAX bytes (or is stored raw, or larger) is left to the
+// sequential kernel (dsize[b] = LZ_PAR_FALLBACK).  Every index is bounds-checked; a malformed
+// block (a chain through an invalid parse, an offset before the block start) sets *status.
+constexpr int LZ_PAR_MAX = 4096;                    // decoded bytes per block on this path
+constexpr int LZ_PAR_CMAX = LZ_PAR_MAX + 64;        // compressed bytes per block on this path
+constexpr int LZ_PAR_CHUNK = 64;                    // walk chunk (bytes of the compressed block)
+constexpr int LZ_PAR_NCH = (LZ_PAR_CMAX + LZ_PAR_CHUNK - 1) / LZ_PAR_CHUNK;
+constexpr int LZ_PAR_PPT = (LZ_PAR_CMAX + 255) / 256;  // positions per thread
+constexpr uint16_t LZ_LIT = 0x8000u;                // src[p]: literal flag (| compressed pos)
+constexpr uint16_t LZ_BAD = 0xFFFFu;                // nxt[p]: no valid sequence at p
+constexpr uint16_t LZ_BIG = 0xFFFEu;                // nxt[p]: decodes past LZ_PAR_MAX
+
+struct LzParLds {
+  uint32_t cb32[(LZ_PAR_CMAX + 256) / 4];  // staged compressed block + zero slack
+  uint16_t nxt[LZ_PAR_CMAX];
+  uint16_t ext[LZ_PAR_CMAX];
+  uint16_t ooff[LZ_PAR_CMAX];              // output offset of the token at p (true tokens)
+  uint8_t tok[LZ_PAR_CMAX];                // 1: a true token
+  uint16_t src[LZ_PAR_MAX];
+  uint16_t entry[LZ_PAR_NCH];
+  uint32_t wsum[8];
+  uint32_t total, state, changed;          // state: 0 ok, 1 bad, 2 fallback
+};
+
+struct LzSeq {
+  uint32_t lit, L, off, M, next;  // next = position after the sequence; kind in the caller
+  int kind;                       // 0 sequence with a match, 1 last (literals only), 2 bad, 3 big
+};
+
+// The sequence a token at p would start (cb holds cs bytes + >= 256 zero bytes of slack).
+__device__ __forceinline__ LzSeq lz_parse_at(const uint8_t* cb, uint32_t p, uint32_t cs) {
+  LzSeq q{0, 0, 0, 0, 0, 2};
+  const uint32_t tok = cb[p];
+  uint32_t ip = p + 1, L = tok >> 4;
+  if (L == 15) {
+    uint32_t x;
+    do {
+      if (ip >= cs || L > (uint32_t)LZ_PAR_MAX) { q.kind = L > (uint32_t)LZ_PAR_MAX ? 3 : 2; return q; }
+      x = cb[ip++];
+      L += x;
+    } while (x == 255);
+  }
+  if (L > (uint32_t)LZ_PAR_MAX) { q.kind = 3; return q; }
+  if (ip + L > cs) return q;
+  q.lit = ip;
+  q.L = L;
+  ip += L;
+  if (ip == cs) {
+    q.kind = 1;
+    q.next = cs;
+    return q;
+  }
+  if (ip + 2 > cs) return q;
+  q.off = cb[ip] | ((uint32_t)cb[ip + 1] << 8);
+  ip += 2;
+  uint32_t M = tok & 15u;
+  if (M == 15) {
+    uint32_t x;
+    do {
+      if (ip >= cs || M > (uint32_t)LZ_PAR_MAX) { q.kind = M > (uint32_t)LZ_PAR_MAX ? 3 : 2; return q; }
+      x = cb[ip++];
+      M += x;
+    } while (x == 255);
+  }
+  M += 4;
+  if (M > (uint32_t)LZ_PAR_MAX) { q.kind = 3; return q; }
+  if (ip > cs) return q;
+  q.M = M;
+  q.next = ip;
+  q.kind = 0;
+  return q;
+}
+
+__global__ void __launch_bounds__(256) lz4_decode_par_kernel(const uint8_t* __restrict__ in,
+                                                             const LzBlock* __restrict__ blocks,
+                                                             uint32_t bmax,
+                                                             uint8_t* __restrict__ slots,
+                                                             uint64_t* __restrict__ dsize,
+                                                             uint32_t* __restrict__ status) {
+  __shared__ LzParLds S;
+  const int t = threadIdx.x, wid = t >> 6;
+  const int64_t b = blockIdx.x;
+  const LzBlock B = blocks[b];
+  uint8_t* cb = reinterpret_cast<uint8_t*>(S.cb32);
+  if (B.raw || B.csize > (uint32_t)LZ_PAR_CMAX || B.csize == 0) {  // the sequential kernel's
+    if (t == 0) dsize[b] = LZ_PAR_FALLBACK;
+    return;
+  }
+  const uint32_t cs = B.csize;
+  if (wid == 0) lz_stage(cb, in + B.in_off, cs);
+  for (uint32_t q = cs + t; q < cs + 256; q += 256) cb[q] = 0;
+  if (t == 0) {
+    S.state = 0;
+    S.total = 0;
+  }
+  __syncthreads();
+  // 1. the sequence a token at every position would start
+  for (uint32_t p = t; p < cs; p += 256) {
+    const LzSeq q = lz_parse_at(cb, p, cs);
+    S.nxt[p] = q.kind <= 1 ? (uint16_t)q.next : (q.kind == 3 ? LZ_BIG : LZ_BAD);
+    S.tok[p] = 0;
+  }
+  for (int c = t; c < LZ_PAR_NCH; c += 256) S.entry[c] = LZ_BAD;
+  __syncthreads();
+  // 2. from every position, the walk to the first position past its chunk (all of a thread's
+  // walks advance in lockstep, so their LDS reads are in flight together)
+  {
+    uint32_t cur[LZ_PAR_PPT], lim[LZ_PAR_PPT];
+#pragma unroll
+    for (int i = 0; i < LZ_PAR_PPT; ++i) {
+      const uint32_t p = t + 256u * i;
+      cur[i] = p < cs ? p : 0xFFFFFFFFu;
+      lim[i] = (p / LZ_PAR_CHUNK + 1) * LZ_PAR_CHUNK;
+    }
+    for (int step = 0; step < LZ_PAR_CHUNK; ++step) {
+      bool any = false;
+#pragma unroll
+      for (int i = 0; i < LZ_PAR_PPT; ++i) {
+        if (cur[i] < lim[i] && cur[i] < cs) {
+          cur[i] = S.nxt[cur[i]];  // > cur (a sequence is >= 1 byte), or cs, or a marker
+          any = true;
+        }
+      }
+      if (!any) break;
+    }
+#pragma unroll
+    for (int i = 0; i < LZ_PAR_PPT; ++i) {
+      const uint32_t p = t + 256u * i;
+      if (p < cs) S.ext[p] = (uint16_t)(cur[i] > 0xFFFFu ? LZ_BAD : cur[i]);
+    }
+  }
+  __syncthreads();
+  // 3. the chain of chunk entries, one step per chunk
+  if (t == 0) {
+    uint32_t p = 0, st = 0, guard = 0;
+    while (p < cs && guard++ < LZ_PAR_NCH + 1) {
+      S.entry[p / LZ_PAR_CHUNK] = (uint16_t)p;
+      const uint32_t x = S.ext[p];
+      if (x == LZ_BAD) { st = 1; break; }
+      if (x == LZ_BIG) { st = 2; break; }
+      p = x;
+    }
+    if (!st && p != cs) st = 1;  // the last sequence must end the block exactly
+    S.state = st;
+  }
+  __syncthreads();
+  if (S.state) {
+    if (t == 0) {
+      if (S.state == 2) {
+        dsize[b] = LZ_PAR_FALLBACK;
+      } else {
+        dsize[b] = 0;
+        atomicOr(status, 1u);
+      }
+    }
+    return;
+  }
+  // 4. each entered chunk flags its true tokens
+  for (int c = t; c < LZ_PAR_NCH; c += 256) {
+    uint32_t p = S.entry[c];
+    if (p == LZ_BAD) continue;
+    const uint32_t lim = (uint32_t)(c + 1) * LZ_PAR_CHUNK;
+    while (p < lim && p < cs) {
+      S.tok[p] = 1;
+      p = S.nxt[p];
+    }
+  }
+  __syncthreads();
+  // 5. output offsets: block scan of the true tokens' decoded lengths (positions in order)
+  uint32_t len[LZ_PAR_PPT], mine = 0;
+  {
+    // thread t owns the contiguous positions [t * PPT, (t + 1) * PPT): scan order = position order
+#pragma unroll
+    for (int i = 0; i < LZ_PAR_PPT; ++i) {
+      const uint32_t p = (uint32_t)t * LZ_PAR_PPT + i;
+      len[i] = 0;
+      if (p < cs && S.tok[p]) {
+        const LzSeq q = lz_parse_at(cb, p, cs);
+        len[i] = q.L + q.M;
+      }
+      mine += len[i];
+    }
+    uint32_t tot;
+    uint32_t run = block_excl_scan(mine, S.wsum, &tot);
+    if (tot > (uint32_t)LZ_PAR_MAX) {
+      if (t == 0) dsize[b] = LZ_PAR_FALLBACK;
+      return;  // identical in every thread
+    }
+#pragma unroll
+    for (int i = 0; i < LZ_PAR_PPT; ++i) {
+      const uint32_t p = (uint32_t)t * LZ_PAR_PPT + i;
+      if (p < cs) S.ooff[p] = (uint16_t)run;
+      run += len[i];
+    }
+    if (t == 0) S.total = tot;
+  }
+  __syncthreads();
+  const uint32_t total = S.total;
+  // 6. every output byte's source (offsets checked against the block's history)
+  bool bad = false;
+  for (uint32_t p = t; p < cs; p += 256) {
+    if (!S.tok[p]) continue;
+    const LzSeq q = lz_parse_at(cb, p, cs);
+    const uint32_t o = S.ooff[p];
+    for (uint32_t j = 0; j < q.L; ++j) S.src[o + j] = (uint16_t)(LZ_LIT | (q.lit + j));
+    if (q.kind == 0) {
+      if (q.off == 0 || q.off > o + q.L) {
+        bad = true;
+        continue;
+      }
+      for (uint32_t j = 0; j < q.M; ++j) S.src[o + q.L + j] = (uint16_t)(o + q.L + j - q.off);
+    }
+  }
+  if (bad) S.state = 1;
+  __syncthreads();
+  if (S.state) {
+    if (t == 0) {
+      dsize[b] = 0;
+      atomicOr(status, 1u);
+    }
+    return;
+  }
+  // pointer jumping: every byte ends on a literal
+  for (int round = 0; round < 14; ++round) {
+    if (t == 0) S.changed = 0;
+    __syncthreads();
+    bool ch = false;
+    for (uint32_t p = t; p < total; p += 256) {
+      const uint16_t v = S.src[p];
+      if (!(v & LZ_LIT)) {
+        const uint16_t u = S.src[v];  // v < p: an earlier output byte
+        S.src[p] = u;
+        ch |= !(u & LZ_LIT);
+      }
+    }
+    if (ch) S.changed = 1;
+    __syncthreads();
+    if (!S.changed) break;
+    __syncthreads();
+  }
+  // 7. bytes out: 4 per thread per step, one 32-bit store when whole
+  uint8_t* dst = slots + (uint64_t)b * bmax;
+  for (uint32_t p0 = 4 * t; p0 < total; p0 += 4 * 256) {
+    uint32_t wv = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t p = p0 + e;
+      if (p < total) {
+        const uint16_t v = S.src[p];
+        const uint32_t c = (v & LZ_LIT) ? cb[v & 0x7FFFu] : 0u;
+        wv |= c << (8 * e);
+      }
+    }
+    if (p0 + 4 <= total) *reinterpret_cast<uint32_t*>(dst + p0) = wv;
+    else
+      for (uint32_t e = 0; p0 + e < total; ++e) dst[p0 + e] = (uint8_t)(wv >> (8 * e));
+  }
+  if (t == 0) dsize[b] = total;
 }
 
 // independent frames: slot b (dsize[b] bytes at b * bmax) -> out + prefix
@@ -677,9 +958,20 @@ extern "C" int dpz_lz4_decompress(const uint8_t* frame_dev, const uint8_t* frame
   hipError_t e = hipMemcpyAsync(tab, tab_h, sizeof(LzBlock) * (size_t)(nb > 0 ? nb : 1),
                                 hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemsetAsync(status, 0, 16, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);  // tab_h is freed below
-  free(tab_h);
-  if (e != hipSuccess) return (int)e;
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(st);
+    free(tab_h);
+    return (int)e;
+  }
+  // tab_h stays allocated until the call's final synchronize (the copy may read it until then)
+  struct FreeAtExit {
+    void* p;
+    hipStream_t s;
+    ~FreeAtExit() {
+      (void)hipStreamSynchronize(s);
+      free(p);
+    }
+  } tab_guard{tab_h, st};
   uint64_t tot = 0;
   uint32_t bad = 0;
   if (nb > 0) {
@@ -691,14 +983,21 @@ extern "C" int dpz_lz4_decompress(const uint8_t* frame_dev, const uint8_t* frame
     if (bmax > 65536 || shm > 160 * 1024) return DPZ_ERR_UNSUPPORTED;
     DPZ_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(lz4_decode_kernel),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    // DPZ_LZ4_PAR=0: every independent block on the sequential decoder (A/B diagnostics)
+    const char* pe = getenv("DPZ_LZ4_PAR");
+    const bool par = !(pe && atoi(pe) == 0);
     if (linked) {
       DPZ_TIMED(DPZ_KT_LZ4, st, lz4_decode_kernel<<<1, 64, shm, st>>>(
                                     frame_dev, tab, nb, 1, (uint32_t)bmax, win, out,
-                                    (uint64_t)out_cap, total, status));
+                                    (uint64_t)out_cap, total, status, 0));
     } else {
+      if (par)
+        DPZ_TIMED(DPZ_KT_LZ4, st, lz4_decode_par_kernel<<<(unsigned)nb, 256, 0, st>>>(
+                                      frame_dev, tab, (uint32_t)bmax, slots, dsize, status));
+      // the blocks the parallel decoder left (raw, large; all of them without it)
       DPZ_TIMED(DPZ_KT_LZ4, st, lz4_decode_kernel<<<(unsigned)nb, 64, shm, st>>>(
                                     frame_dev, tab, nb, 0, (uint32_t)bmax, win, slots,
-                                    (uint64_t)nb * bmax, dsize, status));
+                                    (uint64_t)nb * bmax, dsize, status, par ? 1 : 0));
       DPZ_TIMED(DPZ_KT_LZ4, st, lz4_gather_kernel<<<(unsigned)nb, 256, 0, st>>>(
                                     slots, dsize, nb, (uint32_t)bmax, out, (uint64_t)out_cap,
                                     total));

@@ -20,8 +20,12 @@ def _dev_bytes(b, dev):
         torch.empty(0, dtype=torch.uint8, device=dev)
 
 
+@pytest.mark.parametrize("par", ["1", "0"])
 @pytest.mark.parametrize("name", list(_cases()))
-def test_device_frames_decode_with_liblz4(dev, name):
+def test_device_frames_decode_with_liblz4(dev, name, par, monkeypatch):
+    """par 1: independent blocks that decode to <= 4 KB take the parallel decoder (parse, then
+    pointer jumping); par 0: the sequential decoder for every block (DPZ_LZ4_PAR=0)."""
+    monkeypatch.setenv("DPZ_LZ4_PAR", par)
     from decentralizepy_amd import codec
     data = _cases()[name]
     frame = bytes(codec.lz4_compress(_dev_bytes(data, dev)).cpu().numpy().tobytes())
@@ -38,6 +42,8 @@ def test_device_frames_decode_with_liblz4(dev, name):
 @pytest.mark.parametrize("name", list(_cases()))
 @pytest.mark.parametrize("linked", [True, False])
 def test_device_decodes_liblz4_frames(dev, name, linked):
+    """liblz4's frames: linked 64 KB blocks (sequential decoder), independent blocks (the
+    parallel decoder for those that decode to <= 4 KB, the rest handed to the sequential one)."""
     from decentralizepy_amd import codec
     data = _cases()[name]
     frame = olz4.ref_compress(data, block_linked=linked)
@@ -66,6 +72,28 @@ def test_malformed_frames_are_rejected(dev):
         codec.lz4_decompress(bytes(bad), dev)
     with pytest.raises(ValueError):
         codec.lz4_decompress(bytes(frame[:-10]), dev)
+    # this codec's independent frame (the parallel decoder): the same corruption of the first
+    # match offset, and a literal run reaching past its block
+    own = bytearray(codec.lz4_compress(_dev_bytes(data, dev)).cpu().numpy().tobytes())
+    bad = bytearray(own)
+    tok = bad[body]
+    i = body + 1
+    L = tok >> 4
+    if L == 15:
+        while bad[i] == 255:
+            L += 255
+            i += 1
+        L += bad[i]
+        i += 1
+    i += L
+    bad[i], bad[i + 1] = 0xFF, 0xFF
+    with pytest.raises(ValueError):
+        codec.lz4_decompress(bytes(bad), dev)
+    bad = bytearray(own)
+    bad[body] = 0xF0  # literal length 15 + extension bytes read from the block's data
+    bad[body + 1] = 0xFF
+    with pytest.raises(ValueError):
+        codec.lz4_decompress(bytes(bad), dev)
 
 
 def test_untrusted_content_size_is_bounded_before_allocation(dev):
