@@ -73,37 +73,41 @@ __device__ __forceinline__ void lz_put(uint8_t* ob, int pos, uint32_t v) { ob[po
 // Global bytes -> LDS, one wave: every load of a round issued before its LDS writes (a loop of
 // load -> wait -> write per byte is one memory round trip per 64 bytes).  16-byte loads when the
 // source is aligned, else 16 independent byte loads per lane per round.
+// (No local arrays: indexed temporaries were placed in scratch memory — 80 bytes per lane, a
+// global round trip per staged word; vector-typed temporaries stay in registers.)
 __device__ __forceinline__ void lz_stage(uint8_t* dst, const uint8_t* __restrict__ src, uint32_t n) {
   const int lane = threadIdx.x & 63;
   if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
     const uint32_t nv = n / 16;
-    for (uint32_t v0 = 0; v0 < nv; v0 += 4 * 64) {
-      uint4 r[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t v = v0 + u * 64 + lane;
-        if (v < nv) r[u] = reinterpret_cast<const uint4*>(src)[v];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t v = v0 + u * 64 + lane;
-        if (v < nv) *reinterpret_cast<uint4*>(dst + 16 * v) = r[u];
-      }
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    for (uint32_t v0 = 0; v0 < nv; v0 += 4 * 64) {  // loads branch-free (indices clamped)
+      const uint32_t v = v0 + lane, last = nv - 1;
+      const uint4 r0 = s4[v < nv ? v : last];
+      const uint4 r1 = s4[v + 64 < nv ? v + 64 : last];
+      const uint4 r2 = s4[v + 128 < nv ? v + 128 : last];
+      const uint4 r3 = s4[v + 192 < nv ? v + 192 : last];
+      if (v < nv) d4[v] = r0;
+      if (v + 64 < nv) d4[v + 64] = r1;
+      if (v + 128 < nv) d4[v + 128] = r2;
+      if (v + 192 < nv) d4[v + 192] = r3;
     }
     for (uint32_t t = nv * 16 + lane; t < n; t += 64) dst[t] = src[t];
     return;
   }
+  // unaligned source: 16 independent byte loads per lane per round, packed into four words
   for (uint32_t t0 = 0; t0 < n; t0 += 16 * 64) {
-    uint8_t r[16];
+#define DPZ_LZB(u) ((t0 + (u) * 64u + lane) < n ? (uint32_t)src[t0 + (u) * 64u + lane] : 0u)
+    const uint32_t w0 = DPZ_LZB(0) | DPZ_LZB(1) << 8 | DPZ_LZB(2) << 16 | DPZ_LZB(3) << 24;
+    const uint32_t w1 = DPZ_LZB(4) | DPZ_LZB(5) << 8 | DPZ_LZB(6) << 16 | DPZ_LZB(7) << 24;
+    const uint32_t w2 = DPZ_LZB(8) | DPZ_LZB(9) << 8 | DPZ_LZB(10) << 16 | DPZ_LZB(11) << 24;
+    const uint32_t w3 = DPZ_LZB(12) | DPZ_LZB(13) << 8 | DPZ_LZB(14) << 16 | DPZ_LZB(15) << 24;
+#undef DPZ_LZB
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const uint32_t t = t0 + u * 64 + lane;
-      r[u] = t < n ? src[t] : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const uint32_t t = t0 + u * 64 + lane;
-      if (t < n) dst[t] = r[u];
+      const uint32_t w = u < 4 ? w0 : (u < 8 ? w1 : (u < 12 ? w2 : w3));
+      if (t < n) dst[t] = (uint8_t)(w >> (8 * (u & 3)));
     }
   }
 }
@@ -456,7 +460,9 @@ constexpr int LZ_PAR_MAX = 4096;                    // decoded bytes per block o
 constexpr int LZ_PAR_CMAX = LZ_PAR_MAX + 64;        // compressed bytes per block on this path
 constexpr int LZ_PAR_CHUNK = 64;                    // walk chunk (bytes of the compressed block)
 constexpr int LZ_PAR_NCH = (LZ_PAR_CMAX + LZ_PAR_CHUNK - 1) / LZ_PAR_CHUNK;
-constexpr int LZ_PAR_PPT = (LZ_PAR_CMAX + 255) / 256;  // positions per thread
+constexpr int LZ_PAR_T = 1024;                      // threads per block: 4 waves per SIMD hide the
+                                                    // LDS / VALU latency of each phase (1 block per CU)
+constexpr int LZ_PAR_PPT = (LZ_PAR_CMAX + LZ_PAR_T - 1) / LZ_PAR_T;  // positions per thread
 constexpr uint16_t LZ_LIT = 0x8000u;                // src[p]: literal flag (| compressed pos)
 constexpr uint16_t LZ_BAD = 0xFFFFu;                // nxt[p]: no valid sequence at p
 constexpr uint16_t LZ_BIG = 0xFFFEu;                // nxt[p]: decodes past LZ_PAR_MAX
@@ -469,9 +475,16 @@ struct LzParLds {
   uint8_t tok[LZ_PAR_CMAX];                // 1: a true token
   uint16_t src[LZ_PAR_MAX];
   uint16_t entry[LZ_PAR_NCH];
-  uint32_t wsum[8];
+  uint32_t wsum[16];
   uint32_t total, state, changed;          // state: 0 ok, 1 bad, 2 fallback
 };
+
+#ifdef DPZ_STAMPS
+__device__ unsigned long long g_lz_st[10][512];  // phase stamps of blocks < 512 (diagnostic build)
+#define LZST(i) do { if (threadIdx.x == 0 && blockIdx.x < 512) g_lz_st[i][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define LZST(i) do {} while (0)
+#endif
 
 struct LzSeq {
   uint32_t lit, L, off, M, next;  // next = position after the sequence; kind in the caller
@@ -522,7 +535,7 @@ __device__ __forceinline__ LzSeq lz_parse_at(const uint8_t* cb, uint32_t p, uint
   return q;
 }
 
-__global__ void __launch_bounds__(256) lz4_decode_par_kernel(const uint8_t* __restrict__ in,
+__global__ void __launch_bounds__(LZ_PAR_T) lz4_decode_par_kernel(const uint8_t* __restrict__ in,
                                                              const LzBlock* __restrict__ blocks,
                                                              uint32_t bmax,
                                                              uint8_t* __restrict__ slots,
@@ -538,49 +551,72 @@ __global__ void __launch_bounds__(256) lz4_decode_par_kernel(const uint8_t* __re
     return;
   }
   const uint32_t cs = B.csize;
-  if (wid == 0) lz_stage(cb, in + B.in_off, cs);
-  for (uint32_t q = cs + t; q < cs + 256; q += 256) cb[q] = 0;
+  LZST(0);
+  {  // every wave stages a 1 KB slice (one round of loads in flight per lane)
+    const uint32_t o = (uint32_t)wid * 1024u;
+    if (o < cs) lz_stage(cb + o, in + B.in_off + o, cs - o < 1024u ? cs - o : 1024u);
+  }
+  for (uint32_t q = cs + t; q < cs + 256; q += LZ_PAR_T) cb[q] = 0;
   if (t == 0) {
     S.state = 0;
     S.total = 0;
   }
   __syncthreads();
-  // 1. the sequence a token at every position would start
-  for (uint32_t p = t; p < cs; p += 256) {
-    const LzSeq q = lz_parse_at(cb, p, cs);
-    S.nxt[p] = q.kind <= 1 ? (uint16_t)q.next : (q.kind == 3 ? LZ_BIG : LZ_BAD);
+  LZST(1);
+  // 1. the sequence a token at every position would start: its length follows from the token
+  // byte alone unless a length needs extension bytes (nibble 15); those positions (marked
+  // LZ_SLOW) take the full parse in a second pass (no per-item arrays: nothing goes to scratch)
+  constexpr uint16_t LZ_SLOW = 0xFFFDu;
+  for (uint32_t p = t; p < cs; p += LZ_PAR_T) {
+    const uint32_t tk = cb[p];
+    const uint32_t L = tk >> 4, M = tk & 15u;
+    uint16_t nx;
+    if (L == 15 || M == 15) {
+      nx = LZ_SLOW;
+    } else {  // literals [p + 1, p + 1 + L), then the end of the block or a 2-byte offset
+      const uint32_t ip = p + 1 + L;
+      nx = ip > cs ? LZ_BAD : (ip == cs ? (uint16_t)cs : (ip + 2 > cs ? LZ_BAD : (uint16_t)(ip + 2)));
+    }
+    S.nxt[p] = nx;
     S.tok[p] = 0;
   }
-  for (int c = t; c < LZ_PAR_NCH; c += 256) S.entry[c] = LZ_BAD;
+  for (uint32_t p = t; p < cs; p += LZ_PAR_T) {
+    if (S.nxt[p] != LZ_SLOW) continue;
+    const LzSeq q = lz_parse_at(cb, p, cs);
+    S.nxt[p] = q.kind <= 1 ? (uint16_t)q.next : (q.kind == 3 ? LZ_BIG : LZ_BAD);
+  }
+  for (int c = t; c < LZ_PAR_NCH; c += LZ_PAR_T) S.entry[c] = LZ_BAD;
   __syncthreads();
+  LZST(2);
   // 2. from every position, the walk to the first position past its chunk (all of a thread's
-  // walks advance in lockstep, so their LDS reads are in flight together)
+  // walks advance in lockstep, branch-free, so their LDS reads are in flight together)
   {
-    uint32_t cur[LZ_PAR_PPT], lim[LZ_PAR_PPT];
+    uint32_t cur[LZ_PAR_PPT];
 #pragma unroll
     for (int i = 0; i < LZ_PAR_PPT; ++i) {
-      const uint32_t p = t + 256u * i;
+      const uint32_t p = t + (uint32_t)LZ_PAR_T * i;
       cur[i] = p < cs ? p : 0xFFFFFFFFu;
-      lim[i] = (p / LZ_PAR_CHUNK + 1) * LZ_PAR_CHUNK;
     }
     for (int step = 0; step < LZ_PAR_CHUNK; ++step) {
       bool any = false;
 #pragma unroll
       for (int i = 0; i < LZ_PAR_PPT; ++i) {
-        if (cur[i] < lim[i] && cur[i] < cs) {
-          cur[i] = S.nxt[cur[i]];  // > cur (a sequence is >= 1 byte), or cs, or a marker
-          any = true;
-        }
+        const uint32_t lim = ((t + (uint32_t)LZ_PAR_T * i) / LZ_PAR_CHUNK + 1) * LZ_PAR_CHUNK;
+        const bool act = cur[i] < lim && cur[i] < cs;
+        const uint32_t v = S.nxt[act ? cur[i] : 0u];  // > cur, or cs, or a marker
+        cur[i] = act ? v : cur[i];
+        any |= act;
       }
       if (!any) break;
     }
 #pragma unroll
     for (int i = 0; i < LZ_PAR_PPT; ++i) {
-      const uint32_t p = t + 256u * i;
+      const uint32_t p = t + (uint32_t)LZ_PAR_T * i;
       if (p < cs) S.ext[p] = (uint16_t)(cur[i] > 0xFFFFu ? LZ_BAD : cur[i]);
     }
   }
   __syncthreads();
+  LZST(3);
   // 3. the chain of chunk entries, one step per chunk
   if (t == 0) {
     uint32_t p = 0, st = 0, guard = 0;
@@ -606,8 +642,9 @@ __global__ void __launch_bounds__(256) lz4_decode_par_kernel(const uint8_t* __re
     }
     return;
   }
+  LZST(4);
   // 4. each entered chunk flags its true tokens
-  for (int c = t; c < LZ_PAR_NCH; c += 256) {
+  for (int c = t; c < LZ_PAR_NCH; c += LZ_PAR_T) {
     uint32_t p = S.entry[c];
     if (p == LZ_BAD) continue;
     const uint32_t lim = (uint32_t)(c + 1) * LZ_PAR_CHUNK;
@@ -617,19 +654,21 @@ __global__ void __launch_bounds__(256) lz4_decode_par_kernel(const uint8_t* __re
     }
   }
   __syncthreads();
-  // 5. output offsets: block scan of the true tokens' decoded lengths (positions in order)
-  uint32_t len[LZ_PAR_PPT], mine = 0;
+  LZST(5);
+  // 5. output offsets: block scan of the true tokens' decoded lengths (positions in order;
+  // thread t owns the contiguous positions [t * PPT, (t + 1) * PPT); the lengths are parked in
+  // ooff, then overwritten by the offsets)
   {
-    // thread t owns the contiguous positions [t * PPT, (t + 1) * PPT): scan order = position order
-#pragma unroll
-    for (int i = 0; i < LZ_PAR_PPT; ++i) {
-      const uint32_t p = (uint32_t)t * LZ_PAR_PPT + i;
-      len[i] = 0;
-      if (p < cs && S.tok[p]) {
+    const uint32_t p0 = (uint32_t)t * LZ_PAR_PPT;
+    uint32_t mine = 0;
+    for (uint32_t p = p0; p < p0 + LZ_PAR_PPT && p < cs; ++p) {
+      uint32_t len = 0;
+      if (S.tok[p]) {
         const LzSeq q = lz_parse_at(cb, p, cs);
-        len[i] = q.L + q.M;
+        len = q.L + q.M;
       }
-      mine += len[i];
+      S.ooff[p] = (uint16_t)(len > 0xFFFFu ? 0xFFFFu : len);
+      mine += len;
     }
     uint32_t tot;
     uint32_t run = block_excl_scan(mine, S.wsum, &tot);
@@ -637,19 +676,19 @@ __global__ void __launch_bounds__(256) lz4_decode_par_kernel(const uint8_t* __re
       if (t == 0) dsize[b] = LZ_PAR_FALLBACK;
       return;  // identical in every thread
     }
-#pragma unroll
-    for (int i = 0; i < LZ_PAR_PPT; ++i) {
-      const uint32_t p = (uint32_t)t * LZ_PAR_PPT + i;
-      if (p < cs) S.ooff[p] = (uint16_t)run;
-      run += len[i];
+    for (uint32_t p = p0; p < p0 + LZ_PAR_PPT && p < cs; ++p) {
+      const uint32_t len = S.ooff[p];
+      S.ooff[p] = (uint16_t)run;
+      run += len;
     }
     if (t == 0) S.total = tot;
   }
   __syncthreads();
   const uint32_t total = S.total;
+  LZST(6);
   // 6. every output byte's source (offsets checked against the block's history)
   bool bad = false;
-  for (uint32_t p = t; p < cs; p += 256) {
+  for (uint32_t p = t; p < cs; p += LZ_PAR_T) {
     if (!S.tok[p]) continue;
     const LzSeq q = lz_parse_at(cb, p, cs);
     const uint32_t o = S.ooff[p];
@@ -671,12 +710,13 @@ __global__ void __launch_bounds__(256) lz4_decode_par_kernel(const uint8_t* __re
     }
     return;
   }
+  LZST(7);
   // pointer jumping: every byte ends on a literal
   for (int round = 0; round < 14; ++round) {
     if (t == 0) S.changed = 0;
     __syncthreads();
     bool ch = false;
-    for (uint32_t p = t; p < total; p += 256) {
+    for (uint32_t p = t; p < total; p += LZ_PAR_T) {
       const uint16_t v = S.src[p];
       if (!(v & LZ_LIT)) {
         const uint16_t u = S.src[v];  // v < p: an earlier output byte
@@ -689,9 +729,10 @@ __global__ void __launch_bounds__(256) lz4_decode_par_kernel(const uint8_t* __re
     if (!S.changed) break;
     __syncthreads();
   }
+  LZST(8);
   // 7. bytes out: 4 per thread per step, one 32-bit store when whole
   uint8_t* dst = slots + (uint64_t)b * bmax;
-  for (uint32_t p0 = 4 * t; p0 < total; p0 += 4 * 256) {
+  for (uint32_t p0 = 4 * t; p0 < total; p0 += 4 * LZ_PAR_T) {
     uint32_t wv = 0;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -707,7 +748,14 @@ __global__ void __launch_bounds__(256) lz4_decode_par_kernel(const uint8_t* __re
       for (uint32_t e = 0; p0 + e < total; ++e) dst[p0 + e] = (uint8_t)(wv >> (8 * e));
   }
   if (t == 0) dsize[b] = total;
+  LZST(9);
 }
+
+#ifdef DPZ_STAMPS
+extern "C" int dpz_debug_lz4_stamps(unsigned long long* host_out) {
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_lz_st), sizeof(g_lz_st));
+}
+#endif
 
 // independent frames: slot b (dsize[b] bytes at b * bmax) -> out + prefix
 __global__ void __launch_bounds__(256) lz4_gather_kernel(const uint8_t* __restrict__ slots,
@@ -933,9 +981,21 @@ extern "C" int dpz_lz4_decompress(const uint8_t* frame_dev, const uint8_t* frame
   if (ws_bytes < dpz_lz4_workspace_bytes(0, nb, linked ? 0 : bmax) || !ws) return DPZ_ERR_WORKSPACE;
   const uint8_t flg = frame_host[4];
   const bool bsum = flg & 0x10;
-  // block table from the host bytes
-  LzBlock* tab_h = static_cast<LzBlock*>(malloc(sizeof(LzBlock) * (size_t)(nb + 1)));
-  if (!tab_h) return DPZ_ERR_INTERNAL;
+  // block table from the host bytes, built in a pinned buffer of this thread (the H2D is a true
+  // async DMA; the buffer is reused only after this call's final synchronize)
+  thread_local LzBlock* tab_pin = nullptr;
+  thread_local size_t tab_cap = 0;
+  const size_t tab_need = sizeof(LzBlock) * (size_t)(nb + 1) + 16;
+  if (tab_cap < tab_need) {
+    if (tab_pin) (void)hipHostFree(tab_pin);
+    tab_pin = nullptr;
+    tab_cap = 0;
+    void* pp = nullptr;
+    if (hipHostMalloc(&pp, tab_need * 2) != hipSuccess || !pp) return DPZ_ERR_INTERNAL;
+    tab_pin = static_cast<LzBlock*>(pp);
+    tab_cap = tab_need * 2;
+  }
+  LzBlock* tab_h = tab_pin;
   int64_t pos = 6 + ((flg & 0x08) ? 8 : 0) + ((flg & 0x01) ? 4 : 0) + 1;
   for (int64_t b = 0; b < nb; ++b) {
     const uint8_t* p = frame_host + pos;
@@ -958,20 +1018,12 @@ extern "C" int dpz_lz4_decompress(const uint8_t* frame_dev, const uint8_t* frame
   hipError_t e = hipMemcpyAsync(tab, tab_h, sizeof(LzBlock) * (size_t)(nb > 0 ? nb : 1),
                                 hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemsetAsync(status, 0, 16, st);
-  if (e != hipSuccess) {
-    (void)hipStreamSynchronize(st);
-    free(tab_h);
-    return (int)e;
-  }
-  // tab_h stays allocated until the call's final synchronize (the copy may read it until then)
-  struct FreeAtExit {
-    void* p;
+  // the pinned table is reused by the next call: every return below waits for this one's DMA
+  struct SyncAtExit {
     hipStream_t s;
-    ~FreeAtExit() {
-      (void)hipStreamSynchronize(s);
-      free(p);
-    }
-  } tab_guard{tab_h, st};
+    ~SyncAtExit() { (void)hipStreamSynchronize(s); }
+  } tab_guard{st};
+  if (e != hipSuccess) return (int)e;
   uint64_t tot = 0;
   uint32_t bad = 0;
   if (nb > 0) {
@@ -992,7 +1044,7 @@ extern "C" int dpz_lz4_decompress(const uint8_t* frame_dev, const uint8_t* frame
                                     (uint64_t)out_cap, total, status, 0));
     } else {
       if (par)
-        DPZ_TIMED(DPZ_KT_LZ4, st, lz4_decode_par_kernel<<<(unsigned)nb, 256, 0, st>>>(
+        DPZ_TIMED(DPZ_KT_LZ4, st, lz4_decode_par_kernel<<<(unsigned)nb, LZ_PAR_T, 0, st>>>(
                                       frame_dev, tab, (uint32_t)bmax, slots, dsize, status));
       // the blocks the parallel decoder left (raw, large; all of them without it)
       DPZ_TIMED(DPZ_KT_LZ4, st, lz4_decode_kernel<<<(unsigned)nb, 64, shm, st>>>(
@@ -1002,9 +1054,12 @@ extern "C" int dpz_lz4_decompress(const uint8_t* frame_dev, const uint8_t* frame
                                     slots, dsize, nb, (uint32_t)bmax, out, (uint64_t)out_cap,
                                     total));
     }
-    DPZ_HIP_TRY(hipMemcpyAsync(&tot, total, 8, hipMemcpyDeviceToHost, st));
-    DPZ_HIP_TRY(hipMemcpyAsync(&bad, status, 4, hipMemcpyDeviceToHost, st));
+    // status (4 bytes, padding) and total (8 bytes) are adjacent: one copy back
+    uint64_t back[2] = {0, 0};
+    DPZ_HIP_TRY(hipMemcpyAsync(back, status, 16, hipMemcpyDeviceToHost, st));
     DPZ_HIP_TRY(hipStreamSynchronize(st));
+    bad = (uint32_t)back[0];
+    tot = back[1];
   }
   if (bad) return DPZ_ERR_ARG;
   if (cs >= 0 && (int64_t)tot != cs) return DPZ_ERR_ARG;
