@@ -1606,7 +1606,8 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
       }
     // The walk fold (no offsets pre-pass) takes all-sparse groups of a fresh total where it
     // measured faster on MI355X (M = 25 M, tools/diag/fold_kinds.py): a node's few neighbours
-    // at any alpha; 16 payloads at alpha 0.02 .. 0.2 (the hit-chain fold below that, the phase
+    // at any alpha; 16 payloads at alpha 0.0175 .. 0.2 (16 x 0.015: hit-chain 137 vs walk 147 us,
+    // 16 x 0.02: 163 vs 149 us, profiles/r03_s2_fold_a001.jsonl; the hit-chain fold below, the phase
     // fold above).  DPZ_FOLD_KIND=1 / 2 / 4 forces the classic /
     // 4-slot group / walk fold (A/B diagnostics; a forced kind that cannot take the group runs
     // the classic kernel).
@@ -1619,7 +1620,7 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
       }
     const int kind = getenv("DPZ_FOLD_KIND") ? atoi(getenv("DPZ_FOLD_KIND")) : 0;
     const double avg = fa.np > 0 ? (double)etot / (double)fa.np / (double)n : 0.0;
-    bool use_walk = walk_ok(fa) && (fa.np <= 4 || (avg >= 0.02 && avg <= 0.21));
+    bool use_walk = walk_ok(fa) && (fa.np <= 4 || (avg >= 0.0175 && avg <= 0.21));
     if (kind) use_walk = walk_ok(fa) && kind == 4;
     if (use_walk) {
       const int rc = launch_walk(fa, vec && n >= 1024, dens, st);
