@@ -988,7 +988,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ cidx,
     const uint32_t* __restrict__ ckey, const float* __restrict__ cval, const float* vals_src,
     int32_t* idx_out, float* val_out, int32_t* counter, float* rewind, int32_t* status_out,
-    ReplaceJob pj) {
+    ReplaceJob pj, int64_t nrep_first) {
   __shared__ uint32_t wcnt[CSEG];
   __shared__ uint32_t subbase[NSUB + 1];
   __shared__ uint32_t flag, spec;
@@ -997,13 +997,16 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   __shared__ uint32_t bsk[BLDS], bsi[BLDS];
   const int64_t CB_ = (W + CSEG - 1) / CSEG;
   const int64_t B = (W + 3) / 4;  // filter blocks (above counts)
-  if ((int64_t)blockIdx.x >= CB_) {  // co-scheduled replace decode
-    replace_block(pj, (int64_t)blockIdx.x - CB_);
+  // co-scheduled replace decode: its blocks after compact's own, or (nrep_first > 0) before
+  // them, dispatched first so their stores overlap the compact blocks' dependent prologue
+  if (nrep_first > 0 ? (int64_t)blockIdx.x < nrep_first : (int64_t)blockIdx.x >= CB_) {
+    replace_block(pj, nrep_first > 0 ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - CB_);
     return;
   }
+  const uint32_t blk = (uint32_t)((int64_t)blockIdx.x - (nrep_first > 0 ? nrep_first : 0));
   STAMP_T0(0);
   const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
-  const int64_t seg0 = (int64_t)blockIdx.x * CSEG + wid * 2;
+  const int64_t seg0 = (int64_t)blk * CSEG + wid * 2;
   // every independent load first: control words, sub-list counts, above counts, own candidates
   const uint32_t status = ctrl->status;
   const uint32_t need = ctrl->need, lo = ctrl->lo, shift = ctrl->shift, bstar = ctrl->bstar;
@@ -1026,7 +1029,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
       v1 = reinterpret_cast<const uint4*>(blkabove)[2 * t + 1];
     }
     const uint32_t v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    const uint32_t fbx = blockIdx.x * (uint32_t)(CSEG / 4);  // first filter block of this block
+    const uint32_t fbx = blk * (uint32_t)(CSEG / 4);  // first filter block of this block
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       abv_all += v[q];
@@ -1052,11 +1055,11 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     ii[u][0] = seg < W ? cidx[seg * CAP + lane] : 0u;
     if (cval && seg < W) vv[u][0] = cval[seg * CAP + lane];
   }
-  if (blockIdx.x == 0) {  // leave the sample histogram zeroed for the next call
+  if (blk == 0) {  // leave the sample histogram zeroed for the next call
     for (int b = t; b < CB; b += 256) chist[b] = 0;
   }
   if (status) {  // select reported a miss: the host runs the exact path
-    if (blockIdx.x == 0 && t == 0) {
+    if (blk == 0 && t == 0) {
       atomicOr(&ctrl->sticky, status);
       if (status_out) *status_out = (int32_t)status;
     }
@@ -1093,7 +1096,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   }
   __syncthreads();
   if (flag) {  // identical in every block
-    if (blockIdx.x == 0 && t == 0) {
+    if (blk == 0 && t == 0) {
       ctrl->status = 1;
       atomicOr(&ctrl->sticky, 1u);
       if (status_out) *status_out = 1;
@@ -1115,7 +1118,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   block_resolve(bd, need, lo + (bstar << shift), shift, RL, &T, &icut);
   STAMP_T0(2);
   // selected boundary entries before this block / overall, plus the above counts
-  const uint32_t bstart = (uint32_t)((int64_t)blockIdx.x * CSEG * R);
+  const uint32_t bstart = (uint32_t)((int64_t)blk * CSEG * R);
   uint32_t sb_before = 0, sb_all = 0;
   bd.each([&](uint32_t kv, uint32_t iv) {
     const bool sel = kv > T || (kv == T && iv <= icut);
@@ -1125,7 +1128,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   const uint64_t tot2 = block_sum64(((uint64_t)(abv_all + sb_all) << 32) |
                                         (uint64_t)(abv_before + sb_before), wsum64);
   const uint32_t boff = (uint32_t)tot2, grand = (uint32_t)(tot2 >> 32);
-  if (blockIdx.x == 0 && t == 0) {
+  if (blk == 0 && t == 0) {
     ctrl->T = T;
     ctrl->icut = icut;
     if (grand != (uint32_t)k) {  // internal inconsistency
@@ -1275,7 +1278,7 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
   ReplaceJob jb[3] = {};
   unsigned pb[3] = {0, 0, 0};
   // a scatter job (dpz_topk_encode_replace over the tensor being encoded): the filter writes
-  // out = x as it streams x, and the entries are scattered in the select launch (after it)
+  // out = x as it streams x, and the entries are scattered in blocks of the compact launch
   float* copy_out = (a.job && phases == 3 && a.job->scatter) ? a.job->out : nullptr;
   if (a.job && phases == 3) {
     const int64_t C = a.job->c1 - a.job->c0;
@@ -1360,14 +1363,17 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
   // DPZ_COUNTER_PLAIN=0 / 1 forces the counter update form (A/B diagnostics)
   bool plain = a.k > a.n / 32;
   if (const char* e = getenv("DPZ_COUNTER_PLAIN")) plain = atoi(e) != 0;
+  // DPZ_SCATTER_FIRST=1: the decode's blocks dispatched ahead of compact's own (A/B)
+  const char* sfe = getenv("DPZ_SCATTER_FIRST");
+  const int64_t nrep_first = (sfe && atoi(sfe) != 0) ? (int64_t)pb[2] : 0;
   if (plain)
     DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC, true><<<ncmp + pb[2], 256, 0, a.st>>>(
         s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, cidx,
-        ckey, cval, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, a.status_out, jb[2]));
+        ckey, cval, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, a.status_out, jb[2], nrep_first));
   else
     DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC, false><<<ncmp + pb[2], 256, 0, a.st>>>(
         s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, cidx,
-        ckey, cval, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, a.status_out, jb[2]));
+        ckey, cval, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, a.status_out, jb[2], nrep_first));
   return DPZ_OK;
 }
 

@@ -109,7 +109,11 @@ int dpz_topk_encode(const float* x, const float* x0, float* acc, int acc_mode,
  * does not pay).  Otherwise the decode is enqueued first on `stream`, then the encode.
  * r_out may not overlap r_local or any buffer of the encode (DPZ_ERR_ARG).  The decode is
  * complete when the encode's stream work is (DPZ_TOPK_ASYNC applies to both); the STREAM / TAIL
- * phase flags are not accepted.  r_ws: the decode workspace (only used when not carried).      */
+ * phase flags are not accepted.  r_ws: the decode workspace (only used when not carried).
+ * Decoding over the tensor being encoded (r_local == x, r_n == n, acc_mode DPZ_ACC_NONE: the
+ * reference decodes a neighbour's payload over the node's own model, the one it just encoded)
+ * is FUSED: the encoder's streaming filter writes r_out = x while it reads x, and only the r_k
+ * entries are scattered afterwards, in blocks of the compact launch (4n fewer bytes read). */
 int dpz_topk_encode_replace(const float* x, const float* x0, float* acc, int acc_mode,
                             const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
                             float* val_out, int32_t* counter, void* ws, size_t ws_bytes, int flags,

@@ -671,7 +671,7 @@ def test_coscheduled_replace_rejects_aliasing(dev):
         codec.topk_encode(tx, 10_000, x0=tx0, co_replace=(tx0.clone(), p_idx, p_val, tx))
 
 
-@pytest.mark.parametrize("where", ["select", "compact", "split"])
+@pytest.mark.parametrize("where", ["select", "compact", "split", "compact-first"])
 @pytest.mark.parametrize("n,alpha,rk,dup,layout", [
     (11_000_000, 0.01, 110_000, False, None),      # C2: the bench's one-node step
     (16_777_216, 0.01, 167_772, False, None),      # 64 MiB
@@ -686,7 +686,9 @@ def test_encode_with_fused_replace(dev, n, alpha, rk, dup, layout, where, monkey
     writes out = x as it streams x and the select launch (or, DPZ_SCATTER_AT=compact, the
     compact launch) scatters the entries (dpz_topk_encode_replace); equals encode +
     T = x.copy(); T[idx] = vals, bit-exact."""
-    monkeypatch.setenv("DPZ_SCATTER_AT", where)
+    monkeypatch.setenv("DPZ_SCATTER_AT", where.split("-")[0])
+    # compact-first: the decode's blocks dispatched ahead of compact's own (DPZ_SCATTER_FIRST)
+    monkeypatch.setenv("DPZ_SCATTER_FIRST", "1" if where.endswith("first") else "0")
     codec = _codec()
     k = round(alpha * n)
     if layout == "miss":
