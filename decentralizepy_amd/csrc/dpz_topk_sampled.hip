@@ -652,28 +652,35 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
     const uint32_t cnt = u ? cnt1 : cnt0;
     uint32_t above = 0;
     if (seg < W && cnt != DENSE) {
-      for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
-        const uint32_t j = j0 + lane;
-        uint32_t key = 0, b = 0, idx = 0;
-        if (j < cnt) {
-          const uint32_t c = j0 >> 6;
-          if (c < (uint32_t)PFS) {
-            key = 0u;
-            idx = 0u;
 #pragma unroll
-            for (int cc = 0; cc < PFS; ++cc)
-              if (cc == (int)c) {
-                key = pk[u][cc];
-                idx = pi[u][cc];
-              }
-          } else {
-            key = ckey[seg * CAP + j];
-            idx = cidx[seg * CAP + j];
-          }
-          b = fine_bin(key, lo, hi, shift);
-        }
+      for (int c = 0; c < PFS; ++c) {  // the chunks held in registers
+        const uint32_t j = c * 64u + lane;
+        if (c * 64u >= cnt) break;
+        const uint32_t key = pk[u][c], idx = pi[u][c];
+        const uint32_t b = j < cnt ? fine_bin(key, lo, hi, shift) : 0u;
         above += (uint32_t)__popcll(__ballot(j < cnt && b > bstar));
         append(j < cnt && b == bstar, key, idx);
+      }
+      // dense alpha: the chunks past them four at a time, every key load in flight together
+      // (one chunk per iteration was one dependent round trip each); the index only for the
+      // rare bin-b* entries
+      for (uint32_t j0 = PFS * 64u; j0 < cnt; j0 += 4 * 64u) {
+        uint32_t kg[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint32_t j = j0 + g * 64u + lane;
+          kg[g] = ckey[seg * CAP + (j < cnt ? j : 0u)];
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint32_t j = j0 + g * 64u + lane;
+          const bool v = j < cnt;
+          const uint32_t b = v ? fine_bin(kg[g], lo, hi, shift) : 0u;
+          above += (uint32_t)__popcll(__ballot(v && b > bstar));
+          const bool ap = v && b == bstar;
+          const uint32_t idx = ap ? cidx[seg * CAP + j] : 0u;
+          append(ap, kg[g], idx);
+        }
       }
     } else if (seg < W) {
       const int64_t beg = seg * R;
@@ -1172,11 +1179,22 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
         const uint32_t j = c * 64u + lane;
         mine += (uint32_t)__popcll(__ballot(j < cnt[u] && is_sel(kk[u][c], ii[u][c])));
       }
-      for (uint32_t j0 = PFC * 64u; j0 < cnt[u]; j0 += 64) {
-        const uint32_t j = j0 + lane;
-        bool sel = false;
-        if (j < cnt[u]) sel = is_sel(ckey[seg * CAP + j], cidx[seg * CAP + j]);
-        mine += (uint32_t)__popcll(__ballot(sel));
+      // dense alpha: the chunks past the registers four at a time (keys in flight together;
+      // the index only for a tie with T)
+      for (uint32_t j0 = PFC * 64u; j0 < cnt[u]; j0 += 4 * 64u) {
+        uint32_t kg[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint32_t j = j0 + g * 64u + lane;
+          kg[g] = ckey[seg * CAP + (j < cnt[u] ? j : 0u)];
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint32_t j = j0 + g * 64u + lane;
+          bool sel = false;
+          if (j < cnt[u]) sel = kg[g] > T || (kg[g] == T && cidx[seg * CAP + j] <= icut);
+          mine += (uint32_t)__popcll(__ballot(sel));
+        }
       }
     } else if (seg < W) {
       mine = dense_count<VEC>(s, seg, R, n, lo, T, icut);
@@ -1216,19 +1234,24 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
         if (c * 64u < cnt[u])
           emit(j < cnt[u] && is_sel(kk[u][c], ii[u][c]), ii[u][c], vv[u][c], true, cc[u][c]);
       }
-      for (uint32_t j0 = PFC * 64u; j0 < cnt[u]; j0 += 64) {
-        const uint32_t j = j0 + lane;
-        bool sel = false;
-        uint32_t idx = 0, cw = 0;
-        float v = 0.f;
-        if (j < cnt[u]) {
-          const uint32_t key = ckey[seg * CAP + j];
-          idx = cidx[seg * CAP + j];
-          if (cval) v = cval[seg * CAP + j];
-          sel = is_sel(key, idx);
-          if (PLAIN && counter && sel) cw = (uint32_t)counter[idx];
+      for (uint32_t j0 = PFC * 64u; j0 < cnt[u]; j0 += 4 * 64u) {  // four chunks at a time
+        uint32_t kg[4], ig[4];
+        float vg[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint32_t j = j0 + g * 64u + lane;
+          const uint32_t jc = seg * CAP + (j < cnt[u] ? j : 0u);
+          kg[g] = ckey[jc];
+          ig[g] = cidx[jc];
+          vg[g] = cval ? cval[jc] : 0.f;
         }
-        emit(sel, idx, v, false, cw);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint32_t j = j0 + g * 64u + lane;
+          const bool sel = j < cnt[u] && is_sel(kg[g], ig[g]);
+          const uint32_t cw = (PLAIN && counter && sel) ? (uint32_t)counter[ig[g]] : 0u;
+          emit(sel, ig[g], vg[g], false, cw);
+        }
       }
     } else {
       dense_write<VEC>(s, seg, R, n, k, lo, T, icut, run, vals_src, idx_out, val_out, counter,
