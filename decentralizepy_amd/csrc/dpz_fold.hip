@@ -117,6 +117,14 @@ __global__ void __launch_bounds__(256) fold_offsets_kernel(FoldArgs a, int32_t* 
   }
 }
 
+// A payload pointer rebuilt from lane registers (readlane) or read back from an LDS table has lost
+// its address space: loads through it compile to FLAT loads, which count on lgkmcnt as well as vmcnt, so every LDS wait
+// of the fold would also wait for the window loads in flight.  Global loads count on vmcnt only.
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* as_global(const T* p) {
+  return (const __attribute__((address_space(1))) T*)p;
+}
+
 // one payload term of the fold in the reference's fp32 order: the first term of a fresh total is
 // t*w (+0 first with a zero base), later terms add; replace-only keeps the payload value
 __device__ __forceinline__ void fold_term(float& acc, float tv, float w, bool first_term,
@@ -151,16 +159,16 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
   const int t = threadIdx.x;
   // payload pointer table in LDS: the entry loads below pick their payload per lane, and a
   // per-lane index into the kernel-argument array is a dependent global load per tile
-  __shared__ const int32_t* s_idx[FOLD_MAXP];
-  __shared__ const float* s_val[FOLD_MAXP];
+  __shared__ const __attribute__((address_space(1))) int32_t* s_idx[FOLD_MAXP];  // as_global
+  __shared__ const __attribute__((address_space(1))) float* s_val[FOLD_MAXP];
   __shared__ uint32_t s_nhit;
   __shared__ uint32_t s_pool_n;                // rows of s_pool taken in this tile
   __shared__ float s_pool[FOLD_POOL][FOLD_MAXP];  // payload values of elements hit >= 3 times
   __shared__ float s_w[FOLD_MAXP];
   if (t == 0) {
     for (int p = 0; p < a.np; ++p) {
-      s_idx[p] = a.p[p].idx;
-      s_val[p] = a.p[p].val;
+      s_idx[p] = as_global(a.p[p].idx);
+      s_val[p] = as_global(a.p[p].val);
       s_w[p] = a.p[p].w;
     }
   }
@@ -630,14 +638,14 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_group_kernel(FoldArgs a)
   __shared__ uint32_t hf[FOLD_TILE / 4];  // hit flags: byte e of word w = element 4w + e
   __shared__ int32_t rng[FOLD_MAXP][2];
   __shared__ int32_t pre[FOLD_MAXP + 1];
-  __shared__ const int32_t* s_idx[FOLD_MAXP];
-  __shared__ const float* s_val[FOLD_MAXP];
+  __shared__ const __attribute__((address_space(1))) int32_t* s_idx[FOLD_MAXP];  // as_global
+  __shared__ const __attribute__((address_space(1))) float* s_val[FOLD_MAXP];
   __shared__ float s_w[FOLD_MAXP];
   const int t = threadIdx.x;
   if (t == 0) {
     for (int p = 0; p < a.np; ++p) {
-      s_idx[p] = a.p[p].idx;
-      s_val[p] = a.p[p].val;
+      s_idx[p] = as_global(a.p[p].idx);
+      s_val[p] = as_global(a.p[p].val);
       s_w[p] = a.p[p].w;
     }
   }
@@ -1172,7 +1180,7 @@ constexpr int FW_G = 4;  // payloads per group: the windows of one group are in 
 // registers, so every window load is in flight while the group before it folds, with 16
 // registers of windows whatever the payload count.  Cursors live one per lane (lane p: payload
 // p) in one register.
-template <bool VEC, int EPL, bool ONE>
+template <bool VEC, int EPL, bool ONE, int DIST>
 __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64_t tpw) {
   constexpr int TE = 64 * EPL;
   __shared__ float s_val[FW_WAVES][TE];
@@ -1193,6 +1201,9 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
   // pointers / sizes / weights and cursors stay in scalar registers; otherwise the group loop is
   // dynamic and the cursors live one per lane (lane p: payload p) in one register
   const int ng = ONE ? 1 : (np + FW_G - 1) / FW_G;
+  // CT: every payload number in the loop is a compile-time constant (ONE; DIST 3, whose four
+  // groups are unrolled): the cursors in scalar registers (no readlane / writelane round trips)
+  constexpr bool CT = ONE || DIST == 3;
   const int lp = lane < np && lane < FOLD_MAXP ? lane : 0;
   const int32_t kl = lane < np ? (int32_t)a.p[lp].k : 0;
   // !ONE: payload p's pointers and weight held by lane p, read back with readlane (no scalar
@@ -1215,20 +1226,21 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
   auto P_w = [&](int p) {
     return ONE ? a.p[p].w : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl), p));
   };
-  int32_t cs[FW_G];  // ONE: the cursors
+  static_assert(DIST == 1 || (DIST == 3 && !ONE), "DIST 3: four groups");
+  int32_t cs[FOLD_MAXP];  // CT: the cursors (scalar registers)
   // ---- start cursors: 64-ary lower_bound(idx_p, t0 * TE), payload by payload ----
   int32_t curv = 0;
   {
     const int32_t e0 = (int32_t)(t0 * TE);
     for (int p = 0; p < np; ++p) {
-      const int32_t* ip = P_idx(p);
+      const int32_t* ip = reinterpret_cast<const int32_t*>(rl64(ipl, p));  // p: run time
       int32_t lo = 0, hi = fw_uni(__builtin_amdgcn_readlane(kl, p));
       while (hi > lo) {
         const int32_t len = hi - lo;
         const int32_t stride = len <= 64 ? 1 : (len + 63) / 64;
         const int64_t q = (int64_t)lo + (int64_t)lane * stride;
         const bool ok = q < hi;
-        const int32_t x = ip[ok ? q : lo];
+        const int32_t x = as_global(ip)[ok ? q : lo];
         const int32_t c = (int32_t)__popcll(__ballot(ok && x < e0));  // a prefix
         if (stride == 1) {
           lo += c;
@@ -1242,21 +1254,19 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
       curv = lane == p ? lo : curv;
     }
   }
-  if (ONE) {
+  if (CT) {
 #pragma unroll
-    for (int q = 0; q < FW_G; ++q) cs[q] = fw_uni(__builtin_amdgcn_readlane(curv, q));
+    for (int q = 0; q < (ONE ? FW_G : FOLD_MAXP); ++q) cs[q] = fw_uni(__builtin_amdgcn_readlane(curv, q));
   }
   auto cur_of = [&](int p) {
-    return ONE ? cs[p & (FW_G - 1)] : fw_uni(__builtin_amdgcn_readlane(curv, p));
+    return CT ? cs[ONE ? (p & (FW_G - 1)) : p] : fw_uni(__builtin_amdgcn_readlane(curv, p));
   };
   auto set_cur = [&](int p, int32_t v) {
-    if (ONE) cs[p & (FW_G - 1)] = fw_uni(v);
+    if (CT) cs[ONE ? (p & (FW_G - 1)) : p] = fw_uni(v);
     else curv = lane == p ? v : curv;
   };
   // ---- the windows of one group: (idx, val) at cur + lane, branch-free loads of raw values
   // (lanes past k read entry 0 and are masked when the window is used) ----
-  int32_t wi[FW_G], wn[FW_G];
-  float wvv[FW_G], wvn[FW_G];
   auto load_group = [&](int g, int32_t (&ix)[FW_G], float (&vx)[FW_G]) {
 #pragma unroll
     for (int q = 0; q < FW_G; ++q) {
@@ -1269,12 +1279,25 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
       const int32_t jc = j < k ? j : 0;
       // an empty payload's arrays may be null: read a valid address instead (masked at use)
       const bool has = kp > 0;
-      ix[q] = (has ? P_idx(pc) : reinterpret_cast<const int32_t*>(a.local))[jc];
-      vx[q] = (has ? P_val(pc) : a.local)[jc];
+      ix[q] = as_global(has ? P_idx(pc) : reinterpret_cast<const int32_t*>(a.local))[jc];
+      vx[q] = as_global(has ? P_val(pc) : a.local)[jc];
     }
   };
+  // DIST 1: the windows of the group being folded and of the next one (wi, wn);
+  // DIST 3 (four groups, 13..16 payloads): all four groups' windows in registers, each group's
+  // issued three groups ahead (into the slot the group before it just freed), so three groups'
+  // loads are in flight while one folds
+  constexpr int NSL = DIST == 3 ? FW_G : 2;
+  int32_t WI[NSL][FW_G];
+  float WV[NSL][FW_G];
   FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n), Ln;
-  load_group(0, wi, wvv);
+  if constexpr (DIST == 3) {
+    load_group(0, WI[0], WV[0]);
+    load_group(1, WI[1], WV[1]);
+    load_group(2, WI[2], WV[2]);
+  } else {
+    load_group(0, WI[0], WV[0]);
+  }
   uint32_t seq = 0;
   auto tile_body = [&](int64_t tile, auto guard) {
     constexpr bool GUARD = decltype(guard)::value;
@@ -1289,8 +1312,9 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
       base[e] = a.zero_base ? 0.0f : L.v[e];
       acc[e] = 0.0f;
     }
-    for (int gg = 0; gg < ng; ++gg) {
-      const int g = ONE ? 0 : gg;
+    // one group: its windows (wi, wvv) are in registers; `issue` starts a later group's loads
+    // once this group's cursors have advanced
+    auto fold_group = [&](int g, int32_t (&wi)[FW_G], float (&wvv)[FW_G], auto issue) {
       // this group's window starts; the entries of the tile are the leading lanes below thi
       int32_t c0[FW_G], cnt[FW_G];
 #pragma unroll
@@ -1303,8 +1327,7 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
         // the next tile's window start of this payload (a full window is finished in its phase)
         if (live) set_cur(p, c0[q] + cnt[q]);
       }
-      // the next group's windows (this tile's next group, or group 0 of the next tile)
-      load_group(g + 1 < ng ? g + 1 : 0, wn, wvn);
+      issue();
 #pragma unroll
       for (int q = 0; q < FW_G; ++q) {
         const int p = g * FW_G + q;
@@ -1325,18 +1348,19 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
           int32_t c = 64;
           for (int32_t j0 = c0[q] + 64;; j0 += 64) {
             const int32_t j = j0 + lane;
-            const int32_t iv = j < k ? pi[j] : INT32_MAX;
+            const int32_t iv = j < k ? as_global(pi)[j] : INT32_MAX;
             const int cc = fw_lead(iv < thi32);
             const uint32_t pos = (uint32_t)(iv - tlo32);
             if (lane < cc && pos < (uint32_t)TE) {
-              wv[pos] = pv[j];
+              wv[pos] = as_global(pv)[j];
               wt[pos] = tag;
             }
             c += cc;
             if (cc < 64) break;
           }
           set_cur(p, c0[q] + c);
-          if (ng == 1) load_group(0, wn, wvn);  // the next tile's window of this group moved
+          // the next tile's window of this group moved (DIST 1, one group: already issued)
+          if (DIST == 1 && ng == 1) load_group(0, WI[1], WV[1]);
         }
         // the row is this wave's own and one wave's LDS instructions execute in order, so the
         // lanes' writes above are seen by the reads below with no wait; the scheduling barriers
@@ -1369,10 +1393,27 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
           acc[e] = p == 0 ? (a.zero_base ? 0.0f + term : term) : acc[e] + term;
         }
       }
+    };
+    if constexpr (DIST == 3) {
+      // group g of this tile issues group g + 3: group 3 of this tile (g = 0), else group g - 1
+      // of the next tile, into the slot group g - 1 freed
 #pragma unroll
-      for (int q = 0; q < FW_G; ++q) {
-        wi[q] = wn[q];
-        wvv[q] = wvn[q];
+      for (int g = 0; g < FW_G; ++g) {
+        fold_group(g, WI[g], WV[g], [&] {
+          const int s3 = (g + 3) & (FW_G - 1);
+          load_group(s3, WI[s3], WV[s3]);
+        });
+      }
+    } else {
+      for (int gg = 0; gg < ng; ++gg) {
+        const int g = ONE ? 0 : gg;
+        // the next group's windows (this tile's next group, or group 0 of the next tile)
+        fold_group(g, WI[0], WV[0], [&] { load_group(g + 1 < ng ? g + 1 : 0, WI[1], WV[1]); });
+#pragma unroll
+        for (int q = 0; q < FW_G; ++q) {
+          WI[0][q] = WI[1][q];
+          WV[0][q] = WV[1][q];
+        }
       }
     }
     if (a.add_self) {
@@ -1418,8 +1459,15 @@ static inline int64_t fold_ntiles(int64_t n) { return (n + FOLD_TILE - 1) / FOLD
 // The walk fold's launch: EPL from the densest payload (~32 entries per payload per tile on
 // average at dens <= 0.125: 256-element tiles; denser payloads 128-element tiles); a
 // persistent grid of what the CUs hold, each wave a contiguous run of tiles.
-template <bool VEC, int EPL, int NS>
+template <bool VEC, int EPL, int NS, int DIST = 1>
 static int launch_walk_t(const FoldArgs& fa, hipStream_t st) {
+  // 13..16 payloads (four groups): the groups kernel with windows issued three groups ahead
+  // (DPZ_FOLD_DIST=1: one group ahead, A/B)
+  if constexpr (NS > 4 && DIST == 1) {
+    const char* ds = getenv("DPZ_FOLD_DIST");
+    const bool d3 = !ds || atoi(ds) != 1;
+    if (d3 && (fa.np + FW_G - 1) / FW_G == FW_G) return launch_walk_t<VEC, EPL, NS, 3>(fa, st);
+  }
   static int per = 0, cus = 0;
   if (per == 0) {
     int dev = 0;
@@ -1427,7 +1475,7 @@ static int launch_walk_t(const FoldArgs& fa, hipStream_t st) {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
     const void* kf = NS <= 4 ? reinterpret_cast<const void*>(fold_walk_kernel<VEC, EPL, 4>)
-                             : reinterpret_cast<const void*>(fold_walk_groups_kernel<VEC, EPL, false>);
+                             : reinterpret_cast<const void*>(fold_walk_groups_kernel<VEC, EPL, false, DIST>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kf, 256, 0) !=
             hipSuccess || per < 1)
       per = 1;
@@ -1443,7 +1491,7 @@ static int launch_walk_t(const FoldArgs& fa, hipStream_t st) {
     DPZ_TIMED(DPZ_KT_FOLD, st, fold_walk_kernel<VEC, EPL, NS><<<(unsigned)blocks, 256, 0, st>>>(fa, tpw));
   } else {
     DPZ_TIMED(DPZ_KT_FOLD, st,
-              fold_walk_groups_kernel<VEC, EPL, false><<<(unsigned)blocks, 256, 0, st>>>(fa, tpw));
+              (fold_walk_groups_kernel<VEC, EPL, false, DIST><<<(unsigned)blocks, 256, 0, st>>>(fa, tpw)));
   }
   return DPZ_OK;
 }

@@ -305,14 +305,16 @@ def test_fold_paths_forced(dev, monkeypatch, group, n, alpha, npay):
                                                  (2_000_001, 0.25, 16, 0), (300_001, 0.3, 3, 1),
                                                  (300_001, 0.1, 3, 3), (100_003, 0.99, 2, 0),
                                                  (50_000, 0.05, 7, 4), (4097, 0.2, 5, 2),
-                                                 (300_001, 0.6, 4, 0), (1_000_003, 0.45, 16, 1)])
+                                                 (300_001, 0.6, 4, 0), (1_000_003, 0.45, 16, 1),
+                                                 (300_001, 0.1, 13, 0), (300_001, 0.4, 14, 0)])
 def test_fold_kinds_forced(dev, monkeypatch, kind, n, alpha, npay, ndense):
     """Every fold kernel forced in turn (DPZ_FOLD_KIND 1: classic hit-chain / phase, 2: 4-slot
     group, 4: the walk fold) on sparse groups and on groups with dense (full-share) payloads,
     bit-exact vs the oracle with and without the self term and with a zero base; a kind that
     cannot take a group (dense payloads on the 4-slot and walk paths) runs the classic kernel.
     alpha 0.45 / 0.6 overflow the walk fold's 64-entry windows (its synchronous dense-tile
-    path); 7 and 16 payloads walk in groups of four."""
+    path); 7 and 16 payloads walk in groups of four, 13..16 with every group's windows issued
+    three groups ahead (DPZ_FOLD_DIST=1 below: one group ahead)."""
     monkeypatch.setenv("DPZ_FOLD_KIND", kind)
     codec = _codec()
     rng = np.random.default_rng(int(n * alpha) + npay + 31 * ndense)
@@ -356,10 +358,13 @@ def test_fold_kinds_forced(dev, monkeypatch, kind, n, alpha, npay, ndense):
 
 
 @pytest.mark.parametrize("kind", ["4"])
+@pytest.mark.parametrize("dist", ["3", "1"])
 @pytest.mark.parametrize("alpha", [0.1, 0.3])
-def test_walk_fold_unaligned_views(dev, monkeypatch, kind, alpha):
-    """The walk fold's scalar-load build (local / out 4 bytes off a 16-byte boundary)."""
+def test_walk_fold_unaligned_views(dev, monkeypatch, kind, dist, alpha):
+    """The walk fold's scalar-load build (local / out 4 bytes off a 16-byte boundary), 16
+    payloads' windows issued three groups ahead (DPZ_FOLD_DIST 3, the default) and one."""
     monkeypatch.setenv("DPZ_FOLD_KIND", kind)
+    monkeypatch.setenv("DPZ_FOLD_DIST", dist)
     codec = _codec()
     n, npay = 300_001, 16
     rng = np.random.default_rng(int(alpha * 100) + 9)
