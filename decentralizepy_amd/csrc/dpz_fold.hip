@@ -1180,16 +1180,25 @@ constexpr int FW_G = 4;  // payloads per group: the windows of one group are in 
 // registers, so every window load is in flight while the group before it folds, with 16
 // registers of windows whatever the payload count.  Cursors live one per lane (lane p: payload
 // p) in one register.
-template <bool VEC, int EPL, bool ONE, int DIST>
+template <bool VEC, int EPL, bool ONE, int DIST, bool W2>
 __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64_t tpw) {
   constexpr int TE = 64 * EPL;
   __shared__ float s_val[FW_WAVES][TE];
-  __shared__ uint32_t s_tag[FW_WAVES][TE];
+  // tags (tile sequence << 4 | payload): 16-bit under DPZ_TAG16 (the sequence wraps every 4095
+  // tiles, the row is cleared then), so a lane's read-back of 4 tags is one 8-byte LDS read
+#ifdef DPZ_TAG16
+  using tag_t = uint16_t;
+  constexpr uint32_t SEQ_WRAP = 4095u;
+#else
+  using tag_t = uint32_t;
+  constexpr uint32_t SEQ_WRAP = 0x0FFFFFFFu;
+#endif
+  __shared__ tag_t s_tag[FW_WAVES][TE];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float* wv = s_val[wid];
-  uint32_t* wt = s_tag[wid];
+  tag_t* wt = s_tag[wid];
 #pragma unroll
-  for (int e = 0; e < EPL; ++e) wt[lane + 64 * e] = 0xFFFFFFFFu;
+  for (int e = 0; e < EPL; ++e) wt[lane + 64 * e] = (tag_t)~0u;
   const int64_t n = a.n;
   const int64_t ntl = (n + TE - 1) / TE;
   const int64_t gw = (int64_t)blockIdx.x * FW_WAVES + wid;
@@ -1267,7 +1276,14 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
   };
   // ---- the windows of one group: (idx, val) at cur + lane, branch-free loads of raw values
   // (lanes past k read entry 0 and are masked when the window is used) ----
-  auto load_group = [&](int g, int32_t (&ix)[FW_G], float (&vx)[FW_G]) {
+  // W2: 128-entry windows (entries cur + lane and cur + 64 + lane), so a tile of ~50 entries per
+  // payload on average rarely overflows into the synchronous path (whose loads, the youngest in
+  // flight, make the wave wait for every window load issued ahead: vmcnt(0))
+  constexpr int NSL = DIST == 3 ? FW_G : 2;
+  constexpr int NW2 = W2 ? NSL : 1;
+  int32_t WI[NSL][FW_G], WI2[NW2][FW_G];
+  float WV[NSL][FW_G], WV2[NW2][FW_G];
+  auto load_group = [&](int g, int sl) {
 #pragma unroll
     for (int q = 0; q < FW_G; ++q) {
       const int p = g * FW_G + q;
@@ -1279,24 +1295,28 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
       const int32_t jc = j < k ? j : 0;
       // an empty payload's arrays may be null: read a valid address instead (masked at use)
       const bool has = kp > 0;
-      ix[q] = as_global(has ? P_idx(pc) : reinterpret_cast<const int32_t*>(a.local))[jc];
-      vx[q] = as_global(has ? P_val(pc) : a.local)[jc];
+      const auto* ip = as_global(has ? P_idx(pc) : reinterpret_cast<const int32_t*>(a.local));
+      const auto* vp = as_global(has ? P_val(pc) : a.local);
+      WI[sl][q] = ip[jc];
+      WV[sl][q] = vp[jc];
+      if constexpr (W2) {
+        const int32_t jc2 = j + 64 < k ? j + 64 : 0;
+        WI2[sl][q] = ip[jc2];
+        WV2[sl][q] = vp[jc2];
+      }
     }
   };
   // DIST 1: the windows of the group being folded and of the next one (wi, wn);
   // DIST 3 (four groups, 13..16 payloads): all four groups' windows in registers, each group's
   // issued three groups ahead (into the slot the group before it just freed), so three groups'
   // loads are in flight while one folds
-  constexpr int NSL = DIST == 3 ? FW_G : 2;
-  int32_t WI[NSL][FW_G];
-  float WV[NSL][FW_G];
   FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n), Ln;
   if constexpr (DIST == 3) {
-    load_group(0, WI[0], WV[0]);
-    load_group(1, WI[1], WV[1]);
-    load_group(2, WI[2], WV[2]);
+    load_group(0, 0);
+    load_group(1, 1);
+    load_group(2, 2);
   } else {
-    load_group(0, WI[0], WV[0]);
+    load_group(0, 0);
   }
   uint32_t seq = 0;
   auto tile_body = [&](int64_t tile, auto guard) {
@@ -1314,7 +1334,9 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
     }
     // one group: its windows (wi, wvv) are in registers; `issue` starts a later group's loads
     // once this group's cursors have advanced
-    auto fold_group = [&](int g, int32_t (&wi)[FW_G], float (&wvv)[FW_G], auto issue) {
+    auto fold_group = [&](int g, int sl, auto issue) {
+      const int32_t (&wi)[FW_G] = WI[sl];
+      const float (&wvv)[FW_G] = WV[sl];
       // this group's window starts; the entries of the tile are the leading lanes below thi
       int32_t c0[FW_G], cnt[FW_G];
 #pragma unroll
@@ -1324,6 +1346,7 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
         c0[q] = live ? cur_of(p) : 0;
         const int32_t k = live ? P_k(p) : 0;
         cnt[q] = fw_lead(c0[q] + lane < k && wi[q] < thi32);
+        if (W2 && cnt[q] == 64) cnt[q] += fw_lead(c0[q] + 64 + lane < k && WI2[W2 ? sl : 0][q] < thi32);
         // the next tile's window start of this payload (a full window is finished in its phase)
         if (live) set_cur(p, c0[q] + cnt[q]);
       }
@@ -1338,29 +1361,37 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
           const uint32_t pos = (uint32_t)(wi[q] - tlo32);  // < TE: inside the tile
           if (lane < cnt[q] && pos < (uint32_t)TE) {
             wv[pos] = wvv[q];
-            wt[pos] = tag;
+            wt[pos] = (tag_t)tag;
+          }
+          if constexpr (W2) {
+            const uint32_t pos2 = (uint32_t)(WI2[sl][q] - tlo32);
+            if (lane + 64 < cnt[q] && pos2 < (uint32_t)TE) {
+              wv[pos2] = WV2[sl][q];
+              wt[pos2] = (tag_t)tag;
+            }
           }
         }
-        if (cnt[q] == 64) {  // a dense tile: this payload's further windows, synchronously
+        constexpr int WN = W2 ? 128 : 64;
+        if (cnt[q] == WN) {  // a dense tile: this payload's further windows, synchronously
           const int32_t k = P_k(p);
           const int32_t* pi = P_idx(p);
           const float* pv = P_val(p);
-          int32_t c = 64;
-          for (int32_t j0 = c0[q] + 64;; j0 += 64) {
+          int32_t c = WN;
+          for (int32_t j0 = c0[q] + WN;; j0 += 64) {
             const int32_t j = j0 + lane;
             const int32_t iv = j < k ? as_global(pi)[j] : INT32_MAX;
             const int cc = fw_lead(iv < thi32);
             const uint32_t pos = (uint32_t)(iv - tlo32);
             if (lane < cc && pos < (uint32_t)TE) {
               wv[pos] = as_global(pv)[j];
-              wt[pos] = tag;
+              wt[pos] = (tag_t)tag;
             }
             c += cc;
             if (cc < 64) break;
           }
           set_cur(p, c0[q] + c);
           // the next tile's window of this group moved (DIST 1, one group: already issued)
-          if (DIST == 1 && ng == 1) load_group(0, WI[1], WV[1]);
+          if (DIST == 1 && ng == 1) load_group(0, 1);
         }
         // the row is this wave's own and one wave's LDS instructions execute in order, so the
         // lanes' writes above are seen by the reads below with no wait; the scheduling barriers
@@ -1373,9 +1404,15 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
 #pragma unroll
           for (int c = 0; c < EPL / 4; ++c) {
             const int o = fw_elem<EPL>(lane, 4 * c);
-            const uint4 t4 = *reinterpret_cast<const uint4*>(&wt[o]);
+            if constexpr (sizeof(tag_t) == 2) {
+              const uint2 t2 = *reinterpret_cast<const uint2*>(&wt[o]);
+              tg[4 * c] = t2.x & 0xFFFFu; tg[4 * c + 1] = t2.x >> 16;
+              tg[4 * c + 2] = t2.y & 0xFFFFu; tg[4 * c + 3] = t2.y >> 16;
+            } else {
+              const uint4 t4 = *reinterpret_cast<const uint4*>(&wt[o]);
+              tg[4 * c] = t4.x; tg[4 * c + 1] = t4.y; tg[4 * c + 2] = t4.z; tg[4 * c + 3] = t4.w;
+            }
             const float4 h4 = *reinterpret_cast<const float4*>(&wv[o]);
-            tg[4 * c] = t4.x; tg[4 * c + 1] = t4.y; tg[4 * c + 2] = t4.z; tg[4 * c + 3] = t4.w;
             hv[4 * c] = h4.x; hv[4 * c + 1] = h4.y; hv[4 * c + 2] = h4.z; hv[4 * c + 3] = h4.w;
           }
         } else {
@@ -1399,20 +1436,24 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
       // of the next tile, into the slot group g - 1 freed
 #pragma unroll
       for (int g = 0; g < FW_G; ++g) {
-        fold_group(g, WI[g], WV[g], [&] {
+        fold_group(g, g, [&] {
           const int s3 = (g + 3) & (FW_G - 1);
-          load_group(s3, WI[s3], WV[s3]);
+          load_group(s3, s3);
         });
       }
     } else {
       for (int gg = 0; gg < ng; ++gg) {
         const int g = ONE ? 0 : gg;
         // the next group's windows (this tile's next group, or group 0 of the next tile)
-        fold_group(g, WI[0], WV[0], [&] { load_group(g + 1 < ng ? g + 1 : 0, WI[1], WV[1]); });
+        fold_group(g, 0, [&] { load_group(g + 1 < ng ? g + 1 : 0, 1); });
 #pragma unroll
         for (int q = 0; q < FW_G; ++q) {
           WI[0][q] = WI[1][q];
           WV[0][q] = WV[1][q];
+          if constexpr (W2) {
+            WI2[0][q] = WI2[W2 ? 1 : 0][q];
+            WV2[0][q] = WV2[W2 ? 1 : 0][q];
+          }
         }
       }
     }
@@ -1423,7 +1464,11 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
     fw_store<VEC, EPL, GUARD>(a.out, tlo, lane, n, acc);
     if (a.out2) fw_store<VEC, EPL, GUARD>(a.out2, tlo, lane, n, acc);
     L = Ln;
-    ++seq;
+    if (++seq == SEQ_WRAP) {  // tags restart: no stale tag of this row may match a new one
+      seq = 0;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) wt[lane + 64 * e] = (tag_t)~0u;
+    }
   };
   const int64_t tfull = n / TE;  // tiles wholly inside [0, n)
   const int64_t tf = t1 < tfull ? t1 : (tfull > t0 ? tfull : t0);
@@ -1459,14 +1504,17 @@ static inline int64_t fold_ntiles(int64_t n) { return (n + FOLD_TILE - 1) / FOLD
 // The walk fold's launch: EPL from the densest payload (~32 entries per payload per tile on
 // average at dens <= 0.125: 256-element tiles; denser payloads 128-element tiles); a
 // persistent grid of what the CUs hold, each wave a contiguous run of tiles.
-template <bool VEC, int EPL, int NS, int DIST = 1>
-static int launch_walk_t(const FoldArgs& fa, hipStream_t st) {
+template <bool VEC, int EPL, int NS, int DIST = 1, bool W2 = false>
+static int launch_walk_t(const FoldArgs& fa, bool w2, hipStream_t st) {
   // 13..16 payloads (four groups): the groups kernel with windows issued three groups ahead
-  // (DPZ_FOLD_DIST=1: one group ahead, A/B)
-  if constexpr (NS > 4 && DIST == 1) {
+  // (DPZ_FOLD_DIST=1: one group ahead, A/B); w2: 128-entry windows
+  if constexpr (NS > 4 && DIST == 1 && !W2) {
     const char* ds = getenv("DPZ_FOLD_DIST");
     const bool d3 = !ds || atoi(ds) != 1;
-    if (d3 && (fa.np + FW_G - 1) / FW_G == FW_G) return launch_walk_t<VEC, EPL, NS, 3>(fa, st);
+    if (d3 && (fa.np + FW_G - 1) / FW_G == FW_G)
+      return w2 ? launch_walk_t<VEC, EPL, NS, 3, true>(fa, w2, st)
+                : launch_walk_t<VEC, EPL, NS, 3, false>(fa, w2, st);
+    if (w2) return launch_walk_t<VEC, EPL, NS, 1, true>(fa, w2, st);
   }
   static int per = 0, cus = 0;
   if (per == 0) {
@@ -1475,7 +1523,7 @@ static int launch_walk_t(const FoldArgs& fa, hipStream_t st) {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
     const void* kf = NS <= 4 ? reinterpret_cast<const void*>(fold_walk_kernel<VEC, EPL, 4>)
-                             : reinterpret_cast<const void*>(fold_walk_groups_kernel<VEC, EPL, false, DIST>);
+                             : reinterpret_cast<const void*>(fold_walk_groups_kernel<VEC, EPL, false, DIST, W2>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kf, 256, 0) !=
             hipSuccess || per < 1)
       per = 1;
@@ -1491,7 +1539,7 @@ static int launch_walk_t(const FoldArgs& fa, hipStream_t st) {
     DPZ_TIMED(DPZ_KT_FOLD, st, fold_walk_kernel<VEC, EPL, NS><<<(unsigned)blocks, 256, 0, st>>>(fa, tpw));
   } else {
     DPZ_TIMED(DPZ_KT_FOLD, st,
-              (fold_walk_groups_kernel<VEC, EPL, false, DIST><<<(unsigned)blocks, 256, 0, st>>>(fa, tpw)));
+              (fold_walk_groups_kernel<VEC, EPL, false, DIST, W2><<<(unsigned)blocks, 256, 0, st>>>(fa, tpw)));
   }
   return DPZ_OK;
 }
@@ -1502,36 +1550,45 @@ static bool walk_ok(const FoldArgs& fa) {
 }
 
 template <int NS>
-static int launch_walk_o(const FoldArgs& fa, bool vec, int epl, hipStream_t st) {
+static int launch_walk_o(const FoldArgs& fa, bool vec, int epl, bool w2, hipStream_t st) {
   if (vec) {
     switch (epl) {
-      case 16: return launch_walk_t<true, 16, NS>(fa, st);
-      case 8: return launch_walk_t<true, 8, NS>(fa, st);
-      case 4: return launch_walk_t<true, 4, NS>(fa, st);
-      default: return launch_walk_t<true, 2, NS>(fa, st);
+      case 16: return launch_walk_t<true, 16, NS>(fa, w2, st);
+      case 8: return launch_walk_t<true, 8, NS>(fa, w2, st);
+      case 4: return launch_walk_t<true, 4, NS>(fa, w2, st);
+      default: return launch_walk_t<true, 2, NS>(fa, w2, st);
     }
   }
   switch (epl) {
-    case 16: return launch_walk_t<false, 16, NS>(fa, st);
-    case 8: return launch_walk_t<false, 8, NS>(fa, st);
-    case 4: return launch_walk_t<false, 4, NS>(fa, st);
-    default: return launch_walk_t<false, 2, NS>(fa, st);
+    case 16: return launch_walk_t<false, 16, NS>(fa, w2, st);
+    case 8: return launch_walk_t<false, 8, NS>(fa, w2, st);
+    case 4: return launch_walk_t<false, 4, NS>(fa, w2, st);
+    default: return launch_walk_t<false, 2, NS>(fa, w2, st);
   }
 }
 
-// The largest tile that holds about one 64-entry window per payload on average (the densest
-// payload, `dens`): fewer tiles mean fewer window loads and LDS passes per element, and an
-// overflowing window is re-read synchronously (measured on MI355X, tools/diag/walk_epl.sh).
+// The largest tile that holds about one window per payload on average (the densest payload,
+// `dens`): fewer tiles mean fewer window loads and LDS passes per element, and an overflowing
+// window is re-read synchronously.  Measured on MI355X (M = 25 M, profiles/r03_s3_walk_win_sweep.txt):
+//   <= 4 payloads / 5..12: 64-entry windows, ~52 entries per tile or fewer (16 x 0.1 at
+//     512-element tiles 215 us, 1024: 283, 256: 287; 3 x 0.1: 64 / 72 / 77 us);
+//   13..16 payloads: 64-entry windows up to dens 0.055 (1024-element tiles), then 128-entry
+//     windows: 1024-element tiles to 0.105, 512 to 0.21 (16 x 0.15: 297 -> 247 us, 16 x 0.2:
+//     309 -> 266 us against 64-entry windows at 256-element tiles).
 static int launch_walk(const FoldArgs& fa, bool vec, double dens, hipStream_t st) {
-  // about 52 entries or fewer per payload and tile (M = 25 M: 16 x alpha 0.1 at 512-element tiles
-  // 215 us, 1024: 283, 256: 287; 3 x 0.1: 64 / 72 / 77 us)
-  const int epl = dens <= 0.055 ? 16 : (dens <= 0.105 ? 8 : (dens <= 0.21 ? 4 : 2));
-  int e = epl;
+  const bool four = (fa.np + FW_G - 1) / FW_G == FW_G;
+  int e = dens <= 0.055 ? 16 : (dens <= 0.105 ? 8 : (dens <= 0.21 ? 4 : 2));
+  bool w2 = false;
+  if (four && dens > 0.055 && dens <= 0.21) {
+    w2 = true;
+    e = dens <= 0.105 ? 16 : 8;
+  }
   if (const char* s = getenv("DPZ_FOLD_WALK_EPL")) {
     const int v = atoi(s);
     if (v == 16 || v == 8 || v == 4 || v == 2) e = v;
   }
-  return fa.np <= 4 ? launch_walk_o<4>(fa, vec, e, st) : launch_walk_o<16>(fa, vec, e, st);
+  if (const char* s = getenv("DPZ_FOLD_WIN")) w2 = atoi(s) == 128;
+  return fa.np <= 4 ? launch_walk_o<4>(fa, vec, e, false, st) : launch_walk_o<16>(fa, vec, e, w2, st);
 }
 
 // Replace-only decode of ONE sparse payload (reference PartialModel.py:257-303, T[idx] = params):

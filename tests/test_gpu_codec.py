@@ -306,7 +306,8 @@ def test_fold_paths_forced(dev, monkeypatch, group, n, alpha, npay):
                                                  (300_001, 0.1, 3, 3), (100_003, 0.99, 2, 0),
                                                  (50_000, 0.05, 7, 4), (4097, 0.2, 5, 2),
                                                  (300_001, 0.6, 4, 0), (1_000_003, 0.45, 16, 1),
-                                                 (300_001, 0.1, 13, 0), (300_001, 0.4, 14, 0)])
+                                                 (300_001, 0.1, 13, 0), (300_001, 0.4, 14, 0),
+                                                 (1_000_003, 0.15, 16, 0), (300_001, 0.07, 15, 0)])
 def test_fold_kinds_forced(dev, monkeypatch, kind, n, alpha, npay, ndense):
     """Every fold kernel forced in turn (DPZ_FOLD_KIND 1: classic hit-chain / phase, 2: 4-slot
     group, 4: the walk fold) on sparse groups and on groups with dense (full-share) payloads,
@@ -382,6 +383,35 @@ def test_walk_fold_unaligned_views(dev, monkeypatch, kind, dist, alpha):
     codec.decode_average(tl, tpays, w, 1 - sum(w), out=out)
     ref = ofold.fold(local[1:], pays, w, 1 - sum(w))
     np.testing.assert_array_equal(_bits(out.cpu().numpy()), _bits(ref))
+
+
+@pytest.mark.parametrize("win,epl,alpha", [("128", "16", 0.2), ("128", "8", 0.3), ("128", "16", 0.12),
+                                           ("64", "16", 0.1), ("128", "2", 0.05)])
+def test_walk_fold_windows_overflow(dev, monkeypatch, win, epl, alpha):
+    """The walk fold of 16 payloads with 64- / 128-entry windows forced onto tiles whose entries
+    overflow them (the synchronous extra windows after a full 128-entry window) and onto sparse
+    tiles, bit-exact vs the oracle."""
+    monkeypatch.setenv("DPZ_FOLD_KIND", "4")
+    monkeypatch.setenv("DPZ_FOLD_WIN", win)
+    monkeypatch.setenv("DPZ_FOLD_WALK_EPL", epl)
+    codec = _codec()
+    n, npay = 300_001, 16
+    rng = np.random.default_rng(int(alpha * 1000) + int(epl))
+    local = rng.standard_normal(n).astype(np.float32)
+    k = round(alpha * n)
+    pays, tpays = [], []
+    for i in range(npay):
+        # half the payloads clustered in the first third (denser tiles), half uniform
+        hi = n // 3 if i % 2 else n
+        idx = np.sort(rng.choice(hi, size=min(k, hi), replace=False)).astype(np.int32)
+        vals = rng.standard_normal(len(idx)).astype(np.float32)
+        pays.append((idx, vals))
+        tpays.append((torch.from_numpy(idx).to(dev), torch.from_numpy(vals).to(dev)))
+    w = [1 / (npay + 1)] * npay
+    tl = torch.from_numpy(local).to(dev)
+    out = codec.decode_average(tl, tpays, w, 1 - sum(w)).cpu().numpy()
+    ref = ofold.fold(local, pays, w, 1 - sum(w))
+    np.testing.assert_array_equal(_bits(out), _bits(ref))
 
 
 @pytest.mark.parametrize("group", ["0", "1"])
