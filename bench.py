@@ -31,7 +31,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (GB/s), /opt/skills/guides/MI355
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU); default: WORLD_SIZE under a launcher, else 1")
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--n", type=int, default=11_000_000)
@@ -231,12 +232,90 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     b_enc = 8 * n + 8 * k + 8 * k      # read x, x0; write idx, val; counter[idx] += 1 (r+w)
     b_dec = 8 * n + 8 * k              # read local, payload; write out
     fell_back |= multi.sticky_status(clear=True) != 0
+    product = product_one_node(sets, n, k, stream, ws_list[0], max(2 * R, min(steps, 200)))
+    fell_back |= product["fell_back"]
     return dict(n=n, k=k, s_step=s_step, s_multi=s_multi, s_serial=s_serial, s_host=s_host,
                 mode=mode, streams=S, fell_back=fell_back, t_enc=t_enc, t_dec=t_dec,
                 b_enc=b_enc, b_dec=b_dec, kernels=kernels, rotate=R, repeats=repeats,
+                product=product,
                 spread_ms={"multi": [round(v * 1e3, 5) for v in spread[0]],
                            "serial": [round(v * 1e3, 5) for v in spread[1]]},
                 value=world * 4 * n / s_step / 2 ** 30)
+
+
+def product_one_node(sets, n, k, stream, ws, reps):
+    """``stages.product_one_node``: exactly what the drop-in plugins enqueue for one node's round,
+    on one stream — PartialModel.serialized_model's ``codec.topk_encode`` (|x - x0| top-k with
+    the counter update; sampled path, statuses checked after the loop) then Sharing._averaging's
+    ``codec.decode_average`` (the Metro-Hastings fold of ``npay`` neighbour payloads over the
+    node's pre-share model x into a new buffer, weights 1/(deg+1) of a degree-npay regular graph,
+    w_self = 1 - their Python sum), for npay = 1 and 3.  Step j rotates over the HBM-rotated node
+    states; its neighbours' payloads are those of states j-1 .. j-npay.  Device time: HIP events
+    around the whole loop on the launch stream after a GPU-side spin that lets the host queue it.
+    Algorithmic bytes: encode 8N + 16k, fold 8N + 8·npay·k (reference Sharing.py:156-190,
+    PartialModel.py:188-255)."""
+    from decentralizepy_amd import codec
+    R = len(sets)
+    out = {}
+    fell = False
+
+    for npay, fused in ((1, False), (3, False), (1, True), (3, True)):
+        w = [1.0 / (npay + 1)] * npay
+        w_total = 0
+        for v in w:
+            w_total += v
+        pays = [[(sets[(j - q) % R]["idx"], sets[(j - q) % R]["val"]) for q in range(1, npay + 1)]
+                for j in range(R)]
+
+        def enc(j):
+            d = sets[j % R]
+            codec.topk_encode(d["x"], k, x0=d["x0"], counter=d["counter"], idx_out=d["idx"],
+                              val_out=d["val"], workspace=ws, asynchronous=True,
+                              fold_base=(d["out"], w, 1 - w_total) if fused else None)
+
+        def dec(j):
+            d = sets[j % R]
+            codec.decode_average(d["x"], pays[j % R], w, 1 - w_total, out=d["out"], workspace=ws,
+                                 base_ready=fused)
+
+        def loop(fns):
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            with torch.cuda.stream(stream):
+                torch.cuda._sleep(int(400e6))  # the host queues the loop while the GPU spins
+                ev0.record(stream)
+                t0 = time.perf_counter()
+                for j in range(reps):
+                    for f in fns:
+                        f(j)
+                t_host = time.perf_counter() - t0
+                ev1.record(stream)
+            ev1.synchronize()
+            return ev0.elapsed_time(ev1) / reps * 1e-3, t_host / reps
+
+        with torch.cuda.stream(stream):
+            for j in range(R):  # warm-up: every state encoded once (the payloads exist)
+                enc(j)
+                dec(j)
+        t_step, h_step = loop([enc, dec])
+        t_enc, _ = loop([enc])
+        t_dec, _ = loop([dec])
+        fell |= codec.topk_sticky_status(ws, clear=True) != 0
+        b_enc, b_dec = 8 * n + 16 * k, 8 * n + 8 * npay * k
+        out[f"{npay}_payload" + ("_foldbase" if fused else "")] = {
+            "step_us": round(t_step * 1e6, 3), "encode_us": round(t_enc * 1e6, 3),
+            "fold_us": round(t_dec * 1e6, 3), "host_enqueue_us": round(h_step * 1e6, 3),
+            "alg_bytes": b_enc + b_dec,
+            "GiBps": round(4 * n / t_step / 2 ** 30, 2),
+            "frac_of_hbm_peak": round((b_enc + b_dec) / t_step / 1e9 / HBM_PEAK_GBS, 4)}
+    out["note"] = ("the plugin path: codec.topk_encode then codec.decode_average (MH fold over x "
+                   "into a new buffer), one stream; *_foldbase: the encode's filter also writes "
+                   "the fold's no-hit base (topk_encode fold_base=, dpz_topk_encode_foldbase) and "
+                   "the decode rewrites only the hit elements (base_ready=, DPZ_FOLD_BASE_READY), "
+                   "what PartialModel runs when its predicted MH weights hold")
+    out["fell_back"] = fell
+    return out
 
 
 def _stage_time(batch, what, reps, run_steps, stream):
@@ -304,7 +383,10 @@ def gossip_case(n, alpha, dev, rank, world, dist, rounds, warmup, exchange="allg
 
 def fused_copy():
     """The one-node step's decode copy is written by the encoder's filter (dpz_topk.hip
-    dpz_topk_encode_replace) unless disabled by the A/B switches."""
+    dpz_topk_encode_replace) unless a diagnostic build (DPZ_CODEC_LIB) disables it with its A/B
+    switches; the product library reads no environment."""
+    if not os.environ.get("DPZ_CODEC_LIB"):
+        return True
     return os.environ.get("DPZ_FUSED_COPY", "1") != "0" and \
         os.environ.get("DPZ_BATCH_COSCHED", "1") != "0"
 
@@ -395,7 +477,10 @@ def _finish(dist):
 
 def main():
     args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    launched = "WORLD_SIZE" in os.environ
+    if args.gpus is None:  # under torchrun without --gpus: the launcher's rank count
+        args.gpus = int(os.environ["WORLD_SIZE"]) if launched else 1
+    if args.gpus > 1 and not launched:
         sys.exit(spawn_ranks(args))  # the parent never touches the GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -494,6 +579,7 @@ def main():
                  "one_node_frac_of_hbm_peak": round(b / e["s_serial"] / 1e9 / HBM_PEAK_GBS / world, 4),
                  f"{e['streams']}_node_ms_per_step": round(e["s_multi"] * 1e3, 4),
                  "host_enqueue_ms_per_step": round(e["s_host"] * 1e3, 4),
+                 "product_one_node": {k_: v for k_, v in e["product"].items() if k_ != "fell_back"},
                  "spread_ms": e["spread_ms"],
                  "fell_back": e["fell_back"]}
 
@@ -632,6 +718,7 @@ def main():
                 "one_node_serial_ms_per_step": round(r["s_serial"] * 1e3, 5),
                 f"{r['streams']}_node_ms_per_step": round(r["s_multi"] * 1e3, 5),
                 "host_enqueue_ms_per_step": round(r["s_host"] * 1e3, 5),
+                "product_one_node": {k_: v for k_, v in r["product"].items() if k_ != "fell_back"},
                 "kernels": kern,
                 "torch_copy_GBps_256MiB": copy_gbs,
             },

@@ -12,6 +12,9 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # DPZ_CODEC_LIB selects an alternative build (e.g. the stamped diagnostic build of tools/stamps.py)
 LIB_PATH = os.environ.get("DPZ_CODEC_LIB") or os.path.join(_HERE, "libdpzcodec.so")
+# The diagnostic build (csrc/dpz_knobs.h): the same sources with the tuning / forced-path
+# switches read from DPZ_* environment variables.  The product library reads none.
+DIAG_PATH = os.path.join(_HERE, "libdpzcodec_diag.so")
 
 DPZ_ACC_NONE = 0
 DPZ_ACC_ACCUMULATE = 1
@@ -27,6 +30,7 @@ DPZ_FOLD_ZERO_BASE = 0x4
 DPZ_FOLD_ADD_ONLY = 0x8
 DPZ_FOLD_ACCUMULATE = 0x10
 DPZ_FOLD_ALSO_LOCAL = 0x20
+DPZ_FOLD_BASE_READY = 0x40
 DPZ_BATCH_ENCODE = 0x1
 DPZ_BATCH_DECODE = 0x2
 DPZ_EW_SUB = 1
@@ -54,11 +58,15 @@ SIGNATURES = {
                                _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size, _int, _c_void_p]),
     "dpz_topk_encode_status": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64,
                                       _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
-                                      _c_void_p, _c_void_p]),
+                                      _c_void_p, _int, _c_void_p]),
     "dpz_topk_encode_replace": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64,
                                        _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
                                        _int, _c_void_p, _c_void_p, _c_void_p, _i64, _i64,
                                        _c_void_p, _c_void_p, _size, _c_void_p]),
+    "dpz_topk_encode_foldbase": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64,
+                                        _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
+                                        _int, _int, ctypes.POINTER(ctypes.c_float),
+                                        ctypes.c_float, _c_void_p, _c_void_p]),
     "dpz_topk_threshold": (_int, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _i64, _c_void_p,
                                   _size, ctypes.POINTER(_i64), _c_void_p]),
     "dpz_mask_below_threshold": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p]),
@@ -161,32 +169,42 @@ def source_build_id():
     return h.hexdigest()[:16]
 
 
+def load(path, check_build=True):
+    """Load the codec library at ``path`` with every SIGNATURES binding; raises if it is missing
+    or (check_build) was built from other sources than the checked-out ones."""
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"decentralizepy_amd: HIP codec library not found at {path}; "
+            "build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(or `make -C decentralizepy_amd/csrc`). There is no CPU fallback.")
+    handle = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(handle, name)
+        fn.restype = res
+        fn.argtypes = args
+    if check_build:
+        built = handle.dpz_build_id().decode()
+        want = source_build_id()
+        if built != want:
+            raise RuntimeError(
+                f"decentralizepy_amd: {path} was built from other sources (build id "
+                f"{built}, checked-out sources {want}); rebuild it with "
+                "`make -C decentralizepy_amd/csrc`")
+    return handle
+
+
 def lib():
     """Load (once) and return the codec library; raises if it is missing."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(
-                f"decentralizepy_amd: HIP codec library not found at {LIB_PATH}; "
-                "build it with `python -c 'import __graft_entry__ as g; g.build()'` "
-                "(or `make -C decentralizepy_amd/csrc`). There is no CPU fallback.")
-        handle = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in SIGNATURES.items():
-            fn = getattr(handle, name)
-            fn.restype = res
-            fn.argtypes = args
-        # a library built from other sources than the checked-out ones is refused (diagnostic
-        # builds selected with DPZ_CODEC_LIB are exempt)
-        if not os.environ.get("DPZ_CODEC_LIB"):
-            built = handle.dpz_build_id().decode()
-            want = source_build_id()
-            if built != want:
-                raise RuntimeError(
-                    f"decentralizepy_amd: {LIB_PATH} was built from other sources (build id "
-                    f"{built}, checked-out sources {want}); rebuild it with "
-                    "`make -C decentralizepy_amd/csrc`")
-        _lib = handle
+        # builds selected with DPZ_CODEC_LIB (diagnostic) are exempt from the build-id check
+        _lib = load(LIB_PATH, check_build=not os.environ.get("DPZ_CODEC_LIB"))
     return _lib
+
+
+def diag_lib():
+    """The diagnostic build (DIAG_PATH), for forced-path tests: never the product path."""
+    return load(DIAG_PATH)
 
 
 class CodecError(RuntimeError):

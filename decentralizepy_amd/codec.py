@@ -82,7 +82,7 @@ class Workspace:
 
 def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, counter=None,
                 idx_out=None, val_out=None, workspace=None, exact=False, asynchronous=False,
-                phase=None, co_replace=None, status_out=None, shared=False):
+                phase=None, co_replace=None, status_out=None, shared=False, fold_base=None):
     """Top-k magnitude encode (reference PartialModel.py:164-255 / Wavelet.py:142-197).
 
     Returns ``(idx int32[k], val fp32[k])`` in ascending index order.  Mutates ``acc`` and
@@ -98,6 +98,10 @@ def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, c
     encode whose final status word (0 = final, else re-run with ``exact=True``) is written there
     on the device (dpz_topk_encode_status).  ``shared``: several codecs run concurrently on the
     GPU (DPZ_TOPK_SHARED: the smaller filter grid); identical results.
+    ``fold_base=(base_out, weights, w_self)``: also write the no-hit base of the coming
+    Metro-Hastings fold over x with those weights into ``base_out`` (dpz_topk_encode_foldbase;
+    the filter writes it as it streams x), for a later ``decode_average(x, payloads, weights,
+    w_self, out=base_out, base_ready=True)``.
     """
     _require(x, torch.float32, "x")
     _require(x0, torch.float32, "x0")
@@ -117,6 +121,21 @@ def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, c
              | (_lib.DPZ_TOPK_SHARED if shared else 0))
     if phase is not None:
         flags |= {"stream": DPZ_TOPK_STREAM, "tail": DPZ_TOPK_TAIL}[phase]
+    if fold_base is not None:
+        base_out, fw, fws = fold_base
+        _require(base_out, torch.float32, "base_out")
+        if base_out.numel() != n:
+            raise ValueError("fold base: base_out must hold n values")
+        if co_replace is not None or phase is not None or status_out is not None:
+            raise ValueError("fold_base: a whole encode without co_replace / phase / status_out")
+        nw = len(fw)
+        w_arr = (ctypes.c_float * max(nw, 1))(*[float(v) for v in fw])
+        rc = _lib.lib().dpz_topk_encode_foldbase(
+            _ptr(x), _ptr(x0), _ptr(acc), int(acc_mode), _ptr(vals_src), n, k, _ptr(idx_out),
+            _ptr(val_out), _ptr(counter), _ptr(ws), ws.numel(), flags, nw, w_arr, float(fws),
+            _ptr(base_out), _stream(x.device))
+        check(rc, "dpz_topk_encode_foldbase")
+        return idx_out, val_out
     if status_out is not None:
         _require(status_out, torch.int32, "status_out")
         if co_replace is not None or phase is not None or exact:
@@ -124,7 +143,9 @@ def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, c
         rc = _lib.lib().dpz_topk_encode_status(_ptr(x), _ptr(x0), _ptr(acc), int(acc_mode),
                                                _ptr(vals_src), n, k, _ptr(idx_out), _ptr(val_out),
                                                _ptr(counter), _ptr(ws), ws.numel(),
-                                               _ptr(status_out), _stream(x.device))
+                                               _ptr(status_out),
+                                               _lib.DPZ_TOPK_SHARED if shared else 0,
+                                               _stream(x.device))
         check(rc, "dpz_topk_encode_status")
         return idx_out, val_out
     if co_replace is None:
@@ -257,7 +278,7 @@ class NodeStepBatch:
 
 def decode_average(local, payloads, weights=None, w_self=None, out=None, replace_only=False,
                    workspace=None, zero_base=False, add_only=False, accumulate=False,
-                   also_local=False):
+                   also_local=False, base_ready=False):
     """Batched replace + Metro-Hastings fold (reference Sharing.py:156-229, PartialModel.py:257-303).
 
     payloads : list of ``(idx int32 device tensor or None, vals fp32 device tensor)``
@@ -268,6 +289,9 @@ def decode_average(local, payloads, weights=None, w_self=None, out=None, replace
     add_only : one payload, ``out = local + T`` with T zero-based (DPZ_FOLD_ADD_ONLY)
     accumulate: ``out`` holds a running total the fold continues (DPZ_FOLD_ACCUMULATE)
     also_local: the result is also written over ``local`` in place (DPZ_FOLD_ALSO_LOCAL)
+    base_ready: ``out`` already holds this fold's no-hit base over ``local`` (written by
+               ``topk_encode(..., fold_base=(out, weights, w_self))``): only the elements the
+               payloads hit are rewritten (DPZ_FOLD_BASE_READY)
     """
     _require(local, torch.float32, "local")
     n = local.numel()
@@ -295,7 +319,8 @@ def decode_average(local, payloads, weights=None, w_self=None, out=None, replace
              | (_lib.DPZ_FOLD_ZERO_BASE if zero_base else 0)
              | (_lib.DPZ_FOLD_ADD_ONLY if add_only else 0)
              | (_lib.DPZ_FOLD_ACCUMULATE if accumulate else 0)
-             | (_lib.DPZ_FOLD_ALSO_LOCAL if also_local else 0))
+             | (_lib.DPZ_FOLD_ALSO_LOCAL if also_local else 0)
+             | (_lib.DPZ_FOLD_BASE_READY if base_ready else 0))
     ws = (workspace or Workspace(local.device)).get_decode(n, npay)
     rc = _lib.lib().dpz_decode_average(_ptr(local), n, npay, idx_arr, val_arr, k_arr, w_arr,
                                        float(w_self) if w_self is not None else 0.0, flags,

@@ -79,7 +79,8 @@ extern "C" int dpz_encode_replace_batch(int m, int what, const float* const* x,
   // A node decoding over the model it encodes (r_local[j] == x[j], the reference's
   // deserialized_model base) takes the fused call on any stream count: the encoder's filter
   // writes the decode's copy of x as it streams x (dpz_topk_encode_replace).
-  static const int cs_env = getenv("DPZ_BATCH_COSCHED") ? atoi(getenv("DPZ_BATCH_COSCHED")) : -1;
+  // DPZ_BATCH_COSCHED=0 / 1 forces the plain / co-scheduled enqueue (diagnostic build, A/B)
+  const int cs_env = (int)DPZ_KNOB_INT(BATCH_COSCHED, -1);
   const bool cosched = cs_env >= 0 ? cs_env != 0 : n_streams == 1;
   for (int j = 0; j < m; ++j) {
     const int q = j % n_streams;

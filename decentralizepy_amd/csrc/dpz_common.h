@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/dpz_codec.h"
+#include "dpz_knobs.h"
 
 #define DPZ_WAVE 64
 
@@ -98,5 +99,22 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t* wsum
 __host__ __device__ __forceinline__ bool aligned16(const void* p) {
   return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
 }
+
+// The Metro-Hastings fold's value at an element no payload hits (every term is the local value
+// x): fl(...fl(fl(x*w[0]) + fl(x*w[1])) ... + fl(x*ws)), the reference's fp32 order
+// (sharing/Sharing.py:156-190; the library is compiled with -ffp-contract=off).  Written by the
+// encoder's filter while it streams x (dpz_topk_encode_foldbase) so that the decode only
+// rewrites the elements its payloads hit (DPZ_FOLD_BASE_READY).
+constexpr int FOLDBASE_MAXW = 16;
+struct FoldBase {
+  int nw;                  // payload weights, 1 .. FOLDBASE_MAXW
+  float w[FOLDBASE_MAXW];
+  float ws;                // the self weight
+  __device__ __forceinline__ float of(float x) const {
+    float t = x * w[0];
+    for (int p = 1; p < nw; ++p) t = t + x * w[p];
+    return t + x * ws;
+  }
+};
 
 }  // namespace dpz

@@ -960,6 +960,65 @@ __device__ __forceinline__ int fw_lead(bool in) {
 
 __device__ __forceinline__ int32_t fw_uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// lower_bound(idx_p, e0) of every payload p < np (np <= NSX) as lane p's value: 64-ary searches
+// (one wave-wide probe load per step) run in LOCK STEP over the payloads, so each round's np probe
+// loads are in flight together and a wave's start costs ~log64(k) dependent round trips, not np
+// times that (16 payloads at k = 2.5 M: 4 rounds instead of 64 dependent loads).  Probe loads are
+// branch-free (an idle payload re-reads a valid word: entry 0 of `dflt`) so the compiler waits once
+// per round.  idx_of(p) / k_of(p) take compile-time p.
+template <int NSX, class IdxOf, class KOf, class E0Of>
+__device__ __forceinline__ int32_t fw_lower_bounds_t(int np, E0Of e0_of, int lane, IdxOf idx_of,
+                                                     KOf k_of, const int32_t* dflt) {
+  int32_t slo[NSX], shi[NSX];
+#pragma unroll
+  for (int p = 0; p < NSX; ++p) {
+    slo[p] = 0;
+    shi[p] = p < np ? k_of(p) : 0;
+  }
+  for (;;) {
+    int32_t xv[NSX], st[NSX];
+    bool act = false;
+#pragma unroll
+    for (int p = 0; p < NSX; ++p) {
+      const bool on = shi[p] > slo[p];
+      act |= on;
+      const int32_t len = shi[p] - slo[p];
+      st[p] = on ? (len <= 64 ? 1 : (len + 63) / 64) : 0;
+      const int64_t q = (int64_t)slo[p] + (int64_t)lane * st[p];
+      const bool ok = on && q < shi[p];
+      const auto* ip = as_global(on ? idx_of(p) : dflt);
+      xv[p] = ip[ok ? q : (on ? (int64_t)slo[p] : 0)];
+    }
+    if (!act) break;
+#pragma unroll
+    for (int p = 0; p < NSX; ++p) {
+      if (st[p] == 0) continue;  // uniform
+      const int64_t q = (int64_t)slo[p] + (int64_t)lane * st[p];
+      const int32_t c = (int32_t)__popcll(__ballot(q < shi[p] && xv[p] < e0_of(p)));  // a prefix
+      if (st[p] == 1) {
+        slo[p] += c;
+        shi[p] = slo[p];
+      } else {
+        const int32_t nlo = c > 0 ? slo[p] + (c - 1) * st[p] + 1 : slo[p];
+        const int64_t nhi = (int64_t)slo[p] + (int64_t)c * st[p];
+        shi[p] = nhi < shi[p] ? (int32_t)nhi : shi[p];
+        slo[p] = nlo;
+      }
+    }
+  }
+  int32_t cur = 0;
+#pragma unroll
+  for (int p = 0; p < NSX; ++p) cur = lane == p ? slo[p] : cur;
+  return cur;
+}
+
+// every search of the same target e0
+template <int NSX, class IdxOf, class KOf>
+__device__ __forceinline__ int32_t fw_lower_bounds(int np, int32_t e0, int lane, IdxOf idx_of,
+                                                   KOf k_of, const int32_t* dflt) {
+  return fw_lower_bounds_t<NSX>(np, [e0](int) { return e0; }, lane, idx_of, k_of, dflt);
+}
+
 // Sparse payloads only (dense ones take the classic kernels), a fresh total (a.first),
 // n < 2^31 - 1024 (walk_ok), np <= NS.  NS payload slots, all compile-time: every slot's window
 // of the NEXT tile is issued at the start of this tile (branch-free loads), so the loads are in
@@ -1004,32 +1063,13 @@ __global__ void __launch_bounds__(256, FW_MINB_1(EPL)) fold_walk_kernel(FoldArgs
   auto P_w = [&](int p) {
     return ONE ? a.p[p].w : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl), p));
   };
-  // ---- start cursors: 64-ary lower_bound(idx_p, t0 * TE), payload by payload ----
-  int32_t curv = 0;  // lane p: payload p's cursor (the next window's first entry)
-  {
-    const int32_t e0 = (int32_t)(t0 * TE);
-    for (int p = 0; p < np; ++p) {
-      const int32_t* ip = a.p[p].idx;
-      int32_t lo = 0, hi = fw_uni(__builtin_amdgcn_readlane(kl, p));
-      while (hi > lo) {
-        const int32_t len = hi - lo;
-        const int32_t stride = len <= 64 ? 1 : (len + 63) / 64;
-        const int64_t q = (int64_t)lo + (int64_t)lane * stride;
-        const bool ok = q < hi;
-        const int32_t x = ip[ok ? q : lo];
-        const int32_t c = (int32_t)__popcll(__ballot(ok && x < e0));  // a prefix
-        if (stride == 1) {
-          lo += c;
-          break;
-        }
-        const int32_t nlo = c > 0 ? lo + (c - 1) * stride + 1 : lo;
-        const int64_t nhi = (int64_t)lo + (int64_t)c * stride;
-        hi = nhi < hi ? (int32_t)nhi : hi;
-        lo = nlo;
-      }
-      curv = lane == p ? lo : curv;
-    }
-  }
+  // the first tile's local values are issued before the cursor search (independent of it)
+  FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n), Ln;
+  // ---- start cursors: lower_bound(idx_p, t0 * TE), every payload in lock step ----
+  // lane p: payload p's cursor (the next window's first entry)
+  int32_t curv = fw_lower_bounds<NS>(
+      np, (int32_t)(t0 * TE), lane, [&](int p) { return P_idx(p); },
+      [&](int p) { return P_k(p); }, reinterpret_cast<const int32_t*>(a.local));
   int32_t cs[ONE ? NS : 1];
   if constexpr (ONE) {
 #pragma unroll
@@ -1059,7 +1099,6 @@ __global__ void __launch_bounds__(256, FW_MINB_1(EPL)) fold_walk_kernel(FoldArgs
     ix = (has ? P_idx(pc) : reinterpret_cast<const int32_t*>(a.local))[jc];
     vx = (has ? P_val(pc) : a.local)[jc];
   };
-  FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n), Ln;
 #pragma unroll
   for (int p = 0; p < NS; ++p) load_window(p, wi[p], wvv[p]);
   uint32_t seq = 0;
@@ -1237,32 +1276,14 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
   };
   static_assert(DIST == 1 || (DIST == 3 && !ONE), "DIST 3: four groups");
   int32_t cs[FOLD_MAXP];  // CT: the cursors (scalar registers)
-  // ---- start cursors: 64-ary lower_bound(idx_p, t0 * TE), payload by payload ----
-  int32_t curv = 0;
-  {
-    const int32_t e0 = (int32_t)(t0 * TE);
-    for (int p = 0; p < np; ++p) {
-      const int32_t* ip = reinterpret_cast<const int32_t*>(rl64(ipl, p));  // p: run time
-      int32_t lo = 0, hi = fw_uni(__builtin_amdgcn_readlane(kl, p));
-      while (hi > lo) {
-        const int32_t len = hi - lo;
-        const int32_t stride = len <= 64 ? 1 : (len + 63) / 64;
-        const int64_t q = (int64_t)lo + (int64_t)lane * stride;
-        const bool ok = q < hi;
-        const int32_t x = as_global(ip)[ok ? q : lo];
-        const int32_t c = (int32_t)__popcll(__ballot(ok && x < e0));  // a prefix
-        if (stride == 1) {
-          lo += c;
-          break;
-        }
-        const int32_t nlo = c > 0 ? lo + (c - 1) * stride + 1 : lo;
-        const int64_t nhi = (int64_t)lo + (int64_t)c * stride;
-        hi = nhi < hi ? (int32_t)nhi : hi;
-        lo = nlo;
-      }
-      curv = lane == p ? lo : curv;
-    }
-  }
+  // the first tile's local values are issued before the cursor search (independent of it)
+  FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n), Ln;
+  // ---- start cursors: lower_bound(idx_p, t0 * TE), every payload in lock step ----
+  int32_t curv = fw_lower_bounds<FOLD_MAXP>(
+      np, (int32_t)(t0 * TE), lane,
+      [&](int p) { return reinterpret_cast<const int32_t*>(rl64(ipl, p)); },
+      [&](int p) { return fw_uni(__builtin_amdgcn_readlane(kl, p)); },
+      reinterpret_cast<const int32_t*>(a.local));
   if (CT) {
 #pragma unroll
     for (int q = 0; q < (ONE ? FW_G : FOLD_MAXP); ++q) cs[q] = fw_uni(__builtin_amdgcn_readlane(curv, q));
@@ -1310,7 +1331,6 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
   // DIST 3 (four groups, 13..16 payloads): all four groups' windows in registers, each group's
   // issued three groups ahead (into the slot the group before it just freed), so three groups'
   // loads are in flight while one folds
-  FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n), Ln;
   if constexpr (DIST == 3) {
     load_group(0, 0);
     load_group(1, 1);
@@ -1493,8 +1513,8 @@ static unsigned fold_grid(int64_t ntiles, bool group = false) {
     sl = cus * per;
   }
   const int slots_now = sl;
-  // DPZ_FOLD_BLOCKS=N caps the grid at N blocks (A/B diagnostics; 0 = the occupancy slots)
-  static const int64_t cap = getenv("DPZ_FOLD_BLOCKS") ? atoll(getenv("DPZ_FOLD_BLOCKS")) : 0;
+  // DPZ_FOLD_BLOCKS=N caps the grid at N blocks (diagnostic build; 0 = the occupancy slots)
+  const int64_t cap = DPZ_KNOB_INT(FOLD_BLOCKS, 0);
   const int64_t g = cap > 0 ? cap : slots_now;
   return (unsigned)(ntiles < g ? (ntiles > 0 ? ntiles : 1) : g);
 }
@@ -1509,8 +1529,7 @@ static int launch_walk_t(const FoldArgs& fa, bool w2, hipStream_t st) {
   // 13..16 payloads (four groups): the groups kernel with windows issued three groups ahead
   // (DPZ_FOLD_DIST=1: one group ahead, A/B); w2: 128-entry windows
   if constexpr (NS > 4 && DIST == 1 && !W2) {
-    const char* ds = getenv("DPZ_FOLD_DIST");
-    const bool d3 = !ds || atoi(ds) != 1;
+    const bool d3 = DPZ_KNOB_INT(FOLD_DIST, 3) != 1;
     if (d3 && (fa.np + FW_G - 1) / FW_G == FW_G)
       return w2 ? launch_walk_t<VEC, EPL, NS, 3, true>(fa, w2, st)
                 : launch_walk_t<VEC, EPL, NS, 3, false>(fa, w2, st);
@@ -1583,11 +1602,11 @@ static int launch_walk(const FoldArgs& fa, bool vec, double dens, hipStream_t st
     w2 = true;
     e = dens <= 0.105 ? 16 : 8;
   }
-  if (const char* s = getenv("DPZ_FOLD_WALK_EPL")) {
-    const int v = atoi(s);
+  {  // forced tile / window sizes (diagnostic build)
+    const int v = (int)DPZ_KNOB_INT(FOLD_WALK_EPL, 0);
     if (v == 16 || v == 8 || v == 4 || v == 2) e = v;
+    if (DPZ_KNOB_STR(FOLD_WIN)) w2 = DPZ_KNOB_INT(FOLD_WIN, 64) == 128;
   }
-  if (const char* s = getenv("DPZ_FOLD_WIN")) w2 = atoi(s) == 128;
   return fa.np <= 4 ? launch_walk_o<4>(fa, vec, e, false, st) : launch_walk_o<16>(fa, vec, e, w2, st);
 }
 
@@ -1601,6 +1620,186 @@ __global__ void __launch_bounds__(256) replace_kernel(ReplaceJob j) { replace_bl
 int launch_replace(const ReplaceJob& j, hipStream_t st) {
   if (j.c1 > j.c0)
     DPZ_TIMED(DPZ_KT_FOLD, st, replace_kernel<<<(unsigned)((j.c1 - j.c0 + 3) / 4), 256, 0, st>>>(j));
+  return DPZ_OK;
+}
+
+// ---- the fold base on its own (dpz_topk_encode_foldbase off the pipelined filter) -------------
+template <bool VEC>
+__global__ void __launch_bounds__(256) fold_base_kernel(const float* __restrict__ x, int64_t n,
+                                                        FoldBase fb, float* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  if (VEC) {
+    const int64_t n4 = n >> 2;
+    for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < n4; g += stride) {
+      const float4 v = reinterpret_cast<const float4*>(x)[g];
+      reinterpret_cast<float4*>(out)[g] = make_float4(fb.of(v.x), fb.of(v.y), fb.of(v.z), fb.of(v.w));
+    }
+    for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+      out[i] = fb.of(x[i]);
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) out[i] = fb.of(x[i]);
+  }
+}
+
+int launch_fold_base(const float* x, int64_t n, const FoldBase& fb, float* out, hipStream_t st) {
+  if (n <= 0) return DPZ_OK;
+  const int64_t groups = (n + 3) / 4;
+  unsigned nb = (unsigned)((groups + 255) / 256);
+  if (nb > 4096) nb = 4096;
+  if (aligned16(x) && aligned16(out))
+    DPZ_TIMED(DPZ_KT_FOLD, st, fold_base_kernel<true><<<nb, 256, 0, st>>>(x, n, fb, out));
+  else
+    DPZ_TIMED(DPZ_KT_FOLD, st, fold_base_kernel<false><<<nb, 256, 0, st>>>(x, n, fb, out));
+  return DPZ_OK;
+}
+
+// ---- DPZ_FOLD_BASE_READY: rewrite only the elements the payloads hit --------------------------
+// out already holds the fold of every element's local value alone (FoldBase::of, written by the
+// encoder's filter); an element hit by one or more payloads is folded here exactly, in the
+// reference's order (payload terms in payload order, then the self term).  Block b owns the
+// element range [b R, (b + 1) R) (R from the payloads' density, ~1024 entries per block): the
+// payloads' runs of the range are found by lock-step searches (one wave per four payloads, lower
+// bounds of both ends), staged in LDS, and each entry whose element no EARLIER payload hits (an
+// LDS binary search per earlier run) folds that element: the local value gathered once, the
+// later payloads' values by LDS binary search.  A range whose runs exceed the LDS stage is
+// processed in halves (adversarially clustered payloads; always terminates: one element holds
+// <= 16 entries).  Bytes: the payload entries, a local gather and an out write per hit element.
+constexpr int PT_CAP = 4096;  // entries staged per pass (32 KB of LDS)
+constexpr int PT_EPT = PT_CAP / 256;
+
+__device__ __forceinline__ int pt_find(const int32_t* sidx, int b, int e, int32_t key) {
+  // position of key in the sorted LDS run [b, e), or -1
+  while (b < e) {
+    const int m = (b + e) >> 1;
+    const int32_t v = sidx[m];
+    if (v < key) b = m + 1;
+    else if (v > key) e = m;
+    else return m;
+  }
+  return -1;
+}
+
+__global__ void __launch_bounds__(256) fold_patch_kernel(FoldArgs a, int64_t range) {
+  __shared__ int32_t s_idx[PT_CAP];
+  __shared__ float s_val[PT_CAP];
+  __shared__ int32_t s_rlo[FOLD_MAXP], s_rhi[FOLD_MAXP], s_off[FOLD_MAXP + 1];
+  const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
+  const int np = a.np;
+  const int64_t n = a.n;
+  const int64_t b_lo = (int64_t)blockIdx.x * range;
+  const int64_t b_hi = b_lo + range < n ? b_lo + range : n;
+  int64_t cur = b_lo, len = b_hi - b_lo;
+  while (cur < b_hi) {
+    const int64_t s_end = cur + len < b_hi ? cur + len : b_hi;
+    // runs of [cur, s_end): wave w searches payloads w, w + 4, w + 8, w + 12, both ends, in lock
+    // step (virtual search q: payload w + 4 (q & 3), target q < 4 ? cur : s_end)
+    {
+      const int32_t lo32 = (int32_t)cur, hi32 = (int32_t)s_end;
+      const int32_t r = fw_lower_bounds_t<8>(
+          8, [&](int q) { return q < 4 ? lo32 : hi32; }, lane,
+          [&](int q) { return a.p[wid + 4 * (q & 3)].idx; },
+          [&](int q) {
+            const int pp = wid + 4 * (q & 3);
+            return pp < np ? (int32_t)a.p[pp].k : 0;
+          },
+          reinterpret_cast<const int32_t*>(a.local));
+      if (lane < 8) {
+        const int pp = wid + 4 * (lane & 3);
+        if (pp < np) {
+          if (lane < 4) s_rlo[pp] = r;
+          else s_rhi[pp] = r;
+        }
+      }
+    }
+    __syncthreads();
+    if (t == 0) {
+      int32_t o = 0;
+      for (int p = 0; p < np; ++p) {
+        s_off[p] = o;
+        o += s_rhi[p] > s_rlo[p] ? s_rhi[p] - s_rlo[p] : 0;
+      }
+      s_off[np] = o;
+    }
+    __syncthreads();
+    const int total = s_off[np];
+    if (total > PT_CAP) {  // uniform: halve the range and search again
+      len = (s_end - cur + 1) / 2;
+      __syncthreads();
+      continue;
+    }
+    // stage the runs (payload-major, each run sorted)
+    for (int j = t; j < total; j += 256) {
+      int p = 0;
+      while (p + 1 < np && j >= s_off[p + 1]) ++p;
+      const int64_t src = (int64_t)s_rlo[p] + (j - s_off[p]);
+      s_idx[j] = as_global(a.p[p].idx)[src];
+      s_val[j] = as_global(a.p[p].val)[src];
+    }
+    __syncthreads();
+    // owners: entry j of payload p folds its element iff no earlier payload's run holds it; the
+    // local values of every owned element are gathered before any later-payload search
+    int32_t ee[PT_EPT];
+    int pj[PT_EPT];
+    float xv[PT_EPT];
+#pragma unroll
+    for (int i = 0; i < PT_EPT; ++i) {
+      const int j = t + 256 * i;
+      ee[i] = -1;
+      pj[i] = 0;
+      if (j < total) {
+        int p = 0;
+        while (p + 1 < np && j >= s_off[p + 1]) ++p;
+        const int32_t e = s_idx[j];
+        bool own = e >= cur && e < s_end;  // an invalid (unsorted) payload cannot write outside
+        for (int q = 0; q < p && own; ++q) own = pt_find(s_idx, s_off[q], s_off[q + 1], e) < 0;
+        if (own) {
+          ee[i] = e;
+          pj[i] = p;
+        }
+      }
+      xv[i] = a.local[ee[i] >= 0 ? ee[i] : 0];
+    }
+#pragma unroll
+    for (int i = 0; i < PT_EPT; ++i) {
+      if (ee[i] < 0) continue;
+      const int j = t + 256 * i;
+      const int p = pj[i];
+      const float x = xv[i];
+      float acc = 0.0f;
+      for (int q = 0; q < np; ++q) {
+        float v = x;
+        if (q == p) {
+          v = s_val[j];
+        } else if (q > p) {
+          const int pos = pt_find(s_idx, s_off[q], s_off[q + 1], ee[i]);
+          if (pos >= 0) v = s_val[pos];
+        }
+        const float term = v * a.p[q].w;
+        acc = q == 0 ? term : acc + term;
+      }
+      acc = acc + x * a.w_self;
+      a.out[ee[i]] = acc;
+    }
+    __syncthreads();  // the stage is reused by the next sub-range
+    cur = s_end;
+    len = b_hi - cur;
+  }
+}
+
+static int launch_fold_patch(const FoldArgs& fa, hipStream_t st) {
+  int64_t etot = 0;
+  for (int i = 0; i < fa.np; ++i) etot += fa.p[i].k;
+  if (etot == 0) return DPZ_OK;
+  // ~1024 entries per block on average (a quarter of the stage), at least ~2048 blocks' worth of
+  // parallelism when the payloads are sparse
+  const double dens = (double)etot / (double)fa.n;
+  int64_t range = (int64_t)(1024.0 / dens);
+  const int64_t par = (fa.n + 2047) / 2048;
+  if (range > par) range = par;
+  if (range < 256) range = 256;
+  range = (range + 63) & ~int64_t(63);
+  const int64_t nb = (fa.n + range - 1) / range;
+  DPZ_TIMED(DPZ_KT_FOLD, st, fold_patch_kernel<<<(unsigned)nb, 256, 0, st>>>(fa, range));
   return DPZ_OK;
 }
 
@@ -1649,6 +1848,23 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
     if (!is_dense(i) && k[i] > 0 && (!idx || !idx[i])) return DPZ_ERR_ARG;
   }
   if (!ws || ws_bytes < dpz_decode_workspace_bytes(n, n_payloads)) return DPZ_ERR_WORKSPACE;
+  if (flags & DPZ_FOLD_BASE_READY) {
+    // out holds the no-hit base of exactly this fold (dpz_topk_encode_foldbase over local with
+    // these weights): only the plain Metro-Hastings form of one group of sparse payloads
+    if (flags & ~(DPZ_FOLD_BASE_READY | DPZ_FOLD_SELF)) return DPZ_ERR_ARG;
+    if (!(flags & DPZ_FOLD_SELF) || n_payloads < 1 || n_payloads > FOLD_MAXP) return DPZ_ERR_ARG;
+    if (n >= (int64_t(1) << 31) - 1024) return DPZ_ERR_UNSUPPORTED;
+    FoldArgs fa{};
+    fa.local = local; fa.out = out; fa.n = n; fa.np = n_payloads; fa.w_self = w_self;
+    for (int i = 0; i < n_payloads; ++i) {
+      if (is_dense(i)) return DPZ_ERR_ARG;
+      fa.p[i].idx = (idx && idx[i]) ? idx[i] : reinterpret_cast<const int32_t*>(local);
+      fa.p[i].val = vals[i] ? vals[i] : local;
+      fa.p[i].k = k[i];
+      fa.p[i].w = w[i];
+    }
+    return launch_fold_patch(fa, st);
+  }
   bool vec = ((reinterpret_cast<uintptr_t>(local) | reinterpret_cast<uintptr_t>(out)) & 15u) == 0;
   for (int i = 0; i < n_payloads; ++i)
     if (is_dense(i) && (reinterpret_cast<uintptr_t>(vals[i]) & 15u)) vec = false;
@@ -1700,8 +1916,8 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
       fa.p[i].w = (replace_only || add_only) ? 1.0f : w[base + i];
       if (fa.p[i].idx && fa.p[i].k > kmax) kmax = fa.p[i].k;
     }
-    // DPZ_FOLD_PHASES=1 forces the per-payload phase path (A/B diagnostics)
-    static const bool force_phases = getenv("DPZ_FOLD_PHASES") && atoi(getenv("DPZ_FOLD_PHASES"));
+    // DPZ_FOLD_PHASES=1 forces the per-payload phase path (diagnostic build)
+    const bool force_phases = DPZ_KNOB_INT(FOLD_PHASES, 0) != 0;
     fa.all_sparse = force_phases ? 0 : 1;
     fa.dense_mask = 0;
     for (int i = 0; i < fa.np; ++i)
@@ -1723,7 +1939,7 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
         etot += fa.p[i].k;
         if ((double)fa.p[i].k / (double)n > dens) dens = (double)fa.p[i].k / (double)n;
       }
-    const int kind = getenv("DPZ_FOLD_KIND") ? atoi(getenv("DPZ_FOLD_KIND")) : 0;
+    const int kind = (int)DPZ_KNOB_INT(FOLD_KIND, 0);
     const double avg = fa.np > 0 ? (double)etot / (double)fa.np / (double)n : 0.0;
     bool use_walk = walk_ok(fa) && (fa.np <= 4 || (avg >= 0.0175 && avg <= 0.21));
     if (kind) use_walk = walk_ok(fa) && kind == 4;
@@ -1743,7 +1959,7 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
     if (fa.all_sparse && fa.np > 0 && !fa.replace_only) {
       bool use_group = fa.np >= 8 && etot > FOLD_GROUP_MIN * ntiles &&
                        etot <= 2 * (int64_t)FG_CAP * ntiles;
-      if (const char* e = getenv("DPZ_FOLD_GROUP")) use_group = atoi(e) != 0;
+      if (DPZ_KNOB_STR(FOLD_GROUP)) use_group = DPZ_KNOB_INT(FOLD_GROUP, 0) != 0;
       if (kind) use_group = kind == 2;
       if (use_group) {
         if (vec) DPZ_TIMED(DPZ_KT_FOLD, st, fold_group_kernel<true><<<fold_grid<true>(ntiles, true), FOLD_THREADS, 0, st>>>(fa));

@@ -1035,9 +1035,8 @@ extern "C" int dpz_lz4_decompress(const uint8_t* frame_dev, const uint8_t* frame
     if (bmax > 65536 || shm > 160 * 1024) return DPZ_ERR_UNSUPPORTED;
     DPZ_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(lz4_decode_kernel),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-    // DPZ_LZ4_PAR=0: every independent block on the sequential decoder (A/B diagnostics)
-    const char* pe = getenv("DPZ_LZ4_PAR");
-    const bool par = !(pe && atoi(pe) == 0);
+    // DPZ_LZ4_PAR=0: every independent block on the sequential decoder (diagnostic build)
+    const bool par = DPZ_KNOB_INT(LZ4_PAR, 1) != 0;
     if (linked) {
       DPZ_TIMED(DPZ_KT_LZ4, st, lz4_decode_kernel<<<1, 64, shm, st>>>(
                                     frame_dev, tab, nb, 1, (uint32_t)bmax, win, out,

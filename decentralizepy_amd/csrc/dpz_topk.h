@@ -201,8 +201,8 @@ struct FastGeom {
 static inline FastGeom fast_geom(int64_t n, int64_t k = 0, bool shared = false) {
   FastGeom g;
   int64_t W = (n + W_MIN_RANGE - 1) / W_MIN_RANGE;
-  // DPZ_WLONE=N caps a lone codec's grid at N segments (A/B diagnostics)
-  static const int64_t wlone = getenv("DPZ_WLONE") ? atoll(getenv("DPZ_WLONE")) : 0;
+  // DPZ_WLONE=N caps a lone codec's grid at N segments (diagnostic build, A/B)
+  const int64_t wlone = DPZ_KNOB_INT(WLONE, 0);
   const int64_t wmax = (shared && n <= W_SMALL_N)
                            ? W_SMALL
                            : ((wlone > 0 && wlone < W_MAX) ? wlone : W_MAX);
@@ -274,7 +274,13 @@ struct EncodeArgs {
   int32_t* status_out;    // sampled path, ASYNC: compact's block 0 also writes the call's final
                           // status word here (device), or nullptr
   bool shared;            // DPZ_TOPK_SHARED: the filter grid for several codecs per GPU
+  const FoldBase* fbase;  // dpz_topk_encode_foldbase: the pipelined filter also writes
+  float* base_out;        // base_out[j] = fbase->of(x[j]) (sampled path, fused_foldbase_ok)
 };
+// the fold base can ride on the pipelined filter: aligned, no accumulation, x0 given
+bool fused_foldbase_ok(const EncodeArgs& a, bool vec);
+// base_out[j] = fb.of(x[j]) as its own launch (dpz_fold.hip)
+int launch_fold_base(const float* x, int64_t n, const FoldBase& fb, float* out, hipStream_t st);
 
 // dpz_topk_exact.hip / dpz_topk_sampled.hip
 // keep_ties: select every key >= T (the k-th largest key), no zero keys when T == 0, writing at

@@ -140,16 +140,55 @@ extern "C" int dpz_topk_encode_status(const float* x, const float* x0, float* ac
                                       const float* vals_src, int64_t n, int64_t k,
                                       int32_t* idx_out, float* val_out, int32_t* counter,
                                       void* ws, size_t ws_bytes, int32_t* status_out,
-                                      dpz_stream_t stream) {
+                                      int flags, dpz_stream_t stream) {
   if (!status_out) return DPZ_ERR_ARG;
+  // only DPZ_TOPK_SHARED applies (the call is asynchronous, sampled-path, unsplit by contract)
+  if (flags & ~DPZ_TOPK_SHARED) return DPZ_ERR_ARG;
   return topk_encode_status(x, x0, acc, acc_mode, vals_src, n, k, idx_out, val_out, counter, ws,
-                            ws_bytes, static_cast<hipStream_t>(stream), status_out);
+                            ws_bytes, static_cast<hipStream_t>(stream), status_out,
+                            (flags & DPZ_TOPK_SHARED) != 0);
 }
 
 static bool overlaps(const void* p, size_t pb, const void* q, size_t qb) {
   if (!p || !q || pb == 0 || qb == 0) return false;
   const uintptr_t a = reinterpret_cast<uintptr_t>(p), b = reinterpret_cast<uintptr_t>(q);
   return a < b + qb && b < a + pb;
+}
+
+extern "C" int dpz_topk_encode_foldbase(const float* x, const float* x0, float* acc, int acc_mode,
+                                        const float* vals_src, int64_t n, int64_t k,
+                                        int32_t* idx_out, float* val_out, int32_t* counter,
+                                        void* ws, size_t ws_bytes, int flags, int n_weights,
+                                        const float* w, float w_self, float* base_out,
+                                        dpz_stream_t stream) {
+  EncodeArgs a{x, x0, acc, acc_mode, vals_src, n, k, idx_out, val_out, counter,
+               static_cast<char*>(ws), static_cast<hipStream_t>(stream)};
+  int rc = validate(a, ws_bytes);
+  if (rc != DPZ_OK) return rc;
+  if (flags & (DPZ_TOPK_STREAM | DPZ_TOPK_TAIL)) return DPZ_ERR_ARG;
+  if (n_weights < 1 || n_weights > FOLDBASE_MAXW || !w) return DPZ_ERR_ARG;
+  if (n > 0 && !base_out) return DPZ_ERR_ARG;
+  // the base is an output of its own: it may not overlap anything the encode reads or writes
+  const size_t nb = (size_t)n * 4;
+  if (overlaps(base_out, nb, x, nb) || overlaps(base_out, nb, x0, nb) ||
+      overlaps(base_out, nb, acc, nb) || overlaps(base_out, nb, vals_src, nb) ||
+      overlaps(base_out, nb, counter, nb) || overlaps(base_out, nb, idx_out, (size_t)k * 4) ||
+      overlaps(base_out, nb, val_out, (size_t)k * 4) || overlaps(base_out, nb, ws, ws_bytes))
+    return DPZ_ERR_ARG;
+  if (n == 0) return DPZ_OK;
+  FoldBase fb{};
+  fb.nw = n_weights;
+  for (int i = 0; i < n_weights; ++i) fb.w[i] = w[i];
+  fb.ws = w_self;
+  a.fbase = &fb;
+  a.base_out = base_out;
+  if (!(flags & DPZ_TOPK_EXACT) && k > 0 && fused_foldbase_ok(a, all_aligned(a)))
+    return dpz_topk_dispatch(a, flags);  // the filter writes the base as it streams x
+  rc = launch_fold_base(x, n, fb, base_out, a.st);
+  if (rc != DPZ_OK) return rc;
+  a.fbase = nullptr;
+  a.base_out = nullptr;
+  return dpz_topk_dispatch(a, flags);
 }
 
 extern "C" int dpz_topk_encode_replace(const float* x, const float* x0, float* acc, int acc_mode,
@@ -181,9 +220,10 @@ extern "C" int dpz_topk_encode_replace(const float* x, const float* x0, float* a
   // Decoding over the very tensor being encoded (reference: deserialized_model starts from the
   // node's current state_dict, the model its serialized_model just encoded): the filter, which
   // streams x anyway, writes out = x, and only the payload entries are scattered afterwards —
-  // 4n bytes of reads fewer than an independent replace (DPZ_FUSED_COPY=0 disables, A/B).
-  const char* fe = getenv("DPZ_FUSED_COPY");
-  if (carried && (!fe || atoi(fe) != 0) && r_local == x && r_n == n && acc_mode == DPZ_ACC_NONE) {
+  // 4n bytes of reads fewer than an independent replace (DPZ_FUSED_COPY=0 disables it in the
+  // diagnostic build, A/B).
+  if (carried && DPZ_KNOB_INT(FUSED_COPY, 1) != 0 && r_local == x && r_n == n &&
+      acc_mode == DPZ_ACC_NONE) {
     job.scatter = 1;
     job.c1 = scatter_chunks(r_k);
   }

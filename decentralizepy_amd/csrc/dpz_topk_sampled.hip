@@ -400,11 +400,14 @@ __device__ __forceinline__ void stage_group(WaveList& L, uint32_t* h, const uint
 // segment.
 // SRC: the key's operands — 0: |x|, 1: |x - x0|, 2: |acc + x| (DPZ_ACC_ADD without x0: the
 // wavelet encode's W(x - x0) plus the accumulated changes, C3).
-template <int SRC, bool COPY, int D, int OCC>
+// CP: what the filter also writes as x streams by — 0 nothing, 1 copy_out = x (the fused replace
+// decode), 2 copy_out = fb.of(x) (the Metro-Hastings fold's no-hit base, dpz_topk_encode_foldbase).
+template <int SRC, int CP, int D, int OCC>
 __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
     KeySrc s, int64_t n, uint32_t r_lo, uint32_t r_hi, int64_t W, int64_t R, int64_t CAP,
     TopkCtrl* ctrl, const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt,
-    uint32_t* cidx, uint32_t* ckey, float* cval, float* __restrict__ copy_out) {
+    uint32_t* cidx, uint32_t* ckey, float* cval, float* __restrict__ copy_out, int xnt,
+    FoldBase fb) {
   static_assert(D >= 2, "at least one group in flight");
   typedef float v4f __attribute__((ext_vector_type(4)));
   __shared__ uint32_t h[HBR];
@@ -431,7 +434,9 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
   auto ld = [&](int64_t j, int u) {
     const int64_t i0 = beg + j * 256 + lane * 4;
     const int64_t g4 = (i0 < end4 ? i0 : 0) >> 2;
-    A[u] = __builtin_nontemporal_load(xa + g4);
+    // x: non-temporal unless a decode of this node's round reads x next (xnt == 0: x stays in
+    // the Infinity Cache for it); x0 / acc are read once
+    A[u] = (xnt & 1) ? __builtin_nontemporal_load(xa + g4) : xa[g4];
     if (X0) B[u] = __builtin_nontemporal_load(xb + g4);
   };
 #pragma unroll
@@ -450,7 +455,12 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
   auto proc = [&](int64_t j, int u) {
     const int64_t i0 = beg + j * 256 + lane * 4;
     const int cq = i0 < end4 ? 4 : 0;
-    if (COPY && cq) __builtin_nontemporal_store(A[u], reinterpret_cast<v4f*>(copy_out) + (i0 >> 2));
+    if (CP == 1 && cq) __builtin_nontemporal_store(A[u], reinterpret_cast<v4f*>(copy_out) + (i0 >> 2));
+    if (CP == 2 && cq) {
+      const v4f b = {fb.of(A[u].x), fb.of(A[u].y), fb.of(A[u].z), fb.of(A[u].w)};
+      if (xnt & 2) __builtin_nontemporal_store(b, reinterpret_cast<v4f*>(copy_out) + (i0 >> 2));
+      else reinterpret_cast<v4f*>(copy_out)[i0 >> 2] = b;
+    }
     const float xv[4] = {A[u].x, A[u].y, A[u].z, A[u].w};
     uint32_t kq[4];
     if (SRC == 1) {
@@ -483,7 +493,8 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
     if (v) {
       xv[0] = s.x[i];
       kq[0] = key_of(SRC == 1 ? xv[0] - s.x0[i] : (SRC == 2 ? s.acc[i] + xv[0] : xv[0]));
-      if (COPY) copy_out[i] = xv[0];
+      if (CP == 1) copy_out[i] = xv[0];
+      if (CP == 2) copy_out[i] = fb.of(xv[0]);
     }
     // one element per lane: lane order is index order
     stage_group(L, h, kq, xv, v ? 1 : 0, (uint32_t)i, lane, lo, hi, shift, CAP, run, dense);
@@ -1263,11 +1274,11 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
 }
 
 // Fractions of a co-scheduled replace job's chunks carried by sample / select / compact;
-// DPZ_COSCHED="f0,f1,f2" overrides (read per call: a tuning knob, no global state).
+// DPZ_COSCHED="f0,f1,f2" overrides them in the diagnostic build (dpz_knobs.h).
 // Defaults measured on MI355X, see DESIGN.md §3.6.
 static void cosched_shares(double f[3]) {
   f[0] = 0.45; f[1] = 0.55; f[2] = 0.0;
-  if (const char* e = getenv("DPZ_COSCHED")) {
+  if (const char* e = DPZ_KNOB_STR(COSCHED)) {
     double v[3];
     if (sscanf(e, "%lf,%lf,%lf", &v[0], &v[1], &v[2]) == 3 && v[0] >= 0 && v[1] >= 0 &&
         v[2] >= 0) {
@@ -1312,7 +1323,7 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
       // latency-bound compact leaves most CU slots free: C2 one-node step 57.2 -> 55.6 us on
       // MI355X vs appended to select) or select (DPZ_SCATTER_AT=select, A/B diagnostics)
       // (DPZ_SCATTER_AT=split: half in each)
-      const char* e = getenv("DPZ_SCATTER_AT");
+      const char* e = DPZ_KNOB_STR(SCATTER_AT);
       const bool at_select = e && e[0] == 's' && e[1] == 'e';
       const bool split = e && e[0] == 's' && e[1] == 'p';
       f[0] = 0.0;
@@ -1342,23 +1353,32 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
     // The pipelined filter (PartialModel: aligned, no accumulation): depth 2 at 8 waves / SIMD
     // when the grid needs them (more than 4096 segments), else depth DPZ_FILTER_DEPTH (default
     // 4) at 4 waves / SIMD.  DPZ_FILTER_PIPE=0 selects the batched filter (A/B diagnostics).
-    static const int pipe = getenv("DPZ_FILTER_PIPE") ? atoi(getenv("DPZ_FILTER_PIPE")) : 1;
-    static const int depth = getenv("DPZ_FILTER_DEPTH") ? atoi(getenv("DPZ_FILTER_DEPTH")) : 4;
+    const int pipe = (int)DPZ_KNOB_INT(FILTER_PIPE, 1);
+    const int depth = (int)DPZ_KNOB_INT(FILTER_DEPTH, 4);
     const bool add_only = a.acc_mode == DPZ_ACC_ADD && !a.x0;
     if (VEC && (a.acc_mode == DPZ_ACC_NONE || add_only) && pipe > 0) {
       const bool x0 = a.x0 != nullptr;
+      // bit 0: x loaded non-temporal; bit 1: the fold base stored non-temporal
+      const int xnt = (int)DPZ_KNOB_INT(FILTER_XNT, 3);
+      // the fold base (dpz_topk_encode_foldbase) rides on the same copy slot
+      const bool fbase = a.fbase && a.base_out && x0 && !copy_out;
+      float* const cpo = fbase ? a.base_out : copy_out;
+      FoldBase fbv{};
+      if (fbase) fbv = *a.fbase;
       const int dsel = g.W > 4096 ? 2 : (depth >= 8 ? 8 : (depth >= 6 ? 6 : 4));
 #define DPZ_PIPE(D_, O_)                                                                      \
   do {                                                                                        \
-    if (add_only) DPZ_PIPE1(2, false, D_, O_);                                                \
-    else if (x0 && copy_out) DPZ_PIPE1(1, true, D_, O_);                                      \
-    else if (x0) DPZ_PIPE1(1, false, D_, O_);                                                 \
-    else if (copy_out) DPZ_PIPE1(0, true, D_, O_);                                            \
-    else DPZ_PIPE1(0, false, D_, O_);                                                         \
+    if (add_only) DPZ_PIPE1(2, 0, D_, O_);                                                    \
+    else if (fbase) DPZ_PIPE1(1, 2, D_, O_);                                                  \
+    else if (x0 && copy_out) DPZ_PIPE1(1, 1, D_, O_);                                         \
+    else if (x0) DPZ_PIPE1(1, 0, D_, O_);                                                     \
+    else if (copy_out) DPZ_PIPE1(0, 1, D_, O_);                                               \
+    else DPZ_PIPE1(0, 0, D_, O_);                                                             \
   } while (0)
 #define DPZ_PIPE1(X0_, CP_, D_, O_)                                                           \
   DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_pipe_kernel<X0_, CP_, D_, O_><<<nb, 256, 0, a.st>>>( \
-      s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval, copy_out))
+      s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval, cpo, \
+      xnt, fbv))
       switch (dsel) {
         case 2: DPZ_PIPE(2, 8); break;
         case 8: DPZ_PIPE(8, 4); break;
@@ -1383,12 +1403,10 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
       blidx, jb[1]));
   float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE) ? a.acc : nullptr;
   const unsigned ncmp = (unsigned)((g.W + CSEG - 1) / CSEG);
-  // DPZ_COUNTER_PLAIN=0 / 1 forces the counter update form (A/B diagnostics)
-  bool plain = a.k > a.n / 32;
-  if (const char* e = getenv("DPZ_COUNTER_PLAIN")) plain = atoi(e) != 0;
-  // DPZ_SCATTER_FIRST=1: the decode's blocks dispatched ahead of compact's own (A/B)
-  const char* sfe = getenv("DPZ_SCATTER_FIRST");
-  const int64_t nrep_first = (sfe && atoi(sfe) != 0) ? (int64_t)pb[2] : 0;
+  // DPZ_COUNTER_PLAIN=0 / 1 forces the counter update form (diagnostic build, A/B)
+  const bool plain = DPZ_KNOB_INT(COUNTER_PLAIN, a.k > a.n / 32 ? 1 : 0) != 0;
+  // DPZ_SCATTER_FIRST=1: the decode's blocks dispatched ahead of compact's own (diagnostic, A/B)
+  const int64_t nrep_first = DPZ_KNOB_INT(SCATTER_FIRST, 0) != 0 ? (int64_t)pb[2] : 0;
   if (plain)
     DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC, true><<<ncmp + pb[2], 256, 0, a.st>>>(
         s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, cidx,
@@ -1419,6 +1437,13 @@ extern "C" int dpz_debug_stamps(unsigned long long* host_out, int reset) {
   return 0;
 }
 #endif
+
+bool fused_foldbase_ok(const EncodeArgs& a, bool vec) {
+  // the pipelined filter's PartialModel configuration (run_sampled_t): aligned operands, no
+  // accumulation, a change against x0; the whole encode in one call (no phase split)
+  return vec && a.acc_mode == DPZ_ACC_NONE && a.x0 && aligned16(a.base_out) &&
+         DPZ_KNOB_INT(FILTER_PIPE, 1) > 0 && use_sampled(a.n, a.k) && !a.job;
+}
 
 int run_sampled(const EncodeArgs& a, const WsLayout& L, bool vec, int phases) {
   return vec ? run_sampled_t<true>(a, L, phases) : run_sampled_t<false>(a, L, phases);

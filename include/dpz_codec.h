@@ -69,6 +69,10 @@ typedef void* dpz_stream_t; /* hipStream_t */
                                      s += w * T_i; s += (1 - sum w) * q)                      */
 #define DPZ_FOLD_ADD_ONLY 0x8     /* n_payloads == 1: out = local + T_0 with T_0 zero-based
                                      (reference STC.py:290-303 process_received)              */
+#define DPZ_FOLD_BASE_READY 0x40 /* out already holds this fold's no-hit base over local (written
+                                  * by dpz_topk_encode_foldbase with the same w / w_self): only the
+                                  * elements the (sparse) payloads hit are rewritten.  Only with
+                                  * DPZ_FOLD_SELF, 1 <= n_payloads <= 16, no dense payload.      */
 #define DPZ_FOLD_ALSO_LOCAL 0x20  /* the result is ALSO written over local, in place (the
                                      reference's load_state_dict of the averaged model while
                                      _post_step makes it init_model, Sharing.py:186-190,
@@ -99,6 +103,24 @@ int dpz_topk_encode(const float* x, const float* x0, float* acc, int acc_mode,
                     const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
                     float* val_out, int32_t* counter, void* ws, size_t ws_bytes, int flags,
                     dpz_stream_t stream);
+/* dpz_topk_encode (same arguments, flags and result) that ALSO writes the no-hit base of the
+ * node's coming Metro-Hastings average over x (reference sharing/Sharing.py:156-190 with the
+ * local model x, the fold of PartialModel payloads deserialized over it, PartialModel.py:257-303):
+ *   base_out[j] = fl(...fl(fl(x[j]*w[0]) + fl(x[j]*w[1])) ... + fl(x[j]*w_self))
+ * i.e. what dpz_decode_average(x, ..., w, w_self, DPZ_FOLD_SELF) computes at an element no
+ * payload hits.  On the sampled path with 16-byte aligned operands and DPZ_ACC_NONE the filter
+ * writes it as it streams x (4n bytes written, no extra read); otherwise a separate pass writes it.
+ * A later dpz_decode_average(local = x, the payloads, the SAME w / w_self, DPZ_FOLD_SELF |
+ * DPZ_FOLD_BASE_READY, out = base_out) then rewrites only the elements its payloads hit — the
+ * decode's 8n bytes of streaming become a gather per hit element.  1 <= n_weights <= 16;
+ * base_out (n floats) may not overlap any buffer of the encode (DPZ_ERR_ARG); no STREAM / TAIL
+ * split.                                                                                       */
+int dpz_topk_encode_foldbase(const float* x, const float* x0, float* acc, int acc_mode,
+                             const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
+                             float* val_out, int32_t* counter, void* ws, size_t ws_bytes,
+                             int flags, int n_weights, const float* w, float w_self,
+                             float* base_out, dpz_stream_t stream);
+
 /* Top-k encode (exactly dpz_topk_encode with the same arguments) TOGETHER WITH one independent
  * replace decode (exactly dpz_decode_average(r_local, r_n, 1, &r_idx, &r_val, &r_k, NULL, 0,
  * DPZ_FOLD_REPLACE_ONLY, r_out, r_ws, r_ws_bytes) — reference sharing/PartialModel.py:257-303,
@@ -168,11 +190,12 @@ int dpz_topk_complete(const float* x, const float* x0, float* acc, int acc_mode,
  * the result is final; otherwise the sampled path missed, nothing was written or updated, and the
  * caller re-runs the encode with DPZ_TOPK_EXACT.  Lets a caller enqueue many encodes that share
  * one workspace (a gossip round's nodes, decentralizepy_amd/gossip_jwins.py) and read every
- * status once; replaces the same reference lines as dpz_topk_encode.                          */
+ * status once; replaces the same reference lines as dpz_topk_encode.  flags: 0 or
+ * DPZ_TOPK_SHARED (any other bit is DPZ_ERR_ARG).                                              */
 int dpz_topk_encode_status(const float* x, const float* x0, float* acc, int acc_mode,
                            const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
                            float* val_out, int32_t* counter, void* ws, size_t ws_bytes,
-                           int32_t* status_out, dpz_stream_t stream);
+                           int32_t* status_out, int flags, dpz_stream_t stream);
 
 /* Batched decode + Metro-Hastings fold over n_payloads neighbour payloads.
  * Replaces reference sharing/PartialModel.py:257-303 (T = cat(local); T[idx] = params),

@@ -18,3 +18,19 @@ def dev():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+_DIAG = None
+
+
+@pytest.fixture
+def diag_lib(monkeypatch):
+    """Route codec calls through the diagnostic build (libdpzcodec_diag.so, csrc/dpz_knobs.h)
+    for one test, so DPZ_* environment switches set with monkeypatch force kernel paths.  The
+    product library reads no environment variable."""
+    global _DIAG
+    from decentralizepy_amd import _lib
+    if _DIAG is None:
+        _DIAG = _lib.diag_lib()
+    monkeypatch.setattr(_lib, "_lib", _DIAG)
+    return _DIAG

@@ -29,3 +29,19 @@ def test_world_mismatch_is_refused():
                         "--no-cpu"], capture_output=True, text=True, env=env, timeout=300,
                        cwd=ROOT)
     assert p.returncode != 0 and "WORLD_SIZE=1" in (p.stderr + p.stdout)
+
+
+def test_torchrun_without_gpus_takes_launcher_world():
+    """``torchrun --nproc-per-node 2 bench.py`` (no --gpus): the ranks take WORLD_SIZE from the
+    launcher instead of refusing."""
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr", "127.0.0.1", "--master-port",
+                        "29613", os.path.join(ROOT, "bench.py"), "--selftest-spawn", "--no-cpu"],
+                       capture_output=True, text=True, env=env, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert sorted(d["rank"] for d in lines) == [0, 1]
+    assert {d["world"] for d in lines} == {2}

@@ -113,3 +113,21 @@ def test_staging_pinned_cap_refuses_before_pinning():
     assert st.get("local", 1000, torch.float32) is None and st.total == 0
     names = PayloadNames()
     assert len({names("idx") for _ in range(3 * names.slots)}) == names.slots <= 8
+
+
+def test_product_library_reads_no_environment():
+    """Kernel selection in libdpzcodec.so is compile-time (csrc/dpz_knobs.h): the product library
+    neither imports getenv nor carries a DPZ_* switch name; the diagnostic build does both."""
+    import subprocess
+    from decentralizepy_amd import _lib
+    nm = "/opt/rocm/lib/llvm/bin/llvm-nm"
+    if not os.path.exists(nm):
+        nm = "nm"
+    dyn = subprocess.run([nm, "-D", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    assert "getenv" not in dyn.stdout
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert re.search(rb"DPZ_[A-Z_]{3,}\x00", blob) is None
+    if os.path.exists(_lib.DIAG_PATH):
+        assert b"DPZ_FOLD_KIND\x00" in open(_lib.DIAG_PATH, "rb").read()
+        d = _lib.diag_lib()
+        assert d.dpz_build_id().decode() == _lib.source_build_id()

@@ -264,7 +264,7 @@ def test_fold_all_sparse_overlapping(dev, n, alpha, npay):
 @pytest.mark.parametrize("n,alpha,npay", [(1_000_003, 0.01, 16), (1_000_003, 0.1, 16),
                                           (200_003, 0.4, 3), (100_003, 0.99, 2),
                                           (300_001, 0.12, 20)])
-def test_fold_paths_forced(dev, monkeypatch, group, n, alpha, npay):
+def test_fold_paths_forced(dev, diag_lib, monkeypatch, group, n, alpha, npay):
     """The slotted fold (DPZ_FOLD_GROUP=1: every all-sparse group, incl. sparse alpha, several
     rounds per tile at alpha 0.99 x 2) and the hit-chain / phase paths (DPZ_FOLD_GROUP=0, also at
     dense alpha) are each bit-exact vs the oracle, with and without the self term, and with a
@@ -308,7 +308,7 @@ def test_fold_paths_forced(dev, monkeypatch, group, n, alpha, npay):
                                                  (300_001, 0.6, 4, 0), (1_000_003, 0.45, 16, 1),
                                                  (300_001, 0.1, 13, 0), (300_001, 0.4, 14, 0),
                                                  (1_000_003, 0.15, 16, 0), (300_001, 0.07, 15, 0)])
-def test_fold_kinds_forced(dev, monkeypatch, kind, n, alpha, npay, ndense):
+def test_fold_kinds_forced(dev, diag_lib, monkeypatch, kind, n, alpha, npay, ndense):
     """Every fold kernel forced in turn (DPZ_FOLD_KIND 1: classic hit-chain / phase, 2: 4-slot
     group, 4: the walk fold) on sparse groups and on groups with dense (full-share) payloads,
     bit-exact vs the oracle with and without the self term and with a zero base; a kind that
@@ -361,7 +361,7 @@ def test_fold_kinds_forced(dev, monkeypatch, kind, n, alpha, npay, ndense):
 @pytest.mark.parametrize("kind", ["4"])
 @pytest.mark.parametrize("dist", ["3", "1"])
 @pytest.mark.parametrize("alpha", [0.1, 0.3])
-def test_walk_fold_unaligned_views(dev, monkeypatch, kind, dist, alpha):
+def test_walk_fold_unaligned_views(dev, diag_lib, monkeypatch, kind, dist, alpha):
     """The walk fold's scalar-load build (local / out 4 bytes off a 16-byte boundary), 16
     payloads' windows issued three groups ahead (DPZ_FOLD_DIST 3, the default) and one."""
     monkeypatch.setenv("DPZ_FOLD_KIND", kind)
@@ -387,7 +387,7 @@ def test_walk_fold_unaligned_views(dev, monkeypatch, kind, dist, alpha):
 
 @pytest.mark.parametrize("win,epl,alpha", [("128", "16", 0.2), ("128", "8", 0.3), ("128", "16", 0.12),
                                            ("64", "16", 0.1), ("128", "2", 0.05)])
-def test_walk_fold_windows_overflow(dev, monkeypatch, win, epl, alpha):
+def test_walk_fold_windows_overflow(dev, diag_lib, monkeypatch, win, epl, alpha):
     """The walk fold of 16 payloads with 64- / 128-entry windows forced onto tiles whose entries
     overflow them (the synchronous extra windows after a full 128-entry window) and onto sparse
     tiles, bit-exact vs the oracle."""
@@ -416,7 +416,7 @@ def test_walk_fold_windows_overflow(dev, monkeypatch, win, epl, alpha):
 
 @pytest.mark.parametrize("group", ["0", "1"])
 @pytest.mark.parametrize("alpha", [0.01, 0.1])
-def test_fold_unaligned_views(dev, monkeypatch, group, alpha):
+def test_fold_unaligned_views(dev, diag_lib, monkeypatch, group, alpha):
     """local / out 4 bytes off a 16-byte boundary: the scalar-load (VEC = false) builds of the
     hit-chain, phase and slotted fold kernels, bit-exact."""
     monkeypatch.setenv("DPZ_FOLD_GROUP", group)
@@ -666,7 +666,7 @@ def test_split_stream_tail_enqueue(dev, n, alpha):
     (300_000, 0.2, 500_000, 5_000, None),                   # exact path: decode runs on its own
     (1_000_003, 0.01, 1000, 0, None),                        # empty payload: plain copy
 ])
-def test_encode_with_coscheduled_replace(dev, n, alpha, rn, rk, shares, monkeypatch):
+def test_encode_with_coscheduled_replace(dev, n, alpha, rn, rk, shares, monkeypatch, diag_lib):
     """dpz_topk_encode_replace == dpz_topk_encode + an independent replace decode, bit-exact,
     for any split of the decode's chunks over the encoder's launches (DPZ_COSCHED)."""
     codec = _codec()
@@ -716,7 +716,7 @@ def test_coscheduled_replace_rejects_aliasing(dev):
     (11_000_000, 0.01, 5, True, None),             # far fewer entries than wave segments
     (11_000_000, 0.01, 110_000, True, "cluster"),  # entries packed at both ends: long gaps
 ])
-def test_encode_with_fused_replace(dev, n, alpha, rk, dup, layout, where, monkeypatch):
+def test_encode_with_fused_replace(dev, n, alpha, rk, dup, layout, where, monkeypatch, diag_lib):
     """Decoding over the tensor being encoded (co_replace local is x): the encoder's filter
     writes out = x as it streams x and the select launch (or, DPZ_SCATTER_AT=compact, the
     compact launch) scatters the entries (dpz_topk_encode_replace); equals encode +
@@ -836,7 +836,7 @@ def test_shared_and_lone_filter_grids_agree(dev, n, alpha):
 @pytest.mark.parametrize("n,alpha,mode", [(3_000_017, 0.01, otopk.ACC_NONE),
                                           (3_000_017, 0.1, otopk.ACC_ADD),
                                           (1_000_003, 0.3, otopk.ACC_ACCUMULATE)])
-def test_counter_update_forms_agree(dev, monkeypatch, plain, n, alpha, mode):
+def test_counter_update_forms_agree(dev, diag_lib, monkeypatch, plain, n, alpha, mode):
     """The compact's counter update as memory-side atomics (DPZ_COUNTER_PLAIN=0) and as gathered
     read + plain store (=1, the dense-alpha default) both give counter[idx] += 1 on a counter
     that already holds counts, with the accumulator rewound, bit-exact vs the oracle."""

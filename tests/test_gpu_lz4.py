@@ -22,7 +22,7 @@ def _dev_bytes(b, dev):
 
 @pytest.mark.parametrize("par", ["1", "0"])
 @pytest.mark.parametrize("name", list(_cases()))
-def test_device_frames_decode_with_liblz4(dev, name, par, monkeypatch):
+def test_device_frames_decode_with_liblz4(dev, name, par, monkeypatch, diag_lib):
     """par 1: independent blocks that decode to <= 4 KB take the parallel decoder (parse, then
     pointer jumping); par 0: the sequential decoder for every block (DPZ_LZ4_PAR=0)."""
     monkeypatch.setenv("DPZ_LZ4_PAR", par)
