@@ -41,7 +41,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-extra", action="store_true",
                    help="skip the 64 MiB secondary line and the C4 gossip-round object")
-    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "e2e", "shard", "fft", "wire"],
+    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "e2e", "shard", "fft", "wire",
+                                          "plugin"],
                    default="c2",
                    help="c2: one node's 11M tensor per GPU (default); c4: the 96-node gossip "
                         "round of eval/96_regular.edges sharded over the GPUs; c3: JWINS wavelet "
@@ -537,9 +538,12 @@ def main():
             }), flush=True)
         _finish(dist)
         return
-    if args.workload in ("c3", "c5", "e2e", "shard", "fft", "wire"):
+    if args.workload in ("c3", "c5", "e2e", "shard", "fft", "wire", "plugin"):
         import bench_workloads as bw
-        if args.workload == "fft":
+        if args.workload == "plugin":
+            r = [bw.plugin_case(dev, "partial", cpu_rounds=0 if args.no_cpu else 1),
+                 bw.plugin_case(dev, "jwins")]
+        elif args.workload == "fft":
             r = bw.fft_case(dev, steps=min(args.steps, 30))
         elif args.workload == "wire":
             r = bw.wire_case(dev)

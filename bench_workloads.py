@@ -169,7 +169,8 @@ def c3_round_case(dev, rank, world, dist, n=25_000_000, rounds=10, warmup=2, see
 
 def c5_case(dev, n=67_108_864, alpha=0.001, steps=40, warmup=5, seed=5, streams=3):
     """C5: 256 MiB fp32 tensor, 0.1 % top-k, payload values packed to fp16 (RNE, torch.half
-    semantics): encode = top-k + fp16 pack; decode = fp16 unpack + replace.  B = 16N + 12k."""
+    semantics) by the encode itself (DPZ_TOPK_VAL_FP16: compact writes the fp16 words, no
+    packing launch); decode = fp16 unpack + replace.  B = 16N + 12k."""
     from decentralizepy_amd import codec
     k = round(alpha * n)
     per_set = 4 * n * 4 + 10 * k
@@ -182,7 +183,6 @@ def c5_case(dev, n=67_108_864, alpha=0.001, steps=40, warmup=5, seed=5, streams=
         sets.append(dict(x=x, x0=x - 0.01 * torch.randn(n, device=dev, generator=g),
                          cnt=torch.zeros(n, dtype=torch.int32, device=dev),
                          idx=torch.empty(k, dtype=torch.int32, device=dev),
-                         val=torch.empty(k, device=dev),
                          h=torch.empty(k, dtype=torch.float16, device=dev),
                          v32=torch.empty(k, device=dev), out=torch.empty(n, device=dev)))
     S = [torch.cuda.Stream(dev) for _ in range(streams)]
@@ -190,8 +190,7 @@ def c5_case(dev, n=67_108_864, alpha=0.001, steps=40, warmup=5, seed=5, streams=
 
     def step_on(d, ws):
         codec.topk_encode(d["x"], k, x0=d["x0"], counter=d["cnt"], idx_out=d["idx"],
-                          val_out=d["val"], workspace=ws, asynchronous=True)
-        codec.pack_fp16(d["val"], out=d["h"])
+                          val_out=d["h"], workspace=ws, asynchronous=True, val_fp16=True)
         codec.unpack_fp16(d["h"], out=d["v32"])
         codec.replace(d["x0"], d["idx"], d["v32"], out=d["out"], workspace=ws)
 
@@ -277,11 +276,14 @@ def e2e_case(dev, n, alpha, fp16=False, steps=20, warmup=3, seed=7, streams=3):
                 concurrent_pcie_GBps=pcie / t_multi / 1e9, streams=streams)
 
 
-def shard_case(dev, rank, world, dist, n=67_108_864, alpha=0.001, steps=20, warmup=3, seed=9):
-    """One tensor of N parameters sharded over the ranks (SURVEY §8e, C5 on 8 GPUs): the global
-    top-k with one all-gather of every rank's k candidates (decentralizepy_amd/shard.py), then
-    each rank decodes the global payload into its own slice (replace; indices outside the slice
-    fall outside [0, n_r) and are skipped).  Strong scaling: N fixed, value = N params / time."""
+def shard_case(dev, rank, world, dist, n=67_108_864, alpha=0.001, steps=20, warmup=3, seed=9,
+               fp16=True):
+    """One tensor of N parameters sharded over the ranks (BASELINE config 5: 256 MiB
+    on 8 GPUs, 0.1 % top-k, fp16 value packing): the global top-k with one all-gather of every
+    rank's k candidates (decentralizepy_amd/shard.py; with ``fp16`` the local encodes write fp16
+    values themselves and the candidates travel as 10 bytes), then each rank decodes the global
+    payload into its own slice (fp16 unpack + replace; indices outside the slice fall outside
+    [0, n_r) and are skipped).  Strong scaling: N fixed, value = N params / time."""
     from decentralizepy_amd import codec
     from decentralizepy_amd.shard import HipShardOps, sharded_replace, sharded_topk_encode
     k = round(alpha * n)
@@ -301,7 +303,10 @@ def shard_case(dev, rank, world, dist, n=67_108_864, alpha=0.001, steps=20, warm
 
     def step(i):
         d = sets[i % R]
-        idx, val = sharded_topk_encode(d["x"], d["x0"], k, lo, counter=d["cnt"], ops=ops)
+        idx, val = sharded_topk_encode(d["x"], d["x0"], k, lo, counter=d["cnt"], ops=ops,
+                                       val_fp16=fp16)
+        if fp16:
+            val = codec.unpack_fp16(val)
         sharded_replace(d["x0"], lo, idx, val, out=d["out"], ops=ops)
 
     for i in range(warmup):
@@ -320,7 +325,8 @@ def shard_case(dev, rank, world, dist, n=67_108_864, alpha=0.001, steps=20, warm
         tt = torch.tensor([t], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
-    return dict(workload=f"one N={n} tensor sharded over {world} GPU(s), alpha={alpha}: sharded "
+    return dict(workload=f"one N={n} tensor sharded over {world} GPU(s), alpha={alpha}"
+                         f"{', fp16 values written by the encode' if fp16 else ''}: sharded "
                          f"top-k (one all-gather of {world} x {k} candidates) + slice decode",
                 n=n, k=k, world=world, value=4 * n / t / 2 ** 30, ms_per_step=t * 1e3,
                 scaling="strong")
@@ -410,6 +416,17 @@ def wire_case(dev, n=11_000_000, alpha=0.01, reps=30, seed=13):
     res = {"k": k, "raw_idx_bytes": 4 * k, "raw_val_bytes": 4 * k}
     el, t = timed(lambda: codec.elias_encode(idx, workspace=ws))
     res["elias"] = {"bytes": int(el.numel()), "encode_us": round(t, 1)}
+    # decode = what the receiving plugin runs: the host stream (from pickle) up to the device and
+    # decoded into int32 indices there (compression/Elias.py decompress_device)
+    from decentralizepy_amd.compression.Elias import Elias
+    el_host = el.cpu().numpy()
+    E = Elias()
+    E._dev(dev)
+    dec, t = timed(lambda: E.decompress_device(el_host, device=dev))
+    assert torch.equal(dec, idx)
+    res["elias"]["decode_us"] = round(t, 1)
+    res["elias"]["decode_note"] = ("host bytes -> device int32 indices, H2D included "
+                                   "(Elias.decompress_device)")
     gaps = codec.delta_i32(idx)
     fr, t = timed(lambda: codec.lz4_compress(gaps.view(torch.uint8), workspace=ws))
     frame = fr.cpu().numpy().tobytes()
@@ -445,4 +462,217 @@ def wire_case(dev, n=11_000_000, alpha=0.01, reps=30, seed=13):
                                "decode_us": round(tdc, 1), "decompress_us": round(tfc, 1)}
     except OSError:
         pass
+    # the reference's own Elias decode (compression/Elias.py:54-97: a pure-Python walk over the
+    # codes), restated in oracle/elias.py and timed on one host thread (cpu_baseline leg)
+    from oracle import elias as oelias
+    t0 = time.perf_counter()
+    ref = oelias.decode(el_host)
+    res["elias"]["cpu_reference_decode_us"] = round((time.perf_counter() - t0) * 1e6, 1)
+    t0 = time.perf_counter()
+    oelias.encode(idx.cpu().numpy())
+    res["elias"]["cpu_reference_encode_us"] = round((time.perf_counter() - t0) * 1e6, 1)
+    assert np.array_equal(ref, idx.cpu().numpy().astype(np.int64))
     return res
+
+
+# ---- the drop-in plugins' round, host to host ------------------------------------------------------
+class _Mapping:
+    """The Node's mapping as the plugins use it (get_uid only)."""
+
+    def get_uid(self, rank, machine_id):
+        return machine_id * 16 + rank
+
+
+class _Graph:
+    """A degree-3 neighbourhood (the regular topologies of the tutorial / eval configs)."""
+
+    def __init__(self, nbrs):
+        self.nbrs = set(nbrs)
+
+    def neighbors(self, uid):
+        return self.nbrs
+
+
+def _net(n, seed):
+    """An n-parameter fp32 model on the host (a weight matrix + a bias vector), with the codec
+    fields the reference Model carries (models/Model.py:15-25)."""
+    cols = 2048
+    rows = n // cols
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            g = torch.Generator().manual_seed(seed)
+            self.weight = torch.nn.Parameter(torch.randn(rows, cols, generator=g))
+            self.bias = torch.nn.Parameter(torch.randn(n - rows * cols, generator=g))
+            self.model_change = None
+            self.accumulated_changes = None
+            self.shared_parameters_counter = None
+
+    return Net()
+
+
+def _perturb(model, g, scale=0.01):
+    """The training step's effect on the parameters (excluded from every timed region)."""
+    with torch.no_grad():
+        for p in model.parameters():
+            p.add_(scale * torch.randn(p.shape, generator=g))
+
+
+def plugin_case(dev, kind="partial", rounds=6, warmup=2, seed=17, cpu_rounds=1, tmpdir=None):
+    """One node's gossip round through the drop-in classes, host memory to host memory, as
+    node/DPSGDNode.py:72-115 drives them: ``get_data_to_send(degree=3)`` (state_dict -> pinned H2D
+    -> device encode -> device Elias (+ float codec) -> D2H -> the wire dict), the TCP wire
+    (``pickle.dumps`` / ``pickle.loads``, communication/TCP.py:110-232), and ``_averaging`` of three
+    neighbours' payloads (H2D of the received legs, device decode, Metro-Hastings fold, D2H of the
+    averaged model, ``load_state_dict``).  The neighbours' messages are produced by three more
+    plugin instances before the timed rounds (other processes in a real run).
+
+    kind "partial": PartialModel, alpha 0.01, Elias (C2: N = 11 M).  kind "jwins": the JWINS
+    tutorial [SHARING] (sym2 level 4, alpha list, accumulation, EliasFpzip) at N = 25 M.
+
+    cpu_baseline (partial only): the reference's own op sequence for the same round on the host
+    (oracle/ref_ops.py: cat, sub, abs, std_mean, topk, sort, counter, gather; the reference
+    Elias encode / decode restated in oracle/elias.py — the decode is the reference's pure-Python
+    code walk, compression/Elias.py:54-97; deserialized_model's cat + index_put per payload, the
+    MH fold, load_state_dict) on torch's CPU threads."""
+    import os
+    import pickle
+    import tempfile
+    from collections import deque
+
+    import numpy as np
+
+    from decentralizepy_amd.sharing.JWINS.JWINS import JWINS
+    from decentralizepy_amd.sharing.PartialModel import PartialModel
+
+    tmpdir = tmpdir or tempfile.mkdtemp(prefix="dpz_plugin_")
+    if kind == "partial":
+        n = 11_000_000
+        cls = PartialModel
+        kw = dict(alpha=0.01, compress=True, compression_class="Elias",
+                  compression_package="decentralizepy_amd.compression.Elias")
+    else:
+        n = 25_000_000
+        cls = JWINS
+        kw = dict(change_based_selection=True, alpha_list="[0.1,0.15,0.2,0.25,0.3,0.4,1.0]",
+                  wavelet="sym2", level=4, accumulation=True, accumulate_averaging_changes=True,
+                  metadata_cap=0.5, compress=True, compression_class="EliasFpzip",
+                  compression_package="decentralizepy_amd.compression.EliasFpzip")
+    nbr_uids = [1, 2, 3]
+    models = [_net(n, seed + i) for i in range(4)]
+    plugins = [cls(i, 0, None, _Mapping(), _Graph([u for u in range(4) if u != i]), models[i],
+                   None, tmpdir, **kw) for i in range(4)]
+    g = torch.Generator().manual_seed(seed + 100)
+    node, nmodel = plugins[0], models[0]
+
+    def neighbour_wires():
+        wires = []
+        for i in nbr_uids:
+            _perturb(models[i], g)
+            d = plugins[i].get_data_to_send(degree=3)
+            d["CHANNEL"] = "DPSGD"
+            wires.append(pickle.dumps(d))
+        return wires
+
+    t_send, t_recv, out_bytes, in_bytes = [], [], 0, 0
+    for r in range(warmup + rounds):
+        wires = neighbour_wires()  # the neighbours' round (not this node's work)
+        _perturb(nmodel, g)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        data = node.get_data_to_send(degree=3)
+        data["CHANNEL"] = "DPSGD"
+        wire = pickle.dumps(data)
+        t1 = time.perf_counter()
+        peer = {u: deque([pickle.loads(w)]) for u, w in zip(nbr_uids, wires)}
+        node._averaging(peer)
+        t2 = time.perf_counter()
+        if r >= warmup:
+            t_send.append(t1 - t0)
+            t_recv.append(t2 - t1)
+            out_bytes = len(wire)
+            in_bytes = sum(len(w) for w in wires)
+    send_ms = 1e3 * float(np.median(t_send))
+    recv_ms = 1e3 * float(np.median(t_recv))
+    # the PCIe legs of the round, timed alone with pinned buffers: the flat model up (4N), the
+    # averaged model down (4N), and the payload legs (~ the wire bytes) each way
+    a = torch.empty(n, dtype=torch.float32).pin_memory()
+    b = torch.empty(n, dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        b.copy_(a, non_blocking=True)
+        torch.cuda.synchronize()
+        a.copy_(b, non_blocking=True)
+        torch.cuda.synchronize()
+    pcie_model_ms = (time.perf_counter() - t0) / 5 * 1e3
+    del a, b
+    res = {"kind": kind, "n": n, "class": cls.__name__,
+           "compression": kw["compression_class"], "rounds": rounds,
+           "round_ms": round(send_ms + recv_ms, 3), "send_ms": round(send_ms, 3),
+           "receive_ms": round(recv_ms, 3), "wire_out_bytes": out_bytes,
+           "wire_in_bytes": in_bytes,
+           "pcie_model_up_down_ms": round(pcie_model_ms, 3),
+           "pcie_model_share": round(pcie_model_ms / (send_ms + recv_ms), 3),
+           "GiBps_params": round(4 * n / ((send_ms + recv_ms) * 1e-3) / 2 ** 30, 3)}
+    del plugins, node, models, nmodel
+    torch.cuda.empty_cache()
+    if kind == "partial" and cpu_rounds > 0:
+        res["cpu_baseline"] = _plugin_cpu_round(n, 0.01, cpu_rounds, seed)
+    return res
+
+
+def _plugin_cpu_round(n, alpha, rounds, seed):
+    """The reference's op sequence for the same node round on the host's CPU threads (test
+    infrastructure: oracle/ref_ops.py and oracle/elias.py, imported here only as the baseline)."""
+    import pickle
+
+    import numpy as np
+
+    from oracle import elias as oelias
+    from oracle import ref_ops
+    gen = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, generator=gen)
+    x0 = x - 0.01 * torch.randn(n, generator=gen)
+    counter = torch.zeros(n, dtype=torch.int32)
+    k = round(alpha * n)
+    wires = []
+    for j in range(3):
+        idx = np.sort(np.random.default_rng(seed + j).choice(n, size=k, replace=False))
+        d = {"alpha": alpha, "indices": oelias.encode(idx.astype(np.int32)),
+             "params": np.random.default_rng(seed + 10 + j).standard_normal(k).astype(np.float32),
+             "send_partial": True, "degree": 3, "iteration": 0, "CHANNEL": "DPSGD"}
+        wires.append(pickle.dumps(d))
+    times = {"send": [], "receive": [], "elias_decode": []}
+    for _ in range(rounds):
+        t0 = time.perf_counter()
+        idx, vals = ref_ops.encode(x, x0, alpha, counter)          # PartialModel.py:164-246
+        msg = {"alpha": alpha, "indices": oelias.encode(idx), "params": vals,
+               "send_partial": True, "degree": 3, "iteration": 0}  # Elias.py:20-52
+        pickle.dumps(msg)
+        t1 = time.perf_counter()
+        total = None
+        te = 0.0
+        for w in wires:                                            # Sharing.py:156-190
+            d = pickle.loads(w)
+            t2 = time.perf_counter()
+            ind = oelias.decode(d["indices"])                      # Elias.py:54-97
+            te += time.perf_counter() - t2
+            t_ = ref_ops.decode(x, ind, d["params"])               # PartialModel.py:257-303
+            term = t_ * (1 / 4)
+            total = term if total is None else total + term
+        total += (1 - 3 / 4) * x
+        x0 = total.clone()                                         # load_state_dict / _post_step
+        t3 = time.perf_counter()
+        times["send"].append(t1 - t0)
+        times["receive"].append(t3 - t1)
+        times["elias_decode"].append(te / 3)
+    med = {kk: 1e3 * float(np.median(v)) for kk, v in times.items()}
+    return {"kind": "port", "cores": torch.get_num_threads(),
+            "round_ms": round(med["send"] + med["receive"], 2), "send_ms": round(med["send"], 2),
+            "receive_ms": round(med["receive"], 2),
+            "elias_decode_ms_per_payload": round(med["elias_decode"], 2),
+            "sample": f"{rounds} round(s) of the reference op sequence at N={n}, 3 payloads, "
+                      f"{torch.get_num_threads()} torch threads; the Elias decode is the "
+                      "reference's pure-Python code walk (oracle/elias.py)"}

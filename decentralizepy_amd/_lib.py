@@ -24,6 +24,7 @@ DPZ_TOPK_ASYNC = 0x2
 DPZ_TOPK_STREAM = 0x4
 DPZ_TOPK_TAIL = 0x8
 DPZ_TOPK_SHARED = 0x10
+DPZ_TOPK_VAL_FP16 = 0x20
 DPZ_FOLD_SELF = 0x1
 DPZ_FOLD_REPLACE_ONLY = 0x2
 DPZ_FOLD_ZERO_BASE = 0x4
@@ -75,6 +76,7 @@ SIGNATURES = {
     "dpz_gather_change": (_int, [_c_void_p, _c_void_p, _i64, _c_void_p, _i64, _c_void_p,
                                  _c_void_p]),
     "dpz_gather_u32": (_int, [_c_void_p, _i64, _c_void_p, _i64, _c_void_p, _c_void_p]),
+    "dpz_gather_u16": (_int, [_c_void_p, _i64, _c_void_p, _i64, _c_void_p, _c_void_p]),
     "dpz_scatter_add_i32": (_int, [_c_void_p, _i64, _c_void_p, _i64, _i64, ctypes.c_int32,
                                    _c_void_p]),
     "dpz_topk_complete": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64, _i64,

@@ -82,7 +82,8 @@ class Workspace:
 
 def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, counter=None,
                 idx_out=None, val_out=None, workspace=None, exact=False, asynchronous=False,
-                phase=None, co_replace=None, status_out=None, shared=False, fold_base=None):
+                phase=None, co_replace=None, status_out=None, shared=False, fold_base=None,
+                val_fp16=False):
     """Top-k magnitude encode (reference PartialModel.py:164-255 / Wavelet.py:142-197).
 
     Returns ``(idx int32[k], val fp32[k])`` in ascending index order.  Mutates ``acc`` and
@@ -102,6 +103,8 @@ def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, c
     Metro-Hastings fold over x with those weights into ``base_out`` (dpz_topk_encode_foldbase;
     the filter writes it as it streams x), for a later ``decode_average(x, payloads, weights,
     w_self, out=base_out, base_ready=True)``.
+    ``val_fp16``: the values are written as fp16 (round to nearest even, ``torch.half``), by the
+    encode itself (DPZ_TOPK_VAL_FP16: the C5 payload's value packing); ``val`` is float16[k].
     """
     _require(x, torch.float32, "x")
     _require(x0, torch.float32, "x0")
@@ -114,11 +117,16 @@ def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, c
     _require(vals_src, torch.float32, "vals_src")
     if idx_out is None:
         idx_out = torch.empty(k, dtype=torch.int32, device=x.device)
+    vdt = torch.float16 if val_fp16 else torch.float32
     if val_out is None:
-        val_out = torch.empty(k, dtype=torch.float32, device=x.device)
+        val_out = torch.empty(k, dtype=vdt, device=x.device)
+    _require(val_out, vdt, "val_out")
+    if val_fp16 and (co_replace is not None or fold_base is not None):
+        raise ValueError("val_fp16: a plain encode (no co_replace / fold_base)")
     ws = (workspace or Workspace(x.device)).get(n, k)
     flags = ((DPZ_TOPK_EXACT if exact else 0) | (DPZ_TOPK_ASYNC if asynchronous else 0)
-             | (_lib.DPZ_TOPK_SHARED if shared else 0))
+             | (_lib.DPZ_TOPK_SHARED if shared else 0)
+             | (_lib.DPZ_TOPK_VAL_FP16 if val_fp16 else 0))
     if phase is not None:
         flags |= {"stream": DPZ_TOPK_STREAM, "tail": DPZ_TOPK_TAIL}[phase]
     if fold_base is not None:
@@ -144,7 +152,8 @@ def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, c
                                                _ptr(vals_src), n, k, _ptr(idx_out), _ptr(val_out),
                                                _ptr(counter), _ptr(ws), ws.numel(),
                                                _ptr(status_out),
-                                               _lib.DPZ_TOPK_SHARED if shared else 0,
+                                               (_lib.DPZ_TOPK_SHARED if shared else 0)
+                                               | (_lib.DPZ_TOPK_VAL_FP16 if val_fp16 else 0),
                                                _stream(x.device))
         check(rc, "dpz_topk_encode_status")
         return idx_out, val_out

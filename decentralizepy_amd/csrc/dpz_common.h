@@ -100,6 +100,17 @@ __host__ __device__ __forceinline__ bool aligned16(const void* p) {
   return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
 }
 
+// A payload value as stored: fp32, or (DPZ_TOPK_VAL_FP16) fp16 rounded to nearest even, the
+// torch.Tensor.half() conversion (overflow -> inf, NaN stays NaN), in the same slot order.
+__device__ __forceinline__ void store_val(float* val_out, int val_h, int64_t pos, float v) {
+  if (val_h) {
+    const _Float16 h = (_Float16)v;
+    reinterpret_cast<uint16_t*>(val_out)[pos] = __builtin_bit_cast(uint16_t, h);
+  } else {
+    val_out[pos] = v;
+  }
+}
+
 // The Metro-Hastings fold's value at an element no payload hits (every term is the local value
 // x): fl(...fl(fl(x*w[0]) + fl(x*w[1])) ... + fl(x*ws)), the reference's fp32 order
 // (sharing/Sharing.py:156-190; the library is compiled with -ffp-contract=off).  Written by the

@@ -127,6 +127,16 @@ __global__ void __launch_bounds__(256) gather_u32_kernel(const uint32_t* src, in
   }
 }
 
+// out[j] = src[pos[j]] for 16-bit words (bit copy)
+__global__ void __launch_bounds__(256) gather_u16_kernel(const uint16_t* src, int64_t m,
+                                                         const int32_t* pos, int64_t k,
+                                                         uint16_t* out) {
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < k; j += (int64_t)gridDim.x * 256) {
+    const int64_t p = pos[j];
+    out[j] = (p >= 0 && p < m) ? src[p] : (uint16_t)0;
+  }
+}
+
 // dst[idx[j] - offset] += value for idx[j] in [offset, offset + n)
 __global__ void __launch_bounds__(256) scatter_add_i32_kernel(int32_t* dst, int64_t n,
                                                               const int32_t* idx, int64_t k,
@@ -163,6 +173,17 @@ extern "C" int dpz_gather_u32(const void* src, int64_t m, const int32_t* pos, in
   hipStream_t st = static_cast<hipStream_t>(stream);
   gather_u32_kernel<<<small_grid(k), 256, 0, st>>>(static_cast<const uint32_t*>(src), m, pos, k,
                                                    static_cast<uint32_t*>(out));
+  DPZ_LAUNCH_CHECK();
+  return DPZ_OK;
+}
+
+extern "C" int dpz_gather_u16(const void* src, int64_t m, const int32_t* pos, int64_t k,
+                              void* out, dpz_stream_t stream) {
+  if (m < 0 || k < 0 || (k > 0 && (!src || !pos || !out))) return DPZ_ERR_ARG;
+  if (k == 0) return DPZ_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  gather_u16_kernel<<<small_grid(k), 256, 0, st>>>(static_cast<const uint16_t*>(src), m, pos, k,
+                                                   static_cast<uint16_t*>(out));
   DPZ_LAUNCH_CHECK();
   return DPZ_OK;
 }

@@ -1657,14 +1657,15 @@ int launch_fold_base(const float* x, int64_t n, const FoldBase& fb, float* out, 
 // out already holds the fold of every element's local value alone (FoldBase::of, written by the
 // encoder's filter); an element hit by one or more payloads is folded here exactly, in the
 // reference's order (payload terms in payload order, then the self term).  Block b owns the
-// element range [b R, (b + 1) R) (R from the payloads' density, ~1024 entries per block): the
-// payloads' runs of the range are found by lock-step searches (one wave per four payloads, lower
-// bounds of both ends), staged in LDS, and each entry whose element no EARLIER payload hits (an
-// LDS binary search per earlier run) folds that element: the local value gathered once, the
-// later payloads' values by LDS binary search.  A range whose runs exceed the LDS stage is
-// processed in halves (adversarially clustered payloads; always terminates: one element holds
-// <= 16 entries).  Bytes: the payload entries, a local gather and an out write per hit element.
-constexpr int PT_CAP = 4096;  // entries staged per pass (32 KB of LDS)
+// 4096-element tile b: its payload runs come from fold_offsets_kernel's tile starts (one coalesced
+// pre-pass over the payload indices, so a block's chain is starts -> entries -> local gather ->
+// store), staged in LDS, and each entry whose element no EARLIER payload hits (an LDS binary
+// search per earlier run) folds that element: the local value gathered once, the later payloads'
+// values by LDS binary search.  A tile whose runs exceed the LDS stage is processed in halves,
+// the sub-ranges' runs found by lock-step searches (adversarially clustered payloads; always
+// terminates: one element holds <= 16 entries).  Bytes: the payload entries, a local gather and
+// an out write per hit element.
+constexpr int PT_CAP = 1024;  // entries staged per pass (8 KB of LDS: 8 blocks per CU)
 constexpr int PT_EPT = PT_CAP / 256;
 
 __device__ __forceinline__ int pt_find(const int32_t* sidx, int b, int e, int32_t key) {
@@ -1680,6 +1681,7 @@ __device__ __forceinline__ int pt_find(const int32_t* sidx, int b, int e, int32_
 }
 
 __global__ void __launch_bounds__(256) fold_patch_kernel(FoldArgs a, int64_t range) {
+  // range == FOLD_TILE: the first pass takes its runs from a.starts (fold_offsets_kernel)
   __shared__ int32_t s_idx[PT_CAP];
   __shared__ float s_val[PT_CAP];
   __shared__ int32_t s_rlo[FOLD_MAXP], s_rhi[FOLD_MAXP], s_off[FOLD_MAXP + 1];
@@ -1689,11 +1691,18 @@ __global__ void __launch_bounds__(256) fold_patch_kernel(FoldArgs a, int64_t ran
   const int64_t b_lo = (int64_t)blockIdx.x * range;
   const int64_t b_hi = b_lo + range < n ? b_lo + range : n;
   int64_t cur = b_lo, len = b_hi - b_lo;
+  bool from_starts = a.starts != nullptr;
   while (cur < b_hi) {
     const int64_t s_end = cur + len < b_hi ? cur + len : b_hi;
+    if (from_starts) {  // the whole tile: runs from the pre-pass
+      if (t < np) {
+        const int32_t* st = a.starts + (int64_t)t * (a.ntiles + 1);
+        s_rlo[t] = st[blockIdx.x];
+        s_rhi[t] = st[blockIdx.x + 1];
+      }
+    } else {
     // runs of [cur, s_end): wave w searches payloads w, w + 4, w + 8, w + 12, both ends, in lock
     // step (virtual search q: payload w + 4 (q & 3), target q < 4 ? cur : s_end)
-    {
       const int32_t lo32 = (int32_t)cur, hi32 = (int32_t)s_end;
       const int32_t r = fw_lower_bounds_t<8>(
           8, [&](int q) { return q < 4 ? lo32 : hi32; }, lane,
@@ -1711,6 +1720,7 @@ __global__ void __launch_bounds__(256) fold_patch_kernel(FoldArgs a, int64_t ran
         }
       }
     }
+    from_starts = false;
     __syncthreads();
     if (t == 0) {
       int32_t o = 0;
@@ -1786,20 +1796,19 @@ __global__ void __launch_bounds__(256) fold_patch_kernel(FoldArgs a, int64_t ran
   }
 }
 
-static int launch_fold_patch(const FoldArgs& fa, hipStream_t st) {
-  int64_t etot = 0;
-  for (int i = 0; i < fa.np; ++i) etot += fa.p[i].k;
+static int launch_fold_patch(FoldArgs fa, int32_t* starts, hipStream_t st) {
+  int64_t etot = 0, kmax = 0;
+  for (int i = 0; i < fa.np; ++i) {
+    etot += fa.p[i].k;
+    if (fa.p[i].k > kmax) kmax = fa.p[i].k;
+  }
   if (etot == 0) return DPZ_OK;
-  // ~1024 entries per block on average (a quarter of the stage), at least ~2048 blocks' worth of
-  // parallelism when the payloads are sparse
-  const double dens = (double)etot / (double)fa.n;
-  int64_t range = (int64_t)(1024.0 / dens);
-  const int64_t par = (fa.n + 2047) / 2048;
-  if (range > par) range = par;
-  if (range < 256) range = 256;
-  range = (range + 63) & ~int64_t(63);
-  const int64_t nb = (fa.n + range - 1) / range;
-  DPZ_TIMED(DPZ_KT_FOLD, st, fold_patch_kernel<<<(unsigned)nb, 256, 0, st>>>(fa, range));
+  fa.ntiles = fold_ntiles(fa.n);
+  dim3 og((unsigned)((kmax + 1 + 1023) / 1024), (unsigned)fa.np);
+  DPZ_TIMED(DPZ_KT_FOLD_OFFSETS, st,
+            fold_offsets_kernel<FOLD_TILE_SHIFT><<<og, 256, 0, st>>>(fa, starts, fa.ntiles));
+  fa.starts = starts;
+  DPZ_TIMED(DPZ_KT_FOLD, st, fold_patch_kernel<<<(unsigned)fa.ntiles, 256, 0, st>>>(fa, FOLD_TILE));
   return DPZ_OK;
 }
 
@@ -1863,7 +1872,7 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
       fa.p[i].k = k[i];
       fa.p[i].w = w[i];
     }
-    return launch_fold_patch(fa, st);
+    return launch_fold_patch(fa, static_cast<int32_t*>(ws), st);
   }
   bool vec = ((reinterpret_cast<uintptr_t>(local) | reinterpret_cast<uintptr_t>(out)) & 15u) == 0;
   for (int i = 0; i < n_payloads; ++i)

@@ -118,7 +118,9 @@ struct TopkCtrl {
   uint32_t T, icut;        // final threshold key / last selected index among key == T
   uint32_t sticky;         // OR of every sampled call's final status since the caller cleared it
                            // (dpz_topk_sticky_status): misses of ASYNC calls never completed
-  uint32_t pad[52];
+  uint32_t val_h;          // sampled path: the call's value format (1 = fp16), for the exact
+                           // re-run dpz_topk_complete makes after a miss
+  uint32_t pad[51];
 };
 static_assert(sizeof(TopkCtrl) == 256, "ctrl size");
 
@@ -128,7 +130,6 @@ constexpr int EX_HIST_BLOCKS = 1024;
 constexpr int SMP_N = 65536;       // samples
 constexpr int SMP_CHUNK = 64;      // contiguous elements per sample chunk (one wave)
 constexpr int SMP_NCHUNK = SMP_N / SMP_CHUNK;
-constexpr int SMP_BLOCKS = 64;     // 16 chunks per block: 4 waves x 4 rounds
 constexpr int CB_SHIFT = 20;       // coarse bins: key >> 20 (2048 bins, 8 per octave)
 constexpr int CB = 2048;
 #ifndef DPZ_HB
@@ -274,6 +275,7 @@ struct EncodeArgs {
   int32_t* status_out;    // sampled path, ASYNC: compact's block 0 also writes the call's final
                           // status word here (device), or nullptr
   bool shared;            // DPZ_TOPK_SHARED: the filter grid for several codecs per GPU
+  int val_h;              // DPZ_TOPK_VAL_FP16: val_out holds fp16 values (RNE)
   const FoldBase* fbase;  // dpz_topk_encode_foldbase: the pipelined filter also writes
   float* base_out;        // base_out[j] = fbase->of(x[j]) (sampled path, fused_foldbase_ok)
 };
@@ -294,7 +296,8 @@ int run_sampled(const EncodeArgs& a, const WsLayout& L, bool vec, int phases = 3
 int topk_encode_status(const float* x, const float* x0, float* acc, int acc_mode,
                        const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
                        float* val_out, int32_t* counter, void* ws, size_t ws_bytes,
-                       hipStream_t st, int32_t* status_out, bool shared = false);
+                       hipStream_t st, int32_t* status_out, bool shared = false,
+                       bool val_fp16 = false);
 static inline bool use_sampled(int64_t n, int64_t k) {
   return n >= (1 << 18) && k >= 1 && k <= n / 2;
 }

@@ -79,6 +79,7 @@ extern "C" size_t dpz_topk_workspace_bytes(int64_t n, int64_t k) {
 
 static int dpz_topk_dispatch(EncodeArgs a, int flags) {
   if (flags & DPZ_TOPK_SHARED) a.shared = true;
+  if (flags & DPZ_TOPK_VAL_FP16) a.val_h = 1;
   const WsLayout L = ws_layout(a.n, a.k, a.shared);
   const bool vec = all_aligned(a);
   if (a.k == 0) {
@@ -119,20 +120,21 @@ namespace dpz {
 int topk_encode_status(const float* x, const float* x0, float* acc, int acc_mode,
                        const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
                        float* val_out, int32_t* counter, void* ws, size_t ws_bytes,
-                       hipStream_t st, int32_t* status_out, bool shared) {
+                       hipStream_t st, int32_t* status_out, bool shared, bool val_fp16) {
   EncodeArgs a{x, x0, acc, acc_mode, vals_src, n, k, idx_out, val_out, counter,
                static_cast<char*>(ws), st};
   a.shared = shared;
+  a.val_h = val_fp16 ? 1 : 0;
   int rc = validate(a, ws_bytes);
   if (rc != DPZ_OK) return rc;
   if (n == 0 || k == 0 || !use_sampled(n, k)) {  // no sampled tail writes it: status 0
-    if (n > 0) rc = dpz_topk_dispatch(a, DPZ_TOPK_ASYNC);
+    if (n > 0) rc = dpz_topk_dispatch(a, DPZ_TOPK_ASYNC | (val_fp16 ? DPZ_TOPK_VAL_FP16 : 0));
     if (rc != DPZ_OK) return rc;
     if (status_out) DPZ_HIP_TRY(hipMemsetAsync(status_out, 0, sizeof(int32_t), st));
     return DPZ_OK;
   }
   a.status_out = status_out;
-  return dpz_topk_dispatch(a, DPZ_TOPK_ASYNC);
+  return dpz_topk_dispatch(a, DPZ_TOPK_ASYNC | (val_fp16 ? DPZ_TOPK_VAL_FP16 : 0));
 }
 }  // namespace dpz
 
@@ -143,10 +145,10 @@ extern "C" int dpz_topk_encode_status(const float* x, const float* x0, float* ac
                                       int flags, dpz_stream_t stream) {
   if (!status_out) return DPZ_ERR_ARG;
   // only DPZ_TOPK_SHARED applies (the call is asynchronous, sampled-path, unsplit by contract)
-  if (flags & ~DPZ_TOPK_SHARED) return DPZ_ERR_ARG;
+  if (flags & ~(DPZ_TOPK_SHARED | DPZ_TOPK_VAL_FP16)) return DPZ_ERR_ARG;
   return topk_encode_status(x, x0, acc, acc_mode, vals_src, n, k, idx_out, val_out, counter, ws,
                             ws_bytes, static_cast<hipStream_t>(stream), status_out,
-                            (flags & DPZ_TOPK_SHARED) != 0);
+                            (flags & DPZ_TOPK_SHARED) != 0, (flags & DPZ_TOPK_VAL_FP16) != 0);
 }
 
 static bool overlaps(const void* p, size_t pb, const void* q, size_t qb) {
@@ -275,11 +277,11 @@ extern "C" int dpz_topk_complete(const float* x, const float* x0, float* acc, in
   DPZ_HIP_TRY(hipStreamSynchronize(a.st));
   if (n == 0 || k == 0 || !use_sampled(n, k)) return DPZ_OK;
   const WsLayout L = ws_layout(n, k);
-  uint32_t status = 0;
-  DPZ_HIP_TRY(hipMemcpy(&status, a.ws + L.ctrl + offsetof(TopkCtrl, status), sizeof(status),
-                        hipMemcpyDeviceToHost));
-  if (status == 0) return DPZ_OK;
+  TopkCtrl c;
+  DPZ_HIP_TRY(hipMemcpy(&c, a.ws + L.ctrl, sizeof(c), hipMemcpyDeviceToHost));
+  if (c.status == 0) return DPZ_OK;
   if (used_fallback) *used_fallback = 1;
+  a.val_h = c.val_h ? 1 : 0;  // the value format the sampled call was issued with
   // keys are re-derived from the post-filter state: ACCUMULATE already stored acc += change
   const bool vec = all_aligned(a);
   rc = run_exact(a, L, 1, vec);

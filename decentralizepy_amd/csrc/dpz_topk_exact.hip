@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(256) exact_write_kernel(KeySrc s, int64_t n, c
                                                           const float* vals_src, int32_t* idx_out,
                                                           float* val_out, int32_t* counter,
                                                           float* rewind, int64_t k,
-                                                          int keep_ties) {
+                                                          int keep_ties, int val_h) {
   __shared__ uint32_t wsum[16];
   const uint32_t T = ctrl->prefix;
   const uint32_t ties = exact_ties(ctrl, keep_ties);
@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(256) exact_write_kernel(KeySrc s, int64_t n, c
         if (sel && pos < (uint64_t)k) {
           const int64_t i = i0 + e;
           idx_out[pos] = (int32_t)i;
-          val_out[pos] = vals_src[i];
+          store_val(val_out, val_h, pos, vals_src[i]);
           if (counter) counter[i] += 1;
           if (rewind) rewind[i] = 0.0f;
         }
@@ -231,7 +231,7 @@ static int run_exact_t(const EncodeArgs& a, const WsLayout& L, int rekey, int ke
   float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE) ? a.acc : nullptr;
   DPZ_TIMED(DPZ_KT_EXACT_WRITE, a.st, exact_write_kernel<VEC><<<(unsigned)L.ex_nblk, 256, 0, a.st>>>(
       s, a.n, ctrl, boff, beqb, a.vals_src, a.idx_out, a.val_out, a.counter, rewind,
-      keep_ties ? cap : a.k, keep_ties));
+      keep_ties ? cap : a.k, keep_ties, a.val_h));
   return DPZ_OK;
 }
 

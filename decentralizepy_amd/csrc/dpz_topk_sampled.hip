@@ -68,41 +68,47 @@ __device__ __forceinline__ int64_t sample_pos(int c, int lane, int64_t n) {
   return ((int64_t)c * (n - SMP_CHUNK)) / (SMP_NCHUNK - 1) + lane;  // < 2^41: 64-bit is exact
 }
 
-// 64 blocks x 256: 1024 chunks of 64 contiguous elements spread evenly over [0, n).
-__global__ void __launch_bounds__(256) sampled_sample_kernel(KeySrc s, int64_t n, TopkCtrl* ctrl,
-                                                             uint32_t* chist, uint32_t* ghist,
-                                                             uint32_t* blcnt, ReplaceJob pj) {
-  if (blockIdx.x >= SMP_BLOCKS) {  // co-scheduled replace decode (independent work)
-    replace_block(pj, blockIdx.x - SMP_BLOCKS);
+// SMP_NCHUNK / (4 waves-per-block) blocks: 1024 chunks of 64 contiguous elements spread evenly
+// over [0, n), four per wave.  nsb = the sample's own blocks (blockDim 256 or 1024: fewer,
+// larger blocks fold into the global histogram with fewer same-address atomics per bin).
+__global__ void __launch_bounds__(1024) sampled_sample_kernel(KeySrc s, int64_t n, TopkCtrl* ctrl,
+                                                              uint32_t* chist, uint32_t* ghist,
+                                                              uint32_t* blcnt, ReplaceJob pj,
+                                                              int nsb, int val_h) {
+  if ((int)blockIdx.x >= nsb) {  // co-scheduled replace decode (independent work)
+    replace_block(pj, blockIdx.x - nsb);
     return;
   }
   STAMP_MIN(0);
   __shared__ uint32_t h[CB];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nw = (int)(blockDim.x >> 6);
   float v[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int64_t i = sample_pos(blockIdx.x * 16 + wave * 4 + r, lane, n);
+    const int64_t i = sample_pos((blockIdx.x * nw + wave) * 4 + r, lane, n);
     float d = s.x0 ? (s.x[i] - s.x0[i]) : s.x[i];
     if (s.mode != DPZ_ACC_NONE) d = s.acc[i] + d;
     v[r] = d;
   }
-  for (int b = threadIdx.x; b < CB; b += 256) h[b] = 0;
+  for (int b = threadIdx.x; b < CB; b += blockDim.x) h[b] = 0;
   // this call's window histogram copies and boundary sub-list counters start at zero
-  for (int b = blockIdx.x * 256 + threadIdx.x; b < GH_COPIES * GH_STRIDE; b += SMP_BLOCKS * 256)
+  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < GH_COPIES * GH_STRIDE;
+       b += nsb * blockDim.x)
     ghist[b] = 0;
   if (blockIdx.x == 0) {
     if (threadIdx.x < NSUB) blcnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
       ctrl->status = 0;
       ctrl->nbound = 0;
+      ctrl->val_h = (uint32_t)val_h;
     }
   }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < 4; ++r) atomicAdd(&h[key_of(v[r]) >> CB_SHIFT], 1u);
   __syncthreads();
-  for (int b = threadIdx.x; b < CB; b += 256) {
+  for (int b = threadIdx.x; b < CB; b += blockDim.x) {
     const uint32_t c = h[b];
     if (c) atomicAdd(&chist[b], c);
   }
@@ -619,6 +625,7 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
     gh[t] = sum;
     if (t == 0) gh[HB] = suma;
   }
+  STAMP_T0(12);
   if (t < SEL_SEGS / 4) fbabove[t] = 0;
   if (t == 0) lcnt = 0;
   __syncthreads();
@@ -802,6 +809,46 @@ __device__ __forceinline__ void block_resolve(const Bound& bd, uint32_t need, ui
                                               uint32_t shift, ResolveLds& L, uint32_t* T_out,
                                               uint32_t* icut_out) {
   const int t = threadIdx.x;
+  if (bd.nb <= 256u) {
+    // every entry in LDS, at most one per thread: each entry's rank in (key descending, index
+    // ascending) order against all the others (broadcast LDS reads, no barrier in the loop); the
+    // entry of rank need - 1 is the pivot.  One barrier instead of the digit passes' eight.
+    const uint32_t nb = bd.nb;
+    const bool mine = (uint32_t)t < nb;
+    const uint32_t kt = mine ? bd.sk[t] : 0u, it = mine ? bd.si[t] : 0u;
+    uint32_t rank = 0;
+    // 16 entries per step: four 16-byte LDS reads of keys and of indices in flight together
+    // (one dependent LDS round trip per entry measured 11-18 us per block)
+    const uint4* k4 = reinterpret_cast<const uint4*>(bd.sk);
+    const uint4* i4 = reinterpret_cast<const uint4*>(bd.si);
+    for (uint32_t j0 = 0; j0 < nb; j0 += 16) {
+      uint4 kq[4], iq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        kq[q] = k4[(j0 >> 2) + q];
+        iq[q] = i4[(j0 >> 2) + q];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t kv[4] = {kq[q].x, kq[q].y, kq[q].z, kq[q].w};
+        const uint32_t iv[4] = {iq[q].x, iq[q].y, iq[q].z, iq[q].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t j = j0 + 4 * q + e;
+          rank += (j < nb && (kv[e] > kt || (kv[e] == kt && iv[e] < it))) ? 1u : 0u;
+        }
+      }
+    }
+    if (mine && rank == need - 1) {
+      L.sh[0] = kt;
+      L.sh[1] = it;
+    }
+    __syncthreads();
+    *T_out = L.sh[0];
+    *icut_out = L.sh[1];
+    __syncthreads();  // L is reused by the caller's next phase
+    return;
+  }
   const int d1 = shift >= 8 ? 8 : (int)shift;
   const int low1 = (int)shift - d1;
   const uint32_t m1 = (1u << d1) - 1u;
@@ -946,7 +993,7 @@ __device__ __forceinline__ void dense_write(const KeySrc s, int64_t seg, int64_t
                                                       uint32_t T, uint32_t icut, uint32_t run,
                                                       const float* vals_src, int32_t* idx_out,
                                                       float* val_out, int32_t* counter,
-                                                      float* rewind) {
+                                                      float* rewind, int val_h) {
   const int lane = threadIdx.x & 63;
   const int64_t beg = seg * R;
   const int64_t end = (beg + R < n) ? beg + R : n;
@@ -970,7 +1017,7 @@ __device__ __forceinline__ void dense_write(const KeySrc s, int64_t seg, int64_t
         if (pos < (uint64_t)k) {
           const int64_t i = i0 + e;
           idx_out[pos] = (int32_t)i;
-          val_out[pos] = vals_src[i];
+          store_val(val_out, val_h, pos, vals_src[i]);
           if (counter) atomicAdd(&counter[i], 1);
           if (rewind) rewind[i] = 0.0f;
         }
@@ -981,16 +1028,18 @@ __device__ __forceinline__ void dense_write(const KeySrc s, int64_t seg, int64_t
   }
 }
 
-// One block of 256 threads per CSEG = 8 wave segments (2 filter blocks), two segments per wave:
-// half as many blocks as segments-per-4, so 4 waves per SIMD hold the whole grid and the kernel
-// gets 128 VGPRs (no spills).  Prologue, redundantly in every block (no single-block launch in
-// between — a launch boundary plus a one-CU kernel cost more than the ~15 KB of L2 reads per
-// block): the exact T / icut from the boundary sub-lists, the block's output offset = above-b*
-// counts of the earlier filter blocks + selected boundary entries before the block, and the
-// check that the grand total is k.  Then per wave a count pass over its two segments, in-block
-// offsets, and the ordered write of (idx, vals_src[idx]) with counter / rewind updates.  Block 0
-// re-zeroes the sample histogram and publishes T / icut / status.
-constexpr int CSEG = 8;
+// One block of 256 threads per CSEG = 4 SPW wave segments (SPW / 4 filter blocks... SPW per
+// wave).  Prologue, redundantly in every block (no single-block launch in between — a launch
+// boundary plus a one-CU kernel cost more than the ~15 KB of L2 reads per block): the exact T /
+// icut from the boundary sub-lists, the block's output offset = above-b* counts of the earlier
+// filter blocks + selected boundary entries before the block, and the check that the grand total
+// is k.  Then per wave a count pass over its SPW segments, in-block offsets, and the ordered
+// write of (idx, vals_src[idx]) with counter / rewind updates.  Block 0 re-zeroes the sample
+// histogram and publishes T / icut / status.
+// SPW = 8 (sparse alpha: ~20 candidates per segment): 256 blocks at 8192 segments, ONE per CU,
+// so the redundant prologue (latency-bound LDS phases with barriers) is not shared four ways on
+// every SIMD; every segment's first 64 candidates are loaded with the prologue.  SPW = 2 (dense
+// alpha): four chunks of 64 per segment in registers, 4 blocks per CU.
 // PLAIN (dense alpha, k > n/32): counter[idx] += 1 as a gathered read + plain store instead of a
 // memory-side atomic.  The selected indices are unique, so no two lanes update one word; a wave
 // instruction of atomics whose 64 lanes hit ~40 different lines runs at ~1/13 of the streaming
@@ -998,21 +1047,30 @@ constexpr int CSEG = 8;
 // the C3 compact (k = 2.5 M) atomic-bound; scattered plain stores run at the streaming rate, and
 // the gathers are issued while the threshold is being resolved.  At sparse alpha the atomics stay
 // (reading every candidate's counter ahead measured slower at C2).
-template <bool VEC, bool PLAIN>
-__global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
+template <int SPW>
+struct CompactCfg {
+  static constexpr int CSEG = 4 * SPW;          // wave segments per block
+  static constexpr int PFC = SPW >= 8 ? 1 : 4;  // chunks of 64 per segment held in registers
+};
+
+template <bool VEC, bool PLAIN, int SPW>
+__global__ void __launch_bounds__(256, SPW >= 8 ? 1 : 4) sampled_compact_kernel(
     KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl,
     uint32_t* chist, const uint32_t* __restrict__ blkabove, const uint32_t* __restrict__ blcnt,
     const uint32_t* __restrict__ blkey, const uint32_t* __restrict__ blidx,
     const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ cidx,
     const uint32_t* __restrict__ ckey, const float* __restrict__ cval, const float* vals_src,
     int32_t* idx_out, float* val_out, int32_t* counter, float* rewind, int32_t* status_out,
-    ReplaceJob pj, int64_t nrep_first) {
+    ReplaceJob pj, int64_t nrep_first, int val_h) {
+  constexpr int CSEG = CompactCfg<SPW>::CSEG;
+  constexpr int PFC = CompactCfg<SPW>::PFC;
   __shared__ uint32_t wcnt[CSEG];
   __shared__ uint32_t subbase[NSUB + 1];
   __shared__ uint32_t flag, spec;
   __shared__ uint64_t wsum64[4];
   __shared__ ResolveLds RL;
-  __shared__ uint32_t bsk[BLDS], bsi[BLDS];
+  __shared__ __attribute__((aligned(16))) uint32_t bsk[BLDS];
+  __shared__ __attribute__((aligned(16))) uint32_t bsi[BLDS];
   const int64_t CB_ = (W + CSEG - 1) / CSEG;
   const int64_t B = (W + 3) / 4;  // filter blocks (above counts)
   // co-scheduled replace decode: its blocks after compact's own, or (nrep_first > 0) before
@@ -1024,7 +1082,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   const uint32_t blk = (uint32_t)((int64_t)blockIdx.x - (nrep_first > 0 ? nrep_first : 0));
   STAMP_T0(0);
   const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
-  const int64_t seg0 = (int64_t)blk * CSEG + wid * 2;
+  const int64_t seg0 = (int64_t)blk * CSEG + wid * SPW;
   // every independent load first: control words, sub-list counts, above counts, own candidates
   const uint32_t status = ctrl->status;
   const uint32_t need = ctrl->need, lo = ctrl->lo, shift = ctrl->shift, bstar = ctrl->bstar;
@@ -1054,13 +1112,12 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
       abv_before += fb0 + q < fbx ? v[q] : 0u;
     }
   }
-  // candidate chunks of 64 kept in registers per segment (PFC chunks: up to 256 candidates);
-  // chunk 0 is loaded without waiting for the count (CAP >= 64; entries past it are ignored)
-  constexpr int PFC = 4;
-  uint32_t cnt[2], kk[2][PFC], ii[2][PFC];
-  float vv[2][PFC];
+  // candidate chunks of 64 kept in registers per segment (PFC chunks); chunk 0 is loaded without
+  // waiting for the count (CAP >= 64; entries past it are ignored)
+  uint32_t cnt[SPW], kk[SPW][PFC], ii[SPW][PFC];
+  float vv[SPW][PFC];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < SPW; ++u) {
     const int64_t seg = seg0 + u;
     cnt[u] = seg < W ? segcnt[seg] : 0u;
 #pragma unroll
@@ -1087,13 +1144,13 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   // gathers its value now, while the threshold is resolved, not at write time.  (Reading the
   // counter words ahead the same way, for plain-store updates, measured ~1 us SLOWER than the
   // memory-side atomics at C2: it reads every candidate's line; PLAIN does it at dense alpha.)
-  uint32_t cc[2][PFC];
+  uint32_t cc[SPW][PFC];
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int u = 0; u < SPW; ++u)
 #pragma unroll
     for (int c = 0; c < PFC; ++c) cc[u][c] = 0u;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < SPW; ++u) {
     const int64_t seg = seg0 + u;
     if (seg < W && cnt[u] != DENSE && (uint32_t)lane < cnt[u]) {
       if (!cval) vv[u][0] = vals_src[ii[u][0]];
@@ -1157,31 +1214,33 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
   }
   if (grand != (uint32_t)k) return;  // identical in every block: nothing is written
   // chunks 1 .. PFC-1 of every segment with more than 64 candidates: all issued together
+  if constexpr (PFC > 1) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int64_t seg = seg0 + u;
-    if (seg < W && cnt[u] != DENSE && cnt[u] > 64u) {
+    for (int u = 0; u < SPW; ++u) {
+      const int64_t seg = seg0 + u;
+      if (seg < W && cnt[u] != DENSE && cnt[u] > 64u) {
 #pragma unroll
-      for (int c = 1; c < PFC; ++c) {
-        const uint32_t j = c * 64u + lane;
-        if (j < cnt[u]) {
-          kk[u][c] = ckey[seg * CAP + j];
-          ii[u][c] = cidx[seg * CAP + j];
-          if (cval) vv[u][c] = cval[seg * CAP + j];
+        for (int c = 1; c < PFC; ++c) {
+          const uint32_t j = c * 64u + lane;
+          if (j < cnt[u]) {
+            kk[u][c] = ckey[seg * CAP + j];
+            ii[u][c] = cidx[seg * CAP + j];
+            if (cval) vv[u][c] = cval[seg * CAP + j];
+          }
         }
-      }
 #pragma unroll
-      for (int c = 1; c < PFC; ++c) {
-        const uint32_t j = c * 64u + lane;
-        if (j < cnt[u] && !cval) vv[u][c] = vals_src[ii[u][c]];
-        if (PLAIN && counter && j < cnt[u]) cc[u][c] = (uint32_t)counter[ii[u][c]];
+        for (int c = 1; c < PFC; ++c) {
+          const uint32_t j = c * 64u + lane;
+          if (j < cnt[u] && !cval) vv[u][c] = vals_src[ii[u][c]];
+          if (PLAIN && counter && j < cnt[u]) cc[u][c] = (uint32_t)counter[ii[u][c]];
+        }
       }
     }
   }
   auto is_sel = [&](uint32_t key, uint32_t idx) { return key > T || (key == T && idx <= icut); };
   // count pass (the first PFC chunks from registers), in-block offsets, write pass
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < SPW; ++u) {
     const int64_t seg = seg0 + u;
     uint32_t mine = 0;
     if (seg < W && cnt[u] != DENSE) {
@@ -1210,14 +1269,14 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
     } else if (seg < W) {
       mine = dense_count<VEC>(s, seg, R, n, lo, T, icut);
     }
-    if (lane == 0) wcnt[wid * 2 + u] = mine;
+    if (lane == 0) wcnt[wid * SPW + u] = mine;
   }
   __syncthreads();
   STAMP_T0(3);
   uint32_t run = boff;
-  for (int w = 0; w < wid * 2; ++w) run += wcnt[w];
+  for (int w = 0; w < wid * SPW; ++w) run += wcnt[w];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < SPW; ++u) {
     const int64_t seg = seg0 + u;
     if (seg >= W) break;
     if (cnt[u] != DENSE) {
@@ -1229,7 +1288,7 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
           const uint32_t pos = run + mbcnt64(m);
           if (pos < (uint64_t)k) {
             idx_out[pos] = (int32_t)idx;
-            val_out[pos] = (cval || pre) ? v : vals_src[idx];
+            store_val(val_out, val_h, pos, (cval || pre) ? v : vals_src[idx]);
             if (counter) {
               if (PLAIN) counter[idx] = (int32_t)(cw + 1u);  // unique indices: no race
               else atomicAdd(&counter[idx], 1);  // non-returning: no round trip to wait on
@@ -1266,8 +1325,8 @@ __global__ void __launch_bounds__(256, 4) sampled_compact_kernel(
       }
     } else {
       dense_write<VEC>(s, seg, R, n, k, lo, T, icut, run, vals_src, idx_out, val_out, counter,
-                       rewind);
-      run += wcnt[wid * 2 + u];
+                       rewind, val_h);
+      run += wcnt[wid * SPW + u];
     }
   }
   STAMP_T0(4);
@@ -1311,6 +1370,10 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
   // (sample, select, resolve, compact) and run in blocks appended after each launch's own
   ReplaceJob jb[3] = {};
   unsigned pb[3] = {0, 0, 0};
+  // the sample's block size: 1024 threads (16 blocks) or 256 (64 blocks); DPZ_SAMPLE_THREADS
+  // (diagnostic build) forces either
+  const int smp_threads = DPZ_KNOB_INT(SAMPLE_THREADS, 1024) == 256 ? 256 : 1024;
+  const int smp_blocks = SMP_NCHUNK / (4 * (smp_threads / 64));
   // a scatter job (dpz_topk_encode_replace over the tensor being encoded): the filter writes
   // out = x as it streams x, and the entries are scattered in blocks of the compact launch
   float* copy_out = (a.job && phases == 3 && a.job->scatter) ? a.job->out : nullptr;
@@ -1330,7 +1393,7 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
       f[1] = split ? 0.5 : (at_select ? 1.0 : 0.0);
       f[2] = split ? 0.5 : (at_select ? 0.0 : 1.0);
     }
-    const int per[3] = {4, 16, 4};  // chunks per appended block (one per wave)
+    const int per[3] = {smp_threads / 64, 16, 4};  // chunks per appended block (one per wave)
     int64_t c = a.job->c0;
     double acc_f = 0.0;
     for (int i = 0; i < 3; ++i) {
@@ -1346,8 +1409,9 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
     }
   }
   if (phases & 1) {
-    DPZ_TIMED(DPZ_KT_TOPK_SAMPLE, a.st, sampled_sample_kernel<<<SMP_BLOCKS + pb[0], 256, 0, a.st>>>(
-        s, a.n, ctrl, chist, ghist, blcnt, jb[0]));
+    DPZ_TIMED(DPZ_KT_TOPK_SAMPLE, a.st,
+              sampled_sample_kernel<<<smp_blocks + pb[0], smp_threads, 0, a.st>>>(
+                  s, a.n, ctrl, chist, ghist, blcnt, jb[0], smp_blocks, a.val_h));
     uint32_t r_lo, r_hi;
     window_ranks(a.n, a.k, &r_lo, &r_hi);
     // The pipelined filter (PartialModel: aligned, no accumulation): depth 2 at 8 waves / SIMD
@@ -1402,19 +1466,30 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
       s, a.n, a.k, g.W, g.B, g.R, g.CAP, ctrl, ghist, segcnt, cidx, ckey, blkabove, blcnt, blkey,
       blidx, jb[1]));
   float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE) ? a.acc : nullptr;
-  const unsigned ncmp = (unsigned)((g.W + CSEG - 1) / CSEG);
   // DPZ_COUNTER_PLAIN=0 / 1 forces the counter update form (diagnostic build, A/B)
   const bool plain = DPZ_KNOB_INT(COUNTER_PLAIN, a.k > a.n / 32 ? 1 : 0) != 0;
   // DPZ_SCATTER_FIRST=1: the decode's blocks dispatched ahead of compact's own (diagnostic, A/B)
   const int64_t nrep_first = DPZ_KNOB_INT(SCATTER_FIRST, 0) != 0 ? (int64_t)pb[2] : 0;
-  if (plain)
-    DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC, true><<<ncmp + pb[2], 256, 0, a.st>>>(
-        s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, cidx,
-        ckey, cval, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, a.status_out, jb[2], nrep_first));
-  else
-    DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st, sampled_compact_kernel<VEC, false><<<ncmp + pb[2], 256, 0, a.st>>>(
-        s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, cidx,
-        ckey, cval, a.vals_src, a.idx_out, a.val_out, a.counter, rewind, a.status_out, jb[2], nrep_first));
+  // sparse alpha: 8 segments per wave, one compact block per CU; dense alpha: 2 segments per
+  // wave with four chunks each in registers (DPZ_COMPACT_SPW=2 / 8 forces, diagnostic build)
+  // (8 segments per wave, one block per CU, measured SLOWER at C2: 18.7 vs 12 us — the count and
+  // write passes serialise four times the segments per wave, and the prologue does not get faster)
+  const int spw = (int)DPZ_KNOB_INT(COMPACT_SPW, 2);
+#define DPZ_COMPACT(PL_, SPW_)                                                                    \
+  DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st,                                                            \
+            (sampled_compact_kernel<VEC, PL_, SPW_><<<(unsigned)((g.W + 4 * SPW_ - 1) / (4 * SPW_)) \
+                                                        + pb[2], 256, 0, a.st>>>(                 \
+                s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, \
+                cidx, ckey, cval, a.vals_src, a.idx_out, a.val_out, a.counter, rewind,            \
+                a.status_out, jb[2], nrep_first, a.val_h)))
+  if (plain) {
+    if (spw == 8) DPZ_COMPACT(true, 8);
+    else DPZ_COMPACT(true, 2);
+  } else {
+    if (spw == 8) DPZ_COMPACT(false, 8);
+    else DPZ_COMPACT(false, 2);
+  }
+#undef DPZ_COMPACT
   return DPZ_OK;
 }
 

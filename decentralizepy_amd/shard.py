@@ -8,8 +8,8 @@ ties to the lowest index; sharing/PartialModel.py:164-186) is found with ONE col
   1. every rank selects its local top-k (the full k, not k / world) with the HIP encoder — the
      global top-k is contained in the union: a rank contributes at most k entries, and those are
      its k largest with the lowest local (= lowest global) indices among ties;
-  2. one all-gather of the k candidates of every rank (global index, change, value: 12 B each;
-     6.4 MB for C5 on 8 ranks) over RCCL;
+  2. one all-gather of the k candidates of every rank (global index, change, value: 12 B each,
+     10 B with fp16 values; 6.4 / 5.4 MB for C5 on 8 ranks) over RCCL;
   3. every rank runs the same top-k over the world * k gathered changes (their concatenation is
      in global index order, so the encoder's lowest-position tie rule is the lowest global index)
      and gathers the winners' indices and values — identical on every rank, no second exchange;
@@ -34,6 +34,11 @@ def _gather_change(x, x0, idx):
 
 def _gather_u32(src, pos):
     out = torch.empty(pos.numel(), dtype=src.dtype, device=src.device)
+    if src.element_size() == 2:  # fp16 payload values
+        rc = _lib.lib().dpz_gather_u16(_ptr(src), src.numel(), _ptr(pos), pos.numel(), _ptr(out),
+                                       _stream(src.device))
+        _lib.check(rc, "dpz_gather_u16")
+        return out
     rc = _lib.lib().dpz_gather_u32(_ptr(src), src.numel(), _ptr(pos), pos.numel(), _ptr(out),
                                    _stream(src.device))
     _lib.check(rc, "dpz_gather_u32")
@@ -55,9 +60,9 @@ class HipShardOps:
         self.ws = codec.Workspace(device)
         self.ws_merge = codec.Workspace(device)
 
-    def local_candidates(self, x, x0, k, offset, exact=False):
+    def local_candidates(self, x, x0, k, offset, exact=False, val_fp16=False):
         idx, val = codec.topk_encode(x, k, x0=x0, workspace=self.ws, asynchronous=not exact,
-                                     exact=exact)
+                                     exact=exact, val_fp16=val_fp16)
         chg = _gather_change(x, x0, idx)
         return (idx + int(offset)).to(torch.int32), chg, val
 
@@ -84,13 +89,15 @@ class HipShardOps:
         _lib.check(rc, "dpz_replace_slice")
 
 
-def sharded_topk_encode(x, x0, k, offset, counter=None, group=None, ops=None):
+def sharded_topk_encode(x, x0, k, offset, counter=None, group=None, ops=None, val_fp16=False):
     """Global top-k of a tensor sharded over the ranks of `group`.
 
     x, x0: this rank's slice (flat fp32); offset: the slice's first global index; k: the GLOBAL
     k (every slice must hold at least k elements).  Returns ``(idx int32[k] global ascending,
     val fp32[k])`` — the whole payload, identical on every rank.  ``counter`` (this rank's slice
-    of shared_parameters_counter) gets += 1 at the winners inside the slice.
+    of shared_parameters_counter) gets += 1 at the winners inside the slice.  ``val_fp16``: the
+    values are packed to fp16 (round to nearest even) by the local encodes themselves
+    (DPZ_TOPK_VAL_FP16, BASELINE config 5) and travel as fp16: ``val`` is float16[k].
     """
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -98,20 +105,26 @@ def sharded_topk_encode(x, x0, k, offset, counter=None, group=None, ops=None):
         raise ValueError("every shard must hold at least k elements")
     ops = ops or HipShardOps(x.device)
     for exact in (False, True):
-        idx, chg, val = ops.local_candidates(x, x0, k, offset, exact=exact)
+        if val_fp16:
+            idx, chg, val = ops.local_candidates(x, x0, k, offset, exact=exact, val_fp16=True)
+        else:
+            idx, chg, val = ops.local_candidates(x, x0, k, offset, exact=exact)
         st = (ops.local_status() if hasattr(ops, "local_status")
               else torch.zeros(1, dtype=torch.int32, device=idx.device))
         if world > 1:
-            # one exchange: the three candidate arrays and the status word, packed as 32-bit
-            # words in ONE all-gather
-            pack = torch.cat([idx.view(torch.float32), chg, val, st.view(torch.float32)])
-            gflat = torch.empty(world * (3 * k + 1), dtype=torch.float32, device=idx.device)
+            # one exchange: the candidate arrays and the status word, packed as bytes
+            # (index, change: 4 B; value: 4 or 2 B) in ONE all-gather
+            vb = val.element_size()
+            row = 8 * k + vb * k + 4
+            pack = torch.cat([idx.view(torch.uint8), chg.view(torch.uint8), val.view(torch.uint8),
+                              st.view(torch.uint8)])
+            gflat = torch.empty(world * row, dtype=torch.uint8, device=idx.device)
             dist.all_gather_into_tensor(gflat, pack, group=group)
-            gpack = gflat.view(world, 3 * k + 1)
-            gidx = gpack[:, :k].reshape(-1).contiguous().view(torch.int32)
-            gchg = gpack[:, k:2 * k].reshape(-1).contiguous()
-            gval = gpack[:, 2 * k:3 * k].reshape(-1).contiguous()
-            gst = gpack[:, 3 * k].contiguous().view(torch.int32)
+            gpack = gflat.view(world, row)
+            gidx = gpack[:, :4 * k].reshape(-1).contiguous().view(torch.int32)
+            gchg = gpack[:, 4 * k:8 * k].reshape(-1).contiguous().view(torch.float32)
+            gval = gpack[:, 8 * k:8 * k + vb * k].reshape(-1).contiguous().view(val.dtype)
+            gst = gpack[:, row - 4:].reshape(-1).contiguous().view(torch.int32)
         else:
             gidx, gchg, gval, gst = idx, chg, val, st
         widx, wval = ops.merge(gidx, gchg, gval, k, exact=exact)

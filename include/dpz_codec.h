@@ -57,6 +57,11 @@ typedef void* dpz_stream_t; /* hipStream_t */
  * (the default) takes the larger, faster-alone grid.  Results are identical either way; STREAM
  * and TAIL calls of one encode must pass the same choice.                                     */
 #define DPZ_TOPK_SHARED 0x10
+/* val_out receives fp16 values (uint16 words, round to nearest even: torch.Tensor.half(), the
+ * C5 payload's value packing) written by the encode itself — no separate packing
+ * launch.  val_out then holds k * 2 bytes.  A later dpz_topk_complete re-runs a missed sampled
+ * call in the same format.                                                                    */
+#define DPZ_TOPK_VAL_FP16 0x20
 
 /* ---- fold flags ---- */
 #define DPZ_FOLD_SELF 0x1         /* add the local term w_self*local after the payloads        */
@@ -170,10 +175,13 @@ int dpz_elementwise(int op, const float* a, const float* b, const float* d, floa
                     float* out, dpz_stream_t stream);
 /* Helpers of the sharded top-k (one tensor split over ranks, decentralizepy_amd/shard.py,
  * SURVEY §8e): out[j] = x[idx[j]] - x0[idx[j]] (x0 may be NULL); out[j] = src[pos[j]] for 32-bit
- * words; dst[idx[j] - offset] += value where idx[j] - offset lies in [0, n).                    */
+ * words (dpz_gather_u16: 16-bit words, the fp16 values of a C5 payload); dst[idx[j] - offset] +=
+ * value where idx[j] - offset lies in [0, n).                                                   */
 int dpz_gather_change(const float* x, const float* x0, int64_t n, const int32_t* idx, int64_t k,
                       float* out, dpz_stream_t stream);
 int dpz_gather_u32(const void* src, int64_t m, const int32_t* pos, int64_t k, void* out,
+                   dpz_stream_t stream);
+int dpz_gather_u16(const void* src, int64_t m, const int32_t* pos, int64_t k, void* out,
                    dpz_stream_t stream);
 int dpz_scatter_add_i32(int32_t* dst, int64_t n, const int32_t* idx, int64_t k, int64_t offset,
                         int32_t value, dpz_stream_t stream);
@@ -190,8 +198,8 @@ int dpz_topk_complete(const float* x, const float* x0, float* acc, int acc_mode,
  * the result is final; otherwise the sampled path missed, nothing was written or updated, and the
  * caller re-runs the encode with DPZ_TOPK_EXACT.  Lets a caller enqueue many encodes that share
  * one workspace (a gossip round's nodes, decentralizepy_amd/gossip_jwins.py) and read every
- * status once; replaces the same reference lines as dpz_topk_encode.  flags: 0 or
- * DPZ_TOPK_SHARED (any other bit is DPZ_ERR_ARG).                                              */
+ * status once; replaces the same reference lines as dpz_topk_encode.  flags: DPZ_TOPK_SHARED
+ * and / or DPZ_TOPK_VAL_FP16 (any other bit is DPZ_ERR_ARG).                                   */
 int dpz_topk_encode_status(const float* x, const float* x0, float* acc, int acc_mode,
                            const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
                            float* val_out, int32_t* counter, void* ws, size_t ws_bytes,

@@ -14,9 +14,11 @@ from oracle import topk as otopk
 
 
 class OracleOps:
-    def local_candidates(self, x, x0, k, offset, exact=False):
+    def local_candidates(self, x, x0, k, offset, exact=False, val_fp16=False):
         idx, val = otopk.encode(x.numpy(), x0.numpy(), None, otopk.ACC_NONE, k)
         chg = (x.numpy() - x0.numpy())[idx]
+        if val_fp16:  # the encode's own RNE packing (torch.half)
+            val = val.astype(np.float16)
         return (torch.from_numpy(idx.astype(np.int32)) + int(offset), torch.from_numpy(chg),
                 torch.from_numpy(val))
 
@@ -47,7 +49,7 @@ def _inputs(n, ties):
     return x, x0
 
 
-def _worker(rank, world, port, n, k, ties, out_q):
+def _worker(rank, world, port, n, k, ties, out_q, fp16=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -60,7 +62,10 @@ def _worker(rank, world, port, n, k, ties, out_q):
         from decentralizepy_amd.shard import sharded_replace
         ops = OracleOps()
         idx, val = sharded_topk_encode(x[lo:hi].contiguous(), x0[lo:hi].contiguous(), k, lo,
-                                       counter=cnt, ops=ops)
+                                       counter=cnt, ops=ops, val_fp16=fp16)
+        if fp16:
+            out_q.put((rank, idx.numpy(), val.numpy(), lo, cnt.numpy(), None))
+            return
         # decode of the global payload into this rank's slice: most entries lie outside it
         dec = sharded_replace(x0[lo:hi].contiguous(), lo, idx, val, ops=ops)
         out_q.put((rank, idx.numpy(), val.numpy(), lo, cnt.numpy(), dec.numpy()))
@@ -200,3 +205,28 @@ def test_wavelet_slices_partition_tiles_and_coefficients(n, world):
             assert sl["hi"] == n or span * sl["t_hi"] <= sl["hi"]
             assert sl["lo"] < sl["hi"]
     assert (fwd == 1).all() and (inv == 1).all() and (cov == 1).all()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_topk_fp16_values(world):
+    """BASELINE config 5: fp16 values (RNE) packed by the local encodes travel through the one
+    all-gather (10 bytes per candidate) and the merge: the whole-tensor payload with torch.half
+    values on every rank."""
+    n, k = 30_000, 1_500
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29690 + world
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, k, True, q, True))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    x, x0 = _inputs(n, True)
+    oi, ov = otopk.encode(x.numpy(), x0.numpy(), None, otopk.ACC_NONE, k)
+    for rank, idx, val, lo, cnt, _ in res:
+        assert val.dtype == np.float16
+        np.testing.assert_array_equal(idx, oi)
+        np.testing.assert_array_equal(val.view(np.uint16),
+                                      torch.from_numpy(ov).half().numpy().view(np.uint16))

@@ -860,3 +860,27 @@ def test_counter_update_forms_agree(dev, diag_lib, monkeypatch, plain, n, alpha,
     np.testing.assert_array_equal(tcnt.cpu().numpy(), o_cnt)
     if acc is not None:
         np.testing.assert_array_equal(_bits(tacc.cpu().numpy()), _bits(o_acc))
+
+
+@pytest.mark.parametrize("alpha", [0.1, 0.01])
+def test_fold_c3_full_size_16_payloads(dev, alpha):
+    """The C3 shape the bench times: 16 sparse payloads folded over the sym2
+    level-4 coefficient vector of a 25 M model, M = 25,000,009 (odd: the walk fold's ragged
+    vector path), at the tutorial's alpha 0.1 (walk fold) and 0.01 (hit-chain fold), bit-exact
+    against the oracle's Metro-Hastings fold (reference sharing/JWINS/Wavelet.py:269-309)."""
+    codec = _codec()
+    m, npay = 25_000_009, 16
+    k = round(alpha * m)
+    g = torch.Generator(device=dev).manual_seed(31)
+    local_t = torch.randn(m, device=dev, generator=g)
+    tpays, pays = [], []
+    for i in range(npay):
+        idx = torch.sort(torch.randperm(m, device=dev, generator=g)[:k])[0].to(torch.int32)
+        vals = torch.randn(k, device=dev, generator=g)
+        tpays.append((idx, vals))
+        pays.append((idx.cpu().numpy(), vals.cpu().numpy()))
+    w = [1 / (npay + 1)] * npay
+    w_self = 1 - sum(w)
+    out = codec.decode_average(local_t, tpays, w, w_self).cpu().numpy()
+    ref = ofold.fold(local_t.cpu().numpy(), pays, w, w_self)
+    np.testing.assert_array_equal(_bits(out), _bits(ref))

@@ -169,3 +169,59 @@ def test_sharded_replace_equals_whole_tensor(dev, n, world, alpha):
     if empty_lo is not None:
         loc = x0[:empty_lo].clone()
         assert torch.equal(sharded_replace(loc, 0, idx, val), loc)
+
+
+@pytest.mark.parametrize("n,alpha,world", [(67_108_864, 0.001, 8), (3_000_001, 0.01, 3)])
+def test_sharded_fp16_values_written_by_the_encode(dev, n, alpha, world):
+    """BASELINE config 5 as named: the sharded one-tensor encode whose values are packed to fp16
+    by the local encodes themselves (DPZ_TOPK_VAL_FP16, no pack_fp16 launch) and carried as fp16
+    through the merge: equal to the oracle's top-k with the reference rule and torch.half values
+    (round to nearest even)."""
+    from decentralizepy_amd import codec
+    from decentralizepy_amd.shard import HipShardOps
+    from oracle import topk as otopk
+    g = torch.Generator(device=dev).manual_seed(23)
+    x = torch.randn(n, device=dev, generator=g)
+    x0 = x - 0.01 * torch.randn(n, device=dev, generator=g)
+    k = round(alpha * n)
+    o_cnt = np.zeros(n, dtype=np.int32)
+    oi, ov = otopk.encode(x.cpu().numpy(), x0.cpu().numpy(), None, 0, k, counter=o_cnt)
+    want_h = ov.astype(np.float16)  # RNE, as torch.Tensor.half()
+    # the one-tensor encode with fp16 values
+    cnt1 = torch.zeros(n, dtype=torch.int32, device=dev)
+    i1, v1 = codec.topk_encode(x, k, x0=x0, counter=cnt1, val_fp16=True)
+    assert v1.dtype == torch.float16
+    np.testing.assert_array_equal(i1.cpu().numpy(), oi)
+    np.testing.assert_array_equal(v1.cpu().numpy().view(np.uint16), want_h.view(np.uint16))
+    np.testing.assert_array_equal(cnt1.cpu().numpy(), o_cnt)
+    # the sharded steps, emulated in one process
+    ops = HipShardOps(dev)
+    bounds = np.linspace(0, n, world + 1).astype(int)
+    cands = [ops.local_candidates(x[lo:hi], x0[lo:hi], k, int(lo), val_fp16=True)
+             for lo, hi in zip(bounds[:-1], bounds[1:])]
+    widx, wval = ops.merge(torch.cat([c[0] for c in cands]), torch.cat([c[1] for c in cands]),
+                           torch.cat([c[2] for c in cands]), k)
+    assert int(ops.merge_status().item()) == 0
+    np.testing.assert_array_equal(widx.cpu().numpy(), oi)
+    np.testing.assert_array_equal(wval.cpu().numpy().view(np.uint16), want_h.view(np.uint16))
+
+
+@pytest.mark.parametrize("n,k", [(100_000, 1_000), (1_000_000, 600_000)])
+def test_fp16_values_on_the_exact_path(dev, n, k):
+    """small n / dense alpha take the exact path: the same fp16 values; overflow to inf and NaN
+    keep torch.half semantics"""
+    from decentralizepy_amd import codec
+    from oracle import topk as otopk
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal(n).astype(np.float32) * 1e3
+    x[:5] = [7e4, -7e4, np.inf, np.nan, 65519.0]  # overflow, inf, NaN, rounds up to inf
+    x0 = (x - rng.standard_normal(n).astype(np.float32)).astype(np.float32)
+    x0[:5] = 0.0
+    oi, ov = otopk.encode(x, x0, None, 0, k)
+    i, v = codec.topk_encode(torch.from_numpy(x).to(dev), k, x0=torch.from_numpy(x0).to(dev),
+                             val_fp16=True)
+    np.testing.assert_array_equal(i.cpu().numpy(), oi)
+    np.testing.assert_array_equal(v.cpu().numpy().view(np.uint16),
+                                  ov.astype(np.float16).view(np.uint16))
+    ref_t = torch.from_numpy(ov).half().numpy()
+    np.testing.assert_array_equal(v.cpu().numpy().view(np.uint16), ref_t.view(np.uint16))

@@ -47,7 +47,7 @@ def main():
         if it < 4:
             continue
         out = [f"iter {it}: sample {(arr[1] - t0) / 100:.1f}"]
-        for name, rows in (("select", [8, 9, 10, 11]), ("compact", [0, 1, 2, 3, 4])):
+        for name, rows in (("select", [8, 12, 9, 10, 11]), ("compact", [0, 1, 2, 3, 4])):
             nb = int((ball[rows[0]] > 0).sum())
             for r in rows:
                 v = ball[r][:nb]
