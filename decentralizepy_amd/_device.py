@@ -4,6 +4,7 @@ The reference runs one node per OS process with the model on the CPU (node/Node.
 eval/testing.py:54-80).  The plugins keep the codec state on the GPU chosen by the node's local
 rank and move only the flat model and the payloads across PCIe, through pinned staging buffers.
 """
+import functools
 import os
 
 import numpy as np
@@ -76,6 +77,28 @@ def state_version(state_dict):
     return tuple(v._version for v in state_dict.values())
 
 
+def state_to_device(state_dict, device, staging, name):
+    """``flatten_state`` + H2D in one host pass: the state tensors are concatenated straight
+    into the pinned staging buffer (``torch.cat(..., out=pinned)``), then one async DMA — no
+    intermediate flat copy of the model on the host (the reference's ``torch.cat``,
+    sharing/PartialModel.py:312-316, is this concatenation)."""
+    vals = [v.flatten() for v in state_dict.values()]
+    # the dtype the reference's torch.cat produces (type promotion: int buffers such as
+    # BatchNorm's num_batches_tracked, or fp16 tensors beside fp32 ones, become fp32)
+    dt = functools.reduce(torch.promote_types, [v.dtype for v in vals], torch.bool)
+    if dt != torch.float32:
+        raise NotImplementedError(
+            f"the flattened model is {dt}; the HIP codec handles fp32 models only")
+    n = sum(v.numel() for v in vals)
+    host = staging.get(name, n, torch.float32)
+    if host is None:  # over the pinned cap: pageable copy
+        return torch.cat(vals).to(device)
+    torch.cat(vals, out=host)
+    out = host.to(device, non_blocking=True)
+    staging.mark(name, torch.float32, torch.cuda.current_stream(device))
+    return out
+
+
 def to_device_flat(flat_cpu, device, staging, name):
     """H2D of a host fp32 vector through a pinned buffer."""
     if flat_cpu.dtype != torch.float32:
@@ -123,14 +146,16 @@ class PayloadNames:
         return f"pay{self.i}_{leg}"
 
 
-def to_host(t, staging, name):
-    """D2H into a pinned buffer; returns a numpy array that owns its memory."""
+def to_host(t, staging, name, own=True):
+    """D2H into a pinned buffer; returns a numpy array that owns its memory, or with
+    ``own=False`` a view of the pinned buffer, valid until the next ``to_host`` of ``name`` (for
+    a result consumed at once: the averaged model ``load_state_dict`` copies into the model)."""
     host = staging.get(name, t.numel(), t.dtype)
     if host is None:  # over the pinned cap: pageable copy
         return t.cpu().numpy().copy()
     host.copy_(t, non_blocking=True)
     torch.cuda.current_stream(t.device).synchronize()
-    return host.numpy().copy()
+    return host.numpy().copy() if own else host.numpy()
 
 
 class DeviceCounter:

@@ -981,21 +981,33 @@ extern "C" int dpz_lz4_decompress(const uint8_t* frame_dev, const uint8_t* frame
   if (ws_bytes < dpz_lz4_workspace_bytes(0, nb, linked ? 0 : bmax) || !ws) return DPZ_ERR_WORKSPACE;
   const uint8_t flg = frame_host[4];
   const bool bsum = flg & 0x10;
-  // block table from the host bytes, built in a pinned buffer of this thread (the H2D is a true
-  // async DMA; the buffer is reused only after this call's final synchronize)
-  thread_local LzBlock* tab_pin = nullptr;
-  thread_local size_t tab_cap = 0;
+  // block table from the host bytes, built in pinned memory (the H2D is a true async DMA): a
+  // per-thread buffer of at most PIN_CAP bytes (freed when the thread exits; reused only after
+  // this call's final synchronize), or, for a larger table, a pinned buffer of this call alone
+  struct PinTab {
+    void* p = nullptr;
+    size_t cap = 0;
+    ~PinTab() {
+      if (p) (void)hipHostFree(p);
+    }
+  };
+  constexpr size_t PIN_CAP = 64 * 1024;  // 4K blocks: a 16 MB frame of 4 KB blocks
+  thread_local PinTab tab_tls;
+  PinTab tab_call;  // an oversize table's buffer, freed on return
   const size_t tab_need = sizeof(LzBlock) * (size_t)(nb + 1) + 16;
-  if (tab_cap < tab_need) {
-    if (tab_pin) (void)hipHostFree(tab_pin);
-    tab_pin = nullptr;
-    tab_cap = 0;
-    void* pp = nullptr;
-    if (hipHostMalloc(&pp, tab_need * 2) != hipSuccess || !pp) return DPZ_ERR_INTERNAL;
-    tab_pin = static_cast<LzBlock*>(pp);
-    tab_cap = tab_need * 2;
+  PinTab& pt = tab_need <= PIN_CAP ? tab_tls : tab_call;
+  if (pt.cap < tab_need) {
+    if (pt.p) (void)hipHostFree(pt.p);
+    pt.p = nullptr;
+    pt.cap = 0;
+    const size_t want = tab_need <= PIN_CAP ? PIN_CAP : tab_need;
+    if (hipHostMalloc(&pt.p, want) != hipSuccess || !pt.p) {
+      pt.p = nullptr;
+      return DPZ_ERR_INTERNAL;
+    }
+    pt.cap = want;
   }
-  LzBlock* tab_h = tab_pin;
+  LzBlock* tab_h = static_cast<LzBlock*>(pt.p);
   int64_t pos = 6 + ((flg & 0x08) ? 8 : 0) + ((flg & 0x01) ? 4 : 0) + 1;
   for (int64_t b = 0; b < nb; ++b) {
     const uint8_t* p = frame_host + pos;

@@ -809,46 +809,9 @@ __device__ __forceinline__ void block_resolve(const Bound& bd, uint32_t need, ui
                                               uint32_t shift, ResolveLds& L, uint32_t* T_out,
                                               uint32_t* icut_out) {
   const int t = threadIdx.x;
-  if (bd.nb <= 256u) {
-    // every entry in LDS, at most one per thread: each entry's rank in (key descending, index
-    // ascending) order against all the others (broadcast LDS reads, no barrier in the loop); the
-    // entry of rank need - 1 is the pivot.  One barrier instead of the digit passes' eight.
-    const uint32_t nb = bd.nb;
-    const bool mine = (uint32_t)t < nb;
-    const uint32_t kt = mine ? bd.sk[t] : 0u, it = mine ? bd.si[t] : 0u;
-    uint32_t rank = 0;
-    // 16 entries per step: four 16-byte LDS reads of keys and of indices in flight together
-    // (one dependent LDS round trip per entry measured 11-18 us per block)
-    const uint4* k4 = reinterpret_cast<const uint4*>(bd.sk);
-    const uint4* i4 = reinterpret_cast<const uint4*>(bd.si);
-    for (uint32_t j0 = 0; j0 < nb; j0 += 16) {
-      uint4 kq[4], iq[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        kq[q] = k4[(j0 >> 2) + q];
-        iq[q] = i4[(j0 >> 2) + q];
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t kv[4] = {kq[q].x, kq[q].y, kq[q].z, kq[q].w};
-        const uint32_t iv[4] = {iq[q].x, iq[q].y, iq[q].z, iq[q].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t j = j0 + 4 * q + e;
-          rank += (j < nb && (kv[e] > kt || (kv[e] == kt && iv[e] < it))) ? 1u : 0u;
-        }
-      }
-    }
-    if (mine && rank == need - 1) {
-      L.sh[0] = kt;
-      L.sh[1] = it;
-    }
-    __syncthreads();
-    *T_out = L.sh[0];
-    *icut_out = L.sh[1];
-    __syncthreads();  // L is reused by the caller's next phase
-    return;
-  }
+  // (A rank of every entry against all the others — O(nb^2) compares per thread, no digit
+  // passes — measured 4-7 us per block instead of ~1.7: every one of the ~1024 blocks repeats
+  // the resolve, so its VALU work is paid ~4 times on every SIMD.)
   const int d1 = shift >= 8 ? 8 : (int)shift;
   const int low1 = (int)shift - d1;
   const uint32_t m1 = (1u << d1) - 1u;
@@ -1370,9 +1333,10 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
   // (sample, select, resolve, compact) and run in blocks appended after each launch's own
   ReplaceJob jb[3] = {};
   unsigned pb[3] = {0, 0, 0};
-  // the sample's block size: 1024 threads (16 blocks) or 256 (64 blocks); DPZ_SAMPLE_THREADS
-  // (diagnostic build) forces either
-  const int smp_threads = DPZ_KNOB_INT(SAMPLE_THREADS, 1024) == 256 ? 256 : 1024;
+  // the sample's block size: 256 threads (64 blocks) or 1024 (16 blocks, fewer same-address
+  // atomics per histogram bin); DPZ_SAMPLE_THREADS (diagnostic build) forces either
+  // (1024-thread blocks measured no faster: 4.7-5.3 vs 4.6-5.4 us)
+  const int smp_threads = DPZ_KNOB_INT(SAMPLE_THREADS, 256) == 1024 ? 1024 : 256;
   const int smp_blocks = SMP_NCHUNK / (4 * (smp_threads / 64));
   // a scatter job (dpz_topk_encode_replace over the tensor being encoded): the filter writes
   // out = x as it streams x, and the entries are scattered in blocks of the compact launch

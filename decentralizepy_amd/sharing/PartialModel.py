@@ -27,7 +27,7 @@ import numpy as np
 import torch
 
 from .. import codec
-from .._device import DeviceCounter, flatten_state, state_version, to_device_flat, to_host
+from .._device import DeviceCounter, state_to_device, state_version, to_host
 from ..utils import conditional_value, identity
 from .Sharing import Sharing
 
@@ -59,8 +59,8 @@ class PartialModel(Sharing):
         self._check_transformer()
 
         with torch.no_grad():
-            flat = flatten_state(self.model.state_dict())
-        self.init_model = to_device_flat(flat, self.device, self.staging, "local")
+            self.init_model = state_to_device(self.model.state_dict(), self.device, self.staging,
+                                              "local")
         # the fold output can stand in for a re-read of the loaded model only if every state
         # tensor is fp32 (load_state_dict casts other dtypes)
         self._all_fp32 = all(v.dtype == torch.float32 for v in self.model.state_dict().values())
@@ -141,8 +141,7 @@ class PartialModel(Sharing):
         logging.debug("PartialModel _pre_step")
         with torch.no_grad():
             sd = self.model.state_dict()
-            flat = flatten_state(sd)
-            self.pre_share_model = to_device_flat(flat, self.device, self.staging, "local")
+            self.pre_share_model = state_to_device(sd, self.device, self.staging, "local")
             self._pre_version = state_version(sd)
             self.pre_share_model_transformed, self._change_dev = \
                 self._transform_pre_step(self.pre_share_model)
@@ -153,17 +152,22 @@ class PartialModel(Sharing):
         and with accumulation the accumulated change before the rewind (acc + change, the value
         the encode forms in registers; fp32 addition commutes, so it is the same bits as the
         reference's ``acc += change`` / ``change += acc``).  A device tensor; the selection
-        itself never reads it (the encode fuses the change), so it costs one elementwise pass."""
+        itself never reads it (the encode fuses the change), so it costs one elementwise pass,
+        written into a buffer the plugin keeps across rounds (no allocation per round)."""
         acc = self.model.accumulated_changes if self.accumulation else None
         change = self._change_dev
+        buf = getattr(self, "_mc_buf", None)
+        like = change if change is not None else self.pre_share_model
+        if buf is None or buf.shape != like.shape or buf.dtype != like.dtype:
+            buf = self._mc_buf = torch.empty_like(like)
         if change is None:
-            change = codec.elementwise(codec.DPZ_EW_SUB, self.pre_share_model, self.init_model)
+            codec.elementwise(codec.DPZ_EW_SUB, self.pre_share_model, self.init_model, out=buf)
+            change = buf
         if acc is None:
             return change
-        out = torch.empty_like(change)
         codec.elementwise(codec.DPZ_EW_ADD, acc.view(torch.float32), change.view(torch.float32),
-                          out=out.view(torch.float32))
-        return out
+                          out=buf.view(torch.float32))
+        return buf
 
     def _encode(self, k):
         """Top-k encode; returns device (idx int32[k], val fp32[k])."""
@@ -244,8 +248,7 @@ class PartialModel(Sharing):
         with torch.no_grad():
             post = getattr(self, "_post_model_dev", None)
             if post is None or not self._all_fp32:
-                flat = flatten_state(self.model.state_dict())
-                post = to_device_flat(flat, self.device, self.staging, "local")
+                post = state_to_device(self.model.state_dict(), self.device, self.staging, "local")
             self._post_model_dev = None
             self.init_model = post
             if self.accumulation:

@@ -19,7 +19,7 @@ import torch
 
 from .. import codec
 from .._device import (PayloadNames, Staging, flatten_state, h2d_array, pick_device,
-                       to_device_flat, to_host)
+                       state_to_device, to_host)
 
 
 class Sharing:
@@ -122,8 +122,7 @@ class Sharing:
     def _local_flat_device(self):
         """Current local model as a flat fp32 device vector (the fold's local term)."""
         with torch.no_grad():
-            flat = flatten_state(self.model.state_dict())
-        return to_device_flat(flat, self.device, self.staging, "local")
+            return state_to_device(self.model.state_dict(), self.device, self.staging, "local")
 
     def _h2d(self, arr, dtype, leg):
         """A host payload leg to the device through a pinned buffer (async DMA, overlapping the
@@ -156,7 +155,8 @@ class Sharing:
                                     workspace=self.workspace)
 
     def _load_flat(self, out_dev):
-        flat = to_host(out_dev, self.staging, "result")
+        # a view of the pinned buffer: load_state_dict copies it into the model at once
+        flat = to_host(out_dev, self.staging, "result", own=False)
         self.model.load_state_dict(self._unflatten(flat))
 
     def _averaging(self, peer_deques):
