@@ -33,10 +33,17 @@ namespace dpz {
 #define DPZ_LZ_BLK 2048
 #endif
 #ifndef DPZ_LZ_HASH_LOG
-#define DPZ_LZ_HASH_LOG 11
+#define DPZ_LZ_HASH_LOG 12
+#endif
+// history a block's matches may reach back into (the previous blocks' input): the frame is
+// LINKED (B.Indep = 0, python-lz4's default block mode).  0: independent blocks.
+#ifndef DPZ_LZ_WIN
+#define DPZ_LZ_WIN 14336
 #endif
 constexpr int LZ_BLK = DPZ_LZ_BLK;  // encoder block (one wave)
 constexpr int LZ_HASH_LOG = DPZ_LZ_HASH_LOG;
+constexpr int LZ_WIN = DPZ_LZ_WIN;
+static_assert(LZ_WIN % 64 == 0 && LZ_WIN + LZ_BLK < 65536, "window + block inside LZ4's 64 KB");
 static_assert(LZ_BLK >= 256 && LZ_BLK <= 65536 && (LZ_BLK & 63) == 0, "encoder block size");
 constexpr int LZ_MAXM = 1024;       // match length cap
 constexpr int LZ_MFLIMIT = 12;      // a match starts at least 12 bytes before the block end
@@ -48,7 +55,7 @@ constexpr int LZ_HDR = 15;          // magic 4 + FLG + BD + content size 8 + HC
 
 // ---- encoder --------------------------------------------------------------------------------
 struct LzEncLds {
-  uint32_t data[LZ_BLK / 4 + 2];      // the block (+8 zero bytes of slack)
+  uint32_t data[(LZ_WIN + LZ_BLK) / 4 + 2];  // history + the block (+8 zero bytes of slack)
   uint32_t table[1 << LZ_HASH_LOG];   // position + 1 of the latest occurrence (0 = none)
   uint32_t minfo[LZ_BLK];             // (match length << 16) | offset, per position
   unsigned long long mask[LZ_BLK / 64];
@@ -122,22 +129,38 @@ __global__ void __launch_bounds__(64) lz4_encode_blocks(const uint8_t* __restric
   const int64_t blk = blockIdx.x;
   const int64_t base = blk * LZ_BLK;
   const int len = (int)((n - base) < LZ_BLK ? (n - base) : LZ_BLK);
-  // stage the block (zero slack after it), zero the table and the mask
-  for (int w = lane; w < LZ_BLK / 4 + 2; w += 64) S.data[w] = 0;
+  // LDS holds [base - hist, base + len): the history the block's matches may reach (linked
+  // frame) and the block; every position below is an LDS position (the block starts at hist)
+  const int hist = (int)(base < LZ_WIN ? base : LZ_WIN);
+  for (int w = lane; w < (LZ_WIN + LZ_BLK) / 4 + 2; w += 64) S.data[w] = 0;
   __syncthreads();
-  lz_stage(reinterpret_cast<uint8_t*>(S.data), in + base, (uint32_t)len);
+  lz_stage(reinterpret_cast<uint8_t*>(S.data), in + base - hist, (uint32_t)(hist + len));
   for (int t = lane; t < (1 << LZ_HASH_LOG); t += 64) S.table[t] = 0;
   for (int t = lane; t < LZ_BLK / 64; t += 64) S.mask[t] = 0ull;
   __syncthreads();
-  const int last_start = len - LZ_MFLIMIT;  // match starts i <= last_start
-  const int mend = len - LZ_LASTLIT;        // a match ends at or before mend
-  for (int c0 = 0; c0 <= last_start; c0 += 64) {
+  // 5-byte hash (LZ4's hash5 for 64-bit targets): a candidate that agrees in 5 bytes usually
+  // extends past 4 — on index gaps ("yy 00 00 00" words) 4-byte-hash candidates give 4-5 byte
+  // matches that barely pay for their token, 5-byte ones the longer runs liblz4 finds
+  auto hash5 = [&](int i) {
+    const uint64_t v = (uint64_t)lz_read32(S.data, i) | ((uint64_t)lz_read32(S.data, i + 4) << 32);
+    return (uint32_t)(((v << 24) * 889523592379ull) >> (64 - LZ_HASH_LOG));
+  };
+  // the history's positions into the table, in order (the latest occurrence wins)
+  for (int c0 = 0; c0 < hist; c0 += 64) {
+    const int i = c0 + lane;
+    const uint32_t h = hash5(i);
+    if (i < hist) atomicMax(&S.table[h], (uint32_t)(i + 1));
+    __syncthreads();
+  }
+  const int last_start = hist + len - LZ_MFLIMIT;  // match starts i <= last_start
+  const int mend = hist + len - LZ_LASTLIT;        // a match ends at or before mend
+  for (int c0 = hist; c0 <= last_start; c0 += 64) {
     const int i = c0 + lane;
     const bool ok = i <= last_start;
     uint32_t v = 0, h = 0, cand = 0;
     if (ok) {
       v = lz_read32(S.data, i);
-      h = (v * 2654435761u) >> (32 - LZ_HASH_LOG);
+      h = hash5(i);
       cand = S.table[h];
     }
     __syncthreads();
@@ -163,26 +186,27 @@ __global__ void __launch_bounds__(64) lz4_encode_blocks(const uint8_t* __restric
         if (ml >= 4) info = ((uint32_t)ml << 16) | (uint32_t)(i - j);
       }
     }
-    if (ok) S.minfo[i] = info;
+    if (ok) S.minfo[i - hist] = info;
     const unsigned long long bal = __ballot(info != 0);
-    if (lane == 0) S.mask[c0 >> 6] = bal;
+    if (lane == 0) S.mask[(c0 - hist) >> 6] = bal;
     __syncthreads();
   }
   __syncthreads();
-  // greedy parse (wave-uniform): jump from match end to the next match start by bit scans
+  // greedy parse (wave-uniform): jump from match end to the next match start by bit scans (the
+  // mask and minfo are indexed from the block start; p, q, lit are LDS positions)
   uint32_t nseq = 0;
-  int p = 0, lit = 0;
+  int p = hist, lit = hist;
   for (;;) {
     int q = -1;
     if (p <= last_start) {
-      int wi = p >> 6;
-      unsigned long long w = S.mask[wi] & (~0ull << (p & 63));
-      const int wlast = last_start >> 6;
+      int wi = (p - hist) >> 6;
+      unsigned long long w = S.mask[wi] & (~0ull << ((p - hist) & 63));
+      const int wlast = (last_start - hist) >> 6;
       while (w == 0ull && wi < wlast) w = S.mask[++wi];
-      if (w != 0ull) q = (wi << 6) + __builtin_ctzll(w);
+      if (w != 0ull) q = hist + (wi << 6) + __builtin_ctzll(w);
     }
     if (q < 0) break;
-    const uint32_t info = S.minfo[q];
+    const uint32_t info = S.minfo[q - hist];
     const int ml = (int)(info >> 16), off = (int)(info & 0xFFFFu);
     if (lane == 0)
       S.seq[nseq] = make_uint2((uint32_t)lit | ((uint32_t)(q - lit) << 16),
@@ -192,7 +216,7 @@ __global__ void __launch_bounds__(64) lz4_encode_blocks(const uint8_t* __restric
     lit = p;
   }
   // the last sequence: literals only
-  if (lane == 0) S.seq[nseq] = make_uint2((uint32_t)lit | ((uint32_t)(len - lit) << 16), 0u);
+  if (lane == 0) S.seq[nseq] = make_uint2((uint32_t)lit | ((uint32_t)(hist + len - lit) << 16), 0u);
   __syncthreads();
   const uint32_t ns = nseq + 1;
   // sizes and offsets of the sequences (wave scan in chunks of 64)
@@ -240,7 +264,7 @@ __global__ void __launch_bounds__(64) lz4_encode_blocks(const uint8_t* __restric
   const bool raw = run >= (uint32_t)len;
   uint8_t* dst = slots + blk * LZ_BLK_OUT;
   const int outn = raw ? len : (int)run;
-  for (int t = lane; t < outn; t += 64) dst[t] = raw ? (uint8_t)lz_byte(S.data, t) : ob[t];
+  for (int t = lane; t < outn; t += 64) dst[t] = raw ? (uint8_t)lz_byte(S.data, hist + t) : ob[t];
   if (lane == 0) bsize[blk] = (uint32_t)outn | (raw ? 0x80000000u : 0u);
 }
 
@@ -463,7 +487,10 @@ constexpr int LZ_PAR_NCH = (LZ_PAR_CMAX + LZ_PAR_CHUNK - 1) / LZ_PAR_CHUNK;
 constexpr int LZ_PAR_T = 1024;                      // threads per block: 4 waves per SIMD hide the
                                                     // LDS / VALU latency of each phase (1 block per CU)
 constexpr int LZ_PAR_PPT = (LZ_PAR_CMAX + LZ_PAR_T - 1) / LZ_PAR_T;  // positions per thread
-constexpr uint16_t LZ_LIT = 0x8000u;                // src[p]: literal flag (| compressed pos)
+constexpr uint32_t LZ_LIT = 0x80000000u;            // src[p]: literal flag (| compressed pos)
+constexpr uint32_t LZ_EXT = 0x40000000u;            // src[p]: an earlier block's byte (linked
+                                                    // frames): | (65536 + source position
+                                                    // relative to this block's start, < 0)
 constexpr uint16_t LZ_BAD = 0xFFFFu;                // nxt[p]: no valid sequence at p
 constexpr uint16_t LZ_BIG = 0xFFFEu;                // nxt[p]: decodes past LZ_PAR_MAX
 
@@ -473,7 +500,7 @@ struct LzParLds {
   uint16_t ext[LZ_PAR_CMAX];
   uint16_t ooff[LZ_PAR_CMAX];              // output offset of the token at p (true tokens)
   uint8_t tok[LZ_PAR_CMAX];                // 1: a true token
-  uint16_t src[LZ_PAR_MAX];
+  uint32_t src[LZ_PAR_MAX];
   uint16_t entry[LZ_PAR_NCH];
   uint32_t wsum[16];
   uint32_t total, state, changed;          // state: 0 ok, 1 bad, 2 fallback
@@ -535,17 +562,28 @@ __device__ __forceinline__ LzSeq lz_parse_at(const uint8_t* cb, uint32_t p, uint
   return q;
 }
 
+// wslot (linked frames): per block LZ_PAR_MAX 32-bit words instead of the byte slots: a decoded
+// byte, or LZ_EXT-style reference (bit 31 | (65536 + source position relative to the block
+// start)) of a byte whose copy chain leaves the block (lz4_link_place / lz4_link_resolve finish it)
 __global__ void __launch_bounds__(LZ_PAR_T) lz4_decode_par_kernel(const uint8_t* __restrict__ in,
                                                              const LzBlock* __restrict__ blocks,
                                                              uint32_t bmax,
                                                              uint8_t* __restrict__ slots,
                                                              uint64_t* __restrict__ dsize,
-                                                             uint32_t* __restrict__ status) {
+                                                             uint32_t* __restrict__ status,
+                                                             uint32_t* __restrict__ wslot) {
+  const bool linked = wslot != nullptr;
   __shared__ LzParLds S;
   const int t = threadIdx.x, wid = t >> 6;
   const int64_t b = blockIdx.x;
   const LzBlock B = blocks[b];
   uint8_t* cb = reinterpret_cast<uint8_t*>(S.cb32);
+  if (linked && B.raw && B.csize <= (uint32_t)LZ_PAR_MAX) {  // a stored block: its bytes
+    uint32_t* wd = wslot + (uint64_t)b * LZ_PAR_MAX;
+    for (uint32_t p = t; p < B.csize; p += LZ_PAR_T) wd[p] = in[B.in_off + p];
+    if (t == 0) dsize[b] = B.csize;
+    return;
+  }
   if (B.raw || B.csize > (uint32_t)LZ_PAR_CMAX || B.csize == 0) {  // the sequential kernel's
     if (t == 0) dsize[b] = LZ_PAR_FALLBACK;
     return;
@@ -692,13 +730,16 @@ __global__ void __launch_bounds__(LZ_PAR_T) lz4_decode_par_kernel(const uint8_t*
     if (!S.tok[p]) continue;
     const LzSeq q = lz_parse_at(cb, p, cs);
     const uint32_t o = S.ooff[p];
-    for (uint32_t j = 0; j < q.L; ++j) S.src[o + j] = (uint16_t)(LZ_LIT | (q.lit + j));
+    for (uint32_t j = 0; j < q.L; ++j) S.src[o + j] = LZ_LIT | (q.lit + j);
     if (q.kind == 0) {
-      if (q.off == 0 || q.off > o + q.L) {
+      if (q.off == 0 || (!linked && q.off > o + q.L)) {
         bad = true;
         continue;
       }
-      for (uint32_t j = 0; j < q.M; ++j) S.src[o + q.L + j] = (uint16_t)(o + q.L + j - q.off);
+      for (uint32_t j = 0; j < q.M; ++j) {
+        const int32_t ps = (int32_t)(o + q.L + j) - (int32_t)q.off;  // >= -65535
+        S.src[o + q.L + j] = ps >= 0 ? (uint32_t)ps : (LZ_EXT | (uint32_t)(65536 + ps));
+      }
     }
   }
   if (bad) S.state = 1;
@@ -717,11 +758,11 @@ __global__ void __launch_bounds__(LZ_PAR_T) lz4_decode_par_kernel(const uint8_t*
     __syncthreads();
     bool ch = false;
     for (uint32_t p = t; p < total; p += LZ_PAR_T) {
-      const uint16_t v = S.src[p];
-      if (!(v & LZ_LIT)) {
-        const uint16_t u = S.src[v];  // v < p: an earlier output byte
+      const uint32_t v = S.src[p];
+      if (!(v & (LZ_LIT | LZ_EXT))) {
+        const uint32_t u = S.src[v];  // v < p: an earlier output byte
         S.src[p] = u;
-        ch |= !(u & LZ_LIT);
+        ch |= !(u & (LZ_LIT | LZ_EXT));
       }
     }
     if (ch) S.changed = 1;
@@ -730,6 +771,15 @@ __global__ void __launch_bounds__(LZ_PAR_T) lz4_decode_par_kernel(const uint8_t*
     __syncthreads();
   }
   LZST(8);
+  if (linked) {  // 7'. words out: a decoded byte, or (bit 31) a reference into earlier blocks
+    uint32_t* wd = wslot + (uint64_t)b * LZ_PAR_MAX;
+    for (uint32_t p = t; p < total; p += LZ_PAR_T) {
+      const uint32_t v = S.src[p];
+      wd[p] = (v & LZ_LIT) ? (uint32_t)cb[v & 0x7FFFu] : (0x80000000u | (v & 0x1FFFFu));
+    }
+    if (t == 0) dsize[b] = total;
+    return;
+  }
   // 7. bytes out: 4 per thread per step, one 32-bit store when whole
   uint8_t* dst = slots + (uint64_t)b * bmax;
   for (uint32_t p0 = 4 * t; p0 < total; p0 += 4 * LZ_PAR_T) {
@@ -738,7 +788,7 @@ __global__ void __launch_bounds__(LZ_PAR_T) lz4_decode_par_kernel(const uint8_t*
     for (int e = 0; e < 4; ++e) {
       const uint32_t p = p0 + e;
       if (p < total) {
-        const uint16_t v = S.src[p];
+        const uint32_t v = S.src[p];
         const uint32_t c = (v & LZ_LIT) ? cb[v & 0x7FFFu] : 0u;
         wv |= c << (8 * e);
       }
@@ -756,6 +806,91 @@ extern "C" int dpz_debug_lz4_stamps(unsigned long long* host_out) {
   return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_lz_st), sizeof(g_lz_st));
 }
 #endif
+
+// ---- linked frames on the parallel path ------------------------------------------------------
+// After lz4_decode_par_kernel (wslot), every block's words go to their frame position P (prefix of
+// the decoded sizes): w[P] = the byte, or bit 31 | the frame position its copy chain reaches in an
+// earlier block.  A block the parallel decoder left (FALLBACK) or an offset before the frame's
+// start sets *status (bit 1: re-decode the frame sequentially; bit 0: malformed).
+__global__ void __launch_bounds__(256) lz4_link_place_kernel(const uint32_t* __restrict__ wslot,
+                                                             const uint64_t* __restrict__ dsize,
+                                                             int64_t nblk, uint32_t* __restrict__ w,
+                                                             uint64_t wcap, uint64_t* __restrict__ total,
+                                                             uint32_t* __restrict__ status) {
+  __shared__ uint64_t wsum[4];
+  __shared__ uint64_t base_sh;
+  __shared__ uint32_t fb_sh;
+  const int64_t b = blockIdx.x;
+  if (threadIdx.x == 0) fb_sh = 0;
+  __syncthreads();
+  uint64_t before = 0;
+  for (int64_t c0 = 0; c0 < nblk; c0 += 256) {
+    const int64_t c = c0 + threadIdx.x;
+    const uint64_t d = c < nblk ? dsize[c] : 0ull;
+    if (d == LZ_PAR_FALLBACK) fb_sh = 1;
+    const uint64_t v = d == LZ_PAR_FALLBACK ? 0ull : d;
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan64(v, wsum, &tot);
+    if (c == b) base_sh = before + ex;
+    before += tot;
+  }
+  __syncthreads();
+  if (fb_sh) {
+    if (b == 0 && threadIdx.x == 0) atomicOr(status, 2u);
+    return;
+  }
+  const uint64_t o = base_sh, m = dsize[b];
+  bool bad = false;
+  const uint32_t* wd = wslot + (uint64_t)b * LZ_PAR_MAX;
+  for (uint64_t t = threadIdx.x; t < m; t += 256) {
+    if (o + t >= wcap) {
+      bad = true;
+      break;
+    }
+    uint32_t v = wd[t];
+    if (v & 0x80000000u) {
+      const int64_t rel = (int64_t)(v & 0x1FFFFu) - 65536;  // < 0: before the block's start
+      const int64_t s = (int64_t)o + rel;
+      if (s < 0) {
+        bad = true;
+        v = 0;
+      } else {
+        v = 0x80000000u | (uint32_t)s;
+      }
+    }
+    w[o + t] = v;
+  }
+  if (bad) atomicOr(status, 1u);
+  if (b == 0 && threadIdx.x == 0) *total = before;
+}
+
+// Every referencing word follows its chain to a byte: pointer jumping in place (each step reads the
+// referenced word: a byte ends the chain, a reference is followed; the word is rewritten with how
+// far it got, so later readers skip ahead).  References point strictly backwards and a byte never
+// changes, so any interleaving of the steps is correct; ``steps`` bounds a pass (0: to the end).
+// The last pass also writes the bytes out.
+__global__ void __launch_bounds__(256) lz4_link_resolve_kernel(uint32_t* __restrict__ w,
+                                                               const uint64_t* __restrict__ total,
+                                                               const uint32_t* __restrict__ status,
+                                                               int steps, uint8_t* __restrict__ out,
+                                                               uint64_t out_cap) {
+  if (*status) return;
+  const uint64_t n = *total;
+  for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < n;
+       p += (uint64_t)gridDim.x * 256) {
+    uint32_t v = w[p];
+    if (v & 0x80000000u) {
+      for (int s = 0; steps == 0 || s < steps; ++s) {
+        const uint32_t u = __hip_atomic_load(&w[v & 0x7FFFFFFFu], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        v = u;
+        if (!(v & 0x80000000u)) break;
+      }
+      __hip_atomic_store(&w[p], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (out && p < out_cap) out[p] = (uint8_t)v;
+  }
+}
 
 // independent frames: slot b (dsize[b] bytes at b * bmax) -> out + prefix
 __global__ void __launch_bounds__(256) lz4_gather_kernel(const uint8_t* __restrict__ slots,
@@ -887,7 +1022,9 @@ extern "C" size_t dpz_lz4_workspace_bytes(int64_t n, int64_t nblk_in, int64_t bm
   // encoder: per-block slots + sizes + offsets; decoder: block table + sizes + slots
   const int64_t nb_e = (n + LZ_BLK - 1) / LZ_BLK + 1;
   const size_t enc = (size_t)nb_e * LZ_BLK_OUT + (size_t)nb_e * 4 + (size_t)nb_e * 8 + 64;
-  const size_t dec = (size_t)(nblk_in + 1) * (sizeof(LzBlock) + 8) + (size_t)(nblk_in + 1) * bmax + 512;
+  // linked frames (bmax == 0): the parallel path's per-block words and frame-position words
+  const size_t slot_b = bmax > 0 ? (size_t)bmax : 2 * (size_t)LZ_PAR_MAX * 4;
+  const size_t dec = (size_t)(nblk_in + 1) * (sizeof(LzBlock) + 8) + (size_t)(nblk_in + 1) * slot_b + 512;
   const size_t w = enc > dec ? enc : dec;
   return (w + 255) & ~(size_t)255;
 }
@@ -906,9 +1043,10 @@ extern "C" int dpz_lz4_compress(const uint8_t* in, int64_t n, uint8_t* out, int6
   uint64_t* boff = reinterpret_cast<uint64_t*>(
       w8 + (((size_t)(nblk + 1) * LZ_BLK_OUT + (size_t)(nblk + 1) * 4 + 7) & ~(size_t)7));
   uint64_t* total = boff + nblk + 1;
-  // descriptor: FLG = version 01, B.Indep, C.Size; BD = 64 KB max block
+  // descriptor: FLG = version 01, C.Size, and B.Indep unless blocks reach into their history
+  // (LZ_WIN > 0: linked blocks, python-lz4's default); BD = 64 KB max block
   uint8_t desc[10];
-  desc[0] = 0x40 | 0x20 | 0x08;
+  desc[0] = 0x40 | (LZ_WIN > 0 ? 0 : 0x20) | 0x08;
   desc[1] = 0x40;
   for (int i = 0; i < 8; ++i) desc[2 + i] = (uint8_t)((uint64_t)n >> (8 * i));
   const uint32_t hc = (xxh32_small(desc, 10) >> 8) & 0xFF;
@@ -1049,14 +1187,46 @@ extern "C" int dpz_lz4_decompress(const uint8_t* frame_dev, const uint8_t* frame
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
     // DPZ_LZ4_PAR=0: every independent block on the sequential decoder (diagnostic build)
     const bool par = DPZ_KNOB_INT(LZ4_PAR, 1) != 0;
-    if (linked) {
+    // linked frames whose blocks fit the parallel decoder (this codec's frames: 2 KB blocks
+    // reaching 14 KB back): the blocks decode in parallel, references into earlier blocks are
+    // resolved by pointer jumping over the whole frame; otherwise (python-lz4's 64 KB blocks, or
+    // a block the parallel decoder leaves) one workgroup decodes the frame block after block
+    bool par_linked = linked && par;
+    for (int64_t bb = 0; bb < nb && par_linked; ++bb)
+      par_linked = tab_h[bb].raw ? tab_h[bb].csize <= (uint32_t)LZ_PAR_MAX
+                                 : tab_h[bb].csize <= (uint32_t)LZ_PAR_CMAX;
+    if (par_linked) {
+      uint32_t* wslot = reinterpret_cast<uint32_t*>(slots);
+      uint32_t* wfr = wslot + (size_t)nb * LZ_PAR_MAX;
+      const uint64_t wcap = (uint64_t)nb * LZ_PAR_MAX;
+      DPZ_TIMED(DPZ_KT_LZ4, st, lz4_decode_par_kernel<<<(unsigned)nb, LZ_PAR_T, 0, st>>>(
+                                    frame_dev, tab, (uint32_t)bmax, slots, dsize, status, wslot));
+      DPZ_TIMED(DPZ_KT_LZ4, st, lz4_link_place_kernel<<<(unsigned)nb, 256, 0, st>>>(
+                                    wslot, dsize, nb, wfr, wcap, total, status));
+      int64_t g = (int64_t)((wcap + 255) / 256);
+      if (g > 2048) g = 2048;
+      for (int pass = 0; pass < 2; ++pass)  // bounded passes (path compression), then the end
+        DPZ_TIMED(DPZ_KT_LZ4, st, lz4_link_resolve_kernel<<<(unsigned)g, 256, 0, st>>>(
+                                      wfr, total, status, 16, nullptr, 0));
+      DPZ_TIMED(DPZ_KT_LZ4, st, lz4_link_resolve_kernel<<<(unsigned)g, 256, 0, st>>>(
+                                    wfr, total, status, 0, out, (uint64_t)out_cap));
+      uint64_t back2[2] = {0, 0};
+      DPZ_HIP_TRY(hipMemcpyAsync(back2, status, 16, hipMemcpyDeviceToHost, st));
+      DPZ_HIP_TRY(hipStreamSynchronize(st));
+      if ((uint32_t)back2[0] & 2u) {  // a block the parallel decoder left: decode sequentially
+        DPZ_HIP_TRY(hipMemsetAsync(status, 0, 16, st));
+        par_linked = false;
+      }
+    }
+    if (linked && !par_linked) {
       DPZ_TIMED(DPZ_KT_LZ4, st, lz4_decode_kernel<<<1, 64, shm, st>>>(
                                     frame_dev, tab, nb, 1, (uint32_t)bmax, win, out,
                                     (uint64_t)out_cap, total, status, 0));
-    } else {
+    } else if (!linked) {
       if (par)
         DPZ_TIMED(DPZ_KT_LZ4, st, lz4_decode_par_kernel<<<(unsigned)nb, LZ_PAR_T, 0, st>>>(
-                                      frame_dev, tab, (uint32_t)bmax, slots, dsize, status));
+                                      frame_dev, tab, (uint32_t)bmax, slots, dsize, status,
+                                      nullptr));
       // the blocks the parallel decoder left (raw, large; all of them without it)
       DPZ_TIMED(DPZ_KT_LZ4, st, lz4_decode_kernel<<<(unsigned)nb, 64, shm, st>>>(
                                     frame_dev, tab, nb, 0, (uint32_t)bmax, win, slots,

@@ -157,3 +157,19 @@ def test_running_sum_and_delta_kernels(dev):
                                       np.cumsum(d).astype(np.int32))
         np.testing.assert_array_equal(codec.delta_i32(t).cpu().numpy(),
                                       np.diff(d, prepend=0).astype(np.int32))
+
+
+def test_c2_index_frame_within_15_percent_of_liblz4(dev):
+    """the device encoder's linked frames (2 KB blocks whose matches reach 14 KB
+    back, 5-byte hash) on a C2 payload's index gaps stay within 15 % of liblz4's linked 64 KB
+    frame (python-lz4's default), and both decoders read them."""
+    from decentralizepy_amd import codec
+    rng = np.random.default_rng(13)
+    idx = np.sort(rng.choice(11_000_000, 110_000, replace=False)).astype(np.int32)
+    gaps = np.diff(idx, prepend=0).astype(np.int32).tobytes()
+    frame = bytes(codec.lz4_compress(_dev_bytes(gaps, dev)).cpu().numpy().tobytes())
+    ref = olz4.ref_compress(gaps)
+    assert len(frame) <= 1.15 * len(ref), (len(frame), len(ref))
+    assert not (frame[4] & 0x20)  # linked blocks (B.Indep clear), python-lz4's default mode
+    assert olz4.ref_decompress(frame) == gaps
+    assert bytes(codec.lz4_decompress(frame, dev).cpu().numpy().tobytes()) == gaps
