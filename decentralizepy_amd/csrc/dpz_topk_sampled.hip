@@ -1430,6 +1430,11 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
       s, a.n, a.k, g.W, g.B, g.R, g.CAP, ctrl, ghist, segcnt, cidx, ckey, blkabove, blcnt, blkey,
       blidx, jb[1]));
   float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE) ? a.acc : nullptr;
+  // DPZ_COMPACT_ABLATE (diagnostic build only; results then differ from the reference): bit 0
+  // drops the accumulator rewind, bit 1 the counter update — per-side-effect cost of compact
+  const int ablate = (int)DPZ_KNOB_INT(COMPACT_ABLATE, 0);
+  if (ablate & 1) rewind = nullptr;
+  int32_t* const counter = (ablate & 2) ? nullptr : a.counter;
   // DPZ_COUNTER_PLAIN=0 / 1 forces the counter update form (diagnostic build, A/B)
   const bool plain = DPZ_KNOB_INT(COUNTER_PLAIN, a.k > a.n / 32 ? 1 : 0) != 0;
   // DPZ_SCATTER_FIRST=1: the decode's blocks dispatched ahead of compact's own (diagnostic, A/B)
@@ -1444,7 +1449,7 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
             (sampled_compact_kernel<VEC, PL_, SPW_><<<(unsigned)((g.W + 4 * SPW_ - 1) / (4 * SPW_)) \
                                                         + pb[2], 256, 0, a.st>>>(                 \
                 s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, \
-                cidx, ckey, cval, a.vals_src, a.idx_out, a.val_out, a.counter, rewind,            \
+                cidx, ckey, cval, a.vals_src, a.idx_out, a.val_out, counter, rewind,              \
                 a.status_out, jb[2], nrep_first, a.val_h)))
   if (plain) {
     if (spw == 8) DPZ_COMPACT(true, 8);
