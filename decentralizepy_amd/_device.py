@@ -199,5 +199,85 @@ class DeviceCounter:
         return a if dtype is None else a.astype(dtype)
 
 
+class SlicedCounter(DeviceCounter):
+    """``shared_parameters_counter`` kept as 32 bit planes (dpz_topk_encode_sliced adds the
+    selection to them with coalesced word updates); every read materialises the int32 vector
+    (dpz_counter_unslice), so the node's end-of-run dump (node/DPSGDNode.py:186-194) and any
+    indexing see the reference's counter."""
+
+    def __init__(self, planes, n):
+        self.planes = planes
+        self.n = int(n)
+
+    @property
+    def device_tensor(self):
+        from . import codec
+        return codec.counter_unslice(self.planes, self.n)
+
+    @property
+    def shape(self):
+        return torch.Size([self.n])
+
+    def __len__(self):
+        return self.n
+
+
+class DeviceAccumulator:
+    """``model.accumulated_changes`` when the encode's rewind is deferred
+    (dpz_topk_encode_sliced): ``device_tensor`` is the accumulator as the encode left it and
+    ``pending`` the selection mask whose rewind (reference models/Model.py:53-64,
+    ``accumulated_changes[indices] = 0``) the post-step applies as it adds the averaging change
+    (dpz_dwt_sym2_rewind).  Any read in between (``cpu``, ``numpy``, indexing, ``clone``)
+    settles it first — applies the rewind in place — so it always shows the reference's value."""
+
+    def __init__(self, t):
+        self.device_tensor = t
+        self.pending = None
+
+    def settle(self):
+        if self.pending is not None:
+            from . import codec
+            codec.rewind_apply(self.device_tensor, self.pending)
+            self.pending = None
+        return self.device_tensor
+
+    def zero_(self):
+        self.pending = None
+        self.device_tensor.zero_()
+        return self
+
+    def cpu(self):
+        return self.settle().cpu()
+
+    def numpy(self):
+        return self.cpu().numpy()
+
+    def tolist(self):
+        return self.numpy().tolist()
+
+    def clone(self):
+        return self.settle().clone()
+
+    def view(self, *args):
+        return self.settle().view(*args)
+
+    @property
+    def shape(self):
+        return self.device_tensor.shape
+
+    def numel(self):
+        return self.device_tensor.numel()
+
+    def __len__(self):
+        return self.device_tensor.numel()
+
+    def __getitem__(self, item):
+        return self.settle()[item]
+
+    def __array__(self, dtype=None):
+        a = self.numpy()
+        return a if dtype is None else a.astype(dtype)
+
+
 def np_int32(a):
     return np.ascontiguousarray(np.asarray(a), dtype=np.int32)

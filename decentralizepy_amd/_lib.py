@@ -68,6 +68,17 @@ SIGNATURES = {
                                         _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
                                         _int, _int, ctypes.POINTER(ctypes.c_float),
                                         ctypes.c_float, _c_void_p, _c_void_p]),
+    "dpz_mask_words": (_i64, [_i64]),
+    "dpz_topk_encode_sliced": (_int, [_c_void_p, _c_void_p, _c_void_p, _int, _c_void_p, _i64,
+                                      _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                      _size, _c_void_p, _int, _c_void_p]),
+    "dpz_counter_unslice": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
+    "dpz_counter_slice": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
+    "dpz_rewind_apply": (_int, [_c_void_p, _c_void_p, _i64, _c_void_p]),
+    "dpz_dwt_sym2_rewind": (_int, [_c_void_p, _c_void_p, _i64, _int, _c_void_p, _c_void_p,
+                                   _c_void_p]),
+    "dpz_dwt_haar_rewind": (_int, [_c_void_p, _c_void_p, _i64, _int, _c_void_p, _c_void_p,
+                                   _c_void_p]),
     "dpz_topk_threshold": (_int, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _i64, _c_void_p,
                                   _size, ctypes.POINTER(_i64), _c_void_p]),
     "dpz_mask_below_threshold": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p]),

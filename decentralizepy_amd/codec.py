@@ -22,7 +22,8 @@ __all__ = ["DPZ_ACC_NONE", "DPZ_ACC_ACCUMULATE", "DPZ_ACC_ADD", "DPZ_EW_SUB", "D
            "pack_fp16", "unpack_fp16", "elias_encode", "elias_decode",
            "KernelTimer", "NodeStepBatch", "topk_sticky_status", "rfft", "irfft", "cplx_key",
            "cplx_gather", "cplx_pair_indices", "lz4_compress", "lz4_decompress", "lz4_frame_info",
-           "delta_i32", "running_sum_i32"]
+           "delta_i32", "running_sum_i32", "mask_words", "topk_encode_sliced", "counter_unslice",
+           "counter_slice", "rewind_apply"]
 
 
 def _ptr(t):
@@ -181,6 +182,90 @@ def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, c
         _ptr(r_val), r_idx.numel(), r_n, _ptr(r_out), _ptr(dws), dws.numel(), _stream(x.device))
     check(rc, "dpz_topk_encode_replace")
     return idx_out, val_out
+
+
+def mask_words(n):
+    """uint32 words of a selection mask over n elements (ceil(n / 32)); held as int32 tensors."""
+    return int(_lib.lib().dpz_mask_words(int(n)))
+
+
+def topk_encode_sliced(x, k, sel_mask, planes=None, x0=None, acc=None, acc_mode=DPZ_ACC_NONE,
+                       vals_src=None, idx_out=None, val_out=None, workspace=None, exact=False,
+                       status_out=None, shared=False, val_fp16=False):
+    """The selection of :func:`topk_encode` with its bookkeeping in coalesced form
+    (dpz_topk_encode_sliced; reference Wavelet.py:194-197): ``planes`` (int32[32 * mask_words(n)],
+    the bit-sliced shared_parameters_counter, or None) += 1 at the selected indices, and
+    ``sel_mask`` (int32[mask_words(n)]) gets the selected bits — the accumulator rewind is left
+    to the caller's next accumulating pass (``wavedec(..., rewind_mask=sel_mask)``) or
+    :func:`rewind_apply`.  ``acc`` (DPZ_ACC_ADD) is only read.  Blocking unless ``status_out``
+    (then asynchronous: a nonzero status means re-run with ``exact=True``)."""
+    _require(x, torch.float32, "x")
+    _require(x0, torch.float32, "x0")
+    _require(acc, torch.float32, "acc")
+    _require(sel_mask, torch.int32, "sel_mask")
+    _require(planes, torch.int32, "planes")
+    n = x.numel()
+    k = int(k)
+    nw = mask_words(n)
+    if sel_mask.numel() < nw or (planes is not None and planes.numel() < 32 * nw):
+        raise ValueError("sel_mask / planes too small for n")
+    if vals_src is None:
+        vals_src = x
+    _require(vals_src, torch.float32, "vals_src")
+    if idx_out is None:
+        idx_out = torch.empty(k, dtype=torch.int32, device=x.device)
+    vdt = torch.float16 if val_fp16 else torch.float32
+    if val_out is None:
+        val_out = torch.empty(k, dtype=vdt, device=x.device)
+    _require(val_out, vdt, "val_out")
+    _require(status_out, torch.int32, "status_out")
+    ws = (workspace or Workspace(x.device)).get(n, k)
+    flags = ((DPZ_TOPK_EXACT if exact else 0) | (_lib.DPZ_TOPK_SHARED if shared else 0)
+             | (_lib.DPZ_TOPK_VAL_FP16 if val_fp16 else 0))
+    rc = _lib.lib().dpz_topk_encode_sliced(
+        _ptr(x), _ptr(x0), _ptr(acc), int(acc_mode), _ptr(vals_src), n, k, _ptr(idx_out),
+        _ptr(val_out), _ptr(planes), _ptr(sel_mask), _ptr(ws), ws.numel(), _ptr(status_out),
+        flags, _stream(x.device))
+    check(rc, "dpz_topk_encode_sliced")
+    return idx_out, val_out
+
+
+def counter_unslice(planes, n, out=None):
+    """int32[n] counter from its bit planes (dpz_counter_unslice)."""
+    _require(planes, torch.int32, "planes")
+    if out is None:
+        out = torch.empty(int(n), dtype=torch.int32, device=planes.device)
+    _require(out, torch.int32, "out")
+    if planes.numel() < 32 * mask_words(n) or out.numel() < int(n):
+        raise ValueError("counter_unslice: size mismatch")
+    check(_lib.lib().dpz_counter_unslice(_ptr(planes), int(n), _ptr(out), _stream(out.device)),
+          "dpz_counter_unslice")
+    return out
+
+
+def counter_slice(counter, planes=None):
+    """Bit planes (int32[32 * mask_words(n)]) of an int32 counter (dpz_counter_slice)."""
+    _require(counter, torch.int32, "counter")
+    n = counter.numel()
+    if planes is None:
+        planes = torch.empty(32 * mask_words(n), dtype=torch.int32, device=counter.device)
+    _require(planes, torch.int32, "planes")
+    if planes.numel() < 32 * mask_words(n):
+        raise ValueError("counter_slice: planes too small")
+    check(_lib.lib().dpz_counter_slice(_ptr(counter), n, _ptr(planes), _stream(counter.device)),
+          "dpz_counter_slice")
+    return planes
+
+
+def rewind_apply(acc, sel_mask):
+    """acc[i] = 0 where sel_mask has bit i (the deferred rewind on its own, dpz_rewind_apply)."""
+    _require(acc, torch.float32, "acc")
+    _require(sel_mask, torch.int32, "sel_mask")
+    if sel_mask.numel() < mask_words(acc.numel()):
+        raise ValueError("rewind_apply: mask too small")
+    check(_lib.lib().dpz_rewind_apply(_ptr(acc), _ptr(sel_mask), acc.numel(), _stream(acc.device)),
+          "dpz_rewind_apply")
+    return acc
 
 
 def topk_complete(x, k, idx_out, val_out, workspace, x0=None, acc=None, acc_mode=DPZ_ACC_NONE,
@@ -401,13 +486,32 @@ def wavedec_len(n, level=4, wavelet="sym2"):
 
 
 def wavedec(x, level=4, x0=None, want_x=True, coeffs_x=None, coeffs_diff=None, accumulate=False,
-            wavelet="sym2"):
+            wavelet="sym2", rewind_mask=None):
     """Multilevel DWT (``wavelet`` "sym2" or "haar", mode "symmetric") as one
     ``coeffs_to_array`` vector (reference Wavelet.py:12-32).
 
     Returns ``(W(x) or None, W(x - x0) or None)``; with ``accumulate=True`` adds W(x - x0) into
-    ``coeffs_diff`` instead of overwriting it.
+    ``coeffs_diff`` instead of overwriting it.  ``rewind_mask`` (with ``accumulate``, no W(x)): the
+    selection mask of :func:`topk_encode_sliced` — the deferred rewind is applied first,
+    ``acc = (selected ? 0 : acc) + W(x - x0)`` (dpz_dwt_sym2_rewind / dpz_dwt_haar_rewind).
     """
+    if rewind_mask is not None:
+        if not accumulate or want_x or coeffs_diff is None or x0 is None:
+            raise ValueError("rewind_mask: an accumulating W(x - x0) pass into coeffs_diff only")
+        _require(x, torch.float32, "x")
+        _require(x0, torch.float32, "x0")
+        _require(coeffs_diff, torch.float32, "coeffs_diff")
+        _require(rewind_mask, torch.int32, "rewind_mask")
+        n = x.numel()
+        m = wavedec_len(n, level, wavelet)
+        if coeffs_diff.numel() != m or x0.numel() != n or rewind_mask.numel() < mask_words(m):
+            raise ValueError("rewind_mask: size mismatch")
+        fn = (_lib.lib().dpz_dwt_sym2_rewind if wavelet == "sym2"
+              else _lib.lib().dpz_dwt_haar_rewind)
+        rc = fn(_ptr(x), _ptr(x0), n, int(level), _ptr(coeffs_diff), _ptr(rewind_mask),
+                _stream(x.device))
+        check(rc, f"dpz_dwt_{wavelet}_rewind")
+        return None, coeffs_diff
     _require(x, torch.float32, "x")
     _require(x0, torch.float32, "x0")
     n = x.numel()

@@ -46,7 +46,18 @@ struct Levels {
   int64_t doff[DWT_MAX_LEVEL + 1];  // offset of cD_l in the coefficient array
   int64_t total;
   int level;
+  // accumulate with the deferred rewind (dpz_dwt_sym2_rewind): acc[i] = (bit i ? 0 : acc[i]) + c
+  const uint32_t* rmask;
 };
+
+// the accumulator's value before this pass adds to it: 0 where the encode selected the
+// coefficient (reference: rewind_accumulation zeroed it during the step, models/Model.py:53-64,
+// and the post-step adds 0 + c — kept as a real addition so -0.0 becomes +0.0 as there)
+__device__ __forceinline__ float acc_before(const Levels& LV, const float* dst, int64_t pos) {
+  const float o = *dst;
+  if (LV.rmask && ((LV.rmask[pos >> 5] >> (pos & 31)) & 1u)) return 0.0f;
+  return o;
+}
 
 static inline Levels make_levels(int64_t n, int level) {
   Levels L{};
@@ -243,11 +254,11 @@ __device__ __forceinline__ void dwt_levels(const Levels& LV, float* cx, float* c
         if (l < L) outb[1][r] = conv4r(in[1], i, c_dec_lo, lo_odd);
         if (own) {
           const float dv = conv4r(in[1], i, c_dec_hi, lo_odd);
-          if (ACCUM) cdd[r] = cdd[r] + dv; else cdd[r] = dv;
+          if (ACCUM) cdd[r] = acc_before(LV, cdd + r, LV.doff[l] + sl + r) + dv; else cdd[r] = dv;
         }
         if (l == L && own) {
           const float av = conv4r(in[1], i, c_dec_lo, lo_odd);
-          if (ACCUM) cda[r] = cda[r] + av; else cda[r] = av;
+          if (ACCUM) cda[r] = acc_before(LV, cda + r, sl + r) + av; else cda[r] = av;
         }
       }
     }
@@ -365,8 +376,8 @@ __device__ __forceinline__ void dwt_int_level1(const Levels& LV, float* cx, floa
         const float hi1 = conv4v(v[2], v[3], v[4], v[5], c_dec_hi);
         float* dst = (sp == 0 ? cx : cd) + LV.doff[1] + o;
         if (ACCUM && sp == 1) {
-          dst[0] = dst[0] + hi0;
-          dst[1] = dst[1] + hi1;
+          dst[0] = acc_before(LV, dst, LV.doff[1] + o) + hi0;
+          dst[1] = acc_before(LV, dst + 1, LV.doff[1] + o + 1) + hi1;
         } else {
           dst[0] = hi0;
           dst[1] = hi1;
@@ -400,8 +411,8 @@ __device__ __forceinline__ void dwt_int_level(const Levels& LV, float* cx, float
       if (TOP) {
         if (u >= u_own) {
           float* dst = g + pos;
-          dst[0] = acc ? dst[0] + lo0 : lo0;
-          dst[1] = acc ? dst[1] + lo1 : lo1;
+          dst[0] = acc ? acc_before(LV, dst, pos) + lo0 : lo0;
+          dst[1] = acc ? acc_before(LV, dst + 1, pos + 1) + lo1 : lo1;
         }
       } else {
         *reinterpret_cast<float2*>(out[sp] + u) = make_float2(lo0, lo1);
@@ -410,8 +421,8 @@ __device__ __forceinline__ void dwt_int_level(const Levels& LV, float* cx, float
         const float hi0 = conv4v(A.x, A.y, B.x, B.y, c_dec_hi);
         const float hi1 = conv4v(B.x, B.y, B.z, B.w, c_dec_hi);
         float* dst = g + LV.doff[l] + pos;
-        dst[0] = acc ? dst[0] + hi0 : hi0;
-        dst[1] = acc ? dst[1] + hi1 : hi1;
+        dst[0] = acc ? acc_before(LV, dst, LV.doff[l] + pos) + hi0 : hi0;
+        dst[1] = acc ? acc_before(LV, dst + 1, LV.doff[l] + pos + 1) + hi1 : hi1;
       }
     }
   }
@@ -698,14 +709,15 @@ extern "C" int64_t dpz_wavedec_len(int64_t n, int level) {
 extern "C" int64_t dpz_dwt_tile_width(void) { return DWT_TL; }
 extern "C" int64_t dpz_idwt_tile_width(void) { return IDWT_TILE; }
 
-extern "C" int dpz_dwt_sym2_tiles(const float* x, const float* x0, int64_t n, int level,
-                                  int64_t tile_lo, int64_t tile_hi, float* coeffs_x,
-                                  float* coeffs_diff, int accumulate, dpz_stream_t stream) {
+static int dwt_sym2_run(const float* x, const float* x0, int64_t n, int level, int64_t tile_lo,
+                        int64_t tile_hi, float* coeffs_x, float* coeffs_diff, int accumulate,
+                        const uint32_t* rmask, dpz_stream_t stream) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (!x || n <= 0) return DPZ_ERR_ARG;
   if (!dwt_levels_ok(n, level) || level > 4) return DPZ_ERR_UNSUPPORTED;
   if (coeffs_diff && !x0) return DPZ_ERR_ARG;
-  const Levels LV = make_levels(n, level);
+  Levels LV = make_levels(n, level);
+  LV.rmask = accumulate ? rmask : nullptr;
   const int64_t ntiles = (LV.len[level] + DWT_TL - 1) / DWT_TL;
   if (tile_lo < 0 || tile_hi > ntiles || tile_lo > tile_hi) return DPZ_ERR_ARG;
   if ((!coeffs_x && !coeffs_diff) || tile_lo == tile_hi) return DPZ_OK;
@@ -747,6 +759,13 @@ extern "C" int dpz_dwt_sym2_tiles(const float* x, const float* x0, int64_t n, in
   return DPZ_OK;
 }
 
+extern "C" int dpz_dwt_sym2_tiles(const float* x, const float* x0, int64_t n, int level,
+                                  int64_t tile_lo, int64_t tile_hi, float* coeffs_x,
+                                  float* coeffs_diff, int accumulate, dpz_stream_t stream) {
+  return dwt_sym2_run(x, x0, n, level, tile_lo, tile_hi, coeffs_x, coeffs_diff, accumulate,
+                      nullptr, stream);
+}
+
 extern "C" int dpz_dwt_sym2(const float* x, const float* x0, int64_t n, int level,
                             float* coeffs_x, float* coeffs_diff, int accumulate,
                             dpz_stream_t stream) {
@@ -754,8 +773,17 @@ extern "C" int dpz_dwt_sym2(const float* x, const float* x0, int64_t n, int leve
   if (!dwt_levels_ok(n, level) || level > 4) return DPZ_ERR_UNSUPPORTED;
   const Levels LV = make_levels(n, level);
   const int64_t ntiles = (LV.len[level] + DWT_TL - 1) / DWT_TL;
-  return dpz_dwt_sym2_tiles(x, x0, n, level, 0, ntiles, coeffs_x, coeffs_diff, accumulate,
-                            stream);
+  return dwt_sym2_run(x, x0, n, level, 0, ntiles, coeffs_x, coeffs_diff, accumulate, nullptr,
+                      stream);
+}
+
+extern "C" int dpz_dwt_sym2_rewind(const float* x, const float* x0, int64_t n, int level,
+                                   float* acc, const uint32_t* sel_mask, dpz_stream_t stream) {
+  if (!x || !x0 || !acc || !sel_mask || n <= 0) return DPZ_ERR_ARG;
+  if (!dwt_levels_ok(n, level) || level > 4) return DPZ_ERR_UNSUPPORTED;
+  const Levels LV = make_levels(n, level);
+  const int64_t ntiles = (LV.len[level] + DWT_TL - 1) / DWT_TL;
+  return dwt_sym2_run(x, x0, n, level, 0, ntiles, nullptr, acc, 1, sel_mask, stream);
 }
 
 extern "C" int dpz_idwt_sym2_tiles(const float* coeffs, int64_t n, int level, int64_t tile_lo,

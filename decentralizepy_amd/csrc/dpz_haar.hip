@@ -32,7 +32,18 @@ struct HaarLevels {
   int64_t doff[HAAR_MAX_LEVEL + 1];
   int64_t total;
   int level;
+  const uint32_t* rmask;  // dpz_dwt_haar_rewind: acc = (selected ? 0 : acc) + c
 };
+
+// the accumulator before this pass adds to it: 0 at a coefficient the encode selected (the
+// deferred rewind; 0 + c as the reference computes it)
+__device__ __forceinline__ float hacc_before(const HaarLevels& LV, const float* base,
+                                             const float* p) {
+  const float o = *p;
+  const int64_t pos = p - base;
+  if (LV.rmask && ((LV.rmask[pos >> 5] >> (pos & 31)) & 1u)) return 0.0f;
+  return o;
+}
 
 static inline HaarLevels haar_levels(int64_t n, int level) {
   HaarLevels L{};
@@ -118,10 +129,10 @@ __global__ void __launch_bounds__(256) haar_dwt_kernel(const float* __restrict__
           if (q + j < LV.len[1]) {
             if (L == 1) {
               float* pa = out + q + j;
-              *pa = acc ? *pa + lo : lo;
+              *pa = acc ? hacc_before(LV, out, pa) + lo : lo;
             }
             float* pd = out + LV.doff[1] + q + j;
-            *pd = acc ? *pd + hi : hi;
+            *pd = acc ? hacc_before(LV, out, pd) + hi : hi;
           }
         }
       }
@@ -145,10 +156,10 @@ __global__ void __launch_bounds__(256) haar_dwt_kernel(const float* __restrict__
         if (r < LV.len[2]) {
           if (L == 2) {
             float* pa = out + r;
-            *pa = acc ? *pa + lo : lo;
+            *pa = acc ? hacc_before(LV, out, pa) + lo : lo;
           }
           float* pd = out + LV.doff[2] + r;
-          *pd = acc ? *pd + hi : hi;
+          *pd = acc ? hacc_before(LV, out, pd) + hi : hi;
         }
       }
       // levels 3..L: lane pairs (stride s2) across the wave; the lane holds the level-(l-1) value
@@ -176,10 +187,10 @@ __global__ void __launch_bounds__(256) haar_dwt_kernel(const float* __restrict__
             if (o < LV.len[l]) {
               if (l == L) {
                 float* pa = out + o;
-                *pa = acc ? *pa + lo : lo;
+                *pa = acc ? hacc_before(LV, out, pa) + lo : lo;
               }
               float* pd = out + LV.doff[l] + o;
-              *pd = acc ? *pd + hi : hi;
+              *pd = acc ? hacc_before(LV, out, pd) + hi : hi;
             }
           }
         }
@@ -257,15 +268,16 @@ extern "C" int64_t dpz_haar_wavedec_len(int64_t n, int level) {
   return haar_levels(n, level).total;
 }
 
-extern "C" int dpz_dwt_haar(const float* x, const float* x0, int64_t n, int level,
-                            float* coeffs_x, float* coeffs_diff, int accumulate,
-                            dpz_stream_t stream) {
+static int dwt_haar_run(const float* x, const float* x0, int64_t n, int level, float* coeffs_x,
+                        float* coeffs_diff, int accumulate, const uint32_t* rmask,
+                        dpz_stream_t stream) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (!x || n <= 0) return DPZ_ERR_ARG;
   if (level < 1 || level > HAAR_MAX_LEVEL) return DPZ_ERR_UNSUPPORTED;
   if (coeffs_diff && !x0) return DPZ_ERR_ARG;
   if (!coeffs_x && !coeffs_diff) return DPZ_OK;
-  const HaarLevels LV = haar_levels(n, level);
+  HaarLevels LV = haar_levels(n, level);
+  LV.rmask = accumulate ? rmask : nullptr;
   const int64_t nchunks = (n + HAAR_CHUNK - 1) / HAAR_CHUNK;
   const int vec = aligned16(x) && (!coeffs_diff || aligned16(x0));
   const unsigned g = haar_grid((nchunks + HAAR_UNROLL - 1) / HAAR_UNROLL);
@@ -283,6 +295,18 @@ extern "C" int dpz_dwt_haar(const float* x, const float* x0, int64_t n, int leve
   DPZ_LAUNCH_CHECK();
   timing_end(tslot, st);
   return DPZ_OK;
+}
+
+extern "C" int dpz_dwt_haar(const float* x, const float* x0, int64_t n, int level,
+                            float* coeffs_x, float* coeffs_diff, int accumulate,
+                            dpz_stream_t stream) {
+  return dwt_haar_run(x, x0, n, level, coeffs_x, coeffs_diff, accumulate, nullptr, stream);
+}
+
+extern "C" int dpz_dwt_haar_rewind(const float* x, const float* x0, int64_t n, int level,
+                                   float* acc, const uint32_t* sel_mask, dpz_stream_t stream) {
+  if (!x0 || !acc || !sel_mask) return DPZ_ERR_ARG;
+  return dwt_haar_run(x, x0, n, level, nullptr, acc, 1, sel_mask, stream);
 }
 
 extern "C" int dpz_idwt_haar(const float* coeffs, int64_t n, int level, float* out,

@@ -210,7 +210,9 @@ static inline FastGeom fast_geom(int64_t n, int64_t k = 0, bool shared = false) 
   if (W > wmax) W = wmax;
   if (W < 1) W = 1;
   int64_t R = (n + W - 1) / W;
-  R = (R + 3) & ~int64_t(3);
+  // a multiple of 32: every 32-element word of a selection mask / sliced counter belongs to one
+  // wave segment (dpz_topk_encode_sliced), and of 4 for the float4 streams
+  R = (R + 31) & ~int64_t(31);
   W = (n + R - 1) / R;
   int64_t cap = ((R / 4) + 63) & ~int64_t(63);
   if (k > n / 16) {
@@ -278,7 +280,18 @@ struct EncodeArgs {
   int val_h;              // DPZ_TOPK_VAL_FP16: val_out holds fp16 values (RNE)
   const FoldBase* fbase;  // dpz_topk_encode_foldbase: the pipelined filter also writes
   float* base_out;        // base_out[j] = fbase->of(x[j]) (sampled path, fused_foldbase_ok)
+  // dpz_topk_encode_sliced: the side effects in coalesced form — selmask (ceil(n/32) words, every
+  // word written: bit = selected) instead of the rewind, planes (the counter as 32 bit planes of
+  // ceil(n/32) words) += 1 instead of counter[idx] += 1; counter and the rewind are then unused
+  uint32_t* selmask;
+  uint32_t* planes;
 };
+// the sampled compact builds a segment's mask words in LDS: segments of at most this many elements
+constexpr int64_t SL_RMAX = 8192;
+static inline int64_t mask_words(int64_t n) { return (n + 31) >> 5; }
+// sliced side effects from idx_out (the exact path, a sampled miss, segments over SL_RMAX):
+// selmask zeroed, bits set from idx_out[0..k), planes += selmask (dpz_topk.hip)
+int sliced_from_idx(const EncodeArgs& a);
 // the fold base can ride on the pipelined filter: aligned, no accumulation, x0 given
 bool fused_foldbase_ok(const EncodeArgs& a, bool vec);
 // base_out[j] = fb.of(x[j]) as its own launch (dpz_fold.hip)

@@ -243,6 +243,181 @@ extern "C" int dpz_topk_encode_replace(const float* x, const float* x0, float* a
   return dpz_topk_dispatch(a, flags);
 }
 
+// ---- coalesced side effects (dpz_topk_encode_sliced) ------------------------------------------
+namespace dpz {
+
+static unsigned grid_of(int64_t items, int64_t cap = 8192) {
+  int64_t g = (items + 255) / 256;
+  if (g > cap) g = cap;
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
+// bit idx of mask for every selected index (the exact path / a sampled miss: the sorted indices
+// are unique, the atomics go to distinct bits)
+__global__ void __launch_bounds__(256) selmask_from_idx_kernel(const int32_t* __restrict__ idx,
+                                                               int64_t k, uint32_t* mask) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < k; i += (int64_t)gridDim.x * 256) {
+    const uint32_t v = (uint32_t)idx[i];
+    atomicOr(&mask[v >> 5], 1u << (v & 31));
+  }
+}
+
+// planes += mask, word by word (ripple carry over the bit planes; stops at the first plane with
+// no carry left, usually within two or three)
+__global__ void __launch_bounds__(256) planes_add_kernel(uint32_t* planes,
+                                                         const uint32_t* __restrict__ mask,
+                                                         int64_t nw) {
+  for (int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x; w < nw; w += (int64_t)gridDim.x * 256) {
+    uint32_t carry = mask[w];
+    for (int p = 0; p < 32 && carry != 0u; ++p) {
+      uint32_t* const a = planes + (int64_t)p * nw + w;
+      const uint32_t old = *a;
+      *a = old ^ carry;
+      carry &= old;
+    }
+  }
+}
+
+// counter[i] = sum_p bit(planes[p][i / 32], i % 32) << p
+__global__ void __launch_bounds__(256) counter_unslice_kernel(const uint32_t* __restrict__ planes,
+                                                              int64_t n, int64_t nw,
+                                                              int32_t* out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t w = i >> 5;
+    const uint32_t b = (uint32_t)(i & 31);
+    uint32_t v = 0;
+#pragma unroll 8
+    for (int p = 0; p < 32; ++p) v |= ((planes[(int64_t)p * nw + w] >> b) & 1u) << p;
+    out[i] = (int32_t)v;
+  }
+}
+
+// planes from an int32 counter: one word (32 counters) per thread
+__global__ void __launch_bounds__(256) counter_slice_kernel(const int32_t* __restrict__ c,
+                                                            int64_t n, int64_t nw,
+                                                            uint32_t* planes) {
+  for (int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x; w < nw; w += (int64_t)gridDim.x * 256) {
+    uint32_t v[32];
+#pragma unroll
+    for (int b = 0; b < 32; ++b) {
+      const int64_t i = w * 32 + b;
+      v[b] = i < n ? (uint32_t)c[i] : 0u;
+    }
+#pragma unroll
+    for (int p = 0; p < 32; ++p) {
+      uint32_t word = 0;
+#pragma unroll
+      for (int b = 0; b < 32; ++b) word |= ((v[b] >> p) & 1u) << b;
+      planes[(int64_t)p * nw + w] = word;
+    }
+  }
+}
+
+// acc[i] = 0 where the mask bit is set (the deferred rewind on its own)
+__global__ void __launch_bounds__(256) rewind_apply_kernel(float* acc,
+                                                           const uint32_t* __restrict__ mask,
+                                                           int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    if ((mask[i >> 5] >> (i & 31)) & 1u) acc[i] = 0.0f;
+}
+
+int sliced_from_idx(const EncodeArgs& a) {
+  const int64_t nw = mask_words(a.n);
+  DPZ_HIP_TRY(hipMemsetAsync(a.selmask, 0, (size_t)nw * 4, a.st));
+  if (a.k > 0)
+    DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st,
+              selmask_from_idx_kernel<<<grid_of(a.k), 256, 0, a.st>>>(a.idx_out, a.k, a.selmask));
+  if (a.planes && a.k > 0)
+    DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st,
+              planes_add_kernel<<<grid_of(nw), 256, 0, a.st>>>(a.planes, a.selmask, nw));
+  return DPZ_OK;
+}
+
+}  // namespace dpz
+
+extern "C" int64_t dpz_mask_words(int64_t n) { return n > 0 ? mask_words(n) : 0; }
+
+extern "C" int dpz_topk_encode_sliced(const float* x, const float* x0, const float* acc,
+                                      int acc_mode, const float* vals_src, int64_t n, int64_t k,
+                                      int32_t* idx_out, float* val_out, uint32_t* planes,
+                                      uint32_t* sel_mask, void* ws, size_t ws_bytes,
+                                      int32_t* status_out, int flags, dpz_stream_t stream) {
+  if (acc_mode != DPZ_ACC_NONE && acc_mode != DPZ_ACC_ADD) return DPZ_ERR_ARG;
+  if (flags & ~(DPZ_TOPK_EXACT | DPZ_TOPK_SHARED | DPZ_TOPK_VAL_FP16)) return DPZ_ERR_ARG;
+  // acc is only read (ADD): the rewind is the caller's, through sel_mask
+  EncodeArgs a{x, x0, const_cast<float*>(acc), acc_mode, vals_src, n, k, idx_out, val_out, nullptr,
+               static_cast<char*>(ws), static_cast<hipStream_t>(stream)};
+  int rc = validate(a, ws_bytes);
+  if (rc != DPZ_OK) return rc;
+  if (n > 0 && !sel_mask) return DPZ_ERR_ARG;
+  const size_t mb = (size_t)mask_words(n) * 4;
+  if (overlaps(sel_mask, mb, planes, mb * 32) || overlaps(sel_mask, mb, ws, ws_bytes) ||
+      overlaps(planes, mb * 32, ws, ws_bytes))
+    return DPZ_ERR_ARG;
+  a.shared = (flags & DPZ_TOPK_SHARED) != 0;
+  a.val_h = (flags & DPZ_TOPK_VAL_FP16) ? 1 : 0;
+  a.selmask = sel_mask;
+  a.planes = planes;
+  if (n == 0) {
+    if (status_out) DPZ_HIP_TRY(hipMemsetAsync(status_out, 0, sizeof(int32_t), a.st));
+    return DPZ_OK;
+  }
+  const WsLayout L = ws_layout(n, k, a.shared);
+  const bool vec = all_aligned(a);
+  if (!(flags & DPZ_TOPK_EXACT) && use_sampled(n, k) && L.fg.R <= SL_RMAX) {
+    a.status_out = status_out;
+    rc = run_sampled(a, L, vec, 3);
+    if (rc != DPZ_OK) return rc;
+    if (status_out) return DPZ_OK;  // asynchronous: a nonzero status -> re-run with EXACT
+    DPZ_HIP_TRY(hipStreamSynchronize(a.st));
+    uint32_t st = 0;
+    DPZ_HIP_TRY(hipMemcpy(&st, a.ws + L.ctrl + offsetof(TopkCtrl, status), sizeof(st),
+                          hipMemcpyDeviceToHost));
+    if (st == 0) return DPZ_OK;
+    a.status_out = nullptr;  // the miss wrote nothing: the exact path below
+  }
+  if (k > 0) {
+    rc = run_exact(a, L, 0, vec);
+    if (rc != DPZ_OK) return rc;
+  }
+  rc = sliced_from_idx(a);
+  if (rc != DPZ_OK) return rc;
+  if (status_out) DPZ_HIP_TRY(hipMemsetAsync(status_out, 0, sizeof(int32_t), a.st));
+  else DPZ_HIP_TRY(hipStreamSynchronize(a.st));
+  return DPZ_OK;
+}
+
+extern "C" int dpz_counter_slice(const int32_t* counter, int64_t n, uint32_t* planes,
+                                 dpz_stream_t stream) {
+  if (n < 0 || (n > 0 && (!counter || !planes))) return DPZ_ERR_ARG;
+  if (n == 0) return DPZ_OK;
+  const int64_t nw = mask_words(n);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  counter_slice_kernel<<<grid_of(nw), 256, 0, st>>>(counter, n, nw, planes);
+  DPZ_HIP_TRY(hipGetLastError());
+  return DPZ_OK;
+}
+
+extern "C" int dpz_counter_unslice(const uint32_t* planes, int64_t n, int32_t* counter,
+                                   dpz_stream_t stream) {
+  if (n < 0 || (n > 0 && (!counter || !planes))) return DPZ_ERR_ARG;
+  if (n == 0) return DPZ_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  counter_unslice_kernel<<<grid_of(n), 256, 0, st>>>(planes, n, mask_words(n), counter);
+  DPZ_HIP_TRY(hipGetLastError());
+  return DPZ_OK;
+}
+
+extern "C" int dpz_rewind_apply(float* acc, const uint32_t* sel_mask, int64_t n,
+                                dpz_stream_t stream) {
+  if (n < 0 || (n > 0 && (!acc || !sel_mask))) return DPZ_ERR_ARG;
+  if (n == 0) return DPZ_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  rewind_apply_kernel<<<grid_of(n), 256, 0, st>>>(acc, sel_mask, n);
+  DPZ_HIP_TRY(hipGetLastError());
+  return DPZ_OK;
+}
+
 extern "C" int dpz_topk_threshold(const float* x, int64_t n, int64_t k, int32_t* idx_out,
                                   float* val_out, int64_t cap, void* ws, size_t ws_bytes,
                                   int64_t* count, dpz_stream_t stream) {

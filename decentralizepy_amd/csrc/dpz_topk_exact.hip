@@ -228,7 +228,8 @@ static int run_exact_t(const EncodeArgs& a, const WsLayout& L, int rekey, int ke
   uint32_t* beqb = reinterpret_cast<uint32_t*>(a.ws + L.ex_eqb);
   DPZ_TIMED(DPZ_KT_EXACT_COUNT, a.st, exact_count_kernel<VEC><<<(unsigned)L.ex_nblk, 256, 0, a.st>>>(s, a.n, ctrl, bgt, beq));
   DPZ_TIMED(DPZ_KT_EXACT_SCAN, a.st, exact_scan_kernel<<<1, 1024, 0, a.st>>>(ctrl, L.ex_nblk, bgt, beq, boff, beqb, keep_ties));
-  float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE) ? a.acc : nullptr;
+  // sliced side effects (dpz_topk_encode_sliced): no rewind here, the caller applies selmask
+  float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE && !a.selmask) ? a.acc : nullptr;
   DPZ_TIMED(DPZ_KT_EXACT_WRITE, a.st, exact_write_kernel<VEC><<<(unsigned)L.ex_nblk, 256, 0, a.st>>>(
       s, a.n, ctrl, boff, beqb, a.vals_src, a.idx_out, a.val_out, a.counter, rewind,
       keep_ties ? cap : a.k, keep_ties, a.val_h));

@@ -956,7 +956,8 @@ __device__ __forceinline__ void dense_write(const KeySrc s, int64_t seg, int64_t
                                                       uint32_t T, uint32_t icut, uint32_t run,
                                                       const float* vals_src, int32_t* idx_out,
                                                       float* val_out, int32_t* counter,
-                                                      float* rewind, int val_h) {
+                                                      float* rewind, int val_h,
+                                                      uint32_t* slrow) {
   const int lane = threadIdx.x & 63;
   const int64_t beg = seg * R;
   const int64_t end = (beg + R < n) ? beg + R : n;
@@ -981,6 +982,7 @@ __device__ __forceinline__ void dense_write(const KeySrc s, int64_t seg, int64_t
           const int64_t i = i0 + e;
           idx_out[pos] = (int32_t)i;
           store_val(val_out, val_h, pos, vals_src[i]);
+          if (slrow) atomicOr(&slrow[(i - beg) >> 5], 1u << (i & 31));
           if (counter) atomicAdd(&counter[i], 1);
           if (rewind) rewind[i] = 0.0f;
         }
@@ -1016,7 +1018,11 @@ struct CompactCfg {
   static constexpr int PFC = SPW >= 8 ? 1 : 4;  // chunks of 64 per segment held in registers
 };
 
-template <bool VEC, bool PLAIN, int SPW>
+// SL (dpz_topk_encode_sliced): no scattered counter / rewind; each wave ORs its segment's
+// selected bits into an LDS row (R <= SL_RMAX, R a multiple of 32: the segment owns whole
+// words), then writes every word of the row to selmask and adds it to the bit-sliced counter
+// (planes[p * nwords + w], carry-propagated plane by plane) with coalesced accesses.
+template <bool VEC, bool PLAIN, int SPW, bool SL>
 __global__ void __launch_bounds__(256, SPW >= 8 ? 1 : 4) sampled_compact_kernel(
     KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl,
     uint32_t* chist, const uint32_t* __restrict__ blkabove, const uint32_t* __restrict__ blcnt,
@@ -1024,9 +1030,12 @@ __global__ void __launch_bounds__(256, SPW >= 8 ? 1 : 4) sampled_compact_kernel(
     const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ cidx,
     const uint32_t* __restrict__ ckey, const float* __restrict__ cval, const float* vals_src,
     int32_t* idx_out, float* val_out, int32_t* counter, float* rewind, int32_t* status_out,
-    ReplaceJob pj, int64_t nrep_first, int val_h) {
+    ReplaceJob pj, int64_t nrep_first, int val_h, uint32_t* selmask, uint32_t* planes,
+    int64_t nwords) {
   constexpr int CSEG = CompactCfg<SPW>::CSEG;
   constexpr int PFC = CompactCfg<SPW>::PFC;
+  constexpr int SLW = SL ? (int)(SL_RMAX / 32) : 1;
+  __shared__ uint32_t slrows[SL ? 4 : 1][SLW];
   __shared__ uint32_t wcnt[CSEG];
   __shared__ uint32_t subbase[NSUB + 1];
   __shared__ uint32_t flag, spec;
@@ -1238,10 +1247,17 @@ __global__ void __launch_bounds__(256, SPW >= 8 ? 1 : 4) sampled_compact_kernel(
   STAMP_T0(3);
   uint32_t run = boff;
   for (int w = 0; w < wid * SPW; ++w) run += wcnt[w];
+  uint32_t* const slrow = SL ? slrows[wid] : nullptr;
 #pragma unroll
   for (int u = 0; u < SPW; ++u) {
     const int64_t seg = seg0 + u;
     if (seg >= W) break;
+    const int64_t segbeg = seg * R;
+    const int segw = SL ? (int)((((segbeg + R < n) ? segbeg + R : n) - segbeg + 31) >> 5) : 0;
+    if (SL) {
+      for (int j = lane; j < segw; j += 64) slrow[j] = 0u;
+      __builtin_amdgcn_wave_barrier();
+    }
     if (cnt[u] != DENSE) {
       // pre: the value was read ahead (v valid); otherwise gathered here.  cw: the counter word
       // read ahead (PLAIN)
@@ -1252,6 +1268,7 @@ __global__ void __launch_bounds__(256, SPW >= 8 ? 1 : 4) sampled_compact_kernel(
           if (pos < (uint64_t)k) {
             idx_out[pos] = (int32_t)idx;
             store_val(val_out, val_h, pos, (cval || pre) ? v : vals_src[idx]);
+            if (SL) atomicOr(&slrow[(idx >> 5) - (uint32_t)(segbeg >> 5)], 1u << (idx & 31));
             if (counter) {
               if (PLAIN) counter[idx] = (int32_t)(cw + 1u);  // unique indices: no race
               else atomicAdd(&counter[idx], 1);  // non-returning: no round trip to wait on
@@ -1288,8 +1305,26 @@ __global__ void __launch_bounds__(256, SPW >= 8 ? 1 : 4) sampled_compact_kernel(
       }
     } else {
       dense_write<VEC>(s, seg, R, n, k, lo, T, icut, run, vals_src, idx_out, val_out, counter,
-                       rewind, val_h);
+                       rewind, val_h, slrow);
       run += wcnt[wid * SPW + u];
+    }
+    if (SL) {
+      // this wave's LDS bit-ors precede the reads in program order (one wave: in order)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      for (int j = lane; j < segw; j += 64) {
+        const uint32_t m = slrow[j];
+        const int64_t w = (segbeg >> 5) + j;
+        selmask[w] = m;
+        uint32_t carry = planes ? m : 0u;
+        for (int p = 0; p < 32 && carry != 0u; ++p) {
+          uint32_t* const a = planes + (int64_t)p * nwords + w;
+          const uint32_t old = *a;
+          *a = old ^ carry;
+          carry &= old;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();  // the row is cleared for the next segment after this
     }
   }
   STAMP_T0(4);
@@ -1429,12 +1464,12 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
   DPZ_TIMED(DPZ_KT_TOPK_SELECT, a.st, sampled_select_kernel<VEC><<<nsel + pb[1], 1024, 0, a.st>>>(
       s, a.n, a.k, g.W, g.B, g.R, g.CAP, ctrl, ghist, segcnt, cidx, ckey, blkabove, blcnt, blkey,
       blidx, jb[1]));
-  float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE) ? a.acc : nullptr;
+  float* rewind = (a.acc && a.acc_mode != DPZ_ACC_NONE && !a.selmask) ? a.acc : nullptr;
   // DPZ_COMPACT_ABLATE (diagnostic build only; results then differ from the reference): bit 0
   // drops the accumulator rewind, bit 1 the counter update — per-side-effect cost of compact
   const int ablate = (int)DPZ_KNOB_INT(COMPACT_ABLATE, 0);
   if (ablate & 1) rewind = nullptr;
-  int32_t* const counter = (ablate & 2) ? nullptr : a.counter;
+  int32_t* const counter = ((ablate & 2) || a.selmask) ? nullptr : a.counter;
   // DPZ_COUNTER_PLAIN=0 / 1 forces the counter update form (diagnostic build, A/B)
   const bool plain = DPZ_KNOB_INT(COUNTER_PLAIN, a.k > a.n / 32 ? 1 : 0) != 0;
   // DPZ_SCATTER_FIRST=1: the decode's blocks dispatched ahead of compact's own (diagnostic, A/B)
@@ -1444,19 +1479,23 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
   // (8 segments per wave, one block per CU, measured SLOWER at C2: 18.7 vs 12 us — the count and
   // write passes serialise four times the segments per wave, and the prologue does not get faster)
   const int spw = (int)DPZ_KNOB_INT(COMPACT_SPW, 2);
-#define DPZ_COMPACT(PL_, SPW_)                                                                    \
+#define DPZ_COMPACT(PL_, SPW_, SL_)                                                               \
   DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st,                                                            \
-            (sampled_compact_kernel<VEC, PL_, SPW_><<<(unsigned)((g.W + 4 * SPW_ - 1) / (4 * SPW_)) \
-                                                        + pb[2], 256, 0, a.st>>>(                 \
+            (sampled_compact_kernel<VEC, PL_, SPW_, SL_><<<(unsigned)((g.W + 4 * SPW_ - 1) /       \
+                                                                     (4 * SPW_)) + pb[2],         \
+                                                           256, 0, a.st>>>(                       \
                 s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, \
                 cidx, ckey, cval, a.vals_src, a.idx_out, a.val_out, counter, rewind,              \
-                a.status_out, jb[2], nrep_first, a.val_h)))
-  if (plain) {
-    if (spw == 8) DPZ_COMPACT(true, 8);
-    else DPZ_COMPACT(true, 2);
+                a.status_out, jb[2], nrep_first, a.val_h, a.selmask, a.planes, mask_words(a.n))))
+  if (a.selmask) {
+    // sliced side effects (dpz_topk_encode_sliced): the host checked g.R <= SL_RMAX
+    DPZ_COMPACT(false, 2, true);
+  } else if (plain) {
+    if (spw == 8) DPZ_COMPACT(true, 8, false);
+    else DPZ_COMPACT(true, 2, false);
   } else {
-    if (spw == 8) DPZ_COMPACT(false, 8);
-    else DPZ_COMPACT(false, 2);
+    if (spw == 8) DPZ_COMPACT(false, 8, false);
+    else DPZ_COMPACT(false, 2, false);
   }
 #undef DPZ_COMPACT
   return DPZ_OK;

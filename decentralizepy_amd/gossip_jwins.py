@@ -85,6 +85,30 @@ class HipJwinsOps:
                                workspace=self.wss[j % len(self.wss)], status_out=status,
                                shared=len(self.streams) > 1)
 
+    # the bookkeeping in coalesced form (dpz_topk_encode_sliced): counter as bit planes, the
+    # accumulator rewind deferred to the post-step's accumulating DWT (dpz_dwt_sym2_rewind)
+    sliced = True
+
+    def encode_sliced(self, wc, k, acc, wx, planes, mask, idx_out, val_out, status, j=0):
+        self.codec.topk_encode_sliced(wc, k, mask, planes, acc=acc,
+                                      acc_mode=self.codec.DPZ_ACC_ADD, vals_src=wx,
+                                      idx_out=idx_out, val_out=val_out,
+                                      workspace=self.wss[j % len(self.wss)], status_out=status,
+                                      shared=len(self.streams) > 1)
+
+    def encode_sliced_exact(self, wc, k, acc, wx, planes, mask, idx_out, val_out):
+        self.codec.topk_encode_sliced(wc, k, mask, planes, acc=acc,
+                                      acc_mode=self.codec.DPZ_ACC_ADD, vals_src=wx,
+                                      idx_out=idx_out, val_out=val_out, workspace=self.ws,
+                                      exact=True)
+
+    def accumulate_rewind(self, acc, new, prev, mask):
+        self.codec.wavedec(new, self.level, x0=prev, want_x=False, coeffs_diff=acc,
+                           accumulate=True, wavelet=self.wavelet, rewind_mask=mask)
+
+    def unslice(self, planes, m_len):
+        return self.codec.counter_unslice(planes, m_len)
+
     def encode_exact(self, wc, k, acc, wx, counter, idx_out, val_out):
         self.codec.topk_encode(wc, k, acc=acc, acc_mode=self.codec.DPZ_ACC_ADD, vals_src=wx,
                                counter=counter, idx_out=idx_out, val_out=val_out,
@@ -135,7 +159,9 @@ class JwinsRound:
 
     Node i is uid i (the reference's Linear mapping of one process per node).  Per-node state,
     rows of (hi - lo, ·) tensors: ``x`` (the model after the round), ``x0`` (init_model == prev),
-    ``acc`` (accumulated_changes, M), ``counter`` (shared_parameters_counter, M)."""
+    ``acc`` (accumulated_changes, M), ``counter`` (shared_parameters_counter, M; with the HIP ops
+    kept as bit planes and materialised on read, and the encode's rewind applied by the round's
+    accumulating post-step — exact after every ``step()``)."""
 
     def __init__(self, adj, x_init, alpha_list="[0.1, 0.2, 0.3, 0.4, 1.0]", rank=0, world=1,
                  group=None, wavelet="sym2", level=4, metadata_cap=0.5, ops=None, device=None,
@@ -170,7 +196,15 @@ class JwinsRound:
         self.x = rows(self.N, init=x_init)
         self.x0 = rows(self.N, init=x_init)
         self.acc = rows(M)
-        self.counter = rows(M, torch.int32)
+        self.sliced = bool(getattr(self.ops, "sliced", False))
+        if self.sliced:  # counter as bit planes + selection masks (HipJwinsOps.encode_sliced)
+            from . import codec
+            nw = codec.mask_words(M)
+            self.planes = rows(32 * nw, torch.int32)
+            self.mask = rows(nw, torch.int32)
+            self.pending = [False] * m
+        else:
+            self._counter = rows(M, torch.int32)
         self.wx = rows(M)   # pre_share_model_transformed
         self.wc = rows(M)   # W(x - x0); the fold total reuses it
         f32 = dict(dtype=torch.float32, device=self.device)
@@ -191,6 +225,15 @@ class JwinsRound:
             self.ops.reserve(M, sorted({round(a * M) for a in partial}))
         self.alphas = None
         self.round = 0
+
+    @property
+    def counter(self):
+        """shared_parameters_counter rows (materialised from the bit planes when sliced)."""
+        if not self.sliced:
+            return self._counter
+        return torch.stack([self.ops.unslice(self.planes[j], self.M)
+                            for j in range(self.hi - self.lo)]) if self.hi > self.lo else \
+            torch.zeros(0, self.M, dtype=torch.int32, device=self.device)
 
     # ---- layout of one round's payloads ------------------------------------------------------
     def _layout(self, alphas):
@@ -243,12 +286,19 @@ class JwinsRound:
             with self._on(j):
                 self.ops.transform_pair(self.x[j], self.x0[j], self.wx[j], self.wc[j])
                 partial, k, oi, ov = lay[q]
-                if partial:
+                if partial and self.sliced:
+                    self.ops.encode_sliced(self.wc[j], k, self.acc[j], self.wx[j], self.planes[j],
+                                           self.mask[j], self.send_idx[oi:oi + k],
+                                           self.send_val[ov:ov + k], self.status[j:j + 1], j=j)
+                    self.pending[j] = True
+                elif partial:
                     kw = {"j": j} if hasattr(self.ops, "on") else {}
-                    self.ops.encode(self.wc[j], k, self.acc[j], self.wx[j], self.counter[j],
+                    self.ops.encode(self.wc[j], k, self.acc[j], self.wx[j], self._counter[j],
                                     self.send_idx[oi:oi + k], self.send_val[ov:ov + k],
                                     self.status[j:j + 1], **kw)
                 else:  # Wavelet.py:185-192: all of W(x), accumulated changes zeroed
+                    if self.sliced:
+                        self.pending[j] = False
                     self.acc[j].zero_()
                     self.status[j:j + 1].zero_()
                     if self.world > 1:
@@ -257,8 +307,13 @@ class JwinsRound:
         # a sampled-path miss (rare) left that node's payload and bookkeeping untouched: redo it
         for j in self.ops.missed(self.status[:m]):
             partial, k, oi, ov = lay[self.lo + j]
-            self.ops.encode_exact(self.wc[j], k, self.acc[j], self.wx[j], self.counter[j],
-                                  self.send_idx[oi:oi + k], self.send_val[ov:ov + k])
+            if self.sliced:
+                self.ops.encode_sliced_exact(self.wc[j], k, self.acc[j], self.wx[j],
+                                             self.planes[j], self.mask[j],
+                                             self.send_idx[oi:oi + k], self.send_val[ov:ov + k])
+            else:
+                self.ops.encode_exact(self.wc[j], k, self.acc[j], self.wx[j], self._counter[j],
+                                      self.send_idx[oi:oi + k], self.send_val[ov:ov + k])
 
     def exchange(self, s_idx, s_val):
         if self.world == 1:
@@ -280,7 +335,11 @@ class JwinsRound:
         for j in range(self.hi - self.lo):
             with self._on(j):
                 self.ops.inverse(self.wc[j], self.N, self.x[j])        # model <- waverec(total)
-                self.ops.accumulate(self.acc[j], self.x[j], self.x0[j])  # acc += W(x_new - prev)
+                if self.sliced and self.pending[j]:  # acc = (rewound ? 0 : acc) + W(x_new - prev)
+                    self.ops.accumulate_rewind(self.acc[j], self.x[j], self.x0[j], self.mask[j])
+                    self.pending[j] = False
+                else:
+                    self.ops.accumulate(self.acc[j], self.x[j], self.x0[j])  # acc += W(x_new - prev)
                 self.x0[j].copy_(self.x[j])                              # init = prev = x_new
         self._join()
 

@@ -9,10 +9,13 @@ compression_class``), same wire payloads and the same model side effects.
 Device path per round (all HIP kernels, fp32, pywt-1.1.1-exact summation order):
   pre-step   W(x) and W(x - x0) in ONE multilevel DWT launch (reference Wavelet.py:30-32 called
              twice from PartialModel.py:317-320)
-  encode     top-k on |W(x - x0)| (+ accumulation), values gathered from W(x) (Wavelet.py:142-231)
+  encode     top-k on |W(x - x0)| (+ accumulation), values gathered from W(x) (Wavelet.py:142-231);
+             with accumulate_averaging_changes the counter / rewind bookkeeping is coalesced
+             (bit-sliced counter, selection mask; dpz_topk_encode_sliced)
   averaging  one batched replace+fold over all payloads in the wavelet domain, then one
              multilevel IDWT launch (Wavelet.py:269-329)
-  post-step  acc += W(x_new - prev) as one accumulating DWT launch (PartialModel.py:346-349)
+  post-step  acc += W(x_new - prev) as one accumulating DWT launch (PartialModel.py:346-349),
+             applying the encode's deferred rewind as it goes (dpz_dwt_sym2_rewind)
 
 Device kernels exist for ``wavelet="sym2"`` with ``level <= 4`` (every shipped JWINS config, e.g.
 tutorial/JWINS/config.ini) and for the reference's default ``wavelet="haar"`` with ``level <= 8``;
@@ -22,7 +25,7 @@ import numpy as np
 import torch
 
 from ... import codec
-from ..._device import to_host
+from ..._device import DeviceAccumulator, SlicedCounter, to_host
 from ...utils import identity
 from ..PartialModel import PartialModel
 
@@ -70,6 +73,19 @@ class Wavelet(PartialModel):
         slices, m = coeff_slices(self.number_of_params, self.level, self.wavelet)
         self.wt_shape = (m,)
         self.coeff_slices = slices
+        # accumulation with accumulate_averaging_changes (the JWINS tutorial config): the encode's
+        # bookkeeping in coalesced form — the counter as bit planes, the rewind deferred to the
+        # post-step's accumulating DWT, which rewrites the accumulator anyway
+        # (dpz_topk_encode_sliced, dpz_dwt_sym2_rewind)
+        self._sliced = bool(self.accumulation and self.accumulate_averaging_changes)
+        if self._sliced:
+            nw = codec.mask_words(self.transformed_len)
+            self._planes = torch.zeros(32 * nw, dtype=torch.int32, device=self.device)
+            self._sel_mask = torch.zeros(nw, dtype=torch.int32, device=self.device)
+            self._counter = None
+            self.model.shared_parameters_counter = SlicedCounter(self._planes,
+                                                                 self.transformed_len)
+            self.model.accumulated_changes = DeviceAccumulator(self.model.accumulated_changes)
 
     # ---- PartialModel hooks --------------------------------------------------------------------
     def _check_transformer(self):
@@ -83,8 +99,19 @@ class Wavelet(PartialModel):
         return codec.wavedec(x, self.level, x0=self.init_model, wavelet=self.wavelet)
 
     def _encode(self, k):
-        acc = self.model.accumulated_changes if self.accumulation else None
+        acc = self._acc()
         wx, wc = self.pre_share_model_transformed, self._change_dev
+        if self._sliced:
+            # counter += 1 on the bit planes, rewind left pending (applied by _accumulate_change)
+            if self.change_based_selection:
+                idx, val = codec.topk_encode_sliced(wc, k, self._sel_mask, self._planes, acc=acc,
+                                                    acc_mode=codec.DPZ_ACC_ADD, vals_src=wx,
+                                                    workspace=self.workspace)
+            else:
+                idx, val = codec.topk_encode_sliced(wx, k, self._sel_mask, self._planes,
+                                                    vals_src=wx, workspace=self.workspace)
+            self.model.accumulated_changes.pending = self._sel_mask
+            return idx, val
         if self.change_based_selection:
             return codec.topk_encode(wc, k, acc=acc, acc_mode=self._acc_mode(), vals_src=wx,
                                      counter=self._counter, workspace=self.workspace)
@@ -114,9 +141,17 @@ class Wavelet(PartialModel):
         return m
 
     def _accumulate_change(self, new, prev):
-        """acc += W(new - prev) (reference PartialModel.py:346-349 with T = wavelet)."""
-        codec.wavedec(new, self.level, x0=prev, want_x=False,
-                      coeffs_diff=self.model.accumulated_changes, accumulate=True,
+        """acc += W(new - prev) (reference PartialModel.py:346-349 with T = wavelet); a rewind the
+        encode left pending is applied by the same pass (acc = (selected ? 0 : acc) + W)."""
+        a = self.model.accumulated_changes
+        if isinstance(a, DeviceAccumulator):
+            if a.pending is not None:
+                codec.wavedec(new, self.level, x0=prev, want_x=False, coeffs_diff=a.device_tensor,
+                              accumulate=True, wavelet=self.wavelet, rewind_mask=a.pending)
+                a.pending = None
+                return
+            a = a.device_tensor
+        codec.wavedec(new, self.level, x0=prev, want_x=False, coeffs_diff=a, accumulate=True,
                       wavelet=self.wavelet)
 
     # ---- receive side -------------------------------------------------------------------------

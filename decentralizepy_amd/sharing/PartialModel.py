@@ -27,7 +27,8 @@ import numpy as np
 import torch
 
 from .. import codec
-from .._device import DeviceCounter, state_to_device, state_version, to_host
+from .._device import (DeviceAccumulator, DeviceCounter, state_to_device, state_version,
+                       to_host)
 from ..utils import conditional_value, identity
 from .Sharing import Sharing
 
@@ -154,7 +155,7 @@ class PartialModel(Sharing):
         reference's ``acc += change`` / ``change += acc``).  A device tensor; the selection
         itself never reads it (the encode fuses the change), so it costs one elementwise pass,
         written into a buffer the plugin keeps across rounds (no allocation per round)."""
-        acc = self.model.accumulated_changes if self.accumulation else None
+        acc = self._acc()
         change = self._change_dev
         buf = getattr(self, "_mc_buf", None)
         like = change if change is not None else self.pre_share_model
@@ -173,10 +174,15 @@ class PartialModel(Sharing):
         """Top-k encode; returns device (idx int32[k], val fp32[k])."""
         key_src = self._change_dev if self._change_dev is not None else self.pre_share_model
         x0 = None if self._change_dev is not None else self.init_model
-        acc = self.model.accumulated_changes if self.accumulation else None
+        acc = self._acc()
         return codec.topk_encode(key_src, k, x0=x0, acc=acc, acc_mode=self._acc_mode(),
                                  vals_src=self.pre_share_model_transformed, counter=self._counter,
                                  workspace=self.workspace)
+
+    def _acc(self):
+        """The device accumulator (None without accumulation), any deferred rewind applied."""
+        a = self.model.accumulated_changes if self.accumulation else None
+        return a.settle() if isinstance(a, DeviceAccumulator) else a
 
     def _zero_accumulation(self):
         if getattr(self.model, "accumulated_changes", None) is not None:

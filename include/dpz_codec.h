@@ -205,6 +205,35 @@ int dpz_topk_encode_status(const float* x, const float* x0, float* acc, int acc_
                            float* val_out, int32_t* counter, void* ws, size_t ws_bytes,
                            int32_t* status_out, int flags, dpz_stream_t stream);
 
+/* ---- the encode's side effects in coalesced form (JWINS / Wavelet with accumulation) ----------
+ * Selection mask: ceil(n/32) uint32 words (dpz_mask_words), bit b of word w <-> element 32w + b.
+ * Sliced counter: the share counter (reference shared_parameters_counter, int32 per element,
+ * sharing/PartialModel.py:143-145) as 32 bit planes of ceil(n/32) words, 4 * 32 * ceil(n/32)
+ * bytes: bit b of planes[p * ceil(n/32) + w] is bit p of counter[32w + b].
+ * dpz_topk_encode_sliced: the selection of dpz_topk_encode (same keys, ties, idx_out / val_out;
+ * acc_mode DPZ_ACC_NONE or DPZ_ACC_ADD, acc only read) with its bookkeeping
+ * (sharing/JWINS/Wavelet.py:194-197: shared_parameters_counter[idx] += 1,
+ * rewind_accumulation(idx)) as: planes (may be NULL) += 1 at every selected index, and every word
+ * of sel_mask written with the selected bits.  The rewind acc[idx] = 0 is NOT applied: the caller
+ * folds it into the next pass that rewrites acc — dpz_dwt_sym2_rewind / dpz_dwt_haar_rewind
+ * (the accumulating post-step, sharing/PartialModel.py:346-349: acc = (bit ? 0 : acc) + T(x - x0),
+ * the reference's rewind-then-add) or dpz_rewind_apply.  Scattered 4-byte counter / accumulator
+ * updates over 10 % of a 25 M array touch ~97 % of their 128-byte lines; this form writes
+ * n/8 mask bytes and the few planes a carry reaches.  status_out (DEVICE int32, may be NULL):
+ * non-NULL = asynchronous, the final status written on `stream` (nonzero: the sampled path
+ * missed, nothing was written; re-run with DPZ_TOPK_EXACT); NULL = blocking, a miss re-run
+ * exactly inside the call.  flags: DPZ_TOPK_EXACT, DPZ_TOPK_SHARED, DPZ_TOPK_VAL_FP16.
+ * dpz_counter_unslice / dpz_counter_slice convert between the sliced and the int32 counter
+ * (DeviceCounter materialises on read); dpz_rewind_apply: acc[i] = 0 where the bit is set.      */
+int64_t dpz_mask_words(int64_t n);
+int dpz_topk_encode_sliced(const float* x, const float* x0, const float* acc, int acc_mode,
+                           const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
+                           float* val_out, uint32_t* planes, uint32_t* sel_mask, void* ws,
+                           size_t ws_bytes, int32_t* status_out, int flags, dpz_stream_t stream);
+int dpz_counter_unslice(const uint32_t* planes, int64_t n, int32_t* counter, dpz_stream_t stream);
+int dpz_counter_slice(const int32_t* counter, int64_t n, uint32_t* planes, dpz_stream_t stream);
+int dpz_rewind_apply(float* acc, const uint32_t* sel_mask, int64_t n, dpz_stream_t stream);
+
 /* Batched decode + Metro-Hastings fold over n_payloads neighbour payloads.
  * Replaces reference sharing/PartialModel.py:257-303 (T = cat(local); T[idx] = params),
  * sharing/Sharing.py:156-229 (_averaging / _averaging_server fold) and
@@ -291,6 +320,11 @@ int64_t dpz_wavedec_len(int64_t n, int level);
 int dpz_dwt_sym2(const float* x, const float* x0, int64_t n, int level, float* coeffs_x,
                  float* coeffs_diff, int accumulate, dpz_stream_t stream);
 
+/* dpz_dwt_sym2(x, x0, n, level, NULL, acc, 1) with the deferred rewind of
+ * dpz_topk_encode_sliced: acc[i] = fl((bit i of sel_mask ? +0.0 : acc[i]) + W(x - x0)[i]). */
+int dpz_dwt_sym2_rewind(const float* x, const float* x0, int64_t n, int level, float* acc,
+                        const uint32_t* sel_mask, dpz_stream_t stream);
+
 /* Multilevel sym2 IDWT (pywt.array_to_coeffs + pywt.waverec), first n outputs written.
  * Replaces reference sharing/JWINS/Wavelet.py:311-316.                                        */
 int dpz_idwt_sym2(const float* coeffs, int64_t n, int level, float* out, dpz_stream_t stream);
@@ -319,6 +353,10 @@ int64_t dpz_haar_wavedec_len(int64_t n, int level);
 int dpz_dwt_haar(const float* x, const float* x0, int64_t n, int level, float* coeffs_x,
                  float* coeffs_diff, int accumulate, dpz_stream_t stream);
 int dpz_idwt_haar(const float* coeffs, int64_t n, int level, float* out, dpz_stream_t stream);
+/* the haar counterpart of dpz_dwt_sym2_rewind */
+int dpz_dwt_haar_rewind(const float* x, const float* x0, int64_t n, int level, float* acc,
+                        const uint32_t* sel_mask, dpz_stream_t stream);
+
 
 /* dst[idx[j]] = value for j < k (indices outside [0, n) are ignored).
  * Replaces reference models/Model.py:53-64 (rewind_accumulation: acc[idx] = 0) where the rewind

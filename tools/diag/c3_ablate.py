@@ -49,6 +49,30 @@ def main():
         print(json.dumps({"alpha": alpha, "ablate": int(ablate), "vals": vals, "kernels_us": res,
                           "status": codec.topk_sticky_status(ws, clear=True)}), flush=True)
     os.environ.pop("DPZ_COMPACT_ABLATE", None)
+    # the coalesced side effects (dpz_topk_encode_sliced): bit-sliced counter + selection mask
+    nw = codec.mask_words(m)
+    for d in sets:
+        d["planes"] = torch.zeros(32 * nw, dtype=torch.int32, device=dev)
+        d["mask"] = torch.zeros(nw, dtype=torch.int32, device=dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def enc_sl(d):
+        codec.topk_encode_sliced(d["wc"], k, d["mask"], d["planes"], acc=d["acc"],
+                                 acc_mode=codec.DPZ_ACC_ADD, vals_src=d["wx"], idx_out=d["idx"],
+                                 val_out=d["val"], workspace=ws, status_out=st)
+    for _ in range(3):
+        for d in sets:
+            enc_sl(d)
+    torch.cuda.synchronize()
+    with codec.KernelTimer() as kt:
+        torch.cuda._sleep(int(20e6))
+        for _ in range(5):
+            for d in sets:
+                enc_sl(d)
+        torch.cuda.synchronize()
+    res = {nm: round(ms / c * 1e3, 2) for nm, (ms, c) in kt.result.items()}
+    print(json.dumps({"alpha": alpha, "sliced": True, "vals": "wx", "kernels_us": res,
+                      "status": int(st.item())}), flush=True)
 
 
 if __name__ == "__main__":
