@@ -192,6 +192,8 @@ def load(path, check_build=True):
             "(or `make -C decentralizepy_amd/csrc`). There is no CPU fallback.")
     handle = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
+        if not check_build and not hasattr(handle, name):
+            continue  # a diagnostic build of other sources (A/B against an older tree)
         fn = getattr(handle, name)
         fn.restype = res
         fn.argtypes = args

@@ -1019,6 +1019,60 @@ __device__ __forceinline__ int32_t fw_lower_bounds(int np, int32_t e0, int lane,
   return fw_lower_bounds_t<NSX>(np, [e0](int) { return e0; }, lane, idx_of, k_of, dflt);
 }
 
+// Walk-kernel start, compile-time switches (A/B variants: tools/diag/build_variant.sh):
+// *_LOCKSTEP 1: the payloads' cursor searches in lock step (fw_lower_bounds); 0: one payload after
+// the other.  *_L_FIRST 1: the first tile's local values issued before the search.  WALK4: the
+// 1..4-payload kernel (a node's few neighbours: C4 rounds, the plugins), WALKG: the 5..16-payload
+// groups kernel (C3).  Measured on MI355X (same box, tools/diag/c4_round_ab.py, 96-node C4 round
+// on 3 streams): the fold leg 3.33 ms with lock step + local first, 3.14 sequential + local
+// first, 3.42 lock step + local after, 3.00 sequential + local after — under three concurrent
+// codecs the lock-step probes (and locals issued ahead of them) delay every wave's first window.
+// The 16-payload groups kernel (C3 shape, tools/diag/fold_time.py) is no faster with them either
+// (alpha 0.02: 128.7 vs 122.1 us, 0.1: 171.1 vs 170.2, 0.2: 261.4 vs 255.2), so both kernels
+// search one payload after the other; fw_lower_bounds serves the patch decode.
+#ifndef DPZ_WALK4_LOCKSTEP
+#define DPZ_WALK4_LOCKSTEP 0
+#endif
+#ifndef DPZ_WALK4_L_FIRST
+#define DPZ_WALK4_L_FIRST 0
+#endif
+#ifndef DPZ_WALKG_LOCKSTEP
+#define DPZ_WALKG_LOCKSTEP 0
+#endif
+#ifndef DPZ_WALKG_L_FIRST
+#define DPZ_WALKG_L_FIRST 0
+#endif
+template <int NSX, bool LOCK, class IdxOf, class KOf>
+__device__ __forceinline__ int32_t fw_start_cursors(int np, int32_t e0, int lane, IdxOf idx_of,
+                                                    KOf k_of, const int32_t* dflt) {
+  if (LOCK) return fw_lower_bounds<NSX>(np, e0, lane, idx_of, k_of, dflt);
+  int32_t curv = 0;
+#pragma unroll
+  for (int p = 0; p < NSX; ++p) {
+    if (p >= np) break;
+    const int32_t* ip = idx_of(p);
+    int32_t lo = 0, hi = k_of(p);
+    while (hi > lo) {
+      const int32_t len = hi - lo;
+      const int32_t stride = len <= 64 ? 1 : (len + 63) / 64;
+      const int64_t q = (int64_t)lo + (int64_t)lane * stride;
+      const bool ok = q < hi;
+      const int32_t x = ip[ok ? q : lo];
+      const int32_t c = (int32_t)__popcll(__ballot(ok && x < e0));  // a prefix
+      if (stride == 1) {
+        lo += c;
+        break;
+      }
+      const int32_t nlo = c > 0 ? lo + (c - 1) * stride + 1 : lo;
+      const int64_t nhi = (int64_t)lo + (int64_t)c * stride;
+      hi = nhi < hi ? (int32_t)nhi : hi;
+      lo = nlo;
+    }
+    curv = lane == p ? lo : curv;
+  }
+  return curv;
+}
+
 // Sparse payloads only (dense ones take the classic kernels), a fresh total (a.first),
 // n < 2^31 - 1024 (walk_ok), np <= NS.  NS payload slots, all compile-time: every slot's window
 // of the NEXT tile is issued at the start of this tile (branch-free loads), so the loads are in
@@ -1064,12 +1118,14 @@ __global__ void __launch_bounds__(256, FW_MINB_1(EPL)) fold_walk_kernel(FoldArgs
     return ONE ? a.p[p].w : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl), p));
   };
   // the first tile's local values are issued before the cursor search (independent of it)
-  FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n), Ln;
-  // ---- start cursors: lower_bound(idx_p, t0 * TE), every payload in lock step ----
+  FwV<EPL> L, Ln;
+  if (DPZ_WALK4_L_FIRST) L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n);
+  // ---- start cursors: lower_bound(idx_p, t0 * TE) ----
   // lane p: payload p's cursor (the next window's first entry)
-  int32_t curv = fw_lower_bounds<NS>(
+  int32_t curv = fw_start_cursors<NS, DPZ_WALK4_LOCKSTEP != 0>(
       np, (int32_t)(t0 * TE), lane, [&](int p) { return P_idx(p); },
       [&](int p) { return P_k(p); }, reinterpret_cast<const int32_t*>(a.local));
+  if (!DPZ_WALK4_L_FIRST) L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n);
   int32_t cs[ONE ? NS : 1];
   if constexpr (ONE) {
 #pragma unroll
@@ -1277,13 +1333,15 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
   static_assert(DIST == 1 || (DIST == 3 && !ONE), "DIST 3: four groups");
   int32_t cs[FOLD_MAXP];  // CT: the cursors (scalar registers)
   // the first tile's local values are issued before the cursor search (independent of it)
-  FwV<EPL> L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n), Ln;
+  FwV<EPL> L, Ln;
+  if (DPZ_WALKG_L_FIRST) L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n);
   // ---- start cursors: lower_bound(idx_p, t0 * TE), every payload in lock step ----
-  int32_t curv = fw_lower_bounds<FOLD_MAXP>(
+  int32_t curv = fw_start_cursors<FOLD_MAXP, DPZ_WALKG_LOCKSTEP != 0>(
       np, (int32_t)(t0 * TE), lane,
       [&](int p) { return reinterpret_cast<const int32_t*>(rl64(ipl, p)); },
       [&](int p) { return fw_uni(__builtin_amdgcn_readlane(kl, p)); },
       reinterpret_cast<const int32_t*>(a.local));
+  if (!DPZ_WALKG_L_FIRST) L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n);
   if (CT) {
 #pragma unroll
     for (int q = 0; q < (ONE ? FW_G : FOLD_MAXP); ++q) cs[q] = fw_uni(__builtin_amdgcn_readlane(curv, q));

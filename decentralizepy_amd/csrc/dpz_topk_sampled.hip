@@ -412,7 +412,7 @@ template <int SRC, int CP, int D, int OCC>
 __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
     KeySrc s, int64_t n, uint32_t r_lo, uint32_t r_hi, int64_t W, int64_t R, int64_t CAP,
     TopkCtrl* ctrl, const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt,
-    uint32_t* cidx, uint32_t* ckey, float* cval, float* __restrict__ copy_out, int xnt,
+    uint32_t* cidx, uint32_t* ckey, float* cval, float* __restrict__ copy_out,
     FoldBase fb) {
   static_assert(D >= 2, "at least one group in flight");
   typedef float v4f __attribute__((ext_vector_type(4)));
@@ -440,9 +440,11 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
   auto ld = [&](int64_t j, int u) {
     const int64_t i0 = beg + j * 256 + lane * 4;
     const int64_t g4 = (i0 < end4 ? i0 : 0) >> 2;
-    // x: non-temporal unless a decode of this node's round reads x next (xnt == 0: x stays in
-    // the Infinity Cache for it); x0 / acc are read once
-    A[u] = (xnt & 1) ? __builtin_nontemporal_load(xa + g4) : xa[g4];
+    // x non-temporal, like x0 / acc: a runtime choice between a non-temporal and a plain load
+    // (an xnt kernel argument, tried in round 4) compiled to ONE plain load — the hint was lost,
+    // x stayed in the caches and the compact's counter updates slowed by 1-3 us (same-box A/B
+    // against the round-3 build, tools/diag/enc_ab.py)
+    A[u] = __builtin_nontemporal_load(xa + g4);
     if (X0) B[u] = __builtin_nontemporal_load(xb + g4);
   };
 #pragma unroll
@@ -464,8 +466,7 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
     if (CP == 1 && cq) __builtin_nontemporal_store(A[u], reinterpret_cast<v4f*>(copy_out) + (i0 >> 2));
     if (CP == 2 && cq) {
       const v4f b = {fb.of(A[u].x), fb.of(A[u].y), fb.of(A[u].z), fb.of(A[u].w)};
-      if (xnt & 2) __builtin_nontemporal_store(b, reinterpret_cast<v4f*>(copy_out) + (i0 >> 2));
-      else reinterpret_cast<v4f*>(copy_out)[i0 >> 2] = b;
+      __builtin_nontemporal_store(b, reinterpret_cast<v4f*>(copy_out) + (i0 >> 2));
     }
     const float xv[4] = {A[u].x, A[u].y, A[u].z, A[u].w};
     uint32_t kq[4];
@@ -1421,8 +1422,6 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
     const bool add_only = a.acc_mode == DPZ_ACC_ADD && !a.x0;
     if (VEC && (a.acc_mode == DPZ_ACC_NONE || add_only) && pipe > 0) {
       const bool x0 = a.x0 != nullptr;
-      // bit 0: x loaded non-temporal; bit 1: the fold base stored non-temporal
-      const int xnt = (int)DPZ_KNOB_INT(FILTER_XNT, 3);
       // the fold base (dpz_topk_encode_foldbase) rides on the same copy slot
       const bool fbase = a.fbase && a.base_out && x0 && !copy_out;
       float* const cpo = fbase ? a.base_out : copy_out;
@@ -1441,7 +1440,7 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
 #define DPZ_PIPE1(X0_, CP_, D_, O_)                                                           \
   DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_pipe_kernel<X0_, CP_, D_, O_><<<nb, 256, 0, a.st>>>( \
       s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval, cpo, \
-      xnt, fbv))
+      fbv))
       switch (dsel) {
         case 2: DPZ_PIPE(2, 8); break;
         case 8: DPZ_PIPE(8, 4); break;
