@@ -169,10 +169,16 @@ class Sharing:
             for w in weights:
                 weight_total += w
             local = self._local_flat_device()
-            out = self._fold(local, payloads, weights, 1 - weight_total)
+            out = self._fold_on_base(local, payloads, weights, 1 - weight_total)
+            if out is None:
+                out = self._fold(local, payloads, weights, 1 - weight_total)
             self._load_flat(out)
         self._post_step()
         self.communication_round += 1
+
+    def _fold_on_base(self, local, payloads, weights, w_self):
+        """The fold over a no-hit base the encode already wrote (PartialModel), or None."""
+        return None
 
     def _averaging_server(self, peer_deques):
         """Plain average of the working nodes' models (reference Sharing.py:200-229)."""

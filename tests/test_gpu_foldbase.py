@@ -119,3 +119,48 @@ def test_foldbase_rejects_bad_arguments(dev):
     with pytest.raises(Exception):  # the server form (no self term) is not a base-ready fold
         codec.decode_average(x, [(idx, x0[:idx.numel()])], [0.5], None, out=base,
                              base_ready=True)
+
+
+class _OneNbrGraph:
+    """uid 0 has the single neighbour 1, whose degree is `deg` (a star leaf, a 2-node run)."""
+
+    def __init__(self, deg):
+        self.deg = deg
+
+    def neighbors(self, uid):
+        return {1} if uid == 0 else set(range(10, 10 + self.deg))
+
+
+@pytest.mark.parametrize("msg_degree", [3, 5])
+def test_partialmodel_one_neighbour_folds_on_the_encoded_base(dev, tmp_path, msg_degree):
+    """PartialModel with one neighbour: the encode writes the Metro-Hastings fold's no-hit base
+    (weights predicted from the graph, Sharing.py:156-190) and _averaging patches the payload's
+    elements; with a message whose degree breaks the prediction (5) the plain fold runs.  Both
+    give the oracle's averaged model bit for bit, over two rounds."""
+    from collections import deque
+
+    from decentralizepy_amd.sharing.PartialModel import PartialModel
+    from tests import scenario
+    shape = (1000, 1000, 7)
+    n = shape[0] * shape[1] + shape[2]
+    rng = np.random.default_rng(msg_degree)
+    model = scenario.make_model(shape)
+    x = rng.standard_normal(n).astype(np.float32)
+    scenario.set_flat(model, x)
+    plugin = PartialModel(0, 0, None, scenario._Mapping(), _OneNbrGraph(3), model, None,
+                          str(tmp_path), alpha=0.01)
+    for r in range(2):
+        x = (scenario.get_flat(model) + 0.01 * rng.standard_normal(n)).astype(np.float32)
+        scenario.set_flat(model, x)
+        plugin.get_data_to_send()
+        assert plugin._fb is not None  # the encode wrote the predicted base
+        k = round(0.01 * n)
+        idx = np.sort(rng.choice(n, k, replace=False)).astype(np.int32)
+        val = rng.standard_normal(k).astype(np.float32)
+        msg = {"alpha": 0.01, "indices": idx, "params": val, "send_partial": True,
+               "degree": msg_degree, "iteration": r, "CHANNEL": "DPSGD"}
+        w = 1 / (max(1, msg_degree) + 1)
+        plugin._averaging({1: deque([msg])})
+        got = scenario.get_flat(model)
+        want = ofold.fold(x, [(idx, val)], [w], 1 - w)
+        np.testing.assert_array_equal(_bits(got), _bits(want))
