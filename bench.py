@@ -407,13 +407,16 @@ def kernel_alg_bytes(name, n, k):
     }.get(name, 0)
 
 
-def load_pmc(kernel):
-    """HBM traffic per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
+def load_pmc(kernel, n):
+    """HBM traffic per launch of `kernel` from the committed rocprofv3 PMC summary, if it was
+    collected at this tensor size (its "n"); None otherwise."""
     path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         pmc = json.load(f)
+    if pmc.get("n") != n:
+        return None
     ent = pmc.get("kernels", {}).get(kernel)
     if not ent:
         return None
@@ -667,7 +670,7 @@ def main():
             dk["avg_us"] = round(t_dec * 1e6, 3)
             dk["GBps"] = round(dk["alg_bytes"] / t_dec / 1e9, 1)
             dk["timing"] = "back-to-back launches, HIP events around the loop on the launch stream"
-        traffic = load_pmc(dom)
+        traffic = load_pmc(dom, args.n)
         line = {
             "metric": "GiB/s fp32 params encoded+decoded (device-resident), 1% top-k",
             "value": round(r["value"], 3),

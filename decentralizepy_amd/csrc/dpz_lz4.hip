@@ -7,12 +7,15 @@
 // (python-lz4's lz4.frame, third-party, absent here; its frame format is the LZ4 frame spec and
 // its default preferences are: 64 KB blocks, linked, content size stored, no checksums).
 //
-// Encoder: the input is cut into independent 2 KB blocks (DPZ_LZ_BLK), ONE WAVE per block (the frame says
-// B.Indep, so any LZ4 frame decoder — python-lz4 on a reference node included — reads it):
-//   1. the block is staged in LDS; every position i <= len - 12 hashes its 4 bytes (LZ4's
-//      multiplicative hash, 11 bits) 64 positions at a time: the candidate is the table entry
-//      left by earlier chunks, then the chunk publishes itself with LDS atomicMax (so the nearest
-//      earlier occurrence from a previous chunk wins — deterministic);
+// Encoder: the input is cut into 2 KB blocks (DPZ_LZ_BLK), ONE WAVE per block; the frame is
+// LINKED (B.Indep clear, python-lz4's default mode): a block's matches may reach DPZ_LZ_WIN
+// (14 KB) back into the input before it, which every block reads from the input itself, so the
+// blocks are still encoded in parallel:
+//   1. the history and the block are staged in LDS; the hash table (LZ4's 5-byte multiplicative
+//      hash, 12 bits) is prefilled with the history's positions, then every position
+//      i <= len - 12 of the block hashes its 5 bytes 64 positions at a time: the candidate is the
+//      table entry left by earlier chunks, then the chunk publishes itself with LDS atomicMax
+//      (the nearest earlier occurrence wins — deterministic);
 //   2. each lane extends its candidate word-wise (min match 4, capped at 1024 and at len - 5) and
 //      sets its bit in a per-position match mask;
 //   3. the greedy parse walks the mask with 64-bit bit scans (literal runs cost one scan, not one
@@ -21,10 +24,14 @@
 //      copied out coalesced; a block that does not shrink is stored uncompressed (LZ4 frame
 //      high-bit block size).
 // A second launch scans the block sizes and assembles the frame (header, size-prefixed blocks,
-// end mark).  Decoder: the host walks the frame's block headers (it holds the bytes); linked
-// frames (python-lz4's default) decode in ONE workgroup block after block with a 64 KB LDS ring
-// window; independent frames decode one workgroup per block into per-block slots, then a scan
-// and a compaction.  Every read / write is bounds-checked; a malformed block sets *status.
+// end mark).  Decoder: the host walks the frame's block headers (it holds the bytes).  Blocks
+// that decode to <= 4 KB take the parallel decoder — every block parsed from all byte positions
+// at once, each output byte given its source (a literal, an earlier byte of the block, or for a
+// linked frame an earlier block's byte), pointer jumping inside the block; then the blocks are
+// placed at their frame offsets and references into earlier blocks are resolved by pointer
+// jumping over the whole frame (lz4_link_place_kernel, lz4_link_resolve_kernel).  liblz4's 64 KB
+// linked blocks decode in ONE workgroup block after block with a 64 KB LDS ring window.  Every
+// read / write is bounds-checked; a malformed block sets *status.
 #include "dpz_common.h"
 
 namespace dpz {
