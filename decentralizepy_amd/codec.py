@@ -828,7 +828,12 @@ def lz4_decompress(frame, device, out=None, workspace=None, max_size=None):
         pin = wsp.lz4_pin = torch.empty(max(len(b), 4096), dtype=torch.uint8, pin_memory=True)
     if b:
         pin.numpy()[:len(b)] = np.frombuffer(b, dtype=np.uint8)
-    dframe = pin[:max(len(b), 1)].to(out.device, non_blocking=True)
+    # and into a device buffer kept with it (no allocation per call)
+    dbuf = getattr(wsp, "lz4_dev", None)
+    if dbuf is None or dbuf.numel() < max(len(b), 1) or dbuf.device != out.device:
+        dbuf = wsp.lz4_dev = torch.empty(max(len(b), 4096), dtype=torch.uint8, device=out.device)
+    dframe = dbuf[:max(len(b), 1)]
+    dframe.copy_(pin[:max(len(b), 1)], non_blocking=True)
     workspace = wsp
     need = int(_lib.lib().dpz_lz4_workspace_bytes(0, nb, 0 if linked else bmax))
     ws = _lz4_ws(workspace, out.device, need)

@@ -1183,6 +1183,7 @@ extern "C" int dpz_lz4_decompress(const uint8_t* frame_dev, const uint8_t* frame
   if (e != hipSuccess) return (int)e;
   uint64_t tot = 0;
   uint32_t bad = 0;
+  bool done = false;  // the parallel linked path read back status and total already
   if (nb > 0) {
     // ring of 64 KB (smaller when every block is: independent frames whose block max is
     // smaller) + the largest compressed block
@@ -1223,6 +1224,10 @@ extern "C" int dpz_lz4_decompress(const uint8_t* frame_dev, const uint8_t* frame
       if ((uint32_t)back2[0] & 2u) {  // a block the parallel decoder left: decode sequentially
         DPZ_HIP_TRY(hipMemsetAsync(status, 0, 16, st));
         par_linked = false;
+      } else {  // final: no second copy and synchronize (each costs a host round trip)
+        bad = (uint32_t)back2[0];
+        tot = back2[1];
+        done = true;
       }
     }
     if (linked && !par_linked) {
@@ -1242,12 +1247,14 @@ extern "C" int dpz_lz4_decompress(const uint8_t* frame_dev, const uint8_t* frame
                                     slots, dsize, nb, (uint32_t)bmax, out, (uint64_t)out_cap,
                                     total));
     }
-    // status (4 bytes, padding) and total (8 bytes) are adjacent: one copy back
-    uint64_t back[2] = {0, 0};
-    DPZ_HIP_TRY(hipMemcpyAsync(back, status, 16, hipMemcpyDeviceToHost, st));
-    DPZ_HIP_TRY(hipStreamSynchronize(st));
-    bad = (uint32_t)back[0];
-    tot = back[1];
+    if (!done) {
+      // status (4 bytes, padding) and total (8 bytes) are adjacent: one copy back
+      uint64_t back[2] = {0, 0};
+      DPZ_HIP_TRY(hipMemcpyAsync(back, status, 16, hipMemcpyDeviceToHost, st));
+      DPZ_HIP_TRY(hipStreamSynchronize(st));
+      bad = (uint32_t)back[0];
+      tot = back[1];
+    }
   }
   if (bad) return DPZ_ERR_ARG;
   if (cs >= 0 && (int64_t)tot != cs) return DPZ_ERR_ARG;
