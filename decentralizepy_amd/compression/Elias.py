@@ -54,9 +54,21 @@ class Elias(Compression):
         b = np.frombuffer(memoryview(buf), dtype=np.uint8)
         nbits, first = parse_trailer(b)
         nbytes = b.size
-        padded = torch.zeros(((nbytes + 3) // 4) * 4 + 16, dtype=torch.uint8)
-        padded[:nbytes] = torch.from_numpy(b.copy())
-        dbuf = padded.to(dev)
+        need = ((nbytes + 3) // 4) * 4 + 16
+        # up through a pinned buffer into a device buffer, both kept with the compressor (the
+        # decode synchronizes before it returns, so both are free again for the next call)
+        ws = self._ws
+        pin = getattr(ws, "elias_pin", None)
+        if pin is None or pin.numel() < need:
+            pin = ws.elias_pin = torch.empty(max(need, 4096), dtype=torch.uint8, pin_memory=True)
+        dbuf = getattr(ws, "elias_dev", None)
+        if dbuf is None or dbuf.numel() < need:
+            dbuf = ws.elias_dev = torch.empty(max(need, 4096), dtype=torch.uint8, device=dev)
+        pn = pin.numpy()
+        pn[:nbytes] = b
+        pn[nbytes:need] = 0
+        dbuf[:need].copy_(pin[:need], non_blocking=True)
+        dbuf = dbuf[:need]
         count = max(nbits - 128, 0) + 1
         return codec.elias_decode(dbuf, nbytes, nbits, first, count, dtype=dtype,
                                   workspace=self._ws)
