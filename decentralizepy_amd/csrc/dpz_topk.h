@@ -291,7 +291,9 @@ constexpr int64_t SL_RMAX = 8192;
 static inline int64_t mask_words(int64_t n) { return (n + 31) >> 5; }
 // sliced side effects from idx_out (the exact path, a sampled miss, segments over SL_RMAX):
 // selmask zeroed, bits set from idx_out[0..k), planes += selmask (dpz_topk.hip)
-int sliced_from_idx(const EncodeArgs& a);
+// guard (may be NULL): a device status word; the planes are left alone when it is nonzero (a
+// sampled call that missed: its output is void and the caller re-runs the encode exactly)
+int sliced_from_idx(const EncodeArgs& a, const uint32_t* guard = nullptr);
 // the fold base can ride on the pipelined filter: aligned, no accumulation, x0 given
 bool fused_foldbase_ok(const EncodeArgs& a, bool vec);
 // base_out[j] = fb.of(x[j]) as its own launch (dpz_fold.hip)

@@ -266,7 +266,8 @@ __global__ void __launch_bounds__(256) selmask_from_idx_kernel(const int32_t* __
 // no carry left, usually within two or three)
 __global__ void __launch_bounds__(256) planes_add_kernel(uint32_t* planes,
                                                          const uint32_t* __restrict__ mask,
-                                                         int64_t nw) {
+                                                         int64_t nw, const uint32_t* guard) {
+  if (guard && *guard) return;
   for (int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x; w < nw; w += (int64_t)gridDim.x * 256) {
     uint32_t carry = mask[w];
     for (int p = 0; p < 32 && carry != 0u; ++p) {
@@ -321,7 +322,7 @@ __global__ void __launch_bounds__(256) rewind_apply_kernel(float* acc,
     if ((mask[i >> 5] >> (i & 31)) & 1u) acc[i] = 0.0f;
 }
 
-int sliced_from_idx(const EncodeArgs& a) {
+int sliced_from_idx(const EncodeArgs& a, const uint32_t* guard) {
   const int64_t nw = mask_words(a.n);
   DPZ_HIP_TRY(hipMemsetAsync(a.selmask, 0, (size_t)nw * 4, a.st));
   if (a.k > 0)
@@ -329,7 +330,7 @@ int sliced_from_idx(const EncodeArgs& a) {
               selmask_from_idx_kernel<<<grid_of(a.k), 256, 0, a.st>>>(a.idx_out, a.k, a.selmask));
   if (a.planes && a.k > 0)
     DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st,
-              planes_add_kernel<<<grid_of(nw), 256, 0, a.st>>>(a.planes, a.selmask, nw));
+              planes_add_kernel<<<grid_of(nw), 256, 0, a.st>>>(a.planes, a.selmask, nw, guard));
   return DPZ_OK;
 }
 
@@ -364,15 +365,24 @@ extern "C" int dpz_topk_encode_sliced(const float* x, const float* x0, const flo
   }
   const WsLayout L = ws_layout(n, k, a.shared);
   const bool vec = all_aligned(a);
-  if (!(flags & DPZ_TOPK_EXACT) && use_sampled(n, k) && L.fg.R <= SL_RMAX) {
+  if (!(flags & DPZ_TOPK_EXACT) && use_sampled(n, k)) {
+    // segments of at most SL_RMAX elements: compact writes the mask words and the planes from
+    // its LDS rows; longer ones (n > SL_RMAX * W_MAX): compact writes idx / val only and the
+    // mask and planes are built from idx_out after it (skipped on the device after a miss)
+    const bool post = L.fg.R > SL_RMAX;
     a.status_out = status_out;
     rc = run_sampled(a, L, vec, 3);
     if (rc != DPZ_OK) return rc;
+    const uint32_t* ctrl_status =
+        reinterpret_cast<const uint32_t*>(a.ws + L.ctrl + offsetof(TopkCtrl, status));
+    if (post) {
+      rc = sliced_from_idx(a, ctrl_status);
+      if (rc != DPZ_OK) return rc;
+    }
     if (status_out) return DPZ_OK;  // asynchronous: a nonzero status -> re-run with EXACT
     DPZ_HIP_TRY(hipStreamSynchronize(a.st));
     uint32_t st = 0;
-    DPZ_HIP_TRY(hipMemcpy(&st, a.ws + L.ctrl + offsetof(TopkCtrl, status), sizeof(st),
-                          hipMemcpyDeviceToHost));
+    DPZ_HIP_TRY(hipMemcpy(&st, ctrl_status, sizeof(st), hipMemcpyDeviceToHost));
     if (st == 0) return DPZ_OK;
     a.status_out = nullptr;  // the miss wrote nothing: the exact path below
   }

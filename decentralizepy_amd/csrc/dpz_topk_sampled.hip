@@ -1486,10 +1486,11 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
                 s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, \
                 cidx, ckey, cval, a.vals_src, a.idx_out, a.val_out, counter, rewind,              \
                 a.status_out, jb[2], nrep_first, a.val_h, a.selmask, a.planes, mask_words(a.n))))
-  if (a.selmask) {
-    // sliced side effects (dpz_topk_encode_sliced): the host checked g.R <= SL_RMAX
+  if (a.selmask && g.R <= SL_RMAX) {
+    // sliced side effects (dpz_topk_encode_sliced) from per-wave LDS rows of the segment's words
     DPZ_COMPACT(false, 2, true);
-  } else if (plain) {
+  } else if (plain) {  // (sliced with longer segments: counter and rewind are null here, the
+                       // caller builds the mask and the planes from idx_out)
     if (spw == 8) DPZ_COMPACT(true, 8, false);
     else DPZ_COMPACT(true, 2, false);
   } else {

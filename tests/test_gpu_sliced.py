@@ -171,3 +171,20 @@ def test_sliced_rejects_bad_arguments(dev):
         codec.topk_encode_sliced(x, 3000, mask[:-1])
     with pytest.raises(Exception):  # rewind mask on a non-accumulating pass
         codec.wavedec(x, 4, x0=acc, rewind_mask=mask)
+
+
+@pytest.mark.parametrize("status", [False, True])
+def test_sliced_long_segments_build_the_mask_after_compact(dev, diag_lib, monkeypatch, status):
+    """Segments longer than the LDS rows hold (SL_RMAX; n > 67 M at the full grid, forced here
+    with the diagnostic build's DPZ_WLONE): compact writes idx / val only and the mask and the
+    planes are built from idx_out after it; after a sampled miss the planes stay untouched until
+    the exact re-run (blocking and asynchronous)."""
+    monkeypatch.setenv("DPZ_WLONE", "64")
+    n = 1_000_003
+    x, x0, acc = _inputs(n, seed=21)
+    _run(dev, x - x0, None, acc, otopk.ACC_ADD, round(0.1 * n), vals=x, status=status)
+    from tests.layouts import miss_layout
+    n = 1 << 20
+    k = round(0.01 * n)
+    x, x0 = miss_layout(n, k)
+    _run(dev, x, x0, None, otopk.ACC_NONE, k, status=status)
