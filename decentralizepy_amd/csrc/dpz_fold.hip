@@ -1854,6 +1854,37 @@ __global__ void __launch_bounds__(256) fold_patch_kernel(FoldArgs a, int64_t ran
   }
 }
 
+// One payload: its indices are unique, so every hit element is hit once and each entry folds its
+// element alone (out[e] = v·w + x[e]·w_self, the reference's order) — no tile runs, no pre-pass.
+// Four entries per thread, strided by the block so the idx / val loads stay coalesced; the local
+// gathers of all four are issued before any store.
+__global__ void __launch_bounds__(256) fold_patch1_kernel(const int32_t* __restrict__ idx,
+                                                          const float* __restrict__ val, int64_t k,
+                                                          const float* __restrict__ local,
+                                                          float* __restrict__ out, int64_t n,
+                                                          float w, float w_self) {
+  const int64_t j0 = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+  int32_t e[4];
+  float v[4], xv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t j = j0 + 256 * i;
+    e[i] = j < k ? idx[j] : -1;
+    v[i] = j < k ? val[j] : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (e[i] >= n) e[i] = -1;  // an invalid payload cannot write outside
+    xv[i] = local[e[i] >= 0 ? e[i] : 0];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (e[i] < 0) continue;
+    const float acc = v[i] * w;
+    out[e[i]] = acc + xv[i] * w_self;
+  }
+}
+
 static int launch_fold_patch(FoldArgs fa, int32_t* starts, hipStream_t st) {
   int64_t etot = 0, kmax = 0;
   for (int i = 0; i < fa.np; ++i) {
@@ -1861,6 +1892,12 @@ static int launch_fold_patch(FoldArgs fa, int32_t* starts, hipStream_t st) {
     if (fa.p[i].k > kmax) kmax = fa.p[i].k;
   }
   if (etot == 0) return DPZ_OK;
+  if (fa.np == 1) {
+    DPZ_TIMED(DPZ_KT_FOLD, st,
+              fold_patch1_kernel<<<(unsigned)((kmax + 1023) / 1024), 256, 0, st>>>(
+                  fa.p[0].idx, fa.p[0].val, kmax, fa.local, fa.out, fa.n, fa.p[0].w, fa.w_self));
+    return DPZ_OK;
+  }
   fa.ntiles = fold_ntiles(fa.n);
   dim3 og((unsigned)((kmax + 1 + 1023) / 1024), (unsigned)fa.np);
   DPZ_TIMED(DPZ_KT_FOLD_OFFSETS, st,

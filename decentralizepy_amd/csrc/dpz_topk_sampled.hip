@@ -80,6 +80,7 @@ __global__ void __launch_bounds__(1024) sampled_sample_kernel(KeySrc s, int64_t 
     return;
   }
   STAMP_MIN(0);
+  STAMP_T0(13);
   __shared__ uint32_t h[CB];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nw = (int)(blockDim.x >> 6);
@@ -113,6 +114,7 @@ __global__ void __launch_bounds__(1024) sampled_sample_kernel(KeySrc s, int64_t 
     if (c) atomicAdd(&chist[b], c);
   }
   STAMP_MAX(1);
+  STAMP_T0(14);
 }
 
 // Block-level (256 threads): window [lo, hi) around the k-th key from the coarse sample histogram.
@@ -421,6 +423,7 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t st[4][3 * STAGE];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  STAMP_T0(5);
   for (int b = threadIdx.x; b < HBR; b += 256) h[b] = 0;
   const int64_t seg = (int64_t)blockIdx.x * 4 + wid;
   const int64_t beg = seg * R;  // a multiple of 4 (R is); >= n for the grid's spare waves
@@ -450,6 +453,7 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
 #pragma unroll
   for (int u = 0; u < D - 1; ++u) ld(u, u);
   block_window(cv, r_lo, r_hi, win, wsum);
+  STAMP_T0(6);
   const uint32_t lo = win[0], hi = win[1], shift = win[2];
   if (seg == 0 && lane == 0) {
     ctrl->lo = lo;
@@ -514,6 +518,7 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
     if (v) atomicAdd(&gcopy[b], v);
   }
   if (lane == 0 && seg < W) segcnt[seg] = dense ? DENSE : run;
+  STAMP_T0(7);
 }
 
 // Wave-level threshold bin from the global window histogram gh (LDS, HB fine bins + the

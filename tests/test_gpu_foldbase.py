@@ -52,6 +52,7 @@ def _bits(a):
     # clustered payloads: a block's runs overflow the LDS stage and are halved
     (1_000_000, 0.01, [60_000, 60_000, 60_000], None, 0.0, [0, 10_000, 30_000]),
     (100_000, 0.01, [1_000, 1_000], None, 0.0, None),  # exact-path encode: separate base pass
+    (1_000_003, 0.02, [12_345], [0.3], 0.0, None),  # one payload: the per-entry patch
 ])
 def test_foldbase_encode_and_patch_match_oracle(dev, n, alpha, ks, weights, overlap, cluster):
     rng = np.random.default_rng(n + len(ks))
