@@ -29,7 +29,17 @@ constexpr int DWT_TL = DPZ_DWT_TL;
 #ifndef DPZ_DWT4_WAVES  // the level-4 kernel (interior path)
 #define DPZ_DWT4_WAVES 4
 #endif
-constexpr int IDWT_TILE = 4096;
+#ifndef DPZ_IDWT_TILE
+#define DPZ_IDWT_TILE 4096
+#endif
+constexpr int IDWT_TILE = DPZ_IDWT_TILE;
+// The IDWT's final outputs are stored non-temporally (written once, not re-read by the pass):
+// 50.1 -> 44.1 us at N = 25 M standalone, 46.0 -> 45.2 us inside the C3 round (MI355X, same-box
+// A/B, tools/diag/idwt_ab.py).  Tried and not kept: non-temporal coefficient loads (no gain), one
+// thread per output pair with 8-byte stores (49.5 us), 2048-output tiles (55.1 us).
+#ifndef DPZ_IDWT_NT
+#define DPZ_IDWT_NT 1
+#endif
 
 // sym2 filters (fp32 casts of pywt's double coefficients)
 __constant__ float c_dec_lo[4] = {-0.12940952255092145f, 0.22414386804185735f,
@@ -662,7 +672,12 @@ __device__ __forceinline__ void idwt_levels(const Levels& LV, const IdwtRanges& 
         yd = h1 * dm1; yd = yd + h3 * dm;
       }
       const float y = ya + yd;
-      if (l == 1) o1[qr] = y; else bnext[qr] = y;
+      if (l == 1) {
+        if (DPZ_IDWT_NT) __builtin_nontemporal_store(y, o1 + qr);
+        else o1[qr] = y;
+      } else {
+        bnext[qr] = y;
+      }
     }
     if (l == 1) break;
     __syncthreads();

@@ -243,7 +243,9 @@ __global__ void __launch_bounds__(256) haar_idwt_kernel(const float* __restrict_
     y[2] = h * a11; y[2] = y[2] + h * d11;
     y[3] = h * a11; y[3] = y[3] + (-h) * d11;
     if (vec && Q0 + 4 <= n) {
-      *reinterpret_cast<float4*>(out + Q0) = make_float4(y[0], y[1], y[2], y[3]);
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      const v4f v = {y[0], y[1], y[2], y[3]};  // written once: non-temporal, as the sym2 IDWT
+      __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(out + Q0));
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
