@@ -149,6 +149,12 @@ SIGNATURES = {
     "dpz_dwt_haar": (_int, [_c_void_p, _c_void_p, _i64, _int, _c_void_p, _c_void_p, _int,
                             _c_void_p]),
     "dpz_idwt_haar": (_int, [_c_void_p, _i64, _int, _c_void_p, _c_void_p]),
+    "dpz_wavedec_len_generic": (_i64, [_i64, _int, _int]),
+    "dpz_wavelet_generic_workspace_bytes": (_size, [_i64, _int, _int]),
+    "dpz_dwt_generic": (_int, [_c_void_p, _c_void_p, _i64, _int, _c_void_p, _int, _c_void_p,
+                               _c_void_p, _int, _c_void_p, _c_void_p, _size, _c_void_p]),
+    "dpz_idwt_generic": (_int, [_c_void_p, _i64, _int, _c_void_p, _int, _c_void_p, _c_void_p,
+                                _size, _c_void_p]),
     "dpz_lz4_max_bytes": (_i64, [_i64]),
     "dpz_lz4_workspace_bytes": (_size, [_i64, _i64, _i64]),
     "dpz_lz4_compress": (_int, [_c_void_p, _i64, _c_void_p, _i64, ctypes.POINTER(_i64),

@@ -468,18 +468,72 @@ def replace(local, idx, vals, out=None, workspace=None):
     return decode_average(local, [(idx, vals)], out=out, replace_only=True, workspace=workspace)
 
 
-WAVELETS = ("sym2", "haar")
+WAVELETS = ("sym2", "haar")  # the fused kernels (dpz_dwt.hip, dpz_haar.hip)
+_BANKS = None
+_BANK_DEV = {}
+
+
+def _bank_table():
+    """pywt's fp32 filter banks (decentralizepy_amd/wavelet_filters.json, generated from
+    PyWavelets 1.1.1 by tools/gen_wavelet_filters.py)."""
+    global _BANKS
+    if _BANKS is None:
+        import json
+        import os
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                               "wavelet_filters.json")) as f:
+            _BANKS = json.load(f)["wavelets"]
+    return _BANKS
+
+
+def wavelet_names():
+    """Every wavelet the device kernels implement: sym2 / haar (fused kernels) and every other
+    pywt discrete wavelet with an even filter length <= 64 (dpz_dwt_generic)."""
+    return sorted(set(WAVELETS) | set(_bank_table()))
+
+
+def filter_len(wavelet):
+    _check_wavelet(wavelet)
+    return {"sym2": 4, "haar": 2}.get(wavelet) or len(_bank_table()[wavelet][0])
 
 
 def _check_wavelet(wavelet):
-    if wavelet not in WAVELETS:
-        raise NotImplementedError(f"wavelet '{wavelet}': the device kernels implement {WAVELETS}")
+    if wavelet not in WAVELETS and wavelet not in _bank_table():
+        raise NotImplementedError(
+            f"wavelet '{wavelet}': the device kernels implement sym2, haar and the pywt discrete "
+            f"wavelets with filter length <= 64 ({len(_bank_table())} names, wavelet_names())")
+
+
+def _fused(wavelet, level):
+    """sym2 to level 4 and haar to level 8 run the fused kernels; every other (wavelet, level)
+    the generic-filter path."""
+    return (wavelet == "sym2" and int(level) <= 4) or (wavelet == "haar" and int(level) <= 8)
+
+
+def _bank(wavelet, device):
+    """The filter bank in device memory: dec_lo, dec_hi, rec_lo, rec_hi (4F fp32)."""
+    key = (wavelet, str(device))
+    t = _BANK_DEV.get(key)
+    if t is None:
+        b = np.concatenate([np.array(v, dtype=np.uint32) for v in _bank_table()[wavelet]])
+        t = torch.from_numpy(b.view(np.float32).copy()).to(device)
+        _BANK_DEV[key] = t
+    return t
+
+
+def _generic_ws(n, level, wavelet, device):
+    nb = int(_lib.lib().dpz_wavelet_generic_workspace_bytes(int(n), int(level),
+                                                            filter_len(wavelet)))
+    return torch.empty(max(1, (nb + 3) // 4), dtype=torch.float32, device=device), nb
 
 
 def wavedec_len(n, level=4, wavelet="sym2"):
     _check_wavelet(wavelet)
-    fn = _lib.lib().dpz_wavedec_len if wavelet == "sym2" else _lib.lib().dpz_haar_wavedec_len
-    m = int(fn(int(n), int(level)))
+    if _fused(wavelet, level):
+        fn = _lib.lib().dpz_wavedec_len if wavelet == "sym2" else _lib.lib().dpz_haar_wavedec_len
+        m = int(fn(int(n), int(level)))
+    else:
+        m = int(_lib.lib().dpz_wavedec_len_generic(int(n), int(level), filter_len(wavelet)))
     if m < 0:
         raise ValueError(f"{wavelet} level-{level} wavedec unsupported for n={n}")
     return m
@@ -487,8 +541,9 @@ def wavedec_len(n, level=4, wavelet="sym2"):
 
 def wavedec(x, level=4, x0=None, want_x=True, coeffs_x=None, coeffs_diff=None, accumulate=False,
             wavelet="sym2", rewind_mask=None):
-    """Multilevel DWT (``wavelet`` "sym2" or "haar", mode "symmetric") as one
-    ``coeffs_to_array`` vector (reference Wavelet.py:12-32).
+    """Multilevel DWT (mode "symmetric"; ``wavelet`` "sym2" / "haar" on the fused kernels, any
+    other name of :func:`wavelet_names` on dpz_dwt_generic) as one ``coeffs_to_array`` vector
+    (reference Wavelet.py:12-32).
 
     Returns ``(W(x) or None, W(x - x0) or None)``; with ``accumulate=True`` adds W(x - x0) into
     ``coeffs_diff`` instead of overwriting it.  ``rewind_mask`` (with ``accumulate``, no W(x)): the
@@ -506,6 +561,14 @@ def wavedec(x, level=4, x0=None, want_x=True, coeffs_x=None, coeffs_diff=None, a
         m = wavedec_len(n, level, wavelet)
         if coeffs_diff.numel() != m or x0.numel() != n or rewind_mask.numel() < mask_words(m):
             raise ValueError("rewind_mask: size mismatch")
+        if not _fused(wavelet, level):
+            ws, nb = _generic_ws(n, level, wavelet, x.device)
+            rc = _lib.lib().dpz_dwt_generic(
+                _ptr(x), _ptr(x0), n, int(level), _ptr(_bank(wavelet, x.device)),
+                filter_len(wavelet), None, _ptr(coeffs_diff), 1, _ptr(rewind_mask), _ptr(ws), nb,
+                _stream(x.device))
+            check(rc, f"dpz_dwt_generic({wavelet})")
+            return None, coeffs_diff
         fn = (_lib.lib().dpz_dwt_sym2_rewind if wavelet == "sym2"
               else _lib.lib().dpz_dwt_haar_rewind)
         rc = fn(_ptr(x), _ptr(x0), n, int(level), _ptr(coeffs_diff), _ptr(rewind_mask),
@@ -529,16 +592,25 @@ def wavedec(x, level=4, x0=None, want_x=True, coeffs_x=None, coeffs_diff=None, a
             raise ValueError(f"{nm} must hold wavedec_len(n, level) = {m} values")
     if x0 is not None and x0.numel() != n:
         raise ValueError("x0 must match x")
-    fn = _lib.lib().dpz_dwt_sym2 if wavelet == "sym2" else _lib.lib().dpz_dwt_haar
-    rc = fn(_ptr(x), _ptr(x0), n, int(level), _ptr(coeffs_x if want_x else None),
-            _ptr(coeffs_diff if x0 is not None else None), 1 if accumulate else 0,
-            _stream(x.device))
-    check(rc, f"dpz_dwt_{wavelet}")
+    if not _fused(wavelet, level):
+        ws, nb = _generic_ws(n, level, wavelet, x.device)
+        rc = _lib.lib().dpz_dwt_generic(
+            _ptr(x), _ptr(x0), n, int(level), _ptr(_bank(wavelet, x.device)), filter_len(wavelet),
+            _ptr(coeffs_x if want_x else None), _ptr(coeffs_diff if x0 is not None else None),
+            1 if accumulate else 0, None, _ptr(ws), nb, _stream(x.device))
+        check(rc, f"dpz_dwt_generic({wavelet})")
+    else:
+        fn = _lib.lib().dpz_dwt_sym2 if wavelet == "sym2" else _lib.lib().dpz_dwt_haar
+        rc = fn(_ptr(x), _ptr(x0), n, int(level), _ptr(coeffs_x if want_x else None),
+                _ptr(coeffs_diff if x0 is not None else None), 1 if accumulate else 0,
+                _stream(x.device))
+        check(rc, f"dpz_dwt_{wavelet}")
     return (coeffs_x if want_x else None), (coeffs_diff if x0 is not None else None)
 
 
 def waverec(coeffs, n, level=4, out=None, wavelet="sym2"):
-    """Multilevel IDWT ("sym2" or "haar"), first n outputs (reference Wavelet.py:311-316)."""
+    """Multilevel IDWT (any wavelet of :func:`wavelet_names`), first n outputs (reference
+    Wavelet.py:311-316)."""
     _require(coeffs, torch.float32, "coeffs")
     if coeffs.numel() != wavedec_len(n, level, wavelet):
         raise ValueError("coeffs must hold wavedec_len(n, level) values")
@@ -547,6 +619,13 @@ def waverec(coeffs, n, level=4, out=None, wavelet="sym2"):
     _require(out, torch.float32, "out")
     if out.numel() < int(n):
         raise ValueError("out must hold n values")
+    if not _fused(wavelet, level):
+        ws, nb = _generic_ws(n, level, wavelet, coeffs.device)
+        rc = _lib.lib().dpz_idwt_generic(_ptr(coeffs), int(n), int(level),
+                                         _ptr(_bank(wavelet, coeffs.device)), filter_len(wavelet),
+                                         _ptr(out), _ptr(ws), nb, _stream(coeffs.device))
+        check(rc, f"dpz_idwt_generic({wavelet})")
+        return out
     fn = _lib.lib().dpz_idwt_sym2 if wavelet == "sym2" else _lib.lib().dpz_idwt_haar
     rc = fn(_ptr(coeffs), int(n), int(level), _ptr(out), _stream(coeffs.device))
     check(rc, f"dpz_idwt_{wavelet}")

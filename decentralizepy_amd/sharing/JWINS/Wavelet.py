@@ -17,9 +17,13 @@ Device path per round (all HIP kernels, fp32, pywt-1.1.1-exact summation order):
   post-step  acc += W(x_new - prev) as one accumulating DWT launch (PartialModel.py:346-349),
              applying the encode's deferred rewind as it goes (dpz_dwt_sym2_rewind)
 
-Device kernels exist for ``wavelet="sym2"`` with ``level <= 4`` (every shipped JWINS config, e.g.
-tutorial/JWINS/config.ini) and for the reference's default ``wavelet="haar"`` with ``level <= 8``;
-other wavelets raise NotImplementedError.
+Fused device kernels run ``wavelet="sym2"`` with ``level <= 4`` (every shipped JWINS config,
+e.g. tutorial/JWINS/config.ini) and the reference's default ``wavelet="haar"`` with
+``level <= 8``; every other pywt discrete wavelet with an even filter length <= 64 (db1-32,
+sym2-20, coif1-10, bior / rbio, dmey) and levels to 8 runs the generic-filter kernels
+(dpz_dwt_generic / dpz_idwt_generic), bit-exact with PyWavelets 1.1.1 as well.  A level at which
+an input would be shorter than the filter (pywt's multi-reflection case) raises
+NotImplementedError, as do names pywt does not know.
 """
 import numpy as np
 import torch
@@ -29,15 +33,13 @@ from ..._device import DeviceAccumulator, SlicedCounter, to_host
 from ...utils import identity
 from ..PartialModel import PartialModel
 
-SUPPORTED_WAVELETS = ("sym2", "haar")
-MAX_LEVEL = {"sym2": 4, "haar": 8}
-FILTER_LEN = {"sym2": 4, "haar": 2}
+MAX_LEVEL = 8
 
 
 def coeff_slices(n, level, wavelet="sym2"):
     """``pywt.coeffs_to_array`` slices of a 1-D ``wavedec`` (array layout [cA_L, cD_L..cD_1]);
     level lengths floor((len + filter_len - 1) / 2) (pywt.dwt_coeff_len, mode symmetric)."""
-    f = FILTER_LEN[wavelet]
+    f = codec.filter_len(wavelet)
     lens = [int(n)]
     for _ in range(level):
         lens.append((lens[-1] + f - 1) // 2)
@@ -59,12 +61,12 @@ class Wavelet(PartialModel):
                  compression_package=None, compression_class=None):
         self.wavelet = wavelet
         self.level = int(level)
-        if wavelet not in SUPPORTED_WAVELETS:
+        if wavelet not in codec.wavelet_names():
             raise NotImplementedError(
-                f"wavelet '{wavelet}': the device DWT kernels implement {SUPPORTED_WAVELETS}")
-        if not 1 <= self.level <= MAX_LEVEL[wavelet]:
-            raise NotImplementedError(
-                f"the device {wavelet} DWT kernels implement levels 1..{MAX_LEVEL[wavelet]}")
+                f"wavelet '{wavelet}': the device DWT kernels implement sym2, haar and the pywt "
+                f"discrete wavelets with filter length <= 64 (codec.wavelet_names())")
+        if not 1 <= self.level <= MAX_LEVEL:
+            raise NotImplementedError(f"the device DWT kernels implement levels 1..{MAX_LEVEL}")
         super().__init__(rank, machine_id, communication, mapping, graph, model, dataset, log_dir,
                          alpha, dict_ordered, save_shared, metadata_cap, accumulation,
                          save_accumulated, identity, accumulate_averaging_changes, compress,

@@ -357,6 +357,25 @@ int dpz_idwt_haar(const float* coeffs, int64_t n, int level, float* out, dpz_str
 int dpz_dwt_haar_rewind(const float* x, const float* x0, int64_t n, int level, float* acc,
                         const uint32_t* sel_mask, dpz_stream_t stream);
 
+/* ---- Any other pywt discrete wavelet (db1-32, sym2-20, coif1-10, bior / rbio, dmey: even filter
+ * length flen <= 64), mode "symmetric", levels 1..8 with every level's input >= flen values.
+ * Replaces reference sharing/JWINS/Wavelet.py:12-32 and :311-316 (pywt.wavedec / waverec with
+ * the configured `wavelet`) for the wavelets the fused sym2 / haar kernels do not cover.
+ * `bank` is DEVICE memory: 4*flen floats dec_lo, dec_hi, rec_lo, rec_hi — the fp32 taps pywt
+ * applies to float32 data (decentralizepy_amd/wavelet_filters.json).  Level lengths
+ * len_l = floor((len_{l-1} + flen - 1) / 2), layout [cA_L, cD_L, ..., cD_1].  Bit-exact with
+ * PyWavelets 1.1.1 (csrc/dpz_wvgen.hip gives the summation order).  dpz_dwt_generic: W(x) into
+ * coeffs_x and / or W(x - x0) into coeffs_diff (accumulate: added; sel_mask, with accumulate:
+ * the deferred rewind of dpz_topk_encode_sliced, as dpz_dwt_sym2_rewind); ws of
+ * dpz_wavelet_generic_workspace_bytes (levels >= 2).  Unsupported lengths: -1 / DPZ_ERR_UNSUPPORTED. */
+int64_t dpz_wavedec_len_generic(int64_t n, int level, int flen);
+size_t dpz_wavelet_generic_workspace_bytes(int64_t n, int level, int flen);
+int dpz_dwt_generic(const float* x, const float* x0, int64_t n, int level, const float* bank,
+                    int flen, float* coeffs_x, float* coeffs_diff, int accumulate,
+                    const uint32_t* sel_mask, void* ws, size_t ws_bytes, dpz_stream_t stream);
+int dpz_idwt_generic(const float* coeffs, int64_t n, int level, const float* bank, int flen,
+                     float* out, void* ws, size_t ws_bytes, dpz_stream_t stream);
+
 
 /* dst[idx[j]] = value for j < k (indices outside [0, n) are ignored).
  * Replaces reference models/Model.py:53-64 (rewind_accumulation: acc[idx] = 0) where the rewind

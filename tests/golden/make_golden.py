@@ -529,6 +529,46 @@ def haar_main():
     print("wrote", len(scen), "haar scenarios,", len(cases), "pywt cases")
 
 
+def generic_main():
+    """The reference Wavelet plugin with wavelets other than sym2 / haar (any pywt name reaches
+    pywt.wavedec / waverec, sharing/JWINS/Wavelet.py:12-32, 311-316): multi-round scenarios
+    (plain with mixed full payloads, accumulation, accumulate-averaging, no change-based
+    selection, the federated server, sym2 past level 4) -> tests/golden/wg_*.npz +
+    wavelet_generic_scenarios.json (the pywt vectors: make_golden_wavelets.py)."""
+    torch.set_num_threads(4)
+    wv = {"alpha": 0.1, "metadata_cap": 0.5}
+    mixed = [["partial", "full", "partial"], ["full", "partial", "partial"]]
+    scen = [
+        run_scenario("wg_db4_plain", Wavelet, {**wv, "wavelet": "db4", "level": 4}, 20, 50, 1, 2,
+                     seed=91, wavelet=True, nbr_kinds=mixed),
+        run_scenario("wg_coif3_acc", Wavelet,
+                     {**wv, "wavelet": "coif3", "level": 3, "accumulation": True},
+                     40, 100, 99, 2, seed=92, wavelet=True),
+        run_scenario("wg_sym5_accavg", Wavelet,
+                     {**wv, "wavelet": "sym5", "level": 4, "accumulation": True,
+                      "accumulate_averaging_changes": True}, 40, 100, 99, 2, seed=93,
+                     wavelet=True),
+        run_scenario("wg_bior35_nochange", Wavelet,
+                     {**wv, "wavelet": "bior3.5", "level": 4, "accumulation": True,
+                      "change_based_selection": False}, 40, 100, 99, 2, seed=94, wavelet=True),
+        run_scenario("wg_dmey_plain", Wavelet, {**wv, "wavelet": "dmey", "level": 2},
+                     40, 100, 99, 2, seed=95, wavelet=True),
+        run_scenario("wg_sym2_l6_acc", Wavelet,
+                     {**wv, "wavelet": "sym2", "level": 6, "accumulation": True},
+                     40, 100, 99, 2, seed=96, wavelet=True),
+        run_scenario("wg_db8_server", Wavelet,
+                     {**wv, "wavelet": "db8", "level": 3, "accumulation": True},
+                     40, 100, 99, 2, seed=97, wavelet=True, nbr_kinds=mixed,
+                     averaging="_averaging_server"),
+    ]
+    with open(os.path.join(OUT, "wavelet_generic_scenarios.json"), "w") as f:
+        json.dump({"scenarios": scen, "generator": "tests/golden/make_golden.py --generic",
+                   "reference": "sacs-epfl/decentralizepy v1 (/root/reference/src)",
+                   "pywavelets": "1.1.1 (python3.9 bridge)", "torch": torch.__version__}, f,
+                  indent=1)
+    print("wrote", len(scen), "generic-wavelet scenarios")
+
+
 def model_change_main():
     """``model.model_change`` as the reference leaves it after get_data_to_send
     (PartialModel.py:317-331: T(x - init), with accumulation the accumulated change before the
@@ -564,6 +604,8 @@ if __name__ == "__main__":
         model_change_main()
     elif "--haar" in sys.argv:
         haar_main()
+    elif "--generic" in sys.argv:
+        generic_main()
     elif "--fullsize" in sys.argv:
         fullsize_main()
     elif "--wire" in sys.argv:

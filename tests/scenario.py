@@ -24,7 +24,8 @@ def load_meta():
     """scenarios.json plus the federated-server scenarios (server_scenarios.json), merged."""
     with open(os.path.join(GOLDEN, "scenarios.json")) as f:
         meta = json.load(f)
-    for extra in ("server_scenarios.json", "haar_scenarios.json", "model_change_scenarios.json"):
+    for extra in ("server_scenarios.json", "haar_scenarios.json", "model_change_scenarios.json",
+                  "wavelet_generic_scenarios.json"):
         with open(os.path.join(GOLDEN, extra)) as f:
             meta["scenarios"] = meta["scenarios"] + json.load(f)["scenarios"]
     return meta

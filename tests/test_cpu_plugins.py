@@ -61,14 +61,20 @@ def test_plugin_fails_loudly_without_gpu(tmp_path):
 
 
 def test_unsupported_wavelet_is_rejected(tmp_path):
+    """Names pywt has no discrete filter bank of length <= 64 for (db33+: 66 taps and more,
+    continuous wavelets) and levels past 8 raise; db4 etc. are supported (generic kernels)."""
+    from decentralizepy_amd import codec
     from decentralizepy_amd.sharing.JWINS.Wavelet import Wavelet
     model = scenario.make_model([4, 4, 2])
-    with pytest.raises(NotImplementedError, match="db4"):
+    for name in ("db34", "morl", "nope"):
+        with pytest.raises(NotImplementedError, match=name):
+            Wavelet(0, 0, None, scenario._Mapping(), scenario._Graph([1]), model, None,
+                    str(tmp_path), wavelet=name)
+    with pytest.raises(NotImplementedError, match="levels 1..8"):
         Wavelet(0, 0, None, scenario._Mapping(), scenario._Graph([1]), model, None,
-                str(tmp_path), wavelet="db4")
-    with pytest.raises(NotImplementedError, match="levels 1..4"):
-        Wavelet(0, 0, None, scenario._Mapping(), scenario._Graph([1]), model, None,
-                str(tmp_path), wavelet="sym2", level=5)
+                str(tmp_path), wavelet="sym2", level=9)
+    assert {"db4", "sym5", "coif3", "bior3.5", "rbio2.2", "dmey", "db32"} <= set(
+        codec.wavelet_names())
 
 
 def test_compression_surface_and_trailer():
