@@ -89,6 +89,6 @@ def test_generic_pair_and_accumulate_match_oracle(dev, name, n, level):
 def test_generic_rejects_short_levels(dev):
     from decentralizepy_amd import codec
     with pytest.raises(ValueError):
-        codec.wavedec_len(100, 3, "dmey")  # level-2 input of 80 values < 62 taps
+        codec.wavedec_len(62, 2, "dmey")  # level-2 input of 61 values < 62 taps
     with pytest.raises(NotImplementedError):
         codec.wavedec_len(100_000, 2, "db40")
