@@ -88,6 +88,10 @@ class GossipRound:
         self.adj = adj
         self.n_nodes = len(adj)
         self.rank, self.world, self.group = rank, world, group
+        # the exchange runs through the collectives with more than one rank, or whenever the
+        # caller hands over a process group (one rank too: the RCCL path then runs as a loopback,
+        # tests/test_gpu_rccl.py); one rank without a group exchanges in place
+        self.coll = world > 1 or group is not None
         self.lo, self.hi, self.per = shard(self.n_nodes, world, rank)
         assert x_init.shape[0] == self.hi - self.lo
         self.N = x_init.shape[1]
@@ -104,7 +108,7 @@ class GossipRound:
                 hbm_budget = torch.cuda.mem_get_info(self.device)[0] // 2
             else:
                 hbm_budget = float("inf")
-        if world > 1:
+        if self.coll:
             # the exchange mode and the reduce-scatter group size decide which collectives every
             # rank issues: all ranks must derive them from ONE budget (the smallest), or ranks
             # with slightly different free memory issue mismatched collectives and hang
@@ -274,7 +278,7 @@ class GossipRound:
             # persistent packed buffers sized for the largest group (within the budget)
             self._rs_send = torch.zeros(W, G, 2, N, dtype=torch.float32, device=self.device)
             self._rs_recv = (torch.empty(G, 2, N, dtype=torch.float32, device=self.device)
-                             if W > 1 else None)
+                             if self.coll else None)
             self._rs_args = {}
         t_mark = self._leg_mark(None)  # per-leg timing (bench only, self.leg_times)
         for g0, gsz, jobs, empty in self._rs:
@@ -310,7 +314,7 @@ class GossipRound:
             for r, j in empty:  # rows of destinations with no neighbour on this rank
                 send[r, j].zero_()
             t_mark = self._leg_mark(t_mark, "rs_partial")
-            if W > 1:
+            if self.coll:
                 # the slice [:, :gsz] of a (W, G, 2, N) buffer is contiguous only when gsz == G
                 src = send if send.is_contiguous() else send.contiguous()
                 recv = self._rs_recv[:gsz]
@@ -346,7 +350,7 @@ class GossipRound:
     def exchange(self):
         if self.exchange_mode == "reduce_scatter":
             return  # folded into fold_reduce_scatter
-        if self.world == 1:
+        if not self.coll:
             self.recv_idx, self.recv_val = self.send_idx, self.send_val  # no copy on one rank
             return
         import torch.distributed as dist

@@ -168,6 +168,7 @@ class JwinsRound:
                  m_len=None):
         self.adj, self.n_nodes = adj, len(adj)
         self.rank, self.world, self.group = rank, world, group
+        self.coll = world > 1 or group is not None  # as GossipRound.coll
         self.lo, self.hi, self.per = shard(self.n_nodes, world, rank)
         assert x_init.shape[0] == self.hi - self.lo
         self.N = x_init.shape[1]
@@ -216,7 +217,7 @@ class JwinsRound:
         self.send_idx = torch.zeros(self.per * self.slot_idx, dtype=torch.int32,
                                     device=self.device)
         self.send_val = torch.zeros(self.per * self.slot_val, **f32)
-        if world > 1:
+        if self.coll:
             self.recv_idx = torch.empty(world * self.per * self.slot_idx, dtype=torch.int32,
                                         device=self.device)
             self.recv_val = torch.empty(world * self.per * self.slot_val, **f32)
@@ -255,13 +256,13 @@ class JwinsRound:
     def _payload(self, q, lay, s_idx, s_val):
         partial, k, oi, ov = lay[q]
         r = q // self.per
-        if self.world > 1:
+        if self.coll:
             bi, bv = self.recv_idx[r * s_idx:], self.recv_val[r * s_val:]
         else:
             bi, bv = self.send_idx, self.send_val
         if partial:
             return bi[oi:oi + k], bv[ov:ov + k]
-        if self.world == 1:
+        if not self.coll:
             return None, self.wx[q - self.lo]  # the full W(x), no copy on one rank
         return None, bv[ov:ov + self.M]
 
@@ -301,7 +302,7 @@ class JwinsRound:
                         self.pending[j] = False
                     self.acc[j].zero_()
                     self.status[j:j + 1].zero_()
-                    if self.world > 1:
+                    if self.coll:
                         self.send_val[ov:ov + self.M].copy_(self.wx[j])
         self._join()
         # a sampled-path miss (rare) left that node's payload and bookkeeping untouched: redo it
@@ -316,7 +317,7 @@ class JwinsRound:
                                       self.send_idx[oi:oi + k], self.send_val[ov:ov + k])
 
     def exchange(self, s_idx, s_val):
-        if self.world == 1:
+        if not self.coll:
             return
         import torch.distributed as dist
         dist.all_gather_into_tensor(self.recv_idx[:self.world * s_idx], self.send_idx[:s_idx],

@@ -101,6 +101,8 @@ def sharded_topk_encode(x, x0, k, offset, counter=None, group=None, ops=None, va
     """
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_initialized() else 1
+    # collectives with more than one rank, or with an explicit group (one rank: RCCL loopback)
+    coll = dist.is_initialized() and (world > 1 or group is not None)
     if x.numel() < k:
         raise ValueError("every shard must hold at least k elements")
     ops = ops or HipShardOps(x.device)
@@ -111,7 +113,7 @@ def sharded_topk_encode(x, x0, k, offset, counter=None, group=None, ops=None, va
             idx, chg, val = ops.local_candidates(x, x0, k, offset, exact=exact)
         st = (ops.local_status() if hasattr(ops, "local_status")
               else torch.zeros(1, dtype=torch.int32, device=idx.device))
-        if world > 1:
+        if coll:
             # one exchange: the candidate arrays and the status word, packed as bytes
             # (index, change: 4 B; value: 4 or 2 B) in ONE all-gather
             vb = val.element_size()
@@ -320,7 +322,8 @@ def sharded_wavedec(x_slice, x0_slice, n, level, group=None, accumulate_into=Non
                              "halo)")
     dev = x_slice.device
     xb, x0b, first = x_slice, x0_slice, sl["lo"]
-    if world > 1:
+    coll = dist.is_initialized() and (world > 1 or group is not None)  # as sharded_topk_encode
+    if coll:
         # the left halo: the last H elements of the previous non-empty slice (x and x0), one
         # all-gather; an empty slice sends nothing useful and receives nothing
         tail = torch.zeros(2 * H, dtype=torch.float32, device=dev)
@@ -342,7 +345,7 @@ def sharded_wavedec(x_slice, x0_slice, n, level, group=None, accumulate_into=Non
     if sl["t_lo"] < sl["t_hi"]:
         dwt_rank_part(xb, x0b, first, n, level, sl["t_lo"], sl["t_hi"], cx, cd,
                       accumulate=accumulate_into is not None)
-    if world > 1:
+    if coll:
         _exchange_owned([cx, cd], n, level, world, rank, group, dist, widths)
     return cx, cd
 
