@@ -579,7 +579,6 @@ __host__ __device__ constexpr int idwt_npv() {
   return s;
 }
 constexpr int IDWT_SPAN = IDWT_TILE / 2 + 16;
-constexpr int IDWT_DALL = idwt_doff(DWT_MAX_LEVEL + 1);
 
 struct IdwtRanges {
   int64_t cl[DWT_MAX_LEVEL + 1], dl[DWT_MAX_LEVEL + 1];
@@ -691,7 +690,9 @@ __global__ void __launch_bounds__(256) idwt_kernel(const float* __restrict__ coe
                                                    int64_t ntiles) {
   __shared__ __attribute__((aligned(16))) float A[IDWT_SPAN];
   __shared__ __attribute__((aligned(16))) float B[IDWT_SPAN];
-  __shared__ __attribute__((aligned(16))) float D[IDWT_DALL];
+  // the detail segments of levels 1..LEV only: at LEV = 4 the block's LDS drops under 32 KB,
+  // five blocks per CU instead of four
+  __shared__ __attribute__((aligned(16))) float D[idwt_doff(LEV + 1)];
   int64_t tile = tile0 + blockIdx.x;
   if (tile >= ntiles) return;
   float pv[idwt_npv<LEV>()];
