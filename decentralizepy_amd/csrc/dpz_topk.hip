@@ -270,11 +270,17 @@ __global__ void __launch_bounds__(256) planes_add_kernel(uint32_t* planes,
   if (guard && *guard) return;
   for (int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x; w < nw; w += (int64_t)gridDim.x * 256) {
     uint32_t carry = mask[w];
-    for (int p = 0; p < 32 && carry != 0u; ++p) {
-      uint32_t* const a = planes + (int64_t)p * nw + w;
-      const uint32_t old = *a;
-      *a = old ^ carry;
-      carry &= old;
+    for (int p = 0; p < 32 && carry != 0u; p += 4) {  // four planes' words read together
+      uint32_t o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = planes[(int64_t)(p + q) * nw + w];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (carry != 0u) {
+          planes[(int64_t)(p + q) * nw + w] = o[q] ^ carry;
+          carry &= o[q];
+        }
+      }
     }
   }
 }

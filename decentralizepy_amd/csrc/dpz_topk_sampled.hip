@@ -1024,6 +1024,12 @@ struct CompactCfg {
   static constexpr int PFC = SPW >= 8 ? 1 : 4;  // chunks of 64 per segment held in registers
 };
 
+#ifndef DPZ_SL_PF  // planes read ahead per ripple-carry step (a divisor of 32)
+#define DPZ_SL_PF 4
+#endif
+constexpr int SL_PF = DPZ_SL_PF;
+static_assert(32 % SL_PF == 0, "the planes are read in whole steps");
+
 // SL (dpz_topk_encode_sliced): no scattered counter / rewind; each wave ORs its segment's
 // selected bits into an LDS row (R <= SL_RMAX, R a multiple of 32: the segment owns whole
 // words), then writes every word of the row to selmask and adds it to the bit-sliced counter
@@ -1323,11 +1329,20 @@ __global__ void __launch_bounds__(256, SPW >= 8 ? 1 : 4) sampled_compact_kernel(
         const int64_t w = (segbeg >> 5) + j;
         selmask[w] = m;
         uint32_t carry = planes ? m : 0u;
-        for (int p = 0; p < 32 && carry != 0u; ++p) {
-          uint32_t* const a = planes + (int64_t)p * nwords + w;
-          const uint32_t old = *a;
-          *a = old ^ carry;
-          carry &= old;
+        // the ripple carry through the planes, SL_PF planes' words loaded together per step:
+        // a wave's longest carry chain (~6-7 planes at 64 lanes) costs ceil(chain / SL_PF)
+        // dependent round trips instead of one per plane
+        for (int p = 0; p < 32 && carry != 0u; p += SL_PF) {
+          uint32_t o[SL_PF];
+#pragma unroll
+          for (int q = 0; q < SL_PF; ++q) o[q] = planes[(int64_t)(p + q) * nwords + w];
+#pragma unroll
+          for (int q = 0; q < SL_PF; ++q) {
+            if (carry != 0u) {
+              planes[(int64_t)(p + q) * nwords + w] = o[q] ^ carry;
+              carry &= o[q];
+            }
+          }
         }
       }
       __builtin_amdgcn_wave_barrier();  // the row is cleared for the next segment after this
