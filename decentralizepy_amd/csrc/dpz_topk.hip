@@ -253,12 +253,17 @@ static unsigned grid_of(int64_t items, int64_t cap = 8192) {
 }
 
 // bit idx of mask for every selected index (the exact path / a sampled miss: the sorted indices
-// are unique, the atomics go to distinct bits)
+// are unique, the atomics go to distinct bits).  guard: the sampled run's status word — after a
+// miss compact wrote nothing and idx holds whatever the buffer held before, so nothing is read;
+// an index outside [0, n) is never followed either
 __global__ void __launch_bounds__(256) selmask_from_idx_kernel(const int32_t* __restrict__ idx,
-                                                               int64_t k, uint32_t* mask) {
+                                                               int64_t k, int64_t n,
+                                                               uint32_t* mask,
+                                                               const uint32_t* guard) {
+  if (guard && *guard) return;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < k; i += (int64_t)gridDim.x * 256) {
     const uint32_t v = (uint32_t)idx[i];
-    atomicOr(&mask[v >> 5], 1u << (v & 31));
+    if ((int64_t)v < n) atomicOr(&mask[v >> 5], 1u << (v & 31));
   }
 }
 
@@ -333,7 +338,8 @@ int sliced_from_idx(const EncodeArgs& a, const uint32_t* guard) {
   DPZ_HIP_TRY(hipMemsetAsync(a.selmask, 0, (size_t)nw * 4, a.st));
   if (a.k > 0)
     DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st,
-              selmask_from_idx_kernel<<<grid_of(a.k), 256, 0, a.st>>>(a.idx_out, a.k, a.selmask));
+              selmask_from_idx_kernel<<<grid_of(a.k), 256, 0, a.st>>>(a.idx_out, a.k, a.n,
+                                                                      a.selmask, guard));
   if (a.planes && a.k > 0)
     DPZ_TIMED(DPZ_KT_TOPK_COMPACT, a.st,
               planes_add_kernel<<<grid_of(nw), 256, 0, a.st>>>(a.planes, a.selmask, nw, guard));
