@@ -32,7 +32,7 @@ def _counter0(rng, n):
     return c
 
 
-def _run(dev, x, x0, acc, mode, k, vals=None, status=False, exact=False, seed=0):
+def _run(dev, x, x0, acc, mode, k, vals=None, status=False, exact=False, seed=0, poison=False):
     from decentralizepy_amd import codec
     n = x.size
     rng = np.random.default_rng(seed)
@@ -47,8 +47,12 @@ def _run(dev, x, x0, acc, mode, k, vals=None, status=False, exact=False, seed=0)
     mask = torch.full((nw,), -0x54545455, dtype=torch.int32, device=dev)  # garbage: overwritten
     ws = codec.Workspace(dev)
     st = torch.full((1,), 7, dtype=torch.int32, device=dev) if status else None
+    # poison: idx_out starts with indices far outside [0, n) (what a reused buffer may hold when a
+    # sampled miss leaves it unwritten)
+    io = torch.full((k,), 0x7FFFFFF0, dtype=torch.int32, device=dev) if poison else None
     idx, val = codec.topk_encode_sliced(tx, k, mask, planes, x0=tx0, acc=tacc, acc_mode=mode,
-                                        vals_src=tv, workspace=ws, status_out=st, exact=exact)
+                                        vals_src=tv, idx_out=io, workspace=ws, status_out=st,
+                                        exact=exact)
     if status:
         torch.cuda.synchronize()
         if int(st.item()) != 0:  # a sampled miss wrote nothing: the caller re-runs exactly
@@ -188,3 +192,5 @@ def test_sliced_long_segments_build_the_mask_after_compact(dev, diag_lib, monkey
     k = round(0.01 * n)
     x, x0 = miss_layout(n, k)
     _run(dev, x, x0, None, otopk.ACC_NONE, k, status=status)
+    # the mask build after compact must not follow the stale indices of a missed sampled run
+    _run(dev, x, x0, None, otopk.ACC_NONE, k, status=status, poison=True)
