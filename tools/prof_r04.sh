@@ -5,6 +5,7 @@
 #   clean: the diagnostic build (libdpzcodec_diag.so) with DPZ_BATCH_COSCHED=0 — plain encode +
 #          standalone replace decode, so every kernel's trace and PMC rows are its own
 #   c3   : bench --workload c3 (JWINS 25M) on the product library
+#   mib64: the prod step at the north-star 64 MiB tensor (MODES=mib64)
 # rocprofv3 --kernel-trace --stats, then separate --pmc FETCH_SIZE / WRITE_SIZE passes; per-launch
 # traffic JSON by tools/pmc2json.py.  Outputs under gpurun_out/prof_r04_<mode>*.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -17,6 +18,7 @@ for mode in ${MODES:-prod clean c3}; do
     export DPZ_BATCH_COSCHED=0 DPZ_CODEC_LIB=$PWD/decentralizepy_amd/libdpzcodec_diag.so
   fi
   if [ "$mode" = c3 ]; then CMD="python3 bench.py --workload c3 --steps 20"; fi
+  if [ "$mode" = mib64 ]; then CMD="python3 bench.py --n 16777216 --steps ${STEPS:-100} --warmup 10 --no-cpu --no-extra --streams 1"; fi
   N=prof_r04_$mode
   rm -rf gpurun_out/$N gpurun_out/${N}_fetch gpurun_out/${N}_write
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$N -o run -- $CMD > gpurun_out/$N.log 2>&1 || { echo "$mode trace rc=$?"; tail -5 gpurun_out/$N.log; exit 1; }
