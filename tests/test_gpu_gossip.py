@@ -56,7 +56,7 @@ def test_reduce_scatter_exchange_device_within_tolerance(dev, path, n, alpha, bu
         np.testing.assert_array_equal(rs.counter.cpu().numpy(), exact.counter.cpu().numpy())
 
 
-@pytest.mark.parametrize("wavelet", ["sym2", "haar"])
+@pytest.mark.parametrize("wavelet", ["sym2", "haar", "db4"])
 def test_jwins_round_device_matches_oracle(dev, wavelet):
     """C3 shape (b): the JWINS round of tutorial/JWINS/regular_16.txt with the tutorial alpha
     list (uid-seeded draws, full shares included) — DWT pair, ADD-accumulation top-k, batched
