@@ -6,7 +6,9 @@ compaction with counter update) of an N-element fp32 tensor already resident in 
 matching decode (replace the k payload values into a copy of the local model), exactly the
 reference's PartialModel.serialized_model + deserialized_model pair.
 
-Workload (BASELINE.json configs[1]): N = 11,000,000 (ResNet-18-sized), alpha = 0.01 -> k = 110,000.
+Workload (BASELINE.json north_star): the 64 MiB fp32 tensor, N = 16,777,216, alpha = 0.01 ->
+k = 167,772 — the configuration the north-star target (>= 50 % of HBM peak) is quoted on.  The
+C2 tensor (configs[1], N = 11,000,000, ResNet-18-sized) runs beside it as the `secondary` object.
 Multi-GPU (torchrun): each rank encodes+decodes its own node's tensor (the gossip round is a set
 of independent per-node codecs: no data-path collective) -> weak scaling; value = all ranks'
 params / max-over-ranks time.  Beside it, every run times one C4 gossip round of the 96-node
@@ -27,6 +29,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (GB/s), /opt/skills/guides/MI355X_MICROARCH.md
+NORTH_STAR_N = 16_777_216  # 64 MiB of fp32: BASELINE.json north_star's target tensor
+C2_N = 11_000_000          # BASELINE.json configs[1] (ResNet-18-sized)
+
+
+def workload_name(n):
+    if n == NORTH_STAR_N:
+        return ("north-star: PartialModel top-k encode + decode of one 64 MiB fp32 tensor "
+                "(N=16,777,216), 1% top-k")
+    if n == C2_N:
+        return "C2: PartialModel top-k encode + decode of one 11M-fp32 flattened tensor"
+    return f"PartialModel top-k encode + decode of one {n}-element fp32 tensor"
 
 
 def parse():
@@ -35,12 +48,14 @@ def parse():
                    help="ranks (one per GPU); default: WORLD_SIZE under a launcher, else 1")
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--n", type=int, default=11_000_000)
+    p.add_argument("--n", type=int, default=None,
+                   help="tensor size (default: the 64 MiB north-star tensor; C4: C2's 11M)")
     p.add_argument("--alpha", type=float, default=0.01)
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-extra", action="store_true",
-                   help="skip the 64 MiB secondary line and the C4 gossip-round object")
+                   help="skip the secondary line (C2, or 64 MiB when --n is not 64 MiB) and "
+                        "the C4 gossip-round / shard objects")
     p.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "e2e", "shard", "fft", "wire",
                                           "plugin"],
                    default="c2",
@@ -408,19 +423,19 @@ def kernel_alg_bytes(name, n, k):
 
 
 def load_pmc(kernel, n):
-    """HBM traffic per launch of `kernel` from the committed rocprofv3 PMC summary, if it was
-    collected at this tensor size (its "n"); None otherwise."""
-    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        pmc = json.load(f)
-    if pmc.get("n") != n:
-        return None
-    ent = pmc.get("kernels", {}).get(kernel)
-    if not ent:
-        return None
-    return ent.get("hbm_bytes_per_launch")
+    """HBM traffic per launch of `kernel` from the committed rocprofv3 PMC summaries
+    (profiles/pmc_latest*.json), the one collected at this tensor size (its "n"); None if none
+    was."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_latest*.json"))):
+        with open(path) as f:
+            pmc = json.load(f)
+        if pmc.get("n") != n:
+            continue
+        ent = pmc.get("kernels", {}).get(kernel)
+        if ent:
+            return ent.get("hbm_bytes_per_launch")
+    return None
 
 
 def _cpu_steps(n, alpha, seconds, threads):
@@ -447,27 +462,38 @@ def _cpu_steps(n, alpha, seconds, threads):
 
 
 def cpu_baseline(n, alpha, seconds):
-    """The reference's CPU op sequence on this box's host cores: at the process's
-    thread budget (OMP_NUM_THREADS / torch's default: the cores this job may use), and at the
+    """The reference's CPU op sequence on this box's host cores, on the same
+    tensor as the headline: at the process's thread budget (torch's intra-op threads =
+    OMP_NUM_THREADS, the cores this job may use; `value`), at every CPU in the process's
+    affinity mask (`full_affinity`: the host's best figure, stated beside it), and at the
     per-node share floor(cores / 16) a 16-node machine gives each node process
     (node/DPSGDNode.py:434-439 sets floor(cores / procs_per_machine))."""
     cores = torch.get_num_threads()
     t, times = _cpu_steps(n, alpha, seconds, cores)
-    share = max(1, cores // 16)
-    t1, times1 = _cpu_steps(n, alpha, max(3.0, seconds / 2), share)
     try:
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        affinity = None
+        affinity = os.cpu_count()
+    full = None
+    if affinity and affinity > cores:
+        tf, times_f = _cpu_steps(n, alpha, max(3.0, seconds / 3), affinity)
+        full = {"threads": affinity, "value": round(4 * n / tf / 2 ** 30, 4), "unit": "GiB/s",
+                "steps": len(times_f),
+                "note": "every CPU in the affinity mask (torch.set_num_threads); on a shared "
+                        "host these cores also serve other jobs"}
+    share = max(1, cores // 16)
+    t1, times1 = _cpu_steps(n, alpha, max(3.0, seconds / 3), share)
     return dict(value=4 * n / t / 2 ** 30, unit="GiB/s", cores=cores,
                 host_cpu_count=os.cpu_count(), affinity_cpus=affinity,
                 cores_note=(f"{cores} threads used (torch intra-op threads = this job's CPU "
                             f"share); the host reports {os.cpu_count()} logical CPUs, "
-                            f"{affinity} in this process's affinity mask"),
+                            f"{affinity} in this process's affinity mask (timed in "
+                            f"full_affinity)"),
                 kind="port",
                 sample=f"reference ATen-CPU op sequence (oracle/ref_ops.py), N={n}, k={round(alpha*n)}, "
                        f"median of {len(times)} encode+decode steps ({sum(times):.1f} s) at "
                        f"{cores} threads (torch.get_num_threads(), the job's CPU share)",
+                full_affinity=full,
                 per_node_share={"threads": share, "value": round(4 * n / t1 / 2 ** 30, 4),
                                 "unit": "GiB/s", "steps": len(times1),
                                 "note": "floor(cores / 16): one of 16 node processes per machine"})
@@ -481,6 +507,8 @@ def _finish(dist):
 
 def main():
     args = parse()
+    if args.n is None:
+        args.n = C2_N if args.workload == "c4" else NORTH_STAR_N
     launched = "WORLD_SIZE" in os.environ
     if args.gpus is None:  # under torchrun without --gpus: the launcher's rank count
         args.gpus = int(os.environ["WORLD_SIZE"]) if launched else 1
@@ -573,41 +601,37 @@ def main():
                  rotate=args.rotate, streams=args.streams, repeats=repeats)
     extra = None
     if not args.no_extra:
-        # the north-star tensor, every rank its own node's 64 MiB model (weak, like the headline)
-        e = gpu_case(16_777_216, 0.01, dev, 99 + rank, max(20, args.steps // 2), args.warmup,
+        # the other single-GPU size beside the headline (C2 when the headline is the 64 MiB
+        # north-star tensor), every rank its own node's model (weak, like the headline)
+        n2 = C2_N if args.n != C2_N else NORTH_STAR_N
+        e = gpu_case(n2, 0.01, dev, 99 + rank, max(20, args.steps // 2), args.warmup,
                      world, dist, streams=args.streams, repeats=repeats)
-        b = (e["b_enc"] + e["b_dec"]) * world
-        extra = {"workload": "north-star target: 64 MiB fp32 tensor (N=16,777,216), 1% top-k, "
-                             "one per GPU",
-                 "value": round(e["value"], 2), "ms_per_step": round(e["s_step"] * 1e3, 4),
-                 "frac_of_hbm_peak": round(b / e["s_step"] / 1e9 / HBM_PEAK_GBS / world, 4),
-                 "launch": e["mode"],
-                 "one_node_serial_ms_per_step": round(e["s_serial"] * 1e3, 4),
-                 "one_node_frac_of_hbm_peak": round(b / e["s_serial"] / 1e9 / HBM_PEAK_GBS / world, 4),
-                 f"{e['streams']}_node_ms_per_step": round(e["s_multi"] * 1e3, 4),
-                 "host_enqueue_ms_per_step": round(e["s_host"] * 1e3, 4),
-                 "product_one_node": {k_: v for k_, v in e["product"].items() if k_ != "fell_back"},
-                 "spread_ms": e["spread_ms"],
-                 "fell_back": e["fell_back"]}
+        extra = None
+        if rank == 0:
+            b = (e["b_enc"] + e["b_dec"]) * world
+            kern2, dk2, _ = kernel_table(e)
+            extra = {"workload": workload_name(n2) + ", one per GPU",
+                     "n": e["n"], "k": e["k"],
+                     "value": round(e["value"], 2), "ms_per_step": round(e["s_step"] * 1e3, 4),
+                     "frac_of_hbm_peak": round(b / e["s_step"] / 1e9 / HBM_PEAK_GBS / world, 4),
+                     "launch": e["mode"],
+                     "one_node_serial_ms_per_step": round(e["s_serial"] * 1e3, 4),
+                     "one_node_frac_of_hbm_peak": round(b / e["s_serial"] / 1e9 / HBM_PEAK_GBS / world, 4),
+                     f"{e['streams']}_node_ms_per_step": round(e["s_multi"] * 1e3, 4),
+                     "host_enqueue_ms_per_step": round(e["s_host"] * 1e3, 4),
+                     "roofline": roofline_obj(dk2, e["n"]),
+                     "product_one_node": {k_: v for k_, v in e["product"].items() if k_ != "fell_back"},
+                     "kernels": kern2,
+                     "spread_ms": e["spread_ms"],
+                     "fell_back": e["fell_back"]}
 
     # the gossip round of BASELINE.json C4 (eval/96_regular.edges) at every N: the nodes are
     # sharded over the ranks and each round's payloads cross ranks in one RCCL all-gather, so a
     # multi-GPU run of this bench also times the collective path (strong scaling, 96 nodes fixed)
     gossip = shard_line = None
     if not args.no_extra:
-        gr = gossip_case(args.n, args.alpha, dev, rank, world, dist, rounds=5, warmup=2)
-        gossip = {"workload": "C4: one gossip round of eval/96_regular.edges (96 nodes, 190 "
-                              "edges): every node top-k encodes, payloads all-gathered over RCCL, "
-                              "every node MH-folds its neighbours' payloads",
-                  "value": round(gr["value"], 3), "unit": "GiB/s",
-                  "ms_per_round": round(gr["s_step"] * 1e3, 4), "scaling": "strong",
-                  "parallelism": f"{gr['nodes']} nodes sharded over {world} GPU(s), "
-                                 + ("one RCCL all-gather of the payloads per round" if world > 1
-                                    else "no collective on one GPU"),
-                  "legs_ms": gr["legs_ms"],
-                  "round_alg_bytes": gr["alg_bytes"],
-                  "round_frac_of_hbm_peak": round(gr["alg_bytes"] / gr["s_step"] / 1e9
-                                                  / HBM_PEAK_GBS / world, 4)}
+        gossip = gossip_line(gossip_case(C2_N, 0.01, dev, rank, world, dist, rounds=5, warmup=2),
+                             world)
         torch.cuda.empty_cache()
         # one C5 tensor (256 MiB, alpha 0.001) sharded over the ranks: the sharded top-k's
         # candidate all-gather is the collective (strong scaling)
@@ -644,33 +668,8 @@ def main():
         dec_gbs = r["b_dec"] / t_dec / 1e9
         enc_gbs = r["b_enc"] / t_enc / 1e9
         step_gbs = (r["b_enc"] + r["b_dec"]) / r["s_step"] / 1e9
-        kern = r["kernels"]
-        # a per-launch HIP event pair adds its own overhead to every launch's average; measured
-        # on the replace decode (the one kernel also timed back to back: event-pair average -
-        # back-to-back average) and subtracted from every kernel's event-pair average, so the
-        # averages are what rocprofv3 --kernel-trace reports (profiles/)
-        bias = 0.0
-        if "fold" in kern:
-            bias = max(0.0, kern["fold"]["avg_us"] - t_dec * 1e6)
-        for name, kv in kern.items():
-            b = kernel_alg_bytes(name, r["n"], r["k"])
-            kv["avg_us_event_pair"] = round(kv["avg_us"], 3)
-            kv["avg_us"] = max(kv["avg_us"] - bias, 1e-3)
-            kv["alg_bytes"] = b
-            kv["GBps"] = round(b / (kv["avg_us"] * 1e-6) / 1e9, 1) if b else 0.0
-            kv["avg_us"] = round(kv["avg_us"], 3)
-        dom = max(kern, key=lambda nm: kern[nm]["avg_us"] * kern[nm]["launches_per_step"])
-        dk = dict(kern[dom])
-        dk["timing"] = (f"per-launch HIP event pair (library KernelTimer) minus the event-pair "
-                        f"overhead {bias:.3f} us (replace kernel: event-pair avg - back-to-back avg)")
-        if dom == "fold" and kern[dom]["launches_per_step"] == 1.0:
-            # the decode is this one launch: its back-to-back average on the launch stream
-            # (HIP events around the whole loop) has no per-launch event overhead and is what
-            # rocprofv3 --kernel-trace reports for the kernel
-            dk["avg_us"] = round(t_dec * 1e6, 3)
-            dk["GBps"] = round(dk["alg_bytes"] / t_dec / 1e9, 1)
-            dk["timing"] = "back-to-back launches, HIP events around the loop on the launch stream"
-        traffic = load_pmc(dom, args.n)
+        serial_b = r["b_enc"] + r["b_dec"]
+        kern, dk, _ = kernel_table(r)
         line = {
             "metric": "GiB/s fp32 params encoded+decoded (device-resident), 1% top-k",
             "value": round(r["value"], 3),
@@ -685,7 +684,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic (x ~ N(0,1), x0 = x - 0.01*N(0,1), device-generated)",
             "config": {
-                "workload": "C2: PartialModel top-k encode + decode of one 11M-fp32 flattened tensor",
+                "workload": workload_name(r["n"]),
                 "n": r["n"], "k": r["k"], "alpha": args.alpha,
                 "parallelism": (f"{world} GPU(s) x {r['streams']} concurrent node codecs (one "
                                 f"stream each), no collective" if r["mode"] == "multi" else
@@ -703,18 +702,7 @@ def main():
                            f"steps (each: barrier + synchronize on both sides, max over ranks)"),
             },
             "spread_ms_per_step": r["spread_ms"],
-            "roofline": {
-                "bound": "hbm",
-                "kernel": dom,
-                "achieved": dk["GBps"],
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(dk["GBps"] / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "alg_bytes_per_launch": dk["alg_bytes"],
-                "avg_launch_us": dk["avg_us"],
-                "timing": dk["timing"],
-            },
+            "roofline": roofline_obj(dk, r["n"]),
             "stages": {
                 "encode": {"avg_us": round(t_enc * 1e6, 3), "alg_bytes": r["b_enc"],
                            "GBps": round(enc_gbs, 1), "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
@@ -723,6 +711,7 @@ def main():
                            "GBps": round(dec_gbs, 1), "frac": round(dec_gbs / HBM_PEAK_GBS, 4)},
                 "step_frac_of_hbm_peak": round(step_gbs / HBM_PEAK_GBS, 4),
                 "one_node_serial_ms_per_step": round(r["s_serial"] * 1e3, 5),
+                "one_node_frac_of_hbm_peak": round(serial_b / r["s_serial"] / 1e9 / HBM_PEAK_GBS, 4),
                 f"{r['streams']}_node_ms_per_step": round(r["s_multi"] * 1e3, 5),
                 "host_enqueue_ms_per_step": round(r["s_host"] * 1e3, 5),
                 "product_one_node": {k_: v for k_, v in r["product"].items() if k_ != "fell_back"},
@@ -737,6 +726,70 @@ def main():
         print(json.dumps(line), flush=True)
     _finish(dist)
 
+
+def kernel_table(r):
+    """Per-kernel averages of the one-node step with the per-launch HIP event-pair overhead
+    removed, and the dominant kernel (most device time per step).  The overhead is measured on
+    the replace decode (the one kernel also timed back to back: event-pair average -
+    back-to-back average) and subtracted from every kernel's event-pair average, so the
+    averages are what rocprofv3 --kernel-trace reports (profiles/)."""
+    kern = {nm: dict(v) for nm, v in r["kernels"].items()}
+    t_dec = r["t_dec"]
+    bias = 0.0
+    if "fold" in kern:
+        bias = max(0.0, kern["fold"]["avg_us"] - t_dec * 1e6)
+    for name, kv in kern.items():
+        b = kernel_alg_bytes(name, r["n"], r["k"])
+        kv["avg_us_event_pair"] = round(kv["avg_us"], 3)
+        kv["avg_us"] = max(kv["avg_us"] - bias, 1e-3)
+        kv["alg_bytes"] = b
+        kv["GBps"] = round(b / (kv["avg_us"] * 1e-6) / 1e9, 1) if b else 0.0
+        kv["avg_us"] = round(kv["avg_us"], 3)
+    dom = max(kern, key=lambda nm: kern[nm]["avg_us"] * kern[nm]["launches_per_step"])
+    dk = dict(kern[dom])
+    dk["name"] = dom
+    dk["timing"] = (f"per-launch HIP event pair (library KernelTimer) minus the event-pair "
+                    f"overhead {bias:.3f} us (replace kernel: event-pair avg - back-to-back avg)")
+    if dom == "fold" and kern[dom]["launches_per_step"] == 1.0:
+        # the decode is this one launch: its back-to-back average on the launch stream (HIP
+        # events around the whole loop) has no per-launch event overhead
+        dk["avg_us"] = round(t_dec * 1e6, 3)
+        dk["GBps"] = round(dk["alg_bytes"] / t_dec / 1e9, 1)
+        dk["timing"] = "back-to-back launches, HIP events around the loop on the launch stream"
+    return kern, dk, bias
+
+
+def roofline_obj(dk, n):
+    """The line's `roofline` object for the dominant kernel `dk` (kernel_table) at size n, with
+    the HBM traffic of the committed PMC pass at the same n (profiles/pmc_latest*.json)."""
+    return {
+        "bound": "hbm",
+        "kernel": dk["name"],
+        "achieved": dk["GBps"],
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(dk["GBps"] / HBM_PEAK_GBS, 4),
+        "traffic": load_pmc(dk["name"], n),
+        "alg_bytes_per_launch": dk["alg_bytes"],
+        "avg_launch_us": dk["avg_us"],
+        "timing": dk["timing"],
+    }
+
+
+def gossip_line(gr, world):
+    return {"workload": "C4: one gossip round of eval/96_regular.edges (96 nodes, 190 "
+                        "edges): every node top-k encodes, payloads all-gathered over RCCL, "
+                        "every node MH-folds its neighbours' payloads",
+            "n": gr["n"], "k": gr["k"],
+            "value": round(gr["value"], 3), "unit": "GiB/s",
+            "ms_per_round": round(gr["s_step"] * 1e3, 4), "scaling": "strong",
+            "parallelism": f"{gr['nodes']} nodes sharded over {world} GPU(s), "
+                           + ("one RCCL all-gather of the payloads per round" if world > 1
+                              else "no collective on one GPU"),
+            "legs_ms": gr["legs_ms"],
+            "round_alg_bytes": gr["alg_bytes"],
+            "round_frac_of_hbm_peak": round(gr["alg_bytes"] / gr["s_step"] / 1e9
+                                            / HBM_PEAK_GBS / world, 4)}
 
 if __name__ == "__main__":
     main()

@@ -274,6 +274,38 @@ class DeviceAccumulator:
     def __getitem__(self, item):
         return self.settle()[item]
 
+    def __setitem__(self, item, value):
+        """Reference-style writes (models/Model.py:53-64 ``accumulated_changes[indices] = 0``):
+        settle the pending rewind, then assign on the device tensor (host index arrays and
+        values are moved to its device)."""
+        t = self.settle()
+        if isinstance(item, (np.ndarray, list)):
+            item = torch.as_tensor(np.asarray(item), device=t.device)
+        elif isinstance(item, torch.Tensor):
+            item = item.to(t.device)
+        if isinstance(value, (np.ndarray, torch.Tensor)):
+            value = torch.as_tensor(value).to(t.device)
+        t[item] = value
+
+    def __iadd__(self, other):
+        """``acc += change`` (PartialModel.py:346-349): settle, then add in place."""
+        if isinstance(other, DeviceAccumulator):
+            other = other.settle()
+        self.settle().add_(torch.as_tensor(other).to(self.device_tensor.device))
+        return self
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        """Any torch function handed the wrapper (``torch.zeros_like(acc)``, ``acc + t``,
+        ``torch.cat([acc, ...])``) sees the settled device tensor."""
+        def unwrap(a):
+            if isinstance(a, DeviceAccumulator):
+                return a.settle()
+            if isinstance(a, (list, tuple)):
+                return type(a)(unwrap(v) for v in a)
+            return a
+        return func(*unwrap(tuple(args)), **{k: unwrap(v) for k, v in (kwargs or {}).items()})
+
     def __array__(self, dtype=None):
         a = self.numpy()
         return a if dtype is None else a.astype(dtype)

@@ -535,7 +535,9 @@ def wavedec_len(n, level=4, wavelet="sym2"):
     else:
         m = int(_lib.lib().dpz_wavedec_len_generic(int(n), int(level), filter_len(wavelet)))
     if m < 0:
-        raise ValueError(f"{wavelet} level-{level} wavedec unsupported for n={n}")
+        # a level whose input is shorter than the filter (pywt's multi-reflection branch) or a
+        # level past the kernels' 8: not implemented on the device (Wavelet's documented error)
+        raise NotImplementedError(f"{wavelet} level-{level} wavedec unsupported for n={n}")
     return m
 
 

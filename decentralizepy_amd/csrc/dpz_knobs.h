@@ -2,7 +2,7 @@
 //
 // The product library (libdpzcodec.so) compiles every switch to its measured default: no call
 // path reads the environment, so nothing in a node's environment can change which kernels run.
-// The diagnostic build (`make diag` -> libdpzcodec_diag.so, compiled with -DDPZ_DIAG) reads
+// The diagnostic build (`make diag-lib` or `make all` -> libdpzcodec_diag.so, compiled with -DDPZ_DIAG) reads
 // DPZ_<NAME> on every call instead: the A/B measurements under tools/diag and the forced-path GPU
 // tests (tests/conftest.py `diag_lib`) load it explicitly.
 #pragma once

@@ -115,11 +115,17 @@ def sharded_topk_encode(x, x0, k, offset, counter=None, group=None, ops=None, va
               else torch.zeros(1, dtype=torch.int32, device=idx.device))
         if coll:
             # one exchange: the candidate arrays and the status word, packed as bytes
-            # (index, change: 4 B; value: 4 or 2 B) in ONE all-gather
+            # (index, change: 4 B; value: 4 or 2 B) in ONE all-gather.  The value section is
+            # padded to a multiple of 4 bytes so every section of every row starts 4-byte
+            # aligned (odd k with fp16 values; the int32 / fp32 views below need it even when
+            # a one-rank gather hands back a view without a copy)
             vb = val.element_size()
-            row = 8 * k + vb * k + 4
-            pack = torch.cat([idx.view(torch.uint8), chg.view(torch.uint8), val.view(torch.uint8),
-                              st.view(torch.uint8)])
+            vpad = -(-vb * k // 4) * 4
+            row = 8 * k + vpad + 4
+            parts = [idx.view(torch.uint8), chg.view(torch.uint8), val.view(torch.uint8)]
+            if vpad != vb * k:
+                parts.append(torch.zeros(vpad - vb * k, dtype=torch.uint8, device=idx.device))
+            pack = torch.cat(parts + [st.view(torch.uint8)])
             gflat = torch.empty(world * row, dtype=torch.uint8, device=idx.device)
             dist.all_gather_into_tensor(gflat, pack, group=group)
             gpack = gflat.view(world, row)

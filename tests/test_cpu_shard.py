@@ -207,15 +207,15 @@ def test_wavelet_slices_partition_tiles_and_coefficients(n, world):
     assert (fwd == 1).all() and (inv == 1).all() and (cov == 1).all()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_topk_fp16_values(world):
+@pytest.mark.parametrize("world,k", [(2, 1_500), (3, 1_500), (2, 1_501)])
+def test_sharded_topk_fp16_values(world, k):
     """BASELINE config 5: fp16 values (RNE) packed by the local encodes travel through the one
     all-gather (10 bytes per candidate) and the merge: the whole-tensor payload with torch.half
-    values on every rank."""
-    n, k = 30_000, 1_500
+    values on every rank.  Odd k: the value section is padded to 4 bytes in the packed row."""
+    n = 30_000
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29690 + world
+    port = 29690 + world + (k % 2) * 5
     procs = [ctx.Process(target=_worker, args=(r, world, port, n, k, True, q, True))
              for r in range(world)]
     for p in procs:

@@ -75,3 +75,6 @@ def test_library_generic_lengths_and_workspace():
     assert L.dpz_wavedec_len_generic(1000, 2, 5) == -1     # odd filter length
     assert L.dpz_wavedec_len_generic(1000, 9, 4) == -1     # level past 8
     assert L.dpz_wavelet_generic_workspace_bytes(1000, 1, 8) == 0
+    from decentralizepy_amd import codec
+    with pytest.raises(NotImplementedError):  # the Wavelet plugin's documented error
+        codec.wavedec_len(62, 2, "dmey")

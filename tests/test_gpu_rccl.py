@@ -86,10 +86,13 @@ def test_jwins_round_through_rccl(dev, rccl_group):
     assert kinds == {True, False}  # partial and full shares both crossed the all-gather
 
 
-@pytest.mark.parametrize("val_fp16", [False, True])
-def test_sharded_topk_through_rccl(dev, rccl_group, val_fp16):
+@pytest.mark.parametrize("val_fp16,k", [(False, 20_000), (True, 20_000), (True, 20_001)])
+def test_sharded_topk_through_rccl(dev, rccl_group, val_fp16, k):
+    """k = 20,001 with fp16 values: an odd number of 2-byte values, so the packed row's status
+    word would sit 2 bytes off a 4-byte boundary without the value section's padding (the
+    one-rank gather hands back a view, no copy)."""
     from decentralizepy_amd.shard import sharded_topk_encode
-    n, k = 2_000_003, 20_000
+    n = 2_000_003
     g = torch.Generator(device=dev).manual_seed(5)
     x = torch.randn(n, device=dev, generator=g)
     x0 = x - 0.01 * torch.randn(n, device=dev, generator=g)

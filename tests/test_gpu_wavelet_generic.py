@@ -86,9 +86,17 @@ def test_generic_pair_and_accumulate_match_oracle(dev, name, n, level):
                                   _bits(owav.waverec_array(want_x, n, level, name)))
 
 
-def test_generic_rejects_short_levels(dev):
+def test_generic_rejects_short_levels(dev, tmp_path):
+    """A level whose input is shorter than the filter raises NotImplementedError, from the codec
+    and from the Wavelet plugin's constructor (its documented error)."""
     from decentralizepy_amd import codec
-    with pytest.raises(ValueError):
+    from decentralizepy_amd.sharing.JWINS.Wavelet import Wavelet
+    from tests import scenario
+    with pytest.raises(NotImplementedError):
         codec.wavedec_len(62, 2, "dmey")  # level-2 input of 61 values < 62 taps
+    model = scenario.make_model([4, 4, 2])  # 30 parameters: dmey's 62 taps at level 1 already
+    with pytest.raises(NotImplementedError):
+        Wavelet(0, 0, None, scenario._Mapping(), scenario._Graph([1]), model, None,
+                str(tmp_path), wavelet="dmey", level=2)
     with pytest.raises(NotImplementedError):
         codec.wavedec_len(100_000, 2, "db40")

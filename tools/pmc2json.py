@@ -3,10 +3,13 @@
 FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide
 coalesced reads (MI355X_MICROARCH.md § HBM), so traffic = 2 * FETCH_SIZE + WRITE_SIZE.
 Usage: pmc2json.py fetch.csv write.csv out.json ["source description"]
+The tensor size the pass ran at goes into the JSON's "n" when PMC_N is set (bench.py's
+load_pmc attaches the traffic to the line only at a matching n).
 """
 import collections
 import csv
 import json
+import os
 import sys
 
 NAMES = {"sampled_sample_kernel": "topk_sample", "sampled_filter_kernel": "topk_filter", "sampled_filter_pipe_kernel": "topk_filter",
@@ -18,8 +21,18 @@ NAMES = {"sampled_sample_kernel": "topk_sample", "sampled_filter_kernel": "topk_
          "idwt_kernel": "idwt"}
 
 
+# sampled_filter_pipe_kernel<SRC, CP, D, OCC>: CP = 1 writes the fused decode's copy of x (the
+# bench step, 12N bytes), 2 the fold base (12N), 0 neither (8N) — separate rows, since one average
+# over the variants would mix 8N and 12N launches
+FILTER_CP = {"0": "topk_filter_plain", "1": "topk_filter", "2": "topk_filter_foldbase"}
+
+
 def short(name):
-    base = name.split("(")[0].replace("void ", "").split("::")[-1].split("<")[0]
+    head = name.split("(")[0].replace("void ", "").split("::")[-1]
+    base = head.split("<")[0]
+    if base == "sampled_filter_pipe_kernel" and "<" in head:
+        cp = head.split("<")[1].split(",")[1].strip()
+        return FILTER_CP.get(cp, "topk_filter")
     return NAMES.get(base)
 
 
@@ -46,6 +59,8 @@ def main(fetch, write, out):
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
                      f"{src}; traffic = 2*FETCH_SIZE (gfx950 half-count correction) + WRITE_SIZE",
            "kernels": kernels}
+    if os.environ.get("PMC_N"):
+        doc["n"] = int(os.environ["PMC_N"])
     with open(out, "w") as fh:
         json.dump(doc, fh, indent=1)
     for k, v in kernels.items():

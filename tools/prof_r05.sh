@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-5 profiles, each pass its own run under its own time limit:
+#   mib64: the headline bench step (north-star 64 MiB tensor) on the product library, one stream
+#   c2   : the same step at C2's 11M tensor
+#   clean: the diagnostic build with DPZ_BATCH_COSCHED=0 at 64 MiB (standalone replace decode)
+#   c3   : bench --workload c3 (JWINS 25M)
+# rocprofv3 --kernel-trace --stats, then separate --pmc FETCH_SIZE / WRITE_SIZE passes; per-launch
+# traffic JSON by tools/pmc2json.py (with the pass's n).  Outputs under gpurun_out/*_r05_<mode>*.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for mode in ${MODES:-mib64 c2}; do
+  unset DPZ_BATCH_COSCHED DPZ_CODEC_LIB PMC_N
+  CMD="python3 bench.py --steps ${STEPS:-100} --warmup 10 --no-cpu --no-extra --streams 1"
+  export PMC_N=16777216
+  if [ "$mode" = c2 ]; then CMD="$CMD --n 11000000"; export PMC_N=11000000; fi
+  if [ "$mode" = clean ]; then
+    export DPZ_BATCH_COSCHED=0 DPZ_CODEC_LIB=$PWD/decentralizepy_amd/libdpzcodec_diag.so
+  fi
+  if [ "$mode" = c3 ]; then CMD="python3 bench.py --workload c3 --steps 20"; unset PMC_N; fi
+  N=prof_r05_$mode
+  rm -rf gpurun_out/$N gpurun_out/${N}_fetch gpurun_out/${N}_write
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$N -o run -- $CMD > gpurun_out/$N.log 2>&1 || { echo "$mode trace rc=$?"; tail -5 gpurun_out/$N.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${N}_fetch -o run -- $CMD > gpurun_out/${N}_fetch.log 2>&1 || { echo "$mode fetch rc=$?"; tail -5 gpurun_out/${N}_fetch.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${N}_write -o run -- $CMD > gpurun_out/${N}_write.log 2>&1 || { echo "$mode write rc=$?"; tail -5 gpurun_out/${N}_write.log; exit 1; }
+  F=$(find gpurun_out/${N}_fetch -name '*counter_collection.csv' | head -1)
+  W=$(find gpurun_out/${N}_write -name '*counter_collection.csv' | head -1)
+  python3 tools/pmc2json.py "$F" "$W" gpurun_out/pmc_r05_$mode.json "$mode: $CMD (DPZ_CODEC_LIB=${DPZ_CODEC_LIB:-product} DPZ_BATCH_COSCHED=${DPZ_BATCH_COSCHED:-default})"
+  S=$(find gpurun_out/$N -name '*kernel_stats.csv' | head -1)
+  cp "$S" gpurun_out/kstats_r05_$mode.csv
+  tail -1 gpurun_out/$N.log | cut -c1-600 > gpurun_out/bench_r05_$mode.json
+  rm -rf gpurun_out/$N gpurun_out/${N}_fetch gpurun_out/${N}_write
+  echo "prof $mode done"
+done
