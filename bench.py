@@ -259,14 +259,17 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
                 value=world * 4 * n / s_step / 2 ** 30)
 
 
-def product_one_node(sets, n, k, stream, ws, reps):
+def product_one_node(sets, n, k, stream, ws, reps, hint=True, keep_x=True):
     """``stages.product_one_node``: exactly what the drop-in plugins enqueue for one node's round,
     on one stream — PartialModel.serialized_model's ``codec.topk_encode`` (|x - x0| top-k with
     the counter update; sampled path, statuses checked after the loop) then Sharing._averaging's
     ``codec.decode_average`` (the Metro-Hastings fold of ``npay`` neighbour payloads over the
     node's pre-share model x into a new buffer, weights 1/(deg+1) of a degree-npay regular graph,
-    w_self = 1 - their Python sum), for npay = 1 and 3.  Step j rotates over the HBM-rotated node
-    states; its neighbours' payloads are those of states j-1 .. j-npay.  Device time: HIP events
+    w_self = 1 - their Python sum), for npay = 1 and 3.  The encode is PartialModel._encode's:
+    ``hint`` (the key window from the previous encode's exact threshold on the node's workspace,
+    no sample launch) and ``keep_x`` (x streamed with the default cache policy, the fold re-reads
+    it).  Step j rotates over the HBM-rotated node states; its neighbours' payloads are those of
+    states j-1 .. j-npay.  Device time: HIP events
     around the whole loop on the launch stream after a GPU-side spin that lets the host queue it.
     Algorithmic bytes: encode 8N + 16k, fold 8N + 8·npay·k (reference Sharing.py:156-190,
     PartialModel.py:188-255)."""
@@ -287,7 +290,8 @@ def product_one_node(sets, n, k, stream, ws, reps):
             d = sets[j % R]
             codec.topk_encode(d["x"], k, x0=d["x0"], counter=d["counter"], idx_out=d["idx"],
                               val_out=d["val"], workspace=ws, asynchronous=True,
-                              fold_base=(d["out"], w, 1 - w_total) if fused else None)
+                              fold_base=(d["out"], w, 1 - w_total) if fused else None,
+                              hint=hint, keep_x=keep_x)
 
         def dec(j):
             d = sets[j % R]
@@ -325,8 +329,12 @@ def product_one_node(sets, n, k, stream, ws, reps):
             "alg_bytes": b_enc + b_dec,
             "GiBps": round(4 * n / t_step / 2 ** 30, 2),
             "frac_of_hbm_peak": round((b_enc + b_dec) / t_step / 1e9 / HBM_PEAK_GBS, 4)}
+    out["encode_flags"] = {"hint": hint, "keep_x": keep_x}
     out["note"] = ("the plugin path: codec.topk_encode then codec.decode_average (MH fold over x "
-                   "into a new buffer), one stream; *_foldbase: the encode's filter also writes "
+                   "into a new buffer), one stream; the encode as PartialModel issues it (hint: "
+                   "key window from the previous round's exact threshold, no sample launch; "
+                   "keep_x: x streamed with the default cache policy for the fold's re-read); "
+                   "*_foldbase: the encode's filter also writes "
                    "the fold's no-hit base (topk_encode fold_base=, dpz_topk_encode_foldbase) and "
                    "the decode rewrites only the hit elements (base_ready=, DPZ_FOLD_BASE_READY), "
                    "what PartialModel runs when its predicted MH weights hold")
@@ -349,28 +357,37 @@ def _stage_time(batch, what, reps, run_steps, stream):
     return ev0.elapsed_time(ev1) / reps * 1e-3
 
 
-def gossip_case(n, alpha, dev, rank, world, dist, rounds, warmup, exchange="allgather"):
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def gossip_case(n, alpha, dev, rank, world, dist, rounds, warmup, exchange="allgather",
+                engine_kw=None):
     """C4: one synchronous gossip round of the 96-node regular topology (reference
     eval/96_regular.edges, copied as data under tests/golden/), nodes sharded over the ranks,
     payloads exchanged by one RCCL all-gather (decentralizepy_amd/gossip.py).  A "training"
-    perturbation between rounds is excluded from the timed region."""
+    perturbation between rounds is excluded from the timed region.  ``engine_kw``: the engine's
+    injectable steps (encode / fold / partial / combine; tests/test_cpu_bench_collectives.py runs
+    this function on gloo ranks with the oracle standing in for the HIP codec)."""
     from decentralizepy_amd.gossip import GossipRound, read_edges, shard
     adj = read_edges(os.path.join(ROOT, "tests", "golden", "96_regular.edges"))
     lo, hi, _ = shard(len(adj), world, rank)
     g = torch.Generator(device=dev).manual_seed(77 + rank)
     x = torch.randn(hi - lo, n, device=dev, generator=g)
-    eng = GossipRound(adj, x, alpha, rank=rank, world=world, device=dev, exchange=exchange)
+    eng = GossipRound(adj, x, alpha, rank=rank, world=world, device=dev, exchange=exchange,
+                      **(engine_kw or {}))
     del x
     noise = 0.01 * torch.randn(hi - lo, n, device=dev, generator=g)
     total = 0.0
     for r in range(warmup + rounds):
         eng.x += noise
-        torch.cuda.synchronize()
+        _sync(dev)
         if dist is not None:
             dist.barrier()
         t0 = time.perf_counter()
         eng.step()
-        torch.cuda.synchronize()
+        _sync(dev)
         if dist is not None:
             dist.barrier()
         dt = time.perf_counter() - t0
@@ -540,6 +557,17 @@ def main():
         r = gossip_case(args.n, args.alpha, dev, rank, world, dist, rounds, warm)
         rs = gossip_case(args.n, args.alpha, dev, rank, world, dist, max(3, rounds // 2), warm,
                          exchange="reduce_scatter")
+        cpu = None
+        if rank == 0 and not args.no_cpu:
+            # one node's round of the 96 (encode + the MH fold of its neighbours' payloads;
+            # eval/96_regular.edges' degree ~4), x96 nodes
+            import bench_workloads as bw
+            torch.cuda.empty_cache()
+            deg = round(2 * r["edges"] / r["nodes"])
+            cpu = bw.cpu_partial_round(args.n, args.alpha, deg, 5, scale=r["nodes"], seconds=8.0,
+                                       what=f"one of the {r['nodes']} nodes (degree {deg})")
+            cpu["value"] = round(r["nodes"] * 4 * args.n / cpu["seconds_per_unit"] / 2 ** 30, 5)
+            cpu["unit_note"] = "seconds_per_unit = one round of all 96 nodes"
         if rank == 0:
             print(json.dumps({
                 "metric": "GiB/s fp32 params encoded+decoded (device-resident), 1% top-k",
@@ -566,31 +594,34 @@ def main():
                     "ms_per_round": round(rs["s_step"] * 1e3, 4),
                     "value": round(rs["value"], 3), "legs_ms": rs["legs_ms"],
                     "rs_group": rs["rs_group"]},
+                "cpu_baseline": cpu,
             }), flush=True)
         _finish(dist)
         return
     if args.workload in ("c3", "c5", "e2e", "shard", "fft", "wire", "plugin"):
         import bench_workloads as bw
+        cpu = not args.no_cpu
         if args.workload == "plugin":
-            r = [bw.plugin_case(dev, "partial", cpu_rounds=0 if args.no_cpu else 1),
-                 bw.plugin_case(dev, "jwins")]
+            r = [bw.plugin_case(dev, "partial", cpu_rounds=int(cpu)),
+                 bw.plugin_case(dev, "jwins", cpu_rounds=int(cpu))]
         elif args.workload == "fft":
-            r = bw.fft_case(dev, steps=min(args.steps, 30))
+            r = bw.fft_case(dev, steps=min(args.steps, 30), cpu=cpu)
         elif args.workload == "wire":
             r = bw.wire_case(dev)
         elif args.workload == "shard":
-            r = bw.shard_case(dev, rank, world, dist, steps=min(args.steps, 40))
+            r = bw.shard_case(dev, rank, world, dist, steps=min(args.steps, 40), cpu=cpu)
         elif args.workload == "c3":
-            r = [bw.c3_case(dev, alpha=a, steps=min(args.steps, 40)) for a in (0.01, 0.1)]
-            r.append(bw.c3_case(dev, alpha=0.01, steps=min(args.steps, 40), wavelet="haar"))
-            r.append(bw.c3_round_case(dev, rank, world, dist, rounds=min(args.steps, 10)))
+            r = [bw.c3_case(dev, alpha=a, steps=min(args.steps, 40), cpu=cpu) for a in (0.01, 0.1)]
+            r.append(bw.c3_case(dev, alpha=0.01, steps=min(args.steps, 40), wavelet="haar",
+                                cpu=cpu))
+            r.append(bw.c3_round_case(dev, rank, world, dist, rounds=min(args.steps, 10), cpu=cpu))
         elif args.workload == "c5":
-            r = bw.c5_case(dev, steps=min(args.steps, 40), streams=args.streams)
+            r = bw.c5_case(dev, steps=min(args.steps, 40), streams=args.streams, cpu=cpu)
         else:
-            r = {"c2": bw.e2e_case(dev, 11_000_000, 0.01, streams=args.streams),
-                 "64MiB": bw.e2e_case(dev, 16_777_216, 0.01, streams=args.streams),
+            r = {"c2": bw.e2e_case(dev, 11_000_000, 0.01, streams=args.streams, cpu=cpu),
+                 "64MiB": bw.e2e_case(dev, 16_777_216, 0.01, streams=args.streams, cpu=cpu),
                  "c5_fp16": bw.e2e_case(dev, 67_108_864, 0.001, fp16=True,
-                                        streams=args.streams)}
+                                        streams=args.streams, cpu=cpu)}
         if rank == 0:
             print(json.dumps({"metric": "GiB/s fp32 params encoded+decoded", "unit": "GiB/s",
                               "workload": args.workload, "n_gpus": world, "result": r}),

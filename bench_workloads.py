@@ -10,9 +10,129 @@ Node states rotate so each step streams its inputs from HBM, not the 256 MiB Inf
 import math
 import time
 
+import numpy as np
 import torch
 
 L3_BYTES = 256 * 2 ** 20
+
+
+def _cpu_leg(make_step, units_per_step, unit_bytes, sample, seconds=12.0, scale=1.0,
+             full_affinity=True):
+    """cpu_baseline of a workload: the reference's op sequence (oracle/ref_round.py,
+    oracle/ref_ops.py — test infrastructure, imported by the callers' CPU legs only) timed on this
+    box's host cores.  ``make_step()`` builds the inputs once and returns a step function; steps
+    repeat until ``seconds`` (at least one), at torch's intra-op threads (the job's CPU share) and,
+    when the step is short enough, at every CPU of the affinity mask.  ``scale``: the step is a
+    bounded sample of the workload's unit (e.g. 1 of 16 nodes): time x scale = one unit.
+    value = unit_bytes / (median time x scale) in GiB/s."""
+    import os
+
+    step = make_step()
+
+    def run(threads, budget):
+        prev = torch.get_num_threads()
+        torch.set_num_threads(threads)
+        try:
+            times = []
+            t_start = time.perf_counter()
+            while True:
+                t0 = time.perf_counter()
+                step()
+                times.append(time.perf_counter() - t0)
+                if time.perf_counter() - t_start > budget:
+                    break
+        finally:
+            torch.set_num_threads(prev)
+        return sorted(times)[len(times) // 2], len(times)
+
+    cores = torch.get_num_threads()
+    step()  # warm: first-touch of the inputs, the thread pool
+    t, nsteps = run(cores, seconds)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    res = {"value": round(unit_bytes / (t * scale) / 2 ** 30, 5), "unit": "GiB/s",
+           "cores": cores, "kind": "port", "host_cpu_count": os.cpu_count(),
+           "affinity_cpus": affinity, "seconds_per_unit": round(t * scale, 4),
+           "units_per_step": units_per_step,
+           "sample": f"{sample}; median of {nsteps} step(s) at {cores} torch threads (the job's "
+                     f"CPU share)" + (f", x{scale:g} to one unit" if scale != 1 else "")}
+    if full_affinity and affinity and affinity > cores and t < 0.6:
+        tf, nf = run(affinity, seconds / 3)
+        res["full_affinity"] = {"threads": affinity, "steps": nf,
+                                "value": round(unit_bytes / (tf * scale) / 2 ** 30, 5),
+                                "unit": "GiB/s",
+                                "note": "every CPU of the affinity mask (shared host)"}
+    elif full_affinity and affinity and affinity <= cores:
+        res["full_affinity"] = {"threads": affinity, "value": res["value"],
+                                "note": "the job's threads are every CPU of the affinity mask"}
+    elif full_affinity:
+        res["full_affinity"] = {"threads": affinity, "value": None,
+                                "note": f"not timed: one step takes {t:.2f} s at {cores} threads "
+                                        "(the 64 MiB headline's full-affinity leg measured 20x "
+                                        "slower than its 16-thread leg on a shared host)"}
+    return res
+
+
+def _host_payloads(m, k, npay, seed, dtype=np.float32):
+    """npay sorted, duplicate-free random index sets of about k entries over [0, m) with values
+    (host numpy, for the CPU legs)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(npay):
+        idx = np.unique(rng.integers(0, m, size=int(k * 1.12) + 8))[:k].astype(np.int32)
+        out.append((idx, rng.standard_normal(idx.shape[0]).astype(dtype)))
+    return out
+
+
+def cpu_wavelet_round(n, alpha, npay, seed, level=4, wavelet="sym2", scale=1.0, seconds=10.0,
+                      what="one JWINS node round"):
+    """cpu_baseline of the wavelet rounds: oracle/ref_round.py wavelet_node (the reference's ATen
+    ops, pywt's sym2 / haar as the NumPy restatement) on one node's N-parameter model."""
+    def make():
+        from oracle import ref_round
+        from oracle import wavelet as owav
+        g = torch.Generator().manual_seed(seed)
+        x = torch.randn(n, generator=g)
+        x0 = x - 0.01 * torch.randn(n, generator=g)
+        m = owav.coeff_len(n, level, wavelet)
+        acc = 0.01 * torch.randn(m, generator=g)
+        cnt = torch.zeros(m, dtype=torch.int32)
+        pays = _host_payloads(m, round(alpha * m), npay, seed)
+        w = [1 / (npay + 1)] * npay
+        return lambda: ref_round.wavelet_node(x, x0, acc, alpha, cnt, pays, w, level, wavelet)
+    return _cpu_leg(make, 1, 4 * n, f"{what}: oracle/ref_round.py wavelet_node, N={n}, "
+                                    f"{wavelet} level {level}, alpha={alpha}, {npay} payloads "
+                                    f"(ATen ops + the NumPy pywt restatement)",
+                    seconds=seconds, scale=scale)
+
+
+def cpu_partial_round(n, alpha, npay, seed, fp16=False, scale=1.0, seconds=10.0,
+                      what="one PartialModel node round"):
+    """cpu_baseline of the PartialModel rounds: oracle/ref_round.py partial_node (encode + the MH
+    fold of npay payloads; npay = 0: encode + the replace decode of one payload, C5 / C2 shape)."""
+    def make():
+        from oracle import ref_ops, ref_round
+        g = torch.Generator().manual_seed(seed)
+        x = torch.randn(n, generator=g)
+        x0 = x - 0.01 * torch.randn(n, generator=g)
+        cnt = torch.zeros(n, dtype=torch.int32)
+        if npay == 0:
+            def step():
+                idx, vals = ref_ops.encode(x, x0, alpha, cnt)
+                if fp16:
+                    vals = torch.from_numpy(vals).half().float().numpy()
+                ref_ops.decode(x0, idx, vals)
+            return step
+        pays = _host_payloads(n, round(alpha * n), npay, seed,
+                              dtype=np.float16 if fp16 else np.float32)
+        w = [1 / (npay + 1)] * npay
+        return lambda: ref_round.partial_node(x, x0, alpha, cnt, pays, w, fp16=fp16)
+    shape = (f"{npay} payloads MH-folded" if npay else "encode + replace decode")
+    return _cpu_leg(make, 1, 4 * n, f"{what}: oracle/ref_round.py, N={n}, alpha={alpha}, "
+                                    f"{shape}{', fp16 values' if fp16 else ''}",
+                    seconds=seconds, scale=scale)
 
 
 def _sync_time(fn, steps):
@@ -24,7 +144,8 @@ def _sync_time(fn, steps):
     return (time.perf_counter() - t0) / steps
 
 
-def c3_case(dev, n=25_000_000, alpha=0.01, npay=16, steps=40, warmup=5, seed=3, wavelet="sym2"):
+def c3_case(dev, n=25_000_000, alpha=0.01, npay=16, steps=40, warmup=5, seed=3, wavelet="sym2",
+            cpu=True):
     """C3: one JWINS node round on an N-parameter model (reference Wavelet.py:142-329 with the
     tutorial/JWINS/config.ini settings change_based_selection, accumulation and
     accumulate_averaging_changes on): encode = W(x), W(x - x0) in one DWT launch, top-k of
@@ -133,7 +254,7 @@ def c3_case(dev, n=25_000_000, alpha=0.01, npay=16, steps=40, warmup=5, seed=3, 
     b_dec = 4 * m + 4 * n + 8 * npay * k + 8 * m
     b_post = 8 * n + 8 * m  # read x_new, prev; acc read + write
     b = b_enc + b_dec + b_post
-    return dict(workload=f"C3: JWINS {wavelet} level-4 node round of an N={n} model (M={m} "
+    res = dict(workload=f"C3: JWINS {wavelet} level-4 node round of an N={n} model (M={m} "
                          f"coefficients): DWT pair + top-k (accumulation), {npay}-payload batched "
                          f"decode + MH average + IDWT, accumulating post-step DWT",
                 n=n, m=m, k=k, alpha=alpha, rotated_states=R,
@@ -146,10 +267,14 @@ def c3_case(dev, n=25_000_000, alpha=0.01, npay=16, steps=40, warmup=5, seed=3, 
                 scattered_ms_per_step=t_scat * 1e3, scattered_encode_us=t_scat_enc * 1e6,
                 scattered_step_frac_of_hbm_peak=b / t_scat / 8e12,
                 scattered_kernels_avg_us=kern_scat)
+    if cpu:
+        res["cpu_baseline"] = cpu_wavelet_round(n, alpha, npay, seed, level, wavelet,
+                                                seconds=8.0)
+    return res
 
 
 def c3_round_case(dev, rank, world, dist, n=25_000_000, rounds=10, warmup=2, seed=21,
-                  wavelet="sym2"):
+                  wavelet="sym2", cpu=True):
     """C3 shape (b): the topology-faithful JWINS round of tutorial/JWINS/regular_16.txt (16 nodes
     of degree 3, copied under tests/golden/) with the tutorial config (sym2 level 4, alpha_list
     [0.1, 0.15, 0.2, 0.25, 0.3, 0.4, 1.0] drawn per node from random.seed(uid), metadata_cap
@@ -203,16 +328,24 @@ def c3_round_case(dev, rank, world, dist, n=25_000_000, rounds=10, warmup=2, see
             alg.append(b)
     t = sum(times) / len(times)
     b = sum(alg) / len(alg)
-    return dict(workload=f"C3 shape (b): JWINS round of regular_16 (16 nodes x degree 3), "
+    res = dict(workload=f"C3 shape (b): JWINS round of regular_16 (16 nodes x degree 3), "
                          f"N={n} per node, {wavelet} level 4, tutorial alpha_list",
                 n=n, m=m, nodes=len(adj), world=world, rounds=rounds,
                 ms_per_round=t * 1e3, ms_per_round_min=min(times) * 1e3,
                 value=len(adj) * 4 * n / t / 2 ** 30,
                 alg_bytes_per_round=b, round_frac_of_hbm_peak=b / t / 8e12 / world,
                 scaling="strong (16 nodes fixed)")
+    if cpu and rank == 0:  # one node's round at the alpha list's median draw, x16 nodes
+        res["cpu_baseline"] = cpu_wavelet_round(
+            n, 0.2, 3, seed, 4, wavelet, scale=len(adj), seconds=8.0,
+            what="one of the 16 nodes (alpha 0.2, the tutorial list's median draw; degree 3)")
+        res["cpu_baseline"]["value"] = round(len(adj) * 4 * n / (
+            res["cpu_baseline"]["seconds_per_unit"]) / 2 ** 30, 5)
+        res["cpu_baseline"]["unit_note"] = "seconds_per_unit = one round of all 16 nodes"
+    return res
 
 
-def c5_case(dev, n=67_108_864, alpha=0.001, steps=40, warmup=5, seed=5, streams=3):
+def c5_case(dev, n=67_108_864, alpha=0.001, steps=40, warmup=5, seed=5, streams=3, cpu=True):
     """C5: 256 MiB fp32 tensor, 0.1 % top-k, payload values packed to fp16 (RNE, torch.half
     semantics) by the encode itself (DPZ_TOPK_VAL_FP16: compact writes the fp16 words, no
     packing launch); decode = fp16 unpack + replace.  B = 16N + 12k."""
@@ -253,14 +386,20 @@ def c5_case(dev, n=67_108_864, alpha=0.001, steps=40, warmup=5, seed=5, streams=
     t_one = _sync_time(step, steps)
     fb = codec.topk_status(W[0]) != 0
     b = 16 * n + 12 * k
-    return dict(workload=f"C5: N={n} (256 MiB) fp32, alpha={alpha} top-k, fp16 value packing",
-                n=n, k=k, rotated_states=R, streams=streams,
-                value=4 * n / t_multi / 2 ** 30, ms_per_step=t_multi * 1e3,
-                one_node_ms_per_step=t_one * 1e3, alg_bytes=b,
-                step_frac_of_hbm_peak=b / t_multi / 8e12, fell_back=fb)
+    res = dict(workload=f"C5: N={n} (256 MiB) fp32, alpha={alpha} top-k, fp16 value packing",
+               n=n, k=k, rotated_states=R, streams=streams,
+               value=4 * n / t_multi / 2 ** 30, ms_per_step=t_multi * 1e3,
+               one_node_ms_per_step=t_one * 1e3, alg_bytes=b,
+               step_frac_of_hbm_peak=b / t_multi / 8e12, fell_back=fb)
+    del sets
+    torch.cuda.empty_cache()
+    if cpu:
+        res["cpu_baseline"] = cpu_partial_round(n, alpha, 0, seed, fp16=True,
+                                                what="the C5 step (encode, fp16 values, decode)")
+    return res
 
 
-def e2e_case(dev, n, alpha, fp16=False, steps=20, warmup=3, seed=7, streams=3):
+def e2e_case(dev, n, alpha, fp16=False, steps=20, warmup=3, seed=7, streams=3, cpu=True):
     """PCIe-inclusive rate: the node's flat model arrives from host memory (pinned, H2D 4N), the
     payload leaves for the socket (D2H 8k, or 6k with fp16 values); a received payload arrives
     (H2D) and the averaged model returns to host memory (D2H 4N) — the reference's Sharing path
@@ -315,14 +454,20 @@ def e2e_case(dev, n, alpha, fp16=False, steps=20, warmup=3, seed=7, streams=3):
     t_one = _sync_time(step, steps)
     t_multi = _sync_time(step_multi, steps)
     pcie = 8 * n + (2 * (4 + (2 if fp16 else 4)) * k)
-    return dict(n=n, k=k, fp16_values=fp16, pcie_bytes_per_step=pcie,
-                one_node_GiBps=4 * n / t_one / 2 ** 30, one_node_ms_per_step=t_one * 1e3,
-                concurrent_GiBps=4 * n / t_multi / 2 ** 30, concurrent_ms_per_step=t_multi * 1e3,
-                concurrent_pcie_GBps=pcie / t_multi / 1e9, streams=streams)
+    res = dict(n=n, k=k, fp16_values=fp16, pcie_bytes_per_step=pcie,
+               one_node_GiBps=4 * n / t_one / 2 ** 30, one_node_ms_per_step=t_one * 1e3,
+               concurrent_GiBps=4 * n / t_multi / 2 ** 30, concurrent_ms_per_step=t_multi * 1e3,
+               concurrent_pcie_GBps=pcie / t_multi / 1e9, streams=streams)
+    del sets
+    torch.cuda.empty_cache()
+    if cpu:  # the reference's path is host-resident: no PCIe legs at all
+        res["cpu_baseline"] = cpu_partial_round(n, alpha, 0, seed, fp16=fp16, seconds=6.0,
+                                                what="the host-resident reference step")
+    return res
 
 
 def shard_case(dev, rank, world, dist, n=67_108_864, alpha=0.001, steps=20, warmup=3, seed=9,
-               fp16=True):
+               fp16=True, cpu=False, ops=None, unpack=None):
     """One tensor of N parameters sharded over the ranks (BASELINE config 5: 256 MiB
     on 8 GPUs, 0.1 % top-k, fp16 value packing): the global top-k with one all-gather of every
     rank's k candidates (decentralizepy_amd/shard.py; with ``fp16`` the local encodes write fp16
@@ -343,26 +488,32 @@ def shard_case(dev, rank, world, dist, n=67_108_864, alpha=0.001, steps=20, warm
         sets.append(dict(x=x, x0=x - 0.01 * torch.randn(nl, device=dev, generator=g),
                          cnt=torch.zeros(nl, dtype=torch.int32, device=dev),
                          out=torch.empty(nl, device=dev)))
-    ops = HipShardOps(dev)
-    ws = codec.Workspace(dev)
+    # ops / unpack: injectable device steps (tests/test_cpu_bench_collectives.py runs this
+    # function on gloo ranks with the oracle in place of the HIP codec)
+    ops = ops or HipShardOps(dev)
+    unpack = unpack or codec.unpack_fp16
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
 
     def step(i):
         d = sets[i % R]
         idx, val = sharded_topk_encode(d["x"], d["x0"], k, lo, counter=d["cnt"], ops=ops,
                                        val_fp16=fp16)
         if fp16:
-            val = codec.unpack_fp16(val)
+            val = unpack(val)
         sharded_replace(d["x0"], lo, idx, val, out=d["out"], ops=ops)
 
     for i in range(warmup):
         step(i)
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(steps):
         step(i)
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
     t = (time.perf_counter() - t0) / steps
@@ -370,14 +521,19 @@ def shard_case(dev, rank, world, dist, n=67_108_864, alpha=0.001, steps=20, warm
         tt = torch.tensor([t], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
-    return dict(workload=f"one N={n} tensor sharded over {world} GPU(s), alpha={alpha}"
-                         f"{', fp16 values written by the encode' if fp16 else ''}: sharded "
-                         f"top-k (one all-gather of {world} x {k} candidates) + slice decode",
-                n=n, k=k, world=world, value=4 * n / t / 2 ** 30, ms_per_step=t * 1e3,
-                scaling="strong")
+    res = dict(workload=f"one N={n} tensor sharded over {world} GPU(s), alpha={alpha}"
+                        f"{', fp16 values written by the encode' if fp16 else ''}: sharded "
+                        f"top-k (one all-gather of {world} x {k} candidates) + slice decode",
+               n=n, k=k, world=world, value=4 * n / t / 2 ** 30, ms_per_step=t * 1e3,
+               scaling="strong")
+    if cpu and rank == 0:  # the whole tensor on the host (the reference has no sharding)
+        del sets
+        res["cpu_baseline"] = cpu_partial_round(n, alpha, 0, seed, fp16=fp16,
+                                                what="the whole tensor's step on the host")
+    return res
 
 
-def fft_case(dev, n=11_000_000, alpha=0.01, npay=3, steps=30, warmup=5, seed=9):
+def fft_case(dev, n=11_000_000, alpha=0.01, npay=3, steps=30, warmup=5, seed=9, cpu=True):
     """The FFT sharing plugin's device round (reference sharing/JWINS/FFT.py:132-302) on an
     N-parameter model: encode = x - x0, rfft(x) and rfft(x - x0) (hipFFT), |change| (complex, HIP),
     top-k on it with the counter, complex values gathered from rfft(x); decode = npay complex
@@ -426,11 +582,44 @@ def fft_case(dev, n=11_000_000, alpha=0.01, npay=3, steps=30, warmup=5, seed=9):
             step(i)
         torch.cuda.synchronize()
     kern = {nm: round(ms / c * 1e3, 2) for nm, (ms, c) in kt.result.items()}
-    return dict(workload=f"FFT plugin round: rfft top-k encode + {npay}-payload complex fold + "
-                         f"irfft of an N={n} model (M={m} coefficients)",
-                n=n, m=m, k=k, alpha=alpha, value=4 * n / t / 2 ** 30, ms_per_step=t * 1e3,
-                note="hipFFT transforms are not in the per-kernel table (library kernels)",
-                kernels_avg_us=kern)
+    res = dict(workload=f"FFT plugin round: rfft top-k encode + {npay}-payload complex fold + "
+                        f"irfft of an N={n} model (M={m} coefficients)",
+               n=n, m=m, k=k, alpha=alpha, value=4 * n / t / 2 ** 30, ms_per_step=t * 1e3,
+               note="hipFFT transforms are not in the per-kernel table (library kernels)",
+               kernels_avg_us=kern)
+    if cpu:
+        def make():
+            # the reference's FFT round on the host (sharing/JWINS/FFT.py:12-26 rfft transformer,
+            # :132-148 apply_fft, :170-172 counter, :245-290 _averaging): torch.fft on CPU
+            gq = torch.Generator().manual_seed(seed)
+            x = torch.randn(n, generator=gq)
+            x0 = x - 0.01 * torch.randn(n, generator=gq)
+            cnt = torch.zeros(m, dtype=torch.int32)
+            hp = _host_payloads(m, k, npay, seed)
+            hp = [(torch.from_numpy(i).long(), torch.complex(torch.from_numpy(v),
+                                                             torch.from_numpy(v)))
+                  for i, v in hp]
+
+            def step():
+                fx = torch.fft.rfft(x)
+                ch = torch.fft.rfft(x - x0)
+                _, index = torch.topk(ch.abs(), k, dim=0, sorted=False)
+                index, _ = torch.sort(index)
+                fx[index]
+                cnt[index] += 1
+                total, wt_ = None, 0
+                for (pi, pv), wv in zip(hp, w):
+                    tk = fx.clone()
+                    tk[pi] = pv
+                    wt_ += wv
+                    total = wv * tk if total is None else total + wv * tk
+                total += (1 - wt_) * fx
+                torch.fft.irfft(total, n)
+            return step
+        res["cpu_baseline"] = _cpu_leg(make, 1, 4 * n, f"the reference's FFT round (torch.fft "
+                                                      f"on CPU), N={n}, {npay} payloads",
+                                       seconds=8.0)
+    return res
 
 
 def wire_case(dev, n=11_000_000, alpha=0.01, reps=30, seed=13):
@@ -665,6 +854,14 @@ def plugin_case(dev, kind="partial", rounds=6, warmup=2, seed=17, cpu_rounds=1, 
     torch.cuda.empty_cache()
     if kind == "partial" and cpu_rounds > 0:
         res["cpu_baseline"] = _plugin_cpu_round(n, 0.01, cpu_rounds, seed)
+    elif cpu_rounds > 0:
+        # the JWINS round's reference op sequence (Wavelet.py:142-329 + PartialModel.py:305-350)
+        # at the alpha list's median draw; the payload compression legs are not in it (fpzip is
+        # absent, and the reference Elias walk over ~1-10 M indices takes seconds to minutes:
+        # compression/Elias.py, timed per entry by --workload wire)
+        res["cpu_baseline"] = cpu_wavelet_round(
+            n, 0.2, 3, seed, 4, "sym2", seconds=8.0,
+            what="the JWINS node round's reference ops without the compressor legs")
     return res
 
 

@@ -25,6 +25,8 @@ DPZ_TOPK_STREAM = 0x4
 DPZ_TOPK_TAIL = 0x8
 DPZ_TOPK_SHARED = 0x10
 DPZ_TOPK_VAL_FP16 = 0x20
+DPZ_TOPK_HINT = 0x40
+DPZ_TOPK_KEEP_X = 0x80
 DPZ_FOLD_SELF = 0x1
 DPZ_FOLD_REPLACE_ONLY = 0x2
 DPZ_FOLD_ZERO_BASE = 0x4

@@ -58,6 +58,7 @@ class Workspace:
         self._nk = None
         self.dbuf = None
         self.ebuf = None
+        self.hint_key = None  # signature of the last sampled-path encode enqueued on buf
 
     def get(self, n, k):
         if self.buf is not None and self._nk == (n, k):
@@ -65,6 +66,7 @@ class Workspace:
         need = int(_lib.lib().dpz_topk_workspace_bytes(int(n), int(k)))
         if self.buf is None or self.buf.numel() < need:
             self.buf = torch.zeros(max(need, 256), dtype=torch.uint8, device=self.device)
+            self.hint_key = None
         self._nk = (n, k)
         return self.buf
 
@@ -84,7 +86,7 @@ class Workspace:
 def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, counter=None,
                 idx_out=None, val_out=None, workspace=None, exact=False, asynchronous=False,
                 phase=None, co_replace=None, status_out=None, shared=False, fold_base=None,
-                val_fp16=False):
+                val_fp16=False, hint=False, keep_x=False):
     """Top-k magnitude encode (reference PartialModel.py:164-255 / Wavelet.py:142-197).
 
     Returns ``(idx int32[k], val fp32[k])`` in ascending index order.  Mutates ``acc`` and
@@ -106,6 +108,12 @@ def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, c
     w_self, out=base_out, base_ready=True)``.
     ``val_fp16``: the values are written as fp16 (round to nearest even, ``torch.half``), by the
     encode itself (DPZ_TOPK_VAL_FP16: the C5 payload's value packing); ``val`` is float16[k].
+    ``hint``: a node's next round — take the key window from the previous encode's exact
+    threshold on this ``workspace`` when that encode had the same n, k and key source, skipping
+    the sample launch (DPZ_TOPK_HINT; a window that no longer brackets the k-th key misses and a
+    blocking call re-runs the sampled path).  ``keep_x``: x is read again right after (the node's
+    fold over its own model): stream it with the default cache policy (DPZ_TOPK_KEEP_X).  Both
+    leave the result unchanged.
     """
     _require(x, torch.float32, "x")
     _require(x0, torch.float32, "x0")
@@ -124,10 +132,17 @@ def topk_encode(x, k, x0=None, acc=None, acc_mode=DPZ_ACC_NONE, vals_src=None, c
     _require(val_out, vdt, "val_out")
     if val_fp16 and (co_replace is not None or fold_base is not None):
         raise ValueError("val_fp16: a plain encode (no co_replace / fold_base)")
-    ws = (workspace or Workspace(x.device)).get(n, k)
+    wso = workspace or Workspace(x.device)
+    ws = wso.get(n, k)
     flags = ((DPZ_TOPK_EXACT if exact else 0) | (DPZ_TOPK_ASYNC if asynchronous else 0)
              | (_lib.DPZ_TOPK_SHARED if shared else 0)
-             | (_lib.DPZ_TOPK_VAL_FP16 if val_fp16 else 0))
+             | (_lib.DPZ_TOPK_VAL_FP16 if val_fp16 else 0)
+             | (_lib.DPZ_TOPK_KEEP_X if keep_x else 0))
+    # the device checks the prior's signature itself; this only avoids a predictable miss
+    hkey = (n, k, bool(shared), int(acc_mode), x0 is not None)
+    if hint and not exact and wso.hint_key == hkey:
+        flags |= _lib.DPZ_TOPK_HINT
+    wso.hint_key = None if exact else hkey
     if phase is not None:
         flags |= {"stream": DPZ_TOPK_STREAM, "tail": DPZ_TOPK_TAIL}[phase]
     if fold_base is not None:

@@ -120,7 +120,12 @@ struct TopkCtrl {
                            // (dpz_topk_sticky_status): misses of ASYNC calls never completed
   uint32_t val_h;          // sampled path: the call's value format (1 = fp16), for the exact
                            // re-run dpz_topk_complete makes after a miss
-  uint32_t pad[51];
+  // prior-round window (DPZ_TOPK_HINT): the exact threshold key of the last sampled call that
+  // completed on this workspace and that call's signature (n, k, geometry, key source; never 0);
+  // written by compact on success only
+  uint32_t hint_T, hint_sig;
+  uint32_t hinted;         // this call's filter took its window from hint_T (no sample launch)
+  uint32_t pad[48];
 };
 static_assert(sizeof(TopkCtrl) == 256, "ctrl size");
 
@@ -285,7 +290,29 @@ struct EncodeArgs {
   // ceil(n/32) words) += 1 instead of counter[idx] += 1; counter and the rewind are then unused
   uint32_t* selmask;
   uint32_t* planes;
+  // DPZ_TOPK_HINT: this call's signature when the filter may take its key window from the
+  // previous sampled call's exact threshold (TopkCtrl::hint_T), else 0 (the sample launch runs)
+  uint32_t hint_sig;
+  bool keep_x;            // DPZ_TOPK_KEEP_X: x streamed with the default cache policy
 };
+// Signature of a sampled call's geometry and key source: a prior-round window is only taken from
+// a call with the same one (the same workspace layout, so its window histogram copies are zero)
+static inline uint32_t hint_signature(int64_t n, int64_t k, bool shared, int acc_mode, bool x0) {
+  uint64_t h = 1469598103934665603ull;
+  const uint64_t v[5] = {(uint64_t)n, (uint64_t)k, shared ? 1ull : 0ull, (uint64_t)acc_mode,
+                         x0 ? 1ull : 0ull};
+  for (int i = 0; i < 5; ++i) h = (h ^ v[i]) * 1099511628211ull;
+  return (uint32_t)(h ^ (h >> 32)) | 1u;
+}
+// The key window around a prior threshold key T: [T (1 - 1/16), T (1 + 1/16)] — a drift of the
+// k-th largest |change| of up to 6.25 % between rounds still brackets it (validated by select's
+// counts; a miss re-runs the sampled path with its sample launch).  Measured on MI355X (64 MiB,
+// 1 %): +-1/8 put ~19 boundary entries on each of the 16 sub-lists, past the 16 compact loads
+// speculatively (a dependent load more: compact 13.5 -> 15.0 us, select 6.8 -> 7.5 us)
+#ifndef DPZ_HINT_DELTA
+#define DPZ_HINT_DELTA 0.0625f
+#endif
+constexpr float HINT_LO = 1.0f - DPZ_HINT_DELTA, HINT_HI = 1.0f + DPZ_HINT_DELTA;
 // the sampled compact builds a segment's mask words in LDS: segments of at most this many elements
 constexpr int64_t SL_RMAX = 8192;
 static inline int64_t mask_words(int64_t n) { return (n + 31) >> 5; }

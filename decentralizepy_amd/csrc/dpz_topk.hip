@@ -80,6 +80,11 @@ extern "C" size_t dpz_topk_workspace_bytes(int64_t n, int64_t k) {
 static int dpz_topk_dispatch(EncodeArgs a, int flags) {
   if (flags & DPZ_TOPK_SHARED) a.shared = true;
   if (flags & DPZ_TOPK_VAL_FP16) a.val_h = 1;
+  if (flags & DPZ_TOPK_KEEP_X) a.keep_x = true;
+  // a prior-round window (DPZ_TOPK_HINT): not with ACCUMULATE, whose first pass stores acc (a
+  // missed call could not simply be re-run on the sampled path)
+  if ((flags & DPZ_TOPK_HINT) && a.acc_mode != DPZ_ACC_ACCUMULATE)
+    a.hint_sig = hint_signature(a.n, a.k, a.shared, a.acc_mode, a.x0 != nullptr);
   const WsLayout L = ws_layout(a.n, a.k, a.shared);
   const bool vec = all_aligned(a);
   if (a.k == 0) {
@@ -479,8 +484,18 @@ extern "C" int dpz_topk_complete(const float* x, const float* x0, float* acc, in
   if (c.status == 0) return DPZ_OK;
   if (used_fallback) *used_fallback = 1;
   a.val_h = c.val_h ? 1 : 0;  // the value format the sampled call was issued with
-  // keys are re-derived from the post-filter state: ACCUMULATE already stored acc += change
   const bool vec = all_aligned(a);
+  if (c.hinted && a.acc_mode != DPZ_ACC_ACCUMULATE) {
+    // the prior-round window missed (or there was none): the sampled path again, with its own
+    // sample launch; nothing of the missed call was applied (compact writes nothing after a
+    // miss) and NONE / ADD keys are a pure function of the inputs
+    rc = run_sampled(a, L, vec, 3);
+    if (rc != DPZ_OK) return rc;
+    DPZ_HIP_TRY(hipStreamSynchronize(a.st));
+    DPZ_HIP_TRY(hipMemcpy(&c, a.ws + L.ctrl, sizeof(c), hipMemcpyDeviceToHost));
+    if (c.status == 0) return DPZ_OK;
+  }
+  // keys are re-derived from the post-filter state: ACCUMULATE already stored acc += change
   rc = run_exact(a, L, 1, vec);
   if (rc != DPZ_OK) return rc;
   DPZ_HIP_TRY(hipStreamSynchronize(a.st));

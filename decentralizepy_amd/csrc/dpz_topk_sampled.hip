@@ -103,6 +103,7 @@ __global__ void __launch_bounds__(1024) sampled_sample_kernel(KeySrc s, int64_t 
       ctrl->status = 0;
       ctrl->nbound = 0;
       ctrl->val_h = (uint32_t)val_h;
+      ctrl->hinted = 0;
     }
   }
   __syncthreads();
@@ -410,12 +411,32 @@ __device__ __forceinline__ void stage_group(WaveList& L, uint32_t* h, const uint
 // wavelet encode's W(x - x0) plus the accumulated changes, C3).
 // CP: what the filter also writes as x streams by — 0 nothing, 1 copy_out = x (the fused replace
 // decode), 2 copy_out = fb.of(x) (the Metro-Hastings fold's no-hit base, dpz_topk_encode_foldbase).
-template <int SRC, int CP, int D, int OCC>
+// Key window [lo, hi) around a prior threshold key T (DPZ_TOPK_HINT) and its fine-bin shift.
+__device__ __forceinline__ void hint_window(uint32_t T, uint32_t* lo, uint32_t* hi,
+                                            uint32_t* shift) {
+  const float t = __uint_as_float(T);
+  *lo = __float_as_uint(t * HINT_LO);
+  const uint64_t h64 = (uint64_t)__float_as_uint(t * HINT_HI) + 1u;  // inf + 1 at most
+  *hi = (uint32_t)(h64 > (1ull << 31) ? (1ull << 31) : h64);
+  const uint32_t width = *hi - *lo;
+  uint32_t sft = 0;
+  while ((((uint64_t)width + (1ull << sft) - 1) >> sft) > (uint64_t)HB) ++sft;
+  *shift = sft;
+}
+
+// XNT: x loaded non-temporal (true) or with the default policy (DPZ_TOPK_KEEP_X: the caller reads
+// x again right after, e.g. a node's fold over its own model, which may then hit the Infinity
+// Cache).  hsig != 0 (DPZ_TOPK_HINT): the window comes from the previous call's exact threshold
+// (ctrl->hint_T, valid when ctrl->hint_sig == hsig) and no sample launch ran before this one —
+// block 0 then does the sample launch's per-call resets (status, boundary sub-list counters; the
+// window-histogram copies were left zero by the previous call's compact); an invalid prior makes
+// the call miss at once (every block leaves, select and compact see the status).
+template <int SRC, int CP, int D, int OCC, bool XNT>
 __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
     KeySrc s, int64_t n, uint32_t r_lo, uint32_t r_hi, int64_t W, int64_t R, int64_t CAP,
     TopkCtrl* ctrl, const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt,
     uint32_t* cidx, uint32_t* ckey, float* cval, float* __restrict__ copy_out,
-    FoldBase fb) {
+    FoldBase fb, uint32_t hsig, uint32_t* blcnt, int val_h) {
   static_assert(D >= 2, "at least one group in flight");
   typedef float v4f __attribute__((ext_vector_type(4)));
   __shared__ uint32_t h[HBR];
@@ -429,8 +450,29 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
   const int64_t beg = seg * R;  // a multiple of 4 (R is); >= n for the grid's spare waves
   const int64_t end = (beg + R < n) ? beg + R : n;
   const int64_t end4 = beg < end ? beg + ((end - beg) & ~int64_t(3)) : beg;
-  uint4 cv[2];
-  {
+  uint4 cv[2] = {};
+  uint32_t hT = 0;
+  if (hsig) {
+    hT = ctrl->hint_T;
+    const bool ok = ctrl->hint_sig == hsig && hT > 0u && hT < 0x7F800000u;
+    if (!ok) {  // no usable prior window: the call misses (uniform over the grid)
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctrl->status = 1;
+        ctrl->hinted = 1;
+        ctrl->val_h = (uint32_t)val_h;
+      }
+      return;
+    }
+    if (blockIdx.x == 0) {
+      if (threadIdx.x < NSUB) blcnt[threadIdx.x] = 0;
+      if (threadIdx.x == 0) {
+        ctrl->status = 0;
+        ctrl->nbound = 0;
+        ctrl->val_h = (uint32_t)val_h;
+        ctrl->hinted = 1;
+      }
+    }
+  } else {
     const uint4* c4 = reinterpret_cast<const uint4*>(chist) + (510 - 2 * threadIdx.x);
     cv[0] = c4[0];
     cv[1] = c4[1];
@@ -447,14 +489,22 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
     // (an xnt kernel argument, tried in round 4) compiled to ONE plain load — the hint was lost,
     // x stayed in the caches and the compact's counter updates slowed by 1-3 us (same-box A/B
     // against the round-3 build, tools/diag/enc_ab.py)
-    A[u] = __builtin_nontemporal_load(xa + g4);
+    if (XNT) A[u] = __builtin_nontemporal_load(xa + g4);
+    else A[u] = xa[g4];
     if (X0) B[u] = __builtin_nontemporal_load(xb + g4);
   };
 #pragma unroll
   for (int u = 0; u < D - 1; ++u) ld(u, u);
-  block_window(cv, r_lo, r_hi, win, wsum);
+  uint32_t lo, hi, shift;
+  if (hsig) {
+    hint_window(hT, &lo, &hi, &shift);
+  } else {
+    block_window(cv, r_lo, r_hi, win, wsum);
+    lo = win[0];
+    hi = win[1];
+    shift = win[2];
+  }
   STAMP_T0(6);
-  const uint32_t lo = win[0], hi = win[1], shift = win[2];
   if (seg == 0 && lane == 0) {
     ctrl->lo = lo;
     ctrl->hi = hi;
@@ -576,6 +626,8 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
       return;
     }
   }
+  // a hinted filter without a usable prior window reported a miss: nothing to select
+  if (ctrl->status) return;
   STAMP_MIN(6);
   STAMP_T0(8);
   __shared__ __attribute__((aligned(16))) uint32_t gh[GH_STRIDE];
@@ -1043,7 +1095,7 @@ __global__ void __launch_bounds__(256, SPW >= 8 ? 1 : 4) sampled_compact_kernel(
     const uint32_t* __restrict__ ckey, const float* __restrict__ cval, const float* vals_src,
     int32_t* idx_out, float* val_out, int32_t* counter, float* rewind, int32_t* status_out,
     ReplaceJob pj, int64_t nrep_first, int val_h, uint32_t* selmask, uint32_t* planes,
-    int64_t nwords) {
+    int64_t nwords, uint32_t* ghist, uint32_t sig) {
   constexpr int CSEG = CompactCfg<SPW>::CSEG;
   constexpr int PFC = CompactCfg<SPW>::PFC;
   constexpr int SLW = SL ? (int)(SL_RMAX / 32) : 1;
@@ -1066,6 +1118,10 @@ __global__ void __launch_bounds__(256, SPW >= 8 ? 1 : 4) sampled_compact_kernel(
   const uint32_t blk = (uint32_t)((int64_t)blockIdx.x - (nrep_first > 0 ? nrep_first : 0));
   STAMP_T0(0);
   const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
+  // select has read the window-histogram copies: leave them zero for the next call (a call with
+  // a prior-round window has no sample launch to zero them, DPZ_TOPK_HINT)
+  for (int64_t b = (int64_t)blk * 256 + t; b < (int64_t)GH_COPIES * GH_STRIDE; b += CB_ * 256)
+    ghist[b] = 0u;
   const int64_t seg0 = (int64_t)blk * CSEG + wid * SPW;
   // every independent load first: control words, sub-list counts, above counts, own candidates
   const uint32_t status = ctrl->status;
@@ -1193,6 +1249,9 @@ __global__ void __launch_bounds__(256, SPW >= 8 ? 1 : 4) sampled_compact_kernel(
     if (grand != (uint32_t)k) {  // internal inconsistency
       ctrl->status = 2;
       atomicOr(&ctrl->sticky, 2u);
+    } else {  // the next call with this signature may take its window from T (DPZ_TOPK_HINT)
+      ctrl->hint_T = T;
+      ctrl->hint_sig = sig;
     }
     if (status_out) *status_out = grand != (uint32_t)k ? 2 : 0;
   }
@@ -1428,19 +1487,25 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
       c = e;
     }
   }
+  // The pipelined filter (PartialModel: aligned, no accumulation): depth 2 at 8 waves / SIMD
+  // when the grid needs them (more than 4096 segments), else depth DPZ_FILTER_DEPTH (default
+  // 4) at 4 waves / SIMD.  DPZ_FILTER_PIPE=0 selects the batched filter (A/B diagnostics).
+  const int pipe = (int)DPZ_KNOB_INT(FILTER_PIPE, 1);
+  const bool add_only = a.acc_mode == DPZ_ACC_ADD && !a.x0;
+  const bool piped = VEC && (a.acc_mode == DPZ_ACC_NONE || add_only) && pipe > 0;
+  // a prior-round window replaces the sample launch (pipelined filter only; the job-carrying
+  // co-scheduled decode splits its blocks over the sample launch, so it keeps it)
+  const uint32_t hsig = (piped && !a.job) ? a.hint_sig : 0u;
+  const uint32_t sig = hint_signature(a.n, a.k, a.shared, a.acc_mode, a.x0 != nullptr);
   if (phases & 1) {
-    DPZ_TIMED(DPZ_KT_TOPK_SAMPLE, a.st,
-              sampled_sample_kernel<<<smp_blocks + pb[0], smp_threads, 0, a.st>>>(
-                  s, a.n, ctrl, chist, ghist, blcnt, jb[0], smp_blocks, a.val_h));
+    if (!hsig)
+      DPZ_TIMED(DPZ_KT_TOPK_SAMPLE, a.st,
+                sampled_sample_kernel<<<smp_blocks + pb[0], smp_threads, 0, a.st>>>(
+                    s, a.n, ctrl, chist, ghist, blcnt, jb[0], smp_blocks, a.val_h));
     uint32_t r_lo, r_hi;
     window_ranks(a.n, a.k, &r_lo, &r_hi);
-    // The pipelined filter (PartialModel: aligned, no accumulation): depth 2 at 8 waves / SIMD
-    // when the grid needs them (more than 4096 segments), else depth DPZ_FILTER_DEPTH (default
-    // 4) at 4 waves / SIMD.  DPZ_FILTER_PIPE=0 selects the batched filter (A/B diagnostics).
-    const int pipe = (int)DPZ_KNOB_INT(FILTER_PIPE, 1);
     const int depth = (int)DPZ_KNOB_INT(FILTER_DEPTH, 4);
-    const bool add_only = a.acc_mode == DPZ_ACC_ADD && !a.x0;
-    if (VEC && (a.acc_mode == DPZ_ACC_NONE || add_only) && pipe > 0) {
+    if (piped) {
       const bool x0 = a.x0 != nullptr;
       // the fold base (dpz_topk_encode_foldbase) rides on the same copy slot
       const bool fbase = a.fbase && a.base_out && x0 && !copy_out;
@@ -1457,16 +1522,24 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
     else if (copy_out) DPZ_PIPE1(0, 1, D_, O_);                                               \
     else DPZ_PIPE1(0, 0, D_, O_);                                                             \
   } while (0)
-#define DPZ_PIPE1(X0_, CP_, D_, O_)                                                           \
-  DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, sampled_filter_pipe_kernel<X0_, CP_, D_, O_><<<nb, 256, 0, a.st>>>( \
+#define DPZ_PIPE2(X0_, CP_, D_, O_, XNT_)                                                     \
+  DPZ_TIMED(DPZ_KT_TOPK_FILTER, a.st, (sampled_filter_pipe_kernel<X0_, CP_, D_, O_, XNT_><<<nb, 256, 0, a.st>>>( \
       s, a.n, r_lo, r_hi, g.W, g.R, g.CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval, cpo, \
-      fbv))
+      fbv, hsig, blcnt, a.val_h)))
+      // x with the default cache policy (DPZ_TOPK_KEEP_X) for the plugin's encode (CP 0) and the
+      // fold-base encode (CP 2), whose callers read x again in the fold
+#define DPZ_PIPE1(X0_, CP_, D_, O_)                                                           \
+  do {                                                                                        \
+    if ((CP_ == 0 || CP_ == 2) && X0_ == 1 && a.keep_x) DPZ_PIPE2(X0_, CP_, D_, O_, false);   \
+    else DPZ_PIPE2(X0_, CP_, D_, O_, true);                                                   \
+  } while (0)
       switch (dsel) {
         case 2: DPZ_PIPE(2, 8); break;
         case 8: DPZ_PIPE(8, 4); break;
         case 6: DPZ_PIPE(6, 4); break;
         default: DPZ_PIPE(4, 4); break;
       }
+#undef DPZ_PIPE2
 #undef DPZ_PIPE1
 #undef DPZ_PIPE
     } else if (a.acc_mode == DPZ_ACC_NONE)
@@ -1505,7 +1578,8 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
                                                            256, 0, a.st>>>(                       \
                 s, a.n, a.k, g.W, g.R, g.CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, \
                 cidx, ckey, cval, a.vals_src, a.idx_out, a.val_out, counter, rewind,              \
-                a.status_out, jb[2], nrep_first, a.val_h, a.selmask, a.planes, mask_words(a.n))))
+                a.status_out, jb[2], nrep_first, a.val_h, a.selmask, a.planes, mask_words(a.n),  \
+                ghist, sig)))
   if (a.selmask && g.R <= SL_RMAX) {
     // sliced side effects (dpz_topk_encode_sliced) from per-wave LDS rows of the segment's words
     DPZ_COMPACT(false, 2, true);

@@ -184,12 +184,15 @@ class PartialModel(Sharing):
             base = torch.empty_like(self.pre_share_model)
             out = codec.topk_encode(key_src, k, x0=x0, vals_src=self.pre_share_model_transformed,
                                     counter=self._counter, workspace=self.workspace,
-                                    fold_base=(base, pred[0], pred[1]))
+                                    fold_base=(base, pred[0], pred[1]), hint=True, keep_x=True)
             self._fb = (base, pred, self.pre_share_model)
             return out
+        # hint: the previous round's exact threshold as this round's key window (no sample
+        # launch); keep_x: _averaging folds over this x right after (Infinity Cache)
         return codec.topk_encode(key_src, k, x0=x0, acc=acc, acc_mode=self._acc_mode(),
                                  vals_src=self.pre_share_model_transformed, counter=self._counter,
-                                 workspace=self.workspace)
+                                 workspace=self.workspace, hint=True,
+                                 keep_x=key_src is self.pre_share_model)
 
     def _predicted_fold(self):
         """The Metro-Hastings weights _averaging will use (Sharing.py:156-190), predicted from

@@ -62,6 +62,21 @@ typedef void* dpz_stream_t; /* hipStream_t */
  * launch.  val_out then holds k * 2 bytes.  A later dpz_topk_complete re-runs a missed sampled
  * call in the same format.                                                                    */
 #define DPZ_TOPK_VAL_FP16 0x20
+/* Prior-round key window: the sampled path takes the filter's key window from the exact
+ * threshold of the previous sampled call on this workspace — same n, k, DPZ_TOPK_SHARED choice,
+ * acc_mode and x0 presence, completed without a miss — as [0.9375 T, 1.0625 T], and skips its
+ * sample launch (a node's consecutive rounds: the k-th largest |change| drifts slowly).  The
+ * window is validated like a sampled one; when it does not bracket the k-th key (or no such
+ * previous call exists) the call misses: a blocking call / dpz_topk_complete then re-runs the
+ * SAMPLED path (sample launch included) and only if that misses too the exact path; an
+ * asynchronous caller sees the miss in the status word.  Ignored with DPZ_ACC_ACCUMULATE and on
+ * the paths without the pipelined filter (unaligned operands).  Results are identical.       */
+#define DPZ_TOPK_HINT 0x40
+/* x is streamed with the default cache policy instead of non-temporal loads: for a caller that
+ * reads x again right after the encode (a node's Metro-Hastings fold over its own model,
+ * sharing/Sharing.py:156-190 after PartialModel.py:188-255), whose re-read may then be served
+ * by the 256 MiB Infinity Cache.  Results are identical.                                       */
+#define DPZ_TOPK_KEEP_X 0x80
 
 /* ---- fold flags ---- */
 #define DPZ_FOLD_SELF 0x1         /* add the local term w_self*local after the payloads        */

@@ -1,0 +1,147 @@
+"""GPU: the prior-round key window (DPZ_TOPK_HINT: the filter's window from the previous encode's
+exact threshold on the workspace, no sample launch) and the keep-x cache policy
+(DPZ_TOPK_KEEP_X) leave every result of the reference's top-k encode unchanged
+(sharing/PartialModel.py:164-255): index sets, values and the shared-parameter counter are
+bit-exact against the oracle over a node's consecutive rounds, and a window that no longer
+brackets the k-th key (a jump in the change distribution, a prior of another size) is a miss
+that the blocking call / dpz_topk_complete recovers on the sampled path."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import topk as otopk
+
+pytestmark = pytest.mark.gpu
+
+# TopkCtrl word offsets (csrc/dpz_topk.h)
+_STATUS, _STICKY, _HINT_T, _HINT_SIG, _HINTED = 2, 11, 13, 14, 15
+
+
+def _ctrl(ws):
+    torch.cuda.synchronize()
+    return ws.buf[:256].view(torch.int32).cpu().numpy().view(np.uint32)
+
+
+def _inputs(n, seed, scale):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, generator=g)
+    x0 = x - scale * torch.randn(n, generator=g)
+    return x.numpy(), x0.numpy()
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def _round(dev, ws, x, x0, k, tcnt, o_cnt, **kw):
+    from decentralizepy_amd import codec
+    idx, val = codec.topk_encode(torch.from_numpy(x).to(dev), k, x0=torch.from_numpy(x0).to(dev),
+                                 counter=tcnt, workspace=ws, **kw)
+    oi, ov = otopk.encode(x, x0, None, otopk.ACC_NONE, k, counter=o_cnt)
+    np.testing.assert_array_equal(idx.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(val.cpu().numpy()), _bits(ov))
+    np.testing.assert_array_equal(tcnt.cpu().numpy(), o_cnt)
+
+
+@pytest.mark.parametrize("n,alpha", [(1_000_003, 0.01), (16_777_216, 0.01), (2_000_000, 0.05)])
+def test_hinted_rounds_match_oracle(dev, n, alpha):
+    """A node's rounds with a slowly drifting change scale: from round 1 on the window is the
+    prior one (no sample launch: ctrl.hinted), every round bit-exact; keep_x alternates."""
+    from decentralizepy_amd import codec
+    k = round(alpha * n)
+    ws = codec.Workspace(dev)
+    tcnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    o_cnt = np.zeros(n, dtype=np.int32)
+    for r in range(4):
+        x, x0 = _inputs(n, 100 + r, 0.01 * (1.0 + 0.04 * r))
+        _round(dev, ws, x, x0, k, tcnt, o_cnt, hint=True, keep_x=bool(r % 2))
+        c = _ctrl(ws)
+        assert c[_STATUS] == 0 and c[_HINTED] == (1 if r else 0)
+        assert c[_HINT_SIG] != 0
+    assert codec.topk_sticky_status(ws) == 0
+
+
+def test_hint_miss_blocking_recovers_on_sampled_path(dev):
+    """The change scale doubles between rounds: the prior window misses, the blocking call
+    re-runs the sampled path (its sample launch resets ctrl.hinted) and the result is exact;
+    the miss shows in the sticky status word."""
+    from decentralizepy_amd import codec
+    n, k = 1_000_003, 10_000
+    ws = codec.Workspace(dev)
+    tcnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    o_cnt = np.zeros(n, dtype=np.int32)
+    for r, scale in enumerate((0.01, 0.02, 0.02)):
+        x, x0 = _inputs(n, 200 + r, scale)
+        _round(dev, ws, x, x0, k, tcnt, o_cnt, hint=True)
+        c = _ctrl(ws)
+        assert c[_STATUS] == 0
+        if r == 1:
+            assert c[_HINTED] == 0  # re-run with the sample launch
+            assert codec.topk_sticky_status(ws, clear=True) != 0
+        if r == 2:
+            assert c[_HINTED] == 1  # the re-run's threshold is the new prior
+            assert codec.topk_sticky_status(ws) == 0
+
+
+def test_hint_miss_asynchronous_then_complete(dev):
+    """An asynchronous hinted call that misses wrote nothing and reports it; dpz_topk_complete
+    re-runs it (sampled path) to the exact result."""
+    from decentralizepy_amd import codec
+    n, k = 1_000_003, 10_000
+    ws = codec.Workspace(dev)
+    x, x0 = _inputs(n, 300, 0.01)
+    tcnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    o_cnt = np.zeros(n, dtype=np.int32)
+    _round(dev, ws, x, x0, k, tcnt, o_cnt, hint=True)
+    x, x0 = _inputs(n, 301, 0.005)  # the k-th key halves: below the window
+    tx, tx0 = torch.from_numpy(x).to(dev), torch.from_numpy(x0).to(dev)
+    idx = torch.full((k,), -7, dtype=torch.int32, device=dev)
+    val = torch.empty(k, device=dev)
+    codec.topk_encode(tx, k, x0=tx0, counter=tcnt, idx_out=idx, val_out=val, workspace=ws,
+                      asynchronous=True, hint=True)
+    assert _ctrl(ws)[_STATUS] != 0
+    assert (idx.cpu().numpy() == -7).all()  # a miss writes nothing
+    np.testing.assert_array_equal(tcnt.cpu().numpy(), o_cnt)  # and counts nothing
+    assert codec.topk_complete(tx, k, idx, val, ws, x0=tx0, counter=tcnt)
+    oi, ov = otopk.encode(x, x0, None, otopk.ACC_NONE, k, counter=o_cnt)
+    np.testing.assert_array_equal(idx.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(val.cpu().numpy()), _bits(ov))
+    np.testing.assert_array_equal(tcnt.cpu().numpy(), o_cnt)
+
+
+def test_hint_from_another_signature_is_a_miss(dev):
+    """A prior of another k on the same workspace (the flag forced past the Python check): the
+    device signature does not match, the call misses at once and is re-run, exact."""
+    from decentralizepy_amd import codec
+    n = 1_000_003
+    ws = codec.Workspace(dev)
+    big = int(codec._lib.lib().dpz_topk_workspace_bytes(n, 20_000))
+    ws.buf = torch.zeros(big, dtype=torch.uint8, device=dev)  # room for both k
+    tcnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    o_cnt = np.zeros(n, dtype=np.int32)
+    x, x0 = _inputs(n, 400, 0.01)
+    _round(dev, ws, x, x0, 20_000, tcnt, o_cnt, hint=True)
+    ws.hint_key = (n, 10_000, False, 0, True)  # pretend the prior was a k = 10,000 call
+    _round(dev, ws, x, x0, 10_000, tcnt, o_cnt, hint=True)
+    assert codec.topk_sticky_status(ws, clear=True) != 0  # it missed, then recovered
+
+
+def test_hint_with_fold_base_and_fp16(dev):
+    """The prior window under the fold-base encode (PartialModel's one-neighbour path) and the
+    fp16 value format: results equal the non-hinted encode's."""
+    from decentralizepy_amd import codec
+    n, k = 2_000_003, 20_000
+    x, x0 = _inputs(n, 500, 0.01)
+    tx, tx0 = torch.from_numpy(x).to(dev), torch.from_numpy(x0).to(dev)
+    outs = []
+    for hint in (False, True):
+        ws = codec.Workspace(dev)
+        for _ in range(2):  # the second call takes the prior window when hint is set
+            base = torch.empty(n, device=dev)
+            i1, v1 = codec.topk_encode(tx, k, x0=tx0, workspace=ws, hint=hint, keep_x=True,
+                                       fold_base=(base, [0.25, 0.25], 0.5))
+            i2, v2 = codec.topk_encode(tx, k, x0=tx0, workspace=ws, hint=hint, val_fp16=True)
+        assert _ctrl(ws)[_HINTED] == (1 if hint else 0)
+        outs.append([t.cpu().numpy().copy() for t in (i1, v1, base, i2, v2)])
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8))

@@ -28,12 +28,15 @@ for n in (11_000_000, 16_777_216):
                          idx=torch.empty(k, dtype=torch.int32, device=dev),
                          val=torch.empty(k, device=dev), out=torch.empty(n, device=dev)))
     st = torch.cuda.Stream(dev)
-    res = [bench.product_one_node(sets, n, k, st, codec.Workspace(dev), 120) for _ in range(3)]
+    flags = dict(hint=os.environ.get("AB_HINT", "1") != "0",
+                 keep_x=os.environ.get("AB_KEEP_X", "1") != "0")
+    res = [bench.product_one_node(sets, n, k, st, codec.Workspace(dev), 120, **flags)
+           for _ in range(3)]
     best = {}
     for key in ("1_payload", "3_payload", "1_payload_foldbase", "3_payload_foldbase"):
         rs = sorted(res, key=lambda r: r[key]["step_us"])
         best[key] = rs[1][key]  # the median of three
-    env = {kk: v for kk, v in os.environ.items() if kk.startswith("DPZ_")}
+    env = {kk: v for kk, v in os.environ.items() if kk.startswith(("DPZ_", "AB_"))}
     print(json.dumps({"n": n, "env": env, **best, "fell_back": any(r["fell_back"] for r in res)}),
           flush=True)
     del sets
