@@ -145,7 +145,7 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     value.  Every timed encode's sampled-path status is OR-ed into its workspace's sticky word
     and checked after the loop (fell_back)."""
     from decentralizepy_amd import codec
-    from decentralizepy_amd._lib import DPZ_BATCH_DECODE, DPZ_BATCH_ENCODE
+    from decentralizepy_amd._lib import DPZ_BATCH_DECODE, DPZ_BATCH_ENCODE, DPZ_BATCH_HINT
     k = round(alpha * n)
     per_set = 4 * n * 4 + 8 * k          # x, x0, counter, out + payload
     R = rotate or max(1, math.ceil(2 * L3_BYTES / per_set) + 1)
@@ -167,10 +167,14 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     multi = codec.NodeStepBatch(sets, n, k, s_list, ws_list, decode_src=lambda j: (j - S) % len(sets))
     # one node on one stream decodes a neighbour's payload (the previous state's, encoded in the
     # previous step on the same stream), so its decode is co-scheduled in its encode's launches
-    one = codec.NodeStepBatch(sets, n, k, s_list[:1], ws_list[:1],
+    # its own workspace: a prior window is only taken from an encode of the same grid (the
+    # S-codec batch runs the shared filter grid, DPZ_TOPK_SHARED)
+    one = codec.NodeStepBatch(sets, n, k, s_list[:1], [codec.Workspace(dev)],
                               decode_src=lambda j: (j - 1) % len(sets))
 
-    def run_steps(batch, count, what=DPZ_BATCH_ENCODE | DPZ_BATCH_DECODE):
+    # every encode takes its key window from the previous encode on its stream's workspace
+    # (DPZ_BATCH_HINT: a node's previous round, as PartialModel runs it; no sample launch)
+    def run_steps(batch, count, what=DPZ_BATCH_ENCODE | DPZ_BATCH_DECODE | DPZ_BATCH_HINT):
         for _ in range(count // R):
             batch.run(what)
         if count % R:
@@ -181,6 +185,7 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     run_steps(one, max(warmup, R))
     torch.cuda.synchronize()
     multi.sticky_status(clear=True)
+    one.sticky_status(clear=True)
 
     def timed_once(batch, count):
         if dist is not None:
@@ -211,7 +216,7 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     spread = []
     s_multi, h_multi = timed(multi, steps)
     s_serial, h_serial = timed(one, steps)
-    status = multi.sticky_status(clear=True)  # every timed encode of both loops
+    status = multi.sticky_status(clear=True) | one.sticky_status(clear=True)  # both loops
     fell_back = status != 0
     if dist is not None:
         st = torch.tensor([status], device=dev, dtype=torch.int32)
@@ -225,7 +230,7 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     stream = s_list[0]
     reps = max(2 * R, steps // 2)
 
-    t_enc = _stage_time(one, DPZ_BATCH_ENCODE, reps, run_steps, stream)
+    t_enc = _stage_time(one, DPZ_BATCH_ENCODE | DPZ_BATCH_HINT, reps, run_steps, stream)
     t_dec = _stage_time(one, DPZ_BATCH_DECODE, reps, run_steps, stream)
     # per-kernel device time: the library brackets every launch with a HIP event pair on the
     # stream it launches on.  A GPU-side spin first lets the host queue all `reps` steps, so the
@@ -247,8 +252,8 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
         kernels["fold"]["launches_per_step"] = 0.0 if fused_copy() else 1.0
     b_enc = 8 * n + 8 * k + 8 * k      # read x, x0; write idx, val; counter[idx] += 1 (r+w)
     b_dec = 8 * n + 8 * k              # read local, payload; write out
-    fell_back |= multi.sticky_status(clear=True) != 0
-    product = product_one_node(sets, n, k, stream, ws_list[0], max(2 * R, min(steps, 200)))
+    fell_back |= (multi.sticky_status(clear=True) | one.sticky_status(clear=True)) != 0
+    product = product_one_node(sets, n, k, stream, one.workspaces[0], max(2 * R, min(steps, 200)))
     fell_back |= product["fell_back"]
     return dict(n=n, k=k, s_step=s_step, s_multi=s_multi, s_serial=s_serial, s_host=s_host,
                 mode=mode, streams=S, fell_back=fell_back, t_enc=t_enc, t_dec=t_dec,
@@ -720,11 +725,14 @@ def main():
                 "parallelism": (f"{world} GPU(s) x {r['streams']} concurrent node codecs (one "
                                 f"stream each), no collective" if r["mode"] == "multi" else
                                 f"{world} GPU(s) x 1 node codec, no collective"),
-                "launch": ("native batched enqueue (dpz_encode_replace_batch); step i = encode "
+                "launch": ("native batched enqueue (dpz_encode_replace_batch, DPZ_BATCH_HINT: "
+                           "each encode's key window from the previous encode's exact threshold "
+                           "on its stream's workspace, no sample launch); step i = encode "
                            f"of node state i with the replace decode of state i - {r['streams']}'s "
                            f"payload over its x fused in, on stream i % {r['streams']}"
                            if r["mode"] == "multi" else
-                           "native batched enqueue (dpz_encode_replace_batch), one stream; "
+                           "native batched enqueue (dpz_encode_replace_batch, DPZ_BATCH_HINT), "
+                           "one stream; "
                            "step i = encode of node state i with the replace decode of state "
                            "i - 1's payload over state i's x fused into the encoder's launches "
                            "(filter writes the copy of x, select scatters the entries)"),

@@ -36,6 +36,8 @@ DPZ_FOLD_ALSO_LOCAL = 0x20
 DPZ_FOLD_BASE_READY = 0x40
 DPZ_BATCH_ENCODE = 0x1
 DPZ_BATCH_DECODE = 0x2
+DPZ_BATCH_HINT = 0x4
+DPZ_BATCH_HINT_ALL = 0x8
 DPZ_EW_SUB = 1
 DPZ_EW_ADD = 2
 DPZ_EW_CHOCO = 3

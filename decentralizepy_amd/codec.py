@@ -370,7 +370,13 @@ class NodeStepBatch:
         self._keep = (nodes, wbufs, dbufs, streams)
 
     def run(self, what=_lib.DPZ_BATCH_ENCODE | _lib.DPZ_BATCH_DECODE, m=None):
+        """``what`` with DPZ_BATCH_HINT: the encodes take the prior window (DPZ_TOPK_HINT) —
+        after this batch's first encoding run every encode, the first on each stream too."""
         m = self.m if m is None else int(m)
+        if what & _lib.DPZ_BATCH_HINT and what & _lib.DPZ_BATCH_ENCODE:
+            if getattr(self, "_primed", False):
+                what = (what & ~_lib.DPZ_BATCH_HINT) | _lib.DPZ_BATCH_HINT_ALL
+            self._primed = True
         rc = _lib.lib().dpz_encode_replace_batch(
             m, int(what), self._x, self._x0, self.n, self.k, self._cnt, self._idx, self._val,
             self._rl, self._ri, self._rv, self.k, self._ro, self._ws, self._ws_bytes, self._dws,

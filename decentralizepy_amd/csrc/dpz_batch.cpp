@@ -32,6 +32,14 @@ extern "C" int dpz_topk_encode_batch(int m, const float* const* x, const float* 
   return DPZ_OK;
 }
 
+namespace dpz {
+// dpz_fold.hip: every node's fold in one launch per FW_BATCH nodes (1 = the batch does not qualify)
+int fold_batch_walk(int m, const float* const* local, float* const* out, int64_t n,
+                    const int* n_payloads, const int32_t* const* idx, const float* const* vals,
+                    const int64_t* k, const float* w, const float* w_self, int flags,
+                    hipStream_t st);
+}  // namespace dpz
+
 extern "C" int dpz_decode_average_batch(int m, const float* const* local, float* const* out,
                                         int64_t n, const int* n_payloads,
                                         const int32_t* const* idx, const float* const* vals,
@@ -39,6 +47,15 @@ extern "C" int dpz_decode_average_batch(int m, const float* const* local, float*
                                         int flags, void* const* ws, size_t ws_bytes,
                                         int n_streams, const dpz_stream_t* streams) {
   if (m < 0 || n_streams < 1 || !local || !out || !n_payloads || !ws || !streams) return DPZ_ERR_ARG;
+  for (int j = 0; j < m; ++j)
+    if (n_payloads[j] < 0) return DPZ_ERR_ARG;
+  // a round of plain few-payload folds (the C4 gossip round): one walk launch per 22 nodes on
+  // streams[0] instead of one per node (dpz_fold.hip fold_batch_walk)
+  {
+    const int rc = dpz::fold_batch_walk(m, local, out, n, n_payloads, idx, vals, k, w, w_self,
+                                        flags, static_cast<hipStream_t>(streams[0]));
+    if (rc != 1) return rc;
+  }
   int64_t off = 0;
   for (int j = 0; j < m; ++j) {
     const int q = j % n_streams;
@@ -65,7 +82,7 @@ extern "C" int dpz_encode_replace_batch(int m, int what, const float* const* x,
                                         size_t ws_bytes, void* const* dws, size_t dws_bytes,
                                         int n_streams, const dpz_stream_t* streams) {
   if (m < 0 || n_streams < 1 || !streams || !(what & (DPZ_BATCH_ENCODE | DPZ_BATCH_DECODE)) ||
-      (what & ~(DPZ_BATCH_ENCODE | DPZ_BATCH_DECODE)))
+      (what & ~(DPZ_BATCH_ENCODE | DPZ_BATCH_DECODE | DPZ_BATCH_HINT | DPZ_BATCH_HINT_ALL)))
     return DPZ_ERR_ARG;
   if ((what & DPZ_BATCH_ENCODE) && (!x || !idx_out || !val_out || !ws)) return DPZ_ERR_ARG;
   if ((what & DPZ_BATCH_DECODE) && (!r_local || !r_idx || !r_val || !r_out || !dws))
@@ -84,11 +101,14 @@ extern "C" int dpz_encode_replace_batch(int m, int what, const float* const* x,
   const bool cosched = cs_env >= 0 ? cs_env != 0 : n_streams == 1;
   for (int j = 0; j < m; ++j) {
     const int q = j % n_streams;
+    // the prior window: every encode with HINT_ALL, all but each stream's first with HINT
+    const int hint = ((what & DPZ_BATCH_HINT_ALL) || ((what & DPZ_BATCH_HINT) && j >= n_streams))
+                         ? DPZ_TOPK_HINT : 0;
     const bool both = (what & DPZ_BATCH_ENCODE) && (what & DPZ_BATCH_DECODE) &&
                       r_idx[j] != idx_out[j] && r_val[j] != val_out[j];
     const bool fused = both && r_local[j] == x[j] && cs_env != 0;
     if (both && (cosched || fused)) {
-      const int fl = DPZ_TOPK_ASYNC | (n_streams > 1 ? DPZ_TOPK_SHARED : 0);
+      const int fl = DPZ_TOPK_ASYNC | (n_streams > 1 ? DPZ_TOPK_SHARED : 0) | hint;
       int rc = dpz_topk_encode_replace(x[j], x0 ? x0[j] : nullptr, nullptr, DPZ_ACC_NONE, x[j], n,
                                        k, idx_out[j], val_out[j], counter ? counter[j] : nullptr,
                                        ws[q], ws_bytes, fl, r_local[j], r_idx[j],
@@ -98,7 +118,7 @@ extern "C" int dpz_encode_replace_batch(int m, int what, const float* const* x,
     }
     if (what & DPZ_BATCH_ENCODE) {
       // several streams: several codecs share the GPU, the smaller filter grid (DPZ_TOPK_SHARED)
-      const int fl = DPZ_TOPK_ASYNC | (n_streams > 1 ? DPZ_TOPK_SHARED : 0);
+      const int fl = DPZ_TOPK_ASYNC | (n_streams > 1 ? DPZ_TOPK_SHARED : 0) | hint;
       int rc = dpz_topk_encode(x[j], x0 ? x0[j] : nullptr, nullptr, DPZ_ACC_NONE, x[j], n, k,
                                idx_out[j], val_out[j], counter ? counter[j] : nullptr, ws[q],
                                ws_bytes, fl, streams[q]);

@@ -1084,23 +1084,15 @@ __device__ __forceinline__ int32_t fw_start_cursors(int np, int32_t e0, int lane
 // flight while all of this tile's payloads fold.  NS = 4: the payloads' pointers, sizes, weights
 // and cursors in scalar registers (a generic path holds them one per lane and reads them back
 // with readlane; measured slower than fold_walk_groups_kernel at 16 payloads, which is used there).
-template <bool VEC, int EPL, int NS>
-__global__ void __launch_bounds__(256, FW_MINB_1(EPL)) fold_walk_kernel(FoldArgs a, int64_t tpw) {
+// One wave's run of tiles [t0, t1) of one fold (fold_walk_kernel; fold_walk_batch_kernel runs
+// several folds' runs back to back).  wv / wt: the wave's LDS row; seq: the wave's tile sequence
+// number, carried across runs so a stale tag of an earlier run never matches.
+template <bool VEC, int EPL, int NS, class FA>
+__device__ __forceinline__ void fold_walk_run(const FA& a, int64_t t0, int64_t t1, float* wv,
+                                              uint32_t* wt, int lane, uint32_t& seq) {
   constexpr bool ONE = NS <= 4;
   constexpr int TE = 64 * EPL;
-  __shared__ float s_val[FW_WAVES][TE];
-  __shared__ uint32_t s_tag[FW_WAVES][TE];
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  float* wv = s_val[wid];
-  uint32_t* wt = s_tag[wid];
-#pragma unroll
-  for (int e = 0; e < EPL; ++e) wt[lane + 64 * e] = 0xFFFFFFFFu;
   const int64_t n = a.n;
-  const int64_t ntl = (n + TE - 1) / TE;
-  const int64_t gw = (int64_t)blockIdx.x * FW_WAVES + wid;
-  const int64_t t0 = gw * tpw;
-  const int64_t t1 = (t0 + tpw < ntl) ? t0 + tpw : ntl;
-  if (t0 >= t1) return;  // no block barrier anywhere: a wave may leave alone
   const int np = a.np;
   const int lp = lane < np && lane < FOLD_MAXP ? lane : 0;
   const int32_t kl = lane < np ? (int32_t)a.p[lp].k : 0;
@@ -1162,7 +1154,6 @@ __global__ void __launch_bounds__(256, FW_MINB_1(EPL)) fold_walk_kernel(FoldArgs
   };
 #pragma unroll
   for (int p = 0; p < NS; ++p) load_window(p, wi[p], wvv[p]);
-  uint32_t seq = 0;
   auto tile_body = [&](int64_t tile, auto guard) {
     constexpr bool GUARD = decltype(guard)::value;
     const int64_t tlo = tile * TE;
@@ -1270,6 +1261,90 @@ __global__ void __launch_bounds__(256, FW_MINB_1(EPL)) fold_walk_kernel(FoldArgs
   const int64_t tf = t1 < tfull ? t1 : (tfull > t0 ? tfull : t0);
   for (int64_t tile = t0; tile < tf; ++tile) tile_body(tile, std::false_type{});
   if (tf < t1) tile_body(tf, std::true_type{});  // the global last tile, ragged
+}
+
+template <bool VEC, int EPL, int NS>
+__global__ void __launch_bounds__(256, FW_MINB_1(EPL)) fold_walk_kernel(FoldArgs a, int64_t tpw) {
+  constexpr int TE = 64 * EPL;
+  __shared__ float s_val[FW_WAVES][TE];
+  __shared__ uint32_t s_tag[FW_WAVES][TE];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float* wv = s_val[wid];
+  uint32_t* wt = s_tag[wid];
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) wt[lane + 64 * e] = 0xFFFFFFFFu;
+  const int64_t ntl = (a.n + TE - 1) / TE;
+  const int64_t gw = (int64_t)blockIdx.x * FW_WAVES + wid;
+  const int64_t t0 = gw * tpw;
+  const int64_t t1 = (t0 + tpw < ntl) ? t0 + tpw : ntl;
+  if (t0 >= t1) return;  // no block barrier anywhere: a wave may leave alone
+  uint32_t seq = 0;
+  fold_walk_run<VEC, EPL, NS>(a, t0, t1, wv, wt, lane, seq);
+}
+
+// A node's plain Metro-Hastings walk fold of <= 4 sparse payloads (fold_walk_batch_kernel's
+// kernel-argument table entry) and the view fold_walk_run reads it through.
+struct FoldNode {
+  const float* local;
+  float* out;
+  float* out2;
+  int np;
+  float w_self;
+  FoldPayload p[4];
+};
+constexpr int FW_BATCH = 22;  // nodes per launch: the table stays within the 4 KB of arguments
+struct FoldNodeBatch {
+  FoldNode nd[FW_BATCH];
+  int64_t n;
+  int m;
+  int add_self;
+};
+static_assert(sizeof(FoldNodeBatch) <= 3584, "kernel arguments");
+struct FoldNodeView {
+  const float* local;
+  float* out;
+  float* out2;
+  int64_t n;
+  int np;
+  int add_self;
+  int zero_base;
+  float w_self;
+  const FoldPayload* p;
+};
+
+// ONE launch for the folds of up to FW_BATCH nodes of a gossip round (dpz_decode_average_batch:
+// every node's fold a plain Metro-Hastings walk of <= 4 sparse payloads over the same n): the
+// folds' tiles form one range [0, m * ntl) that the persistent grid's waves split into contiguous
+// runs, a run crossing a node boundary continuing in the next node's fold.  One launch instead of
+// m: the folds' start-up latencies (cursor searches, first windows) overlap and no launch drains
+// alone (a full-GPU persistent grid per node serialises on a few streams).
+template <bool VEC, int EPL>
+__global__ void __launch_bounds__(256, FW_MINB_1(EPL)) fold_walk_batch_kernel(FoldNodeBatch b,
+                                                                              int64_t tpw) {
+  constexpr int TE = 64 * EPL;
+  const int64_t ntl = (b.n + TE - 1) / TE;
+  const int64_t m = b.m;
+  __shared__ float s_val[FW_WAVES][TE];
+  __shared__ uint32_t s_tag[FW_WAVES][TE];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float* wv = s_val[wid];
+  uint32_t* wt = s_tag[wid];
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) wt[lane + 64 * e] = 0xFFFFFFFFu;
+  const int64_t gw = (int64_t)blockIdx.x * FW_WAVES + fw_uni(wid);
+  int64_t g = gw * tpw;
+  const int64_t gend = m * ntl;
+  const int64_t g1 = g + tpw < gend ? g + tpw : gend;
+  uint32_t seq = 0;
+  while (g < g1) {
+    const int64_t node = g / ntl;
+    const int64_t lt0 = g - node * ntl;
+    const int64_t lt1 = lt0 + (g1 - g) < ntl ? lt0 + (g1 - g) : ntl;
+    const FoldNode& nd = b.nd[node];
+    const FoldNodeView v{nd.local, nd.out, nd.out2, b.n, nd.np, b.add_self, 0, nd.w_self, nd.p};
+    fold_walk_run<VEC, EPL, 4>(v, lt0, lt1, wv, wt, lane, seq);
+    g += lt1 - lt0;
+  }
 }
 
 constexpr int FW_G = 4;  // payloads per group: the windows of one group are in registers
@@ -1909,6 +1984,90 @@ static int launch_fold_patch(FoldArgs fa, int32_t* starts, hipStream_t st) {
             fold_offsets_kernel<FOLD_TILE_SHIFT><<<og, 256, 0, st>>>(fa, starts, fa.ntiles));
   fa.starts = starts;
   DPZ_TIMED(DPZ_KT_FOLD, st, fold_patch_kernel<<<(unsigned)fa.ntiles, 256, 0, st>>>(fa, FOLD_TILE));
+  return DPZ_OK;
+}
+
+template <bool VEC, int EPL>
+static int launch_walk_batch_t(const FoldNodeBatch& b, hipStream_t st) {
+  static int per = 0, cus = 0;
+  if (per == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per, reinterpret_cast<const void*>(fold_walk_batch_kernel<VEC, EPL>), 256, 0) !=
+            hipSuccess || per < 1)
+      per = 1;
+  }
+  constexpr int TE = 64 * EPL;
+  const int64_t tiles = (int64_t)b.m * ((b.n + TE - 1) / TE);
+  int64_t blocks = (int64_t)cus * per;
+  const int64_t need = (tiles + FW_WAVES - 1) / FW_WAVES;
+  if (blocks > need) blocks = need;
+  if (blocks < 1) blocks = 1;
+  const int64_t tpw = (tiles + blocks * FW_WAVES - 1) / (blocks * FW_WAVES);
+  DPZ_TIMED(DPZ_KT_FOLD, st, (fold_walk_batch_kernel<VEC, EPL><<<(unsigned)blocks, 256, 0, st>>>(b, tpw)));
+  return DPZ_OK;
+}
+
+// dpz_decode_average_batch's one-launch path: every node's fold a plain Metro-Hastings walk (1..4
+// sparse payloads, a fresh total, DPZ_FOLD_SELF / DPZ_FOLD_ALSO_LOCAL only) over 16-byte aligned
+// rows of the same n.  Returns 1 (nothing enqueued) when the batch does not qualify.
+int fold_batch_walk(int m, const float* const* local, float* const* out, int64_t n,
+                    const int* n_payloads, const int32_t* const* idx, const float* const* vals,
+                    const int64_t* k, const float* w, const float* w_self, int flags,
+                    hipStream_t st) {
+  if (DPZ_KNOB_INT(FOLD_BATCH, 1) == 0) return 1;  // diagnostic build: per-node launches (A/B)
+  if (m < 2 || (flags & ~(DPZ_FOLD_SELF | DPZ_FOLD_ALSO_LOCAL)) || !w || !idx) return 1;
+  if (n < 1024 || n >= (int64_t(1) << 31) - 1024) return 1;
+  double dens = 0.0;
+  int64_t off = 0;
+  for (int j = 0; j < m; ++j) {
+    const int np = n_payloads[j];
+    if (np < 1 || np > 4 || !local[j] || !out[j] || local[j] == out[j]) return 1;
+    if (((reinterpret_cast<uintptr_t>(local[j]) | reinterpret_cast<uintptr_t>(out[j])) & 15u) != 0)
+      return 1;
+    for (int i = 0; i < np; ++i) {
+      const int64_t kk = k[off + i];
+      if (!idx[off + i] || !vals[off + i] || kk < 1 || kk > n) return 1;  // sparse, non-empty
+      if ((double)kk / (double)n > dens) dens = (double)kk / (double)n;
+    }
+    off += np;
+  }
+  // the walk's tile size for the densest payload (launch_walk, <= 4 payloads)
+  const int e = dens <= 0.055 ? 16 : (dens <= 0.105 ? 8 : (dens <= 0.21 ? 4 : 2));
+  off = 0;
+  for (int j0 = 0; j0 < m; j0 += FW_BATCH) {
+    FoldNodeBatch b{};
+    b.n = n;
+    b.m = (m - j0) < FW_BATCH ? (m - j0) : FW_BATCH;
+    b.add_self = (flags & DPZ_FOLD_SELF) ? 1 : 0;
+    for (int j = 0; j < b.m; ++j) {
+      FoldNode& nd = b.nd[j];
+      const int jj = j0 + j;
+      nd.local = local[jj];
+      nd.out = out[jj];
+      nd.out2 = (flags & DPZ_FOLD_ALSO_LOCAL) ? const_cast<float*>(local[jj]) : nullptr;
+      nd.np = n_payloads[jj];
+      nd.w_self = w_self ? w_self[jj] : 0.0f;
+      for (int i = 0; i < nd.np; ++i) {
+        nd.p[i].idx = idx[off + i];
+        nd.p[i].val = vals[off + i];
+        nd.p[i].k = k[off + i];
+        nd.p[i].w = w[off + i];
+      }
+      off += nd.np;
+    }
+    int rc;
+    switch (e) {
+      case 16: rc = launch_walk_batch_t<true, 16>(b, st); break;
+      case 8: rc = launch_walk_batch_t<true, 8>(b, st); break;
+      case 4: rc = launch_walk_batch_t<true, 4>(b, st); break;
+      default: rc = launch_walk_batch_t<true, 2>(b, st); break;
+    }
+    if (rc != DPZ_OK) return rc;
+  }
   return DPZ_OK;
 }
 

@@ -1493,9 +1493,9 @@ static int run_sampled_t(const EncodeArgs& a, const WsLayout& L, int phases) {
   const int pipe = (int)DPZ_KNOB_INT(FILTER_PIPE, 1);
   const bool add_only = a.acc_mode == DPZ_ACC_ADD && !a.x0;
   const bool piped = VEC && (a.acc_mode == DPZ_ACC_NONE || add_only) && pipe > 0;
-  // a prior-round window replaces the sample launch (pipelined filter only; the job-carrying
-  // co-scheduled decode splits its blocks over the sample launch, so it keeps it)
-  const uint32_t hsig = (piped && !a.job) ? a.hint_sig : 0u;
+  // a prior-round window replaces the sample launch (pipelined filter only; a co-scheduled
+  // decode with blocks in the sample launch keeps it — the fused one rides in compact only)
+  const uint32_t hsig = (piped && (!a.job || pb[0] == 0)) ? a.hint_sig : 0u;
   const uint32_t sig = hint_signature(a.n, a.k, a.shared, a.acc_mode, a.x0 != nullptr);
   if (phases & 1) {
     if (!hsig)

@@ -310,6 +310,13 @@ int dpz_decode_average_batch(int m, const float* const* local, float* const* out
  * workspace's sticky status word (dpz_topk_sticky_status), never silently.                     */
 #define DPZ_BATCH_ENCODE 0x1
 #define DPZ_BATCH_DECODE 0x2
+/* with DPZ_BATCH_ENCODE: the encodes pass DPZ_TOPK_HINT — each takes its key window from the
+ * previous encode on its stream's workspace (another node of the same round or the node's own
+ * previous round: the same change distribution), a miss recorded like any other.  HINT: every
+ * encode but the first on each stream (fresh workspaces hold no prior); HINT_ALL: every encode
+ * (the workspaces already hold one of this n, k from an earlier call).                        */
+#define DPZ_BATCH_HINT 0x4
+#define DPZ_BATCH_HINT_ALL 0x8
 int dpz_encode_replace_batch(int m, int what, const float* const* x, const float* const* x0,
                              int64_t n, int64_t k, int32_t* const* counter,
                              int32_t* const* idx_out, float* const* val_out,

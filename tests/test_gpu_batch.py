@@ -24,8 +24,16 @@ def _node(dev, n, k, seed):
                 out=torch.empty(n, dtype=torch.float32, device=dev))
 
 
-@pytest.mark.parametrize("streams", [1, 2, 3])
-def test_node_step_batch_matches_oracle(dev, streams):
+def _what(hint):
+    from decentralizepy_amd._lib import DPZ_BATCH_DECODE, DPZ_BATCH_ENCODE, DPZ_BATCH_HINT
+    return DPZ_BATCH_ENCODE | DPZ_BATCH_DECODE | (DPZ_BATCH_HINT if hint else 0)
+
+
+@pytest.mark.parametrize("streams,hint", [(1, False), (2, False), (3, False), (1, True),
+                                          (3, True)])
+def test_node_step_batch_matches_oracle(dev, streams, hint):
+    """hint: each encode takes its window from the previous encode on its stream's workspace
+    (DPZ_BATCH_HINT), no sample launch after the first; same results."""
     from decentralizepy_amd import codec
     n, k, m = 1_000_003, 10_000, 5
     nodes = [_node(dev, n, k, 40 + j) for j in range(m)]
@@ -36,9 +44,11 @@ def test_node_step_batch_matches_oracle(dev, streams):
     b = codec.NodeStepBatch(nodes, n, k, ss, ws)
     b.sticky_status(clear=True)
     for _ in range(2):  # twice: counters accumulate, workspaces are reused
-        b.run()
+        b.run(_what(hint))
     torch.cuda.synchronize()
     assert b.sticky_status() == 0
+    if hint:  # the last encode on every workspace ran without a sample launch (ctrl.hinted)
+        assert all(int(w.buf[60:64].view(torch.int32).item()) == 1 for w in ws)
     for j, d in enumerate(nodes):
         x = d["x"].cpu().numpy()
         x0 = d["x0"].cpu().numpy()
@@ -52,8 +62,8 @@ def test_node_step_batch_matches_oracle(dev, streams):
         np.testing.assert_array_equal(_bits(d["out"].cpu().numpy()), _bits(ref))
 
 
-@pytest.mark.parametrize("streams", [1, 3])
-def test_node_step_batch_neighbour_decode(dev, streams):
+@pytest.mark.parametrize("streams,hint", [(1, False), (3, False), (1, True), (3, True)])
+def test_node_step_batch_neighbour_decode(dev, streams, hint):
     """Node j decoding node j - S's payload over its own x (S streams): the decode is fused
     into the encode (the filter writes the copy of x, select scatters the entries;
     dpz_encode_replace_batch) and still equals encode + replace."""
@@ -66,7 +76,7 @@ def test_node_step_batch_neighbour_decode(dev, streams):
                             decode_src=lambda j: (j - S) % m)
     b.sticky_status(clear=True)
     for _ in range(2):  # node 0 reads node m-1's payload of the previous run
-        b.run()
+        b.run(_what(hint))
     torch.cuda.synchronize()
     assert b.sticky_status() == 0
     ref = []
