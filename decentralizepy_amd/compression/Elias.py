@@ -25,6 +25,18 @@ def parse_trailer(buf):
     return nbits, first
 
 
+def _grown(ws, name, n, kw):
+    """A uint8 buffer of at least n bytes kept on the workspace object under ``name``; grown
+    geometrically (payload sizes vary round to round: JWINS draws alpha per round), so pinned
+    allocations stay rare."""
+    buf = getattr(ws, name, None)
+    if buf is None or buf.numel() < n:
+        size = max(n, 4096, 0 if buf is None else min(2 * buf.numel(), n + (n >> 1)))
+        buf = torch.empty(size, dtype=torch.uint8, **kw)
+        setattr(ws, name, buf)
+    return buf
+
+
 class Elias(Compression):
     """Elias-gamma coding of sorted index gaps."""
 
@@ -46,7 +58,11 @@ class Elias(Compression):
         """Strictly increasing device int32 indices -> host uint8 stream."""
         self._dev(idx_dev.device)
         enc = codec.elias_encode(idx_dev, workspace=self._ws)
-        return enc.cpu().numpy()
+        # down through a kept pinned buffer, then one host copy (no pageable transfer)
+        pin = _grown(self._ws, "elias_out_pin", enc.numel(), dict(pin_memory=True))[:enc.numel()]
+        pin.copy_(enc, non_blocking=True)
+        torch.cuda.current_stream(enc.device).synchronize()
+        return pin.numpy().copy()
 
     def decompress_device(self, buf, dtype=torch.int32, device=None):
         """Host stream -> device index tensor (int32 for the fold kernels, or int64)."""
@@ -58,12 +74,8 @@ class Elias(Compression):
         # up through a pinned buffer into a device buffer, both kept with the compressor (the
         # decode synchronizes before it returns, so both are free again for the next call)
         ws = self._ws
-        pin = getattr(ws, "elias_pin", None)
-        if pin is None or pin.numel() < need:
-            pin = ws.elias_pin = torch.empty(max(need, 4096), dtype=torch.uint8, pin_memory=True)
-        dbuf = getattr(ws, "elias_dev", None)
-        if dbuf is None or dbuf.numel() < need:
-            dbuf = ws.elias_dev = torch.empty(max(need, 4096), dtype=torch.uint8, device=dev)
+        pin = _grown(ws, "elias_pin", need, dict(pin_memory=True))
+        dbuf = _grown(ws, "elias_dev", need, dict(device=dev))
         pn = pin.numpy()
         pn[:nbytes] = b
         pn[nbytes:need] = 0

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from .. import codec
-from .Elias import Elias
+from .Elias import Elias, _grown
 
 _MAGIC = 0x5A465044
 _BLOCK = 256
@@ -34,20 +34,36 @@ class EliasFpzip(Elias):
     precision = 0
 
     def compress_float_device(self, vals):
-        """Device fp32 values -> host stream bytes (np.uint8)."""
+        """Device fp32 values -> host stream bytes (np.uint8, owned).  The stream comes down
+        through a pinned buffer kept with the compressor (one DMA, then one host copy): a
+        pageable ``.cpu()`` of a full share's 88 MB stream took 12-16 ms against 1.6 + 7-9.5 ms
+        (tools/diag/d2h_probe.py on MI355X)."""
         self._dev(vals.device)
         x = vals.reshape(-1)
         if not x.is_contiguous():
             x = x.contiguous()
-        return codec.fpz_encode(x, self.precision, workspace=self._ws).cpu().numpy()
+        s = codec.fpz_encode(x, self.precision, workspace=self._ws)
+        pin = _grown(self._ws, "fpz_out_pin", s.numel(), dict(pin_memory=True))[:s.numel()]
+        pin.copy_(s, non_blocking=True)
+        torch.cuda.current_stream(s.device).synchronize()
+        return pin.numpy().copy()
 
     def decompress_float_device(self, bytes, device=None):
-        """Host stream bytes -> device fp32 values."""
+        """Host stream bytes -> device fp32 values.  Up through a pinned buffer and into a
+        device buffer, both kept with the compressor (fpz_decode synchronises before it returns,
+        so both are free for the next call): one host copy into page-locked memory and a DMA —
+        a fresh copy of the stream (page faults) plus a pageable transfer had cost ~4 ms per
+        JWINS payload (tools/diag/plugin_breakdown.py)."""
         dev = self._dev(device)
         n, prec = parse_float_header(bytes)
         b = np.frombuffer(memoryview(bytes), dtype=np.uint8)
-        dbuf = torch.from_numpy(b.copy()).to(dev)
-        return codec.fpz_decode(dbuf, n, prec)
+        nb = b.size
+        ws = self._ws
+        pin = _grown(ws, "fpz_pin", nb, dict(pin_memory=True))
+        dbuf = _grown(ws, "fpz_dev", nb, dict(device=dev))
+        pin.numpy()[:nb] = b
+        dbuf[:nb].copy_(pin[:nb], non_blocking=True)
+        return codec.fpz_decode(dbuf[:nb], n, prec)
 
     def compress_float(self, arr):
         x = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float32).reshape(-1))

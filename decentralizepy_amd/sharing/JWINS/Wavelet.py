@@ -128,10 +128,17 @@ class Wavelet(PartialModel):
         return idx, val
 
     def _full_share(self):
-        """alpha >= metadata_cap: all coefficients W(x) (reference Wavelet.py:185-192)."""
+        """alpha >= metadata_cap: all coefficients W(x) (reference Wavelet.py:185-192).  With a
+        device float compressor the coefficients are coded where they are (no D2H of the raw
+        4M bytes and H2D back into the compressor)."""
         m = dict()
-        m["params"] = to_host(self.pre_share_model_transformed, self.staging, "coeffs")
+        wx = self.pre_share_model_transformed
+        dev_codec = self.compress and hasattr(getattr(self, "compressor", None),
+                                              "compress_float_device")
+        m["params"] = None if dev_codec else to_host(wx, self.staging, "coeffs")
         self._zero_accumulation()
+        if dev_codec:
+            return self.compress_data(m, val_dev=wx)
         return self.compress_data(m)
 
     def _message(self, indices, params):
