@@ -413,10 +413,16 @@ def gossip_case(n, alpha, dev, rank, world, dist, rounds, warmup, exchange="allg
     eng.leg_times = None
     k = eng.k
     nsum = sum(len(a) for a in adj)
+    # algorithmic bytes of the round: every node's encode (read x, x0; idx / val out; counter
+    # r+w) and fold (read x and the payloads; the averaged model written as the node's model AND
+    # as its init_model — reference Sharing.py:186-190 load_state_dict, then PartialModel.py:
+    # 340-343 init_model = cat(state): both must hold it for the next round, 12N);
+    # alg_bytes_8n counts the fold's output once (the round-4 convention)
     return dict(n=n, k=k, s_step=s_round, nodes=len(adj), edges=nsum // 2, legs_ms=legs,
                 rs_group=getattr(eng, "rs_group", None),
                 value=len(adj) * 4 * n / s_round / 2 ** 30,
-                alg_bytes=len(adj) * (8 * n + 16 * k) + len(adj) * 8 * n + nsum * 8 * k)
+                alg_bytes=len(adj) * (8 * n + 16 * k) + len(adj) * 12 * n + nsum * 8 * k,
+                alg_bytes_8n=len(adj) * (8 * n + 16 * k) + len(adj) * 8 * n + nsum * 8 * k)
 
 
 def fused_copy():
@@ -589,6 +595,11 @@ def main():
                                           "RCCL all-gather of the payloads per round"},
                 "round_alg_bytes": r["alg_bytes"],
                 "round_frac_of_hbm_peak": round(r["alg_bytes"] / r["s_step"] / 1e9 / HBM_PEAK_GBS / world, 4),
+                "round_frac_of_hbm_peak_fold_8n": round(r["alg_bytes_8n"] / r["s_step"] / 1e9
+                                                        / HBM_PEAK_GBS / world, 4),
+                "alg_bytes_note": "fold 12N: the averaged model is written as the model and as "
+                                  "init_model (Sharing.py:186-190, PartialModel.py:340-343); "
+                                  "*_fold_8n counts it once (round-4 convention)",
                 "legs_ms": r["legs_ms"],
                 "reduce_scatter_mode": {
                     "note": "the over-HBM exchange forced (exchange='reduce_scatter'): payloads "
@@ -828,7 +839,12 @@ def gossip_line(gr, world):
             "legs_ms": gr["legs_ms"],
             "round_alg_bytes": gr["alg_bytes"],
             "round_frac_of_hbm_peak": round(gr["alg_bytes"] / gr["s_step"] / 1e9
-                                            / HBM_PEAK_GBS / world, 4)}
+                                            / HBM_PEAK_GBS / world, 4),
+            "round_frac_of_hbm_peak_fold_8n": round(gr["alg_bytes_8n"] / gr["s_step"] / 1e9
+                                                    / HBM_PEAK_GBS / world, 4),
+            "alg_bytes_note": "fold 12N: the averaged model is written as the model and as "
+                              "init_model (Sharing.py:186-190, PartialModel.py:340-343); "
+                              "*_fold_8n counts it once (round-4 convention)"}
 
 if __name__ == "__main__":
     main()

@@ -12,24 +12,36 @@
 #include "../../include/dpz_codec.h"
 #include "dpz_topk.h"
 
-extern "C" int dpz_topk_encode_batch(int m, const float* const* x, const float* const* x0,
-                                     int64_t n, int64_t k, int32_t* const* counter,
-                                     int32_t* const* idx_out, float* const* val_out,
-                                     void* const* ws, size_t ws_bytes, int n_streams,
-                                     const dpz_stream_t* streams, int32_t* status) {
+extern "C" int dpz_topk_encode_batch_ex(int m, const float* const* x, const float* const* x0,
+                                        int64_t n, int64_t k, int32_t* const* counter,
+                                        int32_t* const* idx_out, float* const* val_out,
+                                        void* const* ws, size_t ws_bytes, int n_streams,
+                                        const dpz_stream_t* streams, int32_t* status, int flags) {
   if (m < 0 || n_streams < 1 || !x || !idx_out || !val_out || !ws || !streams) return DPZ_ERR_ARG;
+  if (flags & ~(DPZ_BATCH_HINT | DPZ_BATCH_HINT_ALL)) return DPZ_ERR_ARG;
   for (int j = 0; j < m; ++j) {
     const int q = j % n_streams;
+    // the prior window: every encode with HINT_ALL, all but each stream's first with HINT
+    const bool hint = (flags & DPZ_BATCH_HINT_ALL) || ((flags & DPZ_BATCH_HINT) && j >= n_streams);
     // the sampled path's compact writes node j's final status word to status[j] itself (a
     // separate 4-byte device copy per node cost a blit launch of ~8 us on its stream)
     int rc = dpz::topk_encode_status(x[j], x0 ? x0[j] : nullptr, nullptr, DPZ_ACC_NONE, x[j],
                                      n, k, idx_out[j],
                                      val_out[j], counter ? counter[j] : nullptr, ws[q], ws_bytes,
                                      static_cast<hipStream_t>(streams[q]),
-                                     status ? status + j : nullptr, n_streams > 1);
+                                     status ? status + j : nullptr, n_streams > 1, false, hint);
     if (rc != DPZ_OK) return rc;
   }
   return DPZ_OK;
+}
+
+extern "C" int dpz_topk_encode_batch(int m, const float* const* x, const float* const* x0,
+                                     int64_t n, int64_t k, int32_t* const* counter,
+                                     int32_t* const* idx_out, float* const* val_out,
+                                     void* const* ws, size_t ws_bytes, int n_streams,
+                                     const dpz_stream_t* streams, int32_t* status) {
+  return dpz_topk_encode_batch_ex(m, x, x0, n, k, counter, idx_out, val_out, ws, ws_bytes,
+                                  n_streams, streams, status, 0);
 }
 
 namespace dpz {

@@ -339,7 +339,7 @@ int topk_encode_status(const float* x, const float* x0, float* acc, int acc_mode
                        const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
                        float* val_out, int32_t* counter, void* ws, size_t ws_bytes,
                        hipStream_t st, int32_t* status_out, bool shared = false,
-                       bool val_fp16 = false);
+                       bool val_fp16 = false, bool hint = false);
 static inline bool use_sampled(int64_t n, int64_t k) {
   return n >= (1 << 18) && k >= 1 && k <= n / 2;
 }

@@ -125,7 +125,8 @@ namespace dpz {
 int topk_encode_status(const float* x, const float* x0, float* acc, int acc_mode,
                        const float* vals_src, int64_t n, int64_t k, int32_t* idx_out,
                        float* val_out, int32_t* counter, void* ws, size_t ws_bytes,
-                       hipStream_t st, int32_t* status_out, bool shared, bool val_fp16) {
+                       hipStream_t st, int32_t* status_out, bool shared, bool val_fp16,
+                       bool hint) {
   EncodeArgs a{x, x0, acc, acc_mode, vals_src, n, k, idx_out, val_out, counter,
                static_cast<char*>(ws), st};
   a.shared = shared;
@@ -139,7 +140,8 @@ int topk_encode_status(const float* x, const float* x0, float* acc, int acc_mode
     return DPZ_OK;
   }
   a.status_out = status_out;
-  return dpz_topk_dispatch(a, DPZ_TOPK_ASYNC | (val_fp16 ? DPZ_TOPK_VAL_FP16 : 0));
+  return dpz_topk_dispatch(a, DPZ_TOPK_ASYNC | (val_fp16 ? DPZ_TOPK_VAL_FP16 : 0) |
+                                  (hint ? DPZ_TOPK_HINT : 0));
 }
 }  // namespace dpz
 

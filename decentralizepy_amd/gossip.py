@@ -196,13 +196,18 @@ class GossipRound:
         for st in self.streams:
             st.wait_stream(cur)
         # one native call enqueues every node's encode (node j on stream j % S) and copies each
-        # node's sampled-path status word to self.status[j]
-        rc = _lib.lib().dpz_topk_encode_batch(
+        # node's sampled-path status word to self.status[j]; every encode takes its key window
+        # from the previous encode on its stream's workspace (DPZ_BATCH_HINT: the nodes' change
+        # distributions are alike; a miss is re-run below), from the second round on the first
+        # one on each stream too (HINT_ALL)
+        hint = _lib.DPZ_BATCH_HINT_ALL if getattr(self, "_primed", False) else _lib.DPZ_BATCH_HINT
+        self._primed = True
+        rc = _lib.lib().dpz_topk_encode_batch_ex(
             m, self._ptrs(self.x[:m]), self._ptrs(self.x0[:m]), self.N, self.k,
             self._ptrs(self.counter[:m]), self._ptrs(self.send_idx[:m]),
             self._ptrs(self.send_val[:m]), wsp, ws_bytes, len(self.streams), streams,
-            self.status.data_ptr())
-        _lib.check(rc, "dpz_topk_encode_batch")
+            self.status.data_ptr(), hint)
+        _lib.check(rc, "dpz_topk_encode_batch_ex")
         for st in self.streams:
             cur.wait_stream(st)
         # a sampled-path miss (rare) re-runs that node's selection exactly

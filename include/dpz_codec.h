@@ -293,6 +293,13 @@ int dpz_topk_encode_batch(int m, const float* const* x, const float* const* x0, 
                           int64_t k, int32_t* const* counter, int32_t* const* idx_out,
                           float* const* val_out, void* const* ws, size_t ws_bytes, int n_streams,
                           const dpz_stream_t* streams, int32_t* status);
+/* dpz_topk_encode_batch with batch flags: DPZ_BATCH_HINT / DPZ_BATCH_HINT_ALL (the encodes'
+ * prior window, as in dpz_encode_replace_batch; a miss shows in status[j] like any other).    */
+int dpz_topk_encode_batch_ex(int m, const float* const* x, const float* const* x0, int64_t n,
+                             int64_t k, int32_t* const* counter, int32_t* const* idx_out,
+                             float* const* val_out, void* const* ws, size_t ws_bytes,
+                             int n_streams, const dpz_stream_t* streams, int32_t* status,
+                             int flags);
 int dpz_decode_average_batch(int m, const float* const* local, float* const* out, int64_t n,
                              const int* n_payloads, const int32_t* const* idx,
                              const float* const* vals, const int64_t* k, const float* w,
