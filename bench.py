@@ -174,7 +174,9 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
 
     # every encode takes its key window from the previous encode on its stream's workspace
     # (DPZ_BATCH_HINT: a node's previous round, as PartialModel runs it; no sample launch)
-    def run_steps(batch, count, what=DPZ_BATCH_ENCODE | DPZ_BATCH_DECODE | DPZ_BATCH_HINT):
+    hint = DPZ_BATCH_HINT if os.environ.get("BENCH_HINT", "1") != "0" else 0  # A/B switch
+
+    def run_steps(batch, count, what=DPZ_BATCH_ENCODE | DPZ_BATCH_DECODE | hint):
         for _ in range(count // R):
             batch.run(what)
         if count % R:
@@ -230,7 +232,7 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     stream = s_list[0]
     reps = max(2 * R, steps // 2)
 
-    t_enc = _stage_time(one, DPZ_BATCH_ENCODE | DPZ_BATCH_HINT, reps, run_steps, stream)
+    t_enc = _stage_time(one, DPZ_BATCH_ENCODE | hint, reps, run_steps, stream)
     t_dec = _stage_time(one, DPZ_BATCH_DECODE, reps, run_steps, stream)
     # per-kernel device time: the library brackets every launch with a HIP event pair on the
     # stream it launches on.  A GPU-side spin first lets the host queue all `reps` steps, so the
@@ -253,7 +255,8 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     b_enc = 8 * n + 8 * k + 8 * k      # read x, x0; write idx, val; counter[idx] += 1 (r+w)
     b_dec = 8 * n + 8 * k              # read local, payload; write out
     fell_back |= (multi.sticky_status(clear=True) | one.sticky_status(clear=True)) != 0
-    product = product_one_node(sets, n, k, stream, one.workspaces[0], max(2 * R, min(steps, 200)))
+    product = product_one_node(sets, n, k, stream, one.workspaces[0], max(2 * R, min(steps, 200)),
+                               hint=bool(hint))
     fell_back |= product["fell_back"]
     return dict(n=n, k=k, s_step=s_step, s_multi=s_multi, s_serial=s_serial, s_host=s_host,
                 mode=mode, streams=S, fell_back=fell_back, t_enc=t_enc, t_dec=t_dec,

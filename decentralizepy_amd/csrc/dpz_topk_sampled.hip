@@ -450,11 +450,39 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
   const int64_t beg = seg * R;  // a multiple of 4 (R is); >= n for the grid's spare waves
   const int64_t end = (beg + R < n) ? beg + R : n;
   const int64_t end4 = beg < end ? beg + ((end - beg) & ~int64_t(3)) : beg;
+  const v4f* __restrict__ xa = reinterpret_cast<const v4f*>(s.x);
+  constexpr bool X0 = SRC != 0;  // a second operand stream (x0 or acc) in the B buffers
+  const v4f* __restrict__ xb = reinterpret_cast<const v4f*>(SRC == 2 ? s.acc : s.x0);
+  v4f A[D], B[D];
+  // group j of the segment (256 elements) into buffer slot u
+  auto ld = [&](int64_t j, int u) {
+    const int64_t i0 = beg + j * 256 + lane * 4;
+    const int64_t g4 = (i0 < end4 ? i0 : 0) >> 2;
+    // x non-temporal, like x0 / acc: a runtime choice between a non-temporal and a plain load
+    // (an xnt kernel argument, tried in round 4) compiled to ONE plain load — the hint was lost,
+    // x stayed in the caches and the compact's counter updates slowed by 1-3 us (same-box A/B
+    // against the round-3 build, tools/diag/enc_ab.py)
+    if (XNT) A[u] = __builtin_nontemporal_load(xa + g4);
+    else A[u] = xa[g4];
+    if (X0) B[u] = __builtin_nontemporal_load(xb + g4);
+  };
+  // the window's inputs are loaded first, the first stream loads right after them, and only
+  // then is anything waited on (a check of the prior before the stream loads would hold every
+  // wave's first load behind its round trip)
   uint4 cv[2] = {};
-  uint32_t hT = 0;
+  uint32_t hT = 0, hS = 0;
   if (hsig) {
     hT = ctrl->hint_T;
-    const bool ok = ctrl->hint_sig == hsig && hT > 0u && hT < 0x7F800000u;
+    hS = ctrl->hint_sig;
+  } else {
+    const uint4* c4 = reinterpret_cast<const uint4*>(chist) + (510 - 2 * threadIdx.x);
+    cv[0] = c4[0];
+    cv[1] = c4[1];
+  }
+#pragma unroll
+  for (int u = 0; u < D - 1; ++u) ld(u, u);
+  if (hsig) {
+    const bool ok = hS == hsig && hT > 0u && hT < 0x7F800000u;
     if (!ok) {  // no usable prior window: the call misses (uniform over the grid)
       if (blockIdx.x == 0 && threadIdx.x == 0) {
         ctrl->status = 1;
@@ -472,29 +500,7 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
         ctrl->hinted = 1;
       }
     }
-  } else {
-    const uint4* c4 = reinterpret_cast<const uint4*>(chist) + (510 - 2 * threadIdx.x);
-    cv[0] = c4[0];
-    cv[1] = c4[1];
   }
-  const v4f* __restrict__ xa = reinterpret_cast<const v4f*>(s.x);
-  constexpr bool X0 = SRC != 0;  // a second operand stream (x0 or acc) in the B buffers
-  const v4f* __restrict__ xb = reinterpret_cast<const v4f*>(SRC == 2 ? s.acc : s.x0);
-  v4f A[D], B[D];
-  // group j of the segment (256 elements) into buffer slot u
-  auto ld = [&](int64_t j, int u) {
-    const int64_t i0 = beg + j * 256 + lane * 4;
-    const int64_t g4 = (i0 < end4 ? i0 : 0) >> 2;
-    // x non-temporal, like x0 / acc: a runtime choice between a non-temporal and a plain load
-    // (an xnt kernel argument, tried in round 4) compiled to ONE plain load — the hint was lost,
-    // x stayed in the caches and the compact's counter updates slowed by 1-3 us (same-box A/B
-    // against the round-3 build, tools/diag/enc_ab.py)
-    if (XNT) A[u] = __builtin_nontemporal_load(xa + g4);
-    else A[u] = xa[g4];
-    if (X0) B[u] = __builtin_nontemporal_load(xb + g4);
-  };
-#pragma unroll
-  for (int u = 0; u < D - 1; ++u) ld(u, u);
   uint32_t lo, hi, shift;
   if (hsig) {
     hint_window(hT, &lo, &hi, &shift);
@@ -626,8 +632,6 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
       return;
     }
   }
-  // a hinted filter without a usable prior window reported a miss: nothing to select
-  if (ctrl->status) return;
   STAMP_MIN(6);
   STAMP_T0(8);
   __shared__ __attribute__((aligned(16))) uint32_t gh[GH_STRIDE];
@@ -649,6 +653,9 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
     pi[u][0] = sg < W ? cidx[sg * CAP + lane] : 0u;
   }
   const uint32_t lo = ctrl->lo, hi = ctrl->hi, shift = ctrl->shift;
+  // a hinted filter without a usable prior window reported a miss (checked once the first loads
+  // are issued: nothing to select)
+  const uint32_t fstatus = ctrl->status;
   // histogram copies (bins t and, for t == 0, the above-window bin HB), then chunks 1 .. PFS-1
   // of segments with more than 64 candidates — all loads issued before any sum is formed
   static_assert(HB == 1024, "select: one fine bin per thread + the above-window bin");
@@ -673,6 +680,7 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
       }
     }
   }
+  if (fstatus) return;  // uniform over the grid
   {
     uint32_t sum = 0, suma = 0;
 #pragma unroll
