@@ -125,6 +125,7 @@ SIGNATURES = {
     "dpz_topk_encode_batch_ex": (_int, [_int, _c_void_p, _c_void_p, _i64, _i64, _c_void_p,
                                      _c_void_p, _c_void_p, _c_void_p, _size, _int, _c_void_p,
                                      _c_void_p, _int]),
+    "dpz_topk_encode_nodes": (_int, [_int, _c_void_p, _i64, _i64, _size, _int, _c_void_p]),
     "dpz_decode_average_batch": (_int, [_int, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
                                         _c_void_p, _c_void_p, _c_void_p, _c_void_p, _int,
                                         _c_void_p, _size, _int, _c_void_p]),

@@ -1688,6 +1688,8 @@ static int launch_walk_t(const FoldArgs& fa, bool w2, hipStream_t st) {
   constexpr int TE = 64 * EPL;
   const int64_t ntl = (fa.n + TE - 1) / TE;
   int64_t blocks = (int64_t)cus * per;
+  // DPZ_WALK_BLOCKS=N: the walk grid at N blocks (diagnostic build, A/B)
+  if (DPZ_KNOB_INT(WALK_BLOCKS, 0) > 0) blocks = DPZ_KNOB_INT(WALK_BLOCKS, 0);
   const int64_t need = (ntl + FW_WAVES - 1) / FW_WAVES;
   if (blocks > need) blocks = need;
   if (blocks < 1) blocks = 1;

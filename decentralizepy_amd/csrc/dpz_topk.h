@@ -340,6 +340,9 @@ int topk_encode_status(const float* x, const float* x0, float* acc, int acc_mode
                        float* val_out, int32_t* counter, void* ws, size_t ws_bytes,
                        hipStream_t st, int32_t* status_out, bool shared = false,
                        bool val_fp16 = false, bool hint = false);
+// dpz_topk_encode_nodes (dpz_topk_sampled.hip): m nodes' encodes, one launch per phase
+int topk_encode_nodes(int m, const void* table, int64_t n, int64_t k, size_t ws_bytes, int flags,
+                      hipStream_t st);
 static inline bool use_sampled(int64_t n, int64_t k) {
   return n >= (1 << 18) && k >= 1 && k <= n / 2;
 }

@@ -504,6 +504,12 @@ extern "C" int dpz_topk_complete(const float* x, const float* x0, float* acc, in
   return DPZ_OK;
 }
 
+extern "C" int dpz_topk_encode_nodes(int m, const void* node_table, int64_t n, int64_t k,
+                                     size_t ws_bytes, int flags, dpz_stream_t stream) {
+  return topk_encode_nodes(m, node_table, n, k, ws_bytes, flags,
+                           static_cast<hipStream_t>(stream));
+}
+
 extern "C" int dpz_topk_sticky_status(void* ws, size_t ws_bytes, int clear, int32_t* out,
                                       dpz_stream_t stream) {
   if (!ws || ws_bytes < sizeof(TopkCtrl)) return DPZ_ERR_ARG;

@@ -71,12 +71,9 @@ __device__ __forceinline__ int64_t sample_pos(int c, int lane, int64_t n) {
 // SMP_NCHUNK / (4 waves-per-block) blocks: 1024 chunks of 64 contiguous elements spread evenly
 // over [0, n), four per wave.  nsb = the sample's own blocks (blockDim 256 or 1024: fewer,
 // larger blocks fold into the global histogram with fewer same-address atomics per bin).
-__global__ void __launch_bounds__(1024) sampled_sample_kernel(KeySrc s, int64_t n, TopkCtrl* ctrl,
-                                                              uint32_t* chist, uint32_t* ghist,
-                                                              uint32_t* blcnt, ReplaceJob pj,
-                                                              int nsb, int val_h) {
-  if ((int)blockIdx.x >= nsb) {  // co-scheduled replace decode (independent work)
-    replace_block(pj, blockIdx.x - nsb);
+__device__ __forceinline__ void sampled_sample_kernel_body(KeySrc s, int64_t n, TopkCtrl* ctrl, uint32_t* chist, uint32_t* ghist, uint32_t* blcnt, ReplaceJob pj, int nsb, int val_h, const uint32_t BID) {
+  if ((int)BID >= nsb) {  // co-scheduled replace decode (independent work)
+    replace_block(pj, BID - nsb);
     return;
   }
   STAMP_MIN(0);
@@ -87,17 +84,17 @@ __global__ void __launch_bounds__(1024) sampled_sample_kernel(KeySrc s, int64_t 
   float v[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int64_t i = sample_pos((blockIdx.x * nw + wave) * 4 + r, lane, n);
+    const int64_t i = sample_pos((BID * nw + wave) * 4 + r, lane, n);
     float d = s.x0 ? (s.x[i] - s.x0[i]) : s.x[i];
     if (s.mode != DPZ_ACC_NONE) d = s.acc[i] + d;
     v[r] = d;
   }
   for (int b = threadIdx.x; b < CB; b += blockDim.x) h[b] = 0;
   // this call's window histogram copies and boundary sub-list counters start at zero
-  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < GH_COPIES * GH_STRIDE;
+  for (int b = BID * blockDim.x + threadIdx.x; b < GH_COPIES * GH_STRIDE;
        b += nsb * blockDim.x)
     ghist[b] = 0;
-  if (blockIdx.x == 0) {
+  if (BID == 0) {
     if (threadIdx.x < NSUB) blcnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
       ctrl->status = 0;
@@ -116,6 +113,10 @@ __global__ void __launch_bounds__(1024) sampled_sample_kernel(KeySrc s, int64_t 
   }
   STAMP_MAX(1);
   STAMP_T0(14);
+}
+
+__global__ void __launch_bounds__(1024) sampled_sample_kernel(KeySrc s, int64_t n, TopkCtrl* ctrl, uint32_t* chist, uint32_t* ghist, uint32_t* blcnt, ReplaceJob pj, int nsb, int val_h) {
+  sampled_sample_kernel_body(s, n, ctrl, chist, ghist, blcnt, pj, nsb, val_h, (uint32_t)blockIdx.x);
 }
 
 // Block-level (256 threads): window [lo, hi) around the k-th key from the coarse sample histogram.
@@ -432,11 +433,7 @@ __device__ __forceinline__ void hint_window(uint32_t T, uint32_t* lo, uint32_t* 
 // window-histogram copies were left zero by the previous call's compact); an invalid prior makes
 // the call miss at once (every block leaves, select and compact see the status).
 template <int SRC, int CP, int D, int OCC, bool XNT>
-__global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
-    KeySrc s, int64_t n, uint32_t r_lo, uint32_t r_hi, int64_t W, int64_t R, int64_t CAP,
-    TopkCtrl* ctrl, const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt,
-    uint32_t* cidx, uint32_t* ckey, float* cval, float* __restrict__ copy_out,
-    FoldBase fb, uint32_t hsig, uint32_t* blcnt, int val_h) {
+__device__ __forceinline__ void sampled_filter_pipe_kernel_body(KeySrc s, int64_t n, uint32_t r_lo, uint32_t r_hi, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl, const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt, uint32_t* cidx, uint32_t* ckey, float* cval, float* __restrict__ copy_out, FoldBase fb, uint32_t hsig, uint32_t* blcnt, int val_h, const uint32_t BID) {
   static_assert(D >= 2, "at least one group in flight");
   typedef float v4f __attribute__((ext_vector_type(4)));
   __shared__ uint32_t h[HBR];
@@ -446,7 +443,7 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   STAMP_T0(5);
   for (int b = threadIdx.x; b < HBR; b += 256) h[b] = 0;
-  const int64_t seg = (int64_t)blockIdx.x * 4 + wid;
+  const int64_t seg = (int64_t)BID * 4 + wid;
   const int64_t beg = seg * R;  // a multiple of 4 (R is); >= n for the grid's spare waves
   const int64_t end = (beg + R < n) ? beg + R : n;
   const int64_t end4 = beg < end ? beg + ((end - beg) & ~int64_t(3)) : beg;
@@ -484,14 +481,14 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
   if (hsig) {
     const bool ok = hS == hsig && hT > 0u && hT < 0x7F800000u;
     if (!ok) {  // no usable prior window: the call misses (uniform over the grid)
-      if (blockIdx.x == 0 && threadIdx.x == 0) {
+      if (BID == 0 && threadIdx.x == 0) {
         ctrl->status = 1;
         ctrl->hinted = 1;
         ctrl->val_h = (uint32_t)val_h;
       }
       return;
     }
-    if (blockIdx.x == 0) {
+    if (BID == 0) {
       if (threadIdx.x < NSUB) blcnt[threadIdx.x] = 0;
       if (threadIdx.x == 0) {
         ctrl->status = 0;
@@ -568,13 +565,18 @@ __global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(
   }
   if (!dense) L.flush(lane, true, h, lo, hi, shift);
   __syncthreads();
-  uint32_t* gcopy = ghist + (blockIdx.x & (GH_COPIES - 1)) * GH_STRIDE;
+  uint32_t* gcopy = ghist + (BID & (GH_COPIES - 1)) * GH_STRIDE;
   for (int b = threadIdx.x; b < HBR; b += 256) {
     const uint32_t v = h[b];
     if (v) atomicAdd(&gcopy[b], v);
   }
   if (lane == 0 && seg < W) segcnt[seg] = dense ? DENSE : run;
   STAMP_T0(7);
+}
+
+template <int SRC, int CP, int D, int OCC, bool XNT>
+__global__ void __launch_bounds__(256, OCC) sampled_filter_pipe_kernel(KeySrc s, int64_t n, uint32_t r_lo, uint32_t r_hi, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl, const uint32_t* __restrict__ chist, uint32_t* ghist, uint32_t* segcnt, uint32_t* cidx, uint32_t* ckey, float* cval, float* __restrict__ copy_out, FoldBase fb, uint32_t hsig, uint32_t* blcnt, int val_h) {
+  sampled_filter_pipe_kernel_body<SRC, CP, D, OCC, XNT>(s, n, r_lo, r_hi, W, R, CAP, ctrl, chist, ghist, segcnt, cidx, ckey, cval, copy_out, fb, hsig, blcnt, val_h, (uint32_t)blockIdx.x);
 }
 
 // Wave-level threshold bin from the global window histogram gh (LDS, HB fine bins + the
@@ -620,15 +622,11 @@ __device__ __forceinline__ bool wave_bstar(const uint32_t* gh, uint32_t above, u
 // (blkabove) and appends the bin-b* entries, staged in LDS, to sub-list (block % 16) with one
 // atomic per block.
 template <bool VEC>
-__global__ void __launch_bounds__(1024) sampled_select_kernel(
-    KeySrc s, int64_t n, int64_t k, int64_t W, int64_t B, int64_t R, int64_t CAP, TopkCtrl* ctrl,
-    const uint32_t* __restrict__ ghist, const uint32_t* __restrict__ segcnt,
-    const uint32_t* __restrict__ cidx, const uint32_t* __restrict__ ckey, uint32_t* blkabove,
-    uint32_t* blcnt, uint32_t* blkey, uint32_t* blidx, ReplaceJob pj) {
+__device__ __forceinline__ void sampled_select_kernel_body(KeySrc s, int64_t n, int64_t k, int64_t W, int64_t B, int64_t R, int64_t CAP, TopkCtrl* ctrl, const uint32_t* __restrict__ ghist, const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ cidx, const uint32_t* __restrict__ ckey, uint32_t* blkabove, uint32_t* blcnt, uint32_t* blkey, uint32_t* blidx, ReplaceJob pj, const uint32_t BID) {
   {
     const int64_t own = (W + SEL_SEGS - 1) / SEL_SEGS;
-    if ((int64_t)blockIdx.x >= own) {  // co-scheduled replace decode
-      replace_block(pj, (int64_t)blockIdx.x - own);
+    if ((int64_t)BID >= own) {  // co-scheduled replace decode
+      replace_block(pj, (int64_t)BID - own);
       return;
     }
   }
@@ -639,7 +637,7 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
   __shared__ uint32_t lkey[SEL_LCAP], lidx[SEL_LCAP];
   __shared__ uint32_t lcnt, gbase, sb_bstar, sb_need, sb_ok;
   const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
-  const int64_t seg0 = (int64_t)blockIdx.x * SEL_SEGS + wid * 2;
+  const int64_t seg0 = (int64_t)BID * SEL_SEGS + wid * 2;
   const uint32_t cnt0 = seg0 < W ? segcnt[seg0] : 0u;
   const uint32_t cnt1 = seg0 + 1 < W ? segcnt[seg0 + 1] : 0u;
   // the first 64 entries of both lists are loaded with the counts and the histogram, not after
@@ -706,12 +704,12 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
   }
   __syncthreads();
   if (!sb_ok) {  // identical in every block: the whole grid leaves
-    if (blockIdx.x == 0 && t == 0) ctrl->status = 1;
+    if (BID == 0 && t == 0) ctrl->status = 1;
     return;
   }
   STAMP_T0(9);
   const uint32_t bstar = sb_bstar;
-  if (blockIdx.x == 0 && t == 0) {
+  if (BID == 0 && t == 0) {
     ctrl->bstar = bstar;
     ctrl->need = sb_need;
   }
@@ -785,13 +783,13 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
   }
   __syncthreads();
   if (t < SEL_SEGS / 4) {
-    const int64_t fb = (int64_t)blockIdx.x * (SEL_SEGS / 4) + t;
+    const int64_t fb = (int64_t)BID * (SEL_SEGS / 4) + t;
     blkabove[fb] = fb < B ? fbabove[t] : 0u;  // zero-padded to a multiple of 8 (compact)
   }
   STAMP_T0(10);
   const uint32_t nl = lcnt;
   if (nl) {
-    const int sub = (int)(blockIdx.x & (NSUB - 1));
+    const int sub = (int)(BID & (NSUB - 1));
     if (t == 0) gbase = atomicAdd(&blcnt[sub], nl > SEL_LCAP ? (uint32_t)BCAP : nl);
     __syncthreads();
     const uint32_t gb = gbase;
@@ -804,6 +802,11 @@ __global__ void __launch_bounds__(1024) sampled_select_kernel(
     }
   }
   STAMP_T0(11);
+}
+
+template <bool VEC>
+__global__ void __launch_bounds__(1024) sampled_select_kernel(KeySrc s, int64_t n, int64_t k, int64_t W, int64_t B, int64_t R, int64_t CAP, TopkCtrl* ctrl, const uint32_t* __restrict__ ghist, const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ cidx, const uint32_t* __restrict__ ckey, uint32_t* blkabove, uint32_t* blcnt, uint32_t* blkey, uint32_t* blidx, ReplaceJob pj) {
+  sampled_select_kernel_body<VEC>(s, n, k, W, B, R, CAP, ctrl, ghist, segcnt, cidx, ckey, blkabove, blcnt, blkey, blidx, pj, (uint32_t)blockIdx.x);
 }
 
 // Boundary entry j (0 <= j < nb) of the 16 sub-lists: sub-list sb with subbase[sb] <= j.
@@ -1095,15 +1098,7 @@ static_assert(32 % SL_PF == 0, "the planes are read in whole steps");
 // words), then writes every word of the row to selmask and adds it to the bit-sliced counter
 // (planes[p * nwords + w], carry-propagated plane by plane) with coalesced accesses.
 template <bool VEC, bool PLAIN, int SPW, bool SL>
-__global__ void __launch_bounds__(256, SPW >= 8 ? 1 : 4) sampled_compact_kernel(
-    KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl,
-    uint32_t* chist, const uint32_t* __restrict__ blkabove, const uint32_t* __restrict__ blcnt,
-    const uint32_t* __restrict__ blkey, const uint32_t* __restrict__ blidx,
-    const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ cidx,
-    const uint32_t* __restrict__ ckey, const float* __restrict__ cval, const float* vals_src,
-    int32_t* idx_out, float* val_out, int32_t* counter, float* rewind, int32_t* status_out,
-    ReplaceJob pj, int64_t nrep_first, int val_h, uint32_t* selmask, uint32_t* planes,
-    int64_t nwords, uint32_t* ghist, uint32_t sig) {
+__device__ __forceinline__ void sampled_compact_kernel_body(KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl, uint32_t* chist, const uint32_t* __restrict__ blkabove, const uint32_t* __restrict__ blcnt, const uint32_t* __restrict__ blkey, const uint32_t* __restrict__ blidx, const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ cidx, const uint32_t* __restrict__ ckey, const float* __restrict__ cval, const float* vals_src, int32_t* idx_out, float* val_out, int32_t* counter, float* rewind, int32_t* status_out, ReplaceJob pj, int64_t nrep_first, int val_h, uint32_t* selmask, uint32_t* planes, int64_t nwords, uint32_t* ghist, uint32_t sig, const uint32_t BID) {
   constexpr int CSEG = CompactCfg<SPW>::CSEG;
   constexpr int PFC = CompactCfg<SPW>::PFC;
   constexpr int SLW = SL ? (int)(SL_RMAX / 32) : 1;
@@ -1119,11 +1114,11 @@ __global__ void __launch_bounds__(256, SPW >= 8 ? 1 : 4) sampled_compact_kernel(
   const int64_t B = (W + 3) / 4;  // filter blocks (above counts)
   // co-scheduled replace decode: its blocks after compact's own, or (nrep_first > 0) before
   // them, dispatched first so their stores overlap the compact blocks' dependent prologue
-  if (nrep_first > 0 ? (int64_t)blockIdx.x < nrep_first : (int64_t)blockIdx.x >= CB_) {
-    replace_block(pj, nrep_first > 0 ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - CB_);
+  if (nrep_first > 0 ? (int64_t)BID < nrep_first : (int64_t)BID >= CB_) {
+    replace_block(pj, nrep_first > 0 ? (int64_t)BID : (int64_t)BID - CB_);
     return;
   }
-  const uint32_t blk = (uint32_t)((int64_t)blockIdx.x - (nrep_first > 0 ? nrep_first : 0));
+  const uint32_t blk = (uint32_t)((int64_t)BID - (nrep_first > 0 ? nrep_first : 0));
   STAMP_T0(0);
   const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
   // select has read the window-histogram copies: leave them zero for the next call (a call with
@@ -1418,6 +1413,11 @@ __global__ void __launch_bounds__(256, SPW >= 8 ? 1 : 4) sampled_compact_kernel(
   STAMP_T0(4);
 }
 
+template <bool VEC, bool PLAIN, int SPW, bool SL>
+__global__ void __launch_bounds__(256, SPW >= 8 ? 1 : 4) sampled_compact_kernel(KeySrc s, int64_t n, int64_t k, int64_t W, int64_t R, int64_t CAP, TopkCtrl* ctrl, uint32_t* chist, const uint32_t* __restrict__ blkabove, const uint32_t* __restrict__ blcnt, const uint32_t* __restrict__ blkey, const uint32_t* __restrict__ blidx, const uint32_t* __restrict__ segcnt, const uint32_t* __restrict__ cidx, const uint32_t* __restrict__ ckey, const float* __restrict__ cval, const float* vals_src, int32_t* idx_out, float* val_out, int32_t* counter, float* rewind, int32_t* status_out, ReplaceJob pj, int64_t nrep_first, int val_h, uint32_t* selmask, uint32_t* planes, int64_t nwords, uint32_t* ghist, uint32_t sig) {
+  sampled_compact_kernel_body<VEC, PLAIN, SPW, SL>(s, n, k, W, R, CAP, ctrl, chist, blkabove, blcnt, blkey, blidx, segcnt, cidx, ckey, cval, vals_src, idx_out, val_out, counter, rewind, status_out, pj, nrep_first, val_h, selmask, planes, nwords, ghist, sig, (uint32_t)blockIdx.x);
+}
+
 // Fractions of a co-scheduled replace job's chunks carried by sample / select / compact;
 // DPZ_COSCHED="f0,f1,f2" overrides them in the diagnostic build (dpz_knobs.h).
 // Defaults measured on MI355X, see DESIGN.md §3.6.
@@ -1622,6 +1622,131 @@ extern "C" int dpz_debug_stamps(unsigned long long* host_out, int reset) {
   return 0;
 }
 #endif
+
+// ---- the encodes of m nodes, one launch per phase (dpz_topk_encode_nodes) ----------------------
+// A simulated gossip round encodes every node's model (reference: each node process runs
+// sharing/PartialModel.py:164-255).  Node after node on a few streams, each encode is four
+// dependent launches whose selection tail leaves the GPU idle; here every phase runs for all m
+// nodes in ONE launch (grid = m x the per-node grid, block b -> node b / per-node blocks), so the
+// tails of all nodes overlap each other and the filter streams all m models back to back.
+struct EncNode {
+  const float* x;
+  const float* x0;
+  int32_t* counter;
+  int32_t* idx_out;
+  float* val_out;
+  char* ws;
+  int32_t* status_out;
+  uint64_t pad;
+};
+static_assert(sizeof(EncNode) == 64, "node table entry: 8 x 64-bit words (dpz_codec.h)");
+struct WsOff {
+  uint64_t ctrl, chist, ghist, segcnt, blkabove, cidx, ckey, cval, blcnt, blkey, blidx;
+};
+
+template <class T>
+__device__ __forceinline__ T* wsp(char* ws, uint64_t off) {
+  return reinterpret_cast<T*>(ws + off);
+}
+
+__global__ void __launch_bounds__(1024) nodes_sample_kernel(const EncNode* __restrict__ tab,
+                                                            WsOff o, int64_t n, int nsb) {
+  const uint32_t node = blockIdx.x / (uint32_t)nsb, bid = blockIdx.x % (uint32_t)nsb;
+  const EncNode e = tab[node];
+  KeySrc s{e.x, e.x0, nullptr, DPZ_ACC_NONE, 0};
+  sampled_sample_kernel_body(s, n, wsp<TopkCtrl>(e.ws, o.ctrl), wsp<uint32_t>(e.ws, o.chist),
+                             wsp<uint32_t>(e.ws, o.ghist), wsp<uint32_t>(e.ws, o.blcnt),
+                             ReplaceJob{}, nsb, 0, bid);
+}
+
+template <int D, int OCC>
+__global__ void __launch_bounds__(256, OCC) nodes_filter_kernel(
+    const EncNode* __restrict__ tab, WsOff o, int64_t n, uint32_t r_lo, uint32_t r_hi, int64_t W,
+    int64_t R, int64_t CAP, uint32_t nb, uint32_t hsig) {
+  const uint32_t node = blockIdx.x / nb, bid = blockIdx.x % nb;
+  const EncNode e = tab[node];
+  KeySrc s{e.x, e.x0, nullptr, DPZ_ACC_NONE, 0};
+  sampled_filter_pipe_kernel_body<1, 0, D, OCC, true>(
+      s, n, r_lo, r_hi, W, R, CAP, wsp<TopkCtrl>(e.ws, o.ctrl), wsp<const uint32_t>(e.ws, o.chist),
+      wsp<uint32_t>(e.ws, o.ghist), wsp<uint32_t>(e.ws, o.segcnt), wsp<uint32_t>(e.ws, o.cidx),
+      wsp<uint32_t>(e.ws, o.ckey), wsp<float>(e.ws, o.cval), nullptr, FoldBase{}, hsig,
+      wsp<uint32_t>(e.ws, o.blcnt), 0, bid);
+}
+
+__global__ void __launch_bounds__(1024) nodes_select_kernel(const EncNode* __restrict__ tab,
+                                                            WsOff o, int64_t n, int64_t k,
+                                                            int64_t W, int64_t B, int64_t R,
+                                                            int64_t CAP, uint32_t nsel) {
+  const uint32_t node = blockIdx.x / nsel, bid = blockIdx.x % nsel;
+  const EncNode e = tab[node];
+  KeySrc s{e.x, e.x0, nullptr, DPZ_ACC_NONE, 1};
+  sampled_select_kernel_body<true>(
+      s, n, k, W, B, R, CAP, wsp<TopkCtrl>(e.ws, o.ctrl), wsp<const uint32_t>(e.ws, o.ghist),
+      wsp<const uint32_t>(e.ws, o.segcnt), wsp<const uint32_t>(e.ws, o.cidx),
+      wsp<const uint32_t>(e.ws, o.ckey), wsp<uint32_t>(e.ws, o.blkabove),
+      wsp<uint32_t>(e.ws, o.blcnt), wsp<uint32_t>(e.ws, o.blkey), wsp<uint32_t>(e.ws, o.blidx),
+      ReplaceJob{}, bid);
+}
+
+template <bool PLAIN>
+__global__ void __launch_bounds__(256, 4) nodes_compact_kernel(const EncNode* __restrict__ tab,
+                                                               WsOff o, int64_t n, int64_t k,
+                                                               int64_t W, int64_t R, int64_t CAP,
+                                                               uint32_t ncb, int64_t nwords,
+                                                               uint32_t sig) {
+  const uint32_t node = blockIdx.x / ncb, bid = blockIdx.x % ncb;
+  const EncNode e = tab[node];
+  KeySrc s{e.x, e.x0, nullptr, DPZ_ACC_NONE, 1};
+  sampled_compact_kernel_body<true, PLAIN, 2, false>(
+      s, n, k, W, R, CAP, wsp<TopkCtrl>(e.ws, o.ctrl), wsp<uint32_t>(e.ws, o.chist),
+      wsp<const uint32_t>(e.ws, o.blkabove), wsp<const uint32_t>(e.ws, o.blcnt),
+      wsp<const uint32_t>(e.ws, o.blkey), wsp<const uint32_t>(e.ws, o.blidx),
+      wsp<const uint32_t>(e.ws, o.segcnt), wsp<const uint32_t>(e.ws, o.cidx),
+      wsp<const uint32_t>(e.ws, o.ckey), wsp<const float>(e.ws, o.cval), e.x, e.idx_out,
+      e.val_out, e.counter, nullptr, e.status_out, ReplaceJob{}, 0, 0, nullptr, nullptr, nwords,
+      wsp<uint32_t>(e.ws, o.ghist), sig, bid);
+}
+
+int topk_encode_nodes(int m, const void* table, int64_t n, int64_t k, size_t ws_bytes, int flags,
+                      hipStream_t st) {
+  if (m < 1 || !table || n <= 0 || n >= (int64_t(1) << 31) || k < 1 || k > n) return DPZ_ERR_ARG;
+  if (flags & ~DPZ_TOPK_HINT) return DPZ_ERR_ARG;
+  if (!use_sampled(n, k)) return DPZ_ERR_UNSUPPORTED;
+  if (ws_bytes < ws_bytes_needed(n, k)) return DPZ_ERR_WORKSPACE;
+  // the shared-GPU geometry (DPZ_TOPK_SHARED): many codecs run at once, and the smaller filter
+  // grid per node leaves CU slots to the other nodes' kernels
+  const WsLayout L = ws_layout(n, k, true);
+  const FastGeom& g = L.fg;
+  const WsOff o{L.ctrl, L.chist, L.f_ghist, L.f_segcnt, L.f_blkabove, L.f_cidx, L.f_ckey,
+                L.f_cval, L.f_blcnt, L.f_blkey, L.f_blidx};
+  const EncNode* tab = static_cast<const EncNode*>(table);
+  const uint32_t sig = hint_signature(n, k, true, DPZ_ACC_NONE, true);
+  const uint32_t hsig = (flags & DPZ_TOPK_HINT) ? sig : 0u;
+  const int nsb = SMP_NCHUNK / 16;  // 256-thread sample blocks per node
+  const uint32_t nb = (uint32_t)g.B, nsel = (uint32_t)((g.W + SEL_SEGS - 1) / SEL_SEGS);
+  const uint32_t ncb = (uint32_t)((g.W + 7) / 8);
+  if ((uint64_t)m * nb >= (1ull << 31) || (uint64_t)m * ncb >= (1ull << 31)) return DPZ_ERR_ARG;
+  if (!hsig)
+    DPZ_TIMED(DPZ_KT_TOPK_SAMPLE, st,
+              nodes_sample_kernel<<<(unsigned)(m * nsb), 256, 0, st>>>(tab, o, n, nsb));
+  uint32_t r_lo, r_hi;
+  window_ranks(n, k, &r_lo, &r_hi);
+  if (g.W > 4096)
+    DPZ_TIMED(DPZ_KT_TOPK_FILTER, st, (nodes_filter_kernel<2, 8><<<(unsigned)(m * nb), 256, 0, st>>>(
+        tab, o, n, r_lo, r_hi, g.W, g.R, g.CAP, nb, hsig)));
+  else
+    DPZ_TIMED(DPZ_KT_TOPK_FILTER, st, (nodes_filter_kernel<4, 4><<<(unsigned)(m * nb), 256, 0, st>>>(
+        tab, o, n, r_lo, r_hi, g.W, g.R, g.CAP, nb, hsig)));
+  DPZ_TIMED(DPZ_KT_TOPK_SELECT, st, nodes_select_kernel<<<(unsigned)(m * nsel), 1024, 0, st>>>(
+      tab, o, n, k, g.W, g.B, g.R, g.CAP, nsel));
+  if (k > n / 32)
+    DPZ_TIMED(DPZ_KT_TOPK_COMPACT, st, nodes_compact_kernel<true><<<(unsigned)(m * ncb), 256, 0, st>>>(
+        tab, o, n, k, g.W, g.R, g.CAP, ncb, mask_words(n), sig));
+  else
+    DPZ_TIMED(DPZ_KT_TOPK_COMPACT, st, nodes_compact_kernel<false><<<(unsigned)(m * ncb), 256, 0, st>>>(
+        tab, o, n, k, g.W, g.R, g.CAP, ncb, mask_words(n), sig));
+  return DPZ_OK;
+}
 
 bool fused_foldbase_ok(const EncodeArgs& a, bool vec) {
   // the pipelined filter's PartialModel configuration (run_sampled_t): aligned operands, no

@@ -300,6 +300,21 @@ int dpz_topk_encode_batch_ex(int m, const float* const* x, const float* const* x
                              float* const* val_out, void* const* ws, size_t ws_bytes,
                              int n_streams, const dpz_stream_t* streams, int32_t* status,
                              int flags);
+/* The encodes of m nodes of one size (n, k) — each exactly dpz_topk_encode(x, x0, NULL,
+ * DPZ_ACC_NONE, x, n, k, idx_out, val_out, counter, ws, ws_bytes, DPZ_TOPK_ASYNC) with its
+ * final status word also written to status_out (as dpz_topk_encode_status) — with ONE launch per
+ * phase of the sampled path for all of them (sample, filter, select, compact over a grid of m x
+ * the per-node grid), so the nodes' latency-bound selection tails overlap each other.
+ * node_table: DEVICE array of m entries of 8 64-bit words {x, x0, counter (or 0), idx_out,
+ * val_out, ws, status_out, 0}; every node its own workspace of ws_bytes >= dpz_topk_workspace_
+ * bytes(n, k) bytes (zero-filled before its first use), x / x0 16-byte aligned.  flags:
+ * DPZ_TOPK_HINT (every node's window from its workspace's previous encode, no sample launch; a
+ * node without a usable prior misses).  Asynchronous: a nonzero status_out[j] means node j
+ * wrote nothing and is re-run with DPZ_TOPK_EXACT.  DPZ_ERR_UNSUPPORTED when (n, k) is not on
+ * the sampled path (n >= 2^18, 1 <= k <= n / 2).  Replaces the per-node loops of reference node
+ * processes (sharing/PartialModel.py:164-255) run side by side.                               */
+int dpz_topk_encode_nodes(int m, const void* node_table, int64_t n, int64_t k, size_t ws_bytes,
+                          int flags, dpz_stream_t stream);
 int dpz_decode_average_batch(int m, const float* const* local, float* const* out, int64_t n,
                              const int* n_payloads, const int32_t* const* idx,
                              const float* const* vals, const int64_t* k, const float* w,

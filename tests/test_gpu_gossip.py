@@ -88,3 +88,34 @@ def test_jwins_round_device_matches_oracle(dev, wavelet):
                                           getattr(ref, name).numpy().view(np.uint32), err_msg=name)
         np.testing.assert_array_equal(eng.counter.cpu().numpy(), ref.counter.numpy())
     assert kinds == {True, False}
+
+
+def test_node_batched_encodes_equal_stream_encodes(dev):
+    """The round's encodes as one launch per phase over all nodes (dpz_topk_encode_nodes, each
+    node its own workspace, the prior window from the second round on) against node-after-node
+    encodes on three streams: bit-identical models and counters over three rounds — one node's
+    change hides its large entries between the sample chunks (tests/layouts.py) in round 0 and
+    jumps x4 in scale in round 2, so its encodes miss and are re-run exactly."""
+    from decentralizepy_amd.gossip import GossipRound, read_edges
+    from tests.layouts import miss_layout
+    adj = read_edges(EDGES16)
+    n = 1 << 20
+    x = _models(len(adj), n)
+    a = GossipRound(adj, x.to(dev), 0.01, node_batch=True)
+    b = GossipRound(adj, x.to(dev), 0.01, node_batch=False)
+    miss, _ = miss_layout(n, round(0.01 * n))
+    for r in range(3):
+        g = torch.Generator().manual_seed(300 + r)
+        noise = (0.01 * torch.randn(len(adj), n, generator=g)).to(dev)
+        if r == 2:
+            noise[5] *= 4.0
+        for eng in (a, b):
+            eng.x += noise
+            if r == 0:
+                eng.x[3] = eng.x0[3] + torch.from_numpy(miss).to(dev)
+            eng.step()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(a.x.cpu().numpy().view(np.uint32),
+                                      b.x.cpu().numpy().view(np.uint32))
+        np.testing.assert_array_equal(a.counter.cpu().numpy(), b.counter.cpu().numpy())
+    assert a.node_ws is not None and getattr(b, "node_ws", None) is None
