@@ -11,7 +11,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 for mode in ${MODES:-mib64 c2}; do
   unset DPZ_BATCH_COSCHED DPZ_CODEC_LIB PMC_N
-  CMD="python3 bench.py --steps ${STEPS:-100} --warmup 10 --no-cpu --no-extra --streams 1"
+  CMD="python3 bench.py --steps ${PROF_STEPS:-100} --warmup 10 --no-cpu --no-extra --streams 1"
   export PMC_N=16777216
   if [ "$mode" = c2 ]; then CMD="$CMD --n 11000000"; export PMC_N=11000000; fi
   if [ "$mode" = clean ]; then
