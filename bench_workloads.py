@@ -8,6 +8,7 @@ across rounds (init_model, accumulated changes, counters); inputs are synthetic 
 Node states rotate so each step streams its inputs from HBM, not the 256 MiB Infinity Cache.
 """
 import math
+import os
 import time
 
 import numpy as np
@@ -194,6 +195,12 @@ def c3_case(dev, n=25_000_000, alpha=0.01, npay=16, steps=40, warmup=5, seed=3, 
     ws = codec.Workspace(dev)
     st = torch.zeros(1, dtype=torch.int32, device=dev)
     mode = {"sliced": True}
+    # BENCH_HINT=1: the key window from the previous encode's exact threshold (DPZ_TOPK_HINT, no
+    # sample launch).  Off by default: this synthetic round's post-step adds W(fold - x0) to the
+    # accumulator every step (the fold mixes in unit-scale random payloads), so the k-th key moves
+    # by more than the window's +-1/16 from step to step and every hinted encode misses (measured
+    # on MI355X: fell_back on every line, filter 92-95 us with the window's extra candidates)
+    hint = {"on": os.environ.get("BENCH_HINT", "0") == "1"}
 
     def encode(d):
         codec.wavedec(d["x"], level, x0=d["x0"], coeffs_x=d["wx"], coeffs_diff=d["wc"],
@@ -202,11 +209,12 @@ def c3_case(dev, n=25_000_000, alpha=0.01, npay=16, steps=40, warmup=5, seed=3, 
             codec.topk_encode_sliced(d["wc"], k, d["mask"], d["planes"], acc=d["acc"],
                                      acc_mode=codec.DPZ_ACC_ADD, vals_src=d["wx"],
                                      idx_out=d["idx"], val_out=d["val"], workspace=ws,
-                                     status_out=st)
+                                     status_out=st, hint=hint["on"])
         else:
             codec.topk_encode(d["wc"], k, acc=d["acc"], acc_mode=codec.DPZ_ACC_ADD,
                               vals_src=d["wx"], counter=d["cnt"], idx_out=d["idx"],
-                              val_out=d["val"], workspace=ws, asynchronous=True)
+                              val_out=d["val"], workspace=ws, asynchronous=True,
+                              hint=hint["on"])
 
     def decode(d):
         codec.decode_average(d["wx"], pays, w, w_self, out=d["tot"], workspace=ws)
@@ -231,7 +239,8 @@ def c3_case(dev, n=25_000_000, alpha=0.01, npay=16, steps=40, warmup=5, seed=3, 
     t_dec = _sync_time(lambda i: decode(sets[i % R]), steps)
     t_post = _sync_time(lambda i: post(sets[i % R]), steps)
     torch.cuda.synchronize()
-    fb = int(st.item()) != 0
+    # any missed encode of the timed steps (the sticky word ORs every call's status)
+    fb = int(st.item()) != 0 or codec.topk_sticky_status(ws) != 0
     with codec.KernelTimer() as kt:
         torch.cuda._sleep(int(100e6))
         for i in range(R * 2):

@@ -129,6 +129,9 @@ SIGNATURES = {
     "dpz_decode_average_batch": (_int, [_int, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
                                         _c_void_p, _c_void_p, _c_void_p, _c_void_p, _int,
                                         _c_void_p, _size, _int, _c_void_p]),
+    "dpz_decode_average_batch_guarded": (_int, [_int, _c_void_p, _c_void_p, _i64, _c_void_p,
+                                                _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                                _c_void_p, _int, _c_void_p, _i64, _c_void_p]),
     "dpz_encode_replace_batch": (_int, [_int, _int, _c_void_p, _c_void_p, _i64, _i64, _c_void_p,
                                         _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                         _i64, _c_void_p, _c_void_p, _size, _c_void_p, _size,

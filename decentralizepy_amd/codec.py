@@ -206,14 +206,16 @@ def mask_words(n):
 
 def topk_encode_sliced(x, k, sel_mask, planes=None, x0=None, acc=None, acc_mode=DPZ_ACC_NONE,
                        vals_src=None, idx_out=None, val_out=None, workspace=None, exact=False,
-                       status_out=None, shared=False, val_fp16=False):
+                       status_out=None, shared=False, val_fp16=False, hint=False):
     """The selection of :func:`topk_encode` with its bookkeeping in coalesced form
     (dpz_topk_encode_sliced; reference Wavelet.py:194-197): ``planes`` (int32[32 * mask_words(n)],
     the bit-sliced shared_parameters_counter, or None) += 1 at the selected indices, and
     ``sel_mask`` (int32[mask_words(n)]) gets the selected bits — the accumulator rewind is left
     to the caller's next accumulating pass (``wavedec(..., rewind_mask=sel_mask)``) or
     :func:`rewind_apply`.  ``acc`` (DPZ_ACC_ADD) is only read.  Blocking unless ``status_out``
-    (then asynchronous: a nonzero status means re-run with ``exact=True``)."""
+    (then asynchronous: a nonzero status means re-run with ``exact=True``).  ``hint``: the key
+    window from the previous encode on ``workspace`` (as :func:`topk_encode`; a blocking call
+    that misses re-runs the sampled path, then the exact one)."""
     _require(x, torch.float32, "x")
     _require(x0, torch.float32, "x0")
     _require(acc, torch.float32, "acc")
@@ -234,9 +236,15 @@ def topk_encode_sliced(x, k, sel_mask, planes=None, x0=None, acc=None, acc_mode=
         val_out = torch.empty(k, dtype=vdt, device=x.device)
     _require(val_out, vdt, "val_out")
     _require(status_out, torch.int32, "status_out")
-    ws = (workspace or Workspace(x.device)).get(n, k)
+    wso = workspace or Workspace(x.device)
+    ws = wso.get(n, k)
     flags = ((DPZ_TOPK_EXACT if exact else 0) | (_lib.DPZ_TOPK_SHARED if shared else 0)
              | (_lib.DPZ_TOPK_VAL_FP16 if val_fp16 else 0))
+    # the device checks the prior's signature itself; this only avoids a predictable miss
+    hkey = (n, k, bool(shared), int(acc_mode), x0 is not None)
+    if hint and not exact and wso.hint_key == hkey:
+        flags |= _lib.DPZ_TOPK_HINT
+    wso.hint_key = None if exact else hkey
     rc = _lib.lib().dpz_topk_encode_sliced(
         _ptr(x), _ptr(x0), _ptr(acc), int(acc_mode), _ptr(vals_src), n, k, _ptr(idx_out),
         _ptr(val_out), _ptr(planes), _ptr(sel_mask), _ptr(ws), ws.numel(), _ptr(status_out),

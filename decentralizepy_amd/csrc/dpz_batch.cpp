@@ -49,7 +49,7 @@ namespace dpz {
 int fold_batch_walk(int m, const float* const* local, float* const* out, int64_t n,
                     const int* n_payloads, const int32_t* const* idx, const float* const* vals,
                     const int64_t* k, const float* w, const float* w_self, int flags,
-                    hipStream_t st);
+                    hipStream_t st, const int32_t* guard, int64_t guard_n);
 }  // namespace dpz
 
 extern "C" int dpz_decode_average_batch(int m, const float* const* local, float* const* out,
@@ -65,7 +65,7 @@ extern "C" int dpz_decode_average_batch(int m, const float* const* local, float*
   // streams[0] instead of one per node (dpz_fold.hip fold_batch_walk)
   {
     const int rc = dpz::fold_batch_walk(m, local, out, n, n_payloads, idx, vals, k, w, w_self,
-                                        flags, static_cast<hipStream_t>(streams[0]));
+                                        flags, static_cast<hipStream_t>(streams[0]), nullptr, 0);
     if (rc != 1) return rc;
   }
   int64_t off = 0;
@@ -80,6 +80,25 @@ extern "C" int dpz_decode_average_batch(int m, const float* const* local, float*
     off += np;
   }
   return DPZ_OK;
+}
+
+// The round's folds with no host check of the round's encodes in between (gossip.py): the
+// one-launch walk path of dpz_decode_average_batch, each launch reading guard[0, guard_n) (DEVICE
+// int32: the encodes' status words) first and writing nothing if any is nonzero.  DPZ_ERR_
+// UNSUPPORTED, nothing enqueued, when the batch does not take the one-launch path.
+extern "C" int dpz_decode_average_batch_guarded(int m, const float* const* local,
+                                                float* const* out, int64_t n,
+                                                const int* n_payloads, const int32_t* const* idx,
+                                                const float* const* vals, const int64_t* k,
+                                                const float* w, const float* w_self, int flags,
+                                                const int32_t* guard, int64_t guard_n,
+                                                dpz_stream_t stream) {
+  if (m < 0 || !local || !out || !n_payloads || !guard || guard_n < 1) return DPZ_ERR_ARG;
+  for (int j = 0; j < m; ++j)
+    if (n_payloads[j] < 0) return DPZ_ERR_ARG;
+  const int rc = dpz::fold_batch_walk(m, local, out, n, n_payloads, idx, vals, k, w, w_self,
+                                      flags, static_cast<hipStream_t>(stream), guard, guard_n);
+  return rc == 1 ? DPZ_ERR_UNSUPPORTED : rc;
 }
 
 // One codec step per node: encode node j's model (as dpz_topk_encode_batch) and/or replace-decode

@@ -1298,6 +1298,10 @@ struct FoldNodeBatch {
   int64_t n;
   int m;
   int add_self;
+  // dpz_decode_average_batch_guarded: int32 words (the round's encode status words) that must
+  // all be 0, or the launch writes nothing (nullptr: no guard)
+  const int32_t* guard;
+  int64_t guard_n;
 };
 static_assert(sizeof(FoldNodeBatch) <= 3584, "kernel arguments");
 struct FoldNodeView {
@@ -1332,6 +1336,11 @@ __global__ void __launch_bounds__(256, FW_MINB_1(EPL)) fold_walk_batch_kernel(Fo
 #pragma unroll
   for (int e = 0; e < EPL; ++e) wt[lane + 64 * e] = 0xFFFFFFFFu;
   const int64_t gw = (int64_t)blockIdx.x * FW_WAVES + fw_uni(wid);
+  if (b.guard) {  // a missed encode: no fold of this launch writes (the host re-runs the round)
+    bool bad = false;
+    for (int64_t i = lane; i < b.guard_n; i += 64) bad |= b.guard[i] != 0;
+    if (__ballot(bad) != 0) return;  // every wave reads the same final words
+  }
   int64_t g = gw * tpw;
   const int64_t gend = m * ntl;
   const int64_t g1 = g + tpw < gend ? g + tpw : gend;
@@ -2019,7 +2028,7 @@ static int launch_walk_batch_t(const FoldNodeBatch& b, hipStream_t st) {
 int fold_batch_walk(int m, const float* const* local, float* const* out, int64_t n,
                     const int* n_payloads, const int32_t* const* idx, const float* const* vals,
                     const int64_t* k, const float* w, const float* w_self, int flags,
-                    hipStream_t st) {
+                    hipStream_t st, const int32_t* guard, int64_t guard_n) {
   if (DPZ_KNOB_INT(FOLD_BATCH, 1) == 0) return 1;  // diagnostic build: per-node launches (A/B)
   if (m < 2 || (flags & ~(DPZ_FOLD_SELF | DPZ_FOLD_ALSO_LOCAL)) || !w || !idx) return 1;
   if (n < 1024 || n >= (int64_t(1) << 31) - 1024) return 1;
@@ -2045,6 +2054,8 @@ int fold_batch_walk(int m, const float* const* local, float* const* out, int64_t
     b.n = n;
     b.m = (m - j0) < FW_BATCH ? (m - j0) : FW_BATCH;
     b.add_self = (flags & DPZ_FOLD_SELF) ? 1 : 0;
+    b.guard = guard;
+    b.guard_n = guard ? guard_n : 0;
     for (int j = 0; j < b.m; ++j) {
       FoldNode& nd = b.nd[j];
       const int jj = j0 + j;

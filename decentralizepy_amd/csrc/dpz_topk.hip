@@ -363,7 +363,8 @@ extern "C" int dpz_topk_encode_sliced(const float* x, const float* x0, const flo
                                       uint32_t* sel_mask, void* ws, size_t ws_bytes,
                                       int32_t* status_out, int flags, dpz_stream_t stream) {
   if (acc_mode != DPZ_ACC_NONE && acc_mode != DPZ_ACC_ADD) return DPZ_ERR_ARG;
-  if (flags & ~(DPZ_TOPK_EXACT | DPZ_TOPK_SHARED | DPZ_TOPK_VAL_FP16)) return DPZ_ERR_ARG;
+  if (flags & ~(DPZ_TOPK_EXACT | DPZ_TOPK_SHARED | DPZ_TOPK_VAL_FP16 | DPZ_TOPK_HINT))
+    return DPZ_ERR_ARG;
   // acc is only read (ADD): the rewind is the caller's, through sel_mask
   EncodeArgs a{x, x0, const_cast<float*>(acc), acc_mode, vals_src, n, k, idx_out, val_out, nullptr,
                static_cast<char*>(ws), static_cast<hipStream_t>(stream)};
@@ -378,6 +379,10 @@ extern "C" int dpz_topk_encode_sliced(const float* x, const float* x0, const flo
   a.val_h = (flags & DPZ_TOPK_VAL_FP16) ? 1 : 0;
   a.selmask = sel_mask;
   a.planes = planes;
+  // a prior-round window (DPZ_TOPK_HINT): the keys (NONE / ADD) are a pure function of the
+  // inputs and a miss writes nothing, so a missed call simply runs the sampled path again
+  if (flags & DPZ_TOPK_HINT)
+    a.hint_sig = hint_signature(a.n, a.k, a.shared, a.acc_mode, a.x0 != nullptr);
   if (n == 0) {
     if (status_out) DPZ_HIP_TRY(hipMemsetAsync(status_out, 0, sizeof(int32_t), a.st));
     return DPZ_OK;
@@ -390,19 +395,24 @@ extern "C" int dpz_topk_encode_sliced(const float* x, const float* x0, const flo
     // mask and planes are built from idx_out after it (skipped on the device after a miss)
     const bool post = L.fg.R > SL_RMAX;
     a.status_out = status_out;
-    rc = run_sampled(a, L, vec, 3);
-    if (rc != DPZ_OK) return rc;
     const uint32_t* ctrl_status =
         reinterpret_cast<const uint32_t*>(a.ws + L.ctrl + offsetof(TopkCtrl, status));
-    if (post) {
-      rc = sliced_from_idx(a, ctrl_status);
+    // blocking: a hinted call that misses runs the sampled path once more (its own sample
+    // launch), then the exact path; asynchronous: the caller re-runs with EXACT
+    for (int pass = 0; pass < (a.hint_sig && !status_out ? 2 : 1); ++pass) {
+      if (pass == 1) a.hint_sig = 0u;
+      rc = run_sampled(a, L, vec, 3);
       if (rc != DPZ_OK) return rc;
+      if (post) {
+        rc = sliced_from_idx(a, ctrl_status);
+        if (rc != DPZ_OK) return rc;
+      }
+      if (status_out) return DPZ_OK;  // asynchronous: a nonzero status -> re-run with EXACT
+      DPZ_HIP_TRY(hipStreamSynchronize(a.st));
+      uint32_t st = 0;
+      DPZ_HIP_TRY(hipMemcpy(&st, ctrl_status, sizeof(st), hipMemcpyDeviceToHost));
+      if (st == 0) return DPZ_OK;
     }
-    if (status_out) return DPZ_OK;  // asynchronous: a nonzero status -> re-run with EXACT
-    DPZ_HIP_TRY(hipStreamSynchronize(a.st));
-    uint32_t st = 0;
-    DPZ_HIP_TRY(hipMemcpy(&st, ctrl_status, sizeof(st), hipMemcpyDeviceToHost));
-    if (st == 0) return DPZ_OK;
     a.status_out = nullptr;  // the miss wrote nothing: the exact path below
   }
   if (k > 0) {

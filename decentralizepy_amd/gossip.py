@@ -76,7 +76,7 @@ class GossipRound:
 
     def __init__(self, adj, x_init, alpha, rank=0, world=1, group=None, encode=None, fold=None,
                  device=None, streams=3, exchange="auto", hbm_budget=None, partial=None,
-                 combine=None, node_batch=True, node_group=4):
+                 combine=None, node_batch=True, node_group=4, guarded=True):
         """adj: adjacency sets of all nodes; x_init: (hi - lo, N) fp32 tensor with this rank's
         nodes' flat models (device tensor for the HIP codec).
 
@@ -93,6 +93,9 @@ class GossipRound:
         # node after node 5.50-5.61
         self.node_batch = node_batch
         self.node_group = max(1, int(node_group))
+        # guarded: (HIP, all-gather exchange) the folds follow the encodes with no host wait in
+        # between, guarded on the device by the encodes' status words (_step_guarded)
+        self.guarded = guarded
         self.n_nodes = len(adj)
         self.rank, self.world, self.group = rank, world, group
         # the exchange runs through the collectives with more than one rank, or whenever the
@@ -148,6 +151,9 @@ class GossipRound:
             self.rs_group = max(1, min(self.per, g))
         self.out = torch.empty_like(self.x)
         self.leg_times = None
+        # the encodes' sampled-path status words (padded to `per`: the all-gathered guard of the
+        # folds, _step_guarded); the injected CPU encodes never miss and leave them 0
+        self.status = torch.zeros(max(1, self.per), dtype=torch.int32, device=self.device)
         self.weights = [mh_weights(adj, i) for i in range(self.lo, self.hi)]
         self._encode = encode or self._hip_encode
         self._fold = fold or self._hip_fold
@@ -158,8 +164,7 @@ class GossipRound:
             from . import codec
             self.streams = [torch.cuda.Stream(self.device) for _ in range(max(1, streams))]
             self.wss = [codec.Workspace(self.device) for _ in self.streams]
-            self.status = torch.zeros(max(1, self.hi - self.lo), dtype=torch.int32,
-                                      device=self.device)
+
 
     # ---- default device implementations ---------------------------------------------------
     def _hip_encode(self, x, x0, k, counter, idx_out, val_out):
@@ -209,7 +214,7 @@ class GossipRound:
                 self.device)
         return tabs[key]
 
-    def _encode_nodes(self, m):
+    def _encode_nodes(self, m, check=True):
         """Every node's encode with one launch per phase (dpz_topk_encode_nodes): each node its
         own workspace; from the second round on every window is the node's previous one
         (DPZ_TOPK_HINT).  Returns False when (N, k) is not on the sampled path."""
@@ -241,14 +246,28 @@ class GossipRound:
         for st in self.streams:
             cur.wait_stream(st)
         self._primed = True
-        bad = torch.nonzero(self.status[:m]).flatten().tolist()
-        for j in bad:  # a missed node wrote nothing (no counter update either): exactly
-            codec.topk_encode(self.x[j], self.k, x0=self.x0[j], counter=self.counter[j],
-                              idx_out=self.send_idx[j], val_out=self.send_val[j],
-                              workspace=self.node_ws[j], exact=True)
+        if check:
+            self._rerun_missed(torch.nonzero(self.status[:m]).flatten().tolist())
         return True
 
-    def encode_all(self):
+    def _rerun_missed(self, bad):
+        """A missed sampled encode wrote nothing (no counter update either): re-run those nodes'
+        selections exactly (local node numbers)."""
+        if not self._hip:
+            for j in bad:
+                self._encode(self.x[j], self.x0[j], self.k, self.counter[j], self.send_idx[j],
+                             self.send_val[j])
+            return
+        from . import codec
+        for j in bad:
+            ws = self.node_ws[j] if getattr(self, "node_ws", None) is not None else self.wss[0]
+            codec.topk_encode(self.x[j], self.k, x0=self.x0[j], counter=self.counter[j],
+                              idx_out=self.send_idx[j], val_out=self.send_val[j],
+                              workspace=ws, exact=True)
+
+    def encode_all(self, check=True):
+        """Every owned node's encode.  check=False (HIP): the status words stay on the device
+        for the guarded fold (step); nothing here waits for the encodes."""
         if not self._hip:
             for j in range(self.hi - self.lo):
                 self._encode(self.x[j], self.x0[j], self.k, self.counter[j], self.send_idx[j],
@@ -256,7 +275,7 @@ class GossipRound:
             return
         from . import _lib, codec
         m = self.hi - self.lo
-        if self.node_batch and m > 1 and self._encode_nodes(m):
+        if self.node_batch and m > 1 and self._encode_nodes(m, check):
             return
         m, streams, ws_bytes, wsp = self._stream_args()
         cur = torch.cuda.current_stream(self.device)
@@ -278,11 +297,8 @@ class GossipRound:
         for st in self.streams:
             cur.wait_stream(st)
         # a sampled-path miss (rare) re-runs that node's selection exactly
-        bad = torch.nonzero(self.status[:m]).flatten().tolist()
-        for j in bad:  # the missed sampled call wrote nothing (no counter update either)
-            codec.topk_encode(self.x[j], self.k, x0=self.x0[j], counter=self.counter[j],
-                              idx_out=self.send_idx[j], val_out=self.send_val[j],
-                              workspace=self.wss[0], exact=True)
+        if check:
+            self._rerun_missed(torch.nonzero(self.status[:m]).flatten().tolist())
 
     def _hip_partial(self, payloads, weights, out):
         from . import codec
@@ -449,8 +465,38 @@ class GossipRound:
                     w=(ctypes.c_float * tot)(*w), w_self=(ctypes.c_float * max(1, m))(*ws_),
                     key=(self.recv_idx.data_ptr(), self.recv_val.data_ptr()))
 
-    def fold_all(self):
+    def fold_all(self, guard=None):
+        """Every owned node's Metro-Hastings fold.  guard (HIP, DEVICE int32): the round's
+        encode status words; the one-launch fold then writes nothing if any is nonzero
+        (dpz_decode_average_batch_guarded).  Returns False, with nothing enqueued, when the
+        guarded launch does not apply to this round (the caller checks the encodes first)."""
         nodes = range(self.hi - self.lo)
+        if guard is not None and not self._hip:  # the injected folds: the guard read on the host
+            if bool(guard.any()):
+                self.x0, self.out = self.out, self.x0
+            else:
+                self.fold_all()
+            return True
+        if guard is not None:
+            from . import _lib
+            from ._lib import DPZ_FOLD_ALSO_LOCAL, DPZ_FOLD_SELF
+            m = self.hi - self.lo
+            tab = getattr(self, "_tab", None)
+            if tab is None or tab["key"] != (self.recv_idx.data_ptr(), self.recv_val.data_ptr()):
+                tab = self._tab = self._fold_tables()
+            ptrs = getattr(self, "_fold_ptrs", None)
+            key = (self.x.data_ptr(), self.out.data_ptr())
+            if ptrs is None or ptrs[0] != key:
+                ptrs = self._fold_ptrs = (key, self._ptrs(self.x[:m]), self._ptrs(self.out[:m]))
+            rc = _lib.lib().dpz_decode_average_batch_guarded(
+                m, ptrs[1], ptrs[2], self.N, tab["np"], tab["idx"], tab["val"], tab["k"],
+                tab["w"], tab["w_self"], DPZ_FOLD_SELF | DPZ_FOLD_ALSO_LOCAL, guard.data_ptr(),
+                guard.numel(), ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
+            if rc == _lib.DPZ_ERR_UNSUPPORTED:
+                return False
+            _lib.check(rc, "dpz_decode_average_batch_guarded")
+            self.x0, self.out = self.out, self.x0
+            return True
         if self._hip:
             from . import _lib
             from ._lib import DPZ_FOLD_ALSO_LOCAL, DPZ_FOLD_SELF
@@ -492,6 +538,8 @@ class GossipRound:
 
     def step(self):
         t = self._leg_mark(None)
+        if self.exchange_mode == "allgather" and self.guarded:
+            return self._step_guarded(t)
         self.encode_all()
         t = self._leg_mark(t, "encode")
         if self.exchange_mode == "reduce_scatter":
@@ -500,4 +548,56 @@ class GossipRound:
         self.exchange()
         t = self._leg_mark(t, "exchange")
         self.fold_all()
+        self._leg_mark(t, "fold")
+
+    def _step_guarded(self, t):
+        """A round with no host wait between the encodes and the folds: the encodes' status words
+        (all-gathered with the payloads over the ranks) guard the one-launch folds on the device,
+        and the host reads them back once the encodes (and the exchange) are done — while the
+        folds run.  A miss (rare) left every fold unwritten: the missed nodes re-encode exactly,
+        the payloads are exchanged again and the round's folds re-run (every rank sees the same
+        gathered words, so all ranks take the same collectives)."""
+        m = self.hi - self.lo
+        self.encode_all(check=False)
+        t = self._leg_mark(t, "encode")
+        self.exchange()
+        if self.coll:
+            import torch.distributed as dist
+            if getattr(self, "status_all", None) is None:
+                self.status_all = torch.zeros(self.per * self.world, dtype=torch.int32,
+                                              device=self.device)
+            dist.all_gather_into_tensor(self.status_all, self.status[:self.per], group=self.group)
+            words = self.status_all
+        else:
+            words = self.status[:m]
+        cuda = self.device.type == "cuda"
+        host = getattr(self, "_status_host", None)
+        if host is None or host.numel() != words.numel():
+            host = self._status_host = torch.zeros(words.numel(), dtype=torch.int32,
+                                                   pin_memory=cuda)
+        host.copy_(words, non_blocking=cuda)
+        ev = None
+        if cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+        t = self._leg_mark(t, "exchange")
+        if not self.fold_all(guard=words):
+            if ev is not None:
+                ev.synchronize()
+            bad = [j for j in range(m) if int(host[self._slot(self.lo + j)]) != 0]
+            self._rerun_missed(bad)
+            if self.coll and bool(host.any()):
+                self.exchange()
+            self.fold_all()
+            self._leg_mark(t, "fold")
+            return
+        if ev is not None:
+            ev.synchronize()  # the encodes and the exchange only: the folds keep running
+        if bool(host.any()):
+            if cuda:
+                torch.cuda.synchronize(self.device)
+            self.x0, self.out = self.out, self.x0  # the guarded folds wrote nothing
+            self._rerun_missed([j for j in range(m) if int(host[self._slot(self.lo + j)]) != 0])
+            self.exchange()
+            self.fold_all()
         self._leg_mark(t, "fold")

@@ -237,7 +237,9 @@ int dpz_topk_encode_status(const float* x, const float* x0, float* acc, int acc_
  * n/8 mask bytes and the few planes a carry reaches.  status_out (DEVICE int32, may be NULL):
  * non-NULL = asynchronous, the final status written on `stream` (nonzero: the sampled path
  * missed, nothing was written; re-run with DPZ_TOPK_EXACT); NULL = blocking, a miss re-run
- * exactly inside the call.  flags: DPZ_TOPK_EXACT, DPZ_TOPK_SHARED, DPZ_TOPK_VAL_FP16.
+ * exactly inside the call (a DPZ_TOPK_HINT call that missed first runs the sampled path once
+ * more).  flags: DPZ_TOPK_EXACT, DPZ_TOPK_SHARED, DPZ_TOPK_VAL_FP16, DPZ_TOPK_HINT (the key
+ * window from the previous sampled encode's exact threshold on ws, as dpz_topk_encode).
  * dpz_counter_unslice / dpz_counter_slice convert between the sliced and the int32 counter
  * (DeviceCounter materialises on read); dpz_rewind_apply: acc[i] = 0 where the bit is set.      */
 int64_t dpz_mask_words(int64_t n);
@@ -320,6 +322,21 @@ int dpz_decode_average_batch(int m, const float* const* local, float* const* out
                              const float* const* vals, const int64_t* k, const float* w,
                              const float* w_self, int flags, void* const* ws, size_t ws_bytes,
                              int n_streams, const dpz_stream_t* streams);
+/* dpz_decode_average_batch's one-launch fold of a gossip round (every node 1..4 sparse payloads,
+ * flags within DPZ_FOLD_SELF | DPZ_FOLD_ALSO_LOCAL, 16-byte aligned rows, out[j] != local[j]) on
+ * ONE stream, guarded by the round's encodes: each launch first reads guard[0, guard_n) (DEVICE
+ * int32, e.g. dpz_topk_encode_nodes' status words) and, if any word is nonzero, writes nothing
+ * (out and, with DPZ_FOLD_ALSO_LOCAL, local unchanged), so the caller checks the encodes once
+ * after the round instead of between encode and fold, and re-runs the round's folds after
+ * re-running a missed encode exactly.  DPZ_ERR_UNSUPPORTED (nothing enqueued) when the batch
+ * does not qualify.  Replaces the reference's encode -> send -> receive -> _averaging order of
+ * every node (sharing/PartialModel.py:188-255, sharing/Sharing.py:156-190), run side by side. */
+int dpz_decode_average_batch_guarded(int m, const float* const* local, float* const* out,
+                                     int64_t n, const int* n_payloads,
+                                     const int32_t* const* idx, const float* const* vals,
+                                     const int64_t* k, const float* w, const float* w_self,
+                                     int flags, const int32_t* guard, int64_t guard_n,
+                                     dpz_stream_t stream);
 
 /* One codec step per node for m nodes of equal size (n, k): with DPZ_BATCH_ENCODE, node j's
  * dpz_topk_encode(x[j], x0[j], NULL, DPZ_ACC_NONE, x[j], n, k, idx_out[j], val_out[j],

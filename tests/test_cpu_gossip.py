@@ -200,3 +200,44 @@ def test_reduce_scatter_round_matches_within_tolerance(path, n, skew):
         assert lo is not None, xs
         ref = single.x.numpy()[lo:lo + xs.shape[0]]
         np.testing.assert_allclose(xs, ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("miss_round", [0, 1])
+def test_guarded_round_reruns_a_missed_encode(miss_round):
+    """The guarded round (encodes, exchange and folds with no host check in between; the encodes'
+    status words guard the folds): a node whose encode reports a miss — its payload poisoned —
+    leaves every fold of the round unwritten, is re-encoded, and the round's folds re-run, so the
+    models and counters equal the host-checked engine's (guarded=False) round for round."""
+    from decentralizepy_amd.gossip import GossipRound, read_edges
+    adj = read_edges(EDGES16)
+    n = 1500
+    x = _models(16, n)
+    a = GossipRound(adj, x, 0.05, encode=_oracle_encode, fold=_oracle_fold, guarded=True)
+    b = GossipRound(adj, x, 0.05, encode=_oracle_encode, fold=_oracle_fold, guarded=False)
+    orig = a.encode_all
+    state = {"r": 0, "reruns": 0}
+
+    def encode_all(check=True):
+        c5 = a.counter[5].clone()
+        orig(check)
+        if state["r"] == miss_round:  # node 5 "missed": no counter update, a garbage payload
+            a.counter[5] = c5
+            a.send_val[5].fill_(float("nan"))
+            a.status[5] = 1
+
+    def rerun(bad, _orig=a._rerun_missed):
+        state["reruns"] += len(bad)
+        a.status[list(bad)] = 0
+        _orig(bad)
+
+    a.encode_all = encode_all
+    a._rerun_missed = rerun
+    for r in range(2):
+        state["r"] = r
+        for eng in (a, b):
+            _train(eng, r)
+            eng.step()
+        np.testing.assert_array_equal(a.x.numpy().view(np.uint32), b.x.numpy().view(np.uint32))
+        np.testing.assert_array_equal(a.x0.numpy().view(np.uint32), b.x0.numpy().view(np.uint32))
+        np.testing.assert_array_equal(a.counter.numpy(), b.counter.numpy())
+    assert state["reruns"] == 1

@@ -103,19 +103,27 @@ def test_node_batched_encodes_equal_stream_encodes(dev):
     x = _models(len(adj), n)
     a = GossipRound(adj, x.to(dev), 0.01, node_batch=True)
     b = GossipRound(adj, x.to(dev), 0.01, node_batch=False)
+    # the host-checked round (a status check between encodes and folds) beside the guarded ones:
+    # a missed encode leaves the guarded folds unwritten and the round re-runs them
+    c = GossipRound(adj, x.to(dev), 0.01, node_batch=True, guarded=False)
     miss, _ = miss_layout(n, round(0.01 * n))
     for r in range(3):
         g = torch.Generator().manual_seed(300 + r)
         noise = (0.01 * torch.randn(len(adj), n, generator=g)).to(dev)
         if r == 2:
             noise[5] *= 4.0
-        for eng in (a, b):
+        for eng in (a, b, c):
             eng.x += noise
             if r == 0:
                 eng.x[3] = eng.x0[3] + torch.from_numpy(miss).to(dev)
             eng.step()
         torch.cuda.synchronize()
-        np.testing.assert_array_equal(a.x.cpu().numpy().view(np.uint32),
-                                      b.x.cpu().numpy().view(np.uint32))
-        np.testing.assert_array_equal(a.counter.cpu().numpy(), b.counter.cpu().numpy())
+        if r == 0:
+            assert int(a.status[:16].count_nonzero()) > 0  # the round's encodes did miss
+        for o in (b, c):
+            np.testing.assert_array_equal(a.x.cpu().numpy().view(np.uint32),
+                                          o.x.cpu().numpy().view(np.uint32))
+            np.testing.assert_array_equal(a.x0.cpu().numpy().view(np.uint32),
+                                          o.x0.cpu().numpy().view(np.uint32))
+            np.testing.assert_array_equal(a.counter.cpu().numpy(), o.counter.cpu().numpy())
     assert a.node_ws is not None and getattr(b, "node_ws", None) is None

@@ -145,3 +145,53 @@ def test_hint_with_fold_base_and_fp16(dev):
         outs.append([t.cpu().numpy().copy() for t in (i1, v1, base, i2, v2)])
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+@pytest.mark.parametrize("alpha,blocking", [(0.01, True), (0.1, False)])
+def test_hinted_sliced_rounds_match_oracle(dev, alpha, blocking):
+    """The JWINS encode in coalesced form (dpz_topk_encode_sliced: keys |W(x - x0) + acc|, values
+    W(x), the counter as bit planes, the selection mask) over a node's rounds with the prior
+    window: rounds 1-2 hinted (no sample launch), round 3 doubles the change scale (the window
+    misses: a blocking call runs the sampled path again, an asynchronous one reports the miss,
+    wrote nothing, and is re-run exactly), round 4 hinted again — every round's index set,
+    values, counter and mask bit-exact against the oracle."""
+    from decentralizepy_amd import codec
+    n = 2_000_003
+    k = round(alpha * n)
+    ws = codec.Workspace(dev)
+    planes = codec.counter_slice(torch.zeros(n, dtype=torch.int32, device=dev))
+    nw = codec.mask_words(n)
+    mask = torch.zeros(nw, dtype=torch.int32, device=dev)
+    o_cnt = np.zeros(n, dtype=np.int32)
+    rng = np.random.default_rng(11)
+    for r, scale in enumerate((0.01, 0.0104, 0.0108, 0.0216, 0.022)):
+        wx = rng.standard_normal(n).astype(np.float32)
+        wc = (scale * rng.standard_normal(n)).astype(np.float32)
+        acc = (0.5 * scale * rng.standard_normal(n)).astype(np.float32)
+        t = [torch.from_numpy(a).to(dev) for a in (wx, wc, acc)]
+        st = None if blocking else torch.full((1,), 7, dtype=torch.int32, device=dev)
+        io = torch.full((k,), 0x7FFFFFF0, dtype=torch.int32, device=dev)
+        idx, val = codec.topk_encode_sliced(t[1], k, mask, planes, acc=t[2],
+                                            acc_mode=codec.DPZ_ACC_ADD, vals_src=t[0],
+                                            idx_out=io, workspace=ws, status_out=st, hint=True)
+        c = _ctrl(ws)
+        # (an exact re-run leaves no prior: the asynchronous caller's next round samples again)
+        if r in (1, 2) or (r == 4 and blocking):
+            assert c[_HINTED] == 1 and c[_STATUS] == 0
+        if r == 3:
+            if blocking:
+                assert c[_HINTED] == 0 and codec.topk_sticky_status(ws, clear=True) != 0
+            else:
+                assert int(st.item()) != 0 and c[_HINTED] == 1
+                assert (io.cpu().numpy() == 0x7FFFFFF0).all()  # a miss writes nothing
+                codec.topk_sticky_status(ws, clear=True)
+                idx, val = codec.topk_encode_sliced(t[1], k, mask, planes, acc=t[2],
+                                                    acc_mode=codec.DPZ_ACC_ADD, vals_src=t[0],
+                                                    idx_out=io, workspace=ws, exact=True)
+        oi, ov = otopk.encode(wc, None, acc.copy(), otopk.ACC_ADD, k, vals_src=wx, counter=o_cnt)
+        np.testing.assert_array_equal(idx.cpu().numpy(), oi)
+        np.testing.assert_array_equal(_bits(val.cpu().numpy()), _bits(ov))
+        np.testing.assert_array_equal(codec.counter_unslice(planes, n).cpu().numpy(), o_cnt)
+        words = np.zeros(nw, dtype=np.uint32)
+        np.bitwise_or.at(words, oi >> 5, (np.uint32(1) << (oi & 31).astype(np.uint32)))
+        np.testing.assert_array_equal(mask.cpu().numpy().view(np.uint32), words)
