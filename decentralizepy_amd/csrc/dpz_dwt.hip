@@ -29,6 +29,9 @@ constexpr int DWT_TL = DPZ_DWT_TL;
 #ifndef DPZ_DWT4_WAVES  // the level-4 kernel (interior path)
 #define DPZ_DWT4_WAVES 4
 #endif
+#ifndef DPZ_DWT4_ACC_WAVES  // the level-4 accumulating kernel with the accumulator prefetch
+#define DPZ_DWT4_ACC_WAVES 4
+#endif
 #ifndef DPZ_IDWT_TILE
 #define DPZ_IDWT_TILE 4096
 #endif
@@ -88,6 +91,49 @@ __device__ __forceinline__ float acc_before(const Levels& LV, const float* dst, 
   const float o = *dst;
   if (LV.rmask && ((LV.rmask[pos >> 5] >> (pos & 31)) & 1u)) return 0.0f;
   return o;
+}
+
+// The accumulating pass's interior tiles (dwt4_kernel): every accumulator pair a thread
+// rewrites in the tile (level 1: up to 3, level 2: 2, level 3: 1, level 4: cA and cD) and its
+// mask words are loaded at the START of the tile, before the next tile's span loads are issued.
+// Loaded at the store instead (acc_pair), each pair was a dependent round trip behind a
+// vmcnt(0) wait that also drained the next tile's prefetched span: 6-8 exposed HBM latencies per
+// tile.  Slots: 0-2 level 1 (group t + 256 q), 3-4 level 2 (pair 1 + t + 256 j), 5 level 3,
+// 6 level-4 cA, 7 level-4 cD.  Loads are branch-free (an unused slot re-reads a valid word).
+#ifndef DPZ_DWT_ACC_PRE
+#define DPZ_DWT_ACC_PRE 1
+#endif
+constexpr int ACC_SLOTS = 8;
+struct AccPre {
+  dwt_f2u v[ACC_SLOTS];
+  uint32_t m0[ACC_SLOTS], m1[ACC_SLOTS];
+};
+
+__device__ __forceinline__ void acc_slot_load(const Levels& LV, const float* cd, int64_t nwords,
+                                              bool ok, int64_t pos, AccPre& P, int s) {
+  const int64_t q = ok ? pos : 0;
+  P.v[s] = *reinterpret_cast<const dwt_f2u*>(cd + q);
+  if (LV.rmask) {
+    const int64_t w = q >> 5;
+    P.m0[s] = LV.rmask[w];
+    P.m1[s] = LV.rmask[w + 1 < nwords ? w + 1 : w];
+  } else {
+    P.m0[s] = 0u;
+    P.m1[s] = 0u;
+  }
+}
+
+// the pair (pos, pos + 1) from its preloaded slot: (bit ? 0 : acc) + c
+__device__ __forceinline__ void acc_pair_pre(float* dst, int64_t pos, float a, float b,
+                                             const AccPre& P, int s) {
+  const uint32_t w0 = P.m0[s];
+  const uint32_t w1 = ((pos & 31) == 31) ? P.m1[s] : w0;
+  const float o0 = ((w0 >> (pos & 31)) & 1u) ? 0.0f : P.v[s].x;
+  const float o1 = ((w1 >> ((pos + 1) & 31)) & 1u) ? 0.0f : P.v[s].y;
+  dwt_f2u r;
+  r.x = o0 + a;
+  r.y = o1 + b;
+  *reinterpret_cast<dwt_f2u*>(dst) = r;
 }
 
 static inline Levels make_levels(int64_t n, int level) {
@@ -363,12 +409,43 @@ __device__ __forceinline__ float conv4v(float i0, float i1, float i2, float i3, 
   return acc;
 }
 
-template <bool WX, bool WD, bool ACCUM>
+// the tile's accumulator pairs and mask words, issued at the tile's start (AccPre above)
+__device__ __forceinline__ void acc_prefetch(const Levels& LV, const float* cd, int64_t tile,
+                                             AccPre& P) {
+  static_assert(DWT_NG <= 3 && DWT_IN2 / 2 <= 1 + 2 * 256 && DWT_IN3 / 2 <= 257 &&
+                (DWT_TL + 2) / 2 <= 257, "the slots cover every owned pair of a thread");
+  const int t = (int)threadIdx.x;
+  const int64_t nwords = (LV.total + 31) >> 5;
+  const int64_t s1 = tile * (8 * DWT_TL) - 16;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int G = t + 256 * q;
+    acc_slot_load(LV, cd, nwords, q < DWT_NG && G >= 8 && G < DWT_NGRP, LV.doff[1] + s1 + 2 * G,
+                  P, q);
+  }
+  const int64_t b2 = tile * (4 * DWT_TL) - 8;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int pp = 1 + t + 256 * j;
+    acc_slot_load(LV, cd, nwords, pp < DWT_IN2 / 2 && 2 * pp >= 8, LV.doff[2] + b2 + 2 * pp, P,
+                  3 + j);
+  }
+  const int64_t b3 = tile * (2 * DWT_TL) - 4;
+  acc_slot_load(LV, cd, nwords, 1 + t < DWT_IN3 / 2 && 2 * (1 + t) >= 4,
+                LV.doff[3] + b3 + 2 * (1 + t), P, 5);
+  const int64_t b4 = tile * DWT_TL - 2;
+  const bool ok4 = 1 + t < (DWT_TL + 2) / 2;
+  acc_slot_load(LV, cd, nwords, ok4, b4 + 2 * (1 + t), P, 6);
+  acc_slot_load(LV, cd, nwords, ok4, LV.doff[4] + b4 + 2 * (1 + t), P, 7);
+}
+
+template <bool WX, bool WD, bool ACCUM, bool PRE = false>
 __device__ __forceinline__ void dwt_int_level1(const Levels& LV, float* cx, float* cd, int64_t tile,
                                                const float4 (&va)[DWT_NG],
                                                const float4 (&vb)[DWT_NG],
                                                const float2 (&hx)[DWT_NG],
-                                               const float2 (&hb)[DWT_NG], float* smem) {
+                                               const float2 (&hb)[DWT_NG], float* smem,
+                                               const AccPre* P = nullptr) {
   float* L1[2] = {smem, smem + DWT_IN1};
   const int64_t s1 = tile * (8 * DWT_TL) - 16;  // level-1 position of LDS index 0
   const int lane = threadIdx.x & 63;
@@ -407,7 +484,8 @@ __device__ __forceinline__ void dwt_int_level1(const Levels& LV, float* cx, floa
         const float hi1 = conv4v(v[2], v[3], v[4], v[5], c_dec_hi);
         float* dst = (sp == 0 ? cx : cd) + LV.doff[1] + o;
         if (ACCUM && sp == 1) {
-          acc_pair(LV, dst, LV.doff[1] + o, hi0, hi1);
+          if constexpr (PRE) acc_pair_pre(dst, LV.doff[1] + o, hi0, hi1, *P, q);
+          else acc_pair(LV, dst, LV.doff[1] + o, hi0, hi1);
         } else {
           dst[0] = hi0;
           dst[1] = hi1;
@@ -420,12 +498,17 @@ __device__ __forceinline__ void dwt_int_level1(const Levels& LV, float* cx, floa
 // one level from LDS `in` (index 0 = position base_in) into LDS `out` (or cA at the top level):
 // outputs u in [2, nu), u = position - base_out, reading in[2u - 2 .. 2u + 1]; owned details for
 // u >= u_own.
-template <bool WX, bool WD, bool ACCUM, bool TOP>
+template <bool WX, bool WD, bool ACCUM, bool TOP, bool PRE = false>
 __device__ __forceinline__ void dwt_int_level(const Levels& LV, float* cx, float* cd, int l,
                                               int64_t base_out, int nu, int u_own, float* const* in,
-                                              float* const* out) {
-  const int npairs = nu / 2;  // pairs p = 1 .. npairs - 1 (u = 2p, 2p + 1)
-  for (int p = 1 + (int)threadIdx.x; p < npairs; p += 256) {
+                                              float* const* out, const AccPre* P = nullptr,
+                                              int slot0 = 0) {
+  const int npairs = nu / 2;  // pairs p = 1 .. npairs - 1 (u = 2p, 2p + 1): <= 2 per thread
+  // iteration j: the preloaded slot slot0 + j (TOP: cA slot0, cD slot0 + 1), compile-time
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int p = 1 + (int)threadIdx.x + 256 * j;
+    if (p >= npairs) break;
     const int u = 2 * p;
     const int64_t pos = base_out + u;
 #pragma unroll
@@ -442,7 +525,8 @@ __device__ __forceinline__ void dwt_int_level(const Levels& LV, float* cx, float
         if (u >= u_own) {
           float* dst = g + pos;
           if (acc) {
-            acc_pair(LV, dst, pos, lo0, lo1);
+            if constexpr (PRE) acc_pair_pre(dst, pos, lo0, lo1, *P, slot0);
+            else acc_pair(LV, dst, pos, lo0, lo1);
           } else {
             dst[0] = lo0;
             dst[1] = lo1;
@@ -456,7 +540,8 @@ __device__ __forceinline__ void dwt_int_level(const Levels& LV, float* cx, float
         const float hi1 = conv4v(B.x, B.y, B.z, B.w, c_dec_hi);
         float* dst = g + LV.doff[l] + pos;
         if (acc) {
-          acc_pair(LV, dst, LV.doff[l] + pos, hi0, hi1);
+          if constexpr (PRE) acc_pair_pre(dst, LV.doff[l] + pos, hi0, hi1, *P, TOP ? slot0 + 1 : slot0 + j);
+          else acc_pair(LV, dst, LV.doff[l] + pos, hi0, hi1);
         } else {
           dst[0] = hi0;
           dst[1] = hi1;
@@ -466,18 +551,22 @@ __device__ __forceinline__ void dwt_int_level(const Levels& LV, float* cx, float
   }
 }
 
-template <bool WX, bool WD, bool ACCUM>
+template <bool WX, bool WD, bool ACCUM, bool PRE = false>
 __device__ __forceinline__ void dwt_int_levels234(const Levels& LV, float* cx, float* cd,
-                                                  int64_t tile, float* smem) {
+                                                  int64_t tile, float* smem,
+                                                  const AccPre* P = nullptr) {
   float* L1[2] = {smem, smem + DWT_IN1};
   float* L2[2] = {smem + 2 * DWT_IN1, smem + 2 * DWT_IN1 + DWT_IN2};
   float* L3[2] = {smem + 2 * DWT_IN1 + 2 * DWT_IN2, smem + 2 * DWT_IN1 + 2 * DWT_IN2 + DWT_IN3};
   // level 2: positions 4 TL t - 8 + u, owned from u = 8
-  dwt_int_level<WX, WD, ACCUM, false>(LV, cx, cd, 2, tile * (4 * DWT_TL) - 8, DWT_IN2, 8, L1, L2);
+  dwt_int_level<WX, WD, ACCUM, false, PRE>(LV, cx, cd, 2, tile * (4 * DWT_TL) - 8, DWT_IN2, 8, L1,
+                                           L2, P, 3);
   __syncthreads();
-  dwt_int_level<WX, WD, ACCUM, false>(LV, cx, cd, 3, tile * (2 * DWT_TL) - 4, DWT_IN3, 4, L2, L3);
+  dwt_int_level<WX, WD, ACCUM, false, PRE>(LV, cx, cd, 3, tile * (2 * DWT_TL) - 4, DWT_IN3, 4, L2,
+                                           L3, P, 5);
   __syncthreads();
-  dwt_int_level<WX, WD, ACCUM, true>(LV, cx, cd, 4, tile * DWT_TL - 2, DWT_TL + 2, 2, L3, nullptr);
+  dwt_int_level<WX, WD, ACCUM, true, PRE>(LV, cx, cd, 4, tile * DWT_TL - 2, DWT_TL + 2, 2, L3,
+                                          nullptr, P, 6);
 }
 
 // Persistent grid (about as many blocks as the CUs hold at once, each walking tiles with a
@@ -519,7 +608,7 @@ __global__ void __launch_bounds__(256, DPZ_DWT_WAVES) dwt_kernel(const float* __
 // two phases, so the span path's registers do not add to the interior loop's (94 VGPRs alone,
 // 194 with both paths in one loop).
 template <bool WX, bool WD, bool ACCUM>
-__global__ void __launch_bounds__(256, DPZ_DWT4_WAVES) dwt4_kernel(const float* __restrict__ x,
+__global__ void __launch_bounds__(256, (ACCUM && WD && DPZ_DWT_ACC_PRE) ? DPZ_DWT4_ACC_WAVES : DPZ_DWT4_WAVES) dwt4_kernel(const float* __restrict__ x,
                                                    const float* __restrict__ x0, Levels LV,
                                                    float* cx, float* cd, int64_t tile0,
                                                    int64_t a, int64_t b, int64_t tile_hi) {
@@ -544,8 +633,11 @@ __global__ void __launch_bounds__(256, DPZ_DWT4_WAVES) dwt4_kernel(const float* 
   dwt_span(LV, tile, &s0, &e0);
   dwt_span_load<WD>(x, x0, n, s0, e0, va, vb);
   dwt_halo_load<WD>(x, x0, s0 & ~int64_t(3), hx, hb);
+  constexpr bool PRE = ACCUM && WD && DPZ_DWT_ACC_PRE != 0;
+  AccPre P;
   for (;;) {
-    dwt_int_level1<WX, WD, ACCUM>(LV, cx, cd, tile, va, vb, hx, hb, smem);
+    if constexpr (PRE) acc_prefetch(LV, cd, tile, P);  // before the next tile's span loads
+    dwt_int_level1<WX, WD, ACCUM, PRE>(LV, cx, cd, tile, va, vb, hx, hb, smem, &P);
     // the next tile's loads are in flight while this tile's levels 2-4 are computed
     const int64_t next = tile + gridDim.x;
     if (next < b) {
@@ -554,7 +646,7 @@ __global__ void __launch_bounds__(256, DPZ_DWT4_WAVES) dwt4_kernel(const float* 
       dwt_halo_load<WD>(x, x0, s0 & ~int64_t(3), hx, hb);
     }
     __syncthreads();  // level-1 approximations in LDS
-    dwt_int_levels234<WX, WD, ACCUM>(LV, cx, cd, tile, smem);
+    dwt_int_levels234<WX, WD, ACCUM, PRE>(LV, cx, cd, tile, smem, &P);
     __syncthreads();  // the next tile reuses the LDS buffers
     if (next >= b) break;
     tile = next;
