@@ -130,6 +130,67 @@ def h2d_array(arr, dtype, device, staging, name):
     return out
 
 
+def load_flat(model, flat_dev, staging, name, chunk=1 << 22):
+    """``model.load_state_dict(unflatten(flat_dev))`` (reference sharing/Sharing.py:186-190) with
+    the D2H pipelined against the host copy: the flat vector comes back in chunks of ``chunk``
+    elements (asynchronous DMAs into one pinned buffer, an event each), and each state tensor's
+    range is copied into the tensor as soon as its chunks have landed, so the copy of chunk i
+    overlaps the DMA of chunk i + 1.  Values, dtype conversion (``copy_``) and the tensors written
+    are those of ``load_state_dict``; a model with load_state_dict hooks, a flat size that does
+    not match, or a buffer over the pinned cap takes ``load_state_dict`` itself."""
+    sd = model.state_dict()
+    n = flat_dev.numel()
+    hooks = any(m._load_state_dict_pre_hooks or m._load_state_dict_post_hooks
+                for m in model.modules())
+    host = None if hooks or sum(v.numel() for v in sd.values()) != n else \
+        staging.get(name, n, torch.float32)
+    if host is None:
+        flat = flat_dev.cpu()
+        out, start = {}, 0
+        for key, v in sd.items():
+            out[key] = flat[start:start + v.numel()].view(v.shape)
+            start += v.numel()
+        model.load_state_dict(out)
+        return
+    stream = torch.cuda.current_stream(flat_dev.device)
+    chunk = max(int(chunk), 1)
+    landed = []
+    for s0 in range(0, n, chunk):
+        e0 = min(n, s0 + chunk)
+        host[s0:e0].copy_(flat_dev[s0:e0], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        landed.append((e0, ev))
+    ci, done = 0, 0
+
+    def wait_to(end):
+        nonlocal ci, done
+        while done < end:
+            e0, ev = landed[ci]
+            ev.synchronize()
+            done, ci = e0, ci + 1
+
+    with torch.no_grad():
+        start = 0
+        for v in sd.values():
+            end = start + v.numel()
+            if v.is_cuda:  # a device-resident model: one device copy
+                v.copy_(flat_dev[start:end].view(v.shape))
+            elif v.is_contiguous():
+                flat_v = v.view(-1)
+                a = start
+                while a < end:  # the tensor's range chunk by chunk, as the chunks land
+                    b = min(end, (a // chunk + 1) * chunk)
+                    wait_to(b)
+                    flat_v[a - start:b - start].copy_(host[a:b])
+                    a = b
+            else:
+                wait_to(end)
+                v.copy_(host[start:end].view(v.shape))
+            start = end
+    wait_to(n)  # the pinned buffer is free for the next call
+
+
 class PayloadNames:
     """Pinned-buffer names for received payload legs: a ring of ``slots`` names, so consecutive
     legs use distinct buffers and a reused buffer waits only for its own earlier DMA (Staging).

@@ -18,8 +18,8 @@ import numpy as np
 import torch
 
 from .. import codec
-from .._device import (PayloadNames, Staging, flatten_state, h2d_array, pick_device,
-                       state_to_device, to_host)
+from .._device import (PayloadNames, Staging, flatten_state, h2d_array, load_flat,
+                       pick_device, state_to_device, to_host)
 
 
 class Sharing:
@@ -155,9 +155,8 @@ class Sharing:
                                     workspace=self.workspace)
 
     def _load_flat(self, out_dev):
-        # a view of the pinned buffer: load_state_dict copies it into the model at once
-        flat = to_host(out_dev, self.staging, "result", own=False)
-        self.model.load_state_dict(self._unflatten(flat))
+        # load_state_dict of the averaged model with its D2H pipelined against the host copy
+        load_flat(self.model, out_dev, self.staging, "result")
 
     def _averaging(self, peer_deques):
         """Metro-Hastings average of the received models with the local one

@@ -5,6 +5,7 @@ from collections import deque
 
 import numpy as np
 import pytest
+import torch
 
 from tests import scenario
 
@@ -128,3 +129,32 @@ def test_staging_over_cap_falls_back_to_pageable_copies(dev):
     assert np.array_equal(to_host(torch.from_numpy(a).to(dev), st, "out"), a)
     small = to_device_flat(torch.ones(100), dev, st, "small")  # within the cap: pinned
     assert st.total == 400 and torch.equal(small.cpu(), torch.ones(100))
+
+
+@pytest.mark.parametrize("chunk", [1000, 1 << 22])
+def test_load_flat_pipelined_equals_load_state_dict(dev, chunk):
+    """The averaged model's D2H pipelined against its copy into the model (_device.load_flat:
+    chunked DMAs, each state tensor filled range by range as its chunks land) leaves every state
+    tensor — fp32 parameters and BatchNorm's int64 counter — exactly as load_state_dict of the
+    unflattened vector does (reference sharing/Sharing.py:186-190)."""
+    import copy
+
+    from decentralizepy_amd._device import Staging, load_flat
+    torch.manual_seed(3)
+    model = torch.nn.Sequential(torch.nn.Linear(300, 200), torch.nn.BatchNorm1d(200),
+                                torch.nn.Linear(200, 7))
+    ref = copy.deepcopy(model)
+    sd = ref.state_dict()
+    n = sum(v.numel() for v in sd.values())
+    flat = torch.randn(n)
+    out, s = {}, 0
+    for key, v in sd.items():
+        if v.dtype == torch.int64:
+            flat[s:s + v.numel()] = 41.0
+        out[key] = flat[s:s + v.numel()].view(v.shape)
+        s += v.numel()
+    ref.load_state_dict(out)
+    load_flat(model, flat.to(dev), Staging(), "result", chunk=chunk)
+    for (k1, a), (k2, b) in zip(model.state_dict().items(), ref.state_dict().items()):
+        assert k1 == k2 and a.dtype == b.dtype
+        assert torch.equal(a, b), k1

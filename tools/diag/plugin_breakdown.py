@@ -21,6 +21,14 @@ from decentralizepy_amd.compression import Elias, EliasFpzip  # noqa: E402
 from decentralizepy_amd.sharing import PartialModel, Sharing  # noqa: E402
 from decentralizepy_amd.sharing.JWINS import Wavelet  # noqa: E402
 
+if os.environ.get("LOAD_FLAT_OLD") == "1":  # A/B: the unpipelined D2H + load_state_dict
+    from decentralizepy_amd._device import to_host
+
+    def _load_flat_old(self, out_dev):
+        flat = to_host(out_dev, self.staging, "result", own=False)
+        self.model.load_state_dict(self._unflatten(flat))
+    Sharing.Sharing._load_flat = _load_flat_old
+
 kind = sys.argv[1] if len(sys.argv) > 1 else "jwins"
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 acc = defaultdict(list)
