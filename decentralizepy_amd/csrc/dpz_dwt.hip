@@ -29,9 +29,6 @@ constexpr int DWT_TL = DPZ_DWT_TL;
 #ifndef DPZ_DWT4_WAVES  // the level-4 kernel (interior path)
 #define DPZ_DWT4_WAVES 4
 #endif
-#ifndef DPZ_DWT4_LATE
-#define DPZ_DWT4_LATE 0
-#endif
 #ifndef DPZ_DWT4_ACC_WAVES  // the level-4 accumulating kernel with the accumulator prefetch
 #define DPZ_DWT4_ACC_WAVES 4
 #endif
@@ -642,20 +639,14 @@ __global__ void __launch_bounds__(256, (ACCUM && WD && DPZ_DWT_ACC_PRE) ? DPZ_DW
     if constexpr (PRE) acc_prefetch(LV, cd, tile, P);  // before the next tile's span loads
     dwt_int_level1<WX, WD, ACCUM, PRE>(LV, cx, cd, tile, va, vb, hx, hb, smem, &P);
     // the next tile's loads are in flight while this tile's levels 2-4 are computed
-    // (DPZ_DWT4_LATE: issued after them instead, A/B)
     const int64_t next = tile + gridDim.x;
-    if (!DPZ_DWT4_LATE && next < b) {
+    if (next < b) {
       dwt_span(LV, next, &s0, &e0);
       dwt_span_load<WD>(x, x0, n, s0, e0, va, vb);
       dwt_halo_load<WD>(x, x0, s0 & ~int64_t(3), hx, hb);
     }
     __syncthreads();  // level-1 approximations in LDS
     dwt_int_levels234<WX, WD, ACCUM, PRE>(LV, cx, cd, tile, smem, &P);
-    if (DPZ_DWT4_LATE && next < b) {
-      dwt_span(LV, next, &s0, &e0);
-      dwt_span_load<WD>(x, x0, n, s0, e0, va, vb);
-      dwt_halo_load<WD>(x, x0, s0 & ~int64_t(3), hx, hb);
-    }
     __syncthreads();  // the next tile reuses the LDS buffers
     if (next >= b) break;
     tile = next;
