@@ -59,11 +59,29 @@ static inline HaarLevels haar_levels(int64_t n, int level) {
   return L;
 }
 
+// The accumulating pipeline's outputs of a chunk (acc += W(x - prev) with the deferred rewind)
+// are collected in compile-time slots and their accumulator words (and mask words) loaded
+// together, one round trip per chunk: read at each store instead, every output waited on its own
+// load with vmcnt(0) (seen in the ISA), which also waited for the chunk's earlier stores.
+// Slots: 0-1 level-1 detail, 2-3 level-1 approximation (L = 1), 4 level-2 detail, 5 level-2
+// approximation (L = 2), 6 + (l - 3) level-l detail (l = 3..8), 12 the level-L approximation
+// (L >= 3).
+#ifndef DPZ_HAAR_ACC_BATCH
+#define DPZ_HAAR_ACC_BATCH 1
+#endif
+constexpr int HAAR_SLOTS = 13;
+struct HaarAcc {
+  float v[HAAR_SLOTS];
+  int64_t pos[HAAR_SLOTS];
+  bool on[HAAR_SLOTS];
+};
+
 template <bool WX, bool WD, bool ACCUM>
 __global__ void __launch_bounds__(256) haar_dwt_kernel(const float* __restrict__ x,
                                                        const float* __restrict__ x0, HaarLevels LV,
                                                        float* cx, float* cd, int64_t nchunks,
                                                        int vec) {
+  constexpr bool BATCH = ACCUM && WD && DPZ_HAAR_ACC_BATCH != 0;
   const int lane = threadIdx.x & 63;
   const int64_t n = LV.len[0];
   const int L = LV.level;
@@ -99,6 +117,31 @@ __global__ void __launch_bounds__(256) haar_dwt_kernel(const float* __restrict__
       const int64_t c = c0 + u;
       if (c >= nchunks) break;  // wave-uniform
       const int64_t p = c * HAAR_CHUNK + 4 * lane;
+      HaarAcc A;
+      if constexpr (BATCH) {
+#pragma unroll
+        for (int q = 0; q < HAAR_SLOTS; ++q) {
+          A.on[q] = false;
+          A.pos[q] = 0;
+          A.v[q] = 0.0f;
+        }
+      }
+      // an output of pipeline s at coefficient position ps: stored now, or (the accumulating
+      // pipeline) kept in slot q for the chunk's batched read-modify-write
+      auto emit = [&](int s, int q, int64_t ps, float val) {
+        float* out = s == 0 ? cx : cd;
+        if (ACCUM && s == 1) {
+          if constexpr (BATCH) {
+            A.on[q] = true;
+            A.pos[q] = ps;
+            A.v[q] = val;
+          } else {
+            out[ps] = hacc_before(LV, out, out + ps) + val;
+          }
+        } else {
+          out[ps] = val;
+        }
+      };
       // pipelines: 0 = x, 1 = x - x0
       float v[2][4];
       v[0][0] = va[u].x; v[0][1] = va[u].y; v[0][2] = va[u].z; v[0][3] = va[u].w;
@@ -116,8 +159,6 @@ __global__ void __launch_bounds__(256) haar_dwt_kernel(const float* __restrict__
       for (int s = 0; s < 2; ++s) {
         if (s == 0 && !WX) continue;
         if (s == 1 && !WD) continue;
-        float* out = s == 0 ? cx : cd;
-        const bool acc = ACCUM && s == 1;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const float a = v[s][2 * j], b = v[s][2 * j + 1];
@@ -127,71 +168,78 @@ __global__ void __launch_bounds__(256) haar_dwt_kernel(const float* __restrict__
           hi = hi + h * a;
           lo1[s][j] = lo;
           if (q + j < LV.len[1]) {
-            if (L == 1) {
-              float* pa = out + q + j;
-              *pa = acc ? hacc_before(LV, out, pa) + lo : lo;
-            }
-            float* pd = out + LV.doff[1] + q + j;
-            *pd = acc ? hacc_before(LV, out, pd) + hi : hi;
+            if (L == 1) emit(s, 2 + j, q + j, lo);
+            emit(s, j, LV.doff[1] + q + j, hi);
           }
         }
       }
-      if (L == 1) continue;
-      // level 2: position r = p / 4 from the lane's two level-1 values
-      const int64_t r = p >> 2;
-      float cur[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        if (s == 0 && !WX) continue;
-        if (s == 1 && !WD) continue;
-        float* out = s == 0 ? cx : cd;
-        const bool acc = ACCUM && s == 1;
-        const float a = lo1[s][0];
-        const float b = (q + 1 == LV.len[1]) ? a : lo1[s][1];
-        float lo = h * b;
-        lo = lo + h * a;
-        float hi = (-h) * b;
-        hi = hi + h * a;
-        cur[s] = lo;
-        if (r < LV.len[2]) {
-          if (L == 2) {
-            float* pa = out + r;
-            *pa = acc ? hacc_before(LV, out, pa) + lo : lo;
-          }
-          float* pd = out + LV.doff[2] + r;
-          *pd = acc ? hacc_before(LV, out, pd) + hi : hi;
-        }
-      }
-      // levels 3..L: lane pairs (stride s2) across the wave; the lane holds the level-(l-1) value
-      // at position r >> (l - 3) when lane % s2 == 0
-      for (int l = 3; l <= L; ++l) {
-        const int s2 = 1 << (l - 3);
-        const int64_t pos = r >> (l - 3);        // this lane's level-(l-1) position (if active)
-        const int64_t o = pos >> 1;              // level-l output position
-        const bool active = (lane & (2 * s2 - 1)) == 0;
+      if (L > 1) {
+        // level 2: position r = p / 4 from the lane's two level-1 values
+        const int64_t r = p >> 2;
+        float cur[2];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           if (s == 0 && !WX) continue;
           if (s == 1 && !WD) continue;
-          const float other = __shfl_down(cur[s], s2, 64);
-          if (active) {
-            float* out = s == 0 ? cx : cd;
-            const bool acc = ACCUM && s == 1;
-            const float a = cur[s];
-            const float b = (pos + 1 == LV.len[l - 1]) ? a : other;
-            float lo = h * b;
-            lo = lo + h * a;
-            float hi = (-h) * b;
-            hi = hi + h * a;
-            cur[s] = lo;
-            if (o < LV.len[l]) {
-              if (l == L) {
-                float* pa = out + o;
-                *pa = acc ? hacc_before(LV, out, pa) + lo : lo;
+          const float a = lo1[s][0];
+          const float b = (q + 1 == LV.len[1]) ? a : lo1[s][1];
+          float lo = h * b;
+          lo = lo + h * a;
+          float hi = (-h) * b;
+          hi = hi + h * a;
+          cur[s] = lo;
+          if (r < LV.len[2]) {
+            if (L == 2) emit(s, 5, r, lo);
+            emit(s, 4, LV.doff[2] + r, hi);
+          }
+        }
+        // levels 3..L: lane pairs (stride s2) across the wave; the lane holds the level-(l-1)
+        // value at position r >> (l - 3) when lane % s2 == 0
+#pragma unroll
+        for (int l = 3; l <= HAAR_MAX_LEVEL; ++l) {
+          if (l > L) break;  // uniform
+          const int s2 = 1 << (l - 3);
+          const int64_t pos = r >> (l - 3);        // this lane's level-(l-1) position (if active)
+          const int64_t o = pos >> 1;              // level-l output position
+          const bool active = (lane & (2 * s2 - 1)) == 0;
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            if (s == 0 && !WX) continue;
+            if (s == 1 && !WD) continue;
+            const float other = __shfl_down(cur[s], s2, 64);
+            if (active) {
+              const float a = cur[s];
+              const float b = (pos + 1 == LV.len[l - 1]) ? a : other;
+              float lo = h * b;
+              lo = lo + h * a;
+              float hi = (-h) * b;
+              hi = hi + h * a;
+              cur[s] = lo;
+              if (o < LV.len[l]) {
+                if (l == L) emit(s, 12, o, lo);
+                emit(s, 6 + (l - 3), LV.doff[l] + o, hi);
               }
-              float* pd = out + LV.doff[l] + o;
-              *pd = acc ? hacc_before(LV, out, pd) + hi : hi;
             }
+          }
+        }
+      }
+      if constexpr (BATCH) {
+        // the chunk's accumulator and mask words, all loads issued before any is used
+        // (branch-free: an unused slot re-reads word 0), then the stores
+        float o[HAAR_SLOTS];
+        uint32_t m[HAAR_SLOTS];
+#pragma unroll
+        for (int k = 0; k < HAAR_SLOTS; ++k) {
+          const int64_t ps = A.on[k] ? A.pos[k] : 0;
+          o[k] = cd[ps];
+          m[k] = LV.rmask ? LV.rmask[ps >> 5] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < HAAR_SLOTS; ++k) {
+          if (A.on[k]) {
+            const int64_t ps = A.pos[k];
+            const float before = ((m[k] >> (ps & 31)) & 1u) ? 0.0f : o[k];
+            cd[ps] = before + A.v[k];
           }
         }
       }
