@@ -46,13 +46,13 @@ constexpr int FOLD_MAXP = 16;  // payloads per launch (longer lists are chained)
 constexpr int FOLD_THREADS = DPZ_FOLD_THREADS;
 constexpr int FOLD_GROUPS = FOLD_TILE / (4 * FOLD_THREADS);  // float4 groups per thread
 constexpr int FOLD_EQ = 4;  // payload entries per thread preloaded at tile start
-constexpr int FOLD_POOL = 192;  // hit path: pool rows of the elements hit twice or more in a tile
+constexpr int FOLD_POOL = 64;  // hit-chain path: elements hit by >= 3 payloads folded from LDS rows
 constexpr int FOLD_NB = 4;  // phase path: next payload's extra entries per thread prefetched
-// hit path: per-element hit count (u32), first value (f32), the tile's local values, the
-// distinct-hit list (u16 x 2816), first payload and pool row (u8 each): 62 KB of LDS (2 blocks of
-// 512 threads per CU with the 13 KB pool, as the registers allow)
+// hit-chain path: per-element chain head (u32) + per-entry value and (next | payload << 16),
+// the tile's local values and the distinct-hit list: 61 KB of LDS at 2816 entries (2 blocks of
+// 512 threads per CU, as the registers allow)
 constexpr int FOLD_CAP = FOLD_TILE / 16 * 11;
-constexpr int FOLD_LDS_MASK = FOLD_TILE * 4 * 3 + FOLD_CAP * 2 + FOLD_TILE * 2;
+constexpr int FOLD_LDS_MASK = FOLD_TILE * 4 + FOLD_CAP * 8 + FOLD_TILE * 4 + FOLD_CAP * 2;
 constexpr int FOLD_LDS_PHASE = FOLD_TILE * 4 + FOLD_TILE;
 constexpr int FOLD_LDS_BYTES = FOLD_LDS_MASK > FOLD_LDS_PHASE ? FOLD_LDS_MASK : FOLD_LDS_PHASE;
 
@@ -163,8 +163,7 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
   __shared__ const __attribute__((address_space(1))) float* s_val[FOLD_MAXP];
   __shared__ uint32_t s_nhit;
   __shared__ uint32_t s_pool_n;                // rows of s_pool taken in this tile
-  __shared__ float s_pool[FOLD_POOL][FOLD_MAXP];  // hit path: further hits of multi-hit elements
-  __shared__ uint32_t s_pmask[FOLD_POOL];          // their payloads (bit p)
+  __shared__ float s_pool[FOLD_POOL][FOLD_MAXP];  // payload values of elements hit >= 3 times
   __shared__ float s_w[FOLD_MAXP];
   if (t == 0) {
     for (int p = 0; p < a.np; ++p) {
@@ -275,28 +274,20 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
     }
   }
 
-  // the hit path keeps every entry of the tile in the FOLD_EQ registers per thread (its scatter
-  // revisits them after a barrier); a tile past them, or past the pool, takes the phase path
-  bool hit_path = a.all_sparse && etot <= FOLD_CAP && etot <= FOLD_EQ * FOLD_THREADS;
-  if (hit_path) {
-    // Hit path.  The fold is VALU-bound when every element runs the per-payload select
+  if (a.all_sparse && etot <= FOLD_CAP) {
+    // Hit-chain path.  The fold is VALU-bound when every element runs the per-payload select
     // (16 payloads x 8 elements x ~6 instructions per thread), so it is split:
     //  A) every element folds its base value alone (no hits): 2 flops per payload term, packed;
     //  B) the tile's hit elements (~15 % at 16 payloads x 1 %), compacted to a list, are folded
     //     exactly with their payload values by one thread each and overwrite A's result.
-    // Scatter without chains: cnt[pos] counts an element's hits (LDS atomicAdd); the first hit
-    // keeps its value and payload in v0 / p0, and the element of a second hit takes a pool row
-    // (after a barrier) into which its further hits write by payload — so B reads an element in
-    // ONE LDS round trip (cnt, v0, p0, the local value) instead of walking a chain (3 dependent
-    // reads per element; 4.1 us of the 8.7 us tile iteration at 16 x 1 %, fold stamps, MI355X).
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(lds_raw);       // hits; B's result afterwards
-    float* v0 = reinterpret_cast<float*>(cnt + FOLD_TILE);       // the first hit's value
-    float* lv = v0 + FOLD_TILE;                                  // the tile's local values
+    // Entries are pushed on per-element hit chains (head[pos] -> j -> ...) in one scatter phase.
+    uint32_t* head = reinterpret_cast<uint32_t*>(lds_raw);
+    uint32_t* meta = head + FOLD_TILE;                       // next (low 16) | payload << 16
+    float* ev = reinterpret_cast<float*>(meta + FOLD_CAP);
+    float* lv = ev + FOLD_CAP;                               // the tile's local values
     uint16_t* hitl = reinterpret_cast<uint16_t*>(lv + FOLD_TILE);  // distinct hit elements
-    uint8_t* p0 = reinterpret_cast<uint8_t*>(hitl + FOLD_CAP);   // the first hit's payload
-    uint8_t* rowid = p0 + FOLD_TILE;                             // pool row of a multi-hit element
     for (int j = t * 4; j < FOLD_TILE; j += 4 * FOLD_THREADS)
-      *reinterpret_cast<uint4*>(&cnt[j]) = make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4*>(&head[j]) = make_uint4(~0u, ~0u, ~0u, ~0u);
 #pragma unroll
     for (int q = 0; q < FOLD_GROUPS; ++q)
       *reinterpret_cast<float4*>(&lv[q * 4 * FOLD_THREADS + t * 4]) =
@@ -306,69 +297,45 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
       s_pool_n = 0;
     }
     __syncthreads();
-    // S1: every entry counts its element; the first keeps its value / payload and lists it
-    uint32_t slot[FOLD_EQ];
 #pragma unroll
     for (int q = 0; q < FOLD_EQ; ++q) {
-      slot[q] = ~0u;
-      const int64_t pos = (int64_t)ei[q] - tlo;
-      if (ep[q] >= 0 && pos >= 0 && pos < FOLD_TILE) {  // guards against an unsorted array
-        const uint32_t sl = atomicAdd(&cnt[pos], 1u);
-        slot[q] = sl;
-        if (sl == 0) {
-          v0[pos] = evl[q];
-          p0[pos] = (uint8_t)ep[q];
-          hitl[atomicAdd(&s_nhit, 1u)] = (uint16_t)pos;
+      if (ep[q] >= 0) {
+        const int32_t j = t + q * FOLD_THREADS;
+        const int64_t pos = (int64_t)ei[q] - tlo;
+        ev[j] = evl[q];
+        if (pos >= 0 && pos < FOLD_TILE) {  // guards against an unsorted caller array
+          const uint32_t old = atomicExch(&head[pos], (uint32_t)j);
+          meta[j] = (old & 0xFFFFu) | ((uint32_t)ep[q] << 16);
+          if (old == ~0u) hitl[atomicAdd(&s_nhit, 1u)] = (uint16_t)pos;
         }
       }
     }
-    int more = 0;
+    for (int32_t j = FOLD_EQ * FOLD_THREADS + t; j < etot; j += FOLD_THREADS) {
+      // payload of flattened entry j: binary search over pre[0..15] (pre[u] = etot > j for
+      // u >= np), four dependent LDS reads instead of a read per payload
+      int p = 0;
 #pragma unroll
-    for (int q = 0; q < FOLD_EQ; ++q) more |= (slot[q] != ~0u && slot[q] >= 1u) ? 1 : 0;
-    // S2 (rare): the second entry of an element takes its pool row
-    if (__syncthreads_or(more)) {
-#pragma unroll
-      for (int q = 0; q < FOLD_EQ; ++q) {
-        if (slot[q] == 1u) {
-          const uint32_t r = atomicAdd(&s_pool_n, 1u);
-          rowid[ei[q] - (int32_t)tlo] = (uint8_t)(r < FOLD_POOL ? r : 0u);
-          if (r < FOLD_POOL) s_pmask[r] = 0u;
-        }
-      }
-      __syncthreads();
-      if (s_pool_n > FOLD_POOL) {
-        hit_path = false;  // uniform: the phase path folds this tile
-      } else {
-        // S3: the further hits into the element's row, by payload
-#pragma unroll
-        for (int q = 0; q < FOLD_EQ; ++q) {
-          if (slot[q] != ~0u && slot[q] >= 1u) {
-            const uint32_t r = rowid[ei[q] - (int32_t)tlo];
-            s_pool[r][ep[q]] = evl[q];
-            atomicOr(&s_pmask[r], 1u << ep[q]);
-          }
-        }
-        __syncthreads();
+      for (int s = FOLD_MAXP / 2; s >= 1; s >>= 1) p += pre[p + s] <= j ? s : 0;
+      const int64_t src = (int64_t)rng[p][0] + (j - pre[p]);
+      const int64_t pos = (int64_t)s_idx[p][src] - tlo;
+      ev[j] = s_val[p][src];
+      if (pos >= 0 && pos < FOLD_TILE) {
+        const uint32_t old = atomicExch(&head[pos], (uint32_t)j);
+        meta[j] = (old & 0xFFFFu) | ((uint32_t)p << 16);
+        if (old == ~0u) hitl[atomicAdd(&s_nhit, 1u)] = (uint16_t)pos;
       }
     }
-  }
-  if (hit_path) {
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(lds_raw);
-    float* v0 = reinterpret_cast<float*>(cnt + FOLD_TILE);
-    float* lv = v0 + FOLD_TILE;
-    uint16_t* hitl = reinterpret_cast<uint16_t*>(lv + FOLD_TILE);
-    uint8_t* p0 = reinterpret_cast<uint8_t*>(hitl + FOLD_CAP);
-    uint8_t* rowid = p0 + FOLD_TILE;
+    __syncthreads();
     FSTAMP(2);
     // A) base fold of this thread's elements; remember which of them carry hits
     uint32_t hitbits = 0;
 #pragma unroll
     for (int q = 0; q < FOLD_GROUPS; ++q) {
-      const uint4 h4 = *reinterpret_cast<const uint4*>(&cnt[q * 4 * FOLD_THREADS + t * 4]);
-      hitbits |= ((h4.x != 0u) ? 1u : 0u) << (4 * q);
-      hitbits |= ((h4.y != 0u) ? 1u : 0u) << (4 * q + 1);
-      hitbits |= ((h4.z != 0u) ? 1u : 0u) << (4 * q + 2);
-      hitbits |= ((h4.w != 0u) ? 1u : 0u) << (4 * q + 3);
+      const uint4 h4 = *reinterpret_cast<const uint4*>(&head[q * 4 * FOLD_THREADS + t * 4]);
+      hitbits |= ((h4.x != ~0u) ? 1u : 0u) << (4 * q);
+      hitbits |= ((h4.y != ~0u) ? 1u : 0u) << (4 * q + 1);
+      hitbits |= ((h4.z != ~0u) ? 1u : 0u) << (4 * q + 2);
+      hitbits |= ((h4.w != ~0u) ? 1u : 0u) << (4 * q + 3);
     }
     {
       typedef float f2 __attribute__((ext_vector_type(2)));
@@ -384,7 +351,7 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
       } else {
         // weights from LDS (uniform reads); an unrolled loop over scalar weights spilled SGPRs
         // into VGPR lanes and cost occupancy
-        int pp0 = 0;
+        int p0 = 0;
         if (a.first) {
           const float w = s_w[0];
           const f2 w2 = {w, w};
@@ -393,9 +360,9 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
             const f2 term = b2[h] * w2;
             a2[h] = a.zero_base ? f2{0.0f, 0.0f} + term : term;
           }
-          pp0 = 1;
+          p0 = 1;
         }
-        for (int p = pp0; p < a.np; ++p) {
+        for (int p = p0; p < a.np; ++p) {
           const float w = s_w[p];
           const f2 w2 = {w, w};
 #pragma unroll
@@ -414,61 +381,85 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
       load_local(tile + gridDim.x);
       l_ahead = true;
     }
-    __syncthreads();  // every owner has read its hit flags before B overwrites cnt[]
+    __syncthreads();  // every owner has read its hit flags before B overwrites head[]
     FSTAMP(3);
-    // B) exact fold of the hit elements, two per thread: an element's count, first hit and local
-    //    value in one LDS round trip; an element hit twice or more (rare) also reads its pool
-    //    row.  The result replaces cnt[pos].
+    // B) exact fold of the hit elements, two per thread with their chain walks interleaved
+    //    (the walks are dependent LDS reads: one latency for both); the result replaces
+    //    head[pos].  The usual one or two hits of an element fold branch-free; an element with
+    //    three or more (rare) is refolded by the general chain walk.
     const uint32_t nhit = s_nhit;
+    float wr[FOLD_MAXP];
+#pragma unroll
+    for (int p = 0; p < FOLD_MAXP; ++p) wr[p] = s_w[p];
     for (uint32_t s0 = t; s0 < nhit; s0 += 2 * FOLD_THREADS) {
       const uint32_t s1 = s0 + FOLD_THREADS;
       const bool two = s1 < nhit;
       int pos[2];
       pos[0] = hitl[s0];
       pos[1] = two ? hitl[s1] : pos[0];
-      float bb[2], av[2], hv0[2];
-      uint32_t hp0[2], c[2], row[2], msk[2];
+      float bb[2], av[2], v1[2], v2[2];
+      uint32_t p1[2], p2[2], more[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        c[h] = cnt[pos[h]];
-        hv0[h] = v0[pos[h]];
-        hp0[h] = p0[pos[h]];
-        row[h] = rowid[pos[h]];
         bb[h] = a.zero_base ? 0.0f : lv[pos[h]];
         av[h] = a.first ? 0.0f : a.out[tlo + pos[h]];
+        const uint32_t c1 = head[pos[h]] & 0xFFFFu;
+        const uint32_t m1 = meta[c1];
+        p1[h] = m1 >> 16;
+        v1[h] = ev[c1];
+        const uint32_t c2 = m1 & 0xFFFFu;
+        const uint32_t m2 = meta[c2 != 0xFFFFu ? c2 : c1];
+        p2[h] = c2 != 0xFFFFu ? (m2 >> 16) : 0xFFFFu;
+        v2[h] = ev[c2 != 0xFFFFu ? c2 : c1];
+        more[h] = c2 != 0xFFFFu ? (m2 & 0xFFFFu) : 0xFFFFu;
       }
-      const bool multi = c[0] >= 2u || c[1] >= 2u;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) msk[h] = c[h] >= 2u ? s_pmask[row[h]] : 0u;
-      if (__ballot(multi) == 0) {  // the usual case: one hit per element
+      for (int p = 0; p < FOLD_MAXP; ++p) {
+        if (p >= a.np) break;
 #pragma unroll
-        for (int p = 0; p < FOLD_MAXP; ++p) {
-          if (p >= a.np) break;
-          const float wp = s_w[p];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const float tv = ((uint32_t)p == hp0[h]) ? hv0[h] : bb[h];
-            fold_term(av[h], tv, wp, a.first && p == 0, a.replace_only, a.zero_base);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int p = 0; p < FOLD_MAXP; ++p) {
-          if (p >= a.np) break;
-          const float wp = s_w[p];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            float tv = bb[h];
-            if ((msk[h] >> p) & 1u) tv = s_pool[row[h]][p];
-            if ((uint32_t)p == hp0[h]) tv = hv0[h];
-            fold_term(av[h], tv, wp, a.first && p == 0, a.replace_only, a.zero_base);
-          }
+        for (int h = 0; h < 2; ++h) {
+          const float tv = ((uint32_t)p == p1[h]) ? v1[h] : (((uint32_t)p == p2[h]) ? v2[h] : bb[h]);
+          fold_term(av[h], tv, wr[p], a.first && p == 0, a.replace_only, a.zero_base);
         }
       }
-      // every hit element's cnt is read above before any result overwrites it: each element
-      // belongs to exactly one (thread, h), and only its own cnt[pos] is written
-      cnt[pos[0]] = __float_as_uint(av[0]);
-      if (two) cnt[pos[1]] = __float_as_uint(av[1]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (more[h] != 0xFFFFu) {  // three or more hits (rare): walk the chain once into a row
+          float acc = a.first ? 0.0f : a.out[tlo + pos[h]];
+          const uint32_t row = atomicAdd(&s_pool_n, 1u);
+          if (row < FOLD_POOL) {
+            uint32_t mask = 0;
+            for (uint32_t c = head[pos[h]] & 0xFFFFu; c != 0xFFFFu;) {
+              const uint32_t m = meta[c];
+              s_pool[row][m >> 16] = ev[c];
+              mask |= 1u << (m >> 16);
+              c = m & 0xFFFFu;
+            }
+            for (int p = 0; p < a.np; ++p) {
+              const float tv = ((mask >> p) & 1u) ? s_pool[row][p] : bb[h];
+              fold_term(acc, tv, wr[p], a.first && p == 0, a.replace_only, a.zero_base);
+            }
+          } else {  // the pool is full: a walk per payload
+            for (int p = 0; p < a.np; ++p) {
+              float tv = bb[h];
+              for (uint32_t c = head[pos[h]] & 0xFFFFu; c != 0xFFFFu;) {
+                const uint32_t m = meta[c];
+                if ((m >> 16) == (uint32_t)p) {
+                  tv = ev[c];
+                  break;
+                }
+                c = m & 0xFFFFu;
+              }
+              fold_term(acc, tv, wr[p], a.first && p == 0, a.replace_only, a.zero_base);
+            }
+          }
+          av[h] = acc;
+        }
+      }
+      // every hit element's chain head is read above before any result overwrites it: each
+      // element belongs to exactly one (thread, h), and only its own head[pos] is written
+      head[pos[0]] = __float_as_uint(av[0]);
+      if (two) head[pos[1]] = __float_as_uint(av[1]);
     }
     __syncthreads();
     FSTAMP(4);
@@ -478,10 +469,9 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if ((hitbits >> (4 * q + e)) & 1u)
-            acc[q * 4 + e] = __uint_as_float(cnt[q * 4 * FOLD_THREADS + t * 4 + e]);
+            acc[q * 4 + e] = __uint_as_float(head[q * 4 * FOLD_THREADS + t * 4 + e]);
     }
   } else {
-  __syncthreads();  // a hit-path scatter that overflowed the pool is done with the LDS tile
   for (int j = t * 4; j < FOLD_TILE; j += 4 * FOLD_THREADS) *reinterpret_cast<uint32_t*>(&htag[j]) = 0xFFFFFFFFu;
   // entries of a payload past the preloaded ones (dense ranges, e.g. JWINS alpha 0.1-0.4):
   // the next payload's first FOLD_NB per thread are loaded while the current payload folds
@@ -579,7 +569,7 @@ __global__ void __launch_bounds__(FOLD_THREADS, 4) fold_kernel(FoldArgs a) {
   }  // phase path
   if (a.add_self) {
     if (l_ahead) {  // hit-chain path: this tile's local values from the LDS copy
-      const float* lv = reinterpret_cast<const float*>(lds_raw) + 2 * FOLD_TILE;
+      const float* lv = reinterpret_cast<const float*>(lds_raw) + FOLD_TILE + 2 * FOLD_CAP;
 #pragma unroll
       for (int q = 0; q < FOLD_GROUPS; ++q) {
         const float4 v = *reinterpret_cast<const float4*>(&lv[q * 4 * FOLD_THREADS + t * 4]);
