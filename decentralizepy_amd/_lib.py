@@ -27,6 +27,7 @@ DPZ_TOPK_SHARED = 0x10
 DPZ_TOPK_VAL_FP16 = 0x20
 DPZ_TOPK_HINT = 0x40
 DPZ_TOPK_KEEP_X = 0x80
+DPZ_TOPK_SLICED = 0x100
 DPZ_FOLD_SELF = 0x1
 DPZ_FOLD_REPLACE_ONLY = 0x2
 DPZ_FOLD_ZERO_BASE = 0x4

@@ -1688,7 +1688,13 @@ __global__ void __launch_bounds__(1024) nodes_select_kernel(const EncNode* __res
       ReplaceJob{}, bid);
 }
 
-template <bool PLAIN>
+#ifndef DPZ_NODES_NO_COUNTER  // ablation only (results then differ): no counter update
+#define DPZ_NODES_NO_COUNTER 0
+#endif
+// SL (DPZ_TOPK_SLICED): the counter in bit-sliced form — the node table's counter word points at
+// its planes and the last word at the selection mask, which compact writes (as
+// dpz_topk_encode_sliced) instead of the scattered counter[idx] += 1 atomics
+template <bool PLAIN, bool SL>
 __global__ void __launch_bounds__(256, 4) nodes_compact_kernel(const EncNode* __restrict__ tab,
                                                                WsOff o, int64_t n, int64_t k,
                                                                int64_t W, int64_t R, int64_t CAP,
@@ -1697,21 +1703,25 @@ __global__ void __launch_bounds__(256, 4) nodes_compact_kernel(const EncNode* __
   const uint32_t node = blockIdx.x / ncb, bid = blockIdx.x % ncb;
   const EncNode e = tab[node];
   KeySrc s{e.x, e.x0, nullptr, DPZ_ACC_NONE, 1};
-  sampled_compact_kernel_body<true, PLAIN, 2, false>(
+  int32_t* const counter = SL || DPZ_NODES_NO_COUNTER ? nullptr : e.counter;
+  uint32_t* const selmask = SL ? reinterpret_cast<uint32_t*>(e.pad) : nullptr;
+  uint32_t* const planes = SL ? reinterpret_cast<uint32_t*>(e.counter) : nullptr;
+  sampled_compact_kernel_body<true, PLAIN, 2, SL>(
       s, n, k, W, R, CAP, wsp<TopkCtrl>(e.ws, o.ctrl), wsp<uint32_t>(e.ws, o.chist),
       wsp<const uint32_t>(e.ws, o.blkabove), wsp<const uint32_t>(e.ws, o.blcnt),
       wsp<const uint32_t>(e.ws, o.blkey), wsp<const uint32_t>(e.ws, o.blidx),
       wsp<const uint32_t>(e.ws, o.segcnt), wsp<const uint32_t>(e.ws, o.cidx),
       wsp<const uint32_t>(e.ws, o.ckey), wsp<const float>(e.ws, o.cval), e.x, e.idx_out,
-      e.val_out, e.counter, nullptr, e.status_out, ReplaceJob{}, 0, 0, nullptr, nullptr, nwords,
+      e.val_out, counter, nullptr, e.status_out, ReplaceJob{}, 0, 0, selmask, planes, nwords,
       wsp<uint32_t>(e.ws, o.ghist), sig, bid);
 }
 
 int topk_encode_nodes(int m, const void* table, int64_t n, int64_t k, size_t ws_bytes, int flags,
                       hipStream_t st) {
   if (m < 1 || !table || n <= 0 || n >= (int64_t(1) << 31) || k < 1 || k > n) return DPZ_ERR_ARG;
-  if (flags & ~DPZ_TOPK_HINT) return DPZ_ERR_ARG;
+  if (flags & ~(DPZ_TOPK_HINT | DPZ_TOPK_SLICED)) return DPZ_ERR_ARG;
   if (!use_sampled(n, k)) return DPZ_ERR_UNSUPPORTED;
+  const bool sl = (flags & DPZ_TOPK_SLICED) != 0;
   if (ws_bytes < ws_bytes_needed(n, k)) return DPZ_ERR_WORKSPACE;
   // the shared-GPU geometry (DPZ_TOPK_SHARED): many codecs run at once, and the smaller filter
   // grid per node leaves CU slots to the other nodes' kernels
@@ -1726,6 +1736,8 @@ int topk_encode_nodes(int m, const void* table, int64_t n, int64_t k, size_t ws_
   const uint32_t nb = (uint32_t)g.B, nsel = (uint32_t)((g.W + SEL_SEGS - 1) / SEL_SEGS);
   const uint32_t ncb = (uint32_t)((g.W + 7) / 8);
   if ((uint64_t)m * nb >= (1ull << 31) || (uint64_t)m * ncb >= (1ull << 31)) return DPZ_ERR_ARG;
+  // a sliced compact builds a segment's mask words in one LDS row
+  if (sl && (g.R > SL_RMAX || (g.R & 31) != 0)) return DPZ_ERR_UNSUPPORTED;
   if (!hsig)
     DPZ_TIMED(DPZ_KT_TOPK_SAMPLE, st,
               nodes_sample_kernel<<<(unsigned)(m * nsb), 256, 0, st>>>(tab, o, n, nsb));
@@ -1739,12 +1751,15 @@ int topk_encode_nodes(int m, const void* table, int64_t n, int64_t k, size_t ws_
         tab, o, n, r_lo, r_hi, g.W, g.R, g.CAP, nb, hsig)));
   DPZ_TIMED(DPZ_KT_TOPK_SELECT, st, nodes_select_kernel<<<(unsigned)(m * nsel), 1024, 0, st>>>(
       tab, o, n, k, g.W, g.B, g.R, g.CAP, nsel));
-  if (k > n / 32)
-    DPZ_TIMED(DPZ_KT_TOPK_COMPACT, st, nodes_compact_kernel<true><<<(unsigned)(m * ncb), 256, 0, st>>>(
-        tab, o, n, k, g.W, g.R, g.CAP, ncb, mask_words(n), sig));
+  if (sl)
+    DPZ_TIMED(DPZ_KT_TOPK_COMPACT, st, (nodes_compact_kernel<false, true><<<(unsigned)(m * ncb), 256, 0, st>>>(
+        tab, o, n, k, g.W, g.R, g.CAP, ncb, mask_words(n), sig)));
+  else if (k > n / 32)
+    DPZ_TIMED(DPZ_KT_TOPK_COMPACT, st, (nodes_compact_kernel<true, false><<<(unsigned)(m * ncb), 256, 0, st>>>(
+        tab, o, n, k, g.W, g.R, g.CAP, ncb, mask_words(n), sig)));
   else
-    DPZ_TIMED(DPZ_KT_TOPK_COMPACT, st, nodes_compact_kernel<false><<<(unsigned)(m * ncb), 256, 0, st>>>(
-        tab, o, n, k, g.W, g.R, g.CAP, ncb, mask_words(n), sig));
+    DPZ_TIMED(DPZ_KT_TOPK_COMPACT, st, (nodes_compact_kernel<false, false><<<(unsigned)(m * ncb), 256, 0, st>>>(
+        tab, o, n, k, g.W, g.R, g.CAP, ncb, mask_words(n), sig)));
   return DPZ_OK;
 }
 

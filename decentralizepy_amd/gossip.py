@@ -76,7 +76,7 @@ class GossipRound:
 
     def __init__(self, adj, x_init, alpha, rank=0, world=1, group=None, encode=None, fold=None,
                  device=None, streams=3, exchange="auto", hbm_budget=None, partial=None,
-                 combine=None, node_batch=True, node_group=4, guarded=True):
+                 combine=None, node_batch=True, node_group=4, guarded=True, sliced_counter=False):
         """adj: adjacency sets of all nodes; x_init: (hi - lo, N) fp32 tensor with this rank's
         nodes' flat models (device tensor for the HIP codec).
 
@@ -109,7 +109,21 @@ class GossipRound:
         self.device = device or x_init.device
         self.x = x_init.contiguous().clone()
         self.x0 = x_init.contiguous().clone()  # init_model of every owned node
-        self.counter = torch.zeros_like(self.x, dtype=torch.int32)
+        # sliced_counter (HIP, node-batched encodes): every node's shared_parameters_counter as 32
+        # bit planes plus a selection mask per round (DPZ_TOPK_SLICED: compact writes the mask
+        # and ripple-adds it to the planes instead of k scattered counter atomics); ``counter``
+        # materialises the int32 counters on read (the reference reads them once, at the end)
+        self.sliced_counter = bool(sliced_counter) and encode is None and fold is None and node_batch
+        if self.sliced_counter:
+            from . import codec
+            nw = codec.mask_words(self.N)
+            self._planes = torch.zeros(self.hi - self.lo, 32 * nw, dtype=torch.int32,
+                                       device=self.device)
+            self._selmask = torch.zeros(self.hi - self.lo, nw, dtype=torch.int32,
+                                        device=self.device)
+            self._counter = None
+        else:
+            self._counter = torch.zeros_like(self.x, dtype=torch.int32)
         self.send_idx = torch.zeros(self.per, self.k, dtype=torch.int32, device=self.device)
         self.send_val = torch.zeros(self.per, self.k, dtype=torch.float32, device=self.device)
         gathered = self.per * world * self.k * 8
@@ -166,6 +180,16 @@ class GossipRound:
             self.wss = [codec.Workspace(self.device) for _ in self.streams]
 
 
+    @property
+    def counter(self):
+        """Every owned node's int32 shared_parameters_counter (m, N): the tensor itself, or with
+        the sliced counter its materialised copy (dpz_counter_unslice per node)."""
+        if self._counter is not None:
+            return self._counter
+        from . import codec
+        return torch.stack([codec.counter_unslice(self._planes[j], self.N)
+                            for j in range(self.hi - self.lo)])
+
     # ---- default device implementations ---------------------------------------------------
     def _hip_encode(self, x, x0, k, counter, idx_out, val_out):
         from . import codec
@@ -206,10 +230,13 @@ class GossipRound:
         if key not in tabs:
             rows = []
             for j in range(m):
+                sl = self.sliced_counter
                 rows.append([self.x[j].data_ptr(), self.x0[j].data_ptr(),
-                             self.counter[j].data_ptr(), self.send_idx[j].data_ptr(),
+                             (self._planes if sl else self._counter)[j].data_ptr(),
+                             self.send_idx[j].data_ptr(),
                              self.send_val[j].data_ptr(), self.node_ws[j].buf.data_ptr(),
-                             self.status.data_ptr() + 4 * j, 0])
+                             self.status.data_ptr() + 4 * j,
+                             self._selmask[j].data_ptr() if sl else 0])
             tabs[key] = torch.from_numpy(np.array(rows, dtype=np.uint64).view(np.int64)).to(
                 self.device)
         return tabs[key]
@@ -232,6 +259,8 @@ class GossipRound:
         ws_bytes = min(w.get(self.N, self.k).numel() for w in self.node_ws)
         tab = self._node_table(m)
         flags = _lib.DPZ_TOPK_HINT if getattr(self, "_primed", False) else 0
+        if self.sliced_counter:
+            flags |= _lib.DPZ_TOPK_SLICED
         # groups of G nodes, round-robin over the streams: one group's latency-bound selection
         # launches (and their scattered counter updates) overlap another group's filter
         cur = torch.cuda.current_stream(self.device)
@@ -261,9 +290,14 @@ class GossipRound:
         from . import codec
         for j in bad:
             ws = self.node_ws[j] if getattr(self, "node_ws", None) is not None else self.wss[0]
-            codec.topk_encode(self.x[j], self.k, x0=self.x0[j], counter=self.counter[j],
-                              idx_out=self.send_idx[j], val_out=self.send_val[j],
-                              workspace=ws, exact=True)
+            if self.sliced_counter:
+                codec.topk_encode_sliced(self.x[j], self.k, self._selmask[j], self._planes[j],
+                                         x0=self.x0[j], idx_out=self.send_idx[j],
+                                         val_out=self.send_val[j], workspace=ws, exact=True)
+            else:
+                codec.topk_encode(self.x[j], self.k, x0=self.x0[j], counter=self._counter[j],
+                                  idx_out=self.send_idx[j], val_out=self.send_val[j],
+                                  workspace=ws, exact=True)
 
     def encode_all(self, check=True):
         """Every owned node's encode.  check=False (HIP): the status words stay on the device
@@ -276,6 +310,9 @@ class GossipRound:
         from . import _lib, codec
         m = self.hi - self.lo
         if self.node_batch and m > 1 and self._encode_nodes(m, check):
+            return
+        if self.sliced_counter:  # (n, k) off the sampled path, or one node: exact sliced encodes
+            self._rerun_missed(list(range(m)))
             return
         m, streams, ws_bytes, wsp = self._stream_args()
         cur = torch.cuda.current_stream(self.device)
@@ -290,7 +327,7 @@ class GossipRound:
         self._primed = True
         rc = _lib.lib().dpz_topk_encode_batch_ex(
             m, self._ptrs(self.x[:m]), self._ptrs(self.x0[:m]), self.N, self.k,
-            self._ptrs(self.counter[:m]), self._ptrs(self.send_idx[:m]),
+            self._ptrs(self._counter[:m]), self._ptrs(self.send_idx[:m]),
             self._ptrs(self.send_val[:m]), wsp, ws_bytes, len(self.streams), streams,
             self.status.data_ptr(), hint)
         _lib.check(rc, "dpz_topk_encode_batch_ex")

@@ -77,6 +77,13 @@ typedef void* dpz_stream_t; /* hipStream_t */
  * sharing/Sharing.py:156-190 after PartialModel.py:188-255), whose re-read may then be served
  * by the 256 MiB Infinity Cache.  Results are identical.                                       */
 #define DPZ_TOPK_KEEP_X 0x80
+/* dpz_topk_encode_nodes only: every node's shared_parameters_counter in bit-sliced form (as
+ * dpz_topk_encode_sliced): the node table's counter word points at its planes
+ * (uint32[32 * dpz_mask_words(n)]) and its last word at a selection mask
+ * (uint32[dpz_mask_words(n)]); compact writes every mask word and adds the mask to the planes
+ * instead of the scattered counter[idx] += 1.  DPZ_ERR_UNSUPPORTED when a node's wave segment is
+ * longer than one LDS mask row (n past ~25 M at the shared grid).                           */
+#define DPZ_TOPK_SLICED 0x100
 
 /* ---- fold flags ---- */
 #define DPZ_FOLD_SELF 0x1         /* add the local term w_self*local after the payloads        */

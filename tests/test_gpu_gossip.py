@@ -127,3 +127,33 @@ def test_node_batched_encodes_equal_stream_encodes(dev):
                                           o.x0.cpu().numpy().view(np.uint32))
             np.testing.assert_array_equal(a.counter.cpu().numpy(), o.counter.cpu().numpy())
     assert a.node_ws is not None and getattr(b, "node_ws", None) is None
+
+
+@pytest.mark.parametrize("path,n,alpha", [(EDGES16, 1 << 20, 0.01), (EDGES96, 40_000, 0.02)])
+def test_gossip_round_sliced_counter(dev, path, n, alpha):
+    """Every node's shared_parameters_counter in bit-sliced form (DPZ_TOPK_SLICED node-batched
+    encodes: compact writes the selection mask and ripple-adds it to the planes): models and the
+    materialised counters bit-identical to the int32-counter engine over three rounds, a forced
+    sampled miss in round 0 included (re-run exactly through dpz_topk_encode_sliced)."""
+    from decentralizepy_amd.gossip import GossipRound, read_edges
+    from tests.layouts import miss_layout
+    adj = read_edges(path)
+    x = _models(len(adj), n)
+    a = GossipRound(adj, x.to(dev), alpha, sliced_counter=True)
+    b = GossipRound(adj, x.to(dev), alpha, sliced_counter=False)
+    assert a.sliced_counter and not b.sliced_counter
+    miss = None
+    if n >= (1 << 20):
+        miss, _ = miss_layout(n, round(alpha * n))
+    for r in range(3):
+        g = torch.Generator().manual_seed(500 + r)
+        noise = (0.01 * torch.randn(len(adj), n, generator=g)).to(dev)
+        for eng in (a, b):
+            eng.x += noise
+            if r == 0 and miss is not None:
+                eng.x[3] = eng.x0[3] + torch.from_numpy(miss).to(dev)
+            eng.step()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(a.x.cpu().numpy().view(np.uint32),
+                                      b.x.cpu().numpy().view(np.uint32))
+        np.testing.assert_array_equal(a.counter.cpu().numpy(), b.counter.cpu().numpy())
