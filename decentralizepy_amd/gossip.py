@@ -76,7 +76,7 @@ class GossipRound:
 
     def __init__(self, adj, x_init, alpha, rank=0, world=1, group=None, encode=None, fold=None,
                  device=None, streams=3, exchange="auto", hbm_budget=None, partial=None,
-                 combine=None, node_batch=True, node_group=4, guarded=True, sliced_counter=False):
+                 combine=None, node_batch=True, node_group=4, guarded=True, sliced_counter=True):
         """adj: adjacency sets of all nodes; x_init: (hi - lo, N) fp32 tensor with this rank's
         nodes' flat models (device tensor for the HIP codec).
 
@@ -112,8 +112,13 @@ class GossipRound:
         # sliced_counter (HIP, node-batched encodes): every node's shared_parameters_counter as 32
         # bit planes plus a selection mask per round (DPZ_TOPK_SLICED: compact writes the mask
         # and ripple-adds it to the planes instead of k scattered counter atomics); ``counter``
-        # materialises the int32 counters on read (the reference reads them once, at the end)
-        self.sliced_counter = bool(sliced_counter) and encode is None and fold is None and node_batch
+        # materialises the int32 counters on read (the reference reads them once, at the end).
+        # Measured on MI355X (C4, 96_regular x 11M, tools/diag/slpf_ab.sh): 4.90-4.92 ms per
+        # round against 5.03-5.05 with the int32 counter.  One node per rank (no node batch) or a
+        # segment geometry the sliced compact does not take (n > 2^26) falls back to the int32
+        # counter (_unslice)
+        self.sliced_counter = (bool(sliced_counter) and encode is None and fold is None
+                               and node_batch and self.hi - self.lo > 1)
         if self.sliced_counter:
             from . import codec
             nw = codec.mask_words(self.N)
@@ -189,6 +194,14 @@ class GossipRound:
         from . import codec
         return torch.stack([codec.counter_unslice(self._planes[j], self.N)
                             for j in range(self.hi - self.lo)])
+
+    def _unslice(self):
+        """Back to the int32 counter (the node-batched sliced encode does not take this
+        geometry): the planes materialised once, the node tables rebuilt."""
+        self._counter = self.counter.contiguous()
+        self._planes = self._selmask = None
+        self.sliced_counter = False
+        self.__dict__.pop("_node_tabs", None)
 
     # ---- default device implementations ---------------------------------------------------
     def _hip_encode(self, x, x0, k, counter, idx_out, val_out):
@@ -271,6 +284,14 @@ class GossipRound:
             rc = _lib.lib().dpz_topk_encode_nodes(min(G, m - g0), tab.data_ptr() + 64 * g0,
                                                   self.N, self.k, ws_bytes, flags,
                                                   ctypes.c_void_p(st.cuda_stream))
+            if rc == _lib.DPZ_ERR_UNSUPPORTED and g0 == 0 and self.sliced_counter:
+                # the sliced geometry check precedes every launch: nothing was enqueued
+                self._unslice()
+                flags &= ~_lib.DPZ_TOPK_SLICED
+                tab = self._node_table(m)
+                rc = _lib.lib().dpz_topk_encode_nodes(min(G, m - g0), tab.data_ptr(), self.N,
+                                                      self.k, ws_bytes, flags,
+                                                      ctypes.c_void_p(st.cuda_stream))
             _lib.check(rc, "dpz_topk_encode_nodes")
         for st in self.streams:
             cur.wait_stream(st)
@@ -311,7 +332,7 @@ class GossipRound:
         m = self.hi - self.lo
         if self.node_batch and m > 1 and self._encode_nodes(m, check):
             return
-        if self.sliced_counter:  # (n, k) off the sampled path, or one node: exact sliced encodes
+        if self.sliced_counter:  # (n, k) off the sampled path: exact sliced encodes
             self._rerun_missed(list(range(m)))
             return
         m, streams, ws_bytes, wsp = self._stream_args()

@@ -157,3 +157,30 @@ def test_gossip_round_sliced_counter(dev, path, n, alpha):
         np.testing.assert_array_equal(a.x.cpu().numpy().view(np.uint32),
                                       b.x.cpu().numpy().view(np.uint32))
         np.testing.assert_array_equal(a.counter.cpu().numpy(), b.counter.cpu().numpy())
+
+
+def test_sliced_counter_falls_back_past_the_sliced_geometry(dev):
+    """n = 2^26 + 64: a wave segment exceeds the sliced compact's LDS row (SL_RMAX), so the first
+    node-batched sliced encode returns UNSUPPORTED before any launch and the engine continues on
+    the int32 counter (GossipRound._unslice) — results bit-identical to an int32 engine; one node
+    per rank never takes the sliced form."""
+    from decentralizepy_amd.gossip import GossipRound
+    n = (1 << 26) + 64
+    adj = [{1}, {0}]
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(2, n, generator=g).to(dev)
+    a = GossipRound(adj, x, 0.01)
+    b = GossipRound(adj, x, 0.01, sliced_counter=False)
+    assert a.sliced_counter
+    for r in range(2):
+        noise = torch.randn(2, n, generator=torch.Generator(device=dev).manual_seed(r), device=dev)
+        for eng in (a, b):
+            eng.x += 0.01 * noise
+            eng.step()
+        torch.cuda.synchronize()
+        assert not a.sliced_counter
+        assert torch.equal(a.x.view(torch.int32), b.x.view(torch.int32))
+        assert torch.equal(a.counter, b.counter)
+    del a, b
+    one = GossipRound([set()], torch.zeros(1, 1 << 18, device=dev), 0.01)
+    assert not one.sliced_counter
