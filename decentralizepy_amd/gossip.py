@@ -90,7 +90,8 @@ class GossipRound:
         # launch per phase and group (dpz_topk_encode_nodes), the groups round-robin over
         # `streams`; False: node after node on the streams.  Measured on MI355X (96_regular x
         # 11M, tools/diag/c4_group_ab.sh): groups of 4 5.21 ms per round, 16: 5.24, 1: 5.36,
-        # node after node 5.50-5.61
+        # node after node 5.50-5.61; with the sliced counters (tools/diag/c4_group_sliced_ab.sh,
+        # group:streams) 4:3 4.90-4.92, 8:3 4.92, 4:2 4.92-4.93, 2:3 4.97-4.99, 4:4 5.02
         self.node_batch = node_batch
         self.node_group = max(1, int(node_group))
         # guarded: (HIP, all-gather exchange) the folds follow the encodes with no host wait in
