@@ -1047,18 +1047,9 @@ __device__ __forceinline__ int32_t fw_lower_bounds(int np, int32_t e0, int lane,
 #ifndef DPZ_WALKG_L_FIRST
 #define DPZ_WALKG_L_FIRST 0
 #endif
-// DPZ_WALK_GUESS 1: each search's first probe brackets the uniform-density guess k * e0 / n
-// (64 probes GUESS_S entries apart around it): a top-k selection of a dense change is spread
-// evenly over [0, n), so the lower bound lies within a few hundred entries of the guess and the
-// search ends one probe later (2 dependent loads instead of ceil(log64 k)); a guess outside the
-// bracket still narrows the range and the 64-ary search continues
-#ifndef DPZ_WALK_GUESS
-#define DPZ_WALK_GUESS 0
-#endif
-constexpr int32_t GUESS_S = 16;
 template <int NSX, bool LOCK, class IdxOf, class KOf>
 __device__ __forceinline__ int32_t fw_start_cursors(int np, int32_t e0, int lane, IdxOf idx_of,
-                                                    KOf k_of, const int32_t* dflt, int64_t n = 0) {
+                                                    KOf k_of, const int32_t* dflt) {
   if (LOCK) return fw_lower_bounds<NSX>(np, e0, lane, idx_of, k_of, dflt);
   int32_t curv = 0;
 #pragma unroll
@@ -1066,24 +1057,6 @@ __device__ __forceinline__ int32_t fw_start_cursors(int np, int32_t e0, int lane
     if (p >= np) break;
     const int32_t* ip = idx_of(p);
     int32_t lo = 0, hi = k_of(p);
-    if (DPZ_WALK_GUESS && n > 0 && hi > 64 * GUESS_S) {
-      const int64_t g = ((int64_t)hi * e0) / n;
-      const int64_t b = g - 32 * GUESS_S;
-      const int64_t q = b + (int64_t)lane * GUESS_S;
-      const bool ok = q >= 0 && q < hi;
-      const int32_t x = ip[ok ? q : 0];
-      // below: entries before the array count as below e0, past its end as not below (a prefix)
-      const int32_t c = (int32_t)__popcll(__ballot(q < 0 || (ok && x < e0)));
-      if (c == 0) {
-        hi = b < hi ? (int32_t)b : hi;  // idx[b] >= e0 (b >= 0: lane 0 would count otherwise)
-      } else if (c == 64) {
-        lo = (int32_t)(b + 63 * GUESS_S + 1);  // idx[b + 63 S] < e0 (inside the array)
-      } else {
-        const int64_t nlo = b + (int64_t)(c - 1) * GUESS_S + 1, nhi = b + (int64_t)c * GUESS_S;
-        lo = nlo > 0 ? (int32_t)nlo : 0;
-        hi = nhi < hi ? (int32_t)nhi : hi;
-      }
-    }
     while (hi > lo) {
       const int32_t len = hi - lo;
       const int32_t stride = len <= 64 ? 1 : (len + 63) / 64;
@@ -1148,7 +1121,7 @@ __device__ __forceinline__ void fold_walk_run(const FA& a, int64_t t0, int64_t t
   // lane p: payload p's cursor (the next window's first entry)
   int32_t curv = fw_start_cursors<NS, DPZ_WALK4_LOCKSTEP != 0>(
       np, (int32_t)(t0 * TE), lane, [&](int p) { return P_idx(p); },
-      [&](int p) { return P_k(p); }, reinterpret_cast<const int32_t*>(a.local), n);
+      [&](int p) { return P_k(p); }, reinterpret_cast<const int32_t*>(a.local));
   if (!DPZ_WALK4_L_FIRST) L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n);
   int32_t cs[ONE ? NS : 1];
   if constexpr (ONE) {
@@ -1456,7 +1429,7 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
       np, (int32_t)(t0 * TE), lane,
       [&](int p) { return reinterpret_cast<const int32_t*>(rl64(ipl, p)); },
       [&](int p) { return fw_uni(__builtin_amdgcn_readlane(kl, p)); },
-      reinterpret_cast<const int32_t*>(a.local), n);
+      reinterpret_cast<const int32_t*>(a.local));
   if (!DPZ_WALKG_L_FIRST) L = fw_load<VEC, EPL>(a.local, t0 * TE, lane, n);
   if (CT) {
 #pragma unroll

@@ -1,4 +1,6 @@
 #!/bin/bash
+# DPZ_WALK_GUESS was removed after the A/B (profiles/r05_fold_start_ab.txt): build lib_guess from
+# commit ff7398b (tools/diag/build_variant.sh guess "-DDPZ_WALK_GUESS=1" ff7398b) to re-run it.
 # The lone walk fold's start-up switches (DPZ_WALK4_LOCKSTEP / DPZ_WALK4_L_FIRST / DPZ_WALK_GUESS,
 # build_variant.sh libraries base / ls / lf / lslf / guess): the fold parity tests on the guess
 # library, then the bench's product-path stage (64 MiB, 1 and 3 payloads), alternating on one box.

@@ -1,4 +1,6 @@
 #!/bin/bash
+# DPZ_WALK_GUESS was removed after the A/B (profiles/r05_fold_start_ab.txt): build lib_guess from
+# commit ff7398b (tools/diag/build_variant.sh guess "-DDPZ_WALK_GUESS=1" ff7398b) to re-run it.
 # DPZ_WALK_GUESS (the walk folds' cursor searches starting at the uniform-density guess): base /
 # guess build_variant.sh libraries, alternating on one box — tools/diag/fold_kinds.py (walk kind)
 # at the C3, 64 MiB and C2/C4 shapes, then the C4 round (tools/diag/c4_round_ab.py).
