@@ -189,7 +189,9 @@ class GossipRound:
     @property
     def counter(self):
         """Every owned node's int32 shared_parameters_counter (m, N): the tensor itself, or with
-        the sliced counter its materialised copy (dpz_counter_unslice per node)."""
+        the sliced counter its materialised copy (dpz_counter_unslice per node) — a snapshot:
+        writes into it do not reach the engine (construct with sliced_counter=False for a live
+        int32 tensor)."""
         if self._counter is not None:
             return self._counter
         from . import codec
