@@ -255,8 +255,7 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
     b_enc = 8 * n + 8 * k + 8 * k      # read x, x0; write idx, val; counter[idx] += 1 (r+w)
     b_dec = 8 * n + 8 * k              # read local, payload; write out
     fell_back |= (multi.sticky_status(clear=True) | one.sticky_status(clear=True)) != 0
-    product = product_one_node(sets, n, k, stream, one.workspaces[0], max(2 * R, min(steps, 200)),
-                               hint=bool(hint))
+    product = product_one_node(sets, n, k, stream, max(2 * R, min(steps, 200)), alpha=alpha)
     fell_back |= product["fell_back"]
     return dict(n=n, k=k, s_step=s_step, s_multi=s_multi, s_serial=s_serial, s_host=s_host,
                 mode=mode, streams=S, fell_back=fell_back, t_enc=t_enc, t_dec=t_dec,
@@ -267,85 +266,177 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
                 value=world * 4 * n / s_step / 2 ** 30)
 
 
-def product_one_node(sets, n, k, stream, ws, reps, hint=True, keep_x=True):
-    """``stages.product_one_node``: exactly what the drop-in plugins enqueue for one node's round,
-    on one stream — PartialModel.serialized_model's ``codec.topk_encode`` (|x - x0| top-k with
-    the counter update; sampled path, statuses checked after the loop) then Sharing._averaging's
-    ``codec.decode_average`` (the Metro-Hastings fold of ``npay`` neighbour payloads over the
-    node's pre-share model x into a new buffer, weights 1/(deg+1) of a degree-npay regular graph,
-    w_self = 1 - their Python sum), for npay = 1 and 3.  The encode is PartialModel._encode's:
-    ``hint`` (the key window from the previous encode's exact threshold on the node's workspace,
-    no sample launch) and ``keep_x`` (x streamed with the default cache policy, the fold re-reads
-    it).  Step j rotates over the HBM-rotated node states; its neighbours' payloads are those of
-    states j-1 .. j-npay.  Device time: HIP events
-    around the whole loop on the launch stream after a GPU-side spin that lets the host queue it.
-    Algorithmic bytes: encode 8N + 16k, fold 8N + 8·npay·k (reference Sharing.py:156-190,
-    PartialModel.py:188-255)."""
+class _BenchMapping:
+    """The Node's mapping as the plugins use it (get_uid only)."""
+
+    def get_uid(self, rank, machine_id):
+        return rank
+
+
+class _BenchGraph:
+    """A regular topology of degree ``deg`` as the plugins read it (neighbors(uid) only)."""
+
+    def __init__(self, deg):
+        self.deg = deg
+
+    def neighbors(self, uid):
+        return set(range(uid + 1, uid + 1 + self.deg))
+
+
+def _bench_model(n):
+    """An n-parameter fp32 model on the host with the reference Model's codec fields
+    (models/Model.py:15-25); zero-initialised (the bench sets the plugin's device state)."""
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.weight = torch.nn.Parameter(torch.zeros(n))
+            self.model_change = None
+            self.accumulated_changes = None
+            self.shared_parameters_counter = None
+    return Net()
+
+
+def make_bench_plugins(count, n, alpha, deg, dev):
+    """``count`` PartialModel plugins (the drop-in class, decentralizepy_amd.sharing.PartialModel)
+    of an n-parameter model on a degree-``deg`` regular graph, one per rotated node state, all on
+    ``dev`` (the plugin's DPZ_DEVICE override; it would otherwise pick rank mod GPUs)."""
+    from decentralizepy_amd.sharing.PartialModel import PartialModel
+    import tempfile
+    tmp = tempfile.mkdtemp(prefix="dpz_bench_")
+    prev = os.environ.get("DPZ_DEVICE")
+    os.environ["DPZ_DEVICE"] = str(torch.device(dev).index or 0)
+    try:
+        return [PartialModel(j, 0, None, _BenchMapping(), _BenchGraph(deg), _bench_model(n), None,
+                             tmp, alpha=alpha) for j in range(count)]
+    finally:
+        if prev is None:
+            del os.environ["DPZ_DEVICE"]
+        else:
+            os.environ["DPZ_DEVICE"] = prev
+
+
+def plugin_device_round(p, x, x0, payloads, degrees, blocking=True):
+    """The device work of one PartialModel round as the plugin enqueues it, with the host legs
+    (state_dict H2D, payload H2D, D2H, load_state_dict) left out: ``_pre_step`` (model_change
+    kept lazily, LazyChange), ``serialized_model``'s ``_encode`` (top-k into the counter ring's
+    slot, prior-round key window, keep-x; the fold base when the node has one neighbour),
+    ``_averaging``'s Metro-Hastings weights and ``_fold_on_base`` / ``_fold`` (reference
+    sharing/PartialModel.py:188-255, 305-331, sharing/Sharing.py:156-190), ``_post_step``.
+    ``x`` / ``x0``: the node's flat model and init_model, already in HBM.  ``blocking=False``:
+    the encode is only enqueued (``_encode(k, blocking=False)``: no host wait for its status;
+    the caller checks the sticky status words after the loop), so back-to-back rounds keep the
+    device busy — the plugin itself waits there for its payload (the D2H to the wire follows).
+    Returns the encode's (idx, val) and the averaged model."""
+    p.pre_share_model = x
+    p.pre_share_model_transformed, p._change_dev = x, None
+    p.init_model = x0
+    p._fb = None
+    p.model.model_change = p._model_change()
+    idx, val = p._encode(round(p.alpha * p.transformed_len), blocking=blocking)
+    weights = [1 / (max(len(payloads), d) + 1) for d in degrees]
+    weight_total = 0
+    for w in weights:
+        weight_total += w
+    out = p._fold_on_base(x, payloads, weights, 1 - weight_total)
+    if out is None:
+        out = p._fold(x, payloads, weights, 1 - weight_total)
+    p._drop_model_change()  # _post_step: init_model = the averaged model (a rebinding)
+    return idx, val, out
+
+
+def product_one_node(sets, n, k, stream, reps, alpha=0.01):
+    """``stages.product_one_node``: the device work of the drop-in PartialModel plugin's round
+    (plugin_device_round: its own _model_change / _encode / _fold_on_base / _fold methods, so the
+    launch sequence is the plugin's, tests/test_gpu_bench_plugin.py) for one node on one stream,
+    with 1 and 3 neighbours (degree-1 / degree-3 regular graphs: the one-neighbour node takes the
+    encode's fold base).  Step j is node state j mod R of the HBM-rotated states; its neighbours'
+    payloads are the ones states j-1 .. j-npay sent.  Each state is its own plugin instance
+    (its workspace / prior window, its counter ring).  The timed region ends with every plugin's
+    counter read (RingCounter flush, the node's end-of-run dump, node/DPSGDNode.py:186-194), so
+    the counter updates the rounds deferred are inside it.  Device time: HIP events around the
+    whole loop on the launch stream after a GPU-side spin that lets the host queue it.
+    Algorithmic bytes: encode 8N + 16k (x, x0; idx, val; counter r+w), fold 8N + 8·npay·k."""
     from decentralizepy_amd import codec
     R = len(sets)
     out = {}
     fell = False
+    with torch.cuda.stream(stream):
+        for npay in (1, 3):
+            plugins = make_bench_plugins(R, n, alpha, npay, stream.device)
+            sent = [None] * R
 
-    for npay, fused in ((1, False), (3, False), (1, True), (3, True)):
-        w = [1.0 / (npay + 1)] * npay
-        w_total = 0
-        for v in w:
-            w_total += v
-        pays = [[(sets[(j - q) % R]["idx"], sets[(j - q) % R]["val"]) for q in range(1, npay + 1)]
-                for j in range(R)]
+            def step(j, encode=True, fold=True):
+                d, p = sets[j % R], plugins[j % R]
+                pays = [sent[(j - q) % R] for q in range(1, npay + 1)]
+                if encode and fold:
+                    i, v, _ = plugin_device_round(p, d["x"], d["x0"], pays, [npay] * npay,
+                                                  blocking=False)
+                    sent[j % R] = (i, v)
+                elif encode:  # the round's first half: pre-step + encode
+                    p.pre_share_model = d["x"]
+                    p.pre_share_model_transformed, p._change_dev = d["x"], None
+                    p.init_model, p._fb = d["x0"], None
+                    p.model.model_change = p._model_change()
+                    sent[j % R] = p._encode(k, blocking=False)
+                    p._fb = None  # (the fold-only loop takes the plain fold)
+                else:  # the second half: the Metro-Hastings fold over the node's model
+                    w = [1 / (npay + 1)] * npay
+                    wt = 0
+                    for v in w:
+                        wt += v
+                    p._fold(d["x"], pays, w, 1 - wt)
 
-        def enc(j):
-            d = sets[j % R]
-            codec.topk_encode(d["x"], k, x0=d["x0"], counter=d["counter"], idx_out=d["idx"],
-                              val_out=d["val"], workspace=ws, asynchronous=True,
-                              fold_base=(d["out"], w, 1 - w_total) if fused else None,
-                              hint=hint, keep_x=keep_x)
+            def flush_all():
+                for p in plugins:
+                    p._ring.flush()
 
-        def dec(j):
-            d = sets[j % R]
-            codec.decode_average(d["x"], pays[j % R], w, 1 - w_total, out=d["out"], workspace=ws,
-                                 base_ready=fused)
-
-        def loop(fns):
-            ev0 = torch.cuda.Event(enable_timing=True)
-            ev1 = torch.cuda.Event(enable_timing=True)
-            torch.cuda.synchronize()
-            with torch.cuda.stream(stream):
+            def loop(**kw):
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev1 = torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
                 torch.cuda._sleep(int(400e6))  # the host queues the loop while the GPU spins
                 ev0.record(stream)
                 t0 = time.perf_counter()
                 for j in range(reps):
-                    for f in fns:
-                        f(j)
+                    step(j, **kw)
+                flush_all()  # every counter read once: the deferred updates are timed
                 t_host = time.perf_counter() - t0
                 ev1.record(stream)
-            ev1.synchronize()
-            return ev0.elapsed_time(ev1) / reps * 1e-3, t_host / reps
+                ev1.synchronize()
+                return ev0.elapsed_time(ev1) / reps * 1e-3, t_host / reps
 
-        with torch.cuda.stream(stream):
-            for j in range(R):  # warm-up: every state encoded once (the payloads exist)
-                enc(j)
-                dec(j)
-        t_step, h_step = loop([enc, dec])
-        t_enc, _ = loop([enc])
-        t_dec, _ = loop([dec])
-        fell |= codec.topk_sticky_status(ws, clear=True) != 0
-        b_enc, b_dec = 8 * n + 16 * k, 8 * n + 8 * npay * k
-        out[f"{npay}_payload" + ("_foldbase" if fused else "")] = {
-            "step_us": round(t_step * 1e6, 3), "encode_us": round(t_enc * 1e6, 3),
-            "fold_us": round(t_dec * 1e6, 3), "host_enqueue_us": round(h_step * 1e6, 3),
-            "alg_bytes": b_enc + b_dec,
-            "GiBps": round(4 * n / t_step / 2 ** 30, 2),
-            "frac_of_hbm_peak": round((b_enc + b_dec) / t_step / 1e9 / HBM_PEAK_GBS, 4)}
-    out["encode_flags"] = {"hint": hint, "keep_x": keep_x}
-    out["note"] = ("the plugin path: codec.topk_encode then codec.decode_average (MH fold over x "
-                   "into a new buffer), one stream; the encode as PartialModel issues it (hint: "
-                   "key window from the previous round's exact threshold, no sample launch; "
-                   "keep_x: x streamed with the default cache policy for the fold's re-read); "
-                   "*_foldbase: the encode's filter also writes "
-                   "the fold's no-hit base (topk_encode fold_base=, dpz_topk_encode_foldbase) and "
-                   "the decode rewrites only the hit elements (base_ready=, DPZ_FOLD_BASE_READY), "
-                   "what PartialModel runs when its predicted MH weights hold")
+            for j in range(R):  # every state encoded once (its payload exists)
+                step(j, fold=False)
+            for j in range(2 * R):  # warm-up rounds (priors set, allocator warm)
+                step(j)
+            flush_all()
+            t_step, h_step = loop()
+            t_enc, _ = loop(fold=False)
+            t_dec, _ = loop(encode=False)
+            # per-kernel device time of the round's launches (library event pairs; the pair
+            # overhead is not removed here: rocprofv3's summary under profiles/ gives the bare
+            # durations)
+            with codec.KernelTimer() as kt:
+                loop()
+            kern = {nm: {"avg_us_event_pair": round(ms / c * 1e3, 3),
+                         "launches_per_step": round(c / reps, 3)}
+                    for nm, (ms, c) in kt.result.items()}
+            fell |= any(codec.topk_sticky_status(p.workspace, clear=True) != 0 for p in plugins)
+            b_enc, b_dec = 8 * n + 16 * k, 8 * n + 8 * npay * k
+            out[f"{npay}_payload"] = {
+                "step_us": round(t_step * 1e6, 3), "encode_us": round(t_enc * 1e6, 3),
+                "fold_us": round(t_dec * 1e6, 3), "host_enqueue_us": round(h_step * 1e6, 3),
+                "fold_path": "fold base (encode writes it)" if npay == 1 else "plain fold",
+                "kernels": kern,
+                "alg_bytes": b_enc + b_dec,
+                "GiBps": round(4 * n / t_step / 2 ** 30, 2),
+                "frac_of_hbm_peak": round((b_enc + b_dec) / t_step / 1e9 / HBM_PEAK_GBS, 4)}
+            del plugins, sent
+    out["note"] = ("the drop-in PartialModel plugin's device round (bench.plugin_device_round: "
+                   "its _model_change / _encode / _fold_on_base / _fold), host legs excluded, one "
+                   "plugin per rotated node state; model_change formed on read only "
+                   "(LazyChange), the counter updates deferred to a ring folded in on read "
+                   "(RingCounter) — every counter is read at the end of each timed region")
     out["fell_back"] = fell
     return out
 

@@ -260,6 +260,120 @@ class DeviceCounter:
         return a if dtype is None else a.astype(dtype)
 
 
+class RingCounter(DeviceCounter):
+    """``shared_parameters_counter`` with each round's ``counter[indices] += 1``
+    (sharing/PartialModel.py:205-207) applied on read: the encode writes the round's payload
+    indices into a slot of a device ring (:meth:`slot`, the payload itself, so nothing extra is
+    written), and the ring is folded into the int32 counter (dpz_counter_flush: scattered atomics
+    for a few rounds, one coalesced sweep of the counter for many) before any read — the node's
+    end-of-run dump (node/DPSGDNode.py:186-194), indexing, ``numpy`` — or when it is full.  The
+    encode itself then touches no counter line (its scattered read-modify-writes were 5.7x the
+    compact launch's payload traffic at 1 % top-k)."""
+
+    MAX_SEGS = 64  # rounds per ring (the flush passes their offsets as kernel arguments)
+
+    def __init__(self, t, cap_bytes=64 * 2 ** 20):
+        self._t = t
+        self.n = t.numel()
+        self.cap_bytes = int(cap_bytes)
+        self.ring = None
+        self.segs = [0]
+
+    def slot(self, k):
+        """int32[k] device view for this round's payload indices (commit with :meth:`commit`)."""
+        k = int(k)
+        if self.ring is None or self.ring.numel() < k:
+            self.flush()
+            rounds = max(1, min(self.MAX_SEGS, self.cap_bytes // max(4 * k, 1)))
+            self.ring = torch.empty(max(k * rounds, 1), dtype=torch.int32, device=self._t.device)
+        if self.segs[-1] + k > self.ring.numel() or len(self.segs) > self.MAX_SEGS:
+            self.flush()
+        return self.ring[self.segs[-1]:self.segs[-1] + k]
+
+    def commit(self, k):
+        """The slot handed out last holds a final payload (sorted, unique): count it."""
+        self.segs.append(self.segs[-1] + int(k))
+
+    def pending_rounds(self):
+        return len(self.segs) - 1
+
+    def flush(self):
+        if len(self.segs) > 1:
+            from . import codec
+            codec.counter_flush(self._t, self.ring, self.segs)
+            self.segs = [0]
+        return self._t
+
+    @property
+    def device_tensor(self):
+        return self.flush()
+
+
+class LazyChange:
+    """``model.model_change`` (sharing/PartialModel.py:317-331: T(x - init_model), plus the
+    accumulated changes with accumulation) formed only when something reads it.  The reference
+    sets it every round, but its only readers are ``extract_top_gradients``, which the fused
+    encode replaces, and ``save_change`` (:385-390, with ``save_accumulated``); forming it eagerly
+    cost one full elementwise pass (12 bytes per element) per round.  ``build`` forms the value from
+    tensors the round does not modify in place before ``_post_step`` drops the attribute; a writer
+    that would (DeviceAccumulator) materialises it first.  Reads behave like the tensor: torch
+    functions, methods and attributes, indexing, operators, ``numpy`` / ``tolist``."""
+
+    def __init__(self, build):
+        self._build = build
+        self._t = None
+
+    @property
+    def materialized(self):
+        return self._t is not None
+
+    def materialize(self):
+        if self._t is None:
+            self._t = self._build()
+            self._build = None
+        return self._t
+
+    def __getattr__(self, name):
+        if name.startswith("__") or name in ("_t", "_build"):
+            raise AttributeError(name)
+        return getattr(self.materialize(), name)
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        def unwrap(a):
+            if isinstance(a, LazyChange):
+                return a.materialize()
+            if isinstance(a, (list, tuple)):
+                return type(a)(unwrap(v) for v in a)
+            return a
+        return func(*unwrap(tuple(args)), **{k: unwrap(v) for k, v in (kwargs or {}).items()})
+
+    def __getitem__(self, item):
+        return self.materialize()[item]
+
+    def __len__(self):
+        return len(self.materialize())
+
+    def __array__(self, dtype=None):
+        a = self.materialize().cpu().numpy()
+        return a if dtype is None else a.astype(dtype)
+
+    __hash__ = object.__hash__
+
+
+def _lazy_op(name):
+    def op(self, *args):
+        return getattr(self.materialize(), name)(*args)
+    op.__name__ = name
+    return op
+
+
+for _name in ("__add__", "__radd__", "__sub__", "__rsub__", "__mul__", "__rmul__",
+              "__truediv__", "__rtruediv__", "__neg__", "__abs__", "__pow__", "__eq__", "__ne__",
+              "__lt__", "__le__", "__gt__", "__ge__", "__iter__", "__bool__", "__float__"):
+    setattr(LazyChange, _name, _lazy_op(_name))
+
+
 class SlicedCounter(DeviceCounter):
     """``shared_parameters_counter`` kept as 32 bit planes (dpz_topk_encode_sliced adds the
     selection to them with coalesced word updates); every read materialises the int32 vector
@@ -294,15 +408,31 @@ class DeviceAccumulator:
     def __init__(self, t):
         self.device_tensor = t
         self.pending = None
+        self._readers = []  # LazyChange values formed from device_tensor (watch)
+
+    def watch(self, lazy):
+        """``lazy`` (a LazyChange) reads device_tensor when it materialises: any in-place write
+        through this wrapper forms it first."""
+        self._readers.append(lazy)
+
+    def unwatch(self):
+        self._readers = []
+
+    def _before_write(self):
+        for lz in self._readers:
+            lz.materialize()
+        self._readers = []
 
     def settle(self):
         if self.pending is not None:
             from . import codec
+            self._before_write()
             codec.rewind_apply(self.device_tensor, self.pending)
             self.pending = None
         return self.device_tensor
 
     def zero_(self):
+        self._before_write()
         self.pending = None
         self.device_tensor.zero_()
         return self
@@ -340,6 +470,7 @@ class DeviceAccumulator:
         settle the pending rewind, then assign on the device tensor (host index arrays and
         values are moved to its device)."""
         t = self.settle()
+        self._before_write()
         if isinstance(item, (np.ndarray, list)):
             item = torch.as_tensor(np.asarray(item), device=t.device)
         elif isinstance(item, torch.Tensor):
@@ -352,7 +483,9 @@ class DeviceAccumulator:
         """``acc += change`` (PartialModel.py:346-349): settle, then add in place."""
         if isinstance(other, DeviceAccumulator):
             other = other.settle()
-        self.settle().add_(torch.as_tensor(other).to(self.device_tensor.device))
+        self.settle()
+        self._before_write()
+        self.device_tensor.add_(torch.as_tensor(other).to(self.device_tensor.device))
         return self
 
     @classmethod

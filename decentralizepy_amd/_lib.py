@@ -43,6 +43,9 @@ DPZ_EW_SUB = 1
 DPZ_EW_ADD = 2
 DPZ_EW_CHOCO = 3
 DPZ_EW_MHCOMBINE = 4
+DPZ_COUNTER_AUTO = 0
+DPZ_COUNTER_SCATTER = 1
+DPZ_COUNTER_SWEEP = 2
 DPZ_OK = 0
 DPZ_ERR_ARG = 1001
 DPZ_ERR_WORKSPACE = 1002
@@ -80,6 +83,8 @@ SIGNATURES = {
     "dpz_counter_unslice": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
     "dpz_counter_slice": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
     "dpz_rewind_apply": (_int, [_c_void_p, _c_void_p, _i64, _c_void_p]),
+    "dpz_counter_flush": (_int, [_c_void_p, _i64, _c_void_p, ctypes.POINTER(_i64), _int, _int,
+                                 _c_void_p]),
     "dpz_dwt_sym2_rewind": (_int, [_c_void_p, _c_void_p, _i64, _int, _c_void_p, _c_void_p,
                                    _c_void_p]),
     "dpz_dwt_haar_rewind": (_int, [_c_void_p, _c_void_p, _i64, _int, _c_void_p, _c_void_p,

@@ -23,7 +23,7 @@ __all__ = ["DPZ_ACC_NONE", "DPZ_ACC_ACCUMULATE", "DPZ_ACC_ADD", "DPZ_EW_SUB", "D
            "KernelTimer", "NodeStepBatch", "topk_sticky_status", "rfft", "irfft", "cplx_key",
            "cplx_gather", "cplx_pair_indices", "lz4_compress", "lz4_decompress", "lz4_frame_info",
            "delta_i32", "running_sum_i32", "mask_words", "topk_encode_sliced", "counter_unslice",
-           "counter_slice", "rewind_apply"]
+           "counter_slice", "rewind_apply", "counter_flush"]
 
 
 def _ptr(t):
@@ -278,6 +278,23 @@ def counter_slice(counter, planes=None):
     check(_lib.lib().dpz_counter_slice(_ptr(counter), n, _ptr(planes), _stream(counter.device)),
           "dpz_counter_slice")
     return planes
+
+
+def counter_flush(counter, ring, seg_off, mode=_lib.DPZ_COUNTER_AUTO):
+    """``counter[ring[j]] += 1`` for every entry of the ring's segments (dpz_counter_flush):
+    ``seg_off`` (host ints, seg_off[0] = 0) delimits segments of strictly ascending indices, one
+    per round's payload (reference PartialModel.py:205-207, applied on read)."""
+    _require(counter, torch.int32, "counter")
+    _require(ring, torch.int32, "ring")
+    m = len(seg_off) - 1
+    if m < 1:
+        return counter
+    if int(seg_off[-1]) > ring.numel():
+        raise ValueError("counter_flush: segments past the ring")
+    offs = (ctypes.c_int64 * (m + 1))(*[int(v) for v in seg_off])
+    check(_lib.lib().dpz_counter_flush(_ptr(counter), counter.numel(), _ptr(ring), offs, m,
+                                       int(mode), _stream(counter.device)), "dpz_counter_flush")
+    return counter
 
 
 def rewind_apply(acc, sel_mask):

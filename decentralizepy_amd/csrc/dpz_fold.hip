@@ -2030,7 +2030,11 @@ int fold_batch_walk(int m, const float* const* local, float* const* out, int64_t
                     const int64_t* k, const float* w, const float* w_self, int flags,
                     hipStream_t st, const int32_t* guard, int64_t guard_n) {
   if (DPZ_KNOB_INT(FOLD_BATCH, 1) == 0) return 1;  // diagnostic build: per-node launches (A/B)
-  if (m < 2 || (flags & ~(DPZ_FOLD_SELF | DPZ_FOLD_ALSO_LOCAL)) || !w || !idx) return 1;
+  // (every array this path reads is checked here: a null one falls through to the per-node
+  // validation, which returns DPZ_ERR_ARG)
+  if (m < 2 || (flags & ~(DPZ_FOLD_SELF | DPZ_FOLD_ALSO_LOCAL)) || !w || !idx || !vals || !k ||
+      !n_payloads || !local || !out)
+    return 1;
   if (n < 1024 || n >= (int64_t(1) << 31) - 1024) return 1;
   double dens = 0.0;
   int64_t off = 0;

@@ -486,6 +486,24 @@ __device__ __forceinline__ void sampled_filter_pipe_kernel_body(KeySrc s, int64_
         ctrl->hinted = 1;
         ctrl->val_h = (uint32_t)val_h;
       }
+      // the copy this launch owes (CP 1: the fused replace's out = x, whose payload entries the
+      // compact launch still scatters; CP 2: the fold's no-hit base) is written all the same:
+      // the re-run after the miss (dpz_topk_complete) encodes only, it has no copy slot
+      if (CP != 0) {
+        const int64_t ngc = (end4 - beg + 255) >> 8;
+        for (int64_t j = 0; j < ngc; ++j) {
+          const int64_t i0 = beg + j * 256 + lane * 4;
+          if (i0 < end4) {
+            const v4f a = xa[i0 >> 2];
+            const v4f b = CP == 1 ? a : v4f{fb.of(a.x), fb.of(a.y), fb.of(a.z), fb.of(a.w)};
+            __builtin_nontemporal_store(b, reinterpret_cast<v4f*>(copy_out) + (i0 >> 2));
+          }
+        }
+        if (end4 < end && end4 + lane < end) {
+          const float xv = s.x[end4 + lane];
+          copy_out[end4 + lane] = CP == 1 ? xv : fb.of(xv);
+        }
+      }
       return;
     }
     if (BID == 0) {
@@ -1252,9 +1270,14 @@ __device__ __forceinline__ void sampled_compact_kernel_body(KeySrc s, int64_t n,
     if (grand != (uint32_t)k) {  // internal inconsistency
       ctrl->status = 2;
       atomicOr(&ctrl->sticky, 2u);
-    } else {  // the next call with this signature may take its window from T (DPZ_TOPK_HINT)
+    } else if (T > 0u && T < 0x7F800000u) {
+      // the next call with this signature may take its window from T (DPZ_TOPK_HINT)
       ctrl->hint_T = T;
       ctrl->hint_sig = sig;
+    } else {
+      // T == 0 (fewer than k nonzero keys) or a non-finite T gives no window: no prior, so a
+      // hinted next call misses at once instead of filtering with a window it must reject
+      ctrl->hint_sig = 0u;
     }
     if (status_out) *status_out = grand != (uint32_t)k ? 2 : 0;
   }

@@ -198,10 +198,23 @@ class GossipRound:
         return torch.stack([codec.counter_unslice(self._planes[j], self.N)
                             for j in range(self.hi - self.lo)])
 
+    def counter_row(self, j, out=None):
+        """Owned node j's int32 counter alone (N values: the reference node's own
+        shared_parameters_counter, node/DPSGDNode.py:186-194) — without the (m, N) stack that
+        ``counter`` materialises for the sliced form; ``out`` (int32[N], device) is reused."""
+        if self._counter is not None:
+            return self._counter[j] if out is None else out.copy_(self._counter[j])
+        from . import codec
+        return codec.counter_unslice(self._planes[j], self.N, out=out)
+
     def _unslice(self):
         """Back to the int32 counter (the node-batched sliced encode does not take this
         geometry): the planes materialised once, the node tables rebuilt."""
-        self._counter = self.counter.contiguous()
+        m = self.hi - self.lo
+        cnt = torch.empty(m, self.N, dtype=torch.int32, device=self.device)
+        for j in range(m):  # row by row: no (m, N) stack beside the result
+            self.counter_row(j, out=cnt[j])
+        self._counter = cnt
         self._planes = self._selmask = None
         self.sliced_counter = False
         self.__dict__.pop("_node_tabs", None)
@@ -305,7 +318,13 @@ class GossipRound:
 
     def _rerun_missed(self, bad):
         """A missed sampled encode wrote nothing (no counter update either): re-run those nodes'
-        selections exactly (local node numbers)."""
+        selections exactly (local node numbers).  Their status words are cleared after: the
+        payloads are final, so a re-exchange and its folds must not see the stale miss."""
+        self._rerun_encodes(bad)
+        if bad:
+            self.status[torch.as_tensor(list(bad), dtype=torch.long, device=self.status.device)] = 0
+
+    def _rerun_encodes(self, bad):
         if not self._hip:
             for j in bad:
                 self._encode(self.x[j], self.x0[j], self.k, self.counter[j], self.send_idx[j],

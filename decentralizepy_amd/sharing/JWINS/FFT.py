@@ -75,7 +75,8 @@ class FFT(PartialModel):
             if mode == codec.DPZ_ACC_ACCUMULATE:  # the _pre_step bookkeeping still happens
                 codec.cplx_key(change, acc, mode)
             key = codec.cplx_key(fx)
-        idx, _ = codec.topk_encode(key, k, counter=self._counter, workspace=self.workspace)
+        idx, _ = codec.topk_encode(key, k, idx_out=self._ring_slot(k), workspace=self.workspace)
+        self._ring_commit(idx)
         vals = codec.cplx_gather(fx, idx, acc=acc)
         return idx, vals
 

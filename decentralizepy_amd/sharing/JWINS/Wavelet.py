@@ -85,6 +85,7 @@ class Wavelet(PartialModel):
             self._planes = torch.zeros(32 * nw, dtype=torch.int32, device=self.device)
             self._sel_mask = torch.zeros(nw, dtype=torch.int32, device=self.device)
             self._counter = None
+            self._ring = None  # the sliced planes replace the int32 counter and its ring
             self.model.shared_parameters_counter = SlicedCounter(self._planes,
                                                                  self.transformed_len)
             self.model.accumulated_changes = DeviceAccumulator(self.model.accumulated_changes)
@@ -115,14 +116,17 @@ class Wavelet(PartialModel):
             self.model.accumulated_changes.pending = self._sel_mask
             return idx, val
         if self.change_based_selection:
-            return codec.topk_encode(wc, k, acc=acc, acc_mode=self._acc_mode(), vals_src=wx,
-                                     counter=self._counter, workspace=self.workspace)
+            idx, val = codec.topk_encode(wc, k, acc=acc, acc_mode=self._acc_mode(), vals_src=wx,
+                                         idx_out=self._ring_slot(k), workspace=self.workspace)
+            self._ring_commit(idx)
+            return idx, val
         # selection on |W(x)|; the accumulation bookkeeping of _pre_step and the rewind still apply
         if self._acc_mode() == codec.DPZ_ACC_ACCUMULATE:
             codec.topk_encode(wc, 0, acc=acc, acc_mode=codec.DPZ_ACC_ACCUMULATE,
                               workspace=self.workspace)
-        idx, val = codec.topk_encode(wx, k, vals_src=wx, counter=self._counter,
+        idx, val = codec.topk_encode(wx, k, vals_src=wx, idx_out=self._ring_slot(k),
                                      workspace=self.workspace)
+        self._ring_commit(idx)
         if acc is not None:
             codec.scatter_fill(acc, idx, 0.0)
         return idx, val

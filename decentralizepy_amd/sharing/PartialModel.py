@@ -27,8 +27,8 @@ import numpy as np
 import torch
 
 from .. import codec
-from .._device import (DeviceAccumulator, DeviceCounter, state_to_device, state_version,
-                       to_host)
+from .._device import (DeviceAccumulator, LazyChange, RingCounter, state_to_device,
+                       state_version, to_host)
 from ..utils import conditional_value, identity
 from .Sharing import Sharing
 
@@ -77,8 +77,11 @@ class PartialModel(Sharing):
         if self.save_shared:
             self.folder_path = os.path.join(self.log_dir, "shared_params/{}".format(self.rank))
             Path(self.folder_path).mkdir(parents=True, exist_ok=True)
+        # the share counter: each round's payload indices are kept in a device ring and added to
+        # the int32 counter when it is read (RingCounter; the encode does no counter update)
         self._counter = torch.zeros(self.transformed_len, dtype=torch.int32, device=self.device)
-        self.model.shared_parameters_counter = DeviceCounter(self._counter)
+        self._ring = RingCounter(self._counter)
+        self.model.shared_parameters_counter = self._ring
         self.pre_share_model = None
         self.pre_share_model_transformed = None
 
@@ -151,19 +154,33 @@ class PartialModel(Sharing):
 
     def _model_change(self):
         """``model.model_change`` as the reference sets it (PartialModel.py:317-331): T(x - init),
-        and with accumulation the accumulated change before the rewind (acc + change, the value
-        the encode forms in registers; fp32 addition commutes, so it is the same bits as the
-        reference's ``acc += change`` / ``change += acc``).  A device tensor; the selection
-        itself never reads it (the encode fuses the change), so it costs one elementwise pass,
-        written into a buffer the plugin keeps across rounds (no allocation per round)."""
-        acc = self._acc()
-        change = self._change_dev
-        buf = getattr(self, "_mc_buf", None)
-        like = change if change is not None else self.pre_share_model
-        if buf is None or buf.shape != like.shape or buf.dtype != like.dtype:
-            buf = self._mc_buf = torch.empty_like(like)
+        and with accumulation the accumulated change before the rewind (acc + change; fp32
+        addition commutes, so it is the same bits as the reference's ``acc += change`` /
+        ``change += acc``).  The selection never reads it (the encode fuses the change), so it is
+        formed on read (LazyChange) whenever the round leaves its inputs untouched until
+        _post_step drops it: no accumulation (x and init_model are never written in place), or
+        the deferred-rewind accumulator (DeviceAccumulator: a write through it forms the value
+        first).  A plain accumulator is written in place by the encode (rewind, or acc += change
+        with DPZ_ACC_ACCUMULATE), so there the value is formed now, before the encode."""
+        x, init, change = self.pre_share_model, self.init_model, self._change_dev
+        acc = self.model.accumulated_changes if self.accumulation else None
+        if acc is None:
+            if change is not None:  # T(x - init) was formed for the key (wavelet, FFT)
+                return change
+            return LazyChange(lambda: self._form_change(x, init, None, None))
+        if isinstance(acc, DeviceAccumulator):
+            acc_t = acc.settle()
+            lz = LazyChange(lambda: self._form_change(x, init, change, acc_t))
+            acc.watch(lz)
+            return lz
+        return self._form_change(x, init, change, acc)
+
+    @staticmethod
+    def _form_change(x, init, change, acc):
+        """T(x - init) [+ acc] into a new device tensor (DPZ_EW_SUB / DPZ_EW_ADD kernels)."""
+        buf = torch.empty_like(change if change is not None else x)
         if change is None:
-            codec.elementwise(codec.DPZ_EW_SUB, self.pre_share_model, self.init_model, out=buf)
+            codec.elementwise(codec.DPZ_EW_SUB, x, init, out=buf)
             change = buf
         if acc is None:
             return change
@@ -171,28 +188,58 @@ class PartialModel(Sharing):
                           out=buf.view(torch.float32))
         return buf
 
-    def _encode(self, k):
-        """Top-k encode; returns device (idx int32[k], val fp32[k])."""
+    def _drop_model_change(self):
+        """``model.model_change = None`` (reference PartialModel.py:350), and the accumulator no
+        longer has to form it before a write."""
+        self.model.model_change = None
+        acc = getattr(self.model, "accumulated_changes", None)
+        if isinstance(acc, DeviceAccumulator):
+            acc.unwatch()
+
+    def _ring_slot(self, k):
+        """Payload index buffer for this round's encode: a slot of the counter ring (None when
+        the counter is kept in another form, e.g. the sliced planes)."""
+        ring = getattr(self, "_ring", None)
+        return ring.slot(k) if ring is not None and self._counter is not None else None
+
+    def _ring_commit(self, idx):
+        """The encode's payload indices are final: they count in shared_parameters_counter."""
+        ring = getattr(self, "_ring", None)
+        if ring is not None and self._counter is not None:
+            ring.commit(idx.numel())
+
+    def _encode(self, k, blocking=True):
+        """Top-k encode; returns device (idx int32[k], val fp32[k]).  ``blocking=False`` only
+        enqueues it (a sampled-path miss then shows in the workspace's sticky status word and the
+        result is not final: the device-time bench's back-to-back rounds, never the plugin's own
+        serialized_model, whose payload must be final)."""
         key_src = self._change_dev if self._change_dev is not None else self.pre_share_model
         x0 = None if self._change_dev is not None else self.init_model
         acc = self._acc()
         self._fb = None
         pred = self._predicted_fold() if self._change_dev is None and acc is None else None
+        # the payload indices go straight into the counter ring's slot (no counter update here)
+        slot = self._ring_slot(k)
         if pred is not None:
             # one neighbour: the encode's filter also writes the fold's no-hit base over x
             # (dpz_topk_encode_foldbase); _averaging then rewrites only the payload's elements
             base = torch.empty_like(self.pre_share_model)
             out = codec.topk_encode(key_src, k, x0=x0, vals_src=self.pre_share_model_transformed,
-                                    counter=self._counter, workspace=self.workspace,
-                                    fold_base=(base, pred[0], pred[1]), hint=True, keep_x=True)
+                                    idx_out=slot, workspace=self.workspace,
+                                    fold_base=(base, pred[0], pred[1]), hint=True, keep_x=True,
+                                    asynchronous=not blocking)
             self._fb = (base, pred, self.pre_share_model)
+            self._ring_commit(out[0])
             return out
         # hint: the previous round's exact threshold as this round's key window (no sample
         # launch); keep_x: _averaging folds over this x right after (Infinity Cache)
-        return codec.topk_encode(key_src, k, x0=x0, acc=acc, acc_mode=self._acc_mode(),
-                                 vals_src=self.pre_share_model_transformed, counter=self._counter,
-                                 workspace=self.workspace, hint=True,
-                                 keep_x=key_src is self.pre_share_model)
+        out = codec.topk_encode(key_src, k, x0=x0, acc=acc, acc_mode=self._acc_mode(),
+                                vals_src=self.pre_share_model_transformed, idx_out=slot,
+                                workspace=self.workspace, hint=True,
+                                keep_x=key_src is self.pre_share_model,
+                                asynchronous=not blocking)
+        self._ring_commit(out[0])
+        return out
 
     def _predicted_fold(self):
         """The Metro-Hastings weights _averaging will use (Sharing.py:156-190), predicted from
@@ -301,6 +348,9 @@ class PartialModel(Sharing):
     def _post_step(self):
         """reference PartialModel.py:333-353; the new model is already on the device (fold output)."""
         logging.debug("PartialModel _post_step")
+        # model_change is None after the post-step (reference PartialModel.py:350); dropped first,
+        # so the accumulating pass below need not form a lazily kept value nobody can read
+        self._drop_model_change()
         with torch.no_grad():
             post = getattr(self, "_post_model_dev", None)
             if post is None or not self._all_fp32:
@@ -311,7 +361,6 @@ class PartialModel(Sharing):
                 if self.accumulate_averaging_changes:
                     self._accumulate_change(self.init_model, self.prev)
                 self.prev = self.init_model
-            self.model.model_change = None
         if self.save_accumulated:
             self.save_change()
 

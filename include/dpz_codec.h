@@ -258,6 +258,23 @@ int dpz_counter_unslice(const uint32_t* planes, int64_t n, int32_t* counter, dpz
 int dpz_counter_slice(const int32_t* counter, int64_t n, uint32_t* planes, dpz_stream_t stream);
 int dpz_rewind_apply(float* acc, const uint32_t* sel_mask, int64_t n, dpz_stream_t stream);
 
+/* ---- the int32 share counter applied on read (ring of sent payload indices) -----------------
+ * Replaces the per-round `shared_parameters_counter[indices] += 1` of reference
+ * sharing/PartialModel.py:205-207 / sharing/JWINS/Wavelet.py:194-195, whose only reader is the
+ * end-of-run dump (node/DPSGDNode.py:186-194): the plugin keeps every round's payload indices (the
+ * encode's idx_out, strictly ascending int32 in [0, n)) in one device ring and, before any read
+ * of the counter or when the ring is full, applies them all:
+ *   counter[ring[j]] += 1 for every j < seg_off[m], segment r = ring[seg_off[r], seg_off[r + 1])
+ * seg_off: HOST int64[m + 1], seg_off[0] = 0, ascending; each segment strictly ascending indices
+ * in [0, n) (an index outside is skipped).  mode DPZ_COUNTER_SCATTER: one atomic per entry;
+ * DPZ_COUNTER_SWEEP: every tile of the counter read, incremented in LDS and written once (8n
+ * coalesced bytes + 4 per entry, per 64 segments); DPZ_COUNTER_AUTO picks the cheaper.        */
+#define DPZ_COUNTER_AUTO 0
+#define DPZ_COUNTER_SCATTER 1
+#define DPZ_COUNTER_SWEEP 2
+int dpz_counter_flush(int32_t* counter, int64_t n, const int32_t* ring, const int64_t* seg_off,
+                      int m, int mode, dpz_stream_t stream);
+
 /* Batched decode + Metro-Hastings fold over n_payloads neighbour payloads.
  * Replaces reference sharing/PartialModel.py:257-303 (T = cat(local); T[idx] = params),
  * sharing/Sharing.py:156-229 (_averaging / _averaging_server fold) and
@@ -469,7 +486,8 @@ enum {
   DPZ_KT_FOLD_OFFSETS, DPZ_KT_FOLD, DPZ_KT_DWT, DPZ_KT_IDWT, DPZ_KT_ELIAS_COUNT,
   DPZ_KT_ELIAS_SCAN, DPZ_KT_ELIAS_PACK, DPZ_KT_ELIAS_SPEC, DPZ_KT_ELIAS_RESOLVE,
   DPZ_KT_ELIAS_WRITE, DPZ_KT_FP16, DPZ_KT_SCATTER, DPZ_KT_FPZ_SIZE, DPZ_KT_FPZ_SCAN,
-  DPZ_KT_FPZ_PACK, DPZ_KT_FPZ_DECODE, DPZ_KT_CPLX, DPZ_KT_FFT_SCALE, DPZ_KT_HAAR, DPZ_KT_LZ4, DPZ_KT_COUNT
+  DPZ_KT_FPZ_PACK, DPZ_KT_FPZ_DECODE, DPZ_KT_CPLX, DPZ_KT_FFT_SCALE, DPZ_KT_HAAR, DPZ_KT_LZ4,
+  DPZ_KT_COUNTER, DPZ_KT_COUNT
 };
 int dpz_timing_enable(int on);  /* also clears the accumulators */
 int dpz_timing_read(double* ms_sum, int64_t* count, int max_ids);

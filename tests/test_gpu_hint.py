@@ -195,3 +195,44 @@ def test_hinted_sliced_rounds_match_oracle(dev, alpha, blocking):
         words = np.zeros(nw, dtype=np.uint32)
         np.bitwise_or.at(words, oi >> 5, (np.uint32(1) << (oi & 31).astype(np.uint32)))
         np.testing.assert_array_equal(mask.cpu().numpy().view(np.uint32), words)
+
+
+@pytest.mark.parametrize("what", ["fold_base", "co_replace"])
+def test_unusable_prior_still_writes_the_copy(dev, what):
+    """A hinted call whose prior window is unusable (here: a prior of another k, the flag forced
+    past the Python check) misses at once and is re-run by the blocking call — which encodes
+    only.  The copy the missed filter owed is written all the same: the fold's no-hit base
+    (dpz_topk_encode_foldbase, PartialModel's one-neighbour fold) and the fused replace decode's
+    out = x (dpz_topk_encode_replace, whose payload entries the compact launch still scatters):
+    reference Sharing.py:156-190 / PartialModel.py:257-303 over the node's own model."""
+    from decentralizepy_amd import codec
+    n, k = 1_000_003, 10_000
+    ws = codec.Workspace(dev)
+    big = int(codec._lib.lib().dpz_topk_workspace_bytes(n, 20_000))
+    ws.buf = torch.zeros(big, dtype=torch.uint8, device=dev)
+    x, x0 = _inputs(n, 600, 0.01)
+    tx, tx0 = torch.from_numpy(x).to(dev), torch.from_numpy(x0).to(dev)
+    codec.topk_encode(tx, 20_000, x0=tx0, workspace=ws, hint=True)  # the prior: another k
+    codec.topk_sticky_status(ws, clear=True)
+    ws.hint_key = (n, k, False, 0, True)  # the flag is passed; the device signature differs
+    if what == "fold_base":
+        out = torch.full((n,), float("nan"), device=dev)
+        i, v = codec.topk_encode(tx, k, x0=tx0, workspace=ws, hint=True, keep_x=True,
+                                 fold_base=(out, [0.25, 0.25], 0.5))
+        q = np.float32(0.25)
+        ref = ((x * q) + (x * q)) + (x * np.float32(0.5))  # fp32, one rounding per op
+    else:
+        rng = np.random.default_rng(601)
+        ri = np.sort(rng.choice(n, size=5_000, replace=False)).astype(np.int32)
+        rv = rng.standard_normal(5_000).astype(np.float32)
+        out = torch.full((n,), float("nan"), device=dev)
+        i, v = codec.topk_encode(tx, k, x0=tx0, workspace=ws, hint=True,
+                                 co_replace=(tx, torch.from_numpy(ri).to(dev),
+                                             torch.from_numpy(rv).to(dev), out))
+        ref = x.copy()
+        ref[ri] = rv
+    assert codec.topk_sticky_status(ws, clear=True) != 0  # the hinted call did miss
+    np.testing.assert_array_equal(_bits(out.cpu().numpy()), _bits(ref))
+    oi, ov = otopk.encode(x, x0, None, otopk.ACC_NONE, k)
+    np.testing.assert_array_equal(i.cpu().numpy(), oi)
+    np.testing.assert_array_equal(_bits(v.cpu().numpy()), _bits(ov))
