@@ -278,6 +278,7 @@ class RingCounter(DeviceCounter):
         self.cap_bytes = int(cap_bytes)
         self.ring = None
         self.segs = [0]
+        self._ws = None  # the flush's scratch (allocated with the ring)
 
     def slot(self, k):
         """int32[k] device view for this round's payload indices (commit with :meth:`commit`)."""
@@ -286,6 +287,11 @@ class RingCounter(DeviceCounter):
             self.flush()
             rounds = max(1, min(self.MAX_SEGS, self.cap_bytes // max(4 * k, 1)))
             self.ring = torch.empty(max(k * rounds, 1), dtype=torch.int32, device=self._t.device)
+            if self._ws is None:
+                from . import _lib
+                self._ws = torch.empty(
+                    int(_lib.lib().dpz_counter_flush_workspace_bytes(self.n)), dtype=torch.uint8,
+                    device=self._t.device)
         if self.segs[-1] + k > self.ring.numel() or len(self.segs) > self.MAX_SEGS:
             self.flush()
         return self.ring[self.segs[-1]:self.segs[-1] + k]
@@ -300,7 +306,7 @@ class RingCounter(DeviceCounter):
     def flush(self):
         if len(self.segs) > 1:
             from . import codec
-            codec.counter_flush(self._t, self.ring, self.segs)
+            codec.counter_flush(self._t, self.ring, self.segs, workspace=self._ws)
             self.segs = [0]
         return self._t
 

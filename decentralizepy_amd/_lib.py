@@ -83,8 +83,9 @@ SIGNATURES = {
     "dpz_counter_unslice": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
     "dpz_counter_slice": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
     "dpz_rewind_apply": (_int, [_c_void_p, _c_void_p, _i64, _c_void_p]),
+    "dpz_counter_flush_workspace_bytes": (_size, [_i64]),
     "dpz_counter_flush": (_int, [_c_void_p, _i64, _c_void_p, ctypes.POINTER(_i64), _int, _int,
-                                 _c_void_p]),
+                                 _c_void_p, _size, _c_void_p]),
     "dpz_dwt_sym2_rewind": (_int, [_c_void_p, _c_void_p, _i64, _int, _c_void_p, _c_void_p,
                                    _c_void_p]),
     "dpz_dwt_haar_rewind": (_int, [_c_void_p, _c_void_p, _i64, _int, _c_void_p, _c_void_p,

@@ -280,10 +280,11 @@ def counter_slice(counter, planes=None):
     return planes
 
 
-def counter_flush(counter, ring, seg_off, mode=_lib.DPZ_COUNTER_AUTO):
+def counter_flush(counter, ring, seg_off, mode=_lib.DPZ_COUNTER_AUTO, workspace=None):
     """``counter[ring[j]] += 1`` for every entry of the ring's segments (dpz_counter_flush):
     ``seg_off`` (host ints, seg_off[0] = 0) delimits segments of strictly ascending indices, one
-    per round's payload (reference PartialModel.py:205-207, applied on read)."""
+    per round's payload (reference PartialModel.py:205-207, applied on read).  ``workspace``: a
+    device uint8 tensor kept by the caller (grown here when too small)."""
     _require(counter, torch.int32, "counter")
     _require(ring, torch.int32, "ring")
     m = len(seg_off) - 1
@@ -291,9 +292,13 @@ def counter_flush(counter, ring, seg_off, mode=_lib.DPZ_COUNTER_AUTO):
         return counter
     if int(seg_off[-1]) > ring.numel():
         raise ValueError("counter_flush: segments past the ring")
+    need = int(_lib.lib().dpz_counter_flush_workspace_bytes(counter.numel()))
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=counter.device)
     offs = (ctypes.c_int64 * (m + 1))(*[int(v) for v in seg_off])
     check(_lib.lib().dpz_counter_flush(_ptr(counter), counter.numel(), _ptr(ring), offs, m,
-                                       int(mode), _stream(counter.device)), "dpz_counter_flush")
+                                       int(mode), _ptr(workspace), workspace.numel(),
+                                       _stream(counter.device)), "dpz_counter_flush")
     return counter
 
 

@@ -268,12 +268,15 @@ int dpz_rewind_apply(float* acc, const uint32_t* sel_mask, int64_t n, dpz_stream
  * seg_off: HOST int64[m + 1], seg_off[0] = 0, ascending; each segment strictly ascending indices
  * in [0, n) (an index outside is skipped).  mode DPZ_COUNTER_SCATTER: one atomic per entry;
  * DPZ_COUNTER_SWEEP: every tile of the counter read, incremented in LDS and written once (8n
- * coalesced bytes + 4 per entry, per 64 segments); DPZ_COUNTER_AUTO picks the cheaper.        */
+ * coalesced bytes + 8 per entry, per 64 segments; ws: device scratch of
+ * dpz_counter_flush_workspace_bytes(n) bytes, only the sweep uses it); DPZ_COUNTER_AUTO picks
+ * the cheaper.                                                                                 */
 #define DPZ_COUNTER_AUTO 0
 #define DPZ_COUNTER_SCATTER 1
 #define DPZ_COUNTER_SWEEP 2
+size_t dpz_counter_flush_workspace_bytes(int64_t n);
 int dpz_counter_flush(int32_t* counter, int64_t n, const int32_t* ring, const int64_t* seg_off,
-                      int m, int mode, dpz_stream_t stream);
+                      int m, int mode, void* ws, size_t ws_bytes, dpz_stream_t stream);
 
 /* Batched decode + Metro-Hastings fold over n_payloads neighbour payloads.
  * Replaces reference sharing/PartialModel.py:257-303 (T = cat(local); T[idx] = params),

@@ -18,7 +18,8 @@ NAMES = {"sampled_sample_kernel": "topk_sample", "sampled_filter_kernel": "topk_
          "fold_kernel": "fold", "fold_group_kernel": "fold_group", "fold_slots_kernel": "fold_slots",
          "fold_walk_kernel": "fold_walk", "fold_walk_groups_kernel": "fold_walk", "replace_kernel": "fold", "dwt_kernel": "dwt", "dwt4_kernel": "dwt",
          "haar_dwt_kernel": "haar_dwt", "haar_idwt_kernel": "haar_idwt",
-         "idwt_kernel": "idwt"}
+         "idwt_kernel": "idwt", "counter_sweep_kernel": "counter_flush",
+         "counter_bounds_kernel": "counter_bounds", "counter_scatter_kernel": "counter_flush"}
 
 
 # sampled_filter_pipe_kernel<SRC, CP, D, OCC>: CP = 1 writes the fused decode's copy of x (the
