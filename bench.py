@@ -687,13 +687,16 @@ def main():
                            "n": r["n"], "k": r["k"], "alpha": args.alpha,
                            "parallelism": f"{r['nodes']} nodes sharded over {world} GPU(s), one "
                                           "RCCL all-gather of the payloads per round"},
-                "round_alg_bytes": r["alg_bytes"],
-                "round_frac_of_hbm_peak": round(r["alg_bytes"] / r["s_step"] / 1e9 / HBM_PEAK_GBS / world, 4),
-                "round_frac_of_hbm_peak_fold_8n": round(r["alg_bytes_8n"] / r["s_step"] / 1e9
-                                                        / HBM_PEAK_GBS / world, 4),
-                "alg_bytes_note": "fold 12N: the averaged model is written as the model and as "
-                                  "init_model (Sharing.py:186-190, PartialModel.py:340-343); "
-                                  "*_fold_8n counts it once (round-4 convention)",
+                "round_alg_bytes": r["alg_bytes_8n"],
+                "round_frac_of_hbm_peak": round(r["alg_bytes_8n"] / r["s_step"] / 1e9
+                                                / HBM_PEAK_GBS / world, 4),
+                "round_frac_of_hbm_peak_fold_12n": round(r["alg_bytes"] / r["s_step"] / 1e9
+                                                         / HBM_PEAK_GBS / world, 4),
+                "alg_bytes_note": "SURVEY §8(d) C4 accounting: per node encode 8N + 16k, fold 8N "
+                                  "+ 8k per payload (the averaged model counted once); "
+                                  "*_fold_12n also counts its second write (the node keeps it as "
+                                  "model and as init_model, Sharing.py:186-190, "
+                                  "PartialModel.py:340-343)",
                 "legs_ms": r["legs_ms"],
                 "reduce_scatter_mode": {
                     "note": "the over-HBM exchange forced (exchange='reduce_scatter'): payloads "
@@ -961,14 +964,15 @@ def gossip_line(gr, world):
                            + ("one RCCL all-gather of the payloads per round" if world > 1
                               else "no collective on one GPU"),
             "legs_ms": gr["legs_ms"],
-            "round_alg_bytes": gr["alg_bytes"],
-            "round_frac_of_hbm_peak": round(gr["alg_bytes"] / gr["s_step"] / 1e9
+            "round_alg_bytes": gr["alg_bytes_8n"],
+            "round_frac_of_hbm_peak": round(gr["alg_bytes_8n"] / gr["s_step"] / 1e9
                                             / HBM_PEAK_GBS / world, 4),
-            "round_frac_of_hbm_peak_fold_8n": round(gr["alg_bytes_8n"] / gr["s_step"] / 1e9
-                                                    / HBM_PEAK_GBS / world, 4),
-            "alg_bytes_note": "fold 12N: the averaged model is written as the model and as "
-                              "init_model (Sharing.py:186-190, PartialModel.py:340-343); "
-                              "*_fold_8n counts it once (round-4 convention)"}
+            "round_frac_of_hbm_peak_fold_12n": round(gr["alg_bytes"] / gr["s_step"] / 1e9
+                                                     / HBM_PEAK_GBS / world, 4),
+            "alg_bytes_note": "SURVEY §8(d) C4 accounting: per node encode 8N + 16k, fold 8N + 8k "
+                              "per payload (the averaged model counted once); *_fold_12n also "
+                              "counts its second write (model and init_model, Sharing.py:186-190, "
+                              "PartialModel.py:340-343)"}
 
 if __name__ == "__main__":
     main()

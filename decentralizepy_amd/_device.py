@@ -6,6 +6,7 @@ rank and move only the flat model and the payloads across PCIe, through pinned s
 """
 import functools
 import os
+import warnings
 
 import numpy as np
 import torch
@@ -67,6 +68,38 @@ class Staging:
         self._events[(name, dtype)] = ev
 
 
+def _as_cpu_tensor(src):
+    """A CPU tensor view (no copy) of a bytes-like object, numpy array or CPU tensor.  A
+    read-only buffer (a bytes object from pickle.loads) is only read, so torch's warning about
+    non-writable memory does not apply."""
+    if isinstance(src, torch.Tensor):
+        return src
+    if isinstance(src, (bytes, bytearray, memoryview)):
+        a = np.frombuffer(memoryview(src), dtype=np.uint8)
+    else:
+        a = np.ascontiguousarray(src)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        return torch.from_numpy(a)
+
+
+def host_copy_into(dst, src):
+    """``dst[:] = src`` for a CPU (pinned staging) tensor with torch's parallel copy (its intra-op
+    threads: the node process's CPU share) instead of numpy's single-threaded slice assignment —
+    the receive path stages tens of MB of payload bytes per round (JWINS)."""
+    t = _as_cpu_tensor(src).reshape(-1)
+    if t.dtype != dst.dtype:
+        t = t.view(dst.dtype) if t.element_size() == dst.element_size() else t.to(dst.dtype)
+    dst.view(-1)[:t.numel()].copy_(t)
+    return dst
+
+
+def host_owned(t):
+    """A numpy array owning a copy of the CPU tensor ``t`` (pinned staging about to be reused),
+    made with torch's parallel copy."""
+    return torch.empty(t.shape, dtype=t.dtype).copy_(t).numpy()
+
+
 def flatten_state(state_dict):
     """``torch.cat`` of the flattened state tensors (reference sharing/Sharing.py:93-112)."""
     return torch.cat([v.flatten() for v in state_dict.values()])
@@ -124,7 +157,7 @@ def h2d_array(arr, dtype, device, staging, name):
     host = staging.get(name, a.size, tdt)
     if host is None:  # over the pinned cap: pageable copy
         return torch.from_numpy(a.reshape(-1)).to(device)
-    host.numpy()[...] = a.reshape(-1)
+    host_copy_into(host, a)
     out = host.to(device, non_blocking=True)
     staging.mark(name, tdt, torch.cuda.current_stream(device))
     return out
@@ -216,7 +249,7 @@ def to_host(t, staging, name, own=True):
         return t.cpu().numpy().copy()
     host.copy_(t, non_blocking=True)
     torch.cuda.current_stream(t.device).synchronize()
-    return host.numpy().copy() if own else host.numpy()
+    return host_owned(host) if own else host.numpy()
 
 
 class DeviceCounter:

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from .. import codec
-from .._device import pick_device
+from .._device import host_copy_into, host_owned, pick_device
 from .Compression import Compression
 
 
@@ -62,7 +62,7 @@ class Elias(Compression):
         pin = _grown(self._ws, "elias_out_pin", enc.numel(), dict(pin_memory=True))[:enc.numel()]
         pin.copy_(enc, non_blocking=True)
         torch.cuda.current_stream(enc.device).synchronize()
-        return pin.numpy().copy()
+        return host_owned(pin)
 
     def decompress_device(self, buf, dtype=torch.int32, device=None):
         """Host stream -> device index tensor (int32 for the fold kernels, or int64)."""
@@ -76,9 +76,8 @@ class Elias(Compression):
         ws = self._ws
         pin = _grown(ws, "elias_pin", need, dict(pin_memory=True))
         dbuf = _grown(ws, "elias_dev", need, dict(device=dev))
-        pn = pin.numpy()
-        pn[:nbytes] = b
-        pn[nbytes:need] = 0
+        host_copy_into(pin[:nbytes], b)
+        pin[nbytes:need].zero_()
         dbuf[:need].copy_(pin[:need], non_blocking=True)
         dbuf = dbuf[:need]
         count = max(nbits - 128, 0) + 1

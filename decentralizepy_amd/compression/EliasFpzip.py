@@ -11,6 +11,7 @@ import numpy as np
 import torch
 
 from .. import codec
+from .._device import host_copy_into, host_owned
 from .Elias import Elias, _grown
 
 _MAGIC = 0x5A465044
@@ -46,7 +47,7 @@ class EliasFpzip(Elias):
         pin = _grown(self._ws, "fpz_out_pin", s.numel(), dict(pin_memory=True))[:s.numel()]
         pin.copy_(s, non_blocking=True)
         torch.cuda.current_stream(s.device).synchronize()
-        return pin.numpy().copy()
+        return host_owned(pin)
 
     def decompress_float_device(self, bytes, device=None):
         """Host stream bytes -> device fp32 values.  Up through a pinned buffer and into a
@@ -61,7 +62,7 @@ class EliasFpzip(Elias):
         ws = self._ws
         pin = _grown(ws, "fpz_pin", nb, dict(pin_memory=True))
         dbuf = _grown(ws, "fpz_dev", nb, dict(device=dev))
-        pin.numpy()[:nb] = b
+        host_copy_into(pin[:nb], b)
         dbuf[:nb].copy_(pin[:nb], non_blocking=True)
         return codec.fpz_decode(dbuf[:nb], n, prec)
 

@@ -2103,6 +2103,430 @@ extern "C" int dpz_debug_fold_stamps(unsigned long long* host_out, int reset) {
 }
 #endif
 
+// ---- merge fold: a group of sparse payloads merged per tile through an LDS hit mask ------------
+// (round 6; the JWINS receive, 16 payloads at alpha 0.01: reference Wavelet.py:269-309)
+// A persistent block walks a contiguous run of TE-element tiles.  Wave w holds the 64-entry
+// windows of payloads w, w + 4, w + 8, w + 12 (the next tile's windows and local values are
+// issued one tile ahead, so the stream's loads are in flight while a tile is merged).  Per tile:
+//   1. every payload's entries in the tile (the leading window lanes below the tile's end) set
+//      bit p of their element's word in an LDS mask;
+//   2. each thread counts its elements' bits; a block scan gives every hit element a contiguous
+//      run of value slots, in payload order (the rank of bit p among the element's bits);
+//   3. every entry writes its value to its slot; the entry with the lowest payload number of an
+//      element (its "owner") appends the element to a list;
+//   4. the threads fold the listed (hit) elements exactly: term p = (bit p ? slot value : local)
+//      * w_p in payload order, then the self term (the reference's fp32 order);
+//   5. every element folds its local value alone (base), and takes the listed result where hit.
+// Every element's local value and output are read / written once, every payload entry read once
+// (extra windows of a payload denser than 64 entries per tile are re-read from L2).  A tile whose
+// entries exceed the value slots (adversarial clustering) folds payload by payload instead.
+// Weights all equal (EQW: a regular graph's Metro-Hastings weights): the base is one product and
+// np - 1 additions of it, the same bits as the general order.
+constexpr int FM_THREADS = 256;
+constexpr int FM_WAVES = FM_THREADS / 64;
+constexpr int FM_SLOTS = FOLD_MAXP / FM_WAVES;  // payload slots per wave: payload wid + 4 j
+
+template <int EPT>
+struct FmCfg {
+  static constexpr int TE = FM_THREADS * EPT;  // elements per tile
+  static constexpr int CAP = 2 * TE;           // value slots per tile
+  static constexpr int CH = EPT / 4;           // float4 chunks per thread
+  static_assert(EPT % 4 == 0 && CAP <= 65535, "float4 chunks, u16 slot offsets");
+};
+
+// element e of thread t (chunk e / 4 at (e / 4) * 4 * FM_THREADS + 4 t + e % 4: float4-coalesced)
+__device__ __forceinline__ int fm_elem(int t, int e) {
+  return (e >> 2) * (4 * FM_THREADS) + 4 * t + (e & 3);
+}
+
+// Branch-free (the compiler then waits only for the registers it uses, never for the next
+// tile's loads in flight): a float4 group reaching past n reads the last whole group instead; the
+// global last tile, if ragged, is reloaded element-wise by fm_load_tail before use.
+template <int EPT>
+__device__ __forceinline__ void fm_load(const float* __restrict__ p, int64_t tlo, int64_t n, int t,
+                                        float (&v)[EPT]) {
+  const int64_t last = (n & ~int64_t(3)) - 4;
+#pragma unroll
+  for (int c = 0; c < EPT / 4; ++c) {
+    const int64_t i0 = tlo + fm_elem(t, 4 * c);
+    const float4 q = *reinterpret_cast<const float4*>(p + (i0 + 4 <= n ? i0 : last));
+    v[4 * c] = q.x; v[4 * c + 1] = q.y; v[4 * c + 2] = q.z; v[4 * c + 3] = q.w;
+  }
+}
+
+template <int EPT>
+__device__ __forceinline__ void fm_load_tail(const float* __restrict__ p, int64_t tlo, int64_t n,
+                                             int t, float (&v)[EPT]) {
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int64_t i = tlo + fm_elem(t, e);
+    v[e] = p[i < n ? i : n - 1];
+  }
+}
+
+template <int EPT>
+__device__ __forceinline__ void fm_store(float* __restrict__ p, int64_t tlo, int64_t n, int t,
+                                         const float (&v)[EPT]) {
+  constexpr int TE = FmCfg<EPT>::TE;
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  if (tlo + TE <= n) {
+#pragma unroll
+    for (int c = 0; c < EPT / 4; ++c) {
+      const v4f q = {v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
+      __builtin_nontemporal_store(q, reinterpret_cast<v4f*>(p + tlo + fm_elem(t, 4 * c)));
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const int64_t i = tlo + fm_elem(t, e);
+      if (i < n) p[i] = v[e];
+    }
+  }
+}
+
+template <int EPT, bool EQW>
+__global__ void __launch_bounds__(FM_THREADS) fold_merge_kernel(FoldArgs a, int64_t tpb, int abl) {
+  using C = FmCfg<EPT>;
+  constexpr int TE = C::TE, CAP = C::CAP;
+  __shared__ __attribute__((aligned(16))) uint32_t s_mask[2][TE];
+  __shared__ __attribute__((aligned(16))) uint16_t s_pre[TE];
+  __shared__ __attribute__((aligned(16))) float s_x[TE];
+  __shared__ float s_val[CAP];
+  __shared__ uint16_t s_list[TE];
+  __shared__ uint32_t s_wsum[16];
+  __shared__ uint32_t s_nown;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int64_t n = a.n;
+  const int np = a.np;
+  const int64_t ntl = (n + TE - 1) / TE;
+  const int64_t t0 = (int64_t)blockIdx.x * tpb;
+  const int64_t t1 = t0 + tpb < ntl ? t0 + tpb : ntl;
+  if (t0 >= t1) return;  // uniform over the block
+  // payload parameters: lane p holds payload p's, read back per slot / per chain step (readlane)
+  const int lp = lane < np ? lane : 0;
+  const uint64_t ipl = reinterpret_cast<uint64_t>(a.p[lp].k > 0 ? a.p[lp].idx
+                                                                : reinterpret_cast<const int32_t*>(a.local));
+  const uint64_t vpl = reinterpret_cast<uint64_t>(a.p[lp].k > 0 ? a.p[lp].val : a.local);
+  const int32_t kl = lane < np ? (int32_t)a.p[lp].k : 0;
+  const float wl = a.p[lp].w;
+  auto rl64 = [](uint64_t v, int p) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, p);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), p);
+    return ((uint64_t)hi << 32) | lo;
+  };
+  const int32_t* sidx[FM_SLOTS];
+  const float* sval[FM_SLOTS];
+  int32_t sk[FM_SLOTS];
+#pragma unroll
+  for (int j = 0; j < FM_SLOTS; ++j) {
+    const int p = wid + FM_WAVES * j;
+    const bool live = p < np;
+    sidx[j] = reinterpret_cast<const int32_t*>(rl64(ipl, live ? p : 0));
+    sval[j] = reinterpret_cast<const float*>(rl64(vpl, live ? p : 0));
+    sk[j] = live ? fw_uni(__builtin_amdgcn_readlane(kl, p)) : 0;
+  }
+  const int nsl = np > wid ? (np - wid + FM_WAVES - 1) / FM_WAVES : 0;  // this wave's live slots
+  for (int i = t; i < 2 * TE; i += FM_THREADS) (&s_mask[0][0])[i] = 0u;
+  if (t == 0) s_nown = 0u;
+  // start cursors: lower_bound(idx_p, t0 * TE) of this wave's payloads (lane j: slot j)
+  const int32_t curv = fw_start_cursors<FM_SLOTS, false>(
+      nsl, (int32_t)(t0 * TE), lane, [&](int j) { return sidx[j]; }, [&](int j) { return sk[j]; },
+      reinterpret_cast<const int32_t*>(a.local));
+  int32_t cs[FM_SLOTS];
+#pragma unroll
+  for (int j = 0; j < FM_SLOTS; ++j) cs[j] = fw_uni(__builtin_amdgcn_readlane(curv, j));
+  int32_t wi[FM_SLOTS], wn[FM_SLOTS];
+  float wv[FM_SLOTS], wvn[FM_SLOTS];
+  auto load_window = [&](int j, int32_t c, int32_t& ix, float& vx) {
+    const int32_t q = c + lane;
+    const bool ok = q < sk[j];
+    const int32_t qq = ok ? q : 0;
+    ix = as_global(sidx[j])[qq];
+    vx = as_global(sval[j])[qq];
+    ix = ok ? ix : INT32_MAX;
+  };
+#pragma unroll
+  for (int j = 0; j < FM_SLOTS; ++j) load_window(j, cs[j], wi[j], wv[j]);
+  float L[EPT], Ln[EPT];
+  fm_load<EPT>(a.local, t0 * TE, n, t, L);
+  const float w0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl), 0));
+  uint32_t buf = 0;
+  __syncthreads();  // masks zeroed
+  for (int64_t tile = t0; tile < t1; ++tile) {
+    const int64_t tlo = tile * TE;
+    const int32_t tlo32 = (int32_t)tlo, thi32 = tlo32 + TE;
+    uint32_t* const mask = s_mask[buf];
+    if (tlo + TE > n) fm_load_tail<EPT>(a.local, tlo, n, t, L);  // the ragged last tile
+    // 1. mask bits of every payload's entries in the tile; the next tile's windows issued
+    int32_t c0[FM_SLOTS], cfirst[FM_SLOTS];
+#pragma unroll
+    for (int j = 0; j < FM_SLOTS; ++j) {
+      c0[j] = cs[j];
+      cfirst[j] = 0;
+      if (j >= nsl) continue;  // uniform
+      const int p = wid + FM_WAVES * j;
+      int32_t c = fw_lead(wi[j] < thi32);
+      cfirst[j] = c;
+      if (!(abl & 4)) {
+        const uint32_t pos = (uint32_t)(wi[j] - tlo32);
+        if (lane < c && pos < (uint32_t)TE) atomicOr(&mask[pos], 1u << p);
+      }
+      if (c == 64) {  // a payload denser than one window per tile: its further windows now
+        for (int32_t q0 = cs[j] + 64;; q0 += 64) {
+          const int32_t q = q0 + lane;
+          const int32_t iv = q < sk[j] ? as_global(sidx[j])[q] : INT32_MAX;
+          const int cc = fw_lead(iv < thi32);
+          const uint32_t pos = (uint32_t)(iv - tlo32);
+          if (lane < cc && pos < (uint32_t)TE) atomicOr(&mask[pos], 1u << p);
+          c += cc;
+          if (cc < 64) break;
+        }
+      }
+      cs[j] = cs[j] + c;
+    }
+#pragma unroll
+    for (int j = 0; j < FM_SLOTS; ++j) load_window(j, cs[j], wn[j], wvn[j]);
+    fm_load<EPT>(a.local, tlo + TE, n, t, Ln);  // clamped past the end
+    // the base: every element's fold of its local value alone (the no-hit value)
+    float base[EPT];
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const float xv = L[e];
+      if (abl & 8) {
+        base[e] = xv;
+        continue;
+      }
+      const float tb = a.zero_base ? 0.0f : xv;
+      float acc;
+      if (EQW) {
+        const float term = tb * w0;
+        acc = a.zero_base ? 0.0f + term : term;
+        for (int p = 1; p < np; ++p) acc = acc + term;
+      } else {
+        acc = 0.0f;
+#pragma unroll
+        for (int p = 0; p < FOLD_MAXP; ++p) {
+          if (p >= np) break;
+          const float term = tb * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl), p));
+          acc = p == 0 ? (a.zero_base ? 0.0f + term : term) : acc + term;
+        }
+      }
+      if (a.add_self) acc = acc + xv * a.w_self;
+      base[e] = acc;
+    }
+    __syncthreads();  // B1: the tile's mask is complete; the previous tile is done everywhere
+    // 2. per-element value runs: block scan of the bit counts
+    uint32_t m[EPT];
+#pragma unroll
+    for (int c = 0; c < EPT / 4; ++c) {
+      const uint4 q = *reinterpret_cast<const uint4*>(&mask[fm_elem(t, 4 * c)]);
+      m[4 * c] = q.x; m[4 * c + 1] = q.y; m[4 * c + 2] = q.z; m[4 * c + 3] = q.w;
+      *reinterpret_cast<float4*>(&s_x[fm_elem(t, 4 * c)]) =
+          make_float4(L[4 * c], L[4 * c + 1], L[4 * c + 2], L[4 * c + 3]);
+    }
+    uint32_t mine = 0;
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) mine += (uint32_t)__popc(m[e]);
+    uint32_t total;
+    uint32_t run = 0;
+    total = 0;
+    if (!(abl & 16)) run = block_excl_scan(mine, s_wsum, &total);
+    const bool over = total > (uint32_t)CAP;  // uniform
+#pragma unroll
+    for (int c = 0; c < EPT / 4; ++c) {
+      uint16_t pr[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        pr[e] = (uint16_t)(run < 65535u ? run : 65535u);
+        run += (uint32_t)__popc(m[4 * c + e]);
+      }
+      *reinterpret_cast<uint2*>(&s_pre[fm_elem(t, 4 * c)]) =
+          make_uint2((uint32_t)pr[0] | ((uint32_t)pr[1] << 16), (uint32_t)pr[2] | ((uint32_t)pr[3] << 16));
+    }
+    __syncthreads();  // B3: runs and local values staged
+    float outv[EPT];
+    if (!over) {
+      // 3. values into their slots; each hit element's lowest payload lists it
+#pragma unroll
+      for (int j = 0; j < FM_SLOTS; ++j) {
+        if (j >= nsl || (abl & 2)) continue;
+        const int p = wid + FM_WAVES * j;
+        const uint32_t below = (1u << p) - 1u;
+        auto place = [&](int32_t iv, float vv, bool in) {
+          const uint32_t pos = (uint32_t)(iv - tlo32);
+          if (in && pos < (uint32_t)TE) {
+            const uint32_t mm = mask[pos];
+            const uint32_t r = (uint32_t)__popc(mm & below);
+            const uint32_t slot = (uint32_t)s_pre[pos] + r;
+            if (slot < (uint32_t)CAP) s_val[slot] = vv;
+            if (r == 0u) {  // (a list past TE only with duplicate indices: invalid payloads)
+              const uint32_t li = atomicAdd(&s_nown, 1u);
+              if (li < (uint32_t)TE) s_list[li] = (uint16_t)pos;
+            }
+          }
+        };
+        place(wi[j], wv[j], lane < cfirst[j]);
+        if (cfirst[j] == 64) {
+          for (int32_t q0 = c0[j] + 64;; q0 += 64) {
+            const int32_t q = q0 + lane;
+            const bool ok = q < sk[j];
+            const int32_t iv = ok ? as_global(sidx[j])[q] : INT32_MAX;
+            const float vv = as_global(sval[j])[ok ? q : 0];
+            const int cc = fw_lead(iv < thi32);
+            place(iv, vv, lane < cc);
+            if (cc < 64) break;
+          }
+        }
+      }
+      __syncthreads();  // B4: values and the hit list complete
+      // 4. every hit element folded exactly (reference order), its result over its local value
+      const uint32_t nown = (abl & 1) ? 0u : (s_nown < (uint32_t)TE ? s_nown : (uint32_t)TE);
+      for (uint32_t i = (uint32_t)t; i < nown; i += FM_THREADS) {
+        const uint32_t pos = s_list[i];
+        const uint32_t mm = mask[pos];
+        const uint32_t sl = s_pre[pos];
+        const float xv = s_x[pos];
+        const float tb = a.zero_base ? 0.0f : xv;
+        // every payload's slot read unconditionally (independent LDS reads in flight together;
+        // a read under the bit test would be one dependent round trip per payload)
+        float hv[FOLD_MAXP];
+#pragma unroll
+        for (int p = 0; p < FOLD_MAXP; ++p) {
+          const uint32_t slot = sl + (uint32_t)__popc(mm & ((1u << p) - 1u));
+          hv[p] = s_val[slot < (uint32_t)CAP ? slot : 0u];
+        }
+        float acc = 0.0f;
+#pragma unroll
+        for (int p = 0; p < FOLD_MAXP; ++p) {
+          if (p >= np) break;
+          const float tv = ((mm >> p) & 1u) ? hv[p] : tb;
+          const float term = tv * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl), p));
+          acc = p == 0 ? (a.zero_base ? 0.0f + term : term) : acc + term;
+        }
+        if (a.add_self) acc = acc + xv * a.w_self;
+        s_x[pos] = acc;
+      }
+      __syncthreads();  // B5: hit results in place
+      // 5. the base, or the hit result
+#pragma unroll
+      for (int c = 0; c < EPT / 4; ++c) {
+        const float4 q = *reinterpret_cast<const float4*>(&s_x[fm_elem(t, 4 * c)]);
+        const float h[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) outv[4 * c + e] = m[4 * c + e] ? h[e] : base[4 * c + e];
+      }
+    } else {
+      // more entries than value slots: payload by payload, an LDS value tile tagged with p + 1
+      uint16_t* const tag = s_pre;  // (the runs are not used on this path)
+      float* const vt = s_val;
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {
+        outv[e] = 0.0f;
+        tag[fm_elem(t, e)] = 0;
+      }
+      __syncthreads();
+      for (int p = 0; p < np; ++p) {
+        if ((p & (FM_WAVES - 1)) == wid) {
+          const int j = p / FM_WAVES;
+          for (int32_t q0 = c0[j];; q0 += 64) {
+            const int32_t q = q0 + lane;
+            const bool ok = q < sk[j];
+            const int32_t iv = ok ? as_global(sidx[j])[q] : INT32_MAX;
+            const float vv = as_global(sval[j])[ok ? q : 0];
+            const int cc = fw_lead(iv < thi32);
+            const uint32_t pos = (uint32_t)(iv - tlo32);
+            if (lane < cc && pos < (uint32_t)TE) {
+              vt[pos] = vv;
+              tag[pos] = (uint16_t)(p + 1);
+            }
+            if (cc < 64) break;
+          }
+        }
+        __syncthreads();
+        const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl), p));
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) {
+          const int el = fm_elem(t, e);
+          const float tb = a.zero_base ? 0.0f : L[e];
+          const float tv = tag[el] == (uint16_t)(p + 1) ? vt[el] : tb;
+          const float term = tv * w;
+          outv[e] = p == 0 ? (a.zero_base ? 0.0f + term : term) : outv[e] + term;
+        }
+        __syncthreads();
+      }
+      if (a.add_self) {
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) outv[e] = outv[e] + L[e] * a.w_self;
+      }
+    }
+    fm_store<EPT>(a.out, tlo, n, t, outv);
+    if (a.out2) fm_store<EPT>(a.out2, tlo, n, t, outv);
+    // this buffer's mask words back to zero (the next tile uses the other buffer)
+#pragma unroll
+    for (int c = 0; c < EPT / 4; ++c)
+      *reinterpret_cast<uint4*>(&mask[fm_elem(t, 4 * c)]) = make_uint4(0u, 0u, 0u, 0u);
+    if (t == 0) s_nown = 0u;  // read by every thread before B5
+    buf ^= 1u;
+#pragma unroll
+    for (int j = 0; j < FM_SLOTS; ++j) {
+      wi[j] = wn[j];
+      wv[j] = wvn[j];
+    }
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) L[e] = Ln[e];
+  }
+}
+
+// The merge fold's launch: a persistent grid of what the CUs hold, each block a contiguous run.
+template <int EPT, bool EQW>
+static int launch_merge_t(const FoldArgs& fa, hipStream_t st) {
+  static int per = 0, cus = 0;
+  if (per == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per, reinterpret_cast<const void*>(fold_merge_kernel<EPT, EQW>), FM_THREADS, 0) !=
+            hipSuccess || per < 1)
+      per = 1;
+  }
+  constexpr int TE = FmCfg<EPT>::TE;
+  const int64_t ntl = (fa.n + TE - 1) / TE;
+  int64_t blocks = (int64_t)cus * per;
+  if (DPZ_KNOB_INT(MERGE_BLOCKS, 0) > 0) blocks = DPZ_KNOB_INT(MERGE_BLOCKS, 0);
+  if (blocks > ntl) blocks = ntl;
+  if (blocks < 1) blocks = 1;
+  const int64_t tpb = (ntl + blocks - 1) / blocks;
+  blocks = (ntl + tpb - 1) / tpb;
+  // DPZ_MERGE_ABL (diagnostic build, timing only: results then differ) skips phases: 1 the hit
+  // folds, 2 the value placement, 4 the mask bits, 8 the base, 16 the scan
+  const int abl = (int)DPZ_KNOB_INT(MERGE_ABL, 0);
+  DPZ_TIMED(DPZ_KT_FOLD, st, (fold_merge_kernel<EPT, EQW><<<(unsigned)blocks, FM_THREADS, 0, st>>>(fa, tpb, abl)));
+  return DPZ_OK;
+}
+
+static bool merge_ok(const FoldArgs& fa) {
+  if (fa.replace_only || !fa.first || !fa.all_sparse || fa.np < 1 || fa.np > FOLD_MAXP) return false;
+  if (fa.n < 1024 || fa.n >= (int64_t(1) << 31) - 8192) return false;
+  return aligned16(fa.local) && aligned16(fa.out) && (!fa.out2 || aligned16(fa.out2));
+}
+
+// elements per thread by the group's average entries per element (value slots hold 2 per element)
+static int launch_merge(const FoldArgs& fa, double avg_per_elem, hipStream_t st) {
+  bool eqw = true;
+  for (int i = 1; i < fa.np; ++i) eqw = eqw && fa.p[i].w == fa.p[0].w;
+  int ept = (int)DPZ_KNOB_INT(MERGE_EPT, 8);
+  if (ept != 4 && ept != 8 && ept != 16) ept = 8;
+  (void)avg_per_elem;
+  switch (ept) {
+    case 4: return eqw ? launch_merge_t<4, true>(fa, st) : launch_merge_t<4, false>(fa, st);
+    case 16: return eqw ? launch_merge_t<16, true>(fa, st) : launch_merge_t<16, false>(fa, st);
+    default: return eqw ? launch_merge_t<8, true>(fa, st) : launch_merge_t<8, false>(fa, st);
+  }
+}
+
 extern "C" size_t dpz_decode_workspace_bytes(int64_t n, int n_payloads) {
   const int64_t np = n_payloads < FOLD_MAXP ? (n_payloads > 0 ? n_payloads : 1) : FOLD_MAXP;
   return (size_t)np * (size_t)(fold_ntiles(n > 0 ? n : 1) + 1) * sizeof(int32_t);
@@ -2226,6 +2650,15 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
       }
     const int kind = (int)DPZ_KNOB_INT(FOLD_KIND, 0);
     const double avg = fa.np > 0 ? (double)etot / (double)fa.np / (double)n : 0.0;
+    // the merge fold (round 6): not the default until it measures faster than the walk
+    // (DPZ_FOLD_KIND=8 forces it, diagnostic build)
+    bool use_merge = false;
+    if (kind) use_merge = merge_ok(fa) && kind == 8;
+    if (use_merge) {
+      const int rc = launch_merge(fa, (double)etot / (double)n, st);
+      if (rc != DPZ_OK) return rc;
+      continue;
+    }
     bool use_walk = walk_ok(fa) && (fa.np <= 4 || (avg >= 0.0175 && avg <= 0.21));
     if (kind) use_walk = walk_ok(fa) && kind == 4;
     if (use_walk) {

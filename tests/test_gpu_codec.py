@@ -300,7 +300,7 @@ def test_fold_paths_forced(dev, diag_lib, monkeypatch, group, n, alpha, npay):
     np.testing.assert_array_equal(_bits(tout.cpu().numpy()), _bits(ref3))
 
 
-@pytest.mark.parametrize("kind", ["1", "2", "4"])
+@pytest.mark.parametrize("kind", ["1", "2", "4", "8"])
 @pytest.mark.parametrize("n,alpha,npay,ndense", [(1_000_003, 0.01, 16, 0), (1_000_003, 0.1, 16, 0),
                                                  (2_000_001, 0.25, 16, 0), (300_001, 0.3, 3, 1),
                                                  (300_001, 0.1, 3, 3), (100_003, 0.99, 2, 0),
