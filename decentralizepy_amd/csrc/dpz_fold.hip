@@ -2109,29 +2109,28 @@ extern "C" int dpz_debug_fold_stamps(unsigned long long* host_out, int reset) {
 // windows of payloads w, w + 4, w + 8, w + 12 (the next tile's windows and local values are
 // issued one tile ahead, so the stream's loads are in flight while a tile is merged).  Per tile:
 //   1. every payload's entries in the tile (the leading window lanes below the tile's end) set
-//      bit p of their element's word in an LDS mask;
-//   2. each thread counts its elements' bits; a block scan gives every hit element a contiguous
-//      run of value slots, in payload order (the rank of bit p among the element's bits);
-//   3. every entry writes its value to its slot; the entry with the lowest payload number of an
-//      element (its "owner") appends the element to a list;
-//   4. the threads fold the listed (hit) elements exactly: term p = (bit p ? slot value : local)
-//      * w_p in payload order, then the self term (the reference's fp32 order);
-//   5. every element folds its local value alone (base), and takes the listed result where hit.
-// Every element's local value and output are read / written once, every payload entry read once
-// (extra windows of a payload denser than 64 entries per tile are re-read from L2).  A tile whose
-// entries exceed the value slots (adversarial clustering) folds payload by payload instead.
-// Weights all equal (EQW: a regular graph's Metro-Hastings weights): the base is one product and
-// np - 1 additions of it, the same bits as the general order.
+//      bit p of their element's 16-bit word in an LDS mask; meanwhile every element folds its
+//      local value alone (the no-hit base; the elements advance through the terms together);
+//   2. each wave numbers its own elements' bits (a wave scan): every hit element gets a run of
+//      value slots in the wave's region, in payload order (the rank of bit p among its bits);
+//   3. every entry writes its value to its slot;
+//   4. each wave lists its own hit elements (ballots) and its lanes fold them exactly — term p
+//      = (bit p ? slot value : local) * w_p in payload order, then the self term (the
+//      reference's fp32 order) — over the base.
+// Three block barriers per tile.  Every element's local value and output are read / written
+// once, every payload entry read once (extra windows of a payload denser than 64 entries per
+// tile are re-read from L2).  A tile whose entries exceed a wave's value slots (1 per element;
+// adversarial clustering) folds payload by payload instead.  Weights all equal (EQW: a regular
+// graph's Metro-Hastings weights): the base is one product and np - 1 additions of it, the same
+// bits as the general order.
 constexpr int FM_THREADS = 256;
 constexpr int FM_WAVES = FM_THREADS / 64;
 constexpr int FM_SLOTS = FOLD_MAXP / FM_WAVES;  // payload slots per wave: payload wid + 4 j
 
 template <int EPT>
 struct FmCfg {
-  static constexpr int TE = FM_THREADS * EPT;  // elements per tile
-  static constexpr int CAP = 2 * TE;           // value slots per tile
-  static constexpr int CH = EPT / 4;           // float4 chunks per thread
-  static_assert(EPT % 4 == 0 && CAP <= 65535, "float4 chunks, u16 slot offsets");
+  static constexpr int TE = FM_THREADS * EPT;  // elements per tile (= value slots per tile)
+  static_assert(EPT % 4 == 0 && TE <= 65535, "float4 chunks, u16 slot offsets");
 };
 
 // element e of thread t (chunk e / 4 at (e / 4) * 4 * FM_THREADS + 4 t + e % 4: float4-coalesced)
@@ -2185,16 +2184,17 @@ __device__ __forceinline__ void fm_store(float* __restrict__ p, int64_t tlo, int
 }
 
 template <int EPT, bool EQW>
-__global__ void __launch_bounds__(FM_THREADS) fold_merge_kernel(FoldArgs a, int64_t tpb, int abl) {
+__global__ void __launch_bounds__(FM_THREADS) __attribute__((amdgpu_waves_per_eu(EPT <= 8 ? 4 : 2, 8))) fold_merge_kernel(FoldArgs a, int64_t tpb, int abl) {
   using C = FmCfg<EPT>;
-  constexpr int TE = C::TE, CAP = C::CAP;
-  __shared__ __attribute__((aligned(16))) uint32_t s_mask[2][TE];
+  constexpr int TE = C::TE;
+  constexpr int WE = 64 * EPT;     // elements of one wave (its value slots: WE, 1 per element)
+  // element e's payload bits: the 16-bit half (e & 1) of word e / 2 (np <= 16)
+  __shared__ __attribute__((aligned(16))) uint32_t s_mask[2][TE / 2];
   __shared__ __attribute__((aligned(16))) uint16_t s_pre[TE];
   __shared__ __attribute__((aligned(16))) float s_x[TE];
-  __shared__ float s_val[CAP];
+  __shared__ float s_val[TE];
   __shared__ uint16_t s_list[TE];
-  __shared__ uint32_t s_wsum[16];
-  __shared__ uint32_t s_nown;
+  __shared__ uint32_t s_over[2];
   const int t = threadIdx.x, lane = t & 63;
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
   const int64_t n = a.n;
@@ -2215,6 +2215,7 @@ __global__ void __launch_bounds__(FM_THREADS) fold_merge_kernel(FoldArgs a, int6
     const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), p);
     return ((uint64_t)hi << 32) | lo;
   };
+  auto W = [&](int p) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl), p)); };
   const int32_t* sidx[FM_SLOTS];
   const float* sval[FM_SLOTS];
   int32_t sk[FM_SLOTS];
@@ -2227,8 +2228,8 @@ __global__ void __launch_bounds__(FM_THREADS) fold_merge_kernel(FoldArgs a, int6
     sk[j] = live ? fw_uni(__builtin_amdgcn_readlane(kl, p)) : 0;
   }
   const int nsl = np > wid ? (np - wid + FM_WAVES - 1) / FM_WAVES : 0;  // this wave's live slots
-  for (int i = t; i < 2 * TE; i += FM_THREADS) (&s_mask[0][0])[i] = 0u;
-  if (t == 0) s_nown = 0u;
+  for (int i = t; i < TE; i += FM_THREADS) (&s_mask[0][0])[i] = 0u;
+  if (t < 2) s_over[t] = 0u;
   // start cursors: lower_bound(idx_p, t0 * TE) of this wave's payloads (lane j: slot j)
   const int32_t curv = fw_start_cursors<FM_SLOTS, false>(
       nsl, (int32_t)(t0 * TE), lane, [&](int j) { return sidx[j]; }, [&](int j) { return sk[j]; },
@@ -2250,8 +2251,9 @@ __global__ void __launch_bounds__(FM_THREADS) fold_merge_kernel(FoldArgs a, int6
   for (int j = 0; j < FM_SLOTS; ++j) load_window(j, cs[j], wi[j], wv[j]);
   float L[EPT], Ln[EPT];
   fm_load<EPT>(a.local, t0 * TE, n, t, L);
-  const float w0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl), 0));
+  const float w0 = W(0);
   uint32_t buf = 0;
+  const int zb = a.zero_base;
   __syncthreads();  // masks zeroed
   for (int64_t tile = t0; tile < t1; ++tile) {
     const int64_t tlo = tile * TE;
@@ -2270,7 +2272,7 @@ __global__ void __launch_bounds__(FM_THREADS) fold_merge_kernel(FoldArgs a, int6
       cfirst[j] = c;
       if (!(abl & 4)) {
         const uint32_t pos = (uint32_t)(wi[j] - tlo32);
-        if (lane < c && pos < (uint32_t)TE) atomicOr(&mask[pos], 1u << p);
+        if (lane < c && pos < (uint32_t)TE) atomicOr(&mask[pos >> 1], 1u << (p + 16 * (pos & 1u)));
       }
       if (c == 64) {  // a payload denser than one window per tile: its further windows now
         for (int32_t q0 = cs[j] + 64;; q0 += 64) {
@@ -2278,7 +2280,7 @@ __global__ void __launch_bounds__(FM_THREADS) fold_merge_kernel(FoldArgs a, int6
           const int32_t iv = q < sk[j] ? as_global(sidx[j])[q] : INT32_MAX;
           const int cc = fw_lead(iv < thi32);
           const uint32_t pos = (uint32_t)(iv - tlo32);
-          if (lane < cc && pos < (uint32_t)TE) atomicOr(&mask[pos], 1u << p);
+          if (lane < cc && pos < (uint32_t)TE) atomicOr(&mask[pos >> 1], 1u << (p + 16 * (pos & 1u)));
           c += cc;
           if (cc < 64) break;
         }
@@ -2288,141 +2290,183 @@ __global__ void __launch_bounds__(FM_THREADS) fold_merge_kernel(FoldArgs a, int6
 #pragma unroll
     for (int j = 0; j < FM_SLOTS; ++j) load_window(j, cs[j], wn[j], wvn[j]);
     fm_load<EPT>(a.local, tlo + TE, n, t, Ln);  // clamped past the end
-    // the base: every element's fold of its local value alone (the no-hit value)
+    // the base: every element's fold of its local value alone (the no-hit value); the elements
+    // advance through the terms together (independent adds, one loop for all), while other
+    // waves still set mask bits
     float base[EPT];
+    if (abl & 8) {
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) {
-      const float xv = L[e];
-      if (abl & 8) {
-        base[e] = xv;
-        continue;
+      for (int e = 0; e < EPT; ++e) base[e] = L[e];
+    } else {
+      float tw[EPT];
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {
+        tw[e] = (zb ? 0.0f : L[e]) * w0;
+        base[e] = zb ? 0.0f + tw[e] : tw[e];
       }
-      const float tb = a.zero_base ? 0.0f : xv;
-      float acc;
-      if (EQW) {
-        const float term = tb * w0;
-        acc = a.zero_base ? 0.0f + term : term;
-        for (int p = 1; p < np; ++p) acc = acc + term;
-      } else {
-        acc = 0.0f;
+      for (int p = 1; p < np; ++p) {
+        if (EQW) {
 #pragma unroll
-        for (int p = 0; p < FOLD_MAXP; ++p) {
-          if (p >= np) break;
-          const float term = tb * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl), p));
-          acc = p == 0 ? (a.zero_base ? 0.0f + term : term) : acc + term;
+          for (int e = 0; e < EPT; ++e) base[e] = base[e] + tw[e];
+        } else {
+          const float w = W(p);
+#pragma unroll
+          for (int e = 0; e < EPT; ++e) base[e] = base[e] + (zb ? 0.0f : L[e]) * w;
         }
       }
-      if (a.add_self) acc = acc + xv * a.w_self;
-      base[e] = acc;
+      if (a.add_self) {
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) base[e] = base[e] + L[e] * a.w_self;
+      }
     }
     __syncthreads();  // B1: the tile's mask is complete; the previous tile is done everywhere
-    // 2. per-element value runs: block scan of the bit counts
+    // 2. per-element value runs: each wave numbers its own elements' entries (slots of the
+    // wave's region, in payload order per element); the local values staged for the hit folds
     uint32_t m[EPT];
 #pragma unroll
     for (int c = 0; c < EPT / 4; ++c) {
-      const uint4 q = *reinterpret_cast<const uint4*>(&mask[fm_elem(t, 4 * c)]);
-      m[4 * c] = q.x; m[4 * c + 1] = q.y; m[4 * c + 2] = q.z; m[4 * c + 3] = q.w;
+      const uint2 q = *reinterpret_cast<const uint2*>(&mask[fm_elem(t, 4 * c) >> 1]);
+      m[4 * c] = q.x & 0xFFFFu; m[4 * c + 1] = q.x >> 16;
+      m[4 * c + 2] = q.y & 0xFFFFu; m[4 * c + 3] = q.y >> 16;
       *reinterpret_cast<float4*>(&s_x[fm_elem(t, 4 * c)]) =
           make_float4(L[4 * c], L[4 * c + 1], L[4 * c + 2], L[4 * c + 3]);
     }
     uint32_t mine = 0;
 #pragma unroll
     for (int e = 0; e < EPT; ++e) mine += (uint32_t)__popc(m[e]);
-    uint32_t total;
-    uint32_t run = 0;
-    total = 0;
-    if (!(abl & 16)) run = block_excl_scan(mine, s_wsum, &total);
-    const bool over = total > (uint32_t)CAP;  // uniform
+    uint32_t wtot = 0;
+    uint32_t run = (abl & 16) ? 0u : wave_excl_scan(mine, &wtot) + (uint32_t)(wid * WE);
+    if (wtot > (uint32_t)WE && lane == 0) s_over[buf] = 1u;  // (uniform read after B3)
 #pragma unroll
     for (int c = 0; c < EPT / 4; ++c) {
-      uint16_t pr[4];
+      uint32_t pr[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        pr[e] = (uint16_t)(run < 65535u ? run : 65535u);
+        pr[e] = run < 65535u ? run : 65535u;
         run += (uint32_t)__popc(m[4 * c + e]);
       }
       *reinterpret_cast<uint2*>(&s_pre[fm_elem(t, 4 * c)]) =
-          make_uint2((uint32_t)pr[0] | ((uint32_t)pr[1] << 16), (uint32_t)pr[2] | ((uint32_t)pr[3] << 16));
+          make_uint2(pr[0] | (pr[1] << 16), pr[2] | (pr[3] << 16));
     }
-    __syncthreads();  // B3: runs and local values staged
-    float outv[EPT];
+    __syncthreads();  // B3: every element's slot run known
+    const bool over = s_over[buf] != 0u;  // uniform
     if (!over) {
-      // 3. values into their slots; each hit element's lowest payload lists it
+      // 3. values into their slots (slot = the run start + the rank of bit p among the bits)
+      if (!(abl & 2)) {
 #pragma unroll
-      for (int j = 0; j < FM_SLOTS; ++j) {
-        if (j >= nsl || (abl & 2)) continue;
-        const int p = wid + FM_WAVES * j;
-        const uint32_t below = (1u << p) - 1u;
-        auto place = [&](int32_t iv, float vv, bool in) {
-          const uint32_t pos = (uint32_t)(iv - tlo32);
-          if (in && pos < (uint32_t)TE) {
-            const uint32_t mm = mask[pos];
-            const uint32_t r = (uint32_t)__popc(mm & below);
-            const uint32_t slot = (uint32_t)s_pre[pos] + r;
-            if (slot < (uint32_t)CAP) s_val[slot] = vv;
-            if (r == 0u) {  // (a list past TE only with duplicate indices: invalid payloads)
-              const uint32_t li = atomicAdd(&s_nown, 1u);
-              if (li < (uint32_t)TE) s_list[li] = (uint16_t)pos;
+        for (int j = 0; j < FM_SLOTS; ++j) {
+          if (j >= nsl) continue;
+          const int p = wid + FM_WAVES * j;
+          const uint32_t below = (1u << p) - 1u;
+          auto place = [&](int32_t iv, float vv, bool in) {
+            const uint32_t pos = (uint32_t)(iv - tlo32);
+            if (in && pos < (uint32_t)TE) {
+              const uint32_t mm = (mask[pos >> 1] >> (16 * (pos & 1u))) & 0xFFFFu;
+              const uint32_t slot = (uint32_t)s_pre[pos] + (uint32_t)__popc(mm & below);
+              if (slot < (uint32_t)TE) s_val[slot] = vv;
+            }
+          };
+          place(wi[j], wv[j], lane < cfirst[j]);
+          if (cfirst[j] == 64) {
+            for (int32_t q0 = c0[j] + 64;; q0 += 64) {
+              const int32_t q = q0 + lane;
+              const bool ok = q < sk[j];
+              const int32_t iv = ok ? as_global(sidx[j])[q] : INT32_MAX;
+              const float vv = as_global(sval[j])[ok ? q : 0];
+              const int cc = fw_lead(iv < thi32);
+              place(iv, vv, lane < cc);
+              if (cc < 64) break;
             }
           }
-        };
-        place(wi[j], wv[j], lane < cfirst[j]);
-        if (cfirst[j] == 64) {
-          for (int32_t q0 = c0[j] + 64;; q0 += 64) {
-            const int32_t q = q0 + lane;
-            const bool ok = q < sk[j];
-            const int32_t iv = ok ? as_global(sidx[j])[q] : INT32_MAX;
-            const float vv = as_global(sval[j])[ok ? q : 0];
-            const int cc = fw_lead(iv < thi32);
-            place(iv, vv, lane < cc);
-            if (cc < 64) break;
+        }
+      }
+      __syncthreads();  // B4: every value in its slot
+      // 4. the wave's own hit elements, listed (ballot order) and folded exactly by its lanes
+      // (reference order: the payload terms, then the self term); results over the staged
+      // local values, then over the base
+      if (!(abl & 1)) {
+        uint16_t* const wl_ = s_list + wid * WE;
+        uint32_t nh = 0;
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) {
+          const uint64_t b = __ballot(m[e] != 0u);
+          if (m[e])
+            wl_[nh + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] =
+                (uint16_t)fm_elem(t, e);
+          nh += (uint32_t)__popcll(b);
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i = (uint32_t)lane; i < nh; i += 64) {
+          const uint32_t pos = wl_[i];
+          const uint32_t mm = (mask[pos >> 1] >> (16 * (pos & 1u))) & 0xFFFFu;
+          const uint32_t sl = s_pre[pos];
+          const float xv = s_x[pos];
+          const float tb = zb ? 0.0f : xv;
+          const int p0 = __ffs((int)mm) - 1;
+          const uint32_t mm1 = mm & (mm - 1u);
+          const int p1 = mm1 ? __ffs((int)mm1) - 1 : 32;
+          const uint32_t mm2 = mm1 & (mm1 - 1u);
+          const int p2 = mm2 ? __ffs((int)mm2) - 1 : 32;
+          float acc;
+          if (abl & 32) {  // (timing ablation: the chain skipped, its loads kept)
+            acc = s_val[sl < (uint32_t)TE ? sl : 0u] + tb + (float)p0 + (float)p1 + (float)p2;
+          } else if ((mm2 & (mm2 - 1u)) == 0u) {  // one to three payloads hit it (all but ~1e-4)
+            const float v0 = s_val[sl < (uint32_t)TE ? sl : 0u];
+            const float v1 = s_val[sl + 1u < (uint32_t)TE ? sl + 1u : 0u];
+            const float v2 = s_val[sl + 2u < (uint32_t)TE ? sl + 2u : 0u];
+            acc = 0.0f;
+            if (EQW) {  // every product once (equal weights: the same bits as w_p each term)
+              const float xw = tb * w0, v0w = v0 * w0, v1w = v1 * w0, v2w = v2 * w0;
+#pragma unroll
+              for (int p = 0; p < FOLD_MAXP; ++p) {
+                if (p >= np) break;
+                const float term = p == p0 ? v0w : (p == p1 ? v1w : (p == p2 ? v2w : xw));
+                acc = p == 0 ? (zb ? 0.0f + term : term) : acc + term;
+              }
+            } else {
+#pragma unroll
+              for (int p = 0; p < FOLD_MAXP; ++p) {
+                if (p >= np) break;
+                const float tv = p == p0 ? v0 : (p == p1 ? v1 : (p == p2 ? v2 : tb));
+                const float term = tv * W(p);
+                acc = p == 0 ? (zb ? 0.0f + term : term) : acc + term;
+              }
+            }
+          } else {  // four or more (adversarial overlap): payload by payload from the slots
+            uint32_t s2 = sl;
+            acc = 0.0f;
+            for (int p = 0; p < np; ++p) {
+              float tv = tb;
+              if ((mm >> p) & 1u) {
+                tv = s_val[s2 < (uint32_t)TE ? s2 : 0u];
+                ++s2;
+              }
+              const float term = tv * W(p);
+              acc = p == 0 ? (zb ? 0.0f + term : term) : acc + term;
+            }
           }
+          if (a.add_self) acc = acc + xv * a.w_self;
+          s_x[pos] = acc;
         }
-      }
-      __syncthreads();  // B4: values and the hit list complete
-      // 4. every hit element folded exactly (reference order), its result over its local value
-      const uint32_t nown = (abl & 1) ? 0u : (s_nown < (uint32_t)TE ? s_nown : (uint32_t)TE);
-      for (uint32_t i = (uint32_t)t; i < nown; i += FM_THREADS) {
-        const uint32_t pos = s_list[i];
-        const uint32_t mm = mask[pos];
-        const uint32_t sl = s_pre[pos];
-        const float xv = s_x[pos];
-        const float tb = a.zero_base ? 0.0f : xv;
-        // every payload's slot read unconditionally (independent LDS reads in flight together;
-        // a read under the bit test would be one dependent round trip per payload)
-        float hv[FOLD_MAXP];
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int p = 0; p < FOLD_MAXP; ++p) {
-          const uint32_t slot = sl + (uint32_t)__popc(mm & ((1u << p) - 1u));
-          hv[p] = s_val[slot < (uint32_t)CAP ? slot : 0u];
+        for (int c = 0; c < EPT / 4; ++c) {
+          const float4 q = *reinterpret_cast<const float4*>(&s_x[fm_elem(t, 4 * c)]);
+          const float h[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (m[4 * c + e]) base[4 * c + e] = h[e];
         }
-        float acc = 0.0f;
-#pragma unroll
-        for (int p = 0; p < FOLD_MAXP; ++p) {
-          if (p >= np) break;
-          const float tv = ((mm >> p) & 1u) ? hv[p] : tb;
-          const float term = tv * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl), p));
-          acc = p == 0 ? (a.zero_base ? 0.0f + term : term) : acc + term;
-        }
-        if (a.add_self) acc = acc + xv * a.w_self;
-        s_x[pos] = acc;
-      }
-      __syncthreads();  // B5: hit results in place
-      // 5. the base, or the hit result
-#pragma unroll
-      for (int c = 0; c < EPT / 4; ++c) {
-        const float4 q = *reinterpret_cast<const float4*>(&s_x[fm_elem(t, 4 * c)]);
-        const float h[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) outv[4 * c + e] = m[4 * c + e] ? h[e] : base[4 * c + e];
       }
     } else {
-      // more entries than value slots: payload by payload, an LDS value tile tagged with p + 1
+      // more entries than a wave's value slots: payload by payload, an LDS value tile tagged
+      // with p + 1 (adversarially clustered payloads)
       uint16_t* const tag = s_pre;  // (the runs are not used on this path)
       float* const vt = s_val;
 #pragma unroll
       for (int e = 0; e < EPT; ++e) {
-        outv[e] = 0.0f;
+        base[e] = 0.0f;
         tag[fm_elem(t, e)] = 0;
       }
       __syncthreads();
@@ -2444,29 +2488,29 @@ __global__ void __launch_bounds__(FM_THREADS) fold_merge_kernel(FoldArgs a, int6
           }
         }
         __syncthreads();
-        const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl), p));
+        const float w = W(p);
 #pragma unroll
         for (int e = 0; e < EPT; ++e) {
           const int el = fm_elem(t, e);
-          const float tb = a.zero_base ? 0.0f : L[e];
+          const float tb = zb ? 0.0f : L[e];
           const float tv = tag[el] == (uint16_t)(p + 1) ? vt[el] : tb;
           const float term = tv * w;
-          outv[e] = p == 0 ? (a.zero_base ? 0.0f + term : term) : outv[e] + term;
+          base[e] = p == 0 ? (zb ? 0.0f + term : term) : base[e] + term;
         }
         __syncthreads();
       }
       if (a.add_self) {
 #pragma unroll
-        for (int e = 0; e < EPT; ++e) outv[e] = outv[e] + L[e] * a.w_self;
+        for (int e = 0; e < EPT; ++e) base[e] = base[e] + L[e] * a.w_self;
       }
     }
-    fm_store<EPT>(a.out, tlo, n, t, outv);
-    if (a.out2) fm_store<EPT>(a.out2, tlo, n, t, outv);
-    // this buffer's mask words back to zero (the next tile uses the other buffer)
+    fm_store<EPT>(a.out, tlo, n, t, base);
+    if (a.out2) fm_store<EPT>(a.out2, tlo, n, t, base);
+    // this buffer's mask words and overflow flag back to zero (the next tile uses the other pair)
 #pragma unroll
     for (int c = 0; c < EPT / 4; ++c)
-      *reinterpret_cast<uint4*>(&mask[fm_elem(t, 4 * c)]) = make_uint4(0u, 0u, 0u, 0u);
-    if (t == 0) s_nown = 0u;  // read by every thread before B5
+      *reinterpret_cast<uint2*>(&mask[fm_elem(t, 4 * c) >> 1]) = make_uint2(0u, 0u);
+    if (t == 0) s_over[buf] = 0u;
     buf ^= 1u;
 #pragma unroll
     for (int j = 0; j < FM_SLOTS; ++j) {
@@ -2650,9 +2694,11 @@ extern "C" int dpz_decode_average(const float* local, int64_t n, int n_payloads,
       }
     const int kind = (int)DPZ_KNOB_INT(FOLD_KIND, 0);
     const double avg = fa.np > 0 ? (double)etot / (double)fa.np / (double)n : 0.0;
-    // the merge fold (round 6): not the default until it measures faster than the walk
-    // (DPZ_FOLD_KIND=8 forces it, diagnostic build)
-    bool use_merge = false;
+    // the merge fold (round 6) for larger groups at sparse alpha, where it measured faster than
+    // the walk on MI355X (M = 25 M, tools/diag/merge_time.py, profiles/r06_merge_time.jsonl:
+    // 16 x 0.005 88 vs 125 us, 16 x 0.01 105 vs 126, 16 x 0.02 129 vs 133, 8 x 0.01 69 vs 79;
+    // 16 x 0.03 173 vs 132, 3 x 0.01 at 64 MiB 41 vs 33: the walk); DPZ_FOLD_KIND=8 forces it
+    bool use_merge = merge_ok(fa) && fa.np >= 6 && (double)etot <= 0.33 * (double)n;
     if (kind) use_merge = merge_ok(fa) && kind == 8;
     if (use_merge) {
       const int rc = launch_merge(fa, (double)etot / (double)n, st);

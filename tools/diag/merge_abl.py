@@ -25,8 +25,8 @@ def main():
         w = [1 / (npay + 1)] * npay
         ws = codec.Workspace(dev)
         res = {}
-        for ept in ("4", "8"):
-            for abl in ("0", "1", "3", "7", "15", "31"):
+        for ept in ("8",):
+            for abl in ("0", "32", "1", "3", "7", "15", "31"):
                 os.environ["DPZ_MERGE_ABL"] = abl
                 os.environ["DPZ_MERGE_EPT"] = ept
                 for i in range(4):

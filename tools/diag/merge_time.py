@@ -14,9 +14,10 @@ from decentralizepy_amd import codec  # noqa: E402
 
 def main():
     dev = torch.device("cuda:0")
-    cases = [(25_000_009, 0.01, 16), (25_000_009, 0.02, 16), (25_000_009, 0.05, 16),
-             (25_000_009, 0.1, 16), (16_777_216, 0.01, 3), (11_000_000, 0.01, 4)]
-    kinds = [("8", "4"), ("8", "8"), ("8", "16"), ("4", "8"), ("1", "8")]
+    cases = [(25_000_009, 0.005, 16), (25_000_009, 0.01, 16), (25_000_009, 0.02, 16),
+             (25_000_009, 0.03, 16), (25_000_009, 0.05, 16), (25_000_009, 0.01, 8),
+             (25_000_009, 0.01, 5), (11_000_000, 0.01, 16), (16_777_216, 0.01, 3)]
+    kinds = [("8", "8"), ("4", "8"), ("1", "8")]
     for m, alpha, npay in cases:
         k = round(alpha * m)
         g = torch.Generator(device=dev).manual_seed(1)
