@@ -151,6 +151,8 @@ SIGNATURES = {
                                 _c_void_p, _size, _c_void_p]),
     "dpz_elias_decode": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _i64,
                                 ctypes.POINTER(_i64), _c_void_p, _size, _c_void_p]),
+    "dpz_elias_decode_async": (_int, [_c_void_p, _i64, _i64, _i64, _c_void_p, _c_void_p, _i64,
+                                      _c_void_p, _c_void_p, _size, _c_void_p]),
     "dpz_fpz_max_bytes": (_i64, [_i64]),
     "dpz_fpz_workspace_bytes": (_size, [_i64]),
     "dpz_fpz_encode": (_int, [_c_void_p, _i64, _int, _c_void_p, _i64, ctypes.POINTER(_i64),

@@ -19,7 +19,7 @@ __all__ = ["DPZ_ACC_NONE", "DPZ_ACC_ACCUMULATE", "DPZ_ACC_ADD", "DPZ_EW_SUB", "D
            "DPZ_EW_CHOCO", "Workspace", "topk_encode",
            "topk_threshold", "mask_below_threshold", "elementwise",
            "topk_complete", "decode_average", "replace", "wavedec_len", "wavedec", "waverec",
-           "pack_fp16", "unpack_fp16", "elias_encode", "elias_decode",
+           "pack_fp16", "unpack_fp16", "elias_encode", "elias_decode", "elias_decode_async",
            "KernelTimer", "NodeStepBatch", "topk_sticky_status", "rfft", "irfft", "cplx_key",
            "cplx_gather", "cplx_pair_indices", "lz4_compress", "lz4_decompress", "lz4_frame_info",
            "delta_i32", "running_sum_i32", "mask_words", "topk_encode_sliced", "counter_unslice",
@@ -763,6 +763,34 @@ def elias_decode(buf, nbytes, nbits, first, count, dtype=torch.int64, workspace=
     return out[:n.value]
 
 
+def elias_decode_async(buf, nbytes, nbits, first, count, status, dtype=torch.int32,
+                       workspace=None):
+    """``elias_decode`` with no host synchronisation: the caller knows the value count (the
+    payload's other leg) and passes a device int32 status word, OR-ed nonzero on the stream when
+    the stream is malformed or holds a different count (the values are then unspecified).  Read
+    the status once, after the round's folds (PartialModel.decompress_data's device path)."""
+    _require(buf, torch.uint8, "buf")
+    _require(status, torch.int32, "status")
+    if buf.numel() < ((nbytes + 3) // 4) * 4 + 16:
+        raise ValueError("buf must be padded to round_up(nbytes, 4) + 16 bytes")
+    if count < 1:
+        raise ValueError("count must be >= 1")
+    if dtype not in (torch.int64, torch.int32):
+        raise ValueError("dtype must be torch.int64 or torch.int32")
+    out = torch.empty(count, dtype=dtype, device=buf.device)
+    workspace = workspace or Workspace(buf.device)
+    ws = workspace.get_elias(2, nbytes)
+    o64 = out if dtype == torch.int64 else None
+    o32 = out if dtype == torch.int32 else None
+    rc = _lib.lib().dpz_elias_decode_async(_ptr(buf), nbytes, nbits, first, _ptr(o64), _ptr(o32),
+                                           count, _ptr(status), _ptr(ws), ws.numel(),
+                                           _stream(buf.device))
+    if rc == _lib.DPZ_ERR_ARG:
+        raise ValueError("malformed Elias stream")
+    check(rc, "dpz_elias_decode_async")
+    return out
+
+
 def fpz_encode(x, precision=0, out=None, workspace=None):
     """Block-floating stream of a device fp32 vector (csrc/dpz_fpz.hip; the float leg of
     compression/EliasFpzip.py:19-51 at precision 0 and EliasFpzipLossy.py:14-58 at precision p).
@@ -786,17 +814,22 @@ def fpz_encode(x, precision=0, out=None, workspace=None):
     return out[:nbytes.value]
 
 
-def fpz_decode(buf, n, precision, out=None, check_status=True):
+def fpz_decode(buf, n, precision, out=None, check_status=True, status=None):
     """Values of a block-floating stream held on the device (a uint8 tensor of the whole stream,
     4-byte aligned); ``n`` and ``precision`` come from its header.  With ``check_status`` the
-    call synchronises and raises ValueError on a malformed stream."""
+    call synchronises and raises ValueError on a malformed stream; a caller's ``status`` (device
+    int32 word) is OR-ed instead, with no synchronisation."""
     _require(buf, torch.uint8, "buf")
     if out is None:
         out = torch.empty(max(n, 1), dtype=torch.float32, device=buf.device)
     _require(out, torch.float32, "out")
     if out.numel() < n:
         raise ValueError("out holds fewer than n values")
-    status = torch.zeros(1, dtype=torch.int32, device=buf.device)
+    if status is None:
+        status = torch.zeros(1, dtype=torch.int32, device=buf.device)
+    else:
+        _require(status, torch.int32, "status")
+        check_status = False
     rc = _lib.lib().dpz_fpz_decode(_ptr(buf), buf.numel(), n, int(precision), _ptr(out),
                                    _ptr(status), _stream(buf.device))
     if rc == _lib.DPZ_ERR_ARG:

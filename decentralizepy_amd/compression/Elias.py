@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from .. import codec
-from .._device import host_copy_into, host_owned, pick_device
+from .._device import PayloadNames, Staging, host_copy_into, host_owned, pick_device
 from .Compression import Compression
 
 
@@ -37,12 +37,41 @@ def _grown(ws, name, n, kw):
     return buf
 
 
+def stage_up(comp, b, need, device):
+    """Host stream bytes ``b`` -> a fresh device uint8 buffer of ``need`` bytes (zero padded),
+    through a ring of pinned buffers kept with the compressor ``comp``: the DMA is asynchronous and
+    a pinned slot is reused only after its own earlier DMA has completed, so the host copy of the
+    next payload's stream overlaps this one's DMA and decode.  The device buffer comes from torch's
+    caching allocator: freed, it is reused only by later work on the same stream."""
+    if comp._staging is None:
+        comp._staging = Staging()
+        comp._names = PayloadNames(slots=4)
+    name = comp._names("stream")
+    pin = comp._staging.get(name, need, torch.uint8)
+    if pin is None:  # over the pinned cap: a pageable copy
+        pad = np.zeros(need, dtype=np.uint8)
+        pad[:b.size] = b
+        return torch.from_numpy(pad).to(device)
+    host_copy_into(pin[:b.size], b)
+    pin[b.size:need].zero_()
+    dbuf = torch.empty(need, dtype=torch.uint8, device=device)
+    dbuf.copy_(pin, non_blocking=True)
+    comp._staging.mark(name, torch.uint8, torch.cuda.current_stream(device))
+    return dbuf
+
+
 class Elias(Compression):
     """Elias-gamma coding of sorted index gaps."""
+
+    # decompress_device takes (count, status): the asynchronous receive path of
+    # PartialModel.decompress_data
+    async_decode = True
 
     def __init__(self, *args, **kwargs):
         self.device = None
         self._ws = None
+        self._staging = None
+        self._names = None
 
     # ---- device ----------------------------------------------------------------------------------
     def _dev(self, device=None):
@@ -64,13 +93,20 @@ class Elias(Compression):
         torch.cuda.current_stream(enc.device).synchronize()
         return host_owned(pin)
 
-    def decompress_device(self, buf, dtype=torch.int32, device=None):
-        """Host stream -> device index tensor (int32 for the fold kernels, or int64)."""
+    def decompress_device(self, buf, dtype=torch.int32, device=None, count=None, status=None):
+        """Host stream -> device index tensor (int32 for the fold kernels, or int64).  With
+        ``count`` (the payload's value count) and ``status`` (a device int32 word) the decode is
+        asynchronous: no host synchronisation, the status word OR-ed nonzero when the stream is
+        malformed or does not hold ``count`` values (``codec.elias_decode_async``)."""
         dev = self._dev(device)
         b = np.frombuffer(memoryview(buf), dtype=np.uint8)
         nbits, first = parse_trailer(b)
         nbytes = b.size
         need = ((nbytes + 3) // 4) * 4 + 16
+        if status is not None:
+            dbuf = stage_up(self, b, need, dev)
+            return codec.elias_decode_async(dbuf, nbytes, nbits, first, int(count), status,
+                                            dtype=dtype, workspace=self._ws)
         # up through a pinned buffer into a device buffer, both kept with the compressor (the
         # decode synchronizes before it returns, so both are free again for the next call)
         ws = self._ws

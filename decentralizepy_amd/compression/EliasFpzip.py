@@ -12,7 +12,7 @@ import torch
 
 from .. import codec
 from .._device import host_copy_into, host_owned
-from .Elias import Elias, _grown
+from .Elias import Elias, _grown, stage_up
 
 _MAGIC = 0x5A465044
 _BLOCK = 256
@@ -49,16 +49,24 @@ class EliasFpzip(Elias):
         torch.cuda.current_stream(s.device).synchronize()
         return host_owned(pin)
 
-    def decompress_float_device(self, bytes, device=None):
+    def value_count(self, bytes):
+        """The number of values a float stream holds (its header), without decoding it."""
+        return parse_float_header(bytes)[0]
+
+    def decompress_float_device(self, bytes, device=None, status=None):
         """Host stream bytes -> device fp32 values.  Up through a pinned buffer and into a
         device buffer, both kept with the compressor (fpz_decode synchronises before it returns,
         so both are free for the next call): one host copy into page-locked memory and a DMA —
         a fresh copy of the stream (page faults) plus a pageable transfer had cost ~4 ms per
-        JWINS payload (tools/diag/plugin_breakdown.py)."""
+        JWINS payload (tools/diag/plugin_breakdown.py).  With ``status`` (a device int32 word)
+        the call does not synchronise: the stream goes up through the compressor's pinned ring
+        and a malformed stream ORs the word nonzero."""
         dev = self._dev(device)
         n, prec = parse_float_header(bytes)
         b = np.frombuffer(memoryview(bytes), dtype=np.uint8)
         nb = b.size
+        if status is not None:
+            return codec.fpz_decode(stage_up(self, b, nb, dev), n, prec, status=status)
         ws = self._ws
         pin = _grown(ws, "fpz_pin", nb, dict(pin_memory=True))
         dbuf = _grown(ws, "fpz_dev", nb, dict(device=dev))

@@ -408,30 +408,36 @@ extern "C" int dpz_elias_encode(const int32_t* idx, int64_t k, uint8_t* out, int
   return DPZ_OK;
 }
 
-extern "C" int dpz_elias_decode(const uint8_t* in, int64_t nbytes, int64_t nbits, int64_t first,
-                                int64_t* out64, int32_t* out32, int64_t out_cap,
-                                int64_t* count_host, void* ws, size_t ws_bytes,
-                                dpz_stream_t stream) {
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  if (!in || nbytes < 16 || nbits < 128 || !count_host || (!out64 && !out32)) return DPZ_ERR_ARG;
+namespace {
+
+// The async decode's tail: the stream must hold exactly `count` values (the caller knows the
+// count from the payload's other leg), else the status word is OR-ed nonzero.
+__global__ void elias_check_kernel(const ElHdr* hdr, int64_t count, uint32_t* status) {
+  if (threadIdx.x == 0 && (hdr->status || (int64_t)hdr->count != count)) atomicOr(status, 1u);
+}
+
+// a one-value stream (L == 0), written on the device (no host source for an async copy)
+__global__ void elias_single_kernel(int64_t first, int64_t count, int64_t* out64, int32_t* out32,
+                                    uint32_t* status) {
+  if (threadIdx.x != 0) return;
+  if (out64) out64[0] = first;
+  if (out32) out32[0] = (int32_t)first;
+  if (status && count != 1) atomicOr(status, 1u);
+}
+
+// argument checks + the three decode launches; *hdr_out = the header the launches fill
+int elias_decode_launch(const uint8_t* in, int64_t nbytes, int64_t nbits, int64_t first,
+                        int64_t* out64, int32_t* out32, int64_t out_cap, void* ws,
+                        size_t ws_bytes, hipStream_t st, ElHdr** hdr_out) {
+  if (!in || nbytes < 16 || nbits < 128 || (!out64 && !out32)) return DPZ_ERR_ARG;
   if (reinterpret_cast<uintptr_t>(in) & 3u) return DPZ_ERR_ARG;
   const uint64_t L = (uint64_t)(nbits - 128);
   if ((uint64_t)nbytes * 8 < L) return DPZ_ERR_ARG;
   const int64_t nch = (int64_t)((L + EL_CHUNK - 1) / EL_CHUNK);
   if ((nch + EL_SUPER - 1) / EL_SUPER > EL_MAX_SUPER) return DPZ_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < dpz_elias_workspace_bytes(2, nbytes)) return DPZ_ERR_WORKSPACE;
-  if (L == 0) {  // a single value (the reference cannot produce it, but decode it consistently)
-    *count_host = 1;
-    if (out_cap >= 1) {
-      if (out64) DPZ_HIP_TRY(hipMemcpyAsync(out64, &first, 8, hipMemcpyHostToDevice, st));
-      if (out32) {
-        const int32_t f32 = (int32_t)first;
-        DPZ_HIP_TRY(hipMemcpyAsync(out32, &f32, 4, hipMemcpyHostToDevice, st));
-      }
-      DPZ_HIP_TRY(hipStreamSynchronize(st));
-    }
-    return DPZ_OK;
-  }
+  *hdr_out = nullptr;
+  if (L == 0) return DPZ_OK;
   char* p = static_cast<char*>(ws);
   size_t o = 0;
   ElHdr* hdr = reinterpret_cast<ElHdr*>(p + o); o += al256(sizeof(ElHdr));
@@ -449,6 +455,30 @@ extern "C" int dpz_elias_decode(const uint8_t* in, int64_t nbytes, int64_t nbits
   DPZ_TIMED(DPZ_KT_ELIAS_RESOLVE, st, elias_resolve_kernel<<<1, 1024, 0, st>>>(nch, exit_tab, cnt_tab, sum_tab, centry, cpos, cbase, hdr));
   DPZ_TIMED(DPZ_KT_ELIAS_WRITE, st, elias_write_kernel<<<grid, 256, 0, st>>>(in32, nwords_in, L, nch, first, centry, cpos, cbase, hdr,
                                            out_cap, out64, out32));
+  *hdr_out = hdr;
+  return DPZ_OK;
+}
+
+}  // namespace
+
+extern "C" int dpz_elias_decode(const uint8_t* in, int64_t nbytes, int64_t nbits, int64_t first,
+                                int64_t* out64, int32_t* out32, int64_t out_cap,
+                                int64_t* count_host, void* ws, size_t ws_bytes,
+                                dpz_stream_t stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!count_host) return DPZ_ERR_ARG;
+  ElHdr* hdr = nullptr;
+  const int rc = elias_decode_launch(in, nbytes, nbits, first, out64, out32, out_cap, ws, ws_bytes,
+                                     st, &hdr);
+  if (rc != DPZ_OK) return rc;
+  if (!hdr) {  // a single value (the reference cannot produce it, but decode it consistently)
+    *count_host = 1;
+    if (out_cap >= 1) {
+      elias_single_kernel<<<1, 64, 0, st>>>(first, 1, out64, out32, nullptr);
+      DPZ_HIP_TRY(hipStreamSynchronize(st));
+    }
+    return DPZ_OK;
+  }
   ElHdr h;
   DPZ_HIP_TRY(hipMemcpyAsync(&h, hdr, sizeof(h), hipMemcpyDeviceToHost, st));
   DPZ_HIP_TRY(hipStreamSynchronize(st));
@@ -456,4 +486,23 @@ extern "C" int dpz_elias_decode(const uint8_t* in, int64_t nbytes, int64_t nbits
   *count_host = (int64_t)h.count;
   if ((int64_t)h.count > out_cap) return DPZ_ERR_WORKSPACE;
   return DPZ_OK;
+}
+
+extern "C" int dpz_elias_decode_async(const uint8_t* in, int64_t nbytes, int64_t nbits,
+                                      int64_t first, int64_t* out64, int32_t* out32, int64_t count,
+                                      uint32_t* status, void* ws, size_t ws_bytes,
+                                      dpz_stream_t stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!status || count < 1) return DPZ_ERR_ARG;
+  ElHdr* hdr = nullptr;
+  const int rc = elias_decode_launch(in, nbytes, nbits, first, out64, out32, count, ws, ws_bytes,
+                                     st, &hdr);
+  if (rc != DPZ_OK) return rc;
+  if (!hdr) {
+    elias_single_kernel<<<1, 64, 0, st>>>(first, count, out64, out32, status);
+  } else {
+    elias_check_kernel<<<1, 64, 0, st>>>(hdr, count, status);
+  }
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DPZ_OK : (int)e;
 }

@@ -121,16 +121,43 @@ class PartialModel(Sharing):
         """reference PartialModel.py:156-162; with ``device`` a device compressor decodes the
         indices straight into a device int32 tensor for the fold."""
         if self.compress:
+            comp = self.compressor
+            if device and getattr(comp, "async_decode", False) and "indices" in data:
+                return self._decompress_async(data)
             if "indices" in data:
-                if device and hasattr(self.compressor, "decompress_device"):
-                    data["indices"] = self.compressor.decompress_device(data["indices"])
+                if device and hasattr(comp, "decompress_device"):
+                    data["indices"] = comp.decompress_device(data["indices"])
                 else:
-                    data["indices"] = self.compressor.decompress(data["indices"])
+                    data["indices"] = comp.decompress(data["indices"])
             if "params" in data:
-                if device and hasattr(self.compressor, "decompress_float_device"):
-                    data["params"] = self.compressor.decompress_float_device(data["params"])
+                if device and hasattr(comp, "decompress_float_device"):
+                    data["params"] = comp.decompress_float_device(data["params"])
                 else:
-                    data["params"] = self.compressor.decompress_float(data["params"])
+                    data["params"] = comp.decompress_float(data["params"])
+        return data
+
+    def _decompress_async(self, data):
+        """The device decode of a received payload with no host synchronisation: the value count
+        comes from the float leg's header (or the raw values' length), both legs go up through
+        the compressor's pinned ring and decode on the stream, and a malformed leg ORs the
+        round's status word, read once after the fold (``_check_received``).  The host copy of
+        the next payload's streams then overlaps this one's DMA and decode."""
+        comp = self.compressor
+        status = self._recv_status_word()
+        params = data.get("params")
+        if params is not None and hasattr(comp, "decompress_float_device"):
+            data["params"] = comp.decompress_float_device(params, status=status)
+            count = data["params"].numel()
+        else:
+            if params is not None:
+                data["params"] = comp.decompress_float(params)
+                count = int(np.asarray(data["params"]).size)
+            else:
+                count = 0
+        if count < 1:  # nothing to check the index count against: the synchronous decode
+            data["indices"] = comp.decompress_device(data["indices"])
+        else:
+            data["indices"] = comp.decompress_device(data["indices"], count=count, status=status)
         return data
 
     # ---- encode -----------------------------------------------------------------------------------

@@ -61,6 +61,8 @@ class Sharing:
         self.staging = Staging()
         self._pay_names = PayloadNames()
         self.workspace = codec.Workspace(self.device)
+        self._recv_status = None  # the round's asynchronous-decode status word
+        self._recv_status_used = False
         if hasattr(getattr(self, "compressor", None), "_dev"):
             self.compressor.device = self.device  # device compressors run on this node's GPU
 
@@ -135,6 +137,25 @@ class Sharing:
         """Received (decompressed) payload dict -> (idx int32 device or None, vals fp32 device)."""
         return None, self._h2d(data["params"], np.float32, "params")
 
+    def _recv_status_word(self):
+        """The round's device status word for asynchronous payload decodes (zeroed on first use
+        in a round; ``_check_received`` reads it once)."""
+        if getattr(self, "_recv_status", None) is None:
+            self._recv_status = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._recv_status_used = False
+        if not self._recv_status_used:
+            self._recv_status.zero_()
+            self._recv_status_used = True
+        return self._recv_status
+
+    def _check_received(self):
+        """Raise if an asynchronous payload decode of this round saw a malformed stream (one
+        synchronisation: the fold output is read back right after anyway)."""
+        if getattr(self, "_recv_status_used", False):
+            self._recv_status_used = False
+            if int(self._recv_status.item()) != 0:
+                raise ValueError("malformed payload stream (Elias or float leg)")
+
     def _pop_payloads(self, peer_deques):
         payloads, degrees = [], []
         for n in peer_deques:
@@ -155,6 +176,7 @@ class Sharing:
                                     workspace=self.workspace)
 
     def _load_flat(self, out_dev):
+        self._check_received()
         # load_state_dict of the averaged model with its D2H pipelined against the host copy
         load_flat(self.model, out_dev, self.staging, "result")
 
@@ -186,6 +208,7 @@ class Sharing:
             weights = [1 / len(peer_deques)] * len(payloads)
             local = self._local_flat_device()
             out = self._fold(local, payloads, weights, None)
+            self._check_received()
             flat = to_host(out, self.staging, "result")
             total = self._unflatten(flat)
         self.model.load_state_dict(total)

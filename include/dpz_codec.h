@@ -520,6 +520,16 @@ int dpz_elias_encode(const int32_t* idx, int64_t k, uint8_t* out, int64_t out_ca
 int dpz_elias_decode(const uint8_t* in, int64_t nbytes, int64_t nbits, int64_t first,
                      int64_t* out64, int32_t* out32, int64_t out_cap, int64_t* count_host,
                      void* ws, size_t ws_bytes, dpz_stream_t stream);
+/* dpz_elias_decode without a host synchronisation, for a receiver that knows the value count
+ * from the payload's other leg (the float header's n, or the raw values' length): decodes into
+ * out64 / out32 (device, `count` entries) and ORs *status (DEVICE uint32) nonzero on `stream`
+ * when the stream is malformed or holds a different number of values — the entries are then
+ * unspecified (the fold kernels stay in bounds on any index values); the caller reads the status
+ * word once after the round's folds.  Same workspace as dpz_elias_decode.  Replaces the same
+ * reference lines (compression/Elias.py:54-97), called from PartialModel.py:156-162.          */
+int dpz_elias_decode_async(const uint8_t* in, int64_t nbytes, int64_t nbits, int64_t first,
+                           int64_t* out64, int32_t* out32, int64_t count, uint32_t* status,
+                           void* ws, size_t ws_bytes, dpz_stream_t stream);
 
 /* ---- Block-floating fp32 value coding (the float leg of EliasFpzip / EliasFpzipLossy) --------
  * Replaces compression/EliasFpzip.py:19-51 (fpzip.compress, precision 0) and

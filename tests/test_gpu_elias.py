@@ -117,3 +117,86 @@ def test_fp16_compressor_roundtrip(dev):
     enc = c.compress_float(x)
     assert enc.dtype == np.uint8 and enc.size == 2 * x.size
     np.testing.assert_array_equal(c.decompress_float(enc), x.astype(np.float16).astype(np.float32))
+
+
+def _padded(enc):
+    nbytes = enc.size
+    buf = torch.zeros(((nbytes + 3) // 4) * 4 + 16, dtype=torch.uint8)
+    buf[:nbytes] = torch.from_numpy(enc)
+    return buf, nbytes, int(enc[-8:].view("<i8")[0]), int(enc[-16:-8].view("<i8")[0])
+
+
+@pytest.mark.parametrize("dt", [torch.int32, torch.int64])
+def test_elias_async_decode(dev, dt):
+    """dpz_elias_decode_async: the values of dpz_elias_decode with no host synchronisation; the
+    status word stays 0 for a well-formed stream of the expected count and is OR-ed nonzero for a
+    count mismatch or a malformed stream (all-zero code bits: no code ever terminates)."""
+    from decentralizepy_amd import codec
+    rng = np.random.default_rng(9)
+    for idx in (np.sort(rng.choice(25_000_009, 250_000, replace=False)).astype(np.int32),
+                np.array([0, 2**31 - 1], np.int32), np.arange(3, 70_003, dtype=np.int32)):
+        buf, nbytes, nbits, first = _padded(oelias.encode(idx))
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+        out = codec.elias_decode_async(buf.to(dev), nbytes, nbits, first, idx.size, status,
+                                       dtype=dt)
+        np.testing.assert_array_equal(out.cpu().numpy(), idx.astype(out.cpu().numpy().dtype))
+        assert int(status.item()) == 0
+        for wrong in (idx.size - 1, idx.size + 1):
+            s2 = torch.zeros(1, dtype=torch.int32, device=dev)
+            codec.elias_decode_async(buf.to(dev), nbytes, nbits, first, wrong, s2, dtype=dt)
+            assert int(s2.item()) != 0
+    # one value (L = 0): the trailer alone
+    one = np.zeros(16, np.uint8)
+    one[:8] = np.frombuffer(np.int64(41).tobytes(), np.uint8)
+    one[8:] = np.frombuffer(np.int64(128).tobytes(), np.uint8)
+    buf, nbytes, nbits, first = _padded(one)
+    for count, bad in ((1, False), (2, True)):
+        s = torch.zeros(1, dtype=torch.int32, device=dev)
+        out = codec.elias_decode_async(buf.to(dev), nbytes, nbits, first, count, s, dtype=dt)
+        assert int(out[0].item()) == 41 and (int(s.item()) != 0) == bad
+    # malformed: 4096 zero code bits
+    zeros = np.zeros(512 + 16, np.uint8)
+    zeros[-16:-8] = np.frombuffer(np.int64(5).tobytes(), np.uint8)
+    zeros[-8:] = np.frombuffer(np.int64(128 + 4096).tobytes(), np.uint8)
+    buf, nbytes, nbits, first = _padded(zeros)
+    s = torch.zeros(1, dtype=torch.int32, device=dev)
+    codec.elias_decode_async(buf.to(dev), nbytes, nbits, first, 100, s, dtype=dt)
+    assert int(s.item()) != 0
+    with pytest.raises(ValueError):
+        codec.elias_decode(buf.to(dev), nbytes, nbits, first, 4096, dtype=dt)
+
+
+@pytest.mark.parametrize("cls", ["Elias", "EliasFpzip"])
+def test_plugin_async_receive_rejects_a_malformed_payload(cls, dev, tmp_path):
+    """The plugin's receive decodes without host synchronisation; a neighbour payload whose
+    index stream holds fewer values than its value leg (or a malformed float stream) raises
+    ValueError at the round's one status check, before the model is loaded, and the next round
+    with good payloads runs normally."""
+    from collections import deque
+
+    from decentralizepy_amd.sharing.PartialModel import PartialModel
+    meta, arrays = scenario.load("pm_a01_plain")
+    model = scenario.make_model(meta["shape"])
+    scenario.set_flat(model, arrays["x0"])
+    kwargs = dict(meta["kwargs"], compress=True, compression_class=cls,
+                  compression_package=f"decentralizepy_amd.compression.{cls}")
+    plugin = PartialModel(0, 0, None, scenario._Mapping(), scenario._Graph([1, 2, 3]), model,
+                          None, str(tmp_path), **kwargs)
+    mr = meta["rounds"][0]
+    scenario.set_flat(model, arrays["r0_x"])
+    plugin.get_data_to_send(degree=3)
+    before = scenario.get_flat(model)
+    msgs = scenario._elias_wire(scenario.neighbour_msgs(mr, arrays, 0), cls)
+    j = next(i for i, m in enumerate(msgs) if "indices" in m)  # a partial share
+    bad = dict(msgs[j])
+    idx = oelias.decode(np.asarray(bad["indices"]))
+    bad["indices"] = oelias.encode(idx[:-1].astype(np.int32))  # one index short
+    msgs[j] = bad
+    peer = {uid: deque([m]) for uid, m in zip([1, 2, 3], msgs)}
+    with pytest.raises(ValueError):
+        plugin._averaging(peer)
+    np.testing.assert_array_equal(scenario.get_flat(model), before)  # nothing loaded
+    # a good round after the failed one: the status word was cleared
+    plugin.get_data_to_send(degree=3)
+    msgs = scenario._elias_wire(scenario.neighbour_msgs(mr, arrays, 0), cls)
+    plugin._averaging({uid: deque([m]) for uid, m in zip([1, 2, 3], msgs)})
