@@ -762,7 +762,8 @@ def _perturb(model, g, scale=0.01):
             p.add_(scale * torch.randn(p.shape, generator=g))
 
 
-def plugin_case(dev, kind="partial", rounds=6, warmup=2, seed=17, cpu_rounds=1, tmpdir=None):
+def plugin_case(dev, kind="partial", rounds=6, warmup=2, seed=17, cpu_rounds=1, tmpdir=None,
+                on_warm=None):
     """One node's gossip round through the drop-in classes, host memory to host memory, as
     node/DPSGDNode.py:72-115 drives them: ``get_data_to_send(degree=3)`` (state_dict -> pinned H2D
     -> device encode -> device Elias (+ float codec) -> D2H -> the wire dict), the TCP wire
@@ -820,6 +821,8 @@ def plugin_case(dev, kind="partial", rounds=6, warmup=2, seed=17, cpu_rounds=1, 
 
     t_send, t_recv, out_bytes, in_bytes = [], [], 0, 0
     for r in range(warmup + rounds):
+        if r == warmup and on_warm is not None:
+            on_warm()  # a diagnostic's counters start with the timed rounds
         wires = neighbour_wires()  # the neighbours' round (not this node's work)
         _perturb(nmodel, g)
         torch.cuda.synchronize()

@@ -51,13 +51,21 @@ class Staging:
             ev.synchronize()
         buf = self._bufs.get(key)
         if buf is None or buf.numel() < n:
-            size = max(int(n), 1) * torch.empty(0, dtype=dtype).element_size()
+            esz = torch.empty(0, dtype=dtype).element_size()
             old = 0 if buf is None else buf.numel() * buf.element_size()
+            # exact the first time (the model-sized buffers never grow); a buffer that grows is
+            # grown to the next power of two (payload sizes vary round to round and each growth
+            # is a page-locked allocation, ~1 ms per 10 MB on the box: it grows a few times in
+            # its life, not every round), exact if that would pass the cap
+            want = max(int(n), 1) if buf is None else 1 << max(int(n) - 1, 1).bit_length()
+            if self.total - old + want * esz > self.cap:
+                want = max(int(n), 1)
+            size = want * esz
             if self.total - old + size > self.cap:
                 return None
             self._bufs.pop(key, None)
             del buf
-            buf = torch.empty(max(int(n), 1), dtype=dtype, pin_memory=True)
+            buf = torch.empty(want, dtype=dtype, pin_memory=True)
             self._bufs[key] = buf
             self.total += size - old
         return buf[:n]

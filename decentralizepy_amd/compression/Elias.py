@@ -37,7 +37,7 @@ def _grown(ws, name, n, kw):
     return buf
 
 
-def stage_up(comp, b, need, device):
+def stage_up(comp, b, need, device, leg):
     """Host stream bytes ``b`` -> a fresh device uint8 buffer of ``need`` bytes (zero padded),
     through a ring of pinned buffers kept with the compressor ``comp``: the DMA is asynchronous and
     a pinned slot is reused only after its own earlier DMA has completed, so the host copy of the
@@ -45,8 +45,8 @@ def stage_up(comp, b, need, device):
     caching allocator: freed, it is reused only by later work on the same stream."""
     if comp._staging is None:
         comp._staging = Staging()
-        comp._names = PayloadNames(slots=4)
-    name = comp._names("stream")
+        comp._names = PayloadNames(slots=3)
+    name = comp._names(leg)  # a ring per leg kind: an index slot never grows to a value leg's size
     pin = comp._staging.get(name, need, torch.uint8)
     if pin is None:  # over the pinned cap: a pageable copy
         pad = np.zeros(need, dtype=np.uint8)
@@ -104,7 +104,7 @@ class Elias(Compression):
         nbytes = b.size
         need = ((nbytes + 3) // 4) * 4 + 16
         if status is not None:
-            dbuf = stage_up(self, b, need, dev)
+            dbuf = stage_up(self, b, need, dev, "idx")
             return codec.elias_decode_async(dbuf, nbytes, nbits, first, int(count), status,
                                             dtype=dtype, workspace=self._ws)
         # up through a pinned buffer into a device buffer, both kept with the compressor (the

@@ -66,7 +66,7 @@ class EliasFpzip(Elias):
         b = np.frombuffer(memoryview(bytes), dtype=np.uint8)
         nb = b.size
         if status is not None:
-            return codec.fpz_decode(stage_up(self, b, nb, dev), n, prec, status=status)
+            return codec.fpz_decode(stage_up(self, b, nb, dev, "vals"), n, prec, status=status)
         ws = self._ws
         pin = _grown(ws, "fpz_pin", nb, dict(pin_memory=True))
         dbuf = _grown(ws, "fpz_dev", nb, dict(device=dev))

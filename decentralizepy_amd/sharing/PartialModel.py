@@ -122,7 +122,7 @@ class PartialModel(Sharing):
         indices straight into a device int32 tensor for the fold."""
         if self.compress:
             comp = self.compressor
-            if device and getattr(comp, "async_decode", False) and "indices" in data:
+            if device and getattr(comp, "async_decode", False):
                 return self._decompress_async(data)
             if "indices" in data:
                 if device and hasattr(comp, "decompress_device"):
@@ -154,6 +154,8 @@ class PartialModel(Sharing):
                 count = int(np.asarray(data["params"]).size)
             else:
                 count = 0
+        if "indices" not in data:  # a full share (Wavelet.py:174-231's metadata cap)
+            return data
         if count < 1:  # nothing to check the index count against: the synchronous decode
             data["indices"] = comp.decompress_device(data["indices"])
         else:

@@ -83,6 +83,38 @@ def main():
             torch.set_num_threads(t)
             r[f"host_copy_torch_{t}t_ms"] = round(med(host_only), 3)
         torch.set_num_threads(t0)
+        # cold: a fresh bytes object every repetition (what pickle.loads hands the receiver)
+        import pickle
+        wire = pickle.dumps({"b": src})
+
+        def cold(way):
+            ts = []
+            for _ in range(7):
+                fresh = pickle.loads(wire)["b"]
+                fa = np.frombuffer(fresh, dtype=np.uint8)
+                with warnings.catch_warnings():
+                    warnings.simplefilter("ignore")
+                    ft = torch.from_numpy(fa)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                if way == "a":
+                    pin.copy_(ft)
+                    dst.copy_(pin, non_blocking=True)
+                elif way == "a_host":
+                    pin.copy_(ft)
+                elif way == "b":
+                    dst.copy_(ft)
+                else:
+                    hip.hipHostRegister(fa.ctypes.data, n, 0)
+                    dst.copy_(ft, non_blocking=True)
+                    torch.cuda.synchronize()
+                    hip.hipHostUnregister(fa.ctypes.data)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t1)
+            return round(1e3 * sorted(ts)[len(ts) // 2], 3)
+
+        for w in ("a", "a_host", "b", "c"):
+            r[f"cold_{w}_ms"] = cold(w)
         r["host_copy_torch_GBps"] = round(n / r["host_copy_torch_ms"] / 1e6, 2)
         r["host_copy_numpy_GBps"] = round(n / r["host_copy_numpy_ms"] / 1e6, 2)
         out.append(r)

@@ -34,16 +34,26 @@ rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 acc = defaultdict(list)
 cur = defaultdict(float)
 cnt = defaultdict(int)
+allocs = []
+
+
+# NOSYNC=1: host time only (no device synchronisation around a part: the asynchronous receive
+# path is timed as it runs; a part then shows the host work plus whatever it waits on)
+SYNC = os.environ.get("NOSYNC") != "1"
+if os.environ.get("ASYNC") == "0":  # A/B: the synchronous payload decodes
+    Elias.Elias.async_decode = False
 
 
 def wrap(owner, name, label):
     fn = getattr(owner, name)
 
     def timed(*a, **kw):
-        torch.cuda.synchronize()
+        if SYNC:
+            torch.cuda.synchronize()
         t0 = time.perf_counter()
         r = fn(*a, **kw)
-        torch.cuda.synchronize()
+        if SYNC:
+            torch.cuda.synchronize()
         cur[label] += time.perf_counter() - t0
         cnt[label] += 1
         return r
@@ -66,6 +76,41 @@ for owner, name, label in [
         (S, "_load_flat", "recv.load_flat"), (P, "_load_flat", "recv.load_flat"),
         (P, "_post_step", "recv.post_step"),
         (codec, "waverec", "recv.waverec")]:
+    wrap(owner, name, label)
+from decentralizepy_amd import _device  # noqa: E402
+
+def _get_stamped(self, name, n, dtype):
+    """Staging.get with its two waits stamped apart: the event of the buffer's previous DMA and
+    a page-locked allocation (a growth), per buffer name."""
+    key = (name, dtype)
+    ev = self._events.pop(key, None)
+    t0 = time.perf_counter()
+    if ev is not None:
+        ev.synchronize()
+    t1 = time.perf_counter()
+    cur["stage.get_event_wait"] += t1 - t0
+    cur[f"stage.get_event_wait[{name}]"] += t1 - t0
+    buf = self._bufs.get(key)
+    grow = buf is None or buf.numel() < n
+    if ev is not None:
+        self._events[key] = ev
+    r = _get_orig(self, name, n, dtype)
+    t2 = time.perf_counter()
+    if grow:
+        allocs.append((name, int(n), None if buf is None else int(buf.numel()),
+                       round(1e3 * (t2 - t1), 3)))
+        cur["stage.get_alloc"] += t2 - t1
+        cur[f"stage.get_alloc[{name}]"] += t2 - t1
+        cnt["stage.get_alloc"] += 1
+    return r
+
+
+_get_orig = _device.Staging.get
+_device.Staging.get = _get_stamped
+for owner, name, label in [  # the staging and launch pieces of the receive decodes (Elias, "host_copy_into", "stage.host_copy"),
+        (EliasFpzip, "host_copy_into", "stage.host_copy"), (codec, "fpz_decode", "stage.fpz_decode"),
+        (codec, "elias_decode_async", "stage.elias_decode_async"),
+        (codec, "elias_decode", "stage.elias_decode_sync")]:
     wrap(owner, name, label)
 for mod in (Sharing, PartialModel, Wavelet):  # the modules' own to_host bindings
     wrap(mod, "to_host", "any.to_host")
@@ -93,13 +138,25 @@ dev = torch.device("cuda", 0)
 bw.plugin_case(dev, kind, rounds=1, warmup=1, cpu_rounds=0)  # warm
 cur.clear()
 cnt.clear()
-res = bw.plugin_case(dev, kind, rounds=rounds, warmup=0, cpu_rounds=0)
+
+
+def _warm():
+    allocs.clear()
+    cur.clear()
+    cnt.clear()
+
+
+# counters from the first timed round on, after 3 warm rounds of the same plugins (their pinned
+# buffers grown to the payload sizes the alpha draws produce)
+res = bw.plugin_case(dev, kind, rounds=rounds, warmup=3, cpu_rounds=0, on_warm=_warm)
 # the neighbours' rounds (3 get_data_to_send per round) are inside the same counters: report the
 # node's own parts per round by dividing the send parts by 4 plugins and the rest by rounds
-out = {"kind": kind, "rounds": rounds, "round": res,
+out = {"kind": kind, "rounds": rounds, "round": res, "sync_wrapped": SYNC,
+       "async_decode": Elias.Elias.async_decode,
        "note": "send.* parts are summed over the node and its 3 neighbours' get_data_to_send "
                "(4 calls per round); recv.* and wire.pickle_loads are the node's own; "
                "ms per round"}
 out["parts_ms_per_round"] = {k: round(v / rounds * 1e3, 3) for k, v in sorted(cur.items())}
+out["pinned_allocs_timed_rounds"] = allocs
 out["calls_per_round"] = {k: round(v / rounds, 2) for k, v in sorted(cnt.items())}
 print(json.dumps(out))
