@@ -390,6 +390,13 @@ def product_one_node(sets, n, k, stream, reps, alpha=0.01):
                 for p in plugins:
                     p._ring.flush()
 
+            # a timed region is one full ring per plugin (its counter flushed once, when full, as
+            # in a run: RingCounter), so the deferred counter work is charged at the rate a node
+            # pays it; at least `reps` steps
+            ring = plugins[0]._ring
+            ring_rounds = max(1, min(ring.MAX_SEGS, ring.cap_bytes // max(4 * k, 1)))
+            reps = max(reps, R * ring_rounds)
+
             def loop(**kw):
                 ev0 = torch.cuda.Event(enable_timing=True)
                 ev1 = torch.cuda.Event(enable_timing=True)
@@ -427,6 +434,7 @@ def product_one_node(sets, n, k, stream, reps, alpha=0.01):
                 "step_us": round(t_step * 1e6, 3), "encode_us": round(t_enc * 1e6, 3),
                 "fold_us": round(t_dec * 1e6, 3), "host_enqueue_us": round(h_step * 1e6, 3),
                 "fold_path": "fold base (encode writes it)" if npay == 1 else "plain fold",
+                "steps_per_region": reps, "ring_rounds": ring_rounds,
                 "kernels": kern,
                 "alg_bytes": b_enc + b_dec,
                 "GiBps": round(4 * n / t_step / 2 ** 30, 2),
@@ -436,7 +444,9 @@ def product_one_node(sets, n, k, stream, reps, alpha=0.01):
                    "its _model_change / _encode / _fold_on_base / _fold), host legs excluded, one "
                    "plugin per rotated node state; model_change formed on read only "
                    "(LazyChange), the counter updates deferred to a ring folded in on read "
-                   "(RingCounter) — every counter is read at the end of each timed region")
+                   "(RingCounter) — a timed region is one full ring per plugin, every counter "
+                   "read (flushed) at its end, so the deferred updates are timed at the rate a "
+                   "node pays them")
     out["fell_back"] = fell
     return out
 
@@ -514,6 +524,7 @@ def gossip_case(n, alpha, dev, rank, world, dist, rounds, warmup, exchange="allg
     # alg_bytes_8n counts the fold's output once (the round-4 convention)
     return dict(n=n, k=k, s_step=s_round, nodes=len(adj), edges=nsum // 2, legs_ms=legs,
                 rs_group=getattr(eng, "rs_group", None),
+                peer_recv_payloads=(eng._peer_n_recv if eng.exchange_mode == "peer" else None),
                 value=len(adj) * 4 * n / s_round / 2 ** 30,
                 alg_bytes=len(adj) * (8 * n + 16 * k) + len(adj) * 12 * n + nsum * 8 * k,
                 alg_bytes_8n=len(adj) * (8 * n + 16 * k) + len(adj) * 8 * n + nsum * 8 * k)
@@ -662,6 +673,8 @@ def main():
         r = gossip_case(args.n, args.alpha, dev, rank, world, dist, rounds, warm)
         rs = gossip_case(args.n, args.alpha, dev, rank, world, dist, max(3, rounds // 2), warm,
                          exchange="reduce_scatter")
+        pe = gossip_case(args.n, args.alpha, dev, rank, world, dist, max(3, rounds // 2), warm,
+                         exchange="peer")
         cpu = None
         if rank == 0 and not args.no_cpu:
             # one node's round of the 96 (encode + the MH fold of its neighbours' payloads;
@@ -707,6 +720,15 @@ def main():
                     "ms_per_round": round(rs["s_step"] * 1e3, 4),
                     "value": round(rs["value"], 3), "legs_ms": rs["legs_ms"],
                     "rs_group": rs["rs_group"]},
+                "peer_mode": {
+                    "note": "exchange='peer': each rank sends each other rank only the payloads "
+                            "its nodes' neighbours there fold (one all_to_all_single, uneven "
+                            "splits), bit-exact fold as in the all-gather mode" +
+                            ("" if world > 1 else " (1 GPU: every neighbour is local, no "
+                                                  "collective)"),
+                    "ms_per_round": round(pe["s_step"] * 1e3, 4),
+                    "value": round(pe["value"], 3), "legs_ms": pe["legs_ms"],
+                    "remote_payloads_per_rank": pe["peer_recv_payloads"]},
                 "cpu_baseline": cpu,
             }), flush=True)
         _finish(dist)

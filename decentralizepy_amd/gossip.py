@@ -22,6 +22,14 @@ the owning rank, which combines them with its model (``DPZ_EW_MHCOMBINE``).  Des
 are sized to the budget.  This path reassociates the fp32 sums (RCCL's reduction order), so it
 matches the reference within fp32 tolerance, not bit for bit.
 
+Peer exchange (``exchange="peer"``): each rank sends every other rank exactly the payloads of
+its nodes that have a neighbour there — one ``all_to_all_single`` with uneven splits (grouped
+point-to-point writes over xGMI on RCCL) — and folds bit-exactly as in the all-gather mode, the
+local neighbours' payloads read in place.  A rank holds only the remote payloads its own
+nodes' neighbourhoods name (96_regular.edges over 8 ranks: about 41 of 84 remote payloads), so
+"auto" takes it over the reduce-scatter whenever those fit the budget and the all-gather does
+not.
+
 The encode / fold callables are injectable so the sharding and exchange logic can be tested with
 the CPU gloo backend; the defaults are the HIP codec (no CPU fallback).
 """
@@ -80,9 +88,10 @@ class GossipRound:
         """adj: adjacency sets of all nodes; x_init: (hi - lo, N) fp32 tensor with this rank's
         nodes' flat models (device tensor for the HIP codec).
 
-        exchange: "allgather" (bit-exact), "reduce_scatter" (over-HBM) or "auto" (reduce-scatter
-        when world > 1 and the all-gathered payloads exceed ``hbm_budget`` bytes; default budget:
-        half of the device's free memory at construction).  ``partial(payloads, weights, out)``
+        exchange: "allgather" (bit-exact), "peer" (bit-exact; only the payloads this rank's
+        neighbourhoods name), "reduce_scatter" (over-HBM) or "auto" (when world > 1 and the
+        all-gathered payloads exceed ``hbm_budget`` bytes: "peer" if its payloads fit, else
+        reduce-scatter; default budget: half of the device's free memory at construction).  ``partial(payloads, weights, out)``
         (zero-based weighted sum of sparse payloads) and ``combine(x, B, A, c, out)`` are
         injectable like encode / fold (CPU tests); the defaults are the HIP codec."""
         self.adj = adj
@@ -148,12 +157,24 @@ class GossipRound:
             dist.all_reduce(b, op=dist.ReduceOp.MIN, group=group)
             hbm_budget = float(b.item())
         self.hbm_budget = hbm_budget
+        self._peer_plan()
         if exchange == "auto":
-            exchange = "reduce_scatter" if world > 1 and gathered > hbm_budget else "allgather"
-        if exchange not in ("allgather", "reduce_scatter"):
+            exchange = "allgather"
+            if world > 1 and gathered > hbm_budget:
+                exchange = "peer" if self._peer_bytes <= hbm_budget else "reduce_scatter"
+        if exchange not in ("allgather", "peer", "reduce_scatter"):
             raise ValueError(f"unknown exchange {exchange!r}")
         self.exchange_mode = exchange
-        if exchange == "allgather":
+        if exchange == "peer":
+            k = self.k
+            n_recv = max(1, self._peer_n_recv)
+            self._peer_recv = torch.empty(n_recv, 2, k, dtype=torch.int32, device=self.device)
+            self._peer_send = torch.empty(max(1, len(self._peer_rows)), 2, k, dtype=torch.int32,
+                                          device=self.device)
+            self._peer_rows_t = torch.tensor(self._peer_rows, dtype=torch.long,
+                                             device=self.device)
+            self.recv_idx = self.recv_val = None
+        elif exchange == "allgather":
             self.recv_idx = torch.empty(self.per * world, self.k, dtype=torch.int32,
                                         device=self.device)
             self.recv_val = torch.empty(self.per * world, self.k, dtype=torch.float32,
@@ -185,6 +206,44 @@ class GossipRound:
             self.streams = [torch.cuda.Stream(self.device) for _ in range(max(1, streams))]
             self.wss = [codec.Workspace(self.device) for _ in self.streams]
 
+
+    def _peer_plan(self):
+        """The peer exchange's static plan (topology and sharding are fixed): for every rank the
+        remote nodes its neighbourhoods name; this rank's send rows (its nodes, grouped by
+        destination rank, ascending) and receive rows (the remote nodes it needs, grouped by
+        source rank, ascending — the order all_to_all_single lands them in)."""
+        W, per, me = self.world, self.per, self.rank
+        need = [set() for _ in range(W)]
+        for d in range(self.n_nodes):
+            r = d // per
+            for q in self.adj[d]:
+                if q // per != r:
+                    need[r].add(q)
+        send = [sorted(q for q in need[r] if q // per == me) if r != me else [] for r in range(W)]
+        recv = [sorted(q for q in need[me] if q // per == s) if s != me else [] for s in range(W)]
+        self._peer_rows = [q - self.lo for r in range(W) for q in send[r]]
+        flat = [q for s in range(W) for q in recv[s]]
+        self._peer_row = {q: i for i, q in enumerate(flat)}
+        self._peer_n_recv = len(flat)
+        self._peer_in_splits = [2 * self.k * len(send[r]) for r in range(W)]
+        self._peer_out_splits = [2 * self.k * len(recv[s]) for s in range(W)]
+        self._peer_bytes = 8 * self.k * (len(flat) + len(self._peer_rows))
+
+    def _payload(self, q):
+        """(idx int32[k], val fp32[k]) device rows of node q's payload as this rank holds it."""
+        if self.exchange_mode == "peer":
+            if self.lo <= q < self.hi:
+                return self.send_idx[q - self.lo], self.send_val[q - self.lo]
+            row = self._peer_recv[self._peer_row[q]]
+            return row[0], row[1].view(torch.float32)
+        return self.recv_idx[self._slot(q)], self.recv_val[self._slot(q)]
+
+    def _recv_key(self):
+        """Identity of the buffers the fold tables point into (rebuilt when they move)."""
+        if self.exchange_mode == "peer":
+            return (self._peer_recv.data_ptr(), self.send_idx.data_ptr(),
+                    self.send_val.data_ptr())
+        return (self.recv_idx.data_ptr(), self.recv_val.data_ptr())
 
     @property
     def counter(self):
@@ -518,6 +577,20 @@ class GossipRound:
     def exchange(self):
         if self.exchange_mode == "reduce_scatter":
             return  # folded into fold_reduce_scatter
+        if self.exchange_mode == "peer":
+            if not self.coll or not (sum(self._peer_in_splits) or sum(self._peer_out_splits)):
+                return  # no remote neighbour anywhere (one rank): the folds read in place
+            import torch.distributed as dist
+            ns = len(self._peer_rows)
+            if ns:  # this rank's payloads that other ranks fold, packed (idx, val) per row
+                self._peer_send[:ns, 0].copy_(self.send_idx.index_select(0, self._peer_rows_t))
+                self._peer_send[:ns, 1].copy_(
+                    self.send_val.index_select(0, self._peer_rows_t).view(torch.int32))
+            dist.all_to_all_single(self._peer_recv.view(-1)[:sum(self._peer_out_splits)],
+                                   self._peer_send.view(-1)[:sum(self._peer_in_splits)],
+                                   output_split_sizes=self._peer_out_splits,
+                                   input_split_sizes=self._peer_in_splits, group=self.group)
+            return
         if not self.coll:
             self.recv_idx, self.recv_val = self.send_idx, self.send_val  # no copy on one rank
             return
@@ -534,8 +607,9 @@ class GossipRound:
             nbrs, wj, w_self = self.weights[j]
             counts.append(len(nbrs))
             for q in nbrs:
-                idx.append(self.recv_idx[self._slot(q)].data_ptr())
-                val.append(self.recv_val[self._slot(q)].data_ptr())
+                pi, pv = self._payload(q)
+                idx.append(pi.data_ptr())
+                val.append(pv.data_ptr())
                 kk.append(self.k)
             w.extend(wj)
             ws_.append(w_self)
@@ -543,7 +617,7 @@ class GossipRound:
         return dict(np=(ctypes.c_int * max(1, m))(*counts), idx=(ctypes.c_void_p * tot)(*idx),
                     val=(ctypes.c_void_p * tot)(*val), k=(ctypes.c_int64 * tot)(*kk),
                     w=(ctypes.c_float * tot)(*w), w_self=(ctypes.c_float * max(1, m))(*ws_),
-                    key=(self.recv_idx.data_ptr(), self.recv_val.data_ptr()))
+                    key=self._recv_key())
 
     def fold_all(self, guard=None):
         """Every owned node's Metro-Hastings fold.  guard (HIP, DEVICE int32): the round's
@@ -562,7 +636,7 @@ class GossipRound:
             from ._lib import DPZ_FOLD_ALSO_LOCAL, DPZ_FOLD_SELF
             m = self.hi - self.lo
             tab = getattr(self, "_tab", None)
-            if tab is None or tab["key"] != (self.recv_idx.data_ptr(), self.recv_val.data_ptr()):
+            if tab is None or tab["key"] != self._recv_key():
                 tab = self._tab = self._fold_tables()
             ptrs = getattr(self, "_fold_ptrs", None)
             key = (self.x.data_ptr(), self.out.data_ptr())
@@ -581,7 +655,7 @@ class GossipRound:
             from . import _lib
             from ._lib import DPZ_FOLD_ALSO_LOCAL, DPZ_FOLD_SELF
             tab = getattr(self, "_tab", None)
-            if tab is None or tab["key"] != (self.recv_idx.data_ptr(), self.recv_val.data_ptr()):
+            if tab is None or tab["key"] != self._recv_key():
                 tab = self._tab = self._fold_tables()
             m = self.hi - self.lo
             streams = (ctypes.c_void_p * len(self.streams))(*[s.cuda_stream for s in self.streams])
@@ -601,8 +675,7 @@ class GossipRound:
         else:
             for j in nodes:
                 nbrs, w, w_self = self.weights[j]
-                payloads = [(self.recv_idx[self._slot(q)], self.recv_val[self._slot(q)])
-                            for q in nbrs]
+                payloads = [self._payload(q) for q in nbrs]
                 self._fold(self.x[j], payloads, w, w_self, self.out[j])
         # post step: the averaged model becomes both the model and init_model (reference
         # Sharing._averaging load_state_dict + PartialModel._post_step): init_model takes the
@@ -618,7 +691,7 @@ class GossipRound:
 
     def step(self):
         t = self._leg_mark(None)
-        if self.exchange_mode == "allgather" and self.guarded:
+        if self.exchange_mode in ("allgather", "peer") and self.guarded:
             return self._step_guarded(t)
         self.encode_all()
         t = self._leg_mark(t, "encode")

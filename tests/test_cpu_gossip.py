@@ -150,9 +150,9 @@ def _rs_worker(rank, world, port, n, path, q, skew=False):
         x = _models(len(adj), n)
         lo, hi, per = shard(len(adj), world, rank)
         k = round(0.05 * n)
-        # an emulated budget one byte below the all-gathered payloads: auto picks the
-        # reduce-scatter, one destination node per group
-        budget = per * world * k * 8 - 1
+        # an emulated budget one byte below ONE payload: neither the all-gathered payloads nor
+        # the peer exchange's fit, auto picks the reduce-scatter, one destination node per group
+        budget = k * 8 - 1
         if skew:  # rank 1 alone would fit the all-gather: the ranks must still agree (MIN)
             budget += rank * 10 ** 12
         eng = GossipRound(adj, x[lo:hi], 0.05, rank=rank, world=world, encode=_oracle_encode,
@@ -241,3 +241,83 @@ def test_guarded_round_reruns_a_missed_encode(miss_round):
         np.testing.assert_array_equal(a.x0.numpy().view(np.uint32), b.x0.numpy().view(np.uint32))
         np.testing.assert_array_equal(a.counter.numpy(), b.counter.numpy())
     assert state["reruns"] == 1
+
+
+def _peer_worker(rank, world, port, n, path, q, budget):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from decentralizepy_amd.gossip import GossipRound, read_edges, shard
+        adj = read_edges(path)
+        x = _models(len(adj), n)
+        lo, hi, _ = shard(len(adj), world, rank)
+        kw = dict(exchange="peer") if budget is None else dict(hbm_budget=budget)
+        eng = GossipRound(adj, x[lo:hi], 0.05, rank=rank, world=world, encode=_oracle_encode,
+                          fold=_oracle_fold, **kw)
+        assert eng.exchange_mode == "peer" and eng.recv_idx is None
+        for r in range(2):
+            _train(eng, r)
+            eng.step()
+        q.put((rank, lo, eng.x.numpy().copy(), eng._peer_n_recv))
+    except Exception as e:  # noqa: BLE001 - reported to the parent instead of a queue timeout
+        q.put((rank, None, repr(e), 0))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("path,n,world,auto", [(EDGES16, 1500, 2, False), (EDGES96, 600, 2, False),
+                                                (EDGES96, 600, 3, True)])
+def test_peer_exchange_round_equals_single_rank(path, n, world, auto):
+    """The peer exchange (each rank sends other ranks only the payloads their nodes' neighbours
+    name, one all_to_all_single with uneven splits) is bit-exact with the single-rank round;
+    "auto" takes it when the all-gathered payloads exceed the budget and its own fit; a rank
+    holds fewer remote payloads than the all-gather would give it."""
+    from decentralizepy_amd.gossip import GossipRound, read_edges, shard
+    adj = read_edges(path)
+    x = _models(len(adj), n)
+    single = GossipRound(adj, x, 0.05, encode=_oracle_encode, fold=_oracle_fold)
+    for r in range(2):
+        _train(single, r)
+        single.step()
+    _, _, per = shard(len(adj), world, 0)
+    k = round(0.05 * n)
+    budget = per * world * k * 8 - 1 if auto else None  # one byte short of the all-gather
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29300 + (os.getpid() % 1000) + 11 * world + (5 if auto else 0)
+    procs = [ctx.Process(target=_peer_worker, args=(r, world, port, n, path, q, budget))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, lo, xs, n_recv in got:
+        assert lo is not None, xs
+        assert n_recv <= per * (world - 1)
+        np.testing.assert_array_equal(xs.view(np.uint32),
+                                      single.x.numpy()[lo:lo + xs.shape[0]].view(np.uint32))
+
+
+def test_peer_plan_counts():
+    """The peer plan of 96_regular.edges over 8 ranks: every rank's receive rows are exactly the
+    remote neighbours of its nodes, and the send and receive splits of all ranks agree."""
+    from decentralizepy_amd.gossip import GossipRound, read_edges, shard
+
+    class _Plan(GossipRound):
+        def __init__(self, adj, rank, world, k):  # the plan alone (no engine state)
+            self.adj, self.n_nodes, self.world, self.rank, self.k = adj, len(adj), world, rank, k
+            self.lo, self.hi, self.per = shard(self.n_nodes, world, rank)
+            self._peer_plan()
+
+    adj = read_edges(EDGES96)
+    plans = [_Plan(adj, r, 8, 10) for r in range(8)]
+    for r, p in enumerate(plans):
+        want = {q for d in range(p.lo, p.hi) for q in adj[d] if not p.lo <= q < p.hi}
+        assert set(p._peer_row) == want
+        assert p._peer_n_recv < 84  # the all-gather gives every rank 84 remote payloads
+        for s, ps in enumerate(plans):
+            assert p._peer_out_splits[s] == ps._peer_in_splits[r]

@@ -28,6 +28,29 @@ def test_gossip_round_device_matches_oracle(dev, path, n, alpha):
         np.testing.assert_array_equal(eng.counter.cpu().numpy(), ref.counter.numpy())
 
 
+@pytest.mark.parametrize("path,n,alpha", [(EDGES16, 300_000, 0.01), (EDGES96, 40_000, 0.02)])
+def test_peer_exchange_device_matches_oracle(dev, path, n, alpha):
+    """The peer exchange's device fold tables (local neighbours' payloads read in place from the
+    send rows, the guarded one-launch fold) on one rank, bit-exact with the oracle round (the
+    multi-rank all_to_all_single is covered with gloo, tests/test_cpu_gossip.py)."""
+    from decentralizepy_amd.gossip import GossipRound, read_edges
+    adj = read_edges(path)
+    x = _models(len(adj), n)
+    ref = GossipRound(adj, x, alpha, encode=_oracle_encode, fold=_oracle_fold)
+    eng = GossipRound(adj, x.to(dev), alpha, exchange="peer")
+    assert eng.exchange_mode == "peer" and eng._peer_n_recv == 0
+    for r in range(2):
+        _train(ref, r)
+        g = torch.Generator().manual_seed(100 + r)
+        eng.x += (0.01 * torch.randn(len(adj), n, generator=g)).to(dev)
+        ref.step()
+        eng.step()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(eng.x.cpu().numpy().view(np.uint32),
+                                      ref.x.numpy().view(np.uint32))
+        np.testing.assert_array_equal(eng.counter.cpu().numpy(), ref.counter.numpy())
+
+
 @pytest.mark.parametrize("path,n,alpha,budget", [(EDGES16, 200_003, 0.01, 1),
                                                   (EDGES96, 30_000, 0.05, 1),
                                                   (EDGES96, 30_000, 0.05, None)])
