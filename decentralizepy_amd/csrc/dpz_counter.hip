@@ -71,7 +71,8 @@ __global__ void __launch_bounds__(256) counter_sweep_kernel(int32_t* __restrict_
                                                             const SegTab tab, int64_t tiles,
                                                             const int32_t* __restrict__ bounds) {
   __shared__ int32_t tile[CT];
-  __shared__ int64_t sb[CSEGS], se[CSEGS];
+  __shared__ int64_t sb[CSEGS];
+  __shared__ int32_t pre[CSEGS + 1];  // the tile's entries of segments < r: pre[r]
   const int m = tab.m;
   const int t = threadIdx.x;
   const int64_t t0 = (int64_t)blockIdx.x * CT;
@@ -97,18 +98,48 @@ __global__ void __launch_bounds__(256) counter_sweep_kernel(int32_t* __restrict_
   } else {
     for (int i = t; i < cnt; i += 256) tile[i] = counter[t0 + i];
   }
-  if (t < m) {
-    sb[t] = lo;
-    se[t] = hi;
+  // the tile's entries of all segments as ONE index space [0, total): a wave scan of the
+  // per-segment counts (m <= 64), then every thread takes entries j, j + 256, ... — the ring
+  // loads are independent (a loop per segment had put one load round trip per segment in
+  // series: 64 rounds, ~50 us per launch)
+  if (t < 64) {
+    const int32_t c = t < m ? (int32_t)(hi - lo) : 0;
+    int32_t v = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t u = __shfl_up(v, d, 64);
+      if (t >= d) v += u;
+    }
+    if (t < m) {
+      sb[t] = lo;
+      pre[t] = v - c;
+    }
+    if (t == 63) pre[m] = v;
   }
   __syncthreads();
-  for (int r = 0; r < m; ++r) {
-    const int64_t b = sb[r], e = se[r];
-    for (int64_t j = b + t; j < e; j += 256) {
+  const int32_t total = pre[m];
+  constexpr int U = 4;
+  for (int32_t j0 = t; j0 < total; j0 += 256 * U) {
+    int32_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int32_t j = j0 + 256 * u;
+      v[u] = -1;
+      if (j < total) {
+        int a = 0, b = m - 1;  // the segment r with pre[r] <= j < pre[r + 1]
+        while (a < b) {
+          const int c = (a + b + 1) >> 1;
+          if (pre[c] <= j) a = c; else b = c - 1;
+        }
+        v[u] = ring[sb[a] + (j - pre[a])];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
       // inside the tile for an ascending segment; checked all the same (a caller's unsorted
       // segment must not write outside the tile)
-      const int64_t i = (int64_t)ring[j] - t0;
-      if (i >= 0 && i < cnt) atomicAdd(&tile[i], 1);
+      const int64_t i = (int64_t)v[u] - t0;
+      if (v[u] >= 0 && i >= 0 && i < cnt) atomicAdd(&tile[i], 1);
     }
   }
   __syncthreads();
