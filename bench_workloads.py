@@ -542,13 +542,18 @@ def shard_case(dev, rank, world, dist, n=67_108_864, alpha=0.001, steps=20, warm
     return res
 
 
+def _lib_native(n):
+    from decentralizepy_amd import _lib
+    return _lib.lib().dpz_fft_native(int(n))
+
+
 def fft_case(dev, n=11_000_000, alpha=0.01, npay=3, steps=30, warmup=5, seed=9, cpu=True):
     """The FFT sharing plugin's device round (reference sharing/JWINS/FFT.py:132-302) on an
-    N-parameter model: encode = x - x0, rfft(x) and rfft(x - x0) (hipFFT), |change| (complex, HIP),
-    top-k on it with the counter, complex values gathered from rfft(x); decode = npay complex
-    payloads folded (Metro-Hastings) over the (re, im) pairs, irfft (hipFFT) + 1/n.  The step
-    rate is reported on the GiB/s metric (4N bytes of model per step) with the HIP kernels'
-    average durations; the hipFFT kernels are library launches outside the per-kernel table."""
+    N-parameter model: encode = x - x0, rfft(x) and rfft(x - x0) (native kernels), |change|
+    (complex), top-k on it with the counter, complex values gathered from rfft(x); decode = npay
+    complex payloads folded (Metro-Hastings) over the (re, im) pairs, irfft (1/n in its last
+    pass).  The step rate is reported on the GiB/s metric (4N bytes of model per step) with the
+    kernels' average durations, and the transforms alone against the HBM roofline."""
     from decentralizepy_amd import codec
     m = n // 2 + 1
     k = round(alpha * m)
@@ -591,11 +596,45 @@ def fft_case(dev, n=11_000_000, alpha=0.01, npay=3, steps=30, warmup=5, seed=9, 
             step(i)
         torch.cuda.synchronize()
     kern = {nm: round(ms / c * 1e3, 2) for nm, (ms, c) in kt.result.items()}
+    # the transforms alone (event pairs around `reps` back-to-back calls on rotated inputs):
+    # algorithmic bytes = the n reals read + the n / 2 + 1 complex written (and back for irfft)
+    reps = 20
+    spec = [codec.rfft(d["x"], workspace=ws) for d in sets]
+    buf = [torch.empty_like(s_) for s_ in spec]
+
+    def t_of(fn):
+        fn(0)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(reps):
+            fn(i)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e3
+
+    def inv(i):
+        buf[i % R].copy_(spec[i % R])
+        codec.irfft(buf[i % R], n, out=sets[i % R]["out"], workspace=ws)
+
+    t_copy = t_of(lambda i: buf[i % R].copy_(spec[i % R]))
+    t_r = t_of(lambda i: codec.rfft(sets[i % R]["x"], out=spec[i % R], workspace=ws))
+    t_i = t_of(inv) - t_copy
+    ab = 4 * n + 8 * m
+    native = bool(_lib_native(n))
     res = dict(workload=f"FFT plugin round: rfft top-k encode + {npay}-payload complex fold + "
                         f"irfft of an N={n} model (M={m} coefficients)",
                n=n, m=m, k=k, alpha=alpha, value=4 * n / t / 2 ** 30, ms_per_step=t * 1e3,
-               note="hipFFT transforms are not in the per-kernel table (library kernels)",
-               kernels_avg_us=kern)
+               transforms=("native mixed-radix Stockham kernels (csrc/dpz_fft.hip)" if native
+                           else "hipFFT fallback (a prime factor above 4096)"),
+               kernels_avg_us=kern,
+               rfft_us=round(t_r, 2), irfft_us=round(t_i, 2),
+               roofline={"bound": "hbm", "kernel": "rfft (all its launches)",
+                         "alg_bytes": ab, "achieved_GBps": round(ab / t_r / 1e3, 1),
+                         "peak_GBps": 8000.0, "frac": round(ab / t_r / 1e3 / 8000.0, 4),
+                         "irfft_frac": round(ab / t_i / 1e3 / 8000.0, 4),
+                         "note": "algorithmic bytes 4N read + 8(N/2+1) written; the passes move "
+                                 "each complex element once per pass (read + write)"})
     if cpu:
         def make():
             # the reference's FFT round on the host (sharing/JWINS/FFT.py:12-26 rfft transformer,

@@ -159,6 +159,7 @@ SIGNATURES = {
                               _c_void_p, _size, _c_void_p]),
     "dpz_fpz_decode": (_int, [_c_void_p, _i64, _i64, _int, _c_void_p, _c_void_p, _c_void_p]),
     "dpz_fft_workspace_bytes": (_i64, [_i64]),
+    "dpz_fft_native": (_int, [_i64]),
     "dpz_rfft": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p, _size, _c_void_p]),
     "dpz_irfft": (_int, [_c_void_p, _i64, _c_void_p, _c_void_p, _size, _c_void_p]),
     "dpz_cplx_key": (_int, [_c_void_p, _c_void_p, _int, _i64, _c_void_p, _c_void_p]),

@@ -20,7 +20,7 @@ __all__ = ["DPZ_ACC_NONE", "DPZ_ACC_ACCUMULATE", "DPZ_ACC_ADD", "DPZ_EW_SUB", "D
            "topk_threshold", "mask_below_threshold", "elementwise",
            "topk_complete", "decode_average", "replace", "wavedec_len", "wavedec", "waverec",
            "pack_fp16", "unpack_fp16", "elias_encode", "elias_decode", "elias_decode_async",
-           "KernelTimer", "NodeStepBatch", "topk_sticky_status", "rfft", "irfft", "cplx_key",
+           "KernelTimer", "NodeStepBatch", "topk_sticky_status", "rfft", "irfft", "fft_native", "cplx_key",
            "cplx_gather", "cplx_pair_indices", "lz4_compress", "lz4_decompress", "lz4_frame_info",
            "delta_i32", "running_sum_i32", "mask_words", "topk_encode_sliced", "counter_unslice",
            "counter_slice", "rewind_apply", "counter_flush"]
@@ -854,8 +854,9 @@ def _fft_ws(n, workspace, device):
 
 
 def rfft(x, out=None, workspace=None):
-    """``torch.fft.rfft(x)`` of a device fp32 vector through hipFFT (reference
-    sharing/JWINS/FFT.py:12-25); returns complex64[n // 2 + 1]."""
+    """``torch.fft.rfft(x)`` of a device fp32 vector (reference sharing/JWINS/FFT.py:12-25):
+    the native mixed-radix kernels, or hipFFT for a size with a prime factor above 4096
+    (``fft_native(n)``); returns complex64[n // 2 + 1]."""
     _require(x, torch.float32, "x")
     n = x.numel()
     if out is None:
@@ -867,6 +868,11 @@ def rfft(x, out=None, workspace=None):
     rc = _lib.lib().dpz_rfft(_ptr(x), n, _ptr(out), _ptr(ws), ws.numel(), _stream(x.device))
     check(rc, "dpz_rfft")
     return out
+
+
+def fft_native(n):
+    """True when rfft / irfft of n reals run this build's kernels (else hipFFT)."""
+    return bool(_lib.lib().dpz_fft_native(int(n)))
 
 
 def irfft(coeffs, n, out=None, workspace=None):

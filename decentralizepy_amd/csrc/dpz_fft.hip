@@ -1,5 +1,6 @@
-// Frequency-domain codec of the FFT sharing plugin: real FFTs through hipFFT (rocFFT), and the
-// complex-coefficient kernels around the shared top-k / fold kernels.
+// Frequency-domain codec of the FFT sharing plugin: the real FFTs (hand-written mixed-radix
+// Stockham passes, below) and the complex-coefficient kernels around the shared top-k / fold
+// kernels.
 //
 // Replaces (reference sacs-epfl/decentralizepy, src/decentralizepy/):
 //   sharing/JWINS/FFT.py:12-25     change_transformer_fft: torch.fft.rfft(x)
@@ -10,18 +11,32 @@
 //   sharing/JWINS/FFT.py:282-299   topkf = flat_fft.clone(); topkf[indices] = params  (fold input:
 //                                  complex entries become float pairs for dpz_decode_average)
 //
-// The transforms are library calls (like hipBLASLt for a plain GEMM): a mixed-radix FFT for an
-// arbitrary model size is rocFFT's job.  Plans are cached per (device, n, direction) with
-// auto-allocation off; the caller passes the work area (dpz_fft_workspace_bytes), so the only
-// device memory the library owns is rocFFT's per-plan twiddle tables.  Complex data is
-// interleaved fp32 (re, im) = torch.complex64's layout.
+// Real FFT of n reals (round 6, native).  Even n: the n reals ARE M = n / 2 complex values
+// z[j] = x[2j] + i x[2j+1]; Z = DFT_M(z), then one pass turns Z into the n / 2 + 1 coefficients
+// X[k] = ((Z[k] + conj Z[M-k]) - i W_n^k (Z[k] - conj Z[M-k])) / 2 (pairs k, M - k in place); the
+// inverse runs the same steps backwards (Im X[0], Im X[M] ignored, as pocketfft's c2r does) with
+// 1/n folded into the last pass.  Odd n: a complex DFT of length n over (x, 0) / the Hermitian
+// extension.  DFT_L is a Stockham autosort over GLOBAL passes of radix R <= 256 (the prime factors
+// packed into as few passes as fit; a prime in 257..4096 gets a pass of its own): a block owns B
+// consecutive columns j of a pass (B * R <= 4096 complex, B <= 16: 128-byte rows), loads the
+// column elements in[j + r L / R] (row r: B consecutive complex), applies the pass twiddle
+// W_{pR}^{r (j mod p)}, runs the column DFTs of length R in LDS as sub-passes of radix 2 / 4 / 8 /
+// 3 / 5 / 7 / 11 / 13 (register butterflies; any other prime one output per thread), and stores
+// out[(j / p) p R + (j mod p) + m p] (consecutive j: consecutive addresses).  Twiddles come from a
+// two-level table W_nt^e = hi[e >> 11] * lo[e & 2047] (fp64-computed, rounded to fp32; cached per
+// size like a plan).  Sizes with a prime factor above 4096 go to hipFFT (rocFFT) instead.
 #include <hipfft/hipfft.h>
 
-#include <mutex>
+#include <algorithm>
+#include <cmath>
+#include <functional>
 #include <map>
+#include <mutex>
 #include <tuple>
+#include <vector>
 
 #include "dpz_common.h"
+#include "dpz_knobs.h"
 #include "dpz_topk.h"
 
 namespace dpz {
@@ -89,6 +104,545 @@ static unsigned grid_for(int64_t n) {
   return (unsigned)g;
 }
 
+// ---- native mixed-radix FFT -------------------------------------------------------------------
+constexpr int FT_THREADS = 256;
+constexpr int FT_ELEMS = 4096;  // B * R complex per block (two LDS buffers of B * (R + 1))
+constexpr int FT_MAXR = 4096;   // the largest prime a pass takes (larger: hipFFT)
+constexpr int FT_PACK = 256;    // the largest packed radix of a pass
+constexpr int FT_MAXPASS = 12;
+constexpr int FT_MAXSUB = 12;
+constexpr int FT_LO = 2048;     // two-level twiddle table: W^e = hi[e >> 11] * lo[e & 2047]
+
+// roots of unity W_nt^e = exp(-2 pi i e / nt), e < nt (conjugated for the inverse)
+struct FtTw {
+  const float2* lo;
+  const float2* hi;
+  uint32_t nt;
+};
+
+__device__ __forceinline__ float2 ft_cmul(float2 a, float2 b) {
+  return make_float2(fmaf(a.x, b.x, -(a.y * b.y)), fmaf(a.x, b.y, a.y * b.x));
+}
+
+__device__ __forceinline__ float2 ft_root(const FtTw& t, uint32_t e, bool inv) {
+  const float2 h = t.hi[e >> 11], l = t.lo[e & (FT_LO - 1)];
+  float2 w = ft_cmul(h, l);
+  if (inv) w.y = -w.y;
+  return w;
+}
+
+struct FtPass {
+  const float2* in;     // complex input (load modes 0 / 2)
+  const float* in_re;   // real input (load mode 1)
+  float2* out;          // complex output (store modes 0 / 1 / 3)
+  float* out_re;        // real output (store mode 2)
+  int64_t L;            // transform length
+  int64_t S;            // L / R: columns (and the input row stride)
+  int64_t p;            // product of the earlier passes' radices
+  int R, B, RP;         // radix, columns per block (a power of two <= 16), LDS column pitch
+  int nsub;
+  int q[FT_MAXSUB];     // the LDS sub-passes' radices (product R)
+  int load_mode;        // 0 complex, 1 real (x, 0), 2 Hermitian extension of n_aux / 2 + 1 values
+  int store_mode;       // 0 complex, 1 complex * scale, 2 real part * scale, 3 indices < n_aux only
+  int64_t n_aux;
+  float scale;
+  int inv;
+  FtTw tw;
+};
+
+__device__ __forceinline__ float2 ft_load(const FtPass& a, int64_t i) {
+  if (a.load_mode == 1) return make_float2(a.in_re[i], 0.0f);
+  if (a.load_mode == 2) {
+    const int64_t h = a.n_aux / 2 + 1;
+    if (i < h) {
+      const float2 v = a.in[i];
+      return i == 0 ? make_float2(v.x, 0.0f) : v;
+    }
+    const float2 v = a.in[a.n_aux - i];
+    return make_float2(v.x, -v.y);
+  }
+  return a.in[i];
+}
+
+__device__ __forceinline__ void ft_store(const FtPass& a, int64_t o, float2 v) {
+  switch (a.store_mode) {
+    case 1: a.out[o] = make_float2(v.x * a.scale, v.y * a.scale); break;
+    case 2: a.out_re[o] = v.x * a.scale; break;
+    case 3: if (o < a.n_aux) a.out[o] = v; break;
+    default: a.out[o] = v;
+  }
+}
+
+// -i z (forward) / +i z (inverse)
+__device__ __forceinline__ float2 ft_mi(float2 z, bool inv) {
+  return inv ? make_float2(-z.y, z.x) : make_float2(z.y, -z.x);
+}
+
+__device__ __forceinline__ void ft_dft4(float2& v0, float2& v1, float2& v2, float2& v3, bool inv) {
+  const float2 a = make_float2(v0.x + v2.x, v0.y + v2.y), b = make_float2(v0.x - v2.x, v0.y - v2.y);
+  const float2 c = make_float2(v1.x + v3.x, v1.y + v3.y);
+  const float2 d = ft_mi(make_float2(v1.x - v3.x, v1.y - v3.y), inv);
+  v0 = make_float2(a.x + c.x, a.y + c.y);
+  v2 = make_float2(a.x - c.x, a.y - c.y);
+  v1 = make_float2(b.x + d.x, b.y + d.y);
+  v3 = make_float2(b.x - d.x, b.y - d.y);
+}
+
+template <int Q>
+__device__ __forceinline__ void ft_dft(float2 (&v)[Q], const float2 (&w)[Q], bool inv) {
+  if constexpr (Q == 2) {
+    const float2 a = v[0], b = v[1];
+    v[0] = make_float2(a.x + b.x, a.y + b.y);
+    v[1] = make_float2(a.x - b.x, a.y - b.y);
+  } else if constexpr (Q == 4) {
+    ft_dft4(v[0], v[1], v[2], v[3], inv);
+  } else if constexpr (Q == 8) {
+    // two radix-4 DFTs (even / odd inputs), then y[m] = E[m] + W_8^m O[m], y[m+4] = E[m] - ...
+    float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6], o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+    ft_dft4(e0, e1, e2, e3, inv);
+    ft_dft4(o0, o1, o2, o3, inv);
+    constexpr float h = 0.70710678118654752f;
+    const float2 t1 = inv ? make_float2(h * (o1.x - o1.y), h * (o1.x + o1.y))
+                          : make_float2(h * (o1.x + o1.y), h * (o1.y - o1.x));
+    const float2 t2 = ft_mi(o2, inv);
+    const float2 t3 = inv ? make_float2(-h * (o3.x + o3.y), h * (o3.x - o3.y))
+                          : make_float2(h * (o3.y - o3.x), -h * (o3.x + o3.y));
+    v[0] = make_float2(e0.x + o0.x, e0.y + o0.y);
+    v[4] = make_float2(e0.x - o0.x, e0.y - o0.y);
+    v[1] = make_float2(e1.x + t1.x, e1.y + t1.y);
+    v[5] = make_float2(e1.x - t1.x, e1.y - t1.y);
+    v[2] = make_float2(e2.x + t2.x, e2.y + t2.y);
+    v[6] = make_float2(e2.x - t2.x, e2.y - t2.y);
+    v[3] = make_float2(e3.x + t3.x, e3.y + t3.y);
+    v[7] = make_float2(e3.x - t3.x, e3.y - t3.y);
+  } else {
+    // odd prime: y[m] / y[Q-m] from a_r = v_r + v_{Q-r}, b_r = v_r - v_{Q-r} and W_Q^{mr} = (C, D):
+    // v_r W^{mr} + v_{Q-r} W^{-mr} = C a_r + i D b_r
+    constexpr int H = (Q - 1) / 2;
+    float2 A[H + 1], Bv[H + 1];
+    float2 y0 = v[0];
+#pragma unroll
+    for (int r = 1; r <= H; ++r) {
+      A[r] = make_float2(v[r].x + v[Q - r].x, v[r].y + v[Q - r].y);
+      Bv[r] = make_float2(v[r].x - v[Q - r].x, v[r].y - v[Q - r].y);
+      y0 = make_float2(y0.x + A[r].x, y0.y + A[r].y);
+    }
+    float2 out[Q];
+    out[0] = y0;
+#pragma unroll
+    for (int m = 1; m <= H; ++m) {
+      float cr = v[0].x, ci = v[0].y, dr = 0.0f, di = 0.0f;
+#pragma unroll
+      for (int r = 1; r <= H; ++r) {
+        const float2 wr = w[(m * r) % Q];
+        cr = fmaf(wr.x, A[r].x, cr);
+        ci = fmaf(wr.x, A[r].y, ci);
+        dr = fmaf(-wr.y, Bv[r].y, dr);
+        di = fmaf(wr.y, Bv[r].x, di);
+      }
+      out[m] = make_float2(cr + dr, ci + di);
+      out[Q - m] = make_float2(cr - dr, ci - di);
+    }
+    (void)inv;
+#pragma unroll
+    for (int m = 0; m < Q; ++m) v[m] = out[m];
+  }
+}
+
+// one LDS sub-pass of radix Q over the block's B columns of length R: butterfly i of a column
+// takes elements i + r R / Q, twiddles them by W_{pp Q}^{r (i mod pp)}, and writes the outputs
+// to (i / pp) pp Q + (i mod pp) + m pp
+template <int Q>
+__device__ __forceinline__ void ft_sub(const float2* src, float2* dst, int B, int R, int RP, int pp,
+                                       const FtTw& tw, bool inv) {
+  const int nb = R / Q;
+  const uint32_t sm = tw.nt / (uint32_t)(pp * Q);
+  float2 w[Q];
+  if constexpr (Q != 2 && Q != 4 && Q != 8) {
+#pragma unroll
+    for (int m = 0; m < Q; ++m) w[m] = ft_root(tw, (uint32_t)m * (tw.nt / Q), inv);
+  }
+  for (int u = threadIdx.x; u < B * nb; u += FT_THREADS) {
+    const int c = u / nb, i = u - c * nb;
+    const int k = i % pp;
+    const float2* s = src + c * RP + i;
+    float2 v[Q];
+#pragma unroll
+    for (int r = 0; r < Q; ++r) v[r] = s[r * nb];
+    if (k) {
+#pragma unroll
+      for (int r = 1; r < Q; ++r) v[r] = ft_cmul(v[r], ft_root(tw, (uint32_t)(r * k) * sm, inv));
+    }
+    ft_dft<Q>(v, w, inv);
+    float2* d = dst + c * RP + (i / pp) * pp * Q + k;
+#pragma unroll
+    for (int m = 0; m < Q; ++m) d[m * pp] = v[m];
+  }
+}
+
+// any other prime radix: one output per thread, O(q) terms
+__device__ __forceinline__ void ft_sub_any(const float2* src, float2* dst, int B, int R, int RP,
+                                           int pp, int q, const FtTw& tw, bool inv) {
+  const int nb = R / q;
+  const uint32_t sm = tw.nt / (uint32_t)(pp * q), sq = tw.nt / (uint32_t)q;
+  for (int u = threadIdx.x; u < B * R; u += FT_THREADS) {
+    const int c = u / R, rem = u - c * R;
+    const int m = rem / nb, i = rem - m * nb;
+    const int k = i % pp;
+    const float2* s = src + c * RP + i;
+    float accr = 0.0f, acci = 0.0f;
+    for (int r = 0; r < q; ++r) {
+      const uint64_t e = ((uint64_t)r * k * sm + (uint64_t)((r * m) % q) * sq) % tw.nt;
+      const float2 z = ft_cmul(s[r * nb], ft_root(tw, (uint32_t)e, inv));
+      accr += z.x;
+      acci += z.y;
+    }
+    dst[c * RP + (i / pp) * pp * q + k + m * pp] = make_float2(accr, acci);
+  }
+}
+
+__global__ void __launch_bounds__(FT_THREADS) ft_pass_kernel(FtPass a) {
+  extern __shared__ float2 ft_lds[];
+  const int B = a.B, R = a.R, RP = a.RP;
+  const int t = threadIdx.x;
+  const int64_t j0 = (int64_t)blockIdx.x * B;
+  const int cols = (int)(a.S - j0 < B ? a.S - j0 : B);
+  float2* src = ft_lds;
+  float2* dst = ft_lds + B * RP;
+  const bool inv = a.inv != 0;
+  // load: element (c, r) = in[j0 + c + r S], twiddled; B divides the block, so a thread's column
+  // is the same for all its elements
+  {
+    const int c = t & (B - 1);
+    const int64_t j = j0 + c;
+    const uint32_t k = a.p > 1 ? (uint32_t)(j % a.p) : 0u;
+    const uint32_t twm = a.tw.nt / (uint32_t)(a.p * R);
+    if (c < cols) {
+      for (int r = t / B; r < R; r += FT_THREADS / B) {
+        float2 v = ft_load(a, j + (int64_t)r * a.S);
+        if (k && r) v = ft_cmul(v, ft_root(a.tw, (uint32_t)(((uint64_t)r * k) * twm), inv));
+        src[c * RP + r] = v;
+      }
+    }
+  }
+  __syncthreads();
+  int pp = 1;
+  for (int s = 0; s < a.nsub; ++s) {
+    const int q = a.q[s];
+    switch (q) {
+      case 2: ft_sub<2>(src, dst, B, R, RP, pp, a.tw, inv); break;
+      case 4: ft_sub<4>(src, dst, B, R, RP, pp, a.tw, inv); break;
+      case 8: ft_sub<8>(src, dst, B, R, RP, pp, a.tw, inv); break;
+      case 3: ft_sub<3>(src, dst, B, R, RP, pp, a.tw, inv); break;
+      case 5: ft_sub<5>(src, dst, B, R, RP, pp, a.tw, inv); break;
+      case 7: ft_sub<7>(src, dst, B, R, RP, pp, a.tw, inv); break;
+      case 11: ft_sub<11>(src, dst, B, R, RP, pp, a.tw, inv); break;
+      case 13: ft_sub<13>(src, dst, B, R, RP, pp, a.tw, inv); break;
+      default: ft_sub_any(src, dst, B, R, RP, pp, q, a.tw, inv);
+    }
+    __syncthreads();
+    float2* x = src;
+    src = dst;
+    dst = x;
+    pp *= q;
+  }
+  // store: column j's output m to (j / p) p R + (j mod p) + m p; consecutive threads take
+  // consecutive columns (p > 1) or consecutive outputs of one column (p = 1: a contiguous run)
+  if (a.p == 1) {
+    for (int e = t; e < cols * R; e += FT_THREADS) {
+      const int c = e / R, m = e - c * R;
+      ft_store(a, (j0 + c) * R + m, src[c * RP + m]);
+    }
+  } else {
+    const int c = t & (B - 1);
+    const int64_t j = j0 + c;
+    const int64_t base = (j / a.p) * a.p * R + j % a.p;
+    if (c < cols)
+      for (int m = t / B; m < R; m += FT_THREADS / B) ft_store(a, base + (int64_t)m * a.p, src[c * RP + m]);
+  }
+}
+
+// even n, forward: X[k] = ((Z[k] + conj Z[M-k]) - i W_n^k (Z[k] - conj Z[M-k])) / 2 for the pair
+// (k, M - k), k <= M / 2; Z read from `z` (may equal out)
+__global__ void __launch_bounds__(256) ft_r2c_post_kernel(const float2* z, float2* out, int64_t M,
+                                                          FtTw tw) {
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k <= M / 2; k += (int64_t)gridDim.x * 256) {
+    if (k == 0) {
+      const float2 z0 = z[0];
+      out[0] = make_float2(z0.x + z0.y, 0.0f);
+      out[M] = make_float2(z0.x - z0.y, 0.0f);
+      continue;
+    }
+    const float2 a = z[k], b = z[M - k];
+    auto one = [&](float2 p, float2 q, int64_t kk) {  // p = Z[kk], q = Z[M - kk]
+      const float2 e = make_float2(p.x + q.x, p.y - q.y);  // Z[kk] + conj Z[M-kk]
+      const float2 d = make_float2(p.x - q.x, p.y + q.y);  // Z[kk] - conj Z[M-kk]
+      const float2 o = ft_mi(ft_cmul(ft_root(tw, (uint32_t)kk, false), d), false);
+      return make_float2(0.5f * (e.x + o.x), 0.5f * (e.y + o.y));
+    };
+    const float2 xk = one(a, b, k);
+    const float2 xm = one(b, a, M - k);
+    out[k] = xk;
+    if (M - k != k) out[M - k] = xm;
+  }
+}
+
+// even n, inverse: Z[k] = (X[k] + conj X[M-k]) + i W_n^{-k} (X[k] - conj X[M-k]) for the pair
+// (k, M - k), Im X[0] = Im X[M] = 0 (c2r); `scale` multiplies (1 unless no pass follows)
+__global__ void __launch_bounds__(256) ft_c2r_pre_kernel(const float2* x, float2* z, int64_t M,
+                                                         FtTw tw, float scale) {
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k <= M / 2; k += (int64_t)gridDim.x * 256) {
+    float2 a = x[k], b = x[M - k];
+    if (k == 0) {
+      a.y = 0.0f;
+      b.y = 0.0f;
+    }
+    auto one = [&](float2 p, float2 q, int64_t kk) {  // p = X[kk], q = X[M - kk]
+      const float2 e = make_float2(p.x + q.x, p.y - q.y);
+      const float2 d = make_float2(p.x - q.x, p.y + q.y);
+      const float2 o = ft_mi(ft_cmul(ft_root(tw, (uint32_t)kk, true), d), true);
+      return make_float2((e.x + o.x) * scale, (e.y + o.y) * scale);
+    };
+    const float2 zk = one(a, b, k);
+    if (k == 0) {
+      z[0] = zk;
+      continue;
+    }
+    const float2 zm = one(b, a, M - k);
+    z[k] = zk;
+    if (M - k != k) z[M - k] = zm;
+  }
+}
+
+struct FtPlan {
+  int64_t L = 0;
+  int npass = 0;
+  int R[FT_MAXPASS];
+  int nsub[FT_MAXPASS];
+  int q[FT_MAXPASS][FT_MAXSUB];
+};
+
+// L = R_1 ... R_s: prime factors <= FT_PACK packed (largest first, each into the pass with the
+// smallest product that stays <= FT_PACK), larger primes (<= FT_MAXR) a pass each; false when a
+// prime exceeds FT_MAXR or the pass / sub-pass tables overflow
+static bool ft_make_plan(int64_t L, FtPlan* pl) {
+  pl->L = L;
+  pl->npass = 0;
+  if (L < 1) return false;
+  std::vector<int64_t> primes;
+  int64_t m = L;
+  for (int64_t f = 2; f * f <= m; ++f)
+    while (m % f == 0) {
+      primes.push_back(f);
+      m /= f;
+    }
+  if (m > 1) primes.push_back(m);
+  std::vector<std::vector<int>> bins;
+  std::vector<int64_t> prod;
+  std::sort(primes.begin(), primes.end(), std::greater<int64_t>());
+  for (int64_t f : primes) {
+    if (f > FT_MAXR) return false;
+    if (f > FT_PACK) {
+      bins.push_back({(int)f});
+      prod.push_back(f);
+      continue;
+    }
+    int best = -1;
+    for (size_t b = 0; b < bins.size(); ++b)
+      if (prod[b] <= FT_PACK && prod[b] * f <= FT_PACK && (best < 0 || prod[b] < prod[best])) best = (int)b;
+    if (best < 0) {
+      bins.push_back({(int)f});
+      prod.push_back(f);
+    } else {
+      bins[best].push_back((int)f);
+      prod[best] *= f;
+    }
+  }
+  if ((int)bins.size() > FT_MAXPASS) return false;
+  for (size_t b = 0; b < bins.size(); ++b) {
+    // sub-passes: the 2s as radix 8 (then 4 / 2), the odd primes as themselves
+    int twos = 0, ns = 0;
+    int qs[FT_MAXSUB];
+    for (int f : bins[b]) {
+      if (f == 2) {
+        ++twos;
+      } else {
+        if (ns == FT_MAXSUB) return false;
+        qs[ns++] = f;
+      }
+    }
+    while (twos > 0) {
+      const int take = twos >= 3 ? 3 : twos;
+      if (ns == FT_MAXSUB) return false;
+      qs[ns++] = 1 << take;
+      twos -= take;
+    }
+    pl->R[pl->npass] = (int)prod[b];
+    pl->nsub[pl->npass] = ns;
+    for (int i = 0; i < ns; ++i) pl->q[pl->npass][i] = qs[i];
+    ++pl->npass;
+  }
+  return true;
+}
+
+// twiddle tables per (device, nt), like a plan: lo[e] = W_nt^e (e < 2048), hi[h] = W_nt^(2048 h)
+struct FtTables {
+  float2* lo = nullptr;
+  float2* hi = nullptr;
+};
+static std::mutex g_ft_mu;
+static std::map<std::pair<int, uint32_t>, FtTables> g_ft_tabs;
+
+static int ft_tables(uint32_t nt, FtTw* tw) {
+  int dev = 0;
+  DPZ_HIP_TRY(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lock(g_ft_mu);
+  auto it = g_ft_tabs.find({dev, nt});
+  if (it == g_ft_tabs.end()) {
+    const size_t nhi = nt / FT_LO + 2;
+    std::vector<float2> h(FT_LO + nhi);
+    for (size_t e = 0; e < (size_t)FT_LO + nhi; ++e) {
+      const uint64_t ex = e < (size_t)FT_LO ? e : (uint64_t)(e - FT_LO) * FT_LO;
+      // angle 2 pi (ex mod nt) / nt in long double (exact reduction of the integer exponent)
+      const long double th = 2.0L * 3.14159265358979323846264338327950288L *
+                             (long double)(ex % nt) / (long double)nt;
+      h[e] = make_float2((float)cosl(th), (float)-sinl(th));
+    }
+    FtTables t;
+    float2* d = nullptr;
+    DPZ_HIP_TRY(hipMalloc(&d, h.size() * sizeof(float2)));
+    if (hipMemcpy(d, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
+      hipFree(d);
+      return DPZ_ERR_INTERNAL;
+    }
+    t.lo = d;
+    t.hi = d + FT_LO;
+    it = g_ft_tabs.emplace(std::make_pair(dev, nt), t).first;
+  }
+  tw->lo = it->second.lo;
+  tw->hi = it->second.hi;
+  tw->nt = nt;
+  return DPZ_OK;
+}
+
+static bool g_ft_lds_set = false;
+
+// the plan's passes: pass 1 reads (in, in_re, load_mode), the last writes (out, out_re,
+// store_mode, scale); the others alternate between bufA and bufB so that the last lands in out
+static int ft_run(const FtPlan& pl, const FtTw& tw, bool inv, const float2* in, const float* in_re,
+                  int load_mode, float2* out, float* out_re, int store_mode, float scale,
+                  int64_t n_aux, float2* bufA, float2* bufB, hipStream_t st) {
+  if (!g_ft_lds_set) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(ft_pass_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            2 * (FT_ELEMS + 16) * (int)sizeof(float2)) != hipSuccess)
+      return DPZ_ERR_INTERNAL;
+    g_ft_lds_set = true;
+  }
+  int64_t p = 1;
+  const float2* cur = in;
+  for (int s = 0; s < pl.npass; ++s) {
+    FtPass a{};
+    const bool first = s == 0, last = s == pl.npass - 1;
+    a.in = cur;
+    a.in_re = in_re;
+    a.load_mode = first ? load_mode : 0;
+    a.L = pl.L;
+    a.R = pl.R[s];
+    a.S = pl.L / a.R;
+    a.p = p;
+    int B = 16;
+    while (B > 1 && (B * a.R > FT_ELEMS || B > 2 * a.S)) B >>= 1;
+    a.B = B;
+    a.RP = a.R + 1;
+    a.nsub = pl.nsub[s];
+    for (int i = 0; i < a.nsub; ++i) a.q[i] = pl.q[s][i];
+    a.n_aux = n_aux;
+    a.scale = 1.0f;
+    a.inv = inv ? 1 : 0;
+    a.tw = tw;
+    float2* dst;
+    if (last) {
+      dst = out;
+      a.out_re = out_re;
+      a.store_mode = store_mode;
+      a.scale = scale;
+    } else {
+      dst = ((pl.npass - 1 - s) & 1) ? bufA : bufB;
+      a.store_mode = 0;
+    }
+    a.out = dst;
+    const int64_t blocks = (a.S + B - 1) / B;
+    const size_t lds = 2 * (size_t)B * a.RP * sizeof(float2);
+    DPZ_TIMED(DPZ_KT_FFT, st, ft_pass_kernel<<<(unsigned)blocks, FT_THREADS, lds, st>>>(a));
+    cur = dst;
+    p *= a.R;
+  }
+  return DPZ_OK;
+}
+
+// native plan of a real FFT of n reals: the complex length (M = n / 2 even, n odd) and whether
+// every prime factor is in range; workspace: M complex (even), 2 n complex (odd)
+static bool ft_native_plan(int64_t n, FtPlan* pl) {
+  if (n < 2 || n > INT32_MAX) return false;
+  if (DPZ_KNOB_INT(FFT_LIB, 0) != 0) return false;  // diagnostic build: hipFFT (A/B)
+  return ft_make_plan(n % 2 == 0 ? n / 2 : n, pl);
+}
+
+static int64_t ft_native_ws(int64_t n) {
+  return n % 2 == 0 ? (n / 2) * 8 + 256 : 2 * n * 8 + 256;
+}
+
+static float2* ft_align(void* ws, size_t off) {
+  const uintptr_t u = (reinterpret_cast<uintptr_t>(ws) + off + 255) & ~uintptr_t(255);
+  return reinterpret_cast<float2*>(u);
+}
+
+static int ft_rfft_native(const FtPlan& pl, const float* x, int64_t n, float2* out, void* ws,
+                          size_t ws_bytes, hipStream_t st) {
+  if ((int64_t)ws_bytes < ft_native_ws(n) || !ws) return DPZ_ERR_WORKSPACE;
+  FtTw tw;
+  const int rc = ft_tables((uint32_t)n, &tw);
+  if (rc != DPZ_OK) return rc;
+  if (n % 2 == 0) {
+    const int64_t M = n / 2;
+    float2* w = ft_align(ws, 0);
+    const float2* z = reinterpret_cast<const float2*>(x);
+    if (pl.npass > 0) {
+      const int r2 = ft_run(pl, tw, false, z, nullptr, 0, out, nullptr, 0, 1.0f, 0, w, out, st);
+      if (r2 != DPZ_OK) return r2;
+      z = out;
+    }
+    DPZ_TIMED(DPZ_KT_FFT, st, ft_r2c_post_kernel<<<grid_for(M / 2 + 1), 256, 0, st>>>(z, out, M, tw));
+    return DPZ_OK;
+  }
+  float2* a = ft_align(ws, 0);
+  float2* b = ft_align(ws, (size_t)n * 8 + 64);
+  return ft_run(pl, tw, false, nullptr, x, 1, out, nullptr, 3, 1.0f, n / 2 + 1, a, b, st);
+}
+
+static int ft_irfft_native(const FtPlan& pl, float2* coeffs, int64_t n, float* out, void* ws,
+                           size_t ws_bytes, hipStream_t st) {
+  if ((int64_t)ws_bytes < ft_native_ws(n) || !ws) return DPZ_ERR_WORKSPACE;
+  FtTw tw;
+  const int rc = ft_tables((uint32_t)n, &tw);
+  if (rc != DPZ_OK) return rc;
+  const float sc = 1.0f / (float)n;
+  if (n % 2 == 0) {
+    const int64_t M = n / 2;
+    float2* w = ft_align(ws, 0);
+    float2* xo = reinterpret_cast<float2*>(out);
+    // Z in place over the coefficients (pairs k, M - k), then the inverse DFT_M into out
+    DPZ_TIMED(DPZ_KT_FFT, st, ft_c2r_pre_kernel<<<grid_for(M / 2 + 1), 256, 0, st>>>(
+                                  coeffs, pl.npass > 0 ? coeffs : xo, M, tw, pl.npass > 0 ? 1.0f : sc));
+    if (pl.npass == 0) return DPZ_OK;
+    return ft_run(pl, tw, true, coeffs, nullptr, 0, xo, nullptr, 1, sc, 0, w, xo, st);
+  }
+  float2* a = ft_align(ws, 0);
+  float2* b = ft_align(ws, (size_t)n * 8 + 64);
+  return ft_run(pl, tw, true, coeffs, nullptr, 2, nullptr, out, 2, sc, n, a, b, st);
+}
+
 // ---- plan cache -------------------------------------------------------------------------------
 struct FftPlan {
   hipfftHandle h;
@@ -144,6 +698,8 @@ using namespace dpz;
 
 extern "C" int64_t dpz_fft_workspace_bytes(int64_t n) {
   if (n < 2 || n > INT32_MAX) return -1;
+  FtPlan pl;
+  if (ft_native_plan(n, &pl)) return ft_native_ws(n);
   std::lock_guard<std::mutex> lock(g_fft_mu);
   FftPlan a, b;
   if (fft_plan(n, 0, &a) != DPZ_OK || fft_plan(n, 1, &b) != DPZ_OK) return -1;
@@ -151,17 +707,29 @@ extern "C" int64_t dpz_fft_workspace_bytes(int64_t n) {
   return (int64_t)(w > 0 ? w : 0);
 }
 
+extern "C" int dpz_fft_native(int64_t n) {
+  FtPlan pl;
+  return ft_native_plan(n, &pl) ? 1 : 0;
+}
+
 extern "C" int dpz_rfft(const float* x, int64_t n, float* out, void* ws, size_t ws_bytes,
                         dpz_stream_t stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
   if (!x || !out || n < 2) return DPZ_ERR_ARG;
+  FtPlan pl;
+  if (ft_native_plan(n, &pl))
+    return ft_rfft_native(pl, x, n, reinterpret_cast<float2*>(out), ws, ws_bytes, st);
   // out-of-place R2C leaves its input untouched
-  return fft_exec(n, 0, const_cast<float*>(x), out, ws, ws_bytes, static_cast<hipStream_t>(stream));
+  return fft_exec(n, 0, const_cast<float*>(x), out, ws, ws_bytes, st);
 }
 
 extern "C" int dpz_irfft(float* coeffs, int64_t n, float* out, void* ws, size_t ws_bytes,
                          dpz_stream_t stream) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (!coeffs || !out || n < 2) return DPZ_ERR_ARG;
+  FtPlan pl;
+  if (ft_native_plan(n, &pl))
+    return ft_irfft_native(pl, reinterpret_cast<float2*>(coeffs), n, out, ws, ws_bytes, st);
   const int rc = fft_exec(n, 1, coeffs, out, ws, ws_bytes, st);
   if (rc != DPZ_OK) return rc;
   DPZ_TIMED(DPZ_KT_FFT_SCALE, st, scale_kernel<<<grid_for(n), 256, 0, st>>>(out, n, 1.0f / (float)n));

@@ -1140,10 +1140,10 @@ __device__ __forceinline__ void fold_walk_run(const FA& a, int64_t t0, int64_t t
   // (lanes past k read entry 0 and are masked when the window is used) ----
   int32_t wi[NS], wn[NS];
   float wvv[NS], wvn[NS];
-  auto load_window = [&](int p, int32_t& ix, float& vx) {
+  auto load_window = [&](int p, int32_t& ix, float& vx, int32_t at) {
     const bool live = p < np;
     const int pc = live ? p : 0;
-    const int32_t j = (live ? cur_of(p) : 0) + lane;
+    const int32_t j = (live ? at : 0) + lane;
     const int32_t kp = P_k(pc);
     const int32_t k = live ? kp : 0;
     const int32_t jc = j < k ? j : 0;
@@ -1153,11 +1153,13 @@ __device__ __forceinline__ void fold_walk_run(const FA& a, int64_t t0, int64_t t
     vx = (has ? P_val(pc) : a.local)[jc];
   };
 #pragma unroll
-  for (int p = 0; p < NS; ++p) load_window(p, wi[p], wvv[p]);
+  for (int p = 0; p < NS; ++p) load_window(p, wi[p], wvv[p], cur_of(p));
   auto tile_body = [&](int64_t tile, auto guard) {
     constexpr bool GUARD = decltype(guard)::value;
     const int64_t tlo = tile * TE;
     const int32_t tlo32 = (int32_t)tlo, thi32 = tlo32 + TE;
+    // the run's last tile issues no windows past it: they re-request this tile's entries (L2)
+    const bool more = tile + 1 < t1;
     // the ragged last tile: its vector groups past the last whole one were clamped on load
     if constexpr (GUARD && VEC) L = fw_load<false, EPL>(a.local, tlo, lane, n);
     // every slot: this tile's window start and entry count (the leading lanes below thi); the
@@ -1172,8 +1174,11 @@ __device__ __forceinline__ void fold_walk_run(const FA& a, int64_t t0, int64_t t
       if (live) set_cur(p, c0[p] + cnt[p]);
     }
 #pragma unroll
-    for (int p = 0; p < NS; ++p) load_window(p, wn[p], wvn[p]);
-    Ln = fw_load<VEC, EPL>(a.local, tlo + TE, lane, n);  // clamped past the end
+    for (int p = 0; p < NS; ++p) load_window(p, wn[p], wvn[p], more ? cur_of(p) : c0[p]);
+    // the next tile's local values; the run's last tile re-requests its own lines instead (L2
+    // hits) — a load of the tile past the run fetched 1 / tpw more model bytes from HBM
+    // (64 MiB, 3 payloads: 4 tiles per wave, PMC 97 MB fetched against 71 MB)
+    Ln = fw_load<VEC, EPL>(a.local, tile + 1 < t1 ? tlo + TE : tlo, lane, n);
     float acc[EPL], base[EPL];
 #pragma unroll
     for (int e = 0; e < EPL; ++e) {
@@ -1210,7 +1215,7 @@ __device__ __forceinline__ void fold_walk_run(const FA& a, int64_t t0, int64_t t
           if (cc < 64) break;
         }
         set_cur(p, c0[p] + c);
-        load_window(p, wn[p], wvn[p]);  // the next tile's window of this payload moved
+        load_window(p, wn[p], wvn[p], more ? cur_of(p) : c0[p]);  // this payload's next window moved
       }
       // the row is this wave's own and one wave's LDS instructions execute in order, so the
       // lanes' writes above are seen by the reads below with no wait; the scheduling barriers
@@ -1492,7 +1497,10 @@ __global__ void __launch_bounds__(256) fold_walk_groups_kernel(FoldArgs a, int64
     const int32_t tlo32 = (int32_t)tlo, thi32 = tlo32 + TE;
     // the ragged last tile: its vector groups past the last whole one were clamped on load
     if constexpr (GUARD && VEC) L = fw_load<false, EPL>(a.local, tlo, lane, n);
-    Ln = fw_load<VEC, EPL>(a.local, tlo + TE, lane, n);  // clamped past the end
+    // the next tile's local values; the run's last tile re-requests its own lines instead (L2
+    // hits) — a load of the tile past the run fetched 1 / tpw more model bytes from HBM
+    // (64 MiB, 3 payloads: 4 tiles per wave, PMC 97 MB fetched against 71 MB)
+    Ln = fw_load<VEC, EPL>(a.local, tile + 1 < t1 ? tlo + TE : tlo, lane, n);
     float acc[EPL], base[EPL];
 #pragma unroll
     for (int e = 0; e < EPL; ++e) {
@@ -2289,7 +2297,7 @@ __global__ void __launch_bounds__(FM_THREADS) __attribute__((amdgpu_waves_per_eu
     }
 #pragma unroll
     for (int j = 0; j < FM_SLOTS; ++j) load_window(j, cs[j], wn[j], wvn[j]);
-    fm_load<EPT>(a.local, tlo + TE, n, t, Ln);  // clamped past the end
+    fm_load<EPT>(a.local, tile + 1 < t1 ? tlo + TE : tlo, n, t, Ln);  // (the run's last: L2)
     // the base: every element's fold of its local value alone (the no-hit value); the elements
     // advance through the terms together (independent adds, one loop for all), while other
     // waves still set mask bits

@@ -91,7 +91,7 @@ static const char* const kNames[DPZ_KT_COUNT] = {
     "topk_exact_write", "topk_accumulate", "fold_offsets", "fold", "dwt", "idwt",
     "elias_count", "elias_scan", "elias_pack", "elias_spec", "elias_resolve", "elias_write",
     "fp16", "scatter_fill", "fpz_size", "fpz_scan", "fpz_pack", "fpz_decode", "cplx",
-    "fft_scale", "haar", "lz4", "counter_flush"};
+    "fft_scale", "haar", "lz4", "counter_flush", "fft"};
 
 extern "C" const char* dpz_kernel_name(int id) {
   return (id >= 0 && id < DPZ_KT_COUNT) ? kNames[id] : nullptr;

@@ -9,14 +9,15 @@ share: ``{params: complex64[n // 2 + 1]}``) and the same model side effects (com
 ``accumulated_changes``, ``shared_parameters_counter`` over the n // 2 + 1 coefficients).
 
 Device path per round:
-  pre-step   F(x) = rfft(x) and F(x - x0) (hipFFT; the difference by dpz_elementwise)
+  pre-step   F(x) = rfft(x) and F(x - x0) (dpz_rfft: the native mixed-radix kernels; the
+             difference by dpz_elementwise)
   encode     |change| after the accumulation step (dpz_cplx_key), the shared top-k kernels on that
              fp32 key (counter fused), complex values gathered from F(x) with the rewind fused
              (dpz_cplx_gather)                                              (FFT.py:132-211)
   averaging  the batched replace + Metro-Hastings fold over the interleaved (re, im) view of the
              coefficients (complex entries as float pairs), then irfft      (FFT.py:252-302)
 
-Parity is a tolerance parity: rocFFT and torch's CPU pocketfft round differently (DESIGN.md §6);
+Parity is a tolerance parity: an fp32 FFT rounds differently from torch's CPU pocketfft (DESIGN.md §6);
 the selection, the fold order and the bookkeeping are the reference's.
 """
 import numpy as np

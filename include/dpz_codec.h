@@ -490,7 +490,7 @@ enum {
   DPZ_KT_ELIAS_SCAN, DPZ_KT_ELIAS_PACK, DPZ_KT_ELIAS_SPEC, DPZ_KT_ELIAS_RESOLVE,
   DPZ_KT_ELIAS_WRITE, DPZ_KT_FP16, DPZ_KT_SCATTER, DPZ_KT_FPZ_SIZE, DPZ_KT_FPZ_SCAN,
   DPZ_KT_FPZ_PACK, DPZ_KT_FPZ_DECODE, DPZ_KT_CPLX, DPZ_KT_FFT_SCALE, DPZ_KT_HAAR, DPZ_KT_LZ4,
-  DPZ_KT_COUNTER, DPZ_KT_COUNT
+  DPZ_KT_COUNTER, DPZ_KT_FFT, DPZ_KT_COUNT
 };
 int dpz_timing_enable(int on);  /* also clears the accumulators */
 int dpz_timing_read(double* ms_sum, int64_t* count, int max_ids);
@@ -558,12 +558,16 @@ int dpz_fpz_decode(const uint8_t* in, int64_t nbytes, int64_t n, int precision, 
  * Replaces sharing/JWINS/FFT.py:12-25 (torch.fft.rfft), :301 (torch.fft.irfft, 1/n on the
  * inverse), :143-156 (top-k over |complex change|, flat_fft[index]), PartialModel.py:315-329 on
  * the complex change, Model.py:53-64 (complex rewind).  Complex = interleaved fp32 (re, im), the
- * torch.complex64 layout; m = n / 2 + 1 coefficients for n reals.  The transforms run in hipFFT
- * (rocFFT; plans cached per device / n / direction, the library's only device allocation is
- * rocFFT's twiddle tables); the work area is the caller's.                                      */
+ * torch.complex64 layout; m = n / 2 + 1 coefficients for n reals.  The transforms are this
+ * build's mixed-radix Stockham kernels (csrc/dpz_fft.hip) whenever every prime factor of the
+ * complex length (n / 2 for even n, n for odd) is <= 4096; other sizes fall back to hipFFT
+ * (rocFFT, plans cached per device / n / direction).  The library's device allocations are the
+ * per-size twiddle tables (and rocFFT's, on the fallback); the work area is the caller's.      */
 /* Work area for dpz_rfft / dpz_irfft of n reals (the max of both directions); -1 if unsupported
- * (n < 2 or n > 2^31 - 1).  Creates (and caches) the plans.                                      */
+ * (n < 2 or n > 2^31 - 1).  Creates (and caches) the hipFFT plans of a fallback size.            */
 int64_t dpz_fft_workspace_bytes(int64_t n);
+/* 1 when dpz_rfft / dpz_irfft of n reals run the native kernels, 0 when they fall back to hipFFT. */
+int dpz_fft_native(int64_t n);
 /* out[m complex] = rfft(x[n]).  Asynchronous on stream.                                          */
 int dpz_rfft(const float* x, int64_t n, float* out, void* ws, size_t ws_bytes, dpz_stream_t stream);
 /* out[n] = irfft(coeffs[m complex], n) with torch's "backward" normalisation (1/n).  coeffs is

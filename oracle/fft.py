@@ -14,8 +14,9 @@ Restates in numpy what the reference ``sharing/JWINS/FFT.py`` computes per round
 * ``PartialModel._post_step``  PartialModel.py:333-353  ``acc += rfft(new - prev)``
 
 The transforms are computed in float64 (numpy's pocketfft) and rounded to complex64 / float32;
-torch's CPU path runs pocketfft in float32, so this oracle — like the device path, which uses
-rocFFT — agrees with the reference to a tolerance, not bit-for-bit.  The selection, the fold order
+torch's CPU path runs pocketfft in float32, so this oracle — like the device path, whose own fp32
+mixed-radix kernels round differently again — agrees with the reference to a tolerance, not
+bit-for-bit.  The selection, the fold order
 (each complex entry as its (re, im) fp32 pair, one rounding per operation) and the bookkeeping
 are the reference's.
 """

@@ -363,7 +363,7 @@ def sharing_section(path, to_build=True):
     return package, cls, sec
 
 
-# ---- FFT plugin (tolerance parity: rocFFT / numpy vs torch's CPU pocketfft) -----------------------
+# ---- FFT plugin (tolerance parity: the device fp32 FFT / numpy vs torch's CPU pocketfft) -----------------------
 def fft_tol(what, n, scale):
     """Absolute tolerance of an FFT-plugin quantity against the reference (torch float32
     pocketfft): 4 x the float32 FFT error bound eps * log2(n) * |x|, times sqrt(n) for the

@@ -1,7 +1,7 @@
-"""GPU: the FFT plugin (decentralizepy_amd/sharing/JWINS/FFT.py: hipFFT transforms + the HIP
+"""GPU: the FFT plugin (decentralizepy_amd/sharing/JWINS/FFT.py: the native real FFTs + the HIP
 complex-key / gather / pair-index kernels + the shared top-k and fold kernels) replays the
 reference FFT plugin's recorded rounds: exact indices and counters, complex values, accumulators
-and averaged models within scenario.fft_tol (rocFFT vs torch's CPU pocketfft)."""
+and averaged models within scenario.fft_tol (an fp32 FFT vs torch's CPU pocketfft)."""
 from collections import deque
 
 import numpy as np
@@ -57,11 +57,21 @@ def test_fft_complex_values_only_through_pass_through_float_leg(dev, tmp_path, c
             plugin.get_data_to_send(degree=1)
 
 
-@pytest.mark.parametrize("n", [4098, 1 << 20, 11_000_000])
-def test_rfft_irfft_against_numpy(dev, n):
+# native kernel sizes: even n (M = n / 2 complex) and odd n (a complex DFT of n), radices 2..13,
+# other primes (one output per thread), a prime pass of its own (683, the reference fixture's M),
+# n = 2 (no pass), and two fallbacks to hipFFT (a prime factor above 4096)
+FFT_SIZES = [(4098, True), (1 << 20, True), (11_000_000, True), (25_000_000, True),
+             (2, True), (3, True), (30030, True), (4097, True), (2 * 17 * 19 * 23, True),
+             (16_777_216, True), (100_003, False), (2 * 9839, False)]
+
+
+@pytest.mark.parametrize("n,native", FFT_SIZES)
+def test_rfft_irfft_against_numpy(dev, n, native):
     """dpz_rfft / dpz_irfft against a float64 numpy FFT (error bound as scenario.fft_tol) and the
-    round trip; sizes include a power of two and the C2 model size (2^6 5^6 11)."""
-    from decentralizepy_amd import codec
+    round trip; sizes include a power of two and the C2 model size (2^6 5^6 11).  dpz_fft_native
+    says which sizes the hand-written kernels take (the rest: hipFFT)."""
+    from decentralizepy_amd import _lib, codec
+    assert _lib.lib().dpz_fft_native(n) == int(native)
     g = torch.Generator(device=dev).manual_seed(5)
     x = torch.randn(n, device=dev, generator=g)
     f = codec.rfft(x)
@@ -70,9 +80,22 @@ def test_rfft_irfft_against_numpy(dev, n):
     scale = float(np.abs(xh).max())
     err = np.abs(f.cpu().numpy() - ref).max()
     assert err <= scenario.fft_tol("params", n, scale), err
-    back = codec.irfft(f.clone(), n)
+    # the inverse ignores Im X[0] (and Im X[n/2] for even n), as torch / pocketfft's c2r does
+    fin = f.clone()
+    fin[0] += 0.25j
+    if n % 2 == 0:
+        fin[-1] -= 0.5j
+    back = codec.irfft(fin, n)
     err2 = np.abs(back.cpu().numpy() - xh).max()
     assert err2 <= scenario.fft_tol("model", n, scale), err2
+    # an arbitrary spectrum (not the transform of a real vector) against numpy's c2r
+    spec = (torch.randn(n // 2 + 1, device=dev, generator=g)
+            + 1j * torch.randn(n // 2 + 1, device=dev, generator=g)).to(torch.complex64)
+    sh = spec.cpu().numpy().astype(np.complex128)
+    got = codec.irfft(spec.clone(), n).cpu().numpy()
+    want = np.fft.irfft(sh, n)
+    err3 = np.abs(got - want).max()
+    assert err3 <= scenario.fft_tol("model", n, float(np.abs(want).max())), err3
 
 
 def test_cplx_kernels_exact(dev):
