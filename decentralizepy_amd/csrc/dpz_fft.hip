@@ -106,7 +106,8 @@ static unsigned grid_for(int64_t n) {
 
 // ---- native mixed-radix FFT -------------------------------------------------------------------
 constexpr int FT_THREADS = 256;
-constexpr int FT_ELEMS = 4096;  // B * R complex per block (two LDS buffers of B * (R + 1))
+constexpr int FT_ELEMS = 2048;  // B * R complex per block (two LDS buffers of B * (R + 1))
+constexpr int FT_REG_ELEMS = 2048;  // tiles up to this size load / store through registers
 constexpr int FT_MAXR = 4096;   // the largest prime a pass takes (larger: hipFFT)
 constexpr int FT_PACK = 256;    // the largest packed radix of a pass
 constexpr int FT_MAXPASS = 12;
@@ -142,6 +143,7 @@ struct FtPass {
   int R, B, RP;         // radix, columns per block (a power of two <= 16), LDS column pitch
   int nsub;
   int q[FT_MAXSUB];     // the LDS sub-passes' radices (product R)
+  uint32_t mnb[FT_MAXSUB], mpp[FT_MAXSUB];  // u / (R / q) and u / pp as umulhi(u, m) (u < 2^16)
   int load_mode;        // 0 complex, 1 real (x, 0), 2 Hermitian extension of n_aux / 2 + 1 values
   int store_mode;       // 0 complex, 1 complex * scale, 2 real part * scale, 3 indices < n_aux only
   int64_t n_aux;
@@ -249,32 +251,50 @@ __device__ __forceinline__ void ft_dft(float2 (&v)[Q], const float2 (&w)[Q], boo
   }
 }
 
+// x / d for x < 2^16, d <= 4096: umulhi(x, floor(2^32 / d) + 1) (exact in that range); m = 0
+// stands for d = 1
+__device__ __forceinline__ int ft_div(int x, uint32_t m) {
+  return m ? (int)__umulhi((uint32_t)x, m) : x;
+}
+
+// W_R^e from the block's LDS table of the pass's R roots (R <= FT_PACK), else the global table
+struct FtRoots {
+  const float2* lds;  // W_R^e, e < R (nullptr: global)
+  int R;
+  uint32_t nt_over_r;
+  __device__ __forceinline__ float2 get(const FtTw& tw, int e, bool inv) const {
+    return lds ? lds[e] : ft_root(tw, (uint32_t)e * nt_over_r, inv);
+  }
+};
+
 // one LDS sub-pass of radix Q over the block's B columns of length R: butterfly i of a column
-// takes elements i + r R / Q, twiddles them by W_{pp Q}^{r (i mod pp)}, and writes the outputs
-// to (i / pp) pp Q + (i mod pp) + m pp
+// takes elements i + r R / Q, twiddles them by W_{pp Q}^{r (i mod pp)} = W_R^{r (i mod pp) R/(pp Q)},
+// and writes the outputs to (i / pp) pp Q + (i mod pp) + m pp
 template <int Q>
 __device__ __forceinline__ void ft_sub(const float2* src, float2* dst, int B, int R, int RP, int pp,
+                                       uint32_t mnb, uint32_t mpp, const FtRoots& rt,
                                        const FtTw& tw, bool inv) {
   const int nb = R / Q;
-  const uint32_t sm = tw.nt / (uint32_t)(pp * Q);
+  const int sm = R / (pp * Q);
   float2 w[Q];
   if constexpr (Q != 2 && Q != 4 && Q != 8) {
 #pragma unroll
-    for (int m = 0; m < Q; ++m) w[m] = ft_root(tw, (uint32_t)m * (tw.nt / Q), inv);
+    for (int m = 0; m < Q; ++m) w[m] = rt.get(tw, m * (R / Q), inv);
   }
   for (int u = threadIdx.x; u < B * nb; u += FT_THREADS) {
-    const int c = u / nb, i = u - c * nb;
-    const int k = i % pp;
+    const int c = ft_div(u, mnb), i = u - c * nb;
+    const int ip = ft_div(i, mpp);
+    const int k = i - ip * pp;
     const float2* s = src + c * RP + i;
     float2 v[Q];
 #pragma unroll
     for (int r = 0; r < Q; ++r) v[r] = s[r * nb];
     if (k) {
 #pragma unroll
-      for (int r = 1; r < Q; ++r) v[r] = ft_cmul(v[r], ft_root(tw, (uint32_t)(r * k) * sm, inv));
+      for (int r = 1; r < Q; ++r) v[r] = ft_cmul(v[r], rt.get(tw, r * k * sm, inv));
     }
     ft_dft<Q>(v, w, inv);
-    float2* d = dst + c * RP + (i / pp) * pp * Q + k;
+    float2* d = dst + c * RP + ip * pp * Q + k;
 #pragma unroll
     for (int m = 0; m < Q; ++m) d[m * pp] = v[m];
   }
@@ -310,15 +330,40 @@ __global__ void __launch_bounds__(FT_THREADS) ft_pass_kernel(FtPass a) {
   float2* src = ft_lds;
   float2* dst = ft_lds + B * RP;
   const bool inv = a.inv != 0;
+  // the pass's R roots W_R^e in LDS (packed passes; a lone large prime reads the global table)
+  FtRoots rt{nullptr, R, a.tw.nt / (uint32_t)R};
+  if (R <= FT_PACK) {
+    float2* tab = ft_lds + 2 * B * RP;
+    for (int e = t; e < R; e += FT_THREADS) tab[e] = ft_root(a.tw, (uint32_t)e * rt.nt_over_r, inv);
+    rt.lds = tab;
+  }
   // load: element (c, r) = in[j0 + c + r S], twiddled; B divides the block, so a thread's column
-  // is the same for all its elements
+  // is the same for all its elements.  B * R <= FT_REG_ELEMS: every element's load (and its
+  // twiddle's table loads) issued before the first is used, branch-free (an idle slot re-reads
+  // column j0's first element); larger (a lone prime pass): element by element
   {
     const int c = t & (B - 1);
     const int64_t j = j0 + c;
     const uint32_t k = a.p > 1 ? (uint32_t)(j % a.p) : 0u;
     const uint32_t twm = a.tw.nt / (uint32_t)(a.p * R);
-    if (c < cols) {
-      for (int r = t / B; r < R; r += FT_THREADS / B) {
+    const int rs = FT_THREADS / B, r0 = t / B;
+    if (B * R <= FT_REG_ELEMS) {
+      float2 v[FT_REG_ELEMS / FT_THREADS], w[FT_REG_ELEMS / FT_THREADS];
+#pragma unroll
+      for (int i = 0; i < FT_REG_ELEMS / FT_THREADS; ++i) {
+        const int r = r0 + i * rs;
+        const bool ok = c < cols && r < R;
+        v[i] = ft_load(a, ok ? j + (int64_t)r * a.S : j0);
+        const uint32_t e = ok ? (uint32_t)(((uint64_t)r * k) * twm) : 0u;
+        w[i] = ft_root(a.tw, e, inv);
+      }
+#pragma unroll
+      for (int i = 0; i < FT_REG_ELEMS / FT_THREADS; ++i) {
+        const int r = r0 + i * rs;
+        if (c < cols && r < R) src[c * RP + r] = k ? ft_cmul(v[i], w[i]) : v[i];
+      }
+    } else if (c < cols) {
+      for (int r = r0; r < R; r += rs) {
         float2 v = ft_load(a, j + (int64_t)r * a.S);
         if (k && r) v = ft_cmul(v, ft_root(a.tw, (uint32_t)(((uint64_t)r * k) * twm), inv));
         src[c * RP + r] = v;
@@ -329,15 +374,16 @@ __global__ void __launch_bounds__(FT_THREADS) ft_pass_kernel(FtPass a) {
   int pp = 1;
   for (int s = 0; s < a.nsub; ++s) {
     const int q = a.q[s];
+    const uint32_t mn = a.mnb[s], mp = a.mpp[s];
     switch (q) {
-      case 2: ft_sub<2>(src, dst, B, R, RP, pp, a.tw, inv); break;
-      case 4: ft_sub<4>(src, dst, B, R, RP, pp, a.tw, inv); break;
-      case 8: ft_sub<8>(src, dst, B, R, RP, pp, a.tw, inv); break;
-      case 3: ft_sub<3>(src, dst, B, R, RP, pp, a.tw, inv); break;
-      case 5: ft_sub<5>(src, dst, B, R, RP, pp, a.tw, inv); break;
-      case 7: ft_sub<7>(src, dst, B, R, RP, pp, a.tw, inv); break;
-      case 11: ft_sub<11>(src, dst, B, R, RP, pp, a.tw, inv); break;
-      case 13: ft_sub<13>(src, dst, B, R, RP, pp, a.tw, inv); break;
+      case 2: ft_sub<2>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+      case 4: ft_sub<4>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+      case 8: ft_sub<8>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+      case 3: ft_sub<3>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+      case 5: ft_sub<5>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+      case 7: ft_sub<7>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+      case 11: ft_sub<11>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+      case 13: ft_sub<13>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
       default: ft_sub_any(src, dst, B, R, RP, pp, q, a.tw, inv);
     }
     __syncthreads();
@@ -347,18 +393,52 @@ __global__ void __launch_bounds__(FT_THREADS) ft_pass_kernel(FtPass a) {
     pp *= q;
   }
   // store: column j's output m to (j / p) p R + (j mod p) + m p; consecutive threads take
-  // consecutive columns (p > 1) or consecutive outputs of one column (p = 1: a contiguous run)
+  // consecutive columns (p > 1) or consecutive outputs of one column (p = 1: a contiguous run);
+  // the LDS reads of a thread's outputs all issued before its stores
+  constexpr int NE = FT_REG_ELEMS / FT_THREADS;
   if (a.p == 1) {
-    for (int e = t; e < cols * R; e += FT_THREADS) {
-      const int c = e / R, m = e - c * R;
-      ft_store(a, (j0 + c) * R + m, src[c * RP + m]);
+    if (B * R <= FT_REG_ELEMS) {
+      float2 v[NE];
+#pragma unroll
+      for (int i = 0; i < NE; ++i) {
+        const int e = t + i * FT_THREADS;
+        const int c = e / R, m = e - c * R;
+        v[i] = src[(c < B ? c : 0) * RP + m];
+      }
+#pragma unroll
+      for (int i = 0; i < NE; ++i) {
+        const int e = t + i * FT_THREADS;
+        const int c = e / R, m = e - c * R;
+        if (c < cols) ft_store(a, (j0 + c) * R + m, v[i]);
+      }
+    } else {
+      for (int e = t; e < cols * R; e += FT_THREADS) {
+        const int c = e / R, m = e - c * R;
+        ft_store(a, (j0 + c) * R + m, src[c * RP + m]);
+      }
     }
   } else {
     const int c = t & (B - 1);
     const int64_t j = j0 + c;
     const int64_t base = (j / a.p) * a.p * R + j % a.p;
-    if (c < cols)
-      for (int m = t / B; m < R; m += FT_THREADS / B) ft_store(a, base + (int64_t)m * a.p, src[c * RP + m]);
+    const int rs = FT_THREADS / B, m0 = t / B;
+    if (B * R <= FT_REG_ELEMS) {
+      float2 v[NE];
+#pragma unroll
+      for (int i = 0; i < NE; ++i) {
+        const int m = m0 + i * rs;
+        v[i] = src[c * RP + (m < R ? m : 0)];
+      }
+      if (c < cols) {
+#pragma unroll
+        for (int i = 0; i < NE; ++i) {
+          const int m = m0 + i * rs;
+          if (m < R) ft_store(a, base + (int64_t)m * a.p, v[i]);
+        }
+      }
+    } else if (c < cols) {
+      for (int m = m0; m < R; m += rs) ft_store(a, base + (int64_t)m * a.p, src[c * RP + m]);
+    }
   }
 }
 
@@ -535,7 +615,7 @@ static int ft_run(const FtPlan& pl, const FtTw& tw, bool inv, const float2* in, 
   if (!g_ft_lds_set) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(ft_pass_kernel),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            2 * (FT_ELEMS + 16) * (int)sizeof(float2)) != hipSuccess)
+                            160 * 1024) != hipSuccess)
       return DPZ_ERR_INTERNAL;
     g_ft_lds_set = true;
   }
@@ -551,12 +631,22 @@ static int ft_run(const FtPlan& pl, const FtTw& tw, bool inv, const float2* in, 
     a.R = pl.R[s];
     a.S = pl.L / a.R;
     a.p = p;
-    int B = 16;
-    while (B > 1 && (B * a.R > FT_ELEMS || B > 2 * a.S)) B >>= 1;
+    // columns per block: B * R <= FT_ELEMS (diagnostic knobs DPZ_FFT_ELEMS / DPZ_FFT_BMAX)
+    const int elems = (int)DPZ_KNOB_INT(FFT_ELEMS, FT_ELEMS);
+    int B = (int)DPZ_KNOB_INT(FFT_BMAX, 16);
+    if (B < 1 || B > 16 || (B & (B - 1))) B = 16;
+    while (B > 1 && (B * a.R > elems || B > 2 * a.S)) B >>= 1;
     a.B = B;
     a.RP = a.R + 1;
     a.nsub = pl.nsub[s];
-    for (int i = 0; i < a.nsub; ++i) a.q[i] = pl.q[s][i];
+    int pp = 1;
+    for (int i = 0; i < a.nsub; ++i) {
+      a.q[i] = pl.q[s][i];
+      const uint64_t nb = (uint64_t)(a.R / a.q[i]);
+      a.mnb[i] = nb == 1 ? 0u : (uint32_t)((1ull << 32) / nb + 1);
+      a.mpp[i] = pp == 1 ? 0u : (uint32_t)((1ull << 32) / (uint64_t)pp + 1);
+      pp *= a.q[i];
+    }
     a.n_aux = n_aux;
     a.scale = 1.0f;
     a.inv = inv ? 1 : 0;
@@ -573,7 +663,7 @@ static int ft_run(const FtPlan& pl, const FtTw& tw, bool inv, const float2* in, 
     }
     a.out = dst;
     const int64_t blocks = (a.S + B - 1) / B;
-    const size_t lds = 2 * (size_t)B * a.RP * sizeof(float2);
+    const size_t lds = (2 * (size_t)B * a.RP + (a.R <= FT_PACK ? a.R : 0)) * sizeof(float2);
     DPZ_TIMED(DPZ_KT_FFT, st, ft_pass_kernel<<<(unsigned)blocks, FT_THREADS, lds, st>>>(a));
     cur = dst;
     p *= a.R;

@@ -84,7 +84,8 @@ class GossipRound:
 
     def __init__(self, adj, x_init, alpha, rank=0, world=1, group=None, encode=None, fold=None,
                  device=None, streams=3, exchange="auto", hbm_budget=None, partial=None,
-                 combine=None, node_batch=True, node_group=4, guarded=True, sliced_counter=True):
+                 combine=None, node_batch=True, node_group=4, guarded=True, sliced_counter=True,
+                 ring_counter=None, ring_slots=None):
         """adj: adjacency sets of all nodes; x_init: (hi - lo, N) fp32 tensor with this rank's
         nodes' flat models (device tensor for the HIP codec).
 
@@ -129,6 +130,16 @@ class GossipRound:
         # counter (_unslice)
         self.sliced_counter = (bool(sliced_counter) and encode is None and fold is None
                                and node_batch and self.hi - self.lo > 1)
+        # ring_counter (HIP, node-batched encodes; round 6, as PartialModel's RingCounter): the
+        # encodes write each round's payload indices into a slot of a per-node ring of rounds and
+        # update no counter at all; the int32 counters take the ring's rounds (dpz_counter_flush)
+        # when read (``counter``: the reference's end-of-run dump, node/DPSGDNode.py:186-194) or
+        # when the ring is full.  None: on whenever the node-batched HIP encode runs
+        self.ring_counter = (encode is None and fold is None and node_batch and
+                             self.hi - self.lo > 1 and (ring_counter is None or bool(ring_counter)))
+        if self.ring_counter:
+            self.sliced_counter = False
+        self._ring = None
         if self.sliced_counter:
             from . import codec
             nw = codec.mask_words(self.N)
@@ -147,6 +158,17 @@ class GossipRound:
                 hbm_budget = torch.cuda.mem_get_info(self.device)[0] // 2
             else:
                 hbm_budget = float("inf")
+        if self.ring_counter:
+            # (per, slots, k): a node's rounds adjacent (one flush segment list per node); the
+            # round's send_idx is the slot's (per, k) view.  At most an eighth of the budget.
+            row = self.per * self.k * 4
+            cap = 64 if hbm_budget == float("inf") else int(hbm_budget // 8 // max(1, row))
+            self.ring_slots = max(2, min(64, cap)) if ring_slots is None else max(1, int(ring_slots))
+            self._ring = torch.zeros(self.per, self.ring_slots, self.k, dtype=torch.int32,
+                                     device=self.device)
+            self._ring_used = 0
+            self._flush_ws = None
+            self.send_idx = self._ring[:, 0, :]
         if self.coll:
             # the exchange mode and the reduce-scatter group size decide which collectives every
             # rank issues: all ranks must derive them from ONE budget (the smallest), or ranks
@@ -251,6 +273,8 @@ class GossipRound:
         the sliced counter its materialised copy (dpz_counter_unslice per node) — a snapshot:
         writes into it do not reach the engine (construct with sliced_counter=False for a live
         int32 tensor)."""
+        if self._ring is not None:
+            self._flush_ring()
         if self._counter is not None:
             return self._counter
         from . import codec
@@ -261,10 +285,38 @@ class GossipRound:
         """Owned node j's int32 counter alone (N values: the reference node's own
         shared_parameters_counter, node/DPSGDNode.py:186-194) — without the (m, N) stack that
         ``counter`` materialises for the sliced form; ``out`` (int32[N], device) is reused."""
+        if self._ring is not None:
+            self._flush_ring()
         if self._counter is not None:
             return self._counter[j] if out is None else out.copy_(self._counter[j])
         from . import codec
         return codec.counter_unslice(self._planes[j], self.N, out=out)
+
+    def _flush_ring(self):
+        """The ring's committed rounds into every owned node's int32 counter (dpz_counter_flush,
+        one call per node: its rounds are adjacent in the ring), the ring emptied."""
+        u = self._ring_used
+        if u == 0:
+            return
+        from . import _lib, codec
+        if self._flush_ws is None:
+            need = max(256, int(_lib.lib().dpz_counter_flush_workspace_bytes(self.N)))
+            self._flush_ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        offs = [i * self.k for i in range(u + 1)]
+        for j in range(self.hi - self.lo):
+            codec.counter_flush(self._counter[j], self._ring[j].view(-1), offs,
+                                workspace=self._flush_ws)
+        self._ring_used = 0
+
+    def _ring_next(self):
+        """The round's payload index buffer: the next free slot of the ring (flushed first when
+        full); the slot is committed once the round's encodes are final (_ring_commit)."""
+        if self._ring_used == self.ring_slots:
+            self._flush_ring()
+        self.send_idx = self._ring[:, self._ring_used, :]
+
+    def _ring_commit(self):
+        self._ring_used += 1
 
     def _unslice(self):
         """Back to the int32 counter (the node-batched sliced encode does not take this
@@ -313,14 +365,14 @@ class GossipRound:
         idx_out, val_out, ws, status_out, 0), one per x0 buffer (init_model swaps with the fold
         output every round, so two tables alternate)."""
         import numpy as np
-        key = self.x0.data_ptr()
+        key = (self.x0.data_ptr(), self.send_idx.data_ptr())
         tabs = self.__dict__.setdefault("_node_tabs", {})
         if key not in tabs:
             rows = []
             for j in range(m):
                 sl = self.sliced_counter
-                rows.append([self.x[j].data_ptr(), self.x0[j].data_ptr(),
-                             (self._planes if sl else self._counter)[j].data_ptr(),
+                cnt = 0 if self.ring_counter else (self._planes if sl else self._counter)[j].data_ptr()
+                rows.append([self.x[j].data_ptr(), self.x0[j].data_ptr(), cnt,
                              self.send_idx[j].data_ptr(),
                              self.send_val[j].data_ptr(), self.node_ws[j].buf.data_ptr(),
                              self.status.data_ptr() + 4 * j,
@@ -396,6 +448,9 @@ class GossipRound:
                 codec.topk_encode_sliced(self.x[j], self.k, self._selmask[j], self._planes[j],
                                          x0=self.x0[j], idx_out=self.send_idx[j],
                                          val_out=self.send_val[j], workspace=ws, exact=True)
+            elif self.ring_counter:  # the round's slot: counted when the ring is flushed
+                codec.topk_encode(self.x[j], self.k, x0=self.x0[j], idx_out=self.send_idx[j],
+                                  val_out=self.send_val[j], workspace=ws, exact=True)
             else:
                 codec.topk_encode(self.x[j], self.k, x0=self.x0[j], counter=self._counter[j],
                                   idx_out=self.send_idx[j], val_out=self.send_val[j],
@@ -411,6 +466,15 @@ class GossipRound:
             return
         from . import _lib, codec
         m = self.hi - self.lo
+        if self.ring_counter:
+            self._ring_next()
+            if self._encode_nodes(m, check):
+                self._ring_commit()
+                return
+            # (n, k) off the sampled path: exact encodes into the slot, no counter update
+            self._rerun_encodes(list(range(m)))
+            self._ring_commit()
+            return
         if self.node_batch and m > 1 and self._encode_nodes(m, check):
             return
         if self.sliced_counter:  # (n, k) off the sampled path: exact sliced encodes
@@ -595,7 +659,7 @@ class GossipRound:
             self.recv_idx, self.recv_val = self.send_idx, self.send_val  # no copy on one rank
             return
         import torch.distributed as dist
-        dist.all_gather_into_tensor(self.recv_idx, self.send_idx, group=self.group)
+        dist.all_gather_into_tensor(self.recv_idx, self.send_idx.contiguous(), group=self.group)
         dist.all_gather_into_tensor(self.recv_val, self.send_val, group=self.group)
 
     def _fold_tables(self):
@@ -619,6 +683,16 @@ class GossipRound:
                     w=(ctypes.c_float * tot)(*w), w_self=(ctypes.c_float * max(1, m))(*ws_),
                     key=self._recv_key())
 
+    def _fold_tab(self):
+        """The fold tables of the current receive buffers (one per ring slot when the payloads
+        are read in place), built once each."""
+        key = self._recv_key()
+        cache = self.__dict__.setdefault("_tabs", {})
+        tab = cache.get(key)
+        if tab is None:
+            tab = cache[key] = self._fold_tables()
+        return tab
+
     def fold_all(self, guard=None):
         """Every owned node's Metro-Hastings fold.  guard (HIP, DEVICE int32): the round's
         encode status words; the one-launch fold then writes nothing if any is nonzero
@@ -635,9 +709,7 @@ class GossipRound:
             from . import _lib
             from ._lib import DPZ_FOLD_ALSO_LOCAL, DPZ_FOLD_SELF
             m = self.hi - self.lo
-            tab = getattr(self, "_tab", None)
-            if tab is None or tab["key"] != self._recv_key():
-                tab = self._tab = self._fold_tables()
+            tab = self._fold_tab()
             ptrs = getattr(self, "_fold_ptrs", None)
             key = (self.x.data_ptr(), self.out.data_ptr())
             if ptrs is None or ptrs[0] != key:
@@ -654,9 +726,7 @@ class GossipRound:
         if self._hip:
             from . import _lib
             from ._lib import DPZ_FOLD_ALSO_LOCAL, DPZ_FOLD_SELF
-            tab = getattr(self, "_tab", None)
-            if tab is None or tab["key"] != self._recv_key():
-                tab = self._tab = self._fold_tables()
+            tab = self._fold_tab()
             m = self.hi - self.lo
             streams = (ctypes.c_void_p * len(self.streams))(*[s.cuda_stream for s in self.streams])
             maxp = max((len(self.weights[j][0]) for j in nodes), default=1)

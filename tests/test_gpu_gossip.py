@@ -171,8 +171,8 @@ def test_gossip_round_sliced_counter(dev, path, n, alpha):
     from tests.layouts import miss_layout
     adj = read_edges(path)
     x = _models(len(adj), n)
-    a = GossipRound(adj, x.to(dev), alpha, sliced_counter=True)
-    b = GossipRound(adj, x.to(dev), alpha, sliced_counter=False)
+    a = GossipRound(adj, x.to(dev), alpha, sliced_counter=True, ring_counter=False)
+    b = GossipRound(adj, x.to(dev), alpha, sliced_counter=False, ring_counter=False)
     assert a.sliced_counter and not b.sliced_counter
     miss = None
     if n >= (1 << 20):
@@ -201,8 +201,8 @@ def test_sliced_counter_falls_back_past_the_sliced_geometry(dev):
     adj = [{1}, {0}]
     g = torch.Generator().manual_seed(7)
     x = torch.randn(2, n, generator=g).to(dev)
-    a = GossipRound(adj, x, 0.01)
-    b = GossipRound(adj, x, 0.01, sliced_counter=False)
+    a = GossipRound(adj, x, 0.01, ring_counter=False)
+    b = GossipRound(adj, x, 0.01, sliced_counter=False, ring_counter=False)
     assert a.sliced_counter
     for r in range(2):
         noise = torch.randn(2, n, generator=torch.Generator(device=dev).manual_seed(r), device=dev)
@@ -215,4 +215,42 @@ def test_sliced_counter_falls_back_past_the_sliced_geometry(dev):
         assert torch.equal(a.counter, b.counter)
     del a, b
     one = GossipRound([set()], torch.zeros(1, 1 << 18, device=dev), 0.01)
-    assert not one.sliced_counter
+    assert not one.sliced_counter and not one.ring_counter
+
+
+@pytest.mark.parametrize("path,n,alpha,slots", [(EDGES16, 1 << 20, 0.01, 2),
+                                                (EDGES96, 40_000, 0.02, 3)])
+def test_gossip_round_ring_counter(dev, path, n, alpha, slots):
+    """The counters deferred to a ring of rounds (the node-batched encodes write each round's
+    payload indices into a ring slot and update no counter; dpz_counter_flush on read or when the
+    ring is full): models and counters bit-identical to the int32-counter engine over five rounds
+    with a 2- / 3-slot ring (wraps: flushes inside the run), the counter read mid-run and at the
+    end, a forced sampled miss in round 0 (re-run exactly into the slot), and the counter a live
+    tensor (a write into it stays)."""
+    from decentralizepy_amd.gossip import GossipRound, read_edges
+    from tests.layouts import miss_layout
+    adj = read_edges(path)
+    x = _models(len(adj), n)
+    a = GossipRound(adj, x.to(dev), alpha, ring_slots=slots)
+    b = GossipRound(adj, x.to(dev), alpha, sliced_counter=False, ring_counter=False)
+    assert a.ring_counter and not a.sliced_counter and a.ring_slots == slots
+    miss = None
+    if n >= (1 << 20):
+        miss, _ = miss_layout(n, round(alpha * n))
+    for r in range(5):
+        g = torch.Generator().manual_seed(700 + r)
+        noise = (0.01 * torch.randn(len(adj), n, generator=g)).to(dev)
+        for eng in (a, b):
+            eng.x += noise
+            if r == 0 and miss is not None:
+                eng.x[3] = eng.x0[3] + torch.from_numpy(miss).to(dev)
+            eng.step()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(a.x.cpu().numpy().view(np.uint32),
+                                      b.x.cpu().numpy().view(np.uint32))
+        if r in (1, 4):
+            np.testing.assert_array_equal(a.counter.cpu().numpy(), b.counter.cpu().numpy())
+            np.testing.assert_array_equal(a.counter_row(2).cpu().numpy(),
+                                          b.counter[2].cpu().numpy())
+    a.counter[0, 0] += 5
+    assert int(a.counter[0, 0]) == int(b.counter[0, 0]) + 5
