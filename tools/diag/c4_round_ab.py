@@ -16,6 +16,9 @@ dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 # ENGINE_SLICED=0: the int32 counters (gossip.py sliced_counter, default on)
 ekw = {"sliced_counter": os.environ.get("ENGINE_SLICED", "1") == "1"}
+# ENGINE_RING=0: no ring of rounds (gossip.py ring_counter, default on): the sliced / int32 form
+if os.environ.get("ENGINE_RING"):
+    ekw["ring_counter"] = os.environ["ENGINE_RING"] == "1"
 # NODE_GROUP / STREAMS: the node-batched encodes' group size and stream count (gossip.py defaults 4 / 3)
 if os.environ.get("NODE_GROUP"):
     ekw["node_group"] = int(os.environ["NODE_GROUP"])
