@@ -365,7 +365,7 @@ class GossipRound:
         idx_out, val_out, ws, status_out, 0), one per x0 buffer (init_model swaps with the fold
         output every round, so two tables alternate)."""
         import numpy as np
-        key = (self.x0.data_ptr(), self.send_idx.data_ptr())
+        key = self.x0.data_ptr()
         tabs = self.__dict__.setdefault("_node_tabs", {})
         if key not in tabs:
             rows = []
@@ -379,7 +379,18 @@ class GossipRound:
                              self._selmask[j].data_ptr() if sl else 0])
             tabs[key] = torch.from_numpy(np.array(rows, dtype=np.uint64).view(np.int64)).to(
                 self.device)
-        return tabs[key]
+        tab = tabs[key]
+        if self.ring_counter:
+            # the idx_out column at this round's slot: slot s of node j lies s * k * 4 bytes past
+            # slot 0 (one small device add on the current stream, ordered before the encodes)
+            if getattr(self, "_ring_col0", None) is None:
+                base = self._ring[:m, 0, :]
+                step = base.stride(0) * base.element_size()
+                self._ring_col0 = torch.tensor([base.data_ptr() + j * step for j in range(m)],
+                                               dtype=torch.int64, device=self.device)
+            off = self.send_idx.data_ptr() - self._ring.data_ptr()
+            torch.add(self._ring_col0, off, out=tab[:m, 3])
+        return tab
 
     def _encode_nodes(self, m, check=True):
         """Every node's encode with one launch per phase (dpz_topk_encode_nodes): each node its
@@ -684,13 +695,29 @@ class GossipRound:
                     key=self._recv_key())
 
     def _fold_tab(self):
-        """The fold tables of the current receive buffers (one per ring slot when the payloads
-        are read in place), built once each."""
-        key = self._recv_key()
-        cache = self.__dict__.setdefault("_tabs", {})
-        tab = cache.get(key)
-        if tab is None:
-            tab = cache[key] = self._fold_tables()
+        """The fold tables of the current receive buffers, built once.  With the ring of rounds
+        the payloads read in place are slot views: the table is built at one slot and its index
+        pointers into the ring moved to the current slot (a numpy add, no rebuild)."""
+        if not self.ring_counter:
+            tab = getattr(self, "_tab", None)
+            if tab is None or tab["key"] != self._recv_key():
+                tab = self._tab = self._fold_tables()
+            return tab
+        import numpy as np
+        off = self.send_idx.data_ptr() - self._ring.data_ptr()  # this slot's byte offset
+        cur = self.send_idx.data_ptr()
+        kn = tuple(v - off if v == cur else v for v in self._recv_key())  # slot-independent
+        tab = getattr(self, "_tab", None)
+        if tab is None or tab["key_ring"] != kn:
+            tab = self._tab = self._fold_tables()
+            idx0 = np.array([int(v or 0) for v in tab["idx"]], dtype=np.int64)
+            lo, hi = self._ring.data_ptr(), self._ring.data_ptr() + self._ring.numel() * 4
+            tab["ring_mask"] = ((idx0 >= lo) & (idx0 < hi)).astype(np.int64)
+            tab["idx0"] = idx0 - tab["ring_mask"] * off
+            tab["idx_now"] = np.empty_like(idx0)
+            tab["idx"] = (ctypes.c_void_p * len(idx0)).from_buffer(tab["idx_now"])
+            tab["key_ring"] = kn
+        np.add(tab["idx0"], tab["ring_mask"] * off, out=tab["idx_now"])
         return tab
 
     def fold_all(self, guard=None):
