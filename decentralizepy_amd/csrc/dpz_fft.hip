@@ -108,6 +108,9 @@ static unsigned grid_for(int64_t n) {
 constexpr int FT_THREADS = 256;
 constexpr int FT_ELEMS = 2048;  // B * R complex per block (two LDS buffers of B * (R + 1))
 constexpr int FT_REG_ELEMS = 2048;  // tiles up to this size load / store through registers
+#ifndef DPZ_FT_IP_WAVES
+#define DPZ_FT_IP_WAVES 6
+#endif
 constexpr int FT_MAXR = 4096;   // the largest prime a pass takes (larger: hipFFT)
 constexpr int FT_PACK = 256;    // the largest packed radix of a pass
 constexpr int FT_MAXPASS = 12;
@@ -300,6 +303,50 @@ __device__ __forceinline__ void ft_sub(const float2* src, float2* dst, int B, in
   }
 }
 
+// the same sub-pass in place (one LDS buffer): each thread reads and transforms all its
+// butterflies into registers, the block syncs, then the outputs are written over the inputs
+template <int Q>
+__device__ __forceinline__ void ft_sub_ip(float2* buf, int B, int R, int RP, int pp, uint32_t mnb,
+                                          uint32_t mpp, const FtRoots& rt, const FtTw& tw,
+                                          bool inv) {
+  constexpr int NBT = (FT_REG_ELEMS / Q + FT_THREADS - 1) / FT_THREADS;
+  const int nb = R / Q;
+  const int sm = R / (pp * Q);
+  float2 w[Q];
+  if constexpr (Q != 2 && Q != 4 && Q != 8) {
+#pragma unroll
+    for (int m = 0; m < Q; ++m) w[m] = rt.get(tw, m * (R / Q), inv);
+  }
+  float2 v[NBT][Q];
+  int dst[NBT];
+#pragma unroll
+  for (int b = 0; b < NBT; ++b) {
+    const int u0 = threadIdx.x + b * FT_THREADS;
+    const bool ok = u0 < B * nb;
+    const int u = ok ? u0 : 0;
+    const int c = ft_div(u, mnb), i = u - c * nb;
+    const int ip = ft_div(i, mpp);
+    const int k = i - ip * pp;
+    const float2* s = buf + c * RP + i;
+#pragma unroll
+    for (int r = 0; r < Q; ++r) v[b][r] = s[r * nb];
+    if (k) {
+#pragma unroll
+      for (int r = 1; r < Q; ++r) v[b][r] = ft_cmul(v[b][r], rt.get(tw, r * k * sm, inv));
+    }
+    ft_dft<Q>(v[b], w, inv);
+    dst[b] = ok ? c * RP + ip * pp * Q + k : -1;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < NBT; ++b) {
+    if (dst[b] >= 0) {
+#pragma unroll
+      for (int m = 0; m < Q; ++m) buf[dst[b] + m * pp] = v[b][m];
+    }
+  }
+}
+
 // any other prime radix: one output per thread, O(q) terms
 __device__ __forceinline__ void ft_sub_any(const float2* src, float2* dst, int B, int R, int RP,
                                            int pp, int q, const FtTw& tw, bool inv) {
@@ -321,19 +368,23 @@ __device__ __forceinline__ void ft_sub_any(const float2* src, float2* dst, int B
   }
 }
 
-__global__ void __launch_bounds__(FT_THREADS) ft_pass_kernel(FtPass a) {
-  extern __shared__ float2 ft_lds[];
+// IP (in place): passes whose sub-radices are all in {2, 3, 4, 5, 7, 8} and whose tile goes
+// through registers run with ONE LDS buffer (sub-passes staged in registers): 72 VGPRs and half
+// the LDS, so more blocks per CU; the others (11, 13, other primes) ping-pong two buffers
+extern __shared__ float2 ft_lds[];
+template <bool IP>
+__device__ __forceinline__ void ft_pass_body(const FtPass& a) {
   const int B = a.B, R = a.R, RP = a.RP;
   const int t = threadIdx.x;
   const int64_t j0 = (int64_t)blockIdx.x * B;
   const int cols = (int)(a.S - j0 < B ? a.S - j0 : B);
   float2* src = ft_lds;
-  float2* dst = ft_lds + B * RP;
+  float2* dst = IP ? ft_lds : ft_lds + B * RP;
   const bool inv = a.inv != 0;
   // the pass's R roots W_R^e in LDS (packed passes; a lone large prime reads the global table)
   FtRoots rt{nullptr, R, a.tw.nt / (uint32_t)R};
   if (R <= FT_PACK) {
-    float2* tab = ft_lds + 2 * B * RP;
+    float2* tab = ft_lds + (IP ? 1 : 2) * B * RP;
     for (int e = t; e < R; e += FT_THREADS) tab[e] = ft_root(a.tw, (uint32_t)e * rt.nt_over_r, inv);
     rt.lds = tab;
   }
@@ -375,21 +426,33 @@ __global__ void __launch_bounds__(FT_THREADS) ft_pass_kernel(FtPass a) {
   for (int s = 0; s < a.nsub; ++s) {
     const int q = a.q[s];
     const uint32_t mn = a.mnb[s], mp = a.mpp[s];
-    switch (q) {
-      case 2: ft_sub<2>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
-      case 4: ft_sub<4>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
-      case 8: ft_sub<8>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
-      case 3: ft_sub<3>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
-      case 5: ft_sub<5>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
-      case 7: ft_sub<7>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
-      case 11: ft_sub<11>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
-      case 13: ft_sub<13>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
-      default: ft_sub_any(src, dst, B, R, RP, pp, q, a.tw, inv);
+    if constexpr (IP) {
+      switch (q) {
+        case 2: ft_sub_ip<2>(src, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+        case 4: ft_sub_ip<4>(src, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+        case 8: ft_sub_ip<8>(src, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+        case 3: ft_sub_ip<3>(src, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+        case 5: ft_sub_ip<5>(src, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+        default: ft_sub_ip<7>(src, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+      }
+      __syncthreads();
+    } else {
+      switch (q) {
+        case 2: ft_sub<2>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+        case 4: ft_sub<4>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+        case 8: ft_sub<8>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+        case 3: ft_sub<3>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+        case 5: ft_sub<5>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+        case 7: ft_sub<7>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+        case 11: ft_sub<11>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+        case 13: ft_sub<13>(src, dst, B, R, RP, pp, mn, mp, rt, a.tw, inv); break;
+        default: ft_sub_any(src, dst, B, R, RP, pp, q, a.tw, inv);
+      }
+      __syncthreads();
+      float2* x = src;
+      src = dst;
+      dst = x;
     }
-    __syncthreads();
-    float2* x = src;
-    src = dst;
-    dst = x;
     pp *= q;
   }
   // store: column j's output m to (j / p) p R + (j mod p) + m p; consecutive threads take
@@ -441,6 +504,13 @@ __global__ void __launch_bounds__(FT_THREADS) ft_pass_kernel(FtPass a) {
     }
   }
 }
+
+// the in-place variant held to 6 waves per SIMD (<= 80 VGPRs), the ping-pong one as it compiles
+__global__ void __launch_bounds__(FT_THREADS) __attribute__((amdgpu_waves_per_eu(DPZ_FT_IP_WAVES, 8)))
+ft_pass_ip_kernel(FtPass a) {
+  ft_pass_body<true>(a);
+}
+__global__ void __launch_bounds__(FT_THREADS) ft_pass_kernel(FtPass a) { ft_pass_body<false>(a); }
 
 // even n, forward: X[k] = ((Z[k] + conj Z[M-k]) - i W_n^k (Z[k] - conj Z[M-k])) / 2 for the pair
 // (k, M - k), k <= M / 2; Z read from `z` (may equal out)
@@ -614,8 +684,9 @@ static int ft_run(const FtPlan& pl, const FtTw& tw, bool inv, const float2* in, 
                   int64_t n_aux, float2* bufA, float2* bufB, hipStream_t st) {
   if (!g_ft_lds_set) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(ft_pass_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess)
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(ft_pass_ip_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
       return DPZ_ERR_INTERNAL;
     g_ft_lds_set = true;
   }
@@ -639,6 +710,11 @@ static int ft_run(const FtPlan& pl, const FtTw& tw, bool inv, const float2* in, 
     a.B = B;
     a.RP = a.R + 1;
     a.nsub = pl.nsub[s];
+    bool ip = B * a.R <= FT_REG_ELEMS && DPZ_KNOB_INT(FFT_INPLACE, 0) != 0;
+    for (int i = 0; i < a.nsub; ++i) {
+      const int q = pl.q[s][i];
+      ip = ip && (q == 2 || q == 3 || q == 4 || q == 5 || q == 7 || q == 8);
+    }
     int pp = 1;
     for (int i = 0; i < a.nsub; ++i) {
       a.q[i] = pl.q[s][i];
@@ -663,8 +739,13 @@ static int ft_run(const FtPlan& pl, const FtTw& tw, bool inv, const float2* in, 
     }
     a.out = dst;
     const int64_t blocks = (a.S + B - 1) / B;
-    const size_t lds = (2 * (size_t)B * a.RP + (a.R <= FT_PACK ? a.R : 0)) * sizeof(float2);
-    DPZ_TIMED(DPZ_KT_FFT, st, ft_pass_kernel<<<(unsigned)blocks, FT_THREADS, lds, st>>>(a));
+    const size_t lds = ((ip ? 1 : 2) * (size_t)B * a.RP + (a.R <= FT_PACK ? a.R : 0)) *
+                       sizeof(float2);
+    if (ip) {
+      DPZ_TIMED(DPZ_KT_FFT, st, ft_pass_ip_kernel<<<(unsigned)blocks, FT_THREADS, lds, st>>>(a));
+    } else {
+      DPZ_TIMED(DPZ_KT_FFT, st, ft_pass_kernel<<<(unsigned)blocks, FT_THREADS, lds, st>>>(a));
+    }
     cur = dst;
     p *= a.R;
   }

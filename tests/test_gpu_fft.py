@@ -130,3 +130,25 @@ def test_cplx_kernels_exact(dev):
     np.testing.assert_array_equal(ad.cpu().numpy().view(np.uint64), a2.view(np.uint64))
     pair = codec.cplx_pair_indices(idd).cpu().numpy()
     np.testing.assert_array_equal(pair, offt.pair_indices(idx).astype(np.int32))
+
+
+@pytest.mark.parametrize("n", [4098, 30030, 11_000_000, 2 * 17 * 19 * 23])
+def test_fft_inplace_passes_forced(dev, diag_lib, monkeypatch, n):
+    """The in-place pass variant (one LDS buffer, sub-passes staged in registers; passes whose
+    radices are all in {2, 3, 4, 5, 7, 8}) forced on through the diagnostic build
+    (DPZ_FFT_INPLACE=1): the same tolerances against numpy as the default passes, and bit-equal
+    to them where both run the same arithmetic (the butterflies and twiddles are the same)."""
+    from decentralizepy_amd import codec
+    g = torch.Generator(device=dev).manual_seed(11)
+    x = torch.randn(n, device=dev, generator=g)
+    monkeypatch.setenv("DPZ_FFT_INPLACE", "0")
+    f0 = codec.rfft(x).cpu().numpy()
+    monkeypatch.setenv("DPZ_FFT_INPLACE", "1")
+    f1 = codec.rfft(x)
+    xh = x.cpu().numpy()
+    scale = float(np.abs(xh).max())
+    ref = np.fft.rfft(xh.astype(np.float64))
+    assert np.abs(f1.cpu().numpy() - ref).max() <= scenario.fft_tol("params", n, scale)
+    np.testing.assert_array_equal(f1.cpu().numpy().view(np.uint64), f0.view(np.uint64))
+    back = codec.irfft(f1.clone(), n).cpu().numpy()
+    assert np.abs(back - xh).max() <= scenario.fft_tol("model", n, scale)
