@@ -109,7 +109,7 @@ constexpr int FT_THREADS = 256;
 constexpr int FT_ELEMS = 2048;  // B * R complex per block (two LDS buffers of B * (R + 1))
 constexpr int FT_REG_ELEMS = 2048;  // tiles up to this size load / store through registers
 #ifndef DPZ_FT_IP_WAVES
-#define DPZ_FT_IP_WAVES 6
+#define DPZ_FT_IP_WAVES 5
 #endif
 constexpr int FT_MAXR = 4096;   // the largest prime a pass takes (larger: hipFFT)
 constexpr int FT_PACK = 256;    // the largest packed radix of a pass
@@ -505,7 +505,9 @@ __device__ __forceinline__ void ft_pass_body(const FtPass& a) {
   }
 }
 
-// the in-place variant held to 6 waves per SIMD (<= 80 VGPRs), the ping-pong one as it compiles
+// the in-place variant held to 5 waves per SIMD (96 VGPRs, 5 spilled; 6 waves spill 21 and run
+// slower: rfft 181 vs 159 us at 11 M, profiles/r06_fft_inplace_ab.jsonl), the ping-pong one as it
+// compiles (125 VGPRs, 4 waves)
 __global__ void __launch_bounds__(FT_THREADS) __attribute__((amdgpu_waves_per_eu(DPZ_FT_IP_WAVES, 8)))
 ft_pass_ip_kernel(FtPass a) {
   ft_pass_body<true>(a);
@@ -710,7 +712,7 @@ static int ft_run(const FtPlan& pl, const FtTw& tw, bool inv, const float2* in, 
     a.B = B;
     a.RP = a.R + 1;
     a.nsub = pl.nsub[s];
-    bool ip = B * a.R <= FT_REG_ELEMS && DPZ_KNOB_INT(FFT_INPLACE, 0) != 0;
+    bool ip = B * a.R <= FT_REG_ELEMS && DPZ_KNOB_INT(FFT_INPLACE, 1) != 0;
     for (int i = 0; i < a.nsub; ++i) {
       const int q = pl.q[s][i];
       ip = ip && (q == 2 || q == 3 || q == 4 || q == 5 || q == 7 || q == 8);

@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from decentralizepy_amd import codec  # noqa: E402
 
 CONFIGS = [("lib", {"DPZ_FFT_LIB": "1"}), ("default", {}),
-           ("inplace", {"DPZ_FFT_INPLACE": "1"}),
+           ("pingpong", {"DPZ_FFT_INPLACE": "0"}),
            ("e4096_b16", {"DPZ_FFT_ELEMS": "4096", "DPZ_FFT_BMAX": "16"}),
            ("e2048_b8", {"DPZ_FFT_ELEMS": "2048", "DPZ_FFT_BMAX": "8"})]
 if os.environ.get("FFT_CONFIGS") == "short":
