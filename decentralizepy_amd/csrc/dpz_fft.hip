@@ -763,7 +763,9 @@ static bool ft_native_plan(int64_t n, FtPlan* pl) {
 }
 
 static int64_t ft_native_ws(int64_t n) {
-  return n % 2 == 0 ? (n / 2) * 8 + 256 : 2 * n * 8 + 256;
+  // even: M complex (aligned up to 256 inside); odd: two n-complex buffers, the second aligned up
+  // to 256 past the first + 64 (ft_align): 16 n + 64 + 2 * 255 bounds both
+  return n % 2 == 0 ? (n / 2) * 8 + 256 : 2 * n * 8 + 1024;
 }
 
 static float2* ft_align(void* ws, size_t off) {
