@@ -147,7 +147,8 @@ struct FtPass {
   int nsub;
   int q[FT_MAXSUB];     // the LDS sub-passes' radices (product R)
   uint32_t mnb[FT_MAXSUB], mpp[FT_MAXSUB];  // u / (R / q) and u / pp as umulhi(u, m) (u < 2^16)
-  int load_mode;        // 0 complex, 1 real (x, 0), 2 Hermitian extension of n_aux / 2 + 1 values
+  int load_mode;        // 0 complex, 1 real (x, 0), 2 Hermitian extension of n_aux / 2 + 1 values,
+                        // 3 the c2r pairing of X[0..n_aux] (even-n inverse, ft_c2r_pair)
   int store_mode;       // 0 complex, 1 complex * scale, 2 real part * scale, 3 indices < n_aux only
   int64_t n_aux;
   float scale;
@@ -155,8 +156,19 @@ struct FtPass {
   FtTw tw;
 };
 
+__device__ __forceinline__ float2 ft_mi(float2 z, bool inv);
+__device__ __forceinline__ float2 ft_c2r_pair(float2 p, float2 q, uint32_t kk, const FtTw& tw);
+
 __device__ __forceinline__ float2 ft_load(const FtPass& a, int64_t i) {
   if (a.load_mode == 1) return make_float2(a.in_re[i], 0.0f);
+  if (a.load_mode == 3) {  // Z[i] from X[i] and X[M - i] (Im X[0], Im X[M] dropped), as the
+    float2 p = a.in[i], q = a.in[a.n_aux - i];  // separate pre pass computes it
+    if (i == 0) {
+      p.y = 0.0f;
+      q.y = 0.0f;
+    }
+    return ft_c2r_pair(p, q, (uint32_t)i, a.tw);
+  }
   if (a.load_mode == 2) {
     const int64_t h = a.n_aux / 2 + 1;
     if (i < h) {
@@ -181,6 +193,15 @@ __device__ __forceinline__ void ft_store(const FtPass& a, int64_t o, float2 v) {
 // -i z (forward) / +i z (inverse)
 __device__ __forceinline__ float2 ft_mi(float2 z, bool inv) {
   return inv ? make_float2(-z.y, z.x) : make_float2(z.y, -z.x);
+}
+
+// even-n inverse pairing: Z[k] = (X[k] + conj X[M-k]) + i W_n^{-k} (X[k] - conj X[M-k]) for
+// p = X[k], q = X[M - k]
+__device__ __forceinline__ float2 ft_c2r_pair(float2 p, float2 q, uint32_t kk, const FtTw& tw) {
+  const float2 e = make_float2(p.x + q.x, p.y - q.y);
+  const float2 d = make_float2(p.x - q.x, p.y + q.y);
+  const float2 o = ft_mi(ft_cmul(ft_root(tw, kk, true), d), true);
+  return make_float2(e.x + o.x, e.y + o.y);
 }
 
 __device__ __forceinline__ void ft_dft4(float2& v0, float2& v1, float2& v2, float2& v3, bool inv) {
@@ -550,10 +571,8 @@ __global__ void __launch_bounds__(256) ft_c2r_pre_kernel(const float2* x, float2
       b.y = 0.0f;
     }
     auto one = [&](float2 p, float2 q, int64_t kk) {  // p = X[kk], q = X[M - kk]
-      const float2 e = make_float2(p.x + q.x, p.y - q.y);
-      const float2 d = make_float2(p.x - q.x, p.y + q.y);
-      const float2 o = ft_mi(ft_cmul(ft_root(tw, (uint32_t)kk, true), d), true);
-      return make_float2((e.x + o.x) * scale, (e.y + o.y) * scale);
+      const float2 z = ft_c2r_pair(p, q, (uint32_t)kk, tw);
+      return make_float2(z.x * scale, z.y * scale);
     };
     const float2 zk = one(a, b, k);
     if (k == 0) {
@@ -807,11 +826,19 @@ static int ft_irfft_native(const FtPlan& pl, float2* coeffs, int64_t n, float* o
     const int64_t M = n / 2;
     float2* w = ft_align(ws, 0);
     float2* xo = reinterpret_cast<float2*>(out);
-    // Z in place over the coefficients (pairs k, M - k), then the inverse DFT_M into out
-    DPZ_TIMED(DPZ_KT_FFT, st, ft_c2r_pre_kernel<<<grid_for(M / 2 + 1), 256, 0, st>>>(
-                                  coeffs, pl.npass > 0 ? coeffs : xo, M, tw, pl.npass > 0 ? 1.0f : sc));
-    if (pl.npass == 0) return DPZ_OK;
-    return ft_run(pl, tw, true, coeffs, nullptr, 0, xo, nullptr, 1, sc, 0, w, xo, st);
+    // the inverse DFT_M into out, its first pass forming Z[k] from X[k] and X[M - k] as it loads
+    // (load mode 3: no separate pairing pass; the coefficients are only read)
+    if (pl.npass == 0) {
+      DPZ_TIMED(DPZ_KT_FFT, st, ft_c2r_pre_kernel<<<grid_for(M / 2 + 1), 256, 0, st>>>(
+                                    coeffs, xo, M, tw, sc));
+      return DPZ_OK;
+    }
+    if (DPZ_KNOB_INT(FFT_PAIR_FUSED, 1) == 0) {  // diagnostic build: the separate pairing pass (A/B)
+      DPZ_TIMED(DPZ_KT_FFT, st, ft_c2r_pre_kernel<<<grid_for(M / 2 + 1), 256, 0, st>>>(
+                                    coeffs, coeffs, M, tw, 1.0f));
+      return ft_run(pl, tw, true, coeffs, nullptr, 0, xo, nullptr, 1, sc, 0, w, xo, st);
+    }
+    return ft_run(pl, tw, true, coeffs, nullptr, 3, xo, nullptr, 1, sc, M, w, xo, st);
   }
   float2* a = ft_align(ws, 0);
   float2* b = ft_align(ws, (size_t)n * 8 + 64);

@@ -12,11 +12,11 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from decentralizepy_amd import codec  # noqa: E402
 
 CONFIGS = [("lib", {"DPZ_FFT_LIB": "1"}), ("default", {}),
-           ("pingpong", {"DPZ_FFT_INPLACE": "0"}),
+           ("pingpong", {"DPZ_FFT_INPLACE": "0"}), ("pair_sep", {"DPZ_FFT_PAIR_FUSED": "0"}),
            ("e4096_b16", {"DPZ_FFT_ELEMS": "4096", "DPZ_FFT_BMAX": "16"}),
            ("e2048_b8", {"DPZ_FFT_ELEMS": "2048", "DPZ_FFT_BMAX": "8"})]
 if os.environ.get("FFT_CONFIGS") == "short":
-    CONFIGS = CONFIGS[:3]
+    CONFIGS = CONFIGS[:4]
 
 
 def main():
@@ -29,7 +29,8 @@ def main():
         outs = [torch.empty(n, device=dev) for _ in range(R)]
         row = {"n": n}
         for name, env in CONFIGS:
-            for k_ in ("DPZ_FFT_LIB", "DPZ_FFT_ELEMS", "DPZ_FFT_BMAX", "DPZ_FFT_INPLACE"):
+            for k_ in ("DPZ_FFT_LIB", "DPZ_FFT_ELEMS", "DPZ_FFT_BMAX", "DPZ_FFT_INPLACE",
+                       "DPZ_FFT_PAIR_FUSED"):
                 os.environ.pop(k_, None)
             os.environ.update(env)
             ws = codec.Workspace(dev)
