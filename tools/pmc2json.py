@@ -20,7 +20,7 @@ NAMES = {"sampled_sample_kernel": "topk_sample", "sampled_filter_kernel": "topk_
          "haar_dwt_kernel": "haar_dwt", "haar_idwt_kernel": "haar_idwt",
          "idwt_kernel": "idwt", "counter_sweep_kernel": "counter_flush",
          "counter_bounds_kernel": "counter_bounds", "counter_scatter_kernel": "counter_flush",
-         "ft_pass_kernel": "fft_pass", "ft_pass_ip_kernel": "fft_pass_ip",
+         "fold_merge_kernel": "fold_merge", "ft_pass_kernel": "fft_pass", "ft_pass_ip_kernel": "fft_pass_ip",
          "ft_r2c_post_kernel": "fft_r2c_post", "ft_c2r_pre_kernel": "fft_c2r_pre"}
 
 
