@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 N=${NAME:?NAME}
 rm -rf gpurun_out/prof_$N gpurun_out/prof_${N}_fetch gpurun_out/prof_${N}_write
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$N -o run -- "$@" > gpurun_out/prof_$N.log 2>&1 || { echo "trace rc=$?"; tail -5 gpurun_out/prof_$N.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$N -o run -- "$@" > gpurun_out/prof_$N.log 2>&1 || { echo "trace rc=$?"; tail -5 gpurun_out/prof_$N.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_${N}_fetch -o run -- "$@" > gpurun_out/prof_${N}_fetch.log 2>&1 || { echo "fetch rc=$?"; tail -5 gpurun_out/prof_${N}_fetch.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_${N}_write -o run -- "$@" > gpurun_out/prof_${N}_write.log 2>&1 || { echo "write rc=$?"; tail -5 gpurun_out/prof_${N}_write.log; exit 1; }
 F=$(find gpurun_out/prof_${N}_fetch -name '*counter_collection.csv' | head -1)
