@@ -1035,6 +1035,9 @@ __device__ __forceinline__ int32_t fw_lower_bounds(int np, int32_t e0, int lane,
 // The 16-payload groups kernel (C3 shape, tools/diag/fold_time.py) is no faster with them either
 // (alpha 0.02: 128.7 vs 122.1 us, 0.1: 171.1 vs 170.2, 0.2: 261.4 vs 255.2), so both kernels
 // search one payload after the other; fw_lower_bounds serves the patch decode.
+#ifndef DPZ_MERGE_HIT2
+#define DPZ_MERGE_HIT2 1
+#endif
 #ifndef DPZ_WALK4_LOCKSTEP
 #define DPZ_WALK4_LOCKSTEP 0
 #endif
@@ -2405,6 +2408,72 @@ __global__ void __launch_bounds__(FM_THREADS) __attribute__((amdgpu_waves_per_eu
           nh += (uint32_t)__popcll(b);
         }
         __builtin_amdgcn_wave_barrier();
+#if DPZ_MERGE_HIT2
+        // two hit elements per lane at a time (i and i + 64): two independent dependent chains
+        // interleave; the one-to-three-hit fold runs for both unconditionally and the rare
+        // element with four or more hits is redone payload by payload afterwards
+        auto fast = [&](uint32_t mm, uint32_t sl, float tb) -> float {
+          const int p0 = __ffs((int)mm) - 1;
+          const uint32_t mm1 = mm & (mm - 1u);
+          const int p1 = mm1 ? __ffs((int)mm1) - 1 : 32;
+          const uint32_t mm2 = mm1 & (mm1 - 1u);
+          const int p2 = mm2 ? __ffs((int)mm2) - 1 : 32;
+          const float v0 = s_val[sl < (uint32_t)TE ? sl : 0u];
+          const float v1 = s_val[sl + 1u < (uint32_t)TE ? sl + 1u : 0u];
+          const float v2 = s_val[sl + 2u < (uint32_t)TE ? sl + 2u : 0u];
+          float acc = 0.0f;
+          if (EQW) {
+            const float xw = tb * w0, v0w = v0 * w0, v1w = v1 * w0, v2w = v2 * w0;
+#pragma unroll
+            for (int p = 0; p < FOLD_MAXP; ++p) {
+              if (p >= np) break;
+              const float term = p == p0 ? v0w : (p == p1 ? v1w : (p == p2 ? v2w : xw));
+              acc = p == 0 ? (zb ? 0.0f + term : term) : acc + term;
+            }
+          } else {
+#pragma unroll
+            for (int p = 0; p < FOLD_MAXP; ++p) {
+              if (p >= np) break;
+              const float tv = p == p0 ? v0 : (p == p1 ? v1 : (p == p2 ? v2 : tb));
+              const float term = tv * W(p);
+              acc = p == 0 ? (zb ? 0.0f + term : term) : acc + term;
+            }
+          }
+          return acc;
+        };
+        auto slow = [&](uint32_t mm, uint32_t sl, float tb) -> float {
+          uint32_t s2 = sl;
+          float acc = 0.0f;
+          for (int p = 0; p < np; ++p) {
+            float tv = tb;
+            if ((mm >> p) & 1u) {
+              tv = s_val[s2 < (uint32_t)TE ? s2 : 0u];
+              ++s2;
+            }
+            const float term = tv * W(p);
+            acc = p == 0 ? (zb ? 0.0f + term : term) : acc + term;
+          }
+          return acc;
+        };
+        for (uint32_t i = (uint32_t)lane; i < nh; i += 128) {
+          const uint32_t i2 = i + 64u < nh ? i + 64u : i;
+          const uint32_t pa = wl_[i], pb = wl_[i2];
+          const uint32_t ma = (mask[pa >> 1] >> (16 * (pa & 1u))) & 0xFFFFu;
+          const uint32_t mb = (mask[pb >> 1] >> (16 * (pb & 1u))) & 0xFFFFu;
+          const uint32_t sa = s_pre[pa], sb = s_pre[pb];
+          const float xa = s_x[pa], xb = s_x[pb];
+          float acca = fast(ma, sa, zb ? 0.0f : xa);
+          float accb = fast(mb, sb, zb ? 0.0f : xb);
+          if (__popc(ma) > 3) acca = slow(ma, sa, zb ? 0.0f : xa);
+          if (__popc(mb) > 3) accb = slow(mb, sb, zb ? 0.0f : xb);
+          if (a.add_self) {
+            acca = acca + xa * a.w_self;
+            accb = accb + xb * a.w_self;
+          }
+          s_x[pb] = accb;  // (i2 == i: the same value twice)
+          s_x[pa] = acca;
+        }
+#else
         for (uint32_t i = (uint32_t)lane; i < nh; i += 64) {
           const uint32_t pos = wl_[i];
           const uint32_t mm = (mask[pos >> 1] >> (16 * (pos & 1u))) & 0xFFFFu;
@@ -2457,6 +2526,7 @@ __global__ void __launch_bounds__(FM_THREADS) __attribute__((amdgpu_waves_per_eu
           if (a.add_self) acc = acc + xv * a.w_self;
           s_x[pos] = acc;
         }
+#endif
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int c = 0; c < EPT / 4; ++c) {
