@@ -1035,8 +1035,13 @@ __device__ __forceinline__ int32_t fw_lower_bounds(int np, int32_t e0, int lane,
 // The 16-payload groups kernel (C3 shape, tools/diag/fold_time.py) is no faster with them either
 // (alpha 0.02: 128.7 vs 122.1 us, 0.1: 171.1 vs 170.2, 0.2: 261.4 vs 255.2), so both kernels
 // search one payload after the other; fw_lower_bounds serves the patch decode.
+// DPZ_MERGE_HIT2 1 (A/B variant, round 6): the merge fold's hit elements two per lane at a time
+// (two independent chains).  Measured on MI355X (tools/diag/merge_keep_ab.sh with lib_keep =
+// this switch, profiles/r06_merge_hit2_ab.jsonl): C3 16 x 0.01 105.1-105.6 -> 110.4-111.1 us,
+// 16 x 0.005 88 -> 106-107 — the second chain's loads and selects cost more than the overlap
+// gains at 4 waves per SIMD; off.
 #ifndef DPZ_MERGE_HIT2
-#define DPZ_MERGE_HIT2 1
+#define DPZ_MERGE_HIT2 0
 #endif
 #ifndef DPZ_WALK4_LOCKSTEP
 #define DPZ_WALK4_LOCKSTEP 0
