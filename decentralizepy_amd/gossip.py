@@ -187,6 +187,12 @@ class GossipRound:
         if exchange not in ("allgather", "peer", "reduce_scatter"):
             raise ValueError(f"unknown exchange {exchange!r}")
         self.exchange_mode = exchange
+        if exchange == "reduce_scatter" and self.ring_counter:
+            # the over-HBM legs keep their payload pointer tables across rounds: the ring's
+            # moving send rows would leave them stale, so this mode keeps the int32 counters
+            self.ring_counter = False
+            self._ring = None
+            self.send_idx = torch.zeros(self.per, self.k, dtype=torch.int32, device=self.device)
         if exchange == "peer":
             k = self.k
             n_recv = max(1, self._peer_n_recv)
