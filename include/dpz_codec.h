@@ -570,8 +570,9 @@ int64_t dpz_fft_workspace_bytes(int64_t n);
 int dpz_fft_native(int64_t n);
 /* out[m complex] = rfft(x[n]).  Asynchronous on stream.                                          */
 int dpz_rfft(const float* x, int64_t n, float* out, void* ws, size_t ws_bytes, dpz_stream_t stream);
-/* out[n] = irfft(coeffs[m complex], n) with torch's "backward" normalisation (1/n).  coeffs is
- * OVERWRITTEN (C2R works in place on its input).                                                  */
+/* out[n] = irfft(coeffs[m complex], n) with torch's "backward" normalisation (1/n).  coeffs may be
+ * OVERWRITTEN (the hipFFT fallback's C2R works in place on its input; the native passes only
+ * read it).                                                                                       */
 int dpz_irfft(float* coeffs, int64_t n, float* out, void* ws, size_t ws_bytes, dpz_stream_t stream);
 /* key[i] = |c[i]| (fp32 sqrt(re^2 + im^2)) of the complex change after the DPZ_ACC_* step
  * (ACCUMULATE: acc += change, key = |acc|; ADD: key = |change + acc|, acc unchanged).          */
