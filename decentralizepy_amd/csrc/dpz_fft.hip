@@ -153,11 +153,14 @@ struct FtPass {
   int64_t n_aux;
   float scale;
   int inv;
+  int pair;             // last pass of an even-n rfft: the block holds columns j and S - j and its
+                        // stores are the X[k] / X[M - k] pairing (n_aux = M)
   FtTw tw;
 };
 
 __device__ __forceinline__ float2 ft_mi(float2 z, bool inv);
 __device__ __forceinline__ float2 ft_c2r_pair(float2 p, float2 q, uint32_t kk, const FtTw& tw);
+__device__ __forceinline__ float2 ft_r2c_pair(float2 p, float2 q, uint32_t kk, const FtTw& tw);
 
 __device__ __forceinline__ float2 ft_load(const FtPass& a, int64_t i) {
   if (a.load_mode == 1) return make_float2(a.in_re[i], 0.0f);
@@ -193,6 +196,15 @@ __device__ __forceinline__ void ft_store(const FtPass& a, int64_t o, float2 v) {
 // -i z (forward) / +i z (inverse)
 __device__ __forceinline__ float2 ft_mi(float2 z, bool inv) {
   return inv ? make_float2(-z.y, z.x) : make_float2(z.y, -z.x);
+}
+
+// even-n forward pairing: X[k] = ((Z[k] + conj Z[M-k]) - i W_n^k (Z[k] - conj Z[M-k])) / 2 for
+// p = Z[k], q = Z[M - k]
+__device__ __forceinline__ float2 ft_r2c_pair(float2 p, float2 q, uint32_t kk, const FtTw& tw) {
+  const float2 e = make_float2(p.x + q.x, p.y - q.y);
+  const float2 d = make_float2(p.x - q.x, p.y + q.y);
+  const float2 o = ft_mi(ft_cmul(ft_root(tw, kk, false), d), false);
+  return make_float2(0.5f * (e.x + o.x), 0.5f * (e.y + o.y));
 }
 
 // even-n inverse pairing: Z[k] = (X[k] + conj X[M-k]) + i W_n^{-k} (X[k] - conj X[M-k]) for
@@ -397,8 +409,12 @@ template <bool IP>
 __device__ __forceinline__ void ft_pass_body(const FtPass& a) {
   const int B = a.B, R = a.R, RP = a.RP;
   const int t = threadIdx.x;
-  const int64_t j0 = (int64_t)blockIdx.x * B;
-  const int cols = (int)(a.S - j0 < B ? a.S - j0 : B);
+  // pair mode: slots c < H hold columns jf0 + c (jf <= S / 2), slots H + c their mirrors S - jf
+  // (column 0 is its own mirror: loaded twice)
+  const int H = B >> 1;
+  const int64_t j0 = a.pair ? (int64_t)blockIdx.x * H : (int64_t)blockIdx.x * B;
+  const int cols = a.pair ? (int)(a.S / 2 - j0 + 1 < H ? a.S / 2 - j0 + 1 : H)
+                          : (int)(a.S - j0 < B ? a.S - j0 : B);
   float2* src = ft_lds;
   float2* dst = IP ? ft_lds : ft_lds + B * RP;
   const bool inv = a.inv != 0;
@@ -415,7 +431,14 @@ __device__ __forceinline__ void ft_pass_body(const FtPass& a) {
   // column j0's first element); larger (a lone prime pass): element by element
   {
     const int c = t & (B - 1);
-    const int64_t j = j0 + c;
+    int64_t j = j0 + c;
+    bool cv = c < cols;
+    if (a.pair) {
+      const int cf = c < H ? c : c - H;
+      const int64_t jf = j0 + cf;
+      cv = cf < cols;
+      j = (c < H || jf == 0) ? jf : a.S - jf;
+    }
     const uint32_t k = a.p > 1 ? (uint32_t)(j % a.p) : 0u;
     const uint32_t twm = a.tw.nt / (uint32_t)(a.p * R);
     const int rs = FT_THREADS / B, r0 = t / B;
@@ -424,7 +447,7 @@ __device__ __forceinline__ void ft_pass_body(const FtPass& a) {
 #pragma unroll
       for (int i = 0; i < FT_REG_ELEMS / FT_THREADS; ++i) {
         const int r = r0 + i * rs;
-        const bool ok = c < cols && r < R;
+        const bool ok = cv && r < R;
         v[i] = ft_load(a, ok ? j + (int64_t)r * a.S : j0);
         const uint32_t e = ok ? (uint32_t)(((uint64_t)r * k) * twm) : 0u;
         w[i] = ft_root(a.tw, e, inv);
@@ -432,9 +455,9 @@ __device__ __forceinline__ void ft_pass_body(const FtPass& a) {
 #pragma unroll
       for (int i = 0; i < FT_REG_ELEMS / FT_THREADS; ++i) {
         const int r = r0 + i * rs;
-        if (c < cols && r < R) src[c * RP + r] = k ? ft_cmul(v[i], w[i]) : v[i];
+        if (cv && r < R) src[c * RP + r] = k ? ft_cmul(v[i], w[i]) : v[i];
       }
-    } else if (c < cols) {
+    } else if (cv) {
       for (int r = r0; r < R; r += rs) {
         float2 v = ft_load(a, j + (int64_t)r * a.S);
         if (k && r) v = ft_cmul(v, ft_root(a.tw, (uint32_t)(((uint64_t)r * k) * twm), inv));
@@ -480,6 +503,28 @@ __device__ __forceinline__ void ft_pass_body(const FtPass& a) {
   // consecutive columns (p > 1) or consecutive outputs of one column (p = 1: a contiguous run);
   // the LDS reads of a thread's outputs all issued before its stores
   constexpr int NE = FT_REG_ELEMS / FT_THREADS;
+  if (a.pair) {
+    // output m of front column j is Z[o], o = j + m S; its partner Z[M - o] is output R - 1 - m
+    // of the mirror column (column 0: output (R - m) mod R of itself); both X are written here
+    const int64_t M = a.n_aux;
+    const int cf = t & (H - 1);
+    const int64_t j = j0 + cf;
+    if (cf < cols) {
+      for (int m = t / H; m < R; m += FT_THREADS / H) {
+        const float2 zp = src[cf * RP + m];
+        const int64_t o = j + (int64_t)m * a.S;
+        if (o == 0) {
+          a.out[0] = make_float2(zp.x + zp.y, 0.0f);
+          a.out[M] = make_float2(zp.x - zp.y, 0.0f);
+          continue;
+        }
+        const float2 zq = j == 0 ? src[cf * RP + (R - m)] : src[(cf + H) * RP + (R - 1 - m)];
+        a.out[o] = ft_r2c_pair(zp, zq, (uint32_t)o, a.tw);
+        a.out[M - o] = ft_r2c_pair(zq, zp, (uint32_t)(M - o), a.tw);
+      }
+    }
+    return;
+  }
   if (a.p == 1) {
     if (B * R <= FT_REG_ELEMS) {
       float2 v[NE];
@@ -547,14 +592,8 @@ __global__ void __launch_bounds__(256) ft_r2c_post_kernel(const float2* z, float
       continue;
     }
     const float2 a = z[k], b = z[M - k];
-    auto one = [&](float2 p, float2 q, int64_t kk) {  // p = Z[kk], q = Z[M - kk]
-      const float2 e = make_float2(p.x + q.x, p.y - q.y);  // Z[kk] + conj Z[M-kk]
-      const float2 d = make_float2(p.x - q.x, p.y + q.y);  // Z[kk] - conj Z[M-kk]
-      const float2 o = ft_mi(ft_cmul(ft_root(tw, (uint32_t)kk, false), d), false);
-      return make_float2(0.5f * (e.x + o.x), 0.5f * (e.y + o.y));
-    };
-    const float2 xk = one(a, b, k);
-    const float2 xm = one(b, a, M - k);
+    const float2 xk = ft_r2c_pair(a, b, (uint32_t)k, tw);
+    const float2 xm = ft_r2c_pair(b, a, (uint32_t)(M - k), tw);
     out[k] = xk;
     if (M - k != k) out[M - k] = xm;
   }
@@ -702,7 +741,10 @@ static bool g_ft_lds_set = false;
 // store_mode, scale); the others alternate between bufA and bufB so that the last lands in out
 static int ft_run(const FtPlan& pl, const FtTw& tw, bool inv, const float2* in, const float* in_re,
                   int load_mode, float2* out, float* out_re, int store_mode, float scale,
-                  int64_t n_aux, float2* bufA, float2* bufB, hipStream_t st) {
+                  int64_t n_aux, float2* bufA, float2* bufB, hipStream_t st,
+                  bool* pair_last = nullptr) {
+  const bool want_pair = pair_last && *pair_last;
+  if (pair_last) *pair_last = false;
   if (!g_ft_lds_set) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(ft_pass_kernel),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
@@ -759,7 +801,13 @@ static int ft_run(const FtPlan& pl, const FtTw& tw, bool inv, const float2* in, 
       a.store_mode = 0;
     }
     a.out = dst;
-    const int64_t blocks = (a.S + B - 1) / B;
+    int64_t blocks = (a.S + B - 1) / B;
+    if (last && want_pair && B >= 2) {  // the even-n rfft pairing in the last pass's stores
+      a.pair = 1;
+      a.n_aux = pl.L;
+      blocks = (a.S / 2 + 1 + B / 2 - 1) / (B / 2);
+      *pair_last = true;
+    }
     const size_t lds = ((ip ? 1 : 2) * (size_t)B * a.RP + (a.R <= FT_PACK ? a.R : 0)) *
                        sizeof(float2);
     if (ip) {
@@ -802,11 +850,20 @@ static int ft_rfft_native(const FtPlan& pl, const float* x, int64_t n, float2* o
     const int64_t M = n / 2;
     float2* w = ft_align(ws, 0);
     const float2* z = reinterpret_cast<const float2*>(x);
+    // the pairing inside the last pass (DPZ_FFT_POST_FUSED=1, diagnostic build): bit-identical and
+    // no faster on MI355X (11 M rfft 168.3 vs 169.1 us, 25 M 368.3 vs 358.4 with the separate
+    // pass, profiles/r06_fft_post_ab.jsonl: the mirrored columns' descending stores cost what the
+    // pass saves), so the separate pass stays the default
+    bool paired = DPZ_KNOB_INT(FFT_POST_FUSED, 0) != 0;
     if (pl.npass > 0) {
-      const int r2 = ft_run(pl, tw, false, z, nullptr, 0, out, nullptr, 0, 1.0f, 0, w, out, st);
+      const int r2 = ft_run(pl, tw, false, z, nullptr, 0, out, nullptr, 0, 1.0f, 0, w, out, st,
+                            &paired);
       if (r2 != DPZ_OK) return r2;
       z = out;
+    } else {
+      paired = false;
     }
+    if (paired) return DPZ_OK;
     DPZ_TIMED(DPZ_KT_FFT, st, ft_r2c_post_kernel<<<grid_for(M / 2 + 1), 256, 0, st>>>(z, out, M, tw));
     return DPZ_OK;
   }

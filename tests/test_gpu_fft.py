@@ -152,3 +152,21 @@ def test_fft_inplace_passes_forced(dev, diag_lib, monkeypatch, n):
     np.testing.assert_array_equal(f1.cpu().numpy().view(np.uint64), f0.view(np.uint64))
     back = codec.irfft(f1.clone(), n).cpu().numpy()
     assert np.abs(back - xh).max() <= scenario.fft_tol("model", n, scale)
+
+
+@pytest.mark.parametrize("n", [2, 4098, 30030, 11_000_000, 2 * 17 * 19 * 23, 1 << 20])
+def test_fft_pairing_fused_matches_separate_pass(dev, diag_lib, monkeypatch, n):
+    """The even-n rfft pairing X[k] / X[M - k] done in the last pass's stores (the block holding
+    columns j and S - j) against the separate pairing pass (DPZ_FFT_POST_FUSED=0, diagnostic
+    build): bit-identical (the same arithmetic), and within tolerance of numpy."""
+    from decentralizepy_amd import codec
+    g = torch.Generator(device=dev).manual_seed(13)
+    x = torch.randn(n, device=dev, generator=g)
+    monkeypatch.setenv("DPZ_FFT_POST_FUSED", "0")
+    f0 = codec.rfft(x).cpu().numpy()
+    monkeypatch.setenv("DPZ_FFT_POST_FUSED", "1")
+    f1 = codec.rfft(x).cpu().numpy()
+    np.testing.assert_array_equal(f1.view(np.uint64), f0.view(np.uint64))
+    xh = x.cpu().numpy()
+    ref = np.fft.rfft(xh.astype(np.float64))
+    assert np.abs(f1 - ref).max() <= scenario.fft_tol("params", n, float(np.abs(xh).max()))
