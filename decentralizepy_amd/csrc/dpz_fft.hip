@@ -647,19 +647,22 @@ static bool ft_make_plan(int64_t L, FtPlan* pl) {
       m /= f;
     }
   if (m > 1) primes.push_back(m);
+  // the packing bound (DPZ_FFT_PACK, diagnostic build: smaller passes of 128-byte rows, A/B)
+  int64_t pack = DPZ_KNOB_INT(FFT_PACK, FT_PACK);
+  if (pack < 2 || pack > FT_PACK) pack = FT_PACK;
   std::vector<std::vector<int>> bins;
   std::vector<int64_t> prod;
   std::sort(primes.begin(), primes.end(), std::greater<int64_t>());
   for (int64_t f : primes) {
     if (f > FT_MAXR) return false;
-    if (f > FT_PACK) {
+    if (f > pack) {
       bins.push_back({(int)f});
       prod.push_back(f);
       continue;
     }
     int best = -1;
     for (size_t b = 0; b < bins.size(); ++b)
-      if (prod[b] <= FT_PACK && prod[b] * f <= FT_PACK && (best < 0 || prod[b] < prod[best])) best = (int)b;
+      if (prod[b] <= pack && prod[b] * f <= pack && (best < 0 || prod[b] < prod[best])) best = (int)b;
     if (best < 0) {
       bins.push_back({(int)f});
       prod.push_back(f);

@@ -13,10 +13,13 @@ from decentralizepy_amd import codec  # noqa: E402
 
 CONFIGS = [("lib", {"DPZ_FFT_LIB": "1"}), ("default", {}),
            ("pingpong", {"DPZ_FFT_INPLACE": "0"}), ("pair_sep", {"DPZ_FFT_PAIR_FUSED": "0"}),
+           ("pack128", {"DPZ_FFT_PACK": "128"}), ("pack64", {"DPZ_FFT_PACK": "64"}),
            ("e4096_b16", {"DPZ_FFT_ELEMS": "4096", "DPZ_FFT_BMAX": "16"}),
            ("e2048_b8", {"DPZ_FFT_ELEMS": "2048", "DPZ_FFT_BMAX": "8"})]
 if os.environ.get("FFT_CONFIGS") == "short":
     CONFIGS = CONFIGS[:4]
+elif os.environ.get("FFT_CONFIGS") == "pack":
+    CONFIGS = [CONFIGS[1], CONFIGS[4], CONFIGS[5], ("default_again", {})]
 
 
 def main():
@@ -30,7 +33,7 @@ def main():
         row = {"n": n}
         for name, env in CONFIGS:
             for k_ in ("DPZ_FFT_LIB", "DPZ_FFT_ELEMS", "DPZ_FFT_BMAX", "DPZ_FFT_INPLACE",
-                       "DPZ_FFT_PAIR_FUSED"):
+                       "DPZ_FFT_PAIR_FUSED", "DPZ_FFT_PACK"):
                 os.environ.pop(k_, None)
             os.environ.update(env)
             ws = codec.Workspace(dev)
