@@ -164,13 +164,21 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
                          out=torch.empty(n, dtype=torch.float32, device=dev)))
     s_list = [torch.cuda.Stream(dev) for _ in range(S)]
     ws_list = [codec.Workspace(dev) for _ in range(S)]
-    multi = codec.NodeStepBatch(sets, n, k, s_list, ws_list, decode_src=lambda j: (j - S) % len(sets))
+    # every state's shared_parameters_counter as the PartialModel plugin keeps it (RingCounter):
+    # the encodes write their payload indices into a ring slot and update no counter line; the
+    # rings are folded into the counters when full and at the end of every timed region
+    # (BENCH_RING=0: the counter updated inside the compact, A/B)
+    from decentralizepy_amd._device import RingCounter
+    rings = ([RingCounter(d["counter"]) for d in sets]
+             if os.environ.get("BENCH_RING", "1") != "0" else None)
+    multi = codec.NodeStepBatch(sets, n, k, s_list, ws_list, decode_src=lambda j: (j - S) % len(sets),
+                                rings=rings)
     # one node on one stream decodes a neighbour's payload (the previous state's, encoded in the
     # previous step on the same stream), so its decode is co-scheduled in its encode's launches
     # its own workspace: a prior window is only taken from an encode of the same grid (the
     # S-codec batch runs the shared filter grid, DPZ_TOPK_SHARED)
     one = codec.NodeStepBatch(sets, n, k, s_list[:1], [codec.Workspace(dev)],
-                              decode_src=lambda j: (j - 1) % len(sets))
+                              decode_src=lambda j: (j - 1) % len(sets), rings=rings)
 
     # every encode takes its key window from the previous encode on its stream's workspace
     # (DPZ_BATCH_HINT: a node's previous round, as PartialModel runs it; no sample launch)
@@ -184,7 +192,10 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
 
     torch.cuda.synchronize()
     run_steps(multi, max(warmup, 2 * R))
+    multi.flush_rings()
+    torch.cuda.synchronize()
     run_steps(one, max(warmup, R))
+    one.flush_rings()
     torch.cuda.synchronize()
     multi.sticky_status(clear=True)
     one.sticky_status(clear=True)
@@ -195,6 +206,7 @@ def gpu_case(n, alpha, dev, seed, steps, warmup, world, dist, rotate=None, strea
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         run_steps(batch, count)
+        batch.flush_rings()  # every deferred counter update of the region, inside it
         t_host = time.perf_counter() - t0  # host enqueue time (host-bound if close to t)
         torch.cuda.synchronize()
         if dist is not None:
@@ -461,6 +473,7 @@ def _stage_time(batch, what, reps, run_steps, stream):
         torch.cuda._sleep(int(50e6))  # the host queues the loop while the GPU spins
         ev0.record(stream)
     run_steps(batch, reps, what)
+    batch.flush_rings()  # (encodes: their deferred counter updates, on the batch's stream)
     ev1.record(stream)
     ev1.synchronize()
     return ev0.elapsed_time(ev1) / reps * 1e-3
@@ -859,7 +872,10 @@ def main():
                            "each encode's key window from the previous encode's exact threshold "
                            "on its stream's workspace, no sample launch); step i = encode "
                            f"of node state i with the replace decode of state i - {r['streams']}'s "
-                           f"payload over its x fused in, on stream i % {r['streams']}"
+                           f"payload over its x fused in, on stream i % {r['streams']}; "
+                           "counters as the PartialModel plugin keeps them (RingCounter: payload "
+                           "indices into a ring slot, folded into the counter when the ring is "
+                           "full and at the end of every timed region, inside it)"
                            if r["mode"] == "multi" else
                            "native batched enqueue (dpz_encode_replace_batch, DPZ_BATCH_HINT), "
                            "one stream; "

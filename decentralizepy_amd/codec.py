@@ -359,7 +359,11 @@ class NodeStepBatch:
     ``streams[j % len(streams)]`` with that stream's workspace.  The pointer arrays are built
     once; :meth:`run` is one ctypes call whatever m is (the host loop is native)."""
 
-    def __init__(self, nodes, n, k, streams, workspaces, decode_src=None):
+    def __init__(self, nodes, n, k, streams, workspaces, decode_src=None, rings=None):
+        """``rings``: one :class:`~decentralizepy_amd._device.RingCounter` per node (over its
+        ``counter``): the encodes then update no counter and write their payload indices into
+        the node's ring slot, as the PartialModel plugin does; the rings are flushed when full
+        and by :meth:`flush_rings` (ordered on each node's stream)."""
         m = len(nodes)
         self.m, self.n, self.k = m, int(n), int(k)
         for d in nodes:
@@ -398,6 +402,32 @@ class NodeStepBatch:
         self._S = S
         self.workspaces = workspaces
         self._keep = (nodes, wbufs, dbufs, streams)
+        self._rings = rings
+        if rings is not None:
+            if len(rings) != m:
+                raise ValueError("one ring per node")
+            self._src = [src(j) for j in range(m)]
+            self._tstreams = list(streams)
+            self._cnt = P(*([0] * m))  # no counter update in the encodes
+            # the last committed payload of every node (its own buffer until the first encode)
+            self._last = [d["idx"].data_ptr() for d in nodes]
+
+    def _ring_slot(self, j):
+        """Node j's next ring slot; a full ring is flushed first, on node j's stream."""
+        r = self._rings[j]
+        if r.ring is None or r.segs[-1] + self.k > r.ring.numel() or len(r.segs) > r.MAX_SEGS:
+            with torch.cuda.stream(self._tstreams[j % self._S]):
+                return r.slot(self.k)
+        return r.slot(self.k)
+
+    def flush_rings(self):
+        """Every node's deferred counter updates into its counter, on its stream."""
+        if self._rings is None:
+            return
+        for j, r in enumerate(self._rings):
+            if r.pending_rounds():
+                with torch.cuda.stream(self._tstreams[j % self._S]):
+                    r.flush()
 
     def run(self, what=_lib.DPZ_BATCH_ENCODE | _lib.DPZ_BATCH_DECODE, m=None):
         """``what`` with DPZ_BATCH_HINT: the encodes take the prior window (DPZ_TOPK_HINT) —
@@ -407,11 +437,24 @@ class NodeStepBatch:
             if getattr(self, "_primed", False):
                 what = (what & ~_lib.DPZ_BATCH_HINT) | _lib.DPZ_BATCH_HINT_ALL
             self._primed = True
+        idx, ri = self._idx, self._ri
+        enc = bool(what & _lib.DPZ_BATCH_ENCODE)
+        if self._rings is not None:
+            P = ctypes.c_void_p * max(self.m, 1)
+            new = [self._ring_slot(j).data_ptr() if enc else self._last[j] for j in range(m)]
+            idx = P(*(new + [0] * (self.m - m)))
+            # a payload encoded earlier in this run (src < j, same stream) is the new slot
+            ri = P(*([(new[q] if (enc and q < j) else self._last[q])
+                      for j, q in ((j, self._src[j]) for j in range(m))] + [0] * (self.m - m)))
         rc = _lib.lib().dpz_encode_replace_batch(
-            m, int(what), self._x, self._x0, self.n, self.k, self._cnt, self._idx, self._val,
-            self._rl, self._ri, self._rv, self.k, self._ro, self._ws, self._ws_bytes, self._dws,
+            m, int(what), self._x, self._x0, self.n, self.k, self._cnt, idx, self._val,
+            self._rl, ri, self._rv, self.k, self._ro, self._ws, self._ws_bytes, self._dws,
             self._dws_bytes, self._S, self._streams)
         check(rc, "dpz_encode_replace_batch")
+        if self._rings is not None and enc:
+            for j in range(m):
+                self._rings[j].commit(self.k)
+                self._last[j] = new[j]
 
     def sticky_status(self, clear=False):
         """OR of every encode's final status on these workspaces since the last clear."""
